@@ -1,0 +1,294 @@
+/*
+ * mmba.h -- C ABI of the MI355X bundle-adjustment core ("mmba").
+ *
+ * This is the drop-in seam for mmSolver's Levenberg-Marquardt hot path.
+ * In the reference, `solveFrames` (src/mmSolver/adjust/adjust_base.cpp:1167-1190)
+ * dispatches to
+ *
+ *   bool solve_3d_cminpack_lmder(SolverOptions&, int numberOfParameters,
+ *                                int numberOfErrors,
+ *                                std::vector<double>& paramList,   // in: x0 (internal), out: x
+ *                                std::vector<double>& errorList,   // out: fvec
+ *                                std::vector<double>& paramWeightList,
+ *                                SolverData& userData, SolverResult& out);
+ *   (src/mmSolver/adjust/adjust_cminpack_lmder.cpp:64-69; lmdif twin at
+ *    src/mmSolver/adjust/adjust_cminpack_lmdif.cpp:61-66)
+ *
+ * `mmba_solve` / `mmba_plan_solve` replace that call.  `mmba_problem` is the
+ * Maya-free flattening of `SolverData` after `construct_scene_graph`
+ * (src/mmSolver/mayahelper/maya_scene_graph.cpp:1114) and
+ * `countUpNumberOfErrors` / `countUpNumberOfUnknownParameters`
+ * (src/mmSolver/adjust/adjust_relationships.cpp:75,223): plain SoA arrays,
+ * host pointers, no ownership transfer.  Nothing is retained after return
+ * except inside an explicitly created plan.
+ *
+ * All arithmetic is IEEE fp64; all indices are int32.
+ */
+#ifndef MMBA_H
+#define MMBA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMBA_ABI_VERSION 1
+
+/* Return codes. */
+#define MMBA_OK 0
+#define MMBA_ERR_INVALID (-1)     /* malformed problem / options          */
+#define MMBA_ERR_DEVICE (-2)      /* HIP runtime error                    */
+#define MMBA_ERR_UNSUPPORTED (-3) /* valid mmSolver input this core does not (yet) map */
+#define MMBA_ERR_INTERRUPTED (-4) /* interrupt callback returned non-zero */
+#define MMBA_ERR_NO_DEVICE (-5)   /* no gfx950 device visible             */
+#define MMBA_ERR_COMM (-6)        /* RCCL communicator error              */
+
+/* Solver types: same numbers as SOLVER_TYPE_CMINPACK_* (adjust_defines.h:44-52). */
+#define MMBA_SOLVER_CMINPACK_LMDIF 1
+#define MMBA_SOLVER_CMINPACK_LMDER 2
+
+/* Scene graph modes: same numbers as SCENE_GRAPH_MODE_* (adjust_defines.h:76-77). */
+#define MMBA_SCENE_GRAPH_MAYA_DAG 1
+#define MMBA_SCENE_GRAPH_MM_SCENE_GRAPH 2
+
+/* Auto-diff types (adjust_defines.h:96-97). */
+#define MMBA_AUTO_DIFF_FORWARD 0
+#define MMBA_AUTO_DIFF_CENTRAL 1
+
+/* Film fit (lib/rust/mmscenegraph/src/math/camera.rs FilmFit; Maya enum). */
+#define MMBA_FILM_FIT_FILL 0
+#define MMBA_FILM_FIT_HORIZONTAL 1
+#define MMBA_FILM_FIT_VERTICAL 2
+#define MMBA_FILM_FIT_OVERSCAN 3
+
+/* Rotate orders (maya_camera.cpp:921-941 / euler.rs). */
+#define MMBA_ROO_XYZ 0
+#define MMBA_ROO_YZX 1
+#define MMBA_ROO_ZXY 2
+#define MMBA_ROO_XZY 3
+#define MMBA_ROO_YXZ 4
+#define MMBA_ROO_ZYX 5
+
+/* Lens model types (mmlens LensModelType); only 3DE Classic is mapped. */
+#define MMBA_LENS_NONE 0
+#define MMBA_LENS_3DE_CLASSIC 1
+
+/* Camera attribute slots in `cam_attrs` (8 per camera). */
+#define MMBA_CAM_FILM_BACK_W_INCH 0
+#define MMBA_CAM_FILM_BACK_H_INCH 1
+#define MMBA_CAM_FOCAL_MM 2
+#define MMBA_CAM_FILM_OFFSET_X_INCH 3
+#define MMBA_CAM_FILM_OFFSET_Y_INCH 4
+#define MMBA_CAM_NEAR_CLIP 5
+#define MMBA_CAM_FAR_CLIP 6
+#define MMBA_CAM_SCALE 7
+#define MMBA_CAM_NUM_ATTRS 8
+
+/* Lens attribute slots in `lens_attrs` (5 per lens; LDPK classic order). */
+#define MMBA_LENS_NUM_ATTRS 5
+
+/*
+ * Flattened problem.  Units are Maya UI units, exactly as the reference
+ * solver sees attribute values: translations in scene units, rotations in
+ * degrees, focal length in mm, film back / film offset in inches.
+ *
+ * Attribute values (the mmscenegraph AttrDataBlock, attr/datablock.rs):
+ * attribute `a` is static (one value at attr_values[attr_offset[a]]) or
+ * animated (num_frames values starting at attr_offset[a]).  An attribute id
+ * of -1 in any attribute slot means "constant" with the slot's default
+ * (0 for translate/rotate/offset, 1 for scale/camera scale/squeeze,
+ * 10000 for far clip, 0.1 for near clip).
+ */
+typedef struct mmba_problem {
+    int32_t num_frames;
+
+    int32_t num_attrs;
+    const int32_t *attr_animated; /* [num_attrs] */
+    const int64_t *attr_offset;   /* [num_attrs] */
+    const double *attr_values;    /* initial (external) values */
+
+    /* Transforms, topologically sorted (parent index < child index). */
+    int32_t num_transforms;
+    const int32_t *tfm_parent;       /* [num_transforms], -1 = world   */
+    const int32_t *tfm_rotate_order; /* [num_transforms]               */
+    const int32_t *tfm_attrs;        /* [9*num_transforms] tx ty tz rx ry rz sx sy sz */
+
+    int32_t num_cameras;
+    const int32_t *cam_tfm;         /* [num_cameras] transform index  */
+    const int32_t *cam_attrs;       /* [8*num_cameras] see MMBA_CAM_* */
+    const int32_t *cam_film_fit;    /* [num_cameras]                  */
+    const int32_t *cam_render_size; /* [2*num_cameras] width, height  */
+    const int32_t *cam_lens;        /* [num_cameras] lens index or -1 (NULL = none) */
+
+    int32_t num_lenses;
+    const int32_t *lens_type;  /* [num_lenses] MMBA_LENS_*     */
+    const int32_t *lens_attrs; /* [5*num_lenses] attribute ids */
+
+    int32_t num_bundles;
+    const int32_t *bnd_tfm; /* [num_bundles] transform index */
+
+    int32_t num_markers;
+    const int32_t *mkr_cam; /* [num_markers] camera index */
+    const int32_t *mkr_bnd; /* [num_markers] bundle index */
+
+    /* Observations = errorToMarkerList (adjust_relationships.cpp:124-160):
+     * marker-major, frame-minor, only enabled frames with weight > 0. */
+    int32_t num_obs;
+    const int32_t *obs_marker; /* [num_obs] */
+    const int32_t *obs_frame;  /* [num_obs] frame index        */
+    const double *obs_xy;      /* [2*num_obs] marker x,y with MarkerGroup overscan applied
+                                  (markerPosList), before film-fit correction */
+    const double *obs_weight;  /* [num_obs] markerWeightList, already normalised per frame
+                                  (adjust_relationships.cpp:166-182); sqrt is taken inside */
+
+    /* Parameters = paramToAttrList (adjust_relationships.cpp:223-337). */
+    int32_t num_params;
+    const int32_t *param_attr;    /* [num_params] attribute id         */
+    const int32_t *param_frame;   /* [num_params] frame index, -1 static */
+    const double *param_min;      /* [num_params] Attr::getMinimumValue (-FLT_MAX = none) */
+    const double *param_max;      /* [num_params] Attr::getMaximumValue (+FLT_MAX = none) */
+    const double *param_offset;   /* [num_params] Attr::getOffsetValue */
+    const double *param_scale;    /* [num_params] Attr::getScaleValue  */
+} mmba_problem;
+
+/* SolverOptions subset that the LM path reads (adjust_data.h:133-185). */
+typedef struct mmba_options {
+    int32_t solver_type;      /* MMBA_SOLVER_CMINPACK_LMDIF / _LMDER     */
+    int32_t iter_max;         /* maxfev                                  */
+    double tau;               /* factor = tau * 100                      */
+    double eps1;              /* ftol */
+    double eps2;              /* xtol */
+    double eps3;              /* gtol */
+    double delta;             /* FD step (lmder) / epsfcn = |delta| (lmdif) */
+    int32_t auto_diff_type;   /* MMBA_AUTO_DIFF_*                        */
+    int32_t auto_param_scale; /* 1 -> MINPACK mode 1, else mode 2        */
+    int32_t scene_graph_mode; /* MMBA_SCENE_GRAPH_*                      */
+    double image_width;       /* pixels (default 2048)                   */
+    int32_t accept_only_better; /* restore x0 when error avg got worse   */
+    int32_t log_level;        /* 0 error .. 4 debug                      */
+} mmba_options;
+
+/* SolverResult mirror (adjust_results.h:59-72) plus run statistics. */
+typedef struct mmba_result {
+    int32_t success;          /* functionEvals > 0 (adjust_cminpack_lmder.cpp:191) */
+    int32_t reason_number;    /* MINPACK info 0..8, negative on interrupt */
+    int32_t iterations;       /* nfev */
+    int32_t function_evals;   /* iflag=1 calls (userData.iterNum)         */
+    int32_t jacobian_evals;   /* FD columns / iflag=2 calls (jacIterNum)  */
+    int32_t outer_iterations; /* njev: LM iterations                      */
+    int32_t user_interrupted;
+    int32_t error_is_better;  /* acceptOnlyBetter outcome (1 = kept solution) */
+    double error_final;       /* enorm(fvec) at returned x                */
+    double error_avg;         /* pixels; errorDistanceList stats (adjust_base.cpp:346) */
+    double error_min;
+    double error_max;
+    double error_initial_avg; /* before solving (adjust_base.cpp:1080-1103) */
+    double error_rms;         /* sqrt(sum dist^2 / M) at returned x, pixels */
+    int32_t num_trace;        /* entries written to the fnorm trace        */
+    int32_t pad0;
+    double time_solve_s;      /* wall time inside the solve                */
+    double time_func_s;       /* residual kernels                          */
+    double time_jac_s;        /* Jacobian + normal-equation kernels        */
+    double time_linear_s;     /* Schur + Cholesky + solves                 */
+} mmba_result;
+
+/* Interrupt / progress callbacks, polled between LM iterations
+ * (MComputation::isInterruptRequested, adjust_solveFunc.cpp:317-325). */
+typedef struct mmba_callbacks {
+    int (*interrupt)(void *user);           /* non-zero -> stop */
+    void (*progress)(void *user, int iter);
+    void *user;
+} mmba_callbacks;
+
+/* Optional per-evaluation trace: fnorm of every iflag=1 residual
+ * evaluation, in call order (first entry = initial point). */
+typedef struct mmba_trace {
+    double *fnorm;     /* [capacity] */
+    int32_t capacity;
+    int32_t count;     /* out */
+} mmba_trace;
+
+typedef struct mmba_context mmba_context;
+typedef struct mmba_plan mmba_plan;
+
+int mmba_abi_version(void);
+/* Number of visible gfx950 devices (0 when none). */
+int mmba_device_count(void);
+/* Last error message of the calling thread. */
+const char *mmba_last_error(void);
+
+/* Defaults identical to the cminpack_lmder defaults (adjust_defines.h:129-141). */
+void mmba_options_default(mmba_options *opt, int32_t solver_type);
+
+/* Box-constraint reparametrisation (adjust_base.cpp:194-258), bug-compatible. */
+double mmba_param_external_to_internal(double value, double xmin, double xmax,
+                                       double offset, double scale);
+double mmba_param_internal_to_external(double value, double xmin, double xmax,
+                                       double offset, double scale);
+
+int mmba_context_create(int device, mmba_context **out);
+void mmba_context_destroy(mmba_context *ctx);
+
+/* Upload a problem into HBM once; the plan can then be solved many times
+ * (cached device context for the many small calls the Python standard solver
+ * issues, _api/solverstandardutils.py). */
+int mmba_plan_create(mmba_context *ctx, const mmba_problem *prob,
+                     const mmba_options *opt, mmba_plan **out);
+void mmba_plan_destroy(mmba_plan *plan);
+
+/* Shard the plan's observations by frame range over `nranks` processes, one
+ * per GPU, and reduce normal equations with RCCL.  `unique_id` is 128 bytes
+ * from mmba_comm_unique_id on rank 0, broadcast by the caller. */
+int mmba_comm_unique_id(unsigned char out_id[128]);
+int mmba_plan_set_comm(mmba_plan *plan, int rank, int nranks,
+                       const unsigned char unique_id[128]);
+
+/* One residual evaluation (measureErrors, adjust_measureErrors.cpp:523) at
+ * internal parameters x.  Any output pointer may be NULL. */
+int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out,
+                      double *err_user_out, double *err_dist_out,
+                      double *avg_min_max_out /* [3] */);
+
+/* Run the LM solve from internal parameters x_inout (replaces the
+ * solve_3d_cminpack_* call inside solveFrames, including the initial
+ * error measurement and accept-only-better logic of adjust_base.cpp:1080-1244).
+ *   fvec_out     [num_residuals]   errorList (weighted, |dx|*imageWidth*sqrt(w))
+ *   err_user_out [num_residuals]   ud->errorList (no weight)
+ *   err_dist_out [num_obs]         ud->errorDistanceList
+ * num_residuals = 2*num_obs.  Any output may be NULL. */
+int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out,
+                    double *err_user_out, double *err_dist_out,
+                    mmba_result *res, const mmba_callbacks *cb,
+                    mmba_trace *trace);
+
+/* One-shot convenience: plan_create + plan_solve + plan_destroy. */
+int mmba_solve(mmba_context *ctx, const mmba_problem *prob,
+               const mmba_options *opt, double *x_inout, double *fvec_out,
+               double *err_user_out, double *err_dist_out, mmba_result *res,
+               const mmba_callbacks *cb, mmba_trace *trace);
+
+/* Kernel-level timing of the last solve for roofline accounting: average
+ * device time (ms) of the dominant kernels measured with HIP events on the
+ * plan's stream, and the algorithmic bytes / flops they moved per launch. */
+typedef struct mmba_kernel_stats {
+    double jac_ms_avg;      /* FD-Jacobian + normal-equation kernel       */
+    double jac_bytes;       /* algorithmic HBM bytes per launch           */
+    int32_t jac_launches;
+    double resid_ms_avg;    /* residual kernel                            */
+    double resid_bytes;
+    int32_t resid_launches;
+    double chol_ms_avg;     /* reduced camera system Cholesky             */
+    double chol_flops;      /* n_r^3/3 per factorisation                  */
+    int32_t chol_launches;
+    int32_t reduced_dim;    /* n_r = camera-frame + global parameters     */
+    int32_t pad1;
+} mmba_kernel_stats;
+int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
+                           mmba_kernel_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MMBA_H */

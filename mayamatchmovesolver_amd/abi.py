@@ -1,0 +1,193 @@
+"""ctypes mirror of include/mmba.h (the drop-in C ABI).
+
+Only plain data layouts live here; loading the HIP library is in ``_lib.py``.
+Field order and types must match ``include/mmba.h`` exactly.
+"""
+import ctypes as C
+
+MMBA_OK = 0
+MMBA_ERR_INVALID = -1
+MMBA_ERR_DEVICE = -2
+MMBA_ERR_UNSUPPORTED = -3
+MMBA_ERR_INTERRUPTED = -4
+MMBA_ERR_NO_DEVICE = -5
+MMBA_ERR_COMM = -6
+
+SOLVER_TYPE_CMINPACK_LMDIF = 1
+SOLVER_TYPE_CMINPACK_LMDER = 2
+SCENE_GRAPH_MODE_MAYA_DAG = 1
+SCENE_GRAPH_MODE_MM_SCENE_GRAPH = 2
+AUTO_DIFF_TYPE_FORWARD = 0
+AUTO_DIFF_TYPE_CENTRAL = 1
+
+FILM_FIT_FILL = 0
+FILM_FIT_HORIZONTAL = 1
+FILM_FIT_VERTICAL = 2
+FILM_FIT_OVERSCAN = 3
+
+ROO_XYZ, ROO_YZX, ROO_ZXY, ROO_XZY, ROO_YXZ, ROO_ZYX = range(6)
+
+LENS_NONE = 0
+LENS_3DE_CLASSIC = 1
+
+CAM_FILM_BACK_W_INCH = 0
+CAM_FILM_BACK_H_INCH = 1
+CAM_FOCAL_MM = 2
+CAM_FILM_OFFSET_X_INCH = 3
+CAM_FILM_OFFSET_Y_INCH = 4
+CAM_NEAR_CLIP = 5
+CAM_FAR_CLIP = 6
+CAM_SCALE = 7
+CAM_NUM_ATTRS = 8
+LENS_NUM_ATTRS = 5
+
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_f64p = C.POINTER(C.c_double)
+
+
+class MmbaProblem(C.Structure):
+    _fields_ = [
+        ("num_frames", C.c_int32),
+        ("num_attrs", C.c_int32),
+        ("attr_animated", _i32p),
+        ("attr_offset", _i64p),
+        ("attr_values", _f64p),
+        ("num_transforms", C.c_int32),
+        ("tfm_parent", _i32p),
+        ("tfm_rotate_order", _i32p),
+        ("tfm_attrs", _i32p),
+        ("num_cameras", C.c_int32),
+        ("cam_tfm", _i32p),
+        ("cam_attrs", _i32p),
+        ("cam_film_fit", _i32p),
+        ("cam_render_size", _i32p),
+        ("cam_lens", _i32p),
+        ("num_lenses", C.c_int32),
+        ("lens_type", _i32p),
+        ("lens_attrs", _i32p),
+        ("num_bundles", C.c_int32),
+        ("bnd_tfm", _i32p),
+        ("num_markers", C.c_int32),
+        ("mkr_cam", _i32p),
+        ("mkr_bnd", _i32p),
+        ("num_obs", C.c_int32),
+        ("obs_marker", _i32p),
+        ("obs_frame", _i32p),
+        ("obs_xy", _f64p),
+        ("obs_weight", _f64p),
+        ("num_params", C.c_int32),
+        ("param_attr", _i32p),
+        ("param_frame", _i32p),
+        ("param_min", _f64p),
+        ("param_max", _f64p),
+        ("param_offset", _f64p),
+        ("param_scale", _f64p),
+    ]
+
+
+class MmbaOptions(C.Structure):
+    _fields_ = [
+        ("solver_type", C.c_int32),
+        ("iter_max", C.c_int32),
+        ("tau", C.c_double),
+        ("eps1", C.c_double),
+        ("eps2", C.c_double),
+        ("eps3", C.c_double),
+        ("delta", C.c_double),
+        ("auto_diff_type", C.c_int32),
+        ("auto_param_scale", C.c_int32),
+        ("scene_graph_mode", C.c_int32),
+        ("image_width", C.c_double),
+        ("accept_only_better", C.c_int32),
+        ("log_level", C.c_int32),
+    ]
+
+
+class MmbaResult(C.Structure):
+    _fields_ = [
+        ("success", C.c_int32),
+        ("reason_number", C.c_int32),
+        ("iterations", C.c_int32),
+        ("function_evals", C.c_int32),
+        ("jacobian_evals", C.c_int32),
+        ("outer_iterations", C.c_int32),
+        ("user_interrupted", C.c_int32),
+        ("error_is_better", C.c_int32),
+        ("error_final", C.c_double),
+        ("error_avg", C.c_double),
+        ("error_min", C.c_double),
+        ("error_max", C.c_double),
+        ("error_initial_avg", C.c_double),
+        ("error_rms", C.c_double),
+        ("num_trace", C.c_int32),
+        ("pad0", C.c_int32),
+        ("time_solve_s", C.c_double),
+        ("time_func_s", C.c_double),
+        ("time_jac_s", C.c_double),
+        ("time_linear_s", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "pad0"}
+
+
+INTERRUPT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p)
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+
+
+class MmbaCallbacks(C.Structure):
+    _fields_ = [
+        ("interrupt", INTERRUPT_FN),
+        ("progress", PROGRESS_FN),
+        ("user", C.c_void_p),
+    ]
+
+
+class MmbaTrace(C.Structure):
+    _fields_ = [
+        ("fnorm", _f64p),
+        ("capacity", C.c_int32),
+        ("count", C.c_int32),
+    ]
+
+
+class MmbaKernelStats(C.Structure):
+    _fields_ = [
+        ("jac_ms_avg", C.c_double),
+        ("jac_bytes", C.c_double),
+        ("jac_launches", C.c_int32),
+        ("resid_ms_avg", C.c_double),
+        ("resid_bytes", C.c_double),
+        ("resid_launches", C.c_int32),
+        ("chol_ms_avg", C.c_double),
+        ("chol_flops", C.c_double),
+        ("chol_launches", C.c_int32),
+        ("reduced_dim", C.c_int32),
+        ("pad1", C.c_int32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "pad1"}
+
+
+# Functions exported by libmmba.so (checked by tests/test_abi.py against
+# include/mmba.h).
+EXPORTED_SYMBOLS = [
+    "mmba_abi_version",
+    "mmba_device_count",
+    "mmba_last_error",
+    "mmba_options_default",
+    "mmba_param_external_to_internal",
+    "mmba_param_internal_to_external",
+    "mmba_context_create",
+    "mmba_context_destroy",
+    "mmba_plan_create",
+    "mmba_plan_destroy",
+    "mmba_comm_unique_id",
+    "mmba_plan_set_comm",
+    "mmba_plan_measure",
+    "mmba_plan_solve",
+    "mmba_solve",
+    "mmba_plan_kernel_stats",
+]

@@ -1,0 +1,427 @@
+"""Synthetic scenes.
+
+Two families:
+
+1. ``known_scene(name)`` -- the reference's Maya solver tests rebuilt without
+   Maya (tests/test/test_solver/*.py).  They carry the published known answers
+   (SURVEY.md section 4).
+2. ``make_config(i)`` -- the five BASELINE.json configurations as concrete
+   synthetic inputs: numpy PCG64 seeded with
+   ``20241008 + i``, 35 mm lens on a 36 x 24 mm back, Horizontal film fit,
+   2048 x 1556 render, zero film offsets, markers = true projection +
+   N(0, 0.5 px) noise, initial guesses = truth + perturbation, gauge locked
+   (camera-0 pose at frame 0 and bundle 0) when cameras and bundles are both
+   solved.
+
+Everything here is host-side input generation (the role Maya + the Python
+caller play for the reference); it contains no solver arithmetic.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import abi
+from .problem import AttrRef, FLOAT_MAX, Problem, SceneBuilder, param_external_to_internal
+
+FOCAL_MM = 35.0
+FILM_W_MM = 36.0
+FILM_H_MM = 24.0
+FILM_W_IN = FILM_W_MM / 25.4
+FILM_H_IN = FILM_H_MM / 25.4
+RENDER = (2048, 1556)
+IMAGE_WIDTH = 2048.0
+
+# ---------------------------------------------------------------------------
+# Reference known-answer scenes (tests/test/test_solver).
+# ---------------------------------------------------------------------------
+KNOWN_ANSWERS = {
+    # name: (expected external values of the solved attrs, tolerance)
+    "test1": ([-6.0, 3.6], 1e-4),                       # test1.py:116-121
+    "test3": ([7.44014, -32.3891], 1e-3),               # test3.py:117-118
+    "minmax_both": ([-5.0, 2.3], 1e-4),                 # test_min_max_values.py:43-99
+    "minmax_lower": ([-5.0, 2.3], 1e-4),                # :101-160
+    "minmax_upper": ([-6.0, 2.3], 1e-4),                # :163-220
+    "weight_high": ([-2.2252424, 1.65], 1e-4),          # test_marker_weight.py:86-146
+    "weight_low": ([-2.2252424, 1.65], 1e-4),           # :148-206
+    "weight_ratio": ([-0.333333333333, 1.3], 1e-4),     # :208-274
+    "weight_same": ([-1.00000134, 1.65000055], 1e-4),   # :276-336
+    "weight_zero": ([-2.25, 1.65], 1e-3),               # :338-398
+    "test12_single": ([-6.0, 3.6], 1e-4),               # test12.py (driven bundle)
+}
+
+
+def _camera(b: SceneBuilder, t, r=(0.0, 0.0, 0.0)):
+    tfm, tids = b.transform(t=t, r=r)
+    cam, cids = b.camera(tfm, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
+                         film_fit=abi.FILM_FIT_HORIZONTAL, render_size=RENDER)
+    return cam, tids, cids
+
+
+def known_scene(name: str) -> Problem:
+    """Rebuild one of the reference's Maya test scenes as a flat problem."""
+    b = SceneBuilder(1)
+    if name in ("test1", "test3", "test12_single"):
+        cam, ctids, _ = _camera(b, (-1.0, 1.0, -5.0))
+        if name == "test12_single":
+            # tfm_a drives tfm_b drives the bundle: one shared attribute block.
+            ta, aids = b.transform(t=(-5.5, 6.4, -25.0))
+            btfm, _ = b.transform(t=tuple(AttrRef(a) for a in aids[:3]))
+            solve_ids = aids[:2]
+        else:
+            btfm, bids = b.transform(t=(5.5, 6.4, -25.0))
+            solve_ids = bids[:2] if name == "test1" else ctids[3:5]
+        bnd = b.bundle(btfm)
+        b.marker(cam, bnd, [[-0.243056042, 0.189583713]])
+        for a in solve_ids:
+            b.solve(a)
+        return b.build(meta={"name": name})
+    if name.startswith("minmax"):
+        cam, _, _ = _camera(b, (-1.0, 1.0, 10.0))
+        btfm, bids = b.transform()
+        bnd = b.bundle(btfm)
+        b.marker(cam, bnd, [[-0.486112083, 0.189583713]])
+        lo, hi = {"minmax_both": (-5.0, 5.0), "minmax_lower": (-5.0, None),
+                  "minmax_upper": (None, 5.0)}[name]
+        b.solve(bids[0], xmin=lo, xmax=hi)
+        b.solve(bids[1])
+        return b.build(meta={"name": name})
+    if name.startswith("weight"):
+        w1, w2 = {"weight_high": (100.0, 1.0), "weight_low": (1.0, 0.01),
+                  "weight_ratio": (100.0, 50.0), "weight_same": (0.5, 0.5),
+                  "weight_zero": (1.0, 0.0)}[name]
+        ratio = name == "weight_ratio"  # test_marker_weight.py:227-232
+        cam, _, _ = _camera(b, (0.0, 0.0, 0.0) if ratio else (-1.0, 1.0, -5.0))
+        mx = 0.097222417 if ratio else 0.243056042
+        grp, gids = b.transform(t=(0.0, 0.0, -10.0))
+        b1t, _ = b.transform(parent=grp)
+        b2t, _ = b.transform(parent=grp)
+        bnd1, bnd2 = b.bundle(b1t), b.bundle(b2t)
+        b.marker(cam, bnd1, [[-mx, 0.189583713]], weight=w1)
+        b.marker(cam, bnd2, [[mx, 0.189583713]], weight=w2)
+        b.solve(gids[0])
+        b.solve(gids[1])
+        return b.build(meta={"name": name})
+    raise KeyError(name)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configurations.
+# ---------------------------------------------------------------------------
+def _euler_xyz(rx, ry, rz):
+    """Column-vector rotation Rz @ Ry @ Rx (degrees), vectorised over frames."""
+    rx, ry, rz = (np.radians(np.asarray(v, dtype=np.float64)) for v in (rx, ry, rz))
+    cx, sx, cy, sy, cz, sz = np.cos(rx), np.sin(rx), np.cos(ry), np.sin(ry), np.cos(rz), np.sin(rz)
+    R = np.empty(rx.shape + (3, 3))
+    R[..., 0, 0] = cz * cy
+    R[..., 0, 1] = cz * sy * sx - sz * cx
+    R[..., 0, 2] = cz * sy * cx + sz * sx
+    R[..., 1, 0] = sz * cy
+    R[..., 1, 1] = sz * sy * sx + cz * cx
+    R[..., 1, 2] = sz * sy * cx - cz * sx
+    R[..., 2, 0] = -sy
+    R[..., 2, 1] = cy * sx
+    R[..., 2, 2] = cy * cx
+    return R
+
+
+def _project(cam_t, cam_r, focal, pts):
+    """True marker coordinates of world points for one camera pose
+    (pinhole, Horizontal film fit: x in film-width units, y in film-height units)."""
+    R = _euler_xyz(*cam_r)
+    pc = (pts - cam_t) @ R  # R^T (p - t)
+    depth = -pc[..., 2]
+    mx = focal * pc[..., 0] / (FILM_W_MM * depth)
+    my = focal * pc[..., 1] / (FILM_H_MM * depth)
+    return mx, my, depth
+
+
+def _lens_distort_truth(c, x, y):
+    """Forward model used only to synthesise lens-distorted markers
+    (LDPK classic map_inverse of the undistort polynomial, fixed-point)."""
+    ld, sq, cx, cy, qu = c
+    w, h = 3.6, 2.4
+    r = math.sqrt(w * w + h * h) / 2.0
+    qx, qy = x * w / r, y * h / r
+
+    def ev(px, py):
+        p02, p12 = px * px, py * py
+        fx = px * (1 + ld / sq * p02 + (ld + cx) / sq * p12 + qu / sq * p02 * p02
+                   + 2 * qu / sq * p02 * p12 + qu / sq * p12 * p12)
+        fy = py * (1 + (ld + cy) * p02 + ld * p12 + qu * p02 * p02 + 2 * qu * p02 * p12
+                   + qu * p12 * p12)
+        return fx, fy
+
+    fx, fy = ev(qx, qy)
+    px, py = qx - (fx - qx), qy - (fy - qy)
+    for _ in range(40):
+        ix, iy = ev(px, py)
+        px, py = px + qx - ix, py + qy - iy
+    return px * r / w, py * r / h
+
+
+CONFIG_NAMES = {
+    0: "c1_1cam_20bnd_50mkr_10f_lmdif",
+    1: "c2_1cam_1kbnd_5kmkr_120f_pose_focal",
+    2: "c3_10cam_10kbnd_50kmkr_500f_schur",
+    3: "c4_500pose_50kbnd_200kobs",
+    4: "c5_lens3de_2cam_2kmkr_240f",
+}
+
+
+def make_config(index: int, frames: int | None = None, scale: float = 1.0,
+                scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH) -> Problem:
+    """Concrete synthetic input for BASELINE.json ``configs[index]``.
+
+    ``frames`` / ``scale`` shrink a configuration (frame-window subsets and
+    fewer markers) for parity tests and the bounded CPU-baseline sample;
+    the defaults give the full configuration.
+    """
+    rng = np.random.Generator(np.random.PCG64(20241008 + index))
+    if index == 0:
+        return _config_c1(rng, frames or 10)
+    if index == 1:
+        return _config_c2(rng, frames or 120, scale)
+    if index == 2:
+        return _config_ba(rng, index, n_cams=10, F=frames or 500, B=int(10000 * scale),
+                          K=int(50000 * scale), window=20, per_cam_markers=True)
+    if index == 3:
+        return _config_ba(rng, index, n_cams=1, F=frames or 500, B=int(50000 * scale),
+                          K=int(50000 * scale), window=4, per_cam_markers=False)
+    if index == 4:
+        return _config_c5(rng, frames or 240, scale)
+    raise KeyError(index)
+
+
+def _camera_path(rng, F, c):
+    f = np.arange(F, dtype=np.float64)
+    phase = rng.uniform(0, 2 * math.pi, size=6)
+    t = np.stack([2.0 * c + 0.04 * f + 0.3 * np.sin(0.05 * f + phase[0]),
+                  1.5 + 0.2 * np.sin(0.03 * f + phase[1]),
+                  0.02 * f + 0.2 * np.sin(0.04 * f + phase[2])], axis=1)
+    r = np.stack([2.0 * np.sin(0.02 * f + phase[3]),
+                  -3.0 * c + 4.0 * np.sin(0.015 * f + phase[4]),
+                  1.0 * np.sin(0.025 * f + phase[5])], axis=1)
+    return t, r
+
+
+def _bundles_in_front(rng, B, depth_lo=20.0, depth_hi=200.0):
+    depth = rng.uniform(depth_lo, depth_hi, size=B)
+    x = rng.uniform(-0.35, 0.35, size=B) * depth
+    y = rng.uniform(-0.22, 0.22, size=B) * depth
+    return np.stack([x, y + 1.5, -depth], axis=1)
+
+
+def _noisy(rng, v):
+    return v + rng.normal(0.0, 0.5, size=v.shape) / IMAGE_WIDTH
+
+
+def _config_c1(rng, F):
+    """1 cam, F frames, 20 bundles, 50 markers (k -> bundle k mod 20);
+    solve bundle translate (static) + camera rotate (animated); lmdif."""
+    B, K = 20, 50
+    b = SceneBuilder(F)
+    t_true, r_true = _camera_path(rng, F, 0)
+    r_init = r_true + rng.uniform(-2.0, 2.0, size=r_true.shape)
+    tfm, tids = b.transform(t=[t_true[:, 0], t_true[:, 1], t_true[:, 2]],
+                            r=[r_init[:, 0], r_init[:, 1], r_init[:, 2]])
+    cam, _ = b.camera(tfm, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN), render_size=RENDER)
+    P = _bundles_in_front(rng, B, 20.0, 60.0)
+    P_init = P * (1.0 + rng.uniform(-0.05, 0.05, size=(B, 1)))
+    bnd_attr = []
+    for j in range(B):
+        bt, bids = b.transform(t=tuple(P_init[j]))
+        b.bundle(bt)
+        bnd_attr.append(bids[:3])
+    for k in range(K):
+        j = k % B
+        fs = np.arange(F)
+        mx, my = _pose_project(t_true, r_true, FOCAL_MM, np.repeat(P[j][None], F, 0), fs)
+        b.marker(cam, j, np.stack([_noisy(rng, mx), _noisy(rng, my)], axis=1))
+    for ids in bnd_attr:
+        for a in ids:
+            b.solve(a)
+    for a in tids[3:6]:
+        b.solve(a)
+    return b.build(meta={"name": CONFIG_NAMES[0], "solver_type": abi.SOLVER_TYPE_CMINPACK_LMDIF,
+                         "iterations": 1000})
+
+
+def _bulk_problem(F, cams_t, cams_r, cams_focal, cam_solve, bnd_init, bnd_solved, mkr_cam,
+                  mkr_bnd, obs_m, obs_f, obs_xy, lens=None, gauge_cam0=False,
+                  lens_first=False, meta=None):
+    """Vectorised problem assembly (same semantics as SceneBuilder.build)."""
+    b = SceneBuilder(F)
+    lens_ids = []
+    lens_idx = -1
+    if lens is not None:
+        lens_idx, lens_ids = b.lens_3de_classic(*lens["init"])
+    cam_attr_ids = []
+    for c in range(len(cams_t)):
+        tfm, tids = b.transform(t=[cams_t[c][:, 0], cams_t[c][:, 1], cams_t[c][:, 2]],
+                                r=[cams_r[c][:, 0], cams_r[c][:, 1], cams_r[c][:, 2]])
+        _, cids = b.camera(tfm, focal=cams_focal[c], film_back=(FILM_W_IN, FILM_H_IN),
+                           render_size=RENDER, lens=lens_idx)
+        cam_attr_ids.append((tids, cids))
+    bnd_attr_ids = []
+    for j in range(len(bnd_init)):
+        bt, bids = b.transform(t=tuple(bnd_init[j]))
+        b.bundle(bt)
+        bnd_attr_ids.append(bids[:3])
+    b.markers_bulk(mkr_cam, mkr_bnd, obs_m, obs_f, obs_xy)
+    # solve list (attribute-major)
+    if lens is not None and lens_first:
+        for slot in lens["solve_slots"]:
+            b.solve(lens_ids[slot])
+    params_excluded = set()
+    for c, (tids, cids) in enumerate(cam_attr_ids):
+        for a in cam_solve(tids, cids):
+            b.solve(a)
+            if gauge_cam0 and c == 0:
+                params_excluded.add(a)
+    for j, ids in enumerate(bnd_attr_ids):
+        if bnd_solved[j]:
+            for a in ids:
+                b.solve(a)
+    prob = b.build(meta=meta)
+    if gauge_cam0:
+        keep = ~(np.isin(prob.param_attr, list(params_excluded)) & (prob.param_frame == 0))
+        for name in ("param_attr", "param_frame", "param_min", "param_max", "param_offset",
+                     "param_scale", "x0"):
+            setattr(prob, name, np.ascontiguousarray(getattr(prob, name)[keep]))
+    return prob
+
+
+def _windows(rng, K, F, mean_len, lo=None, hi=None):
+    if lo is None:
+        length = np.clip(rng.poisson(mean_len, size=K), 2, F)
+    else:
+        length = rng.integers(lo, hi + 1, size=K)
+        length = np.minimum(length, F)
+    start = rng.integers(0, F - length + 1)
+    return start, length
+
+
+def _obs_from_windows(rng, start, length, project_fn):
+    ks = np.repeat(np.arange(start.size), length)
+    offs = np.arange(length.sum()) - np.repeat(np.cumsum(length) - length, length)
+    fs = np.repeat(start, length) + offs
+    mx, my = project_fn(ks, fs)
+    xy = np.stack([_noisy(rng, mx), _noisy(rng, my)], axis=1)
+    return ks, fs, xy
+
+
+def _pose_project(t, r, focal, pts, fs):
+    R = _euler_xyz(r[fs, 0], r[fs, 1], r[fs, 2])
+    pc = np.einsum("nij,ni->nj", R, pts - t[fs])
+    depth = -pc[:, 2]
+    fcl = focal[fs] if np.ndim(focal) else focal
+    return fcl * pc[:, 0] / (FILM_W_MM * depth), fcl * pc[:, 1] / (FILM_H_MM * depth)
+
+
+def _config_c2(rng, F, scale):
+    """1 camera, 1k locked bundles, 5k markers (k -> k mod 1000), windows U[20,60];
+    solve camera translate/rotate + focal per frame."""
+    B, K = max(1, int(1000 * scale)), max(1, int(5000 * scale))
+    t, r = _camera_path(rng, F, 0)
+    focal = FOCAL_MM * (1.0 + 0.05 * np.sin(0.02 * np.arange(F)))
+    P = _bundles_in_front(rng, B)
+    start, length = _windows(rng, K, F, None, 20, 60)
+    mkr_bnd = np.arange(K) % B
+    ks, fs, xy = _obs_from_windows(rng, start, length,
+                                   lambda ks, fs: _pose_project(t, r, focal, P[mkr_bnd[ks]], fs))
+    t0 = t + rng.uniform(-0.05, 0.05, size=t.shape)
+    r0 = r + rng.uniform(-2.0, 2.0, size=r.shape)
+    f0 = focal * (1.0 + rng.uniform(-0.05, 0.05, size=F))
+    return _bulk_problem(F, [t0], [r0], [f0],
+                         lambda tids, cids: list(tids[:6]) + [cids[abi.CAM_FOCAL_MM]],
+                         P, np.zeros(B, bool), np.zeros(K, np.int32), mkr_bnd, ks, fs, xy,
+                         meta={"name": CONFIG_NAMES[1]})
+
+
+def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers):
+    """Full BA: animated cameras (t, r per frame) + static bundles, gauge-locked."""
+    ts, rs = zip(*[_camera_path(rng, F, c) for c in range(n_cams)])
+    P = _bundles_in_front(rng, B)
+    if per_cam_markers:
+        mkr_cam = np.repeat(np.arange(n_cams), K // n_cams)
+        K = mkr_cam.size
+        mkr_bnd = np.arange(K) % B
+        start, length = _windows(rng, K, F, window)
+    else:
+        mkr_cam = np.zeros(K, np.int64)
+        mkr_bnd = np.arange(K) % B
+        length = np.full(K, window)
+        start = rng.integers(0, F - window + 1, size=K)
+
+    def proj(ks, fs):
+        mx = np.empty(ks.size)
+        my = np.empty(ks.size)
+        for c in range(n_cams):
+            sel = mkr_cam[ks] == c
+            mx[sel], my[sel] = _pose_project(ts[c], rs[c], FOCAL_MM, P[mkr_bnd[ks[sel]]], fs[sel])
+        return mx, my
+
+    ks, fs, xy = _obs_from_windows(rng, start, length, proj)
+    t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
+    r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
+    for c in (0,):  # gauge: camera-0 pose at frame 0 exact
+        t0[c][0] = ts[c][0]
+        r0[c][0] = rs[c][0]
+    P0 = P.copy()
+    ray = P0 - ts[0][0]
+    P0 = ts[0][0] + ray * (1.0 + rng.uniform(-0.05, 0.05, size=(B, 1)))
+    P0[0] = P[0]  # gauge: bundle 0 locked at truth
+    solved = np.ones(B, bool)
+    solved[0] = False
+    return _bulk_problem(F, t0, r0, [FOCAL_MM] * n_cams, lambda tids, cids: list(tids[:6]),
+                         P0, solved, mkr_cam, mkr_bnd, ks, fs, xy, gauge_cam0=True,
+                         meta={"name": CONFIG_NAMES[index]})
+
+
+def _config_c5(rng, F, scale):
+    """2 cams, 1k locked bundles, 2k markers (1k per cam), windows mean 60,
+    one shared 3DE-classic lens with distortion + quartic solved (lens attrs first)."""
+    B, K = max(1, int(1000 * scale)), max(2, int(2000 * scale))
+    ts, rs = zip(*[_camera_path(rng, F, c) for c in range(2)])
+    P = _bundles_in_front(rng, B)
+    mkr_cam = np.repeat(np.arange(2), K // 2)
+    K = mkr_cam.size
+    mkr_bnd = np.arange(K) % B
+    start, length = _windows(rng, K, F, 60)
+    lens_true = (0.05, 1.0, 0.0, 0.0, 0.01)
+
+    def proj(ks, fs):
+        mx = np.empty(ks.size)
+        my = np.empty(ks.size)
+        for c in range(2):
+            sel = mkr_cam[ks] == c
+            mx[sel], my[sel] = _pose_project(ts[c], rs[c], FOCAL_MM, P[mkr_bnd[ks[sel]]], fs[sel])
+        # Horizontal fit marker y is in film-height units; the lens works on the
+        # projected (film-fit scaled) point, see adjust_measureErrors.cpp:458-472.
+        ra = RENDER[0] / RENDER[1]
+        fa = FILM_W_MM / FILM_H_MM
+        py = my * (ra / fa)
+        dx, dy = _lens_distort_truth(lens_true, mx, py)
+        return dx, dy / (ra / fa)
+
+    ks, fs, xy = _obs_from_windows(rng, start, length, proj)
+    t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
+    r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
+    lens = {"init": (0.0, 1.0, 0.0, 0.0, 0.0), "solve_slots": (0, 4)}
+    return _bulk_problem(F, t0, r0, [FOCAL_MM, FOCAL_MM], lambda tids, cids: list(tids[:6]),
+                         P, np.zeros(B, bool), mkr_cam, mkr_bnd, ks, fs, xy, lens=lens,
+                         lens_first=True, meta={"name": CONFIG_NAMES[4]})
+
+
+def config_options(prob: Problem, scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH,
+                   **overrides):
+    """Solver options for a synthetic config (lmder, forward FD,
+    delta 1e-4, tau 1, mode 1, tolerances 1e-6; C1 uses lmdif with iterMax 1000)."""
+    from .options import make_options
+    kw = dict(solver_type=prob.meta.get("solver_type", abi.SOLVER_TYPE_CMINPACK_LMDER),
+              iterations=prob.meta.get("iterations", 1000), scene_graph_mode=scene_graph_mode,
+              image_width=IMAGE_WIDTH)
+    kw.update(overrides)
+    return make_options(**kw)

@@ -1,0 +1,237 @@
+"""ctypes binding of the CPU oracle (oracle/librefcpu.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product package never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from mayamatchmovesolver_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "librefcpu.so")
+_lib = None
+
+FCN_DER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int)
+FCN_DIF = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                      C.POINTER(C.c_double), C.c_int)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int)
+        L.ref_enorm.restype = C.c_double
+        L.ref_enorm.argtypes = [C.c_int, dp]
+        L.ref_lmder.restype = C.c_int
+        L.ref_lmder.argtypes = [FCN_DER, C.c_void_p, C.c_int, C.c_int, dp, dp, dp, C.c_int,
+                                C.c_double, C.c_double, C.c_double, C.c_int, dp, C.c_int,
+                                C.c_double, C.c_int, ip, ip, ip, dp, dp, dp, dp, dp]
+        L.ref_lmdif.restype = C.c_int
+        L.ref_lmdif.argtypes = [FCN_DIF, C.c_void_p, C.c_int, C.c_int, dp, dp,
+                                C.c_double, C.c_double, C.c_double, C.c_int, C.c_double,
+                                dp, C.c_int, C.c_double, C.c_int, ip, dp, C.c_int, ip,
+                                dp, dp, dp, dp, dp]
+        L.ref_trs_matrix.restype = None
+        L.ref_trs_matrix.argtypes = [C.c_double] * 9 + [C.c_int, dp]
+        L.ref_projection_matrix.restype = None
+        L.ref_projection_matrix.argtypes = [C.c_int] + [C.c_double] * 7 + [C.c_int, C.c_double,
+                                                                          C.c_double, dp]
+        L.ref_reproject.restype = None
+        L.ref_reproject.argtypes = [dp, dp, dp, dp]
+        for name in ("ref_lens_3de_classic_distort", "ref_lens_3de_classic_undistort"):
+            f = getattr(L, name)
+            f.restype = None
+            f.argtypes = [dp, C.c_double, C.c_double, dp, dp]
+        L.ref_measure.restype = C.c_int
+        L.ref_measure.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions), dp, dp,
+                                  dp, dp, dp]
+        L.ref_solve.restype = C.c_int
+        L.ref_solve.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions), dp, dp,
+                                dp, dp, C.POINTER(abi.MmbaResult), C.POINTER(abi.MmbaTrace)]
+        L.ref_jacobian.restype = C.c_int
+        L.ref_jacobian.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions), dp, dp,
+                                   dp]
+        for name in ("ref_param_external_to_internal", "ref_param_internal_to_external"):
+            f = getattr(L, name)
+            f.restype = C.c_double
+            f.argtypes = [C.c_double] * 5
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def enorm(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return lib().ref_enorm(x.size, _dp(x))
+
+
+def lmder(fun, jac, x0, m, ftol=1e-6, xtol=1e-6, gtol=1e-6, maxfev=1000, factor=100.0,
+          mode=1, diag=None):
+    """MINPACK lmder restatement on Python callbacks.  ``fun(x)->f[m]``,
+    ``jac(x)->J[m,n]``.  Returns (x, info, nfev, njev, trace) where trace is
+    the list of (iflag, x) call records."""
+    n = len(x0)
+    x = np.array(x0, dtype=np.float64)
+    fvec = np.zeros(m)
+    fjac = np.zeros(m * n)
+    dg = np.ones(n) if diag is None else np.array(diag, dtype=np.float64)
+    ipvt = np.zeros(n, dtype=np.int32)
+    qtf, wa1, wa2, wa3 = (np.zeros(n) for _ in range(4))
+    wa4 = np.zeros(m)
+    calls = []
+
+    def cb(_p, mm, nn, xp, fp, jp, ld, iflag):
+        xv = np.ctypeslib.as_array(xp, shape=(nn,)).copy()
+        calls.append((iflag, xv))
+        if iflag == 1:
+            np.ctypeslib.as_array(fp, shape=(mm,))[:] = fun(xv)
+        elif iflag == 2:
+            J = np.asarray(jac(xv), dtype=np.float64)
+            out = np.ctypeslib.as_array(jp, shape=(nn * ld,))
+            for j in range(nn):
+                out[j * ld:j * ld + mm] = J[:, j]
+        return 0
+
+    cfun = FCN_DER(cb)
+    nfev = C.c_int(0)
+    njev = C.c_int(0)
+    ip = ipvt.ctypes.data_as(C.POINTER(C.c_int))
+    info = lib().ref_lmder(cfun, None, m, n, _dp(x), _dp(fvec), _dp(fjac), m, ftol, xtol, gtol,
+                           maxfev, _dp(dg), mode, factor, 0, C.byref(nfev), C.byref(njev), ip,
+                           _dp(qtf), _dp(wa1), _dp(wa2), _dp(wa3), _dp(wa4))
+    return x, info, nfev.value, njev.value, calls
+
+
+def lmdif(fun, x0, m, ftol=1e-6, xtol=1e-6, gtol=1e-6, maxfev=1000, epsfcn=0.0, factor=100.0,
+          mode=1, diag=None):
+    n = len(x0)
+    x = np.array(x0, dtype=np.float64)
+    fvec = np.zeros(m)
+    fjac = np.zeros(m * n)
+    dg = np.ones(n) if diag is None else np.array(diag, dtype=np.float64)
+    ipvt = np.zeros(n, dtype=np.int32)
+    qtf, wa1, wa2, wa3 = (np.zeros(n) for _ in range(4))
+    wa4 = np.zeros(m)
+    calls = []
+
+    def cb(_p, mm, nn, xp, fp, iflag):
+        xv = np.ctypeslib.as_array(xp, shape=(nn,)).copy()
+        calls.append((iflag, xv))
+        np.ctypeslib.as_array(fp, shape=(mm,))[:] = fun(xv)
+        return 0
+
+    cfun = FCN_DIF(cb)
+    nfev = C.c_int(0)
+    ip = ipvt.ctypes.data_as(C.POINTER(C.c_int))
+    info = lib().ref_lmdif(cfun, None, m, n, _dp(x), _dp(fvec), ftol, xtol, gtol, maxfev, epsfcn,
+                           _dp(dg), mode, factor, 0, C.byref(nfev), _dp(fjac), m, ip, _dp(qtf),
+                           _dp(wa1), _dp(wa2), _dp(wa3), _dp(wa4))
+    return x, info, nfev.value, calls
+
+
+def trs_matrix(t, r, s=(1.0, 1.0, 1.0), roo=abi.ROO_XYZ):
+    out = np.zeros(16)
+    lib().ref_trs_matrix(*[float(v) for v in (*t, *r, *s)], int(roo), _dp(out))
+    return out.reshape(4, 4)
+
+
+def projection_matrix(mode, focal, fbw_inch, fbh_inch, offx=0.0, offy=0.0, image_w=2048.0,
+                      image_h=1556.0, film_fit=abi.FILM_FIT_HORIZONTAL, far_clip=10000.0,
+                      camera_scale=1.0):
+    out = np.zeros(16)
+    lib().ref_projection_matrix(int(mode), focal, fbw_inch, fbh_inch, offx, offy, image_w,
+                                image_h, int(film_fit), far_clip, camera_scale, _dp(out))
+    return out.reshape(4, 4)
+
+
+def reproject(cam_world, proj, point):
+    cw = np.ascontiguousarray(cam_world, dtype=np.float64).reshape(-1)
+    pm = np.ascontiguousarray(proj, dtype=np.float64).reshape(-1)
+    pt = np.ascontiguousarray(point, dtype=np.float64).reshape(-1)
+    out = np.zeros(2)
+    lib().ref_reproject(_dp(cw), _dp(pm), _dp(pt), _dp(out))
+    return out
+
+
+def lens_distort(coeff, x, y):
+    c = np.ascontiguousarray(coeff, dtype=np.float64)
+    ox, oy = C.c_double(), C.c_double()
+    lib().ref_lens_3de_classic_distort(_dp(c), x, y, C.byref(ox), C.byref(oy))
+    return ox.value, oy.value
+
+
+def lens_undistort(coeff, x, y):
+    c = np.ascontiguousarray(coeff, dtype=np.float64)
+    ox, oy = C.c_double(), C.c_double()
+    lib().ref_lens_3de_classic_undistort(_dp(c), x, y, C.byref(ox), C.byref(oy))
+    return ox.value, oy.value
+
+
+def _prob_opt(problem, options):
+    p, keep = problem.to_ctypes()
+    return p, keep
+
+
+def measure(problem, options, x=None):
+    p, keep = problem.to_ctypes()
+    m, M = problem.num_residuals, problem.num_obs
+    fvec, eu, ed, st = np.zeros(m), np.zeros(m), np.zeros(M), np.zeros(3)
+    xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+    rc = lib().ref_measure(C.byref(p), C.byref(options), None if xx is None else _dp(xx),
+                           _dp(fvec), _dp(eu), _dp(ed), _dp(st))
+    if rc != 0:
+        raise RuntimeError("ref_measure failed rc=%d" % rc)
+    return fvec, eu, ed, st
+
+
+def jacobian(problem, options, x):
+    p, keep = problem.to_ctypes()
+    m, n = problem.num_residuals, problem.num_params
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    fvec, fjac = np.zeros(m), np.zeros(m * n)
+    rc = lib().ref_jacobian(C.byref(p), C.byref(options), _dp(xx), _dp(fvec), _dp(fjac))
+    if rc != 0:
+        raise RuntimeError("ref_jacobian failed rc=%d" % rc)
+    return fvec, fjac.reshape(n, m).T
+
+
+def solve(problem, options, x0=None, trace_capacity=4096):
+    """Reference CPU solve.  Returns (x, fvec, err_user, err_dist, result, fnorm_trace)."""
+    p, keep = problem.to_ctypes()
+    m, M = problem.num_residuals, problem.num_obs
+    x = np.array(problem.x0 if x0 is None else x0, dtype=np.float64)
+    fvec, eu, ed = np.zeros(m), np.zeros(m), np.zeros(M)
+    res = abi.MmbaResult()
+    tbuf = np.zeros(trace_capacity)
+    tr = abi.MmbaTrace(_dp(tbuf), trace_capacity, 0)
+    rc = lib().ref_solve(C.byref(p), C.byref(options), _dp(x), _dp(fvec), _dp(eu), _dp(ed),
+                         C.byref(res), C.byref(tr))
+    if rc != 0:
+        raise RuntimeError("ref_solve failed rc=%d" % rc)
+    return x, fvec, eu, ed, res, tbuf[:min(tr.count, trace_capacity)].copy()
+
+
+def param_external_to_internal(v, xmin, xmax, off, scl):
+    return lib().ref_param_external_to_internal(v, xmin, xmax, off, scl)
+
+
+def param_internal_to_external(v, xmin, xmax, off, scl):
+    return lib().ref_param_internal_to_external(v, xmin, xmax, off, scl)
