@@ -250,6 +250,12 @@ int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out,
                       double *err_user_out, double *err_dist_out,
                       double *avg_min_max_out /* [3] */);
 
+/* Reference-layout Jacobian at internal parameters x (the fjac the reference
+ * builds in solveFunc_calculateJacobianMatrix, adjust_solveFunc.cpp:482-525):
+ * column-major num_residuals x num_params, ldfjac = num_residuals.  Dense
+ * output -- meant for tests and small problems. */
+int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac);
+
 /* Run the LM solve from internal parameters x_inout (replaces the
  * solve_3d_cminpack_* call inside solveFrames, including the initial
  * error measurement and accept-only-better logic of adjust_base.cpp:1080-1244).

@@ -1,0 +1,84 @@
+"""Loader for ``csrc/libmmba.so`` (the HIP/gfx950 product library).
+
+There is deliberately no fallback: if the library is missing or no gfx950
+device is visible, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(_HERE, "csrc")
+LIB_PATH = os.path.join(CSRC, "libmmba.so")
+_lib = None
+
+
+class MmbaError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__("mmba error %d: %s" % (code, message))
+        self.code = code
+
+
+def build(jobs=8):
+    """Compile libmmba.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", CSRC])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MmbaError(abi.MMBA_ERR_NO_DEVICE,
+                            "libmmba.so not built (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        dp = C.POINTER(C.c_double)
+        L.mmba_abi_version.restype = C.c_int
+        L.mmba_device_count.restype = C.c_int
+        L.mmba_last_error.restype = C.c_char_p
+        L.mmba_options_default.restype = None
+        L.mmba_options_default.argtypes = [C.POINTER(abi.MmbaOptions), C.c_int32]
+        for name in ("mmba_param_external_to_internal", "mmba_param_internal_to_external"):
+            f = getattr(L, name)
+            f.restype = C.c_double
+            f.argtypes = [C.c_double] * 5
+        L.mmba_context_create.restype = C.c_int
+        L.mmba_context_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.mmba_context_destroy.restype = None
+        L.mmba_context_destroy.argtypes = [C.c_void_p]
+        L.mmba_plan_create.restype = C.c_int
+        L.mmba_plan_create.argtypes = [C.c_void_p, C.POINTER(abi.MmbaProblem),
+                                       C.POINTER(abi.MmbaOptions), C.POINTER(C.c_void_p)]
+        L.mmba_plan_destroy.restype = None
+        L.mmba_plan_destroy.argtypes = [C.c_void_p]
+        L.mmba_plan_measure.restype = C.c_int
+        L.mmba_plan_measure.argtypes = [C.c_void_p, dp, dp, dp, dp, dp]
+        L.mmba_plan_jacobian.restype = C.c_int
+        L.mmba_plan_jacobian.argtypes = [C.c_void_p, dp, dp]
+        L.mmba_plan_solve.restype = C.c_int
+        L.mmba_plan_solve.argtypes = [C.c_void_p, dp, dp, dp, dp, C.POINTER(abi.MmbaResult),
+                                      C.POINTER(abi.MmbaCallbacks), C.POINTER(abi.MmbaTrace)]
+        L.mmba_solve.restype = C.c_int
+        L.mmba_solve.argtypes = [C.c_void_p, C.POINTER(abi.MmbaProblem),
+                                 C.POINTER(abi.MmbaOptions), dp, dp, dp, dp,
+                                 C.POINTER(abi.MmbaResult), C.POINTER(abi.MmbaCallbacks),
+                                 C.POINTER(abi.MmbaTrace)]
+        L.mmba_plan_kernel_stats.restype = C.c_int
+        L.mmba_plan_kernel_stats.argtypes = [C.c_void_p, C.c_int, C.POINTER(abi.MmbaKernelStats)]
+        L.mmba_comm_unique_id.restype = C.c_int
+        L.mmba_comm_unique_id.argtypes = [C.c_char_p]
+        L.mmba_plan_set_comm.restype = C.c_int
+        L.mmba_plan_set_comm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != abi.MMBA_OK:
+        msg = lib().mmba_last_error()
+        raise MmbaError(rc, msg.decode() if msg else "")
+    return rc

@@ -187,6 +187,7 @@ EXPORTED_SYMBOLS = [
     "mmba_comm_unique_id",
     "mmba_plan_set_comm",
     "mmba_plan_measure",
+    "mmba_plan_jacobian",
     "mmba_plan_solve",
     "mmba_solve",
     "mmba_plan_kernel_stats",

@@ -1,0 +1,214 @@
+// mmba_api.cpp -- extern "C" entry points declared in include/mmba.h.
+//
+// Error convention: 0 on success, negative MMBA_ERR_* on
+// failure with a message retrievable through mmba_last_error(); the MINPACK
+// info code goes to mmba_result::reason_number exactly as cminpack returns it
+// (adjust_cminpack_base.h:51-83).
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "mmba_geom.h"
+#include "mmba_plan.h"
+
+namespace mmba {
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+}  // namespace mmba
+
+using namespace mmba;
+
+#define MMBA_GUARD(body)                              \
+    try {                                             \
+        body                                          \
+    } catch (const DeviceError &) {                   \
+        return MMBA_ERR_DEVICE;                       \
+    } catch (const Unsupported &u) {                  \
+        set_error("unsupported: " + u.what);          \
+        return MMBA_ERR_UNSUPPORTED;                  \
+    } catch (const Invalid &v) {                      \
+        set_error("invalid: " + v.what);              \
+        return MMBA_ERR_INVALID;                      \
+    } catch (const std::exception &e) {               \
+        set_error(std::string("exception: ") + e.what()); \
+        return MMBA_ERR_INVALID;                      \
+    }
+
+extern "C" {
+
+int mmba_abi_version(void) { return MMBA_ABI_VERSION; }
+
+const char *mmba_last_error(void) { return g_last_error.c_str(); }
+
+int mmba_device_count(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return 0;
+    int ok = 0;
+    for (int d = 0; d < count; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++ok;
+    }
+    return ok;
+}
+
+void mmba_options_default(mmba_options *o, int32_t solver_type) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->solver_type = solver_type ? solver_type : MMBA_SOLVER_CMINPACK_LMDER;
+    o->iter_max = 100;  // CMINPACK_LM*_ITERATIONS_DEFAULT_VALUE
+    o->tau = 1.0;
+    o->eps1 = 1e-6;
+    o->eps2 = 1e-6;
+    o->eps3 = 1e-6;
+    o->delta = 1e-4;
+    o->auto_diff_type = MMBA_AUTO_DIFF_FORWARD;
+    o->auto_param_scale = 1;
+    o->scene_graph_mode = MMBA_SCENE_GRAPH_MAYA_DAG;  // SCENE_GRAPH_MODE_DEFAULT_VALUE
+    o->image_width = 2048.0;
+    o->accept_only_better = 1;
+    o->log_level = 0;
+}
+
+double mmba_param_internal_to_external(double value, double xmin, double xmax, double offset,
+                                       double scale) {
+    return int_to_ext(value, xmin, xmax, offset, scale);
+}
+
+double mmba_param_external_to_internal(double value, double xmin, double xmax, double offset,
+                                       double scale) {
+    value = value > xmin ? value : xmin;
+    value = value < xmax ? value : xmax;
+    value = (value * scale) + offset;
+    xmin = (xmin * scale) + offset;
+    xmax = (xmax * scale) + offset;
+    const double float_max = FLT_MAX;
+    if ((xmin <= float_max) && (xmax >= float_max)) return value;  // B2
+    if (xmax >= float_max) return std::sqrt(std::pow(((value - xmin) + 1.0), 2.0) - 1.0);
+    if (xmin <= -float_max) return std::sqrt(std::pow((xmax - value) + 1.0, 2.0) - 1.0);
+    return std::asin((2.0 * (value - xmin) / (xmax - xmin)) - 1.0);
+}
+
+int mmba_context_create(int device, mmba_context **out) {
+    if (!out) return MMBA_ERR_INVALID;
+    *out = nullptr;
+    if (mmba_device_count() <= 0) {
+        set_error("no gfx950 (MI355X) device visible");
+        return MMBA_ERR_NO_DEVICE;
+    }
+    MMBA_GUARD({
+        auto *c = new mmba_context();
+        c->device = device;
+        MMBA_HIP(hipSetDevice(device));
+        MMBA_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        *out = c;
+        return MMBA_OK;
+    })
+}
+
+void mmba_context_destroy(mmba_context *ctx) {
+    if (!ctx) return;
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int mmba_plan_create(mmba_context *ctx, const mmba_problem *prob, const mmba_options *opt,
+                     mmba_plan **out) {
+    if (!ctx || !prob || !opt || !out) return MMBA_ERR_INVALID;
+    *out = nullptr;
+    mmba_plan *p = new mmba_plan();
+    int rc = [&]() -> int {
+        MMBA_GUARD({
+            MMBA_HIP(hipSetDevice(ctx->device));
+            p->impl.ctx = ctx;
+            p->impl.build(prob, opt);
+            return MMBA_OK;
+        })
+    }();
+    if (rc != MMBA_OK) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return MMBA_OK;
+}
+
+void mmba_plan_destroy(mmba_plan *plan) { delete plan; }
+
+int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out, double *err_user_out,
+                      double *err_dist_out, double *avg_min_max_out) {
+    if (!plan) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        return plan->impl.measure(x, fvec_out, err_user_out, err_dist_out, avg_min_max_out);
+    })
+}
+
+int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac) {
+    if (!plan || !x || !fjac) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        return plan->impl.dense_jacobian(x, fjac);
+    })
+}
+
+int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *err_user_out,
+                    double *err_dist_out, mmba_result *res, const mmba_callbacks *cb,
+                    mmba_trace *trace) {
+    if (!plan || !x_inout) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        return plan->impl.solve(x_inout, fvec_out, err_user_out, err_dist_out, res, cb, trace);
+    })
+}
+
+int mmba_solve(mmba_context *ctx, const mmba_problem *prob, const mmba_options *opt,
+               double *x_inout, double *fvec_out, double *err_user_out, double *err_dist_out,
+               mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {
+    mmba_plan *plan = nullptr;
+    int rc = mmba_plan_create(ctx, prob, opt, &plan);
+    if (rc != MMBA_OK) return rc;
+    rc = mmba_plan_solve(plan, x_inout, fvec_out, err_user_out, err_dist_out, res, cb, trace);
+    mmba_plan_destroy(plan);
+    return rc;
+}
+
+int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats *out) {
+    if (!plan) return MMBA_ERR_INVALID;
+    Plan &p = plan->impl;
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        out->jac_launches = p.jac_n;
+        out->jac_ms_avg = p.jac_n ? p.jac_ms / p.jac_n : 0.;
+        out->resid_launches = p.resid_n;
+        out->resid_ms_avg = p.resid_n ? p.resid_ms / p.resid_n : 0.;
+        out->chol_launches = p.chol_n;
+        out->chol_ms_avg = p.chol_n ? p.chol_ms / p.chol_n : 0.;
+        out->reduced_dim = p.nR;
+        // Algorithmic bytes: B_J = 48 + 8 p_c p_b per observation
+        // for the Jacobian + normal-equation pass, B_f = 48 per observation for
+        // the residual pass.
+        double bj = 0.;
+        {
+            // average p_c * p_b over observations, from the plan structure
+            const double pc = p.ncf ? (double)p.nCF / p.ncf : 0.;
+            const double pb = p.nB ? 3.0 * p.nB_solved / p.nB : 0.;
+            bj = 48.0 + 8.0 * pc * pb;
+        }
+        out->jac_bytes = bj * p.M;
+        out->resid_bytes = 48.0 * p.M;
+        out->chol_flops = (double)p.nRpad * p.nRpad * p.nRpad / 3.0;
+    }
+    p.timing = enable_timing != 0;
+    if (enable_timing) {
+        p.jac_ms = p.resid_ms = p.chol_ms = 0.;
+        p.jac_n = p.resid_n = p.chol_n = 0;
+    }
+    return MMBA_OK;
+}
+
+int mmba_comm_unique_id(unsigned char out_id[128]);
+int mmba_plan_set_comm(mmba_plan *plan, int rank, int nranks, const unsigned char unique_id[128]);
+
+}  // extern "C"

@@ -1,0 +1,445 @@
+// mmba_geom.h -- per-element geometry of the reference residual, as device code.
+//
+// Arithmetic follows (operation for operation, compiled with
+// -ffp-contract=off so no FMA is introduced):
+//   TRS matrix            lib/rust/mmscenegraph/src/math/transform.rs:338-452
+//   world matrices        math/dag.rs:234-327 (parent_world * local)
+//   projection matrix     math/camera.rs:153-327 (MMSG) /
+//                         src/mmSolver/mayahelper/maya_camera.cpp:75-414 (Maya DAG)
+//   reprojection          math/reprojection.rs:28-63 ((P * C^-1) * B, /w, *0.5)
+//   marker film fit       scene/flat.rs:73-97, maya_camera.cpp:213-330
+//   residual              src/mmSolver/adjust/adjust_measureErrors.cpp:231-292 (DAG),
+//                         :444-499 (MMSG)
+//   3DE classic distort   lib/cppbind/mmlens/src/lens_model_3de_classic.cpp:75-113,
+//                         distortion_operations.h:34-96, include/mmlens/lib.h:36-75,
+//                         LDPK classic_3de_mixed_distortion + generic map_inverse
+#pragma once
+
+#include "mmba_internal.h"
+
+namespace mmba {
+
+#define MMBA_DEV __device__ __forceinline__
+
+constexpr double DEG2RAD = 0.017453292519943295;
+constexpr double MM_TO_INCH = 0.03937007874015748;
+constexpr double INCH_TO_MM = 25.4;
+constexpr double MM_TO_CM = 0.1;
+constexpr int MAX_DEPTH = 16;
+
+// One attribute override: the perturbed parameter of an FD column.
+struct Override {
+    int attr;
+    double value;
+};
+
+MMBA_DEV double attr_get(const DevProblem &P, int a, int f, double dflt,
+                         const Override &ov) {
+    if (a < 0) return dflt;
+    if (a == ov.attr) return ov.value;
+    return P.attr_anim[a] ? P.attr_val[P.attr_off[a] + f] : P.attr_val[P.attr_off[a]];
+}
+
+MMBA_DEV void mat4_mul(const double *a, const double *b, double *out) {
+    double t[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            t[r * 4 + c] = a[r * 4 + 0] * b[0 * 4 + c] + a[r * 4 + 1] * b[1 * 4 + c] +
+                           a[r * 4 + 2] * b[2 * 4 + c] + a[r * 4 + 3] * b[3 * 4 + c];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[i] = t[i];
+}
+
+MMBA_DEV void mat4_inverse(const double *m, double *out) {
+    double inv[16];
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] +
+             m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] -
+             m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] +
+             m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] -
+              m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] -
+             m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] +
+             m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] -
+             m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] +
+              m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] +
+             m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] -
+             m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] +
+              m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] -
+              m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] -
+             m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] +
+             m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] -
+              m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] +
+              m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    if (det == 0.) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) out[i] = (i % 5 == 0) ? 1. : 0.;
+        return;
+    }
+    double inv_det = 1.0 / det;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[i] = inv[i] * inv_det;
+}
+
+MMBA_DEV void trs_matrix(double tx, double ty, double tz, double rx, double ry,
+                         double rz, double sx, double sy, double sz, int roo,
+                         double *out) {
+    double srx, crx, sry, cry, srz, crz;
+    srx = sin(rx * DEG2RAD);
+    crx = cos(rx * DEG2RAD);
+    sry = sin(ry * DEG2RAD);
+    cry = cos(ry * DEG2RAD);
+    srz = sin(rz * DEG2RAD);
+    crz = cos(rz * DEG2RAD);
+    const double RX[16] = {1, 0, 0, 0, 0, crx, -srx, 0, 0, srx, crx, 0, 0, 0, 0, 1};
+    const double RY[16] = {cry, 0, sry, 0, 0, 1, 0, 0, -sry, 0, cry, 0, 0, 0, 0, 1};
+    const double RZ[16] = {crz, -srz, 0, 0, srz, crz, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    const double S[16] = {sx, 0, 0, 0, 0, sy, 0, 0, 0, 0, sz, 0, 0, 0, 0, 1};
+    const double T[16] = {1, 0, 0, tx, 0, 1, 0, ty, 0, 0, 1, tz, 0, 0, 0, 1};
+    const double *a, *b, *c;
+    switch (roo) {
+        default:
+        case MMBA_ROO_XYZ: a = RZ; b = RY; c = RX; break;
+        case MMBA_ROO_YZX: a = RX; b = RZ; c = RY; break;
+        case MMBA_ROO_ZXY: a = RY; b = RX; c = RZ; break;
+        case MMBA_ROO_XZY: a = RY; b = RZ; c = RX; break;
+        case MMBA_ROO_YXZ: a = RZ; b = RX; c = RY; break;
+        case MMBA_ROO_ZYX: a = RX; b = RY; c = RZ; break;
+    }
+    double R[16];
+    mat4_mul(a, b, R);
+    mat4_mul(R, c, R);
+    mat4_mul(T, R, out);
+    mat4_mul(out, S, out);
+}
+
+MMBA_DEV void local_matrix(const DevProblem &P, int t, int f, const Override &ov,
+                           double *out) {
+    const int *ta = &P.tfm_attrs[9 * t];
+    trs_matrix(attr_get(P, ta[0], f, 0., ov), attr_get(P, ta[1], f, 0., ov),
+               attr_get(P, ta[2], f, 0., ov), attr_get(P, ta[3], f, 0., ov),
+               attr_get(P, ta[4], f, 0., ov), attr_get(P, ta[5], f, 0., ov),
+               attr_get(P, ta[6], f, 1., ov), attr_get(P, ta[7], f, 1., ov),
+               attr_get(P, ta[8], f, 1., ov), P.tfm_roo[t], out);
+}
+
+// World matrix of transform t at frame f: root-first products (dag.rs:293-313).
+MMBA_DEV void world_matrix(const DevProblem &P, int t, int f, const Override &ov,
+                           double *W) {
+    int chain[MAX_DEPTH];
+    int d = 0;
+    for (int u = t; u >= 0 && d < MAX_DEPTH; u = P.tfm_parent[u]) chain[d++] = u;
+    local_matrix(P, chain[d - 1], f, ov, W);
+    for (int j = d - 2; j >= 0; --j) {
+        double L[16];
+        local_matrix(P, chain[j], f, ov, L);
+        mat4_mul(W, L, W);
+    }
+}
+
+// Bundle world position = column 3 of world matrix (flat.rs:317-321 uses B[:,3]).
+MMBA_DEV void bundle_position(const DevProblem &P, int b, int f, const Override &ov,
+                              double *pos) {
+    const int t = P.bnd_tfm[b];
+    const int *ta = &P.tfm_attrs[9 * t];
+    double tx = attr_get(P, ta[0], f, 0., ov);
+    double ty = attr_get(P, ta[1], f, 0., ov);
+    double tz = attr_get(P, ta[2], f, 0., ov);
+    const int parent = P.tfm_parent[t];
+    if (parent < 0) {
+        pos[0] = tx;
+        pos[1] = ty;
+        pos[2] = tz;
+        return;
+    }
+    double W[16];
+    world_matrix(P, parent, f, ov, W);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        pos[r] = W[r * 4 + 0] * tx + W[r * 4 + 1] * ty + W[r * 4 + 2] * tz + W[r * 4 + 3] * 1.0;
+}
+
+// Projection matrix in column-vector convention; see oracle/refcpu.c
+// ref_projection_matrix for the mode differences (Appendix B5/B6).
+MMBA_DEV void projection_matrix(int mode, double focal_mm, double fbw_inch,
+                                double fbh_inch, double offx_inch, double offy_inch,
+                                double image_w, double image_h, int film_fit,
+                                double far_clip, double camera_scale, double *P) {
+    const double near_clip = 0.1;
+    double film_aspect = fbw_inch / fbh_inch;
+    double image_aspect = image_w / image_h;
+    double film_w_mm = fbw_inch * INCH_TO_MM, film_h_mm = fbh_inch * INCH_TO_MM;
+    double off_x_mm = offx_inch * INCH_TO_MM, off_y_mm = offy_inch * INCH_TO_MM;
+    double ftn = (near_clip / focal_mm) * camera_scale;
+    double right = ftn * (0.5 * film_w_mm + off_x_mm);
+    double left = ftn * (-0.5 * film_w_mm + off_x_mm);
+    double top = ftn * (0.5 * film_h_mm + off_y_mm);
+    double bottom = ftn * (-0.5 * film_h_mm + off_y_mm);
+    double fsx = 1., fsy = 1., size_x = 0., size_y = 0.;
+    const bool rust = (mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH);
+    switch (film_fit) {
+        default:
+        case MMBA_FILM_FIT_HORIZONTAL:
+            if (rust)
+                fsx = image_aspect / film_aspect;
+            else
+                fsy = image_aspect / film_aspect;
+            size_x = right - left;
+            size_y = size_x / image_aspect;
+            break;
+        case MMBA_FILM_FIT_VERTICAL:
+            fsx = 1.0 / (image_aspect / film_aspect);
+            size_y = top - bottom;
+            size_x = size_y * image_aspect;
+            break;
+        case MMBA_FILM_FIT_FILL:
+            if (film_aspect > image_aspect) {
+                fsx = film_aspect / image_aspect;
+                size_y = top - bottom;
+                size_x = size_y * image_aspect;
+            } else {
+                fsy = image_aspect / film_aspect;
+                size_x = right - left;
+                size_y = (size_x * (film_aspect / image_aspect)) / film_aspect;
+            }
+            break;
+        case MMBA_FILM_FIT_OVERSCAN:
+            if (film_aspect > image_aspect) {
+                fsy = image_aspect / film_aspect;
+                size_x = right - left;
+                size_y = (right - left) / image_aspect;
+            } else {
+                fsx = film_aspect / image_aspect;
+                size_x = (right - left) * (image_aspect / film_aspect);
+                size_y = top - bottom;
+            }
+            break;
+    }
+    right *= fsx;
+    left *= fsx;
+    top *= fsy;
+    bottom *= fsy;
+    double p00 = 1.0 / (size_x * 0.5) * MM_TO_CM;
+    double p11 = 1.0 / (size_y * 0.5) * MM_TO_CM;
+    double ox = (right + left) / (right - left) * fsx;
+    double oy = (top + bottom) / (top - bottom) * fsy;
+    double zz = (far_clip + near_clip) / (far_clip - near_clip);
+    double zw = 2.0 * far_clip * near_clip / (far_clip - near_clip);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) P[i] = 0.;
+    P[0] = p00;
+    P[5] = p11;
+    if (rust) {
+        P[8] = ox;
+        P[9] = oy;
+        P[10] = zz;
+        P[11] = zw;
+        P[14] = -1.;
+    } else {
+        P[2] = ox;
+        P[6] = oy;
+        P[10] = zz;
+        P[14] = -1.;
+        P[11] = zw;
+    }
+}
+
+// Camera-frame record: rows 0,1,3 of P*C^-1 (12), camera position (3),
+// normalised forward direction (3), marker film-fit factors (2).
+MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &ov,
+                            double *rec) {
+    const int *ca = &P.cam_attrs[MMBA_CAM_NUM_ATTRS * c];
+    double w = attr_get(P, ca[MMBA_CAM_FILM_BACK_W_INCH], f, 36.0 / 25.4, ov);
+    double h = attr_get(P, ca[MMBA_CAM_FILM_BACK_H_INCH], f, 24.0 / 25.4, ov);
+    double ox = attr_get(P, ca[MMBA_CAM_FILM_OFFSET_X_INCH], f, 0., ov);
+    double oy = attr_get(P, ca[MMBA_CAM_FILM_OFFSET_Y_INCH], f, 0., ov);
+    double fbw, fbh, offx, offy, fa;
+    if (P.mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        double w_mm = w * 25.4, h_mm = h * 25.4;
+        fbw = w_mm * MM_TO_INCH;
+        fbh = h_mm * MM_TO_INCH;
+        offx = (ox * 25.4) * MM_TO_INCH;
+        offy = (oy * 25.4) * MM_TO_INCH;
+        fa = w_mm / h_mm;
+    } else {
+        fbw = w;
+        fbh = h;
+        offx = ox;
+        offy = oy;
+        fa = w / h;
+    }
+    double focal = attr_get(P, ca[MMBA_CAM_FOCAL_MM], f, 35.0, ov);
+    double far_clip = attr_get(P, ca[MMBA_CAM_FAR_CLIP], f, 10000.0, ov);
+    double cscale = attr_get(P, ca[MMBA_CAM_SCALE], f, 1.0, ov);
+    double iw = (double)P.cam_size[2 * c];
+    double ih = (double)P.cam_size[2 * c + 1];
+    double Pm[16];
+    const int fit = P.cam_fit[c];
+    projection_matrix(P.mode, focal, fbw, fbh, offx, offy, iw, ih, fit, far_clip, cscale, Pm);
+    double ra = iw / ih;
+    double W[16], Ci[16], PV[16];
+    world_matrix(P, P.cam_tfm[c], f, ov, W);
+    mat4_inverse(W, Ci);
+    mat4_mul(Pm, Ci, PV);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rec[k] = PV[k];
+        rec[4 + k] = PV[4 + k];
+        rec[8 + k] = PV[12 + k];
+    }
+    rec[12] = W[3] / W[15];
+    rec[13] = W[7] / W[15];
+    rec[14] = W[11] / W[15];
+    double cdir[3] = {-W[2], -W[6], -W[10]};
+    double cl = sqrt(cdir[0] * cdir[0] + cdir[1] * cdir[1] + cdir[2] * cdir[2]);
+    rec[15] = cdir[0] / cl;
+    rec[16] = cdir[1] / cl;
+    rec[17] = cdir[2] / cl;
+    // marker film-fit factors (x *= rec[18], y *= rec[19])
+    double sx = 1.0, sy = 1.0;
+    switch (fit) {
+        case MMBA_FILM_FIT_HORIZONTAL: sy = ra / fa; break;
+        case MMBA_FILM_FIT_VERTICAL: sx = 1.0 / (ra / fa); break;
+        case MMBA_FILM_FIT_FILL:
+            if (fa > ra) sx = fa / ra; else sy = ra / fa;
+            break;
+        case MMBA_FILM_FIT_OVERSCAN:
+            if (fa > ra) sy = ra / fa; else sx = fa / ra;
+            break;
+        default: break;
+    }
+    rec[18] = sx;
+    rec[19] = sy;
+}
+
+// ---- LDPK classic 3DE model (undistort polynomial + fixed-point inverse) ----
+MMBA_DEV void lens_eval(const double *c, double px, double py, double &qx, double &qy) {
+    const double ld = c[0], sq = c[1], cx = c[2], cy = c[3], qu = c[4];
+    const double cxx = ld / sq, cxy = (ld + cx) / sq, cyx = ld + cy, cyy = ld;
+    const double cxxx = qu / sq, cxxy = 2.0 * qu / sq, cxyy = qu / sq;
+    const double cyxx = qu, cyyx = 2.0 * qu, cyyy = qu;
+    double p0_2 = px * px, p1_2 = py * py;
+    double p0_4 = p0_2 * p0_2, p1_4 = p1_2 * p1_2, p01_2 = p0_2 * p1_2;
+    qx = px * (1 + cxx * p0_2 + cxy * p1_2 + cxxx * p0_4 + cxxy * p01_2 + cxyy * p1_4);
+    qy = py * (1 + cyx * p0_2 + cyy * p1_2 + cyxx * p0_4 + cyyx * p01_2 + cyyy * p1_4);
+}
+
+MMBA_DEV void lens_distort(const double *coeff, double x, double y, double &ox, double &oy) {
+    const double w = 3.6, h = 2.4;  // LensModel defaults (lens_model.h:42)
+    const double r = sqrt(w * w + h * h) / 2.0;
+    double ux = x + 0.5, uy = y + 0.5;
+    double qx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
+    double qy = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+    double fx, fy;
+    lens_eval(coeff, qx, qy, fx, fy);
+    double px = qx - (fx - qx), py = qy - (fy - qy);
+    for (int i = 0; i < 20; ++i) {
+        double ix, iy;
+        lens_eval(coeff, px, py, ix, iy);
+        px = px + qx - ix;
+        py = py + qy - iy;
+        double dx = ix - qx, dy = iy - qy;
+        if (sqrt(dx * dx + dy * dy) < 1e-6) break;
+    }
+    for (int i = 0; i < 2; ++i) {
+        double ix, iy;
+        lens_eval(coeff, px, py, ix, iy);
+        px = px + qx - ix;
+        py = py + qy - iy;
+    }
+    double cxm = px * r + ((w / 2) + 0.0);
+    double cym = py * r + ((h / 2) + 0.0);
+    ox = cxm / w - 0.5;
+    oy = cym / h - 0.5;
+}
+
+struct Resid {
+    double ex, ey;    // weighted errors (fvec)
+    double ux, uy;    // user deviation (errorList)
+    double dist;      // errorDistanceList
+};
+
+// One observation's residual from a camera record and a bundle position.
+MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, double mkr_y,
+                        double sqrtw, int mode, double image_width, bool has_lens,
+                        const double *lens) {
+    double sp0 = rec[0] * bp[0] + rec[1] * bp[1] + rec[2] * bp[2] + rec[3];
+    double sp1 = rec[4] * bp[0] + rec[5] * bp[1] + rec[6] * bp[2] + rec[7];
+    double sp3 = rec[8] * bp[0] + rec[9] * bp[1] + rec[10] * bp[2] + rec[11];
+    double point_x = (sp0 / sp3) * 0.5;
+    double point_y = (sp1 / sp3) * 0.5;
+    mkr_x *= rec[18];
+    mkr_y *= rec[19];
+    double factor = 1.0;
+    if (mode != MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        double bd0 = bp[0] - rec[12], bd1 = bp[1] - rec[13], bd2 = bp[2] - rec[14];
+        double bl = sqrt(bd0 * bd0 + bd1 * bd1 + bd2 * bd2);
+        double dot = rec[15] * (bd0 / bl) + rec[16] * (bd1 / bl) + rec[17] * (bd2 / bl);
+        if (dot < 0.0) factor = 1e+6;
+    }
+    if (has_lens) {
+        double ox, oy;
+        lens_distort(lens, point_x, point_y, ox, oy);
+        if (isfinite(ox)) point_x = ox;
+        if (isfinite(oy)) point_y = oy;
+    }
+    double dx = fabs(mkr_x - point_x), dy = fabs(mkr_y - point_y);
+    double dxp = dx * image_width, dyp = dy * image_width;
+    Resid r;
+    r.ex = dxp * sqrtw * factor;
+    r.ey = dyp * sqrtw * factor;
+    r.ux = dxp * factor;
+    r.uy = dyp * factor;
+    r.dist = sqrt((dx * dx) + (dy * dy)) * image_width;
+    return r;
+}
+
+MMBA_DEV void lens_coeffs(const DevProblem &P, int lens, int f, const Override &ov,
+                          double *c) {
+    const int *la = &P.lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
+    c[0] = attr_get(P, la[0], f, 0., ov);
+    c[1] = attr_get(P, la[1], f, 1., ov);
+    c[2] = attr_get(P, la[2], f, 0., ov);
+    c[3] = attr_get(P, la[3], f, 0., ov);
+    c[4] = attr_get(P, la[4], f, 0., ov);
+}
+
+// Box-constraint reparametrisation (adjust_base.cpp:194-220).
+__host__ __device__ inline double int_to_ext(double value, double xmin, double xmax,
+                                             double offset, double scale) {
+    const double float_max = 3.40282346638528859811704183484516925440e+38;
+    if ((xmin <= -float_max) && (xmax >= float_max)) {
+        value = (value / scale) - offset;
+        value = value > xmin ? value : xmin;
+        value = value < xmax ? value : xmax;
+        return value;
+    } else if (xmax >= float_max) {
+        value = xmin - (1.0 + sqrt(value * value + 1.0));
+    } else if (xmin <= -float_max) {
+        value = xmax + (1.0 - sqrt(value * value + 1.0));
+    } else {
+        value = xmin + ((xmax - xmin) / 2.0) * (sin(value) + 1.0);
+    }
+    value = (value / scale) - offset;
+    value = value > xmin ? value : xmin;
+    value = value < xmax ? value : xmax;
+    return value;
+}
+
+}  // namespace mmba

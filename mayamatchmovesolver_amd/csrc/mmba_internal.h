@@ -1,0 +1,69 @@
+// mmba_internal.h -- shared host/device definitions of the MI355X BA core.
+//
+// Data layout in HBM (all fp64 unless noted, int32 indices):
+//   problem tables   attr block (offset/animated/values), transforms, cameras,
+//                    lenses, bundles: small, read through L2.
+//   observations     device order = sorted by camera-frame ("cf"), so every
+//                    cf owns a contiguous segment; SoA arrays obs_* [M].
+//   Jacobian blocks  J[(2*l + r) * M + i]: local column l (<= LMAX), residual
+//                    row r (x/y) of observation i; jcol[l * M + i] = param id.
+//   normal equations per-cf dense blocks Acc[cf][PCMAX][PCMAX], per-bundle
+//                    Abb[b][3][3], globals Agg[NG][NG], couplings Acg/Abg.
+//   reduced system   S over R = {cf params} + {globals}, stored as 64x64
+//                    lower tiles (only structurally non-zero tiles allocated).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mmba.h"
+
+namespace mmba {
+
+constexpr int PCMAX = 10;   // params per camera-frame block
+constexpr int PBMAX = 3;    // params per bundle block
+constexpr int NGMAX = 16;   // global parameters
+constexpr int LMAX = 20;    // local Jacobian columns per observation
+constexpr int TILE = 64;    // reduced-system tile edge
+constexpr int CAMREC = 20;  // doubles per camera-frame record
+
+// Parameter classes.
+enum ParamClass : int { PC_CF = 0, PC_B = 1, PC_G = 2 };
+
+// Flags on camera-variant entries.
+enum VarFlags : int { VF_BUNDLE_SIDE = 1 };
+
+// Device view of the problem + derived structure (all device pointers).
+struct DevProblem {
+    int F, nA, nT, nC, nL, nB, nK, M, n, ncf, nR, nG, mode;
+    double image_width;
+    const int64_t *attr_off;
+    const int *attr_anim;
+    double *attr_val;  // working copy (setParameters target)
+    const int *tfm_parent, *tfm_roo, *tfm_attrs;
+    const int *cam_tfm, *cam_attrs, *cam_fit, *cam_size, *cam_lens;
+    const int *lens_attrs, *lens_type;
+    const int *bnd_tfm;
+    // observations (device order)
+    const int *obs_cf, *obs_bnd, *obs_frame, *obs_cam;
+    const double *obs_xy, *obs_sqrtw;
+    // camera-frame structure
+    const int *cf_cam, *cf_frame, *cf_obs_off, *cf_var_off, *cf_var_param, *cf_var_flags;
+    const int *cf_pc, *cf_roff;  // CF-block size and offset in R
+    // bundle-side parameter lists (B-class first, then bundle-side globals)
+    const int *bnd_par_off, *bnd_par;
+    const int *bnd_pb;     // B-block size
+    const int *bnd_xoff;   // offset of the B block in x (param ids are contiguous? no: list)
+    const int *bobs_off, *bobs;  // observations grouped by bundle
+    // per camera lens parameter lists
+    const int *cam_lpar_off, *cam_lpar;
+    // parameters
+    const int *p_attr, *p_frame, *p_class, *p_pos, *p_both, *p_blk;
+    const double *p_min, *p_max, *p_off, *p_scale;
+    const int *g_param;  // global index -> param id
+};
+
+}  // namespace mmba

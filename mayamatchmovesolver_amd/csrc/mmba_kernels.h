@@ -1,0 +1,68 @@
+// mmba_kernels.h -- host launch wrappers for the kernels in mmba_kernels.hip.
+#pragma once
+
+#include "mmba_internal.h"
+
+namespace mmba {
+
+void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, double *ext,
+                       double *ext_pert, double *step, int solver_type, double delta,
+                       double eps_dif);
+void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext);
+void launch_cam_records(hipStream_t s, const DevProblem &P, const int *var_cf,
+                        const double *ext_pert, double *recs, int nvar, int base_only);
+int residual_blocks(const DevProblem &P);
+void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
+                     double *ed, double *partial);
+void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
+                     const double *ext_pert, const double *step, int solver_type, double *J,
+                     int *jcol, int *nloc, const int *stale_param, double *eu, double *ed);
+void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
+               const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
+               double *Abg, double *Agg, double *g, double *glob_partial, int glob_chunk,
+               double *acnorm);
+void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
+                          const double *Abg, const double *g, const double *diag, double lam,
+                          double *Lb, double *tb, double *Wg, int *fail);
+void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
+                      double *W);
+void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
+                       const double *Agg, const double *g, const double *diag, double lam,
+                       double *S, const int *slot, int NT, double *rhs);
+void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                        const double *tb, double *S, const int *slot, int NT, double *rhs);
+void launch_chol_panel(hipStream_t s, double *S, const int *slot, int NT, int k, const int *rows,
+                       int nrows, double *Linv, int *fail);
+void launch_chol_update(hipStream_t s, double *S, const int *slot, int NT, int k,
+                        const int2 *pairs, int npairs);
+void launch_trsv_fwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
+                     const int *rows, int nrows, const double *Linv, double *r, double *y);
+void launch_trsv_bwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
+                     const int *cols, int ncols, const double *Linv, double *y, double *x);
+void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                           const double *tb, const double *Lb, const double *xR, double *x);
+void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);
+void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                          const double *Lb, const double *v, double *wR, double *usq);
+void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double *vR, int nRpad);
+void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
+                  int nparts, double *out);
+void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
+                      int nparts, double *out);
+void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out);
+void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
+                  double *partial, int nparts, double *out);
+void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
+                     const int *nloc, const double *p, double *partial, int nparts,
+                     double *out);
+void launch_lm_step(hipStream_t s, int n, const double *xs, const double *x, const double *diag,
+                    double *wa1, double *wa2, double *wa3);
+void launch_diag_init(hipStream_t s, int n, const double *acnorm, double *diag, int first,
+                      int mode);
+void launch_newton_v(hipStream_t s, int n, const double *diag, const double *x, double dxnorm,
+                     double *v);
+void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const double *f2,
+                      const double *eu2, const double *ed, double *f2o, double *eu2o,
+                      double *edo);
+
+}  // namespace mmba

@@ -1,0 +1,1251 @@
+// mmba_kernels.hip -- CDNA4 (gfx950) kernels of the bundle-adjustment core.
+//
+// Roofline classes:
+//   k_residual, k_jacobian, k_ne_*   HBM / latency bound, one thread per
+//                                    observation or per block, coalesced SoA.
+//   k_chol_update                    fp64 MFMA (v_mfma_f64_16x16x4_f64),
+//                                    64x64 tiles staged in LDS.
+//   everything else                  small O(n) vector work.
+#include "mmba_geom.h"
+#include "mmba_kernels.h"
+
+namespace mmba {
+
+// -------------------------------------------------------------------------
+// Parameters: external values, FD perturbations (adjust_solveFunc.cpp:148-180,
+// cminpack fdjac2), setParameters (adjust_setParameters.cpp:174-250).
+// -------------------------------------------------------------------------
+__global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double *ext,
+                             double *ext_pert, double *step, int solver_type, double delta,
+                             double eps_dif) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    const double xmin = P.p_min[p], xmax = P.p_max[p], off = P.p_off[p], sc = P.p_scale[p];
+    const double v = x[p];
+    ext[p] = int_to_ext(v, xmin, xmax, off, sc);
+    double xp;
+    if (solver_type == MMBA_SOLVER_CMINPACK_LMDER) {
+        double sign = 1.0;
+        if ((v + delta) > xmax) sign = -1;
+        if ((v - delta) < xmin) sign = 1;
+        double d = delta * sign;
+        xp = v + d;
+        step[p] = 1.0 / d;  // inv_delta, multiplied (adjust_solveFunc.cpp:395-402)
+    } else {
+        double h = eps_dif * fabs(v);
+        if (h == 0.) h = eps_dif;
+        xp = v + h;
+        step[p] = h;  // divided (fdjac2)
+    }
+    ext_pert[p] = int_to_ext(xp, xmin, xmax, off, sc);
+}
+
+__global__ void k_set_attrs(DevProblem P, const double *__restrict__ ext) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    const int a = P.p_attr[p];
+    const int f = P.p_frame[p];
+    const int64_t idx = P.attr_off[a] + (P.attr_anim[a] ? (f < 0 ? 0 : f) : 0);
+    P.attr_val[idx] = ext[p];
+}
+
+// -------------------------------------------------------------------------
+// Camera-frame records: variant 0 = base, variant v = one cam-side parameter
+// perturbed (K0 in SURVEY 7).
+// -------------------------------------------------------------------------
+__global__ void k_cam_records(DevProblem P, const int *__restrict__ var_cf,
+                              const double *__restrict__ ext_pert, double *recs, int nvar,
+                              int base_only) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    int cf, idx;
+    if (base_only) {
+        if (t >= P.ncf) return;
+        cf = t;
+        idx = P.cf_var_off[cf];
+    } else {
+        if (t >= nvar) return;
+        idx = t;
+        cf = var_cf[t];
+    }
+    Override ov{-1, 0.};
+    const int p = P.cf_var_param[idx];
+    if (p >= 0) {
+        ov.attr = P.p_attr[p];
+        ov.value = ext_pert[p];
+    }
+    camera_record(P, P.cf_cam[cf], P.cf_frame[cf], ov, &recs[(size_t)idx * CAMREC]);
+}
+
+__device__ __forceinline__ bool obs_lens(const DevProblem &P, int cam, int &lens) {
+    if (!P.cam_lens) return false;
+    lens = P.cam_lens[cam];
+    return lens >= 0 && P.lens_type[lens] == MMBA_LENS_3DE_CLASSIC;
+}
+
+// -------------------------------------------------------------------------
+// Residuals (measureErrors).  Writes f (device order), user deviation and
+// distance, and one partial sum of squares per block.
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__restrict__ recs,
+                                                  double *f, double *eu, double *ed,
+                                                  double *partial) {
+    __shared__ double red[256];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0.;
+    if (i < P.M) {
+        const int cf = P.obs_cf[i];
+        const int b = P.obs_bnd[i];
+        const int fr = P.obs_frame[i];
+        const int cam = P.obs_cam[i];
+        const Override none{-1, 0.};
+        double bp[3];
+        bundle_position(P, b, fr, none, bp);
+        double lc[5];
+        int lens;
+        const bool hl = obs_lens(P, cam, lens);
+        if (hl) lens_coeffs(P, lens, fr, none, lc);
+        const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
+        Resid r = residual(rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i], P.mode,
+                           P.image_width, hl, lc);
+        f[2 * i] = r.ex;
+        f[2 * i + 1] = r.ey;
+        if (eu) {
+            eu[2 * i] = r.ux;
+            eu[2 * i + 1] = r.uy;
+            ed[i] = r.dist;
+        }
+        s = r.ex * r.ex + r.ey * r.ey;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// -------------------------------------------------------------------------
+// FD Jacobian blocks per observation (K1/K2 in SURVEY 7): same differences
+// as solveFunc_calculateJacobianMatrixForParameter, evaluated only for the
+// parameters that can change this observation (all other entries of the
+// reference column are exactly zero).
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__restrict__ recs,
+                                                  const double *__restrict__ ext_pert,
+                                                  const double *__restrict__ step,
+                                                  int solver_type, double *J, int *jcol,
+                                                  int *nloc, const int *__restrict__ stale_param,
+                                                  double *eu, double *ed) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    const int M = P.M;
+    const int cf = P.obs_cf[i];
+    const int b = P.obs_bnd[i];
+    const int fr = P.obs_frame[i];
+    const int cam = P.obs_cam[i];
+    const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
+    const Override none{-1, 0.};
+    double bp0[3];
+    bundle_position(P, b, fr, none, bp0);
+    double lc0[5];
+    int lens = -1;
+    const bool hl = obs_lens(P, cam, lens);
+    if (hl) lens_coeffs(P, lens, fr, none, lc0);
+    const int voff = P.cf_var_off[cf];
+    const int nvar = P.cf_var_off[cf + 1] - voff;
+    const double *rec0 = &recs[(size_t)voff * CAMREC];
+    const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, hl, lc0);
+    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
+    const int pstale = stale_param[fr];
+    Resid rs = r0;
+    int l = 0;
+    auto emit = [&](int p, const Resid &r) {
+        double jx, jy;
+        if (lmder) {
+            const double inv = step[p];
+            jx = (r.ex - r0.ex) * inv;
+            jy = (r.ey - r0.ey) * inv;
+        } else {
+            const double h = step[p];
+            jx = (r.ex - r0.ex) / h;
+            jy = (r.ey - r0.ey) / h;
+        }
+        J[(size_t)(2 * l) * M + i] = jx;
+        J[(size_t)(2 * l + 1) * M + i] = jy;
+        jcol[(size_t)l * M + i] = p;
+        if (p == pstale) rs = r;
+        ++l;
+    };
+    // camera-side parameters (variants 1..nvar-1)
+    for (int v = 1; v < nvar && l < LMAX; ++v) {
+        const int t = voff + v;
+        const int p = P.cf_var_param[t];
+        const double *rec = &recs[(size_t)t * CAMREC];
+        double bp[3] = {bp0[0], bp0[1], bp0[2]};
+        if (P.cf_var_flags[t] & VF_BUNDLE_SIDE) {
+            const Override ov{P.p_attr[p], ext_pert[p]};
+            bundle_position(P, b, fr, ov, bp);
+        }
+        emit(p, residual(rec, bp, mx, my, sw, P.mode, P.image_width, hl, lc0));
+    }
+    // bundle-side parameters not already covered by a camera variant
+    for (int q = P.bnd_par_off[b]; q < P.bnd_par_off[b + 1] && l < LMAX; ++q) {
+        const int p = P.bnd_par[q];
+        if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
+        if (P.p_both[p]) {
+            bool seen = false;
+            for (int v = 1; v < nvar; ++v) seen |= (P.cf_var_param[voff + v] == p);
+            if (seen) continue;
+        }
+        const Override ov{P.p_attr[p], ext_pert[p]};
+        double bp[3];
+        bundle_position(P, b, fr, ov, bp);
+        emit(p, residual(rec0, bp, mx, my, sw, P.mode, P.image_width, hl, lc0));
+    }
+    // lens parameters of this camera's lens
+    if (hl) {
+        for (int q = P.cam_lpar_off[cam]; q < P.cam_lpar_off[cam + 1] && l < LMAX; ++q) {
+            const int p = P.cam_lpar[q];
+            if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
+            const Override ov{P.p_attr[p], ext_pert[p]};
+            double lc[5];
+            lens_coeffs(P, lens, fr, ov, lc);
+            emit(p, residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, hl, lc));
+        }
+    }
+    nloc[i] = l;
+    // errorList / errorDistanceList as left by the last FD column (Appendix B13).
+    if (eu) {
+        eu[2 * i] = rs.ux;
+        eu[2 * i + 1] = rs.uy;
+        ed[i] = rs.dist;
+    }
+}
+
+// -------------------------------------------------------------------------
+// Normal equations.  Per camera-frame segment (contiguous observations):
+// Acc (pc x pc), gC (pc), Acg (pc x nG).  One workgroup per cf; each thread
+// owns output entries; J is staged through LDS in chunks of 64 observations.
+// -------------------------------------------------------------------------
+constexpr int NE_CHUNK = 64;
+
+__global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__restrict__ J,
+                                               const int *__restrict__ jcol,
+                                               const int *__restrict__ nloc,
+                                               const double *__restrict__ f, double *Acc,
+                                               double *Acg, double *g) {
+    __shared__ double sJ[2 * LMAX][NE_CHUNK];
+    __shared__ int sC[LMAX][NE_CHUNK];
+    __shared__ int sN[NE_CHUNK];
+    __shared__ double sF[2][NE_CHUNK];
+    const int cf = blockIdx.x;
+    const int pc = P.cf_pc[cf];
+    const int nG = P.nG;
+    const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
+    const int M = P.M;
+    const int ncc = pc * (pc + 1) / 2;
+    const int nent = ncc + pc + pc * nG;
+    const int e = threadIdx.x;
+    int ea = 0, eb = 0, kind = -1;
+    if (e < ncc) {
+        // decode upper-triangular index
+        int rem = e, r = 0;
+        while (rem >= pc - r) {
+            rem -= pc - r;
+            ++r;
+        }
+        ea = r;
+        eb = r + rem;
+        kind = 0;
+    } else if (e < ncc + pc) {
+        ea = e - ncc;
+        kind = 1;
+    } else if (e < nent) {
+        ea = (e - ncc - pc) / nG;
+        eb = (e - ncc - pc) % nG;
+        kind = 2;
+    }
+    const int gp = (kind == 2) ? P.g_param[eb] : -1;
+    double acc = 0.;
+    for (int c0 = o0; c0 < o1; c0 += NE_CHUNK) {
+        const int cnt = min(NE_CHUNK, o1 - c0);
+        __syncthreads();
+        for (int t = threadIdx.x; t < 2 * LMAX * NE_CHUNK; t += blockDim.x) {
+            const int row = t / NE_CHUNK, o = t % NE_CHUNK;
+            sJ[row][o] = (o < cnt) ? J[(size_t)row * M + c0 + o] : 0.;
+        }
+        if (nG > 0)
+            for (int t = threadIdx.x; t < LMAX * NE_CHUNK; t += blockDim.x) {
+                const int row = t / NE_CHUNK, o = t % NE_CHUNK;
+                sC[row][o] = (o < cnt) ? jcol[(size_t)row * M + c0 + o] : -1;
+            }
+        for (int t = threadIdx.x; t < NE_CHUNK; t += blockDim.x) {
+            sN[t] = (t < cnt) ? nloc[c0 + t] : 0;
+            sF[0][t] = (t < cnt) ? f[2 * (c0 + t)] : 0.;
+            sF[1][t] = (t < cnt) ? f[2 * (c0 + t) + 1] : 0.;
+        }
+        __syncthreads();
+        if (kind == 0) {
+            for (int o = 0; o < cnt; ++o)
+                acc += sJ[2 * ea][o] * sJ[2 * eb][o] + sJ[2 * ea + 1][o] * sJ[2 * eb + 1][o];
+        } else if (kind == 1) {
+            for (int o = 0; o < cnt; ++o)
+                acc += sJ[2 * ea][o] * sF[0][o] + sJ[2 * ea + 1][o] * sF[1][o];
+        } else if (kind == 2) {
+            for (int o = 0; o < cnt; ++o) {
+                for (int l = pc; l < sN[o]; ++l) {
+                    if (sC[l][o] == gp) {
+                        acc += sJ[2 * ea][o] * sJ[2 * l][o] + sJ[2 * ea + 1][o] * sJ[2 * l + 1][o];
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
+    if (kind == 0) {
+        A[ea * PCMAX + eb] = acc;
+        A[eb * PCMAX + ea] = acc;
+    } else if (kind == 1) {
+        g[P.cf_var_param[P.cf_var_off[cf] + 1 + ea]] = acc;
+    } else if (kind == 2) {
+        Acg[((size_t)cf * PCMAX + ea) * NGMAX + eb] = acc;
+    }
+}
+
+// Per bundle: Abb (pb x pb), gB, Abg (pb x nG).  One thread per bundle.
+__global__ void k_ne_bnd(DevProblem P, const double *__restrict__ J,
+                         const int *__restrict__ jcol, const int *__restrict__ nloc,
+                         const double *__restrict__ f, double *Abb, double *Abg, double *g) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int pb = P.bnd_pb[b];
+    if (pb == 0) return;
+    const int M = P.M, nG = P.nG;
+    double A[PBMAX][PBMAX] = {};
+    double gb[PBMAX] = {};
+    double G[PBMAX][NGMAX];
+    for (int a = 0; a < PBMAX; ++a)
+        for (int q = 0; q < NGMAX; ++q) G[a][q] = 0.;
+    for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
+        const int i = P.bobs[q];
+        const int cf = P.obs_cf[i];
+        const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
+        double jx[PBMAX], jy[PBMAX];
+        for (int a = 0; a < pb; ++a) {
+            jx[a] = J[(size_t)(2 * (s + a)) * M + i];
+            jy[a] = J[(size_t)(2 * (s + a) + 1) * M + i];
+        }
+        const double fx = f[2 * i], fy = f[2 * i + 1];
+        for (int a = 0; a < pb; ++a) {
+            for (int c = 0; c < pb; ++c) A[a][c] += jx[a] * jx[c] + jy[a] * jy[c];
+            gb[a] += jx[a] * fx + jy[a] * fy;
+        }
+        if (nG > 0) {
+            const int nl = nloc[i];
+            for (int l = 0; l < nl; ++l) {
+                const int p = jcol[(size_t)l * M + i];
+                if (P.p_class[p] != PC_G) continue;
+                const int gi = P.p_pos[p] - (P.nR - nG);
+                const double gx = J[(size_t)(2 * l) * M + i], gy = J[(size_t)(2 * l + 1) * M + i];
+                for (int a = 0; a < pb; ++a) G[a][gi] += jx[a] * gx + jy[a] * gy;
+            }
+        }
+    }
+    double *Ab = &Abb[(size_t)b * 9];
+    for (int a = 0; a < PBMAX; ++a)
+        for (int c = 0; c < PBMAX; ++c) Ab[a * 3 + c] = (a < pb && c < pb) ? A[a][c] : 0.;
+    const int po = P.bnd_par_off[b];
+    for (int a = 0; a < pb; ++a) g[P.bnd_par[po + a]] = gb[a];
+    for (int a = 0; a < PBMAX; ++a)
+        for (int q = 0; q < nG; ++q) Abg[((size_t)b * PBMAX + a) * NGMAX + q] = G[a][q];
+}
+
+// Globals: partial sums of Agg (nG x nG) and gG per block of observations.
+__global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__restrict__ J,
+                                                 const int *__restrict__ jcol,
+                                                 const int *__restrict__ nloc,
+                                                 const double *__restrict__ f,
+                                                 double *partial, int chunk) {
+    __shared__ double acc[NGMAX * NGMAX + NGMAX];
+    const int nG = P.nG;
+    const int nent = nG * nG + nG;
+    for (int t = threadIdx.x; t < nent; t += blockDim.x) acc[t] = 0.;
+    __syncthreads();
+    const int i0 = blockIdx.x * chunk;
+    const int i1 = min(P.M, i0 + chunk);
+    const int M = P.M;
+    // thread t handles observations i0 + t, i0 + t + 256, ... and accumulates
+    // into LDS with per-entry ownership by (t % nent) rounds to stay deterministic:
+    // each observation's contributions are applied by one thread serially.
+    for (int t = 0; t < nent; ++t) {
+        // serialised over entries: entry t owned by thread (t % blockDim.x)
+        if ((int)threadIdx.x != (t % (int)blockDim.x)) continue;
+        const int ga = t < nG * nG ? t / nG : t - nG * nG;
+        const int gb = t < nG * nG ? t % nG : -1;
+        const int pa = P.g_param[ga];
+        const int pbp = gb >= 0 ? P.g_param[gb] : -1;
+        double s = 0.;
+        for (int i = i0; i < i1; ++i) {
+            const int nl = nloc[i];
+            int la = -1, lb = -1;
+            for (int l = 0; l < nl; ++l) {
+                const int p = jcol[(size_t)l * M + i];
+                if (p == pa) la = l;
+                if (p == pbp) lb = l;
+            }
+            if (la < 0) continue;
+            const double ax = J[(size_t)(2 * la) * M + i], ay = J[(size_t)(2 * la + 1) * M + i];
+            if (gb < 0) {
+                s += ax * f[2 * i] + ay * f[2 * i + 1];
+            } else if (lb >= 0) {
+                s += ax * J[(size_t)(2 * lb) * M + i] + ay * J[(size_t)(2 * lb + 1) * M + i];
+            }
+        }
+        acc[t] = s;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nent; t += blockDim.x)
+        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = acc[t];
+}
+
+__global__ void k_ne_glob_reduce(DevProblem P, const double *__restrict__ partial, int nblk,
+                                 double *Agg, double *g) {
+    const int nG = P.nG;
+    const int nent = nG * nG + nG;
+    for (int t = threadIdx.x; t < nent; t += blockDim.x) {
+        double s = 0.;
+        for (int k = 0; k < nblk; ++k) s += partial[(size_t)k * (NGMAX * NGMAX + NGMAX) + t];
+        if (t < nG * nG)
+            Agg[(t / nG) * NGMAX + (t % nG)] = s;
+        else
+            g[P.g_param[t - nG * nG]] = s;
+    }
+}
+
+// Column norms acnorm_p = sqrt(A_pp) in parameter order.
+__global__ void k_colnorms(DevProblem P, const double *__restrict__ Acc,
+                           const double *__restrict__ Abb, const double *__restrict__ Agg,
+                           double *acnorm) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    const int cls = P.p_class[p];
+    double d = 0.;
+    if (cls == PC_CF) {
+        const int r = P.p_pos[p];  // R index; find cf by the block table
+        const int cf = P.p_blk[p];
+        const int a = r - P.cf_roff[cf];
+        d = Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + a];
+    } else if (cls == PC_B) {
+        const int b = P.p_blk[p];
+        const int a = P.p_pos[p];
+        d = Abb[(size_t)b * 9 + a * 3 + a];
+    } else {
+        const int gi = P.p_pos[p] - (P.nR - P.nG);
+        d = Agg[gi * NGMAX + gi];
+    }
+    acnorm[p] = sqrt(d);
+}
+
+// -------------------------------------------------------------------------
+// Damped system, bundle blocks: Abb + lam D^2 = Lb Lb^T (3x3), tb = Lb^-1 gb,
+// Wg_b = Abg^T Lb^-T (nG x pb).  At lam == 0 an exactly-zero diagonal (zero
+// Jacobian column) is replaced by 1 so that component solves to 0 (MINPACK's
+// nsing truncation for exactly zero columns).
+// -------------------------------------------------------------------------
+__global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
+                                const double *__restrict__ Abg, const double *__restrict__ g,
+                                const double *__restrict__ diag, double lam, double *Lb,
+                                double *tb, double *Wg, int *fail) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int pb = P.bnd_pb[b];
+    if (pb == 0) return;
+    const int po = P.bnd_par_off[b];
+    double A[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) A[a][c] = Abb[(size_t)b * 9 + a * 3 + c];
+    double rhs[3] = {0., 0., 0.};
+    for (int a = 0; a < pb; ++a) {
+        const int p = P.bnd_par[po + a];
+        const double d = diag[p];
+        A[a][a] += lam * (d * d);
+        rhs[a] = g[p];
+        if (A[a][a] == 0.) {
+            A[a][a] = 1.;
+            rhs[a] = 0.;
+        }
+    }
+    double L[3][3] = {};
+    bool ok = true;
+    for (int j = 0; j < pb; ++j) {
+        double s = A[j][j];
+        for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+        if (!(s > 0.)) {
+            ok = false;
+            s = 1.;
+        }
+        L[j][j] = sqrt(s);
+        for (int i = j + 1; i < pb; ++i) {
+            double t = A[i][j];
+            for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
+            L[i][j] = t / L[j][j];
+        }
+    }
+    if (!ok) atomicOr(fail, 1);
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) Lb[(size_t)b * 9 + a * 3 + c] = L[a][c];
+    double t[3] = {0., 0., 0.};
+    for (int a = 0; a < pb; ++a) {
+        double s = rhs[a];
+        for (int k = 0; k < a; ++k) s -= L[a][k] * t[k];
+        t[a] = s / L[a][a];
+    }
+    for (int a = 0; a < 3; ++a) tb[(size_t)b * 3 + a] = t[a];
+    for (int q = 0; q < P.nG; ++q) {
+        // row q of Abg^T, forward-solve against L: w L^T = a  ->  L w^T = a^T
+        double w[3] = {0., 0., 0.};
+        for (int a = 0; a < pb; ++a) {
+            double s = Abg[((size_t)b * PBMAX + a) * NGMAX + q];
+            for (int k = 0; k < a; ++k) s -= L[a][k] * w[k];
+            w[a] = s / L[a][a];
+        }
+        for (int a = 0; a < 3; ++a) Wg[((size_t)b * NGMAX + q) * 3 + a] = w[a];
+    }
+}
+
+// W_i = (J_c(i)^T J_b(i)) Lb^-T per observation (PCMAX x 3, SoA over i).
+__global__ void k_schur_obs(DevProblem P, const double *__restrict__ J,
+                            const double *__restrict__ Lb, double *W) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    const int M = P.M;
+    const int b = P.obs_bnd[i];
+    const int pb = P.bnd_pb[b];
+    if (pb == 0) return;
+    const int cf = P.obs_cf[i];
+    const int pc = P.cf_pc[cf];
+    const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
+    double bx[3], by[3];
+    for (int a = 0; a < pb; ++a) {
+        bx[a] = J[(size_t)(2 * (s + a)) * M + i];
+        by[a] = J[(size_t)(2 * (s + a) + 1) * M + i];
+    }
+    double L[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+    for (int r = 0; r < pc; ++r) {
+        const double cx = J[(size_t)(2 * r) * M + i], cy = J[(size_t)(2 * r + 1) * M + i];
+        double e[3];
+        for (int a = 0; a < pb; ++a) e[a] = cx * bx[a] + cy * by[a];
+        double w[3] = {0., 0., 0.};
+        for (int a = 0; a < pb; ++a) {
+            double t = e[a];
+            for (int k = 0; k < a; ++k) t -= L[a][k] * w[k];
+            w[a] = t / L[a][a];
+        }
+        for (int a = 0; a < 3; ++a) W[((size_t)(r * 3 + a)) * M + i] = w[a];
+    }
+}
+
+__device__ __forceinline__ double *s_at(double *S, const int *__restrict__ slot, int NT, int R,
+                                        int C) {
+    const int s = slot[(R / TILE) * NT + (C / TILE)];
+    return &S[(size_t)s * TILE * TILE + (R % TILE) * TILE + (C % TILE)];
+}
+
+// S = (Acc + lam D^2 | Acg | Agg + lam D^2), lower triangle, plus identity
+// on the padded tail; rhs = g_R.
+__global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
+                             const double *__restrict__ Acg, const double *__restrict__ Agg,
+                             const double *__restrict__ g, const double *__restrict__ diag,
+                             double lam, double *S, const int *__restrict__ slot, int NT,
+                             double *rhs) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nG = P.nG;
+    const int nCF = P.nR - nG;
+    if (t < P.ncf) {
+        const int cf = t;
+        const int pc = P.cf_pc[cf];
+        const int r0 = P.cf_roff[cf];
+        const int v0 = P.cf_var_off[cf] + 1;
+        for (int a = 0; a < pc; ++a) {
+            const int pa = P.cf_var_param[v0 + a];
+            for (int c = 0; c <= a; ++c) {
+                double v = Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + c];
+                if (a == c) {
+                    const double d = diag[pa];
+                    v += lam * (d * d);
+                    if (v == 0.) v = 1.;
+                }
+                *s_at(S, slot, NT, r0 + a, r0 + c) = v;
+            }
+            rhs[r0 + a] = (Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + a] == 0. && lam == 0.)
+                              ? 0.
+                              : g[pa];
+            for (int q = 0; q < nG; ++q)
+                *s_at(S, slot, NT, nCF + q, r0 + a) = Acg[((size_t)cf * PCMAX + a) * NGMAX + q];
+        }
+    } else if (t < P.ncf + nG) {
+        const int q = t - P.ncf;
+        const int p = P.g_param[q];
+        for (int c = 0; c <= q; ++c) {
+            double v = Agg[q * NGMAX + c];
+            if (c == q) {
+                const double d = diag[p];
+                v += lam * (d * d);
+                if (v == 0.) v = 1.;
+            }
+            *s_at(S, slot, NT, nCF + q, nCF + c) = v;
+        }
+        rhs[nCF + q] = (Agg[q * NGMAX + q] == 0. && lam == 0.) ? 0. : g[p];
+    } else {
+        const int r = P.nR + (t - P.ncf - nG);
+        if (r < NT * TILE) {
+            *s_at(S, slot, NT, r, r) = 1.;
+            rhs[r] = 0.;
+        }
+    }
+}
+
+// Schur complement over bundles: S -= sum_b W_b W_b^T, rhs -= W_b tb.
+__global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
+                              const double *__restrict__ Wg, const double *__restrict__ tb,
+                              double *S, const int *__restrict__ slot, int NT, double *rhs) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int pb = P.bnd_pb[b];
+    if (pb == 0) return;
+    const int M = P.M, nG = P.nG;
+    const int nCF = P.nR - nG;
+    const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
+    const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1], t2 = tb[(size_t)b * 3 + 2];
+    for (int qi = q0; qi < q1; ++qi) {
+        const int i = P.bobs[qi];
+        const int cfi = P.obs_cf[i];
+        const int pci = P.cf_pc[cfi];
+        const int ri = P.cf_roff[cfi];
+        for (int a = 0; a < pci; ++a) {
+            const double wa0 = W[(size_t)(a * 3) * M + i], wa1 = W[(size_t)(a * 3 + 1) * M + i],
+                         wa2 = W[(size_t)(a * 3 + 2) * M + i];
+            atomicAdd(&rhs[ri + a], -(wa0 * t0 + wa1 * t1 + wa2 * t2));
+            for (int qj = q0; qj < q1; ++qj) {
+                const int j = P.bobs[qj];
+                const int cfj = P.obs_cf[j];
+                const int pcj = P.cf_pc[cfj];
+                const int rj = P.cf_roff[cfj];
+                for (int c = 0; c < pcj; ++c) {
+                    const int R = ri + a, C = rj + c;
+                    if (R < C) continue;
+                    const double v = wa0 * W[(size_t)(c * 3) * M + j] +
+                                     wa1 * W[(size_t)(c * 3 + 1) * M + j] +
+                                     wa2 * W[(size_t)(c * 3 + 2) * M + j];
+                    atomicAdd(s_at(S, slot, NT, R, C), -v);
+                }
+            }
+        }
+    }
+    for (int q = 0; q < nG; ++q) {
+        const double *wg = &Wg[((size_t)b * NGMAX + q) * 3];
+        atomicAdd(&rhs[nCF + q], -(wg[0] * t0 + wg[1] * t1 + wg[2] * t2));
+        for (int qj = q0; qj < q1; ++qj) {
+            const int j = P.bobs[qj];
+            const int cfj = P.obs_cf[j];
+            const int pcj = P.cf_pc[cfj];
+            const int rj = P.cf_roff[cfj];
+            for (int c = 0; c < pcj; ++c) {
+                const double v = wg[0] * W[(size_t)(c * 3) * M + j] +
+                                 wg[1] * W[(size_t)(c * 3 + 1) * M + j] +
+                                 wg[2] * W[(size_t)(c * 3 + 2) * M + j];
+                atomicAdd(s_at(S, slot, NT, nCF + q, rj + c), -v);
+            }
+        }
+        for (int q2 = 0; q2 <= q; ++q2) {
+            const double *wh = &Wg[((size_t)b * NGMAX + q2) * 3];
+            atomicAdd(s_at(S, slot, NT, nCF + q, nCF + q2),
+                      -(wg[0] * wh[0] + wg[1] * wh[1] + wg[2] * wh[2]));
+        }
+    }
+}
+
+// -------------------------------------------------------------------------
+// Tiled Cholesky of S (64x64 tiles, right-looking).
+// -------------------------------------------------------------------------
+constexpr int LDP = TILE + 1;  // padded LDS row (conflict-free column walks)
+
+// Factor a diagonal tile in LDS; returns false on a non-positive pivot.
+__device__ bool lds_potrf(double (*A)[LDP], int *bad) {
+    for (int j = 0; j < TILE; ++j) {
+        if (threadIdx.x == 0) {
+            double d = A[j][j];
+            if (!(d > 0.) || !isfinite(d)) {
+                *bad = 1;
+                d = 1.;
+            }
+            A[j][j] = sqrt(d);
+        }
+        __syncthreads();
+        const double piv = A[j][j];
+        for (int r = j + 1 + threadIdx.x; r < TILE; r += blockDim.x) A[r][j] /= piv;
+        __syncthreads();
+        const int m = TILE - j - 1;
+        for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
+            const int r = j + 1 + t / m, c = j + 1 + t % m;
+            if (c <= r) A[r][c] -= A[r][j] * A[c][j];
+        }
+        __syncthreads();
+    }
+    return *bad == 0;
+}
+
+// Linv = L^-1 (lower), one column per thread.
+__device__ void lds_trtri(double (*L)[LDP], double (*Li)[LDP]) {
+    for (int c = threadIdx.x; c < TILE; c += blockDim.x) {
+        for (int r = 0; r < TILE; ++r) Li[r][c] = 0.;
+        for (int r = c; r < TILE; ++r) {
+            double s = (r == c) ? 1. : 0.;
+            for (int k = c; k < r; ++k) s -= L[r][k] * Li[k][c];
+            Li[r][c] = s / L[r][r];
+        }
+    }
+    __syncthreads();
+}
+
+// Panel k: block 0 factors the diagonal tile and stores L_kk and Linv_kk;
+// block j>0 factors it redundantly and solves L_Ik = S_Ik L_kk^-T.
+__global__ void __launch_bounds__(256) k_chol_panel(double *S, const int *__restrict__ slot,
+                                                    int NT, int k,
+                                                    const int *__restrict__ rows,
+                                                    double *Linv, int *fail) {
+    __shared__ double A[TILE][LDP];
+    __shared__ double Li[TILE][LDP];
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    const double *D = &S[(size_t)slot[k * NT + k] * TILE * TILE];
+    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) A[t / TILE][t % TILE] = D[t];
+    __syncthreads();
+    lds_potrf(A, &bad);
+    __syncthreads();
+    if (threadIdx.x == 0 && bad && blockIdx.x == 0) atomicOr(fail, 1);
+    lds_trtri(A, Li);
+    if (blockIdx.x == 0) {
+        double *Dw = &S[(size_t)slot[k * NT + k] * TILE * TILE];
+        for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) {
+            const int r = t / TILE, c = t % TILE;
+            Dw[t] = (c <= r) ? A[r][c] : 0.;
+            Linv[(size_t)k * TILE * TILE + t] = Li[r][c];
+        }
+        return;
+    }
+    const int I = rows[blockIdx.x - 1];
+    double *B = &S[(size_t)slot[I * NT + k] * TILE * TILE];
+    // reuse A as the row tile
+    __syncthreads();
+    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) A[t / TILE][t % TILE] = B[t];
+    __syncthreads();
+    // X = B * Linv^T : X[r][c] = sum_{t<=c} B[r][t] * Linv[c][t]
+    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) {
+        const int r = t / TILE, c = t % TILE;
+        double s = 0.;
+        for (int q = 0; q <= c; ++q) s += A[r][q] * Li[c][q];
+        B[t] = s;
+    }
+}
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// Trailing update S_IJ -= L_Ik L_Jk^T for the listed (I, J) pairs of panel k,
+// fp64 MFMA 16x16x4: 4 waves, each owns a 16x64 row strip (4 MFMA tiles).
+__global__ void __launch_bounds__(256) k_chol_update(double *S, const int *__restrict__ slot,
+                                                     int NT, int k,
+                                                     const int2 *__restrict__ pairs) {
+    __shared__ double A[TILE][LDP];
+    __shared__ double B[TILE][LDP];
+    const int2 pr = pairs[blockIdx.x];
+    const int I = pr.x, Jt = pr.y;
+    const double *Lik = &S[(size_t)slot[I * NT + k] * TILE * TILE];
+    const double *Ljk = &S[(size_t)slot[Jt * NT + k] * TILE * TILE];
+    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) {
+        A[t / TILE][t % TILE] = Lik[t];
+        B[t / TILE][t % TILE] = Ljk[t];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int li = lane & 15, lk = lane >> 4;
+    dbl4 acc[4];
+    for (int tj = 0; tj < 4; ++tj) acc[tj] = (dbl4){0., 0., 0., 0.};
+    const int ti = wave;
+    for (int ks = 0; ks < TILE / 4; ++ks) {
+        const double a = A[ti * 16 + li][ks * 4 + lk];
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj) {
+            const double bv = B[tj * 16 + li][ks * 4 + lk];
+            acc[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[tj], 0, 0, 0);
+        }
+    }
+    double *C = &S[(size_t)slot[I * NT + Jt] * TILE * TILE];
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = ti * 16 + lk + 4 * r;
+            const int col = tj * 16 + li;
+            C[row * TILE + col] -= acc[tj][r];
+        }
+}
+
+// Forward substitution L y = r, panel k: y_k = Linv_kk r_k, r_I -= L_Ik y_k.
+__global__ void k_trsv_fwd(const double *__restrict__ S, const int *__restrict__ slot, int NT,
+                           int k, const int *__restrict__ rows, const double *__restrict__ Linv,
+                           double *r, double *y) {
+    __shared__ double yk[TILE];
+    const double *Li = &Linv[(size_t)k * TILE * TILE];
+    for (int row = threadIdx.x; row < TILE; row += blockDim.x) {
+        double s = 0.;
+        for (int t = 0; t <= row; ++t) s += Li[row * TILE + t] * r[k * TILE + t];
+        yk[row] = s;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        for (int row = threadIdx.x; row < TILE; row += blockDim.x) y[k * TILE + row] = yk[row];
+        return;
+    }
+    const int I = rows[blockIdx.x - 1];
+    const double *L = &S[(size_t)slot[I * NT + k] * TILE * TILE];
+    for (int row = threadIdx.x; row < TILE; row += blockDim.x) {
+        double s = 0.;
+        for (int c = 0; c < TILE; ++c) s += L[row * TILE + c] * yk[c];
+        r[I * TILE + row] -= s;
+    }
+}
+
+// Back substitution L^T x = y, panel k (descending): x_k = Linv_kk^T y_k,
+// y_J -= L_kJ^T x_k for every J < k with L_kJ structurally non-zero.
+__global__ void k_trsv_bwd(const double *__restrict__ S, const int *__restrict__ slot, int NT,
+                           int k, const int *__restrict__ cols, const double *__restrict__ Linv,
+                           double *y, double *x) {
+    __shared__ double xk[TILE];
+    const double *Li = &Linv[(size_t)k * TILE * TILE];
+    for (int row = threadIdx.x; row < TILE; row += blockDim.x) {
+        double s = 0.;
+        for (int t = row; t < TILE; ++t) s += Li[t * TILE + row] * y[k * TILE + t];
+        xk[row] = s;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        for (int row = threadIdx.x; row < TILE; row += blockDim.x) x[k * TILE + row] = xk[row];
+        return;
+    }
+    const int Jt = cols[blockIdx.x - 1];
+    const double *L = &S[(size_t)slot[k * NT + Jt] * TILE * TILE];
+    for (int c = threadIdx.x; c < TILE; c += blockDim.x) {
+        double s = 0.;
+        for (int rr = 0; rr < TILE; ++rr) s += L[rr * TILE + c] * xk[rr];
+        y[Jt * TILE + c] -= s;
+    }
+}
+
+// x_b = Lb^-T (tb - sum_i W_i^T x_cf(i) - Wg_b^T x_G), scatter to parameter order.
+__global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
+                                 const double *__restrict__ Wg, const double *__restrict__ tb,
+                                 const double *__restrict__ Lb, const double *__restrict__ xR,
+                                 double *x) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int pb = P.bnd_pb[b];
+    if (pb == 0) return;
+    const int M = P.M, nG = P.nG;
+    const int nCF = P.nR - nG;
+    double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
+    for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
+        const int i = P.bobs[q];
+        const int cf = P.obs_cf[i];
+        const int pc = P.cf_pc[cf];
+        const int r0 = P.cf_roff[cf];
+        for (int a = 0; a < pc; ++a) {
+            const double xv = xR[r0 + a];
+            for (int c = 0; c < 3; ++c) s[c] -= W[(size_t)(a * 3 + c) * M + i] * xv;
+        }
+    }
+    for (int q = 0; q < nG; ++q) {
+        const double xv = xR[nCF + q];
+        for (int c = 0; c < 3; ++c) s[c] -= Wg[((size_t)b * NGMAX + q) * 3 + c] * xv;
+    }
+    double L[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+    double xb[3] = {0., 0., 0.};
+    for (int a = pb - 1; a >= 0; --a) {
+        double t = s[a];
+        for (int k = a + 1; k < pb; ++k) t -= L[k][a] * xb[k];
+        xb[a] = t / L[a][a];
+    }
+    const int po = P.bnd_par_off[b];
+    for (int a = 0; a < pb; ++a) x[P.bnd_par[po + a]] = xb[a];
+}
+
+// Reduced-system solution (R order) -> parameter order.
+__global__ void k_scatter_xR(DevProblem P, const double *__restrict__ xR, double *x) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    if (P.p_class[p] != PC_B) x[p] = xR[P.p_pos[p]];
+}
+
+// Newton-correction helpers: u_b = Lb^-1 v_b (sum |u_b|^2 per bundle into
+// usq[b]) and w_R = v_R - sum_b W_b u_b.
+__global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
+                                const double *__restrict__ Wg, const double *__restrict__ Lb,
+                                const double *__restrict__ v, double *wR, double *usq) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int pb = P.bnd_pb[b];
+    if (pb == 0) {
+        usq[b] = 0.;
+        return;
+    }
+    const int M = P.M, nG = P.nG;
+    const int nCF = P.nR - nG;
+    const int po = P.bnd_par_off[b];
+    double L[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+    double u[3] = {0., 0., 0.};
+    for (int a = 0; a < pb; ++a) {
+        double t = v[P.bnd_par[po + a]];
+        for (int k = 0; k < a; ++k) t -= L[a][k] * u[k];
+        u[a] = t / L[a][a];
+    }
+    usq[b] = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+    for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
+        const int i = P.bobs[q];
+        const int cf = P.obs_cf[i];
+        const int pc = P.cf_pc[cf];
+        const int r0 = P.cf_roff[cf];
+        for (int a = 0; a < pc; ++a) {
+            double s = 0.;
+            for (int c = 0; c < 3; ++c) s += W[(size_t)(a * 3 + c) * M + i] * u[c];
+            atomicAdd(&wR[r0 + a], -s);
+        }
+    }
+    for (int q = 0; q < nG; ++q) {
+        double s = 0.;
+        for (int c = 0; c < 3; ++c) s += Wg[((size_t)b * NGMAX + q) * 3 + c] * u[c];
+        atomicAdd(&wR[nCF + q], -s);
+    }
+}
+
+// v (parameter order) -> R order (non-bundle parameters); padded tail zero.
+__global__ void k_gather_R(DevProblem P, const double *__restrict__ v, double *vR, int nRpad) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P.n && P.p_class[p] != PC_B) vR[P.p_pos[p]] = v[p];
+    const int r = P.nR + p;
+    if (r < nRpad && p < nRpad) vR[r] = 0.;
+}
+
+// -------------------------------------------------------------------------
+// Vector helpers and deterministic two-pass reductions.
+// -------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_sumsq(const double *__restrict__ a,
+                                               const double *__restrict__ d, int n,
+                                               double *partial) {
+    __shared__ double red[256];
+    double s = 0.;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        double v = d ? d[i] * a[i] : a[i];
+        s += v * v;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) k_sumsq_div(const double *__restrict__ a,
+                                                   const double *__restrict__ d, int n,
+                                                   double *partial) {
+    __shared__ double red[256];
+    double s = 0.;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        double v = a[i] / d[i];
+        s += v * v;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) k_reduce_sum(const double *__restrict__ partial, int n,
+                                                    double *out) {
+    __shared__ double red[256];
+    double s = 0.;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+// gnorm (lmder.c): max_l |g_l / fnorm| / acnorm_l over acnorm_l != 0.
+__global__ void __launch_bounds__(256) k_gnorm(const double *__restrict__ g,
+                                               const double *__restrict__ acnorm, int n,
+                                               double fnorm, double *partial) {
+    __shared__ double red[256];
+    double m = 0.;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (acnorm[i] != 0.) m = fmax(m, fabs((g[i] / fnorm) / acnorm[i]));
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void k_reduce_max(const double *__restrict__ partial, int n, double *out) {
+    __shared__ double red[256];
+    double m = 0.;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmax(m, partial[i]);
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+// ||J p||^2 partial sums (prered in lmder): (J p)_obs = sum_l J_l p[jcol_l].
+__global__ void __launch_bounds__(256) k_jp_sumsq(DevProblem P, const double *__restrict__ J,
+                                                  const int *__restrict__ jcol,
+                                                  const int *__restrict__ nloc,
+                                                  const double *__restrict__ p,
+                                                  double *partial) {
+    __shared__ double red[256];
+    const int M = P.M;
+    double s = 0.;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        double ax = 0., ay = 0.;
+        const int nl = nloc[i];
+        for (int l = 0; l < nl; ++l) {
+            const double pv = p[jcol[(size_t)l * M + i]];
+            ax += J[(size_t)(2 * l) * M + i] * pv;
+            ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+        }
+        s += ax * ax + ay * ay;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// Elementwise LM vector updates.
+__global__ void k_lm_step(int n, const double *__restrict__ xs, const double *__restrict__ x,
+                          const double *__restrict__ diag, double *wa1, double *wa2,
+                          double *wa3) {
+    // wa1 = -xs (step), wa2 = x + wa1, wa3 = diag * wa1
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const double s = -xs[j];
+    wa1[j] = s;
+    wa2[j] = x[j] + s;
+    wa3[j] = diag[j] * s;
+}
+
+__global__ void k_diag_init(int n, const double *__restrict__ acnorm, double *diag, int first,
+                            int mode) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    if (first && mode != 2) diag[j] = acnorm[j] == 0. ? 1. : acnorm[j];
+    if (mode != 2) diag[j] = fmax(diag[j], acnorm[j]);
+}
+
+__global__ void k_newton_v(int n, const double *__restrict__ diag, const double *__restrict__ x,
+                           double dxnorm, double *v) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    v[j] = diag[j] * ((diag[j] * x[j]) / dxnorm);
+}
+
+// Device order -> reference (errorToMarkerList) order.
+__global__ void k_unpermute(int M, const int *__restrict__ ref_of_dev,
+                            const double *__restrict__ f2, const double *__restrict__ eu2,
+                            const double *__restrict__ ed, double *f2o, double *eu2o,
+                            double *edo) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const int r = ref_of_dev[i];
+    if (f2) {
+        f2o[2 * r] = f2[2 * i];
+        f2o[2 * r + 1] = f2[2 * i + 1];
+    }
+    if (eu2) {
+        eu2o[2 * r] = eu2[2 * i];
+        eu2o[2 * r + 1] = eu2[2 * i + 1];
+    }
+    if (ed) edo[r] = ed[i];
+}
+
+}  // namespace mmba
+
+// =========================================================================
+// Host launch wrappers (declared in mmba_kernels.h).
+// =========================================================================
+namespace mmba {
+
+static inline int nblk(long n, int bs) { return (int)((n + bs - 1) / bs); }
+
+void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, double *ext,
+                       double *ext_pert, double *step, int solver_type, double delta,
+                       double eps_dif) {
+    if (P.n == 0) return;
+    k_param_prep<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext, ext_pert, step, solver_type, delta,
+                                                 eps_dif);
+}
+void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
+    k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);
+}
+void launch_cam_records(hipStream_t s, const DevProblem &P, const int *var_cf,
+                        const double *ext_pert, double *recs, int nvar, int base_only) {
+    const int n = base_only ? P.ncf : nvar;
+    if (n == 0) return;
+    k_cam_records<<<nblk(n, 64), 64, 0, s>>>(P, var_cf, ext_pert, recs, nvar, base_only);
+}
+int residual_blocks(const DevProblem &P) { return nblk(P.M, 256); }
+void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
+                     double *ed, double *partial) {
+    k_residual<<<nblk(P.M, 256), 256, 0, s>>>(P, recs, f, eu, ed, partial);
+}
+void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
+                     const double *ext_pert, const double *step, int solver_type, double *J,
+                     int *jcol, int *nloc, const int *stale_param, double *eu, double *ed) {
+    k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
+                                                nloc, stale_param, eu, ed);
+}
+void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
+               const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
+               double *Abg, double *Agg, double *g, double *glob_partial, int glob_chunk,
+               double *acnorm) {
+    if (P.ncf > 0) k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
+    if (P.nB > 0) k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
+    if (P.nG > 0) {
+        const int nb = nblk(P.M, glob_chunk);
+        k_ne_glob<<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+        k_ne_glob_reduce<<<1, 256, 0, s>>>(P, glob_partial, nb, Agg, g);
+    }
+    k_colnorms<<<nblk(P.n, 256), 256, 0, s>>>(P, Acc, Abb, Agg, acnorm);
+}
+void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
+                          const double *Abg, const double *g, const double *diag, double lam,
+                          double *Lb, double *tb, double *Wg, int *fail) {
+    if (P.nB == 0) return;
+    k_bundle_factor<<<nblk(P.nB, 64), 64, 0, s>>>(P, Abb, Abg, g, diag, lam, Lb, tb, Wg, fail);
+}
+void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
+                      double *W) {
+    k_schur_obs<<<nblk(P.M, 128), 128, 0, s>>>(P, J, Lb, W);
+}
+void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
+                       const double *Agg, const double *g, const double *diag, double lam,
+                       double *S, const int *slot, int NT, double *rhs) {
+    const int n = P.ncf + P.nG + (NT * TILE - P.nR);
+    k_schur_init<<<nblk(n, 64), 64, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, S, slot, NT, rhs);
+}
+void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                        const double *tb, double *S, const int *slot, int NT, double *rhs) {
+    if (P.nB == 0) return;
+    k_schur_pairs<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, S, slot, NT, rhs);
+}
+void launch_chol_panel(hipStream_t s, double *S, const int *slot, int NT, int k, const int *rows,
+                       int nrows, double *Linv, int *fail) {
+    k_chol_panel<<<1 + nrows, 256, 0, s>>>(S, slot, NT, k, rows, Linv, fail);
+}
+void launch_chol_update(hipStream_t s, double *S, const int *slot, int NT, int k,
+                        const int2 *pairs, int npairs) {
+    if (npairs == 0) return;
+    k_chol_update<<<npairs, 256, 0, s>>>(S, slot, NT, k, pairs);
+}
+void launch_trsv_fwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
+                     const int *rows, int nrows, const double *Linv, double *r, double *y) {
+    k_trsv_fwd<<<1 + nrows, 64, 0, s>>>(S, slot, NT, k, rows, Linv, r, y);
+}
+void launch_trsv_bwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
+                     const int *cols, int ncols, const double *Linv, double *y, double *x) {
+    k_trsv_bwd<<<1 + ncols, 64, 0, s>>>(S, slot, NT, k, cols, Linv, y, x);
+}
+void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                           const double *tb, const double *Lb, const double *xR, double *x) {
+    if (P.nB > 0)
+        k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, Lb, xR, x);
+}
+void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x) {
+    k_scatter_xR<<<nblk(P.n, 256), 256, 0, s>>>(P, xR, x);
+}
+void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                          const double *Lb, const double *v, double *wR, double *usq) {
+    if (P.nB > 0)
+        k_newton_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, Lb, v, wR, usq);
+}
+void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double *vR, int nRpad) {
+    const int n = P.n > nRpad ? P.n : nRpad;
+    k_gather_R<<<nblk(n, 256), 256, 0, s>>>(P, v, vR, nRpad);
+}
+void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
+                  int nparts, double *out) {
+    k_sumsq<<<nparts, 256, 0, s>>>(a, d, n, partial);
+    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
+                      int nparts, double *out) {
+    k_sumsq_div<<<nparts, 256, 0, s>>>(a, d, n, partial);
+    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out) {
+    k_reduce_sum<<<1, 256, 0, s>>>(partial, n, out);
+}
+void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
+                  double *partial, int nparts, double *out) {
+    k_gnorm<<<nparts, 256, 0, s>>>(g, acnorm, n, fnorm, partial);
+    k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
+                     const int *nloc, const double *p, double *partial, int nparts,
+                     double *out) {
+    k_jp_sumsq<<<nparts, 256, 0, s>>>(P, J, jcol, nloc, p, partial);
+    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_lm_step(hipStream_t s, int n, const double *xs, const double *x, const double *diag,
+                    double *wa1, double *wa2, double *wa3) {
+    k_lm_step<<<nblk(n, 256), 256, 0, s>>>(n, xs, x, diag, wa1, wa2, wa3);
+}
+void launch_diag_init(hipStream_t s, int n, const double *acnorm, double *diag, int first,
+                      int mode) {
+    k_diag_init<<<nblk(n, 256), 256, 0, s>>>(n, acnorm, diag, first, mode);
+}
+void launch_newton_v(hipStream_t s, int n, const double *diag, const double *x, double dxnorm,
+                     double *v) {
+    k_newton_v<<<nblk(n, 256), 256, 0, s>>>(n, diag, x, dxnorm, v);
+}
+void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const double *f2,
+                      const double *eu2, const double *ed, double *f2o, double *eu2o,
+                      double *edo) {
+    k_unpermute<<<nblk(M, 256), 256, 0, s>>>(M, ref_of_dev, f2, eu2, ed, f2o, eu2o, edo);
+}
+
+}  // namespace mmba

@@ -1,0 +1,461 @@
+// mmba_lm.cpp -- device-resident Levenberg-Marquardt, MINPACK-1 lmder/lmdif
+// control flow on normal equations.
+//
+// Mapping to the reference (cminpack 1.3.8 lmder.c / lmpar.c as called from
+// src/mmSolver/adjust/adjust_cminpack_lmder.cpp:94-184):
+//   qrfac column norms acnorm_j       -> sqrt(A_jj), A = J^T J
+//   R^T (Q^T f)                       -> g = J^T f
+//   ||R P^T p||                       -> ||J p|| (k_jp_sumsq, exact products)
+//   qrsolv(par): (A + par D^2) x = g  -> bundle-Schur + tiled Cholesky
+//   ||S^-T P^T v|| in lmpar           -> sqrt(v^T (A + par D^2)^-1 v)
+//                                        = ||Lb^-1 v_b|| (+) ||Ls^-1 w_R||
+// Scalar control (trust region, ratio tests, info codes) runs on the host
+// with the same constants and operation order as the restatement in
+// oracle/refcpu.c (lm_core / lmpar).
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "mmba_kernels.h"
+#include "mmba_plan.h"
+
+namespace mmba {
+
+static double wall_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+double Plan::read_scalar(int slot) {
+    MMBA_HIP(hipMemcpyAsync(h_scalar + slot, d_scalar + slot, sizeof(double),
+                            hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+    return h_scalar[slot];
+}
+
+double Plan::dnorm(const double *dv) {
+    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + 1);
+    return std::sqrt(read_scalar(1));
+}
+
+// iflag = 1: setParameters + measureErrors.  Returns ||f||.
+double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
+    const double t0 = wall_now();
+    launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
+    launch_set_attrs(s, P, d_ext);
+    launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
+    if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
+    launch_residual(s, P, d_recs, df, eu, ed, d_partial);
+    if (timing) {
+        MMBA_HIP(hipEventRecord(ev_b, s));
+        MMBA_HIP(hipEventSynchronize(ev_b));
+        float ms = 0.f;
+        MMBA_HIP(hipEventElapsedTime(&ms, ev_a, ev_b));
+        resid_ms += ms;
+        resid_n++;
+    }
+    launch_reduce_sum(s, d_partial, residual_blocks(P), d_scalar);
+    const double r = std::sqrt(read_scalar(0));
+    t_func += wall_now() - t0;
+    return r;
+}
+
+// iflag = 2: FD Jacobian blocks + normal equations + column norms at x.
+void Plan::jac(const double *dx) {
+    const double t0 = wall_now();
+    const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
+    launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
+    launch_set_attrs(s, P, d_ext);
+    launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 0);
+    if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
+    launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
+                    d_stale, d_eu, d_ed);
+    launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
+              d_glob_partial, glob_chunk, d_acnorm);
+    if (timing) {
+        MMBA_HIP(hipEventRecord(ev_b, s));
+        MMBA_HIP(hipEventSynchronize(ev_b));
+        float ms = 0.f;
+        MMBA_HIP(hipEventElapsedTime(&ms, ev_a, ev_b));
+        jac_ms += ms;
+        jac_n++;
+    }
+    MMBA_HIP(hipStreamSynchronize(s));
+    t_jac += wall_now() - t0;
+}
+
+// d_xs = (A + lam D^2)^-1 g.  Returns false if a factorisation failed.
+bool Plan::solve_damped(double lam) {
+    const double t0 = wall_now();
+    MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));
+    if (nB_solved > 0) {
+        launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
+        launch_schur_obs(s, P, d_J, d_Lb, d_W);
+    }
+    if (nR > 0) {
+        MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
+        launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, d_S, d_slot, NT, d_rhs);
+        if (nB_solved > 0) launch_schur_pairs(s, P, d_W, d_Wg, d_tb, d_S, d_slot, NT, d_rhs);
+        if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
+        for (int k = 0; k < NT; ++k) {
+            const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
+            launch_chol_panel(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_fail);
+            const int q0 = panel_pairs_off[k], nq = panel_pairs_off[k + 1] - q0;
+            launch_chol_update(s, d_S, d_slot, NT, k, d_pairs + q0, nq);
+        }
+        if (timing) {
+            MMBA_HIP(hipEventRecord(ev_b, s));
+            MMBA_HIP(hipEventSynchronize(ev_b));
+            float ms = 0.f;
+            MMBA_HIP(hipEventElapsedTime(&ms, ev_a, ev_b));
+            chol_ms += ms;
+            chol_n++;
+        }
+        for (int k = 0; k < NT; ++k) {
+            const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
+            launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_rhs, d_yR);
+        }
+        for (int k = NT - 1; k >= 0; --k) {
+            const int c0 = panel_cols_off[k], nc = panel_cols_off[k + 1] - c0;
+            launch_trsv_bwd(s, d_S, d_slot, NT, k, d_cols + c0, nc, d_Linv, d_yR, d_xR);
+        }
+        launch_scatter_xR(s, P, d_xR, d_xs);
+    }
+    if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_xs);
+    MMBA_HIP(hipMemcpyAsync(h_fail, d_fail, sizeof(int), hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+    t_linear += wall_now() - t0;
+    return *h_fail == 0;
+}
+
+// sqrt(v^T (A + lam D^2)^-1 v) with v = D^2 xs / dxnorm, using the current
+// factorisation (lmpar's parl / parc denominators).
+double Plan::newton_term(double dxnorm) {
+    const double t0 = wall_now();
+    launch_newton_v(s, n, d_diag, d_xs, dxnorm, d_v);
+    double acc = 0.;
+    if (nR > 0) launch_gather_R(s, P, d_v, d_wR, nRpad);
+    if (nB_solved > 0) {
+        launch_newton_bundle(s, P, d_W, d_Wg, d_Lb, d_v, d_wR, d_usq);
+        launch_reduce_sum(s, d_usq, nB, d_scalar + 2);
+        acc += read_scalar(2);
+    }
+    if (nR > 0) {
+        for (int k = 0; k < NT; ++k) {
+            const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
+            launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
+        }
+        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + 3);
+        acc += read_scalar(3);
+    }
+    t_linear += wall_now() - t0;
+    return std::sqrt(acc);
+}
+
+// lmpar restated on normal equations (see oracle/refcpu.c lmpar).
+static double lmpar_ne(Plan &pl, double delta, double *par) {
+    const double p1 = .1, p001 = .001;
+    const double dwarf = DBL_MIN;
+    int iter = 0;
+    const bool ok0 = pl.solve_damped(0.0);
+    double dxnorm = ok0 ? pl.dnorm(pl.d_xs) : HUGE_VAL;
+    double fp = dxnorm - delta;
+    if (fp <= p1 * delta) {
+        if (iter == 0) *par = 0.;
+        return dxnorm;
+    }
+    double parl = 0.;
+    if (!pl.rank_deficient && ok0) {
+        const double temp = pl.newton_term(dxnorm);
+        parl = fp / delta / temp / temp;
+    }
+    launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts, pl.d_scalar + 4);
+    const double gnorm = std::sqrt(pl.read_scalar(4));
+    double paru = gnorm / delta;
+    if (paru == 0.) paru = dwarf / std::min(delta, p1);
+    *par = std::max(*par, parl);
+    *par = std::min(*par, paru);
+    if (*par == 0.) *par = gnorm / dxnorm;
+    for (;;) {
+        ++iter;
+        if (*par == 0.) *par = std::max(dwarf, p001 * paru);
+        pl.solve_damped(*par);
+        dxnorm = pl.dnorm(pl.d_xs);
+        double temp = fp;
+        fp = dxnorm - delta;
+        if (std::fabs(fp) <= p1 * delta || (parl == 0. && fp <= temp && temp < 0.) || iter == 10)
+            break;
+        temp = pl.newton_term(dxnorm);
+        const double parc = fp / delta / temp / temp;
+        if (fp > 0.) parl = std::max(parl, *par);
+        if (fp < 0.) paru = std::min(paru, *par);
+        *par = std::max(parl, *par + parc);
+    }
+    if (iter == 0) *par = 0.;
+    return dxnorm;
+}
+
+void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
+                              double *f_out, double *eu_out, double *ed_out) {
+    double *tf = f_out ? d_ftrial : nullptr;  // scratch buffers for the permutation
+    double *te = eu_out ? d_J : nullptr;
+    double *td = ed_out ? d_J + m : nullptr;
+    launch_unpermute(s, M, d_ref_of_dev, f_out ? d_f2 : nullptr, eu_out ? d_eu2 : nullptr,
+                     ed_out ? d_ed1 : nullptr, tf, te, td);
+    if (f_out) MMBA_HIP(hipMemcpyAsync(f_out, tf, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+    if (eu_out)
+        MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+    if (ed_out)
+        MMBA_HIP(hipMemcpyAsync(ed_out, td, sizeof(double) * M, hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+}
+
+static void error_stats(const double *dist, int M, double *avg, double *mn, double *mx) {
+    double a = 0., lo = DBL_MAX, hi = -0.0;
+    for (int i = 0; i < M; ++i) {
+        const double e = dist[i];
+        if (!std::isfinite(e)) continue;
+        a += e;
+        if (e < lo) lo = e;
+        if (e > hi) hi = e;
+    }
+    a /= M;
+    *avg = a;
+    *mn = lo;
+    *mx = hi;
+}
+
+int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
+                  double *stats) {
+    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    if (x) {
+        MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
+        fun(d_x, d_f, d_eu, d_ed);
+    } else {
+        launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
+        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
+    }
+    std::vector<double> ed(M);
+    download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed.data());
+    if (ed_out) std::memcpy(ed_out, ed.data(), sizeof(double) * M);
+    if (stats) error_stats(ed.data(), M, &stats[0], &stats[1], &stats[2]);
+    return MMBA_OK;
+}
+
+// Dense reference-order Jacobian at x (column-major, ldfjac = m); for tests
+// and small problems only.
+int Plan::dense_jacobian(const double *x, double *fjac) {
+    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    fun(d_x, d_f, d_eu, d_ed);
+    jac(d_x);
+    std::vector<double> J((size_t)2 * LMAX * M);
+    std::vector<int> jc((size_t)LMAX * M), nl(M);
+    MMBA_HIP(hipMemcpyAsync(J.data(), d_J, sizeof(double) * J.size(), hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipMemcpyAsync(jc.data(), d_jcol, sizeof(int) * jc.size(), hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipMemcpyAsync(nl.data(), d_nloc, sizeof(int) * M, hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+    std::memset(fjac, 0, sizeof(double) * (size_t)m * n);
+    for (int i = 0; i < M; ++i) {
+        const int r = ref_of_dev[i];
+        for (int l = 0; l < nl[i]; ++l) {
+            const int p = jc[(size_t)l * M + i];
+            fjac[(size_t)p * m + 2 * r] = J[(size_t)(2 * l) * M + i];
+            fjac[(size_t)p * m + 2 * r + 1] = J[(size_t)(2 * l + 1) * M + i];
+        }
+    }
+    return MMBA_OK;
+}
+
+int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
+                mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {
+    const double t_start = wall_now();
+    t_func = t_jac = t_linear = 0.;
+    mmba_result r;
+    std::memset(&r, 0, sizeof(r));
+    if (trace) trace->count = 0;
+    auto push_trace = [&](double fn) {
+        if (trace) {
+            if (trace->count < trace->capacity) trace->fnorm[trace->count] = fn;
+            trace->count++;
+        }
+    };
+    // fresh attribute block (the scene's current values)
+    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    std::vector<double> ed_host(M);
+    double init_avg = 0., init_min = 0., init_max = 0.;
+    if (opt.accept_only_better) {
+        // measureErrors before any parameter is set (adjust_base.cpp:1080-1103)
+        launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
+        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
+        download_ref_order(nullptr, nullptr, d_ed, nullptr, nullptr, ed_host.data());
+        error_stats(ed_host.data(), M, &init_avg, &init_min, &init_max);
+    }
+    r.error_initial_avg = init_avg;
+
+    std::vector<double> x0(x_inout, x_inout + n);
+    MMBA_HIP(hipMemcpyAsync(d_x, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    MMBA_HIP(hipMemsetAsync(d_diag, 0, sizeof(double) * n, s));
+
+    const double p1 = .1, p5 = .5, p25 = .25, p75 = .75, p0001 = 1e-4;
+    const double epsmch = DBL_EPSILON;
+    const int mode = opt.auto_param_scale == 1 ? 1 : 2;
+    const double factor = opt.tau * 100.0;
+    const double ftol = opt.eps1, xtol = opt.eps2, gtol = opt.eps3;
+    const int maxfev = opt.iter_max;
+    const bool lmdif = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDIF;
+    int info = 0, nfev = 0, njev = 0, func_evals = 0, jac_evals = 0;
+    bool interrupted = false;
+    double delta = 0., xnorm = 0., par = 0., fnorm = 0., gnorm = 0., ratio = 0.;
+
+    if (n <= 0 || m < n || ftol < 0. || xtol < 0. || gtol < 0. || maxfev <= 0 || factor <= 0.)
+        goto TERMINATE;
+    if (mode == 2) {
+        // diag = paramWeightList = 1.0 (adjust_base.cpp: countUpNumberOfUnknownParameters)
+        std::vector<double> ones(n, 1.0);
+        MMBA_HIP(hipMemcpyAsync(d_diag, ones.data(), sizeof(double) * n, hipMemcpyHostToDevice, s));
+    }
+    fnorm = fun(d_x, d_f, d_eu, d_ed);
+    nfev = 1;
+    func_evals = 1;
+    push_trace(fnorm);
+    {
+        int iter = 1;
+        for (;;) {
+            if (cb && cb->interrupt && cb->interrupt(cb->user)) {
+                interrupted = true;
+                info = -1;
+                goto TERMINATE;
+            }
+            if (cb && cb->progress) cb->progress(cb->user, njev);
+            jac(d_x);
+            ++njev;
+            jac_evals += n;
+            if (lmdif) nfev += n;
+            {
+                // rank deficiency from exactly-zero columns (MINPACK nsing < n)
+                std::vector<double> acn(n);
+                MMBA_HIP(hipMemcpyAsync(acn.data(), d_acnorm, sizeof(double) * n,
+                                        hipMemcpyDeviceToHost, s));
+                MMBA_HIP(hipStreamSynchronize(s));
+                rank_deficient = false;
+                for (double v : acn)
+                    if (v == 0.) rank_deficient = true;
+            }
+            launch_diag_init(s, n, d_acnorm, d_diag, iter == 1, mode);
+            if (iter == 1) {
+                // diag set from acnorm (mode 1) *before* the max() update in
+                // lmder; both happen before xnorm only on the first pass, and
+                // max(diag, acnorm) == acnorm there, so one kernel suffices.
+                xnorm = dnorm(d_x);
+                delta = factor * xnorm;
+                if (delta == 0.) delta = factor;
+            }
+            gnorm = 0.;
+            if (fnorm != 0.) {
+                launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + 6);
+                gnorm = read_scalar(6);
+            }
+            if (gnorm <= gtol) info = 4;
+            if (info != 0) goto TERMINATE;
+            do {
+                const double dxn = lmpar_ne(*this, delta, &par);
+                (void)dxn;
+                launch_lm_step(s, n, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3);
+                launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + 1);
+                const double pnorm = std::sqrt(read_scalar(1));
+                if (iter == 1) delta = std::min(delta, pnorm);
+                const double fnorm1 = fun(d_wa2, d_ftrial, d_eu, d_ed);
+                ++nfev;
+                ++func_evals;
+                push_trace(fnorm1);
+                double actred = -1.;
+                if (p1 * fnorm1 < fnorm) {
+                    const double d1 = fnorm1 / fnorm;
+                    actred = 1. - d1 * d1;
+                }
+                launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, d_partial, nparts, d_scalar + 1);
+                const double temp1 = std::sqrt(read_scalar(1)) / fnorm;
+                const double temp2 = (std::sqrt(par) * pnorm) / fnorm;
+                const double prered = temp1 * temp1 + temp2 * temp2 / p5;
+                const double dirder = -(temp1 * temp1 + temp2 * temp2);
+                ratio = 0.;
+                if (prered != 0.) ratio = actred / prered;
+                if (ratio <= p25) {
+                    double temp;
+                    if (actred >= 0.)
+                        temp = p5;
+                    else
+                        temp = p5 * dirder / (dirder + p5 * actred);
+                    if (p1 * fnorm1 >= fnorm || temp < p1) temp = p1;
+                    delta = temp * std::min(delta, pnorm / p1);
+                    par /= temp;
+                } else if (par == 0. || ratio >= p75) {
+                    delta = pnorm / p5;
+                    par = p5 * par;
+                }
+                if (ratio >= p0001) {
+                    MMBA_HIP(hipMemcpyAsync(d_x, d_wa2, sizeof(double) * n,
+                                            hipMemcpyDeviceToDevice, s));
+                    std::swap(d_f, d_ftrial);
+                    xnorm = dnorm(d_x);
+                    fnorm = fnorm1;
+                    ++iter;
+                }
+                if (std::fabs(actred) <= ftol && prered <= ftol && p5 * ratio <= 1.) info = 1;
+                if (delta <= xtol * xnorm) info = 2;
+                if (std::fabs(actred) <= ftol && prered <= ftol && p5 * ratio <= 1. && info == 2)
+                    info = 3;
+                if (info != 0) goto TERMINATE;
+                if (nfev >= maxfev) info = 5;
+                if (std::fabs(actred) <= epsmch && prered <= epsmch && p5 * ratio <= 1.) info = 6;
+                if (delta <= epsmch * xnorm) info = 7;
+                if (gnorm <= epsmch) info = 8;
+                if (info != 0) goto TERMINATE;
+            } while (ratio < p0001);
+        }
+    }
+TERMINATE:
+    r.reason_number = info;
+    r.iterations = nfev;
+    r.function_evals = func_evals;
+    r.jacobian_evals = jac_evals;
+    r.outer_iterations = njev;
+    r.user_interrupted = interrupted ? 1 : 0;
+    r.success = func_evals > 0;
+    r.error_final = fnorm;
+    {
+        std::vector<double> xh(n);
+        MMBA_HIP(hipMemcpyAsync(xh.data(), d_x, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+        download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_host.data());
+        if (ed_out) std::memcpy(ed_out, ed_host.data(), sizeof(double) * M);
+        double avg, mn, mx;
+        error_stats(ed_host.data(), M, &avg, &mn, &mx);
+        r.error_avg = avg;
+        r.error_min = mn;
+        r.error_max = mx;
+        int better = 1;
+        if (opt.accept_only_better) better = avg <= init_avg;
+        r.error_is_better = better;
+        if (better)
+            std::memcpy(x_inout, xh.data(), sizeof(double) * n);
+        else
+            std::memcpy(x_inout, x0.data(), sizeof(double) * n);
+        // RMS at the returned parameters
+        MMBA_HIP(hipMemcpyAsync(d_wa2, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
+        fun(d_wa2, d_ftrial, d_J, d_J + m);  // scratch user buffers
+        launch_sumsq(s, d_J + m, nullptr, M, d_partial, nparts, d_scalar + 7);
+        r.error_rms = std::sqrt(read_scalar(7) / M);
+    }
+    r.num_trace = trace ? trace->count : 0;
+    r.time_solve_s = wall_now() - t_start;
+    r.time_func_s = t_func;
+    r.time_jac_s = t_jac;
+    r.time_linear_s = t_linear;
+    if (res) *res = r;
+    return interrupted ? MMBA_ERR_INTERRUPTED : MMBA_OK;
+}
+
+}  // namespace mmba

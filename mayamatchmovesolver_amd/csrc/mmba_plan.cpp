@@ -1,0 +1,508 @@
+// mmba_plan.cpp -- plan construction: validation, parameter classification,
+// observation ordering and the symbolic structure of the reduced system.
+//
+// The classification replaces the dense errorToParamList / paramFrameList of
+// the reference (adjust_relationships.cpp:565-617, :270-329): every
+// parameter is one of
+//   CF  animated attribute that only reaches one camera at one frame
+//       (camera pose, focal per frame)          -> camera-frame block
+//   B   static attribute that only reaches one bundle
+//       (bundle translate)                      -> bundle block (Schur)
+//   G   anything else (static camera attrs, lens coefficients, group
+//       transforms shared by several bundles/cameras) -> dense arrow rows
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <set>
+
+#include "mmba_kernels.h"
+#include "mmba_plan.h"
+
+namespace mmba {
+
+Plan::~Plan() {
+    if (ev_a) (void)hipEventDestroy(ev_a);
+    if (ev_b) (void)hipEventDestroy(ev_b);
+    for (void *p : allocs) (void)hipFree(p);
+    if (h_scalar) (void)hipHostFree(h_scalar);
+    if (h_fail) (void)hipHostFree(h_fail);
+}
+
+static void require(bool c, const char *what) {
+    if (!c) throw Invalid{what};
+}
+
+void Plan::build(const mmba_problem *pr, const mmba_options *o) {
+    require(pr && o, "null problem/options");
+    opt = *o;
+    s = ctx->stream;
+    F = pr->num_frames;
+    const int nA = pr->num_attrs, nT = pr->num_transforms, nC = pr->num_cameras;
+    const int nL = pr->num_lenses, nK = pr->num_markers;
+    nB = pr->num_bundles;
+    M = pr->num_obs;
+    n = pr->num_params;
+    m = 2 * M;
+    require(F > 0 && M > 0 && n > 0, "empty problem");
+    require(n <= m, "more parameters than errors (adjust_base.cpp:864)");
+    require(opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER ||
+                opt.solver_type == MMBA_SOLVER_CMINPACK_LMDIF,
+            "solver_type");
+    require(opt.scene_graph_mode == MMBA_SCENE_GRAPH_MAYA_DAG ||
+                opt.scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH,
+            "scene_graph_mode");
+    if (opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER &&
+        opt.auto_diff_type == MMBA_AUTO_DIFF_CENTRAL)
+        throw Unsupported{"central differences (B15: reference zero-initialises errorListB)"};
+
+    // ---- validate indices ----
+    for (int a = 0; a < nA; ++a) require(pr->attr_offset[a] >= 0, "attr_offset");
+    for (int t = 0; t < nT; ++t) {
+        require(pr->tfm_parent[t] < t, "transforms must be topologically sorted");
+        for (int k = 0; k < 9; ++k) require(pr->tfm_attrs[9 * t + k] < nA, "tfm attr id");
+    }
+    for (int c = 0; c < nC; ++c) {
+        require(pr->cam_tfm[c] >= 0 && pr->cam_tfm[c] < nT, "cam_tfm");
+        for (int k = 0; k < MMBA_CAM_NUM_ATTRS; ++k)
+            require(pr->cam_attrs[MMBA_CAM_NUM_ATTRS * c + k] < nA, "cam attr id");
+        if (pr->cam_lens) require(pr->cam_lens[c] < nL, "cam_lens");
+    }
+    for (int b = 0; b < nB; ++b) require(pr->bnd_tfm[b] >= 0 && pr->bnd_tfm[b] < nT, "bnd_tfm");
+    for (int k = 0; k < nK; ++k) {
+        require(pr->mkr_cam[k] >= 0 && pr->mkr_cam[k] < nC, "mkr_cam");
+        require(pr->mkr_bnd[k] >= 0 && pr->mkr_bnd[k] < nB, "mkr_bnd");
+    }
+    if (opt.scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH)
+        for (int k = 1; k < nK; ++k)
+            if (pr->mkr_cam[k] < pr->mkr_cam[k - 1])
+                throw Unsupported{"MMSG needs markers grouped by ascending camera (B4)"};
+    for (int i = 0; i < M; ++i) {
+        require(pr->obs_marker[i] >= 0 && pr->obs_marker[i] < nK, "obs_marker");
+        require(pr->obs_frame[i] >= 0 && pr->obs_frame[i] < F, "obs_frame");
+        require(pr->obs_weight[i] > 0.0, "obs_weight must be > 0");
+    }
+    for (int p = 0; p < n; ++p) {
+        const int a = pr->param_attr[p];
+        require(a >= 0 && a < nA, "param_attr");
+        require(pr->attr_animated[a] ? (pr->param_frame[p] >= 0 && pr->param_frame[p] < F)
+                                     : pr->param_frame[p] < 0,
+                "param_frame must be -1 for static and a frame for animated attrs");
+    }
+    int lens_owner = -2;
+    for (int c = 0; c < nC; ++c) {
+        const int l = pr->cam_lens ? pr->cam_lens[c] : -1;
+        if (l >= 0 && pr->lens_type[l] != MMBA_LENS_3DE_CLASSIC)
+            throw Unsupported{"only the 3DE classic lens model is mapped"};
+        // B3: the reference mixes per-marker/per-attr lens indices; it is only
+        // well defined when every camera shares one lens (or none has one).
+        if (lens_owner == -2) lens_owner = l;
+        else if (l != lens_owner)
+            throw Unsupported{"cameras with different lens models (B3)"};
+    }
+
+    // ---- attribute -> dependent cameras / bundles / lens-cameras ----
+    std::vector<std::vector<int>> chain(nT);
+    for (int t = 0; t < nT; ++t) {
+        for (int u = t; u >= 0; u = pr->tfm_parent[u]) chain[t].push_back(u);
+        if ((int)chain[t].size() > 16) throw Unsupported{"transform hierarchy deeper than 16"};
+    }
+    std::vector<std::vector<int>> attr_cams(nA), attr_bnds(nA), attr_lcams(nA);
+    for (int c = 0; c < nC; ++c) {
+        std::set<int> dep;
+        for (int t : chain[pr->cam_tfm[c]])
+            for (int k = 0; k < 9; ++k) dep.insert(pr->tfm_attrs[9 * t + k]);
+        for (int k = 0; k < MMBA_CAM_NUM_ATTRS; ++k) dep.insert(pr->cam_attrs[MMBA_CAM_NUM_ATTRS * c + k]);
+        for (int a : dep)
+            if (a >= 0) attr_cams[a].push_back(c);
+        const int l = pr->cam_lens ? pr->cam_lens[c] : -1;
+        if (l >= 0)
+            for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+                const int a = pr->lens_attrs[MMBA_LENS_NUM_ATTRS * l + k];
+                if (a >= 0) attr_lcams[a].push_back(c);
+            }
+    }
+    for (int b = 0; b < nB; ++b) {
+        std::set<int> dep;
+        const int t0 = pr->bnd_tfm[b];
+        for (int k = 0; k < 3; ++k) dep.insert(pr->tfm_attrs[9 * t0 + k]);
+        for (size_t q = 1; q < chain[t0].size(); ++q)
+            for (int k = 0; k < 9; ++k) dep.insert(pr->tfm_attrs[9 * chain[t0][q] + k]);
+        for (int a : dep)
+            if (a >= 0) attr_bnds[a].push_back(b);
+    }
+
+    // ---- camera-frame keys: every (camera, frame) with observations ----
+    std::vector<int> obs_cam(M);
+    for (int i = 0; i < M; ++i) obs_cam[i] = pr->mkr_cam[pr->obs_marker[i]];
+    std::map<std::pair<int, int>, int> cf_id;
+    for (int i = 0; i < M; ++i) cf_id[{obs_cam[i], pr->obs_frame[i]}] = 0;
+
+    // ---- classify parameters ----
+    std::vector<int> p_class(n), p_blk(n, -1), p_pos(n, -1), p_both(n, 0);
+    std::vector<std::pair<int, int>> p_cfkey(n, {-1, -1});
+    for (int p = 0; p < n; ++p) {
+        const int a = pr->param_attr[p], fp = pr->param_frame[p];
+        const auto &cams = attr_cams[a];
+        const auto &bnds = attr_bnds[a];
+        const auto &lc = attr_lcams[a];
+        if (!lc.empty() && (!cams.empty() || !bnds.empty()))
+            throw Unsupported{"attribute used both as lens coefficient and geometry"};
+        p_both[p] = (!cams.empty() && !bnds.empty()) ? 1 : 0;
+        if (lc.empty() && bnds.empty() && cams.size() == 1 && fp >= 0) {
+            p_class[p] = PC_CF;
+            p_cfkey[p] = {cams[0], fp};
+            cf_id[{cams[0], fp}] = 0;
+        } else if (lc.empty() && cams.empty() && bnds.size() == 1 && fp < 0) {
+            p_class[p] = PC_B;
+            p_blk[p] = bnds[0];
+        } else {
+            p_class[p] = PC_G;
+        }
+    }
+    // number the camera-frames (camera-major, frame-minor)
+    ncf = 0;
+    std::vector<int> cf_cam, cf_frame;
+    for (auto &kv : cf_id) {
+        kv.second = ncf++;
+        cf_cam.push_back(kv.first.first);
+        cf_frame.push_back(kv.first.second);
+    }
+    // CF blocks
+    std::vector<std::vector<int>> cf_params(ncf);
+    for (int p = 0; p < n; ++p)
+        if (p_class[p] == PC_CF) {
+            const int cf = cf_id[p_cfkey[p]];
+            p_blk[p] = cf;
+            cf_params[cf].push_back(p);
+        }
+    std::vector<int> cf_pc(ncf), cf_roff(ncf);
+    nCF = 0;
+    for (int cf = 0; cf < ncf; ++cf) {
+        cf_pc[cf] = (int)cf_params[cf].size();
+        if (cf_pc[cf] > PCMAX) throw Unsupported{"more than 10 parameters on one camera-frame"};
+        cf_roff[cf] = nCF;
+        for (int a = 0; a < cf_pc[cf]; ++a) p_pos[cf_params[cf][a]] = nCF + a;
+        nCF += cf_pc[cf];
+    }
+    // globals
+    std::vector<int> g_param;
+    for (int p = 0; p < n; ++p)
+        if (p_class[p] == PC_G) g_param.push_back(p);
+    nG = (int)g_param.size();
+    if (nG > NGMAX) throw Unsupported{"more than 16 global parameters"};
+    for (int q = 0; q < nG; ++q) p_pos[g_param[q]] = nCF + q;
+    nR = nCF + nG;
+
+    // camera variants: base, CF-block params, cam-side globals valid at the frame
+    std::vector<int> cf_var_off(ncf + 1, 0), cf_var_param, cf_var_flags, var_cf;
+    for (int cf = 0; cf < ncf; ++cf) {
+        cf_var_off[cf] = (int)cf_var_param.size();
+        cf_var_param.push_back(-1);
+        cf_var_flags.push_back(0);
+        var_cf.push_back(cf);
+        for (int p : cf_params[cf]) {
+            cf_var_param.push_back(p);
+            cf_var_flags.push_back(p_both[p] ? VF_BUNDLE_SIDE : 0);
+            var_cf.push_back(cf);
+        }
+        for (int p : g_param) {
+            const int a = pr->param_attr[p], fp = pr->param_frame[p];
+            if (fp >= 0 && fp != cf_frame[cf]) continue;
+            const auto &cams = attr_cams[a];
+            if (std::find(cams.begin(), cams.end(), cf_cam[cf]) == cams.end()) continue;
+            cf_var_param.push_back(p);
+            cf_var_flags.push_back(p_both[p] ? VF_BUNDLE_SIDE : 0);
+            var_cf.push_back(cf);
+        }
+    }
+    cf_var_off[ncf] = (int)cf_var_param.size();
+    nvar = cf_var_off[ncf];
+
+    // bundle-side lists: B params first, then bundle-side globals
+    std::vector<std::vector<int>> bpar(nB);
+    for (int p = 0; p < n; ++p)
+        if (p_class[p] == PC_B) bpar[p_blk[p]].push_back(p);
+    std::vector<int> bnd_pb(nB), bnd_par_off(nB + 1, 0), bnd_par;
+    nB_solved = 0;
+    for (int b = 0; b < nB; ++b) {
+        bnd_pb[b] = (int)bpar[b].size();
+        if (bnd_pb[b] > PBMAX) throw Unsupported{"more than 3 parameters on one bundle"};
+        if (bnd_pb[b] > 0) ++nB_solved;
+        for (int a = 0; a < bnd_pb[b]; ++a) p_pos[bpar[b][a]] = a;
+    }
+    std::vector<std::vector<int>> bglob(nB);
+    for (int p : g_param)
+        for (int b : attr_bnds[pr->param_attr[p]]) bglob[b].push_back(p);
+    for (int b = 0; b < nB; ++b) {
+        bnd_par_off[b] = (int)bnd_par.size();
+        for (int p : bpar[b]) bnd_par.push_back(p);
+        for (int p : bglob[b]) bnd_par.push_back(p);
+    }
+    bnd_par_off[nB] = (int)bnd_par.size();
+    // lens params per camera
+    std::vector<int> cam_lpar_off(nC + 1, 0), cam_lpar;
+    for (int c = 0; c < nC; ++c) {
+        cam_lpar_off[c] = (int)cam_lpar.size();
+        for (int p : g_param) {
+            const auto &lc = attr_lcams[pr->param_attr[p]];
+            if (std::find(lc.begin(), lc.end(), c) != lc.end()) cam_lpar.push_back(p);
+        }
+    }
+    cam_lpar_off[nC] = (int)cam_lpar.size();
+
+    // ---- observations in device order (by camera-frame) ----
+    std::vector<int> obs_cf(M);
+    for (int i = 0; i < M; ++i) obs_cf[i] = cf_id[{obs_cam[i], pr->obs_frame[i]}];
+    ref_of_dev.resize(M);
+    std::iota(ref_of_dev.begin(), ref_of_dev.end(), 0);
+    std::stable_sort(ref_of_dev.begin(), ref_of_dev.end(),
+                     [&](int a, int b) { return obs_cf[a] < obs_cf[b]; });
+    std::vector<int> d_cf(M), d_bnd(M), d_frame(M), d_cam(M);
+    std::vector<double> d_xy(2 * (size_t)M), d_sqrtw(M);
+    std::vector<int> cf_obs_off(ncf + 1, 0);
+    for (int i = 0; i < M; ++i) {
+        const int r = ref_of_dev[i];
+        d_cf[i] = obs_cf[r];
+        d_bnd[i] = pr->mkr_bnd[pr->obs_marker[r]];
+        d_frame[i] = pr->obs_frame[r];
+        d_cam[i] = obs_cam[r];
+        d_xy[2 * i] = pr->obs_xy[2 * r];
+        d_xy[2 * i + 1] = pr->obs_xy[2 * r + 1];
+        d_sqrtw[i] = std::sqrt(pr->obs_weight[r]);
+        cf_obs_off[d_cf[i] + 1]++;
+    }
+    for (int cf = 0; cf < ncf; ++cf) cf_obs_off[cf + 1] += cf_obs_off[cf];
+    // local column bound
+    for (int i = 0; i < M; ++i) {
+        const int cf = d_cf[i];
+        const int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
+                       (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) +
+                       (cam_lpar_off[d_cam[i] + 1] - cam_lpar_off[d_cam[i]]);
+        if (nl > LMAX) throw Unsupported{"more than 20 parameters reach one observation"};
+    }
+    // observations grouped by bundle
+    std::vector<int> bobs_off(nB + 1, 0), bobs(M);
+    for (int i = 0; i < M; ++i) bobs_off[d_bnd[i] + 1]++;
+    for (int b = 0; b < nB; ++b) bobs_off[b + 1] += bobs_off[b];
+    {
+        std::vector<int> fill(bobs_off.begin(), bobs_off.end() - 1);
+        for (int i = 0; i < M; ++i) bobs[fill[d_bnd[i]]++] = i;
+    }
+    // stale errorDistanceList source per frame (B13): last parameter whose
+    // frame mask includes the frame; lmdif re-measures everything per column.
+    std::vector<int> stale(F, -1);
+    for (int f = 0; f < F; ++f) {
+        if (opt.solver_type == MMBA_SOLVER_CMINPACK_LMDIF) {
+            stale[f] = n - 1;
+            continue;
+        }
+        for (int p = n - 1; p >= 0; --p)
+            if (pr->param_frame[p] < 0 || pr->param_frame[p] == f) {
+                stale[f] = p;
+                break;
+            }
+    }
+
+    // ---- symbolic tile structure of the reduced system ----
+    NT = nR > 0 ? (nR + TILE - 1) / TILE : 0;
+    nRpad = NT * TILE;
+    std::vector<uint8_t> nz((size_t)NT * NT, 0);
+    auto mark = [&](int R, int C) {
+        int I = R / TILE, J = C / TILE;
+        if (I < J) std::swap(I, J);
+        nz[(size_t)I * NT + J] = 1;
+    };
+    for (int I = 0; I < NT; ++I) nz[(size_t)I * NT + I] = 1;
+    for (int cf = 0; cf < ncf; ++cf)
+        if (cf_pc[cf] > 0) {
+            mark(cf_roff[cf], cf_roff[cf]);
+            mark(cf_roff[cf] + cf_pc[cf] - 1, cf_roff[cf]);
+            mark(cf_roff[cf] + cf_pc[cf] - 1, cf_roff[cf] + cf_pc[cf] - 1);
+        }
+    if (nG > 0)
+        for (int R = nCF; R < nR; R += 1)
+            for (int J = 0; J < NT; ++J) {
+                int I = R / TILE;
+                if (J <= I) nz[(size_t)I * NT + J] = 1;
+            }
+    for (int b = 0; b < nB; ++b) {
+        if (bnd_pb[b] == 0) continue;
+        std::set<int> tiles;
+        for (int q = bobs_off[b]; q < bobs_off[b + 1]; ++q) {
+            const int cf = d_cf[bobs[q]];
+            if (cf_pc[cf] == 0) continue;
+            tiles.insert(cf_roff[cf] / TILE);
+            tiles.insert((cf_roff[cf] + cf_pc[cf] - 1) / TILE);
+        }
+        for (int I : tiles)
+            for (int J : tiles)
+                if (J <= I) nz[(size_t)I * NT + J] = 1;
+    }
+    // symbolic fill-in
+    panel_rows_off.assign(NT + 1, 0);
+    panel_rows.clear();
+    std::vector<int2> pairs;
+    panel_pairs_off.assign(NT + 1, 0);
+    for (int k = 0; k < NT; ++k) {
+        std::vector<int> rows;
+        for (int I = k + 1; I < NT; ++I)
+            if (nz[(size_t)I * NT + k]) rows.push_back(I);
+        for (size_t a = 0; a < rows.size(); ++a)
+            for (size_t c = 0; c <= a; ++c) nz[(size_t)rows[a] * NT + rows[c]] = 1;
+        panel_rows_off[k] = (int)panel_rows.size();
+        for (int I : rows) panel_rows.push_back(I);
+        panel_pairs_off[k] = (int)pairs.size();
+        for (size_t a = 0; a < rows.size(); ++a)
+            for (size_t c = 0; c <= a; ++c) pairs.push_back(make_int2(rows[a], rows[c]));
+    }
+    panel_rows_off[NT] = (int)panel_rows.size();
+    panel_pairs_off[NT] = (int)pairs.size();
+    panel_cols_off.assign(NT + 1, 0);
+    panel_cols.clear();
+    for (int k = 0; k < NT; ++k) {
+        panel_cols_off[k] = (int)panel_cols.size();
+        for (int J = 0; J < k; ++J)
+            if (nz[(size_t)k * NT + J]) panel_cols.push_back(J);
+    }
+    panel_cols_off[NT] = (int)panel_cols.size();
+    std::vector<int> slot((size_t)NT * NT, -1);
+    nslots = 0;
+    for (int I = 0; I < NT; ++I)
+        for (int J = 0; J <= I; ++J)
+            if (nz[(size_t)I * NT + J]) slot[(size_t)I * NT + J] = nslots++;
+
+    // ---- device upload ----
+    size_t nvals = 0;
+    for (int a = 0; a < nA; ++a)
+        nvals = std::max(nvals, (size_t)pr->attr_offset[a] + (pr->attr_animated[a] ? F : 1));
+    host_attr0.assign(pr->attr_values, pr->attr_values + nvals);
+    attr_bytes = nvals * sizeof(double);
+
+    DevProblem D{};
+    D.F = F;
+    D.nA = nA;
+    D.nT = nT;
+    D.nC = nC;
+    D.nL = nL;
+    D.nB = nB;
+    D.nK = nK;
+    D.M = M;
+    D.n = n;
+    D.ncf = ncf;
+    D.nR = nR;
+    D.nG = nG;
+    D.mode = opt.scene_graph_mode;
+    D.image_width = opt.image_width;
+    D.attr_off = upload(pr->attr_offset, nA);
+    D.attr_anim = upload(pr->attr_animated, nA);
+    d_attr0 = upload(host_attr0);
+    D.attr_val = dalloc<double>(nvals);
+    D.tfm_parent = upload(pr->tfm_parent, nT);
+    D.tfm_roo = upload(pr->tfm_rotate_order, nT);
+    D.tfm_attrs = upload(pr->tfm_attrs, 9 * (size_t)nT);
+    D.cam_tfm = upload(pr->cam_tfm, nC);
+    D.cam_attrs = upload(pr->cam_attrs, MMBA_CAM_NUM_ATTRS * (size_t)nC);
+    D.cam_fit = upload(pr->cam_film_fit, nC);
+    D.cam_size = upload(pr->cam_render_size, 2 * (size_t)nC);
+    D.cam_lens = pr->cam_lens ? upload(pr->cam_lens, nC) : nullptr;
+    D.lens_attrs = upload(pr->lens_attrs, MMBA_LENS_NUM_ATTRS * (size_t)nL);
+    D.lens_type = upload(pr->lens_type, nL);
+    D.bnd_tfm = upload(pr->bnd_tfm, nB);
+    D.obs_cf = upload(d_cf);
+    D.obs_bnd = upload(d_bnd);
+    D.obs_frame = upload(d_frame);
+    D.obs_cam = upload(d_cam);
+    D.obs_xy = upload(d_xy);
+    D.obs_sqrtw = upload(d_sqrtw);
+    D.cf_cam = upload(cf_cam);
+    D.cf_frame = upload(cf_frame);
+    D.cf_obs_off = upload(cf_obs_off);
+    D.cf_var_off = upload(cf_var_off);
+    D.cf_var_param = upload(cf_var_param);
+    D.cf_var_flags = upload(cf_var_flags);
+    D.cf_pc = upload(cf_pc);
+    D.cf_roff = upload(cf_roff);
+    D.bnd_par_off = upload(bnd_par_off);
+    D.bnd_par = upload(bnd_par);
+    D.bnd_pb = upload(bnd_pb);
+    D.bnd_xoff = nullptr;
+    D.bobs_off = upload(bobs_off);
+    D.bobs = upload(bobs);
+    D.cam_lpar_off = upload(cam_lpar_off);
+    D.cam_lpar = upload(cam_lpar);
+    D.p_attr = upload(pr->param_attr, n);
+    D.p_frame = upload(pr->param_frame, n);
+    D.p_class = upload(p_class);
+    D.p_pos = upload(p_pos);
+    D.p_both = upload(p_both);
+    D.p_blk = upload(p_blk);
+    D.p_min = upload(pr->param_min, n);
+    D.p_max = upload(pr->param_max, n);
+    D.p_off = upload(pr->param_offset, n);
+    D.p_scale = upload(pr->param_scale, n);
+    D.g_param = upload(g_param);
+    P = D;
+
+    d_var_cf = upload(var_cf);
+    d_stale = upload(stale);
+    d_ref_of_dev = upload(ref_of_dev);
+    d_slot = upload(slot);
+    d_rows = upload(panel_rows);
+    d_cols = upload(panel_cols);
+    d_pairs = upload(pairs);
+    d_S = dalloc<double>((size_t)nslots * TILE * TILE);
+    d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
+
+    d_x = dalloc<double>(n);
+    d_ext = dalloc<double>(n);
+    d_ext_pert = dalloc<double>(n);
+    d_step = dalloc<double>(n);
+    d_diag = dalloc<double>(n);
+    d_acnorm = dalloc<double>(n);
+    d_g = dalloc<double>(n);
+    d_wa1 = dalloc<double>(n);
+    d_wa2 = dalloc<double>(n);
+    d_wa3 = dalloc<double>(n);
+    d_xs = dalloc<double>(n);
+    d_v = dalloc<double>(n);
+    d_f = dalloc<double>(m);
+    d_ftrial = dalloc<double>(m);
+    d_eu = dalloc<double>(m);
+    d_ed = dalloc<double>(M);
+    d_recs = dalloc<double>((size_t)nvar * CAMREC);
+    d_J = dalloc<double>((size_t)2 * LMAX * M);
+    d_jcol = dalloc<int>((size_t)LMAX * M);
+    d_nloc = dalloc<int>(M);
+    d_Acc = dalloc<double>((size_t)ncf * PCMAX * PCMAX);
+    d_Acg = dalloc<double>((size_t)ncf * PCMAX * NGMAX);
+    d_Abb = dalloc<double>((size_t)nB * 9);
+    d_Abg = dalloc<double>((size_t)nB * PBMAX * NGMAX);
+    d_Agg = dalloc<double>(NGMAX * NGMAX);
+    d_glob_partial = dalloc<double>((size_t)((M + glob_chunk - 1) / glob_chunk) * (NGMAX * NGMAX + NGMAX));
+    d_Lb = dalloc<double>((size_t)nB * 9);
+    d_tb = dalloc<double>((size_t)nB * 3);
+    d_Wg = dalloc<double>((size_t)nB * NGMAX * 3);
+    d_W = dalloc<double>((size_t)PCMAX * 3 * (nB_solved > 0 ? M : 1));
+    d_rhs = dalloc<double>(nRpad);
+    d_yR = dalloc<double>(nRpad);
+    d_xR = dalloc<double>(nRpad);
+    d_wR = dalloc<double>(nRpad);
+    d_usq = dalloc<double>(nB);
+    d_partial = dalloc<double>(std::max(nparts, residual_blocks(P)));
+    d_scalar = dalloc<double>(8);
+    d_fail = dalloc<int>(1);
+    MMBA_HIP(hipMemsetAsync(d_Acg, 0, sizeof(double) * (size_t)ncf * PCMAX * NGMAX, s));
+    MMBA_HIP(hipMemsetAsync(d_Agg, 0, sizeof(double) * NGMAX * NGMAX, s));
+    MMBA_HIP(hipMemsetAsync(d_Abg, 0, sizeof(double) * (size_t)nB * PBMAX * NGMAX, s));
+    MMBA_HIP(hipMemsetAsync(d_Abb, 0, sizeof(double) * (size_t)nB * 9, s));
+    MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
+    MMBA_HIP(hipHostMalloc(&h_scalar, 8 * sizeof(double)));
+    MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
+    MMBA_HIP(hipEventCreate(&ev_a));
+    MMBA_HIP(hipEventCreate(&ev_b));
+    MMBA_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace mmba

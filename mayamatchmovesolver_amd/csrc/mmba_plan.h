@@ -1,0 +1,145 @@
+// mmba_plan.h -- host-side plan: problem resident in HBM + derived structure.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "mmba_internal.h"
+
+struct mmba_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace mmba {
+
+void set_error(const std::string &msg);
+
+#define MMBA_HIP(call)                                                             \
+    do {                                                                           \
+        hipError_t e_ = (call);                                                    \
+        if (e_ != hipSuccess) {                                                    \
+            ::mmba::set_error(std::string(#call) + ": " + hipGetErrorString(e_));  \
+            throw ::mmba::DeviceError();                                           \
+        }                                                                          \
+    } while (0)
+
+struct DeviceError {};
+struct Unsupported {
+    std::string what;
+};
+struct Invalid {
+    std::string what;
+};
+
+struct Comm;  // RCCL communicator (mmba_comm.cpp)
+
+struct Plan {
+    mmba_context *ctx = nullptr;
+    hipStream_t s = nullptr;
+    mmba_options opt{};
+    DevProblem P{};
+
+    // sizes
+    int n = 0, M = 0, m = 0, F = 0;
+    int ncf = 0, nB = 0, nG = 0, nCF = 0, nR = 0, NT = 0, nRpad = 0, nvar = 0, nslots = 0;
+    int nB_solved = 0;  // bundles with a B block
+    bool rank_deficient = false;
+    int nparts = 256;
+    int glob_chunk = 4096;
+
+    // host structure
+    std::vector<int> ref_of_dev;
+    std::vector<int> panel_rows_off, panel_rows;    // rows(k) flattened
+    std::vector<int> panel_cols_off, panel_cols;    // colsT(k) flattened
+    std::vector<int> panel_pairs_off;               // pairs(k) offsets into d_pairs
+    std::vector<double> host_attr0;
+
+    // device allocations (owned)
+    std::vector<void *> allocs;
+    int *d_slot = nullptr;
+    double *d_S = nullptr, *d_Linv = nullptr;
+    int *d_rows = nullptr, *d_cols = nullptr;
+    int2 *d_pairs = nullptr;
+    int *d_var_cf = nullptr, *d_stale = nullptr, *d_ref_of_dev = nullptr;
+    double *d_attr0 = nullptr;
+    size_t attr_bytes = 0;
+
+    double *d_x = nullptr, *d_ext = nullptr, *d_ext_pert = nullptr, *d_step = nullptr;
+    double *d_diag = nullptr, *d_acnorm = nullptr, *d_g = nullptr;
+    double *d_wa1 = nullptr, *d_wa2 = nullptr, *d_wa3 = nullptr, *d_xs = nullptr,
+           *d_v = nullptr;
+    double *d_f = nullptr, *d_ftrial = nullptr, *d_eu = nullptr, *d_ed = nullptr;
+    double *d_recs = nullptr;
+    double *d_J = nullptr;
+    int *d_jcol = nullptr, *d_nloc = nullptr;
+    double *d_Acc = nullptr, *d_Acg = nullptr, *d_Abb = nullptr, *d_Abg = nullptr,
+           *d_Agg = nullptr, *d_glob_partial = nullptr;
+    double *d_Lb = nullptr, *d_tb = nullptr, *d_Wg = nullptr, *d_W = nullptr;
+    double *d_rhs = nullptr, *d_yR = nullptr, *d_xR = nullptr, *d_wR = nullptr,
+           *d_usq = nullptr;
+    double *d_partial = nullptr, *d_scalar = nullptr;
+    int *d_fail = nullptr;
+    double *h_scalar = nullptr;  // pinned
+    int *h_fail = nullptr;       // pinned
+
+    // timing (HIP events on the plan stream)
+    bool timing = false;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;
+    double jac_ms = 0., resid_ms = 0., chol_ms = 0.;
+    int jac_n = 0, resid_n = 0, chol_n = 0;
+    double t_func = 0., t_jac = 0., t_linear = 0.;
+
+    // multi-GPU
+    Comm *comm = nullptr;
+
+    ~Plan();
+
+    template <class T>
+    T *dalloc(size_t count) {
+        void *p = nullptr;
+        if (count == 0) count = 1;
+        MMBA_HIP(hipMalloc(&p, count * sizeof(T)));
+        allocs.push_back(p);
+        return static_cast<T *>(p);
+    }
+    template <class T>
+    T *upload(const std::vector<T> &v) {
+        T *d = dalloc<T>(v.size());
+        if (!v.empty())
+            MMBA_HIP(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+        return d;
+    }
+    template <class T>
+    T *upload(const T *src, size_t count) {
+        T *d = dalloc<T>(count);
+        if (count && src)
+            MMBA_HIP(hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+        return d;
+    }
+
+    void build(const mmba_problem *prob, const mmba_options *o);
+
+    // LM building blocks
+    double read_scalar(int slot = 0);
+    double fun(const double *dx, double *df, double *eu, double *ed);
+    void jac(const double *dx);
+    bool solve_damped(double lam);
+    double newton_term(double dxnorm);
+    double dnorm(const double *dv);
+    int solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
+              mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace);
+    int dense_jacobian(const double *x, double *fjac);
+    int measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
+                double *stats);
+    void download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
+                            double *f_out, double *eu_out, double *ed_out);
+};
+
+}  // namespace mmba
+
+struct mmba_plan {
+    mmba::Plan impl;
+};

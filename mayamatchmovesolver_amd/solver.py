@@ -1,0 +1,168 @@
+"""Solve entry point: the host-side mirror of ``solveFrames`` -> LM -> results.
+
+``Solver`` keeps the problem resident in HBM (an ``mmba_plan``) so repeated
+solves on the same structure (the Python standard solver issues many,
+``_api/solverstandardutils.py``) do not re-upload.  Results are returned both
+as raw doubles and as the reference's ``key=value`` result strings
+(``SolverResult::appendToMStringArray``, adjust_results.h:117-160) parsed by
+``mmSolver.api.SolveResult`` (python/mmSolver/_api/solveresult.py:127-149).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import abi
+from ._lib import check, lib
+from .problem import Problem
+
+
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _num(v):
+    # mmstring::numberToString uses default 6 significant digits (B10)
+    return "%g" % v
+
+
+@dataclass
+class SolveResult:
+    x: np.ndarray
+    fvec: np.ndarray
+    err_user: np.ndarray
+    err_dist: np.ndarray
+    result: Dict
+    fnorm_trace: np.ndarray
+    kernel_stats: Optional[Dict] = None
+
+    @property
+    def external(self):
+        return self._external
+
+    def result_strings(self) -> List[str]:
+        r = self.result
+        return [
+            "success=%d" % int(r["success"]),
+            "reason_num=%d" % int(r["reason_number"]),
+            "error_final=" + _num(r["error_final"]),
+            "error_final_average=" + _num(r["error_avg"]),
+            "error_final_maximum=" + _num(r["error_max"]),
+            "error_final_minimum=" + _num(r["error_min"]),
+            "iteration_num=%d" % int(r["iterations"]),
+            "iteration_function_num=%d" % int(r["function_evals"]),
+            "iteration_jacobian_num=%d" % int(r["jacobian_evals"]),
+            "user_interrupted=%d" % int(r["user_interrupted"]),
+        ]
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        check(lib().mmba_context_create(int(device), C.byref(self._h)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().mmba_context_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Solver:
+    """A problem uploaded to one MI355X (``mmba_plan``)."""
+
+    def __init__(self, problem: Problem, options, context: Optional[Context] = None,
+                 device: int = 0):
+        self.problem = problem
+        self.options = options
+        self.ctx = context or Context(device)
+        self._prob_c, self._keep = problem.to_ctypes()
+        self._h = C.c_void_p()
+        check(lib().mmba_plan_create(self.ctx.handle, C.byref(self._prob_c),
+                                     C.byref(self.options), C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            lib().mmba_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, enable=True):
+        st = abi.MmbaKernelStats()
+        check(lib().mmba_plan_kernel_stats(self._h, 1 if enable else 0, C.byref(st)))
+
+    def kernel_stats(self):
+        st = abi.MmbaKernelStats()
+        check(lib().mmba_plan_kernel_stats(self._h, 1, C.byref(st)))
+        return st.as_dict()
+
+    def set_comm(self, rank: int, nranks: int, unique_id: bytes):
+        check(lib().mmba_plan_set_comm(self._h, rank, nranks, unique_id))
+
+    def measure(self, x=None):
+        p = self.problem
+        m, M = p.num_residuals, p.num_obs
+        fvec, eu, ed, st = np.zeros(m), np.zeros(m), np.zeros(M), np.zeros(3)
+        xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+        check(lib().mmba_plan_measure(self._h, _dp(xx), _dp(fvec), _dp(eu), _dp(ed), _dp(st)))
+        return fvec, eu, ed, st
+
+    def jacobian(self, x):
+        """Dense reference-layout Jacobian (m x n) at internal parameters x."""
+        p = self.problem
+        m, n = p.num_residuals, p.num_params
+        xx = np.ascontiguousarray(x, dtype=np.float64)
+        fjac = np.zeros(m * n)
+        check(lib().mmba_plan_jacobian(self._h, _dp(xx), _dp(fjac)))
+        return fjac.reshape(n, m).T
+
+    def solve(self, x0=None, trace_capacity=4096, interrupt=None) -> SolveResult:
+        p = self.problem
+        m, M = p.num_residuals, p.num_obs
+        x = np.array(p.x0 if x0 is None else x0, dtype=np.float64)
+        fvec, eu, ed = np.zeros(m), np.zeros(m), np.zeros(M)
+        res = abi.MmbaResult()
+        tbuf = np.zeros(max(1, trace_capacity))
+        tr = abi.MmbaTrace(_dp(tbuf), trace_capacity, 0)
+        cbs = None
+        if interrupt is not None:
+            cbs = abi.MmbaCallbacks(abi.INTERRUPT_FN(lambda _u: 1 if interrupt() else 0),
+                                    abi.PROGRESS_FN(lambda _u, _i: None), None)
+        rc = lib().mmba_plan_solve(self._h, _dp(x), _dp(fvec), _dp(eu), _dp(ed), C.byref(res),
+                                   C.byref(cbs) if cbs is not None else None, C.byref(tr))
+        if rc not in (abi.MMBA_OK, abi.MMBA_ERR_INTERRUPTED):
+            check(rc)
+        out = SolveResult(x=x, fvec=fvec, err_user=eu, err_dist=ed, result=res.as_dict(),
+                          fnorm_trace=tbuf[:min(tr.count, trace_capacity)].copy())
+        out._external = p.external_params(x)
+        return out
+
+
+def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
+    """One-shot solve (``mmba_solve``)."""
+    s = Solver(problem, options, device=device)
+    try:
+        return s.solve(x0)
+    finally:
+        s.close()
+
+
+def device_count() -> int:
+    return int(lib().mmba_device_count())

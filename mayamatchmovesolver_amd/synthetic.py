@@ -341,19 +341,50 @@ def _config_c2(rng, F, scale):
 
 
 def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers):
-    """Full BA: animated cameras (t, r per frame) + static bundles, gauge-locked."""
-    ts, rs = zip(*[_camera_path(rng, F, c) for c in range(n_cams)])
-    P = _bundles_in_front(rng, B)
+    """Full BA: animated cameras (t, r per frame) + static bundles, gauge-locked.
+
+    C3 (``per_cam_markers``): a 10-camera rig (2 units apart) moving slowly,
+    bundles in a box in front, 5 markers per bundle spread over the cameras.
+    C4: one camera dollying 0.5 units/frame; every bundle is placed in front of
+    the camera at the middle of its 4-frame window so the window's baseline
+    (1.5 units) gives usable parallax at depth 20-200."""
     if per_cam_markers:
-        mkr_cam = np.repeat(np.arange(n_cams), K // n_cams)
+        ts, rs = zip(*[_camera_path(rng, F, c) for c in range(n_cams)])
+        P = _bundles_in_front(rng, B)
+        L = K // n_cams
+        mkr_cam = np.repeat(np.arange(n_cams), L)
         K = mkr_cam.size
-        mkr_bnd = np.arange(K) % B
+        # camera c sees bundles [c*B/n_cams, c*B/n_cams + L) mod B: every bundle
+        # is seen by K/B consecutive cameras and the camera/bundle graph is
+        # connected (a plain k mod B splits odd/even cameras into two
+        # disconnected, gauge-free components).
+        k = np.arange(K)
+        mkr_bnd = ((k % L) + (k // L) * max(1, B // n_cams)) % B
         start, length = _windows(rng, K, F, window)
     else:
+        f = np.arange(F, dtype=np.float64)
+        phase = rng.uniform(0, 2 * math.pi, size=4)
+        t = np.stack([0.5 * f, 1.5 + 0.3 * np.sin(0.05 * f + phase[0]),
+                      -0.1 * f + 0.3 * np.sin(0.03 * f + phase[1])], axis=1)
+        r = np.stack([1.5 * np.sin(0.02 * f + phase[2]), -10.0 + 3.0 * np.sin(0.01 * f + phase[3]),
+                      0.5 * np.sin(0.04 * f)], axis=1)
+        ts, rs = (t,), (r,)
         mkr_cam = np.zeros(K, np.int64)
         mkr_bnd = np.arange(K) % B
-        length = np.full(K, window)
-        start = rng.integers(0, F - window + 1, size=K)
+        length = np.full(K, min(window, F))
+        start = rng.integers(0, F - length[0] + 1, size=K)
+        # bundle j placed relative to the camera at the middle of its window
+        mid = np.minimum(start + length // 2, F - 1)
+        P = np.empty((B, 3))
+        depth = rng.uniform(20.0, 200.0, size=B)
+        u = rng.uniform(-0.35, 0.35, size=B)
+        v = rng.uniform(-0.22, 0.22, size=B)
+        owner = np.full(B, -1)
+        owner[mkr_bnd[::-1]] = np.arange(K)[::-1]  # first marker of each bundle
+        fm = mid[np.maximum(owner, 0)]
+        Rm = _euler_xyz(r[fm, 0], r[fm, 1], r[fm, 2])
+        pc = np.stack([u * depth, v * depth, -depth], axis=1)
+        P = t[fm] + np.einsum("nij,nj->ni", Rm, pc)
 
     def proj(ks, fs):
         mx = np.empty(ks.size)
@@ -369,9 +400,18 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers):
     for c in (0,):  # gauge: camera-0 pose at frame 0 exact
         t0[c][0] = ts[c][0]
         r0[c][0] = rs[c][0]
-    P0 = P.copy()
-    ray = P0 - ts[0][0]
-    P0 = ts[0][0] + ray * (1.0 + rng.uniform(-0.05, 0.05, size=(B, 1)))
+    # bundles perturbed +-5% along the ray from the camera that first sees them
+    first_f = np.zeros(B, np.int64)
+    first_c = np.zeros(B, np.int64)
+    seen = np.zeros(B, bool)
+    for q in range(ks.size):
+        j = mkr_bnd[ks[q]]
+        if not seen[j]:
+            seen[j] = True
+            first_f[j] = fs[q]
+            first_c[j] = mkr_cam[ks[q]]
+    origin = np.stack([ts[first_c[j]][first_f[j]] for j in range(B)]) if B else np.zeros((0, 3))
+    P0 = origin + (P - origin) * (1.0 + rng.uniform(-0.05, 0.05, size=(B, 1)))
     P0[0] = P[0]  # gauge: bundle 0 locked at truth
     solved = np.ones(B, bool)
     solved[0] = False

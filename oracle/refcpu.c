@@ -271,6 +271,10 @@ typedef int (*lm_jac_fn)(void *ctx, int m, int n, double *x, double *fvec,
                          double *fjac, int ldfjac, int *nfev, int *njev);
 typedef int (*lm_fun_fn)(void *ctx, int m, int n, const double *x, double *fvec);
 
+#include <stdio.h>
+static int g_debug = 0;
+void ref_set_debug(int d) { g_debug = d; }
+
 static int lm_core(lm_fun_fn fun, lm_jac_fn jac, void *ctx, int m, int n,
                    double *x, double *fvec, double *fjac, int ldfjac,
                    double ftol, double xtol, double gtol, int maxfev,
@@ -351,6 +355,7 @@ static int lm_core(lm_fun_fn fun, lm_jac_fn jac, void *ctx, int m, int n,
                 wa3[j] = diag[j] * wa1[j];
             }
             double pnorm = ref_enorm(n, wa3);
+            if (g_debug) fprintf(stderr, "ref trial: delta=%.17g par=%.17g pnorm=%.17g\n", delta, par, pnorm);
             if (iter == 1) delta = RMIN(delta, pnorm);
             iflag = fun(ctx, m, n, wa2, wa4);
             ++(*nfev);

@@ -1,0 +1,97 @@
+"""GPU parity: libmmba.so (HIP, gfx950) against the CPU oracle on the same inputs.
+
+Bar (BASELINE.json north_star): final parameter vector and per-iteration
+residual norm within 1e-6 relative (fp64).
+"""
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import abi, make_options, synthetic as S
+from mayamatchmovesolver_amd.solver import Solver
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-6
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300))) if a.size else 0.0
+
+
+def check_solve(prob, opt, oracle, gpu_ctx, x_tol=REL, trace_tol=REL):
+    xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        out = s.solve()
+    finally:
+        s.close()
+    g = out.result
+    assert g["reason_number"] == rr.reason_number, (g, rr.as_dict())
+    assert g["iterations"] == rr.iterations
+    assert g["outer_iterations"] == rr.outer_iterations
+    assert g["function_evals"] == rr.function_evals
+    assert g["jacobian_evals"] == rr.jacobian_evals
+    assert len(out.fnorm_trace) == len(trr)
+    # Relative 1e-6 per evaluation; exact-fit scenes converge to ||f|| ~ 1e-10
+    # where only roundoff is left, so an absolute floor of 1e-9 * ||f0|| applies.
+    np.testing.assert_allclose(out.fnorm_trace, trr, rtol=trace_tol, atol=1e-9 * trr[0])
+    xs = np.maximum(np.abs(xr), 1e-3)
+    assert np.max(np.abs(out.x - xr) / xs) <= x_tol, (out.x, xr)
+    assert abs(g["error_final"] - rr.error_final) <= REL * rr.error_final + 1e-9 * trr[0]
+    return out, (xr, rr)
+
+
+@pytest.mark.parametrize("name", sorted(S.KNOWN_ANSWERS))
+@pytest.mark.parametrize("solver_type", [abi.SOLVER_TYPE_CMINPACK_LMDER,
+                                         abi.SOLVER_TYPE_CMINPACK_LMDIF])
+@pytest.mark.parametrize("mode", [abi.SCENE_GRAPH_MODE_MAYA_DAG,
+                                  abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH])
+def test_known_scenes(name, solver_type, mode, oracle, gpu_ctx):
+    prob = S.known_scene(name)
+    opt = make_options(solver_type=solver_type, scene_graph_mode=mode,
+                       iterations=1000 if name == "test1" else 100,
+                       delta=1e-5 if name == "test3" else 1e-4)
+    out, _ = check_solve(prob, opt, oracle, gpu_ctx)
+    expected, tol = S.KNOWN_ANSWERS[name]
+    ext = prob.external_params(out.x)
+    assert np.all(np.abs(ext - np.array(expected)) <= tol), (ext, expected)
+
+
+@pytest.mark.parametrize("mode", [abi.SCENE_GRAPH_MODE_MAYA_DAG,
+                                  abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH])
+def test_measure_and_jacobian_small(mode, oracle, gpu_ctx):
+    prob = S.make_config(3, frames=8, scale=0.001)
+    opt = S.config_options(prob, scene_graph_mode=mode)
+    f_ref, eu_ref, ed_ref, st_ref = oracle.measure(prob, opt)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        f, eu, ed, st = s.measure()
+        np.testing.assert_allclose(f, f_ref, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(ed, ed_ref, rtol=1e-12, atol=1e-12)
+        f2, _, _, _ = s.measure(prob.x0)
+        f2_ref, _, _, _ = oracle.measure(prob, opt, prob.x0)
+        np.testing.assert_allclose(f2, f2_ref, rtol=1e-12, atol=1e-12)
+        J = s.jacobian(prob.x0)
+        _, J_ref = oracle.jacobian(prob, opt, prob.x0)
+        scale = np.max(np.abs(J_ref))
+        assert np.max(np.abs(J - J_ref)) <= 1e-7 * scale
+        assert np.array_equal(J != 0, J_ref != 0) or np.max(np.abs(J[J_ref == 0])) < 1e-9 * scale
+    finally:
+        s.close()
+
+
+SMALL_CONFIGS = [
+    (0, dict()),                              # C1 full (lmdif, 90 params)
+    (1, dict(frames=12, scale=0.05)),         # C2 subset (pose + focal per frame)
+    (2, dict(frames=8, scale=0.002)),         # C3 subset (10 cams, Schur)
+    (3, dict(frames=8, scale=0.001)),         # C4 subset (Schur BA)
+    (4, dict(frames=8, scale=0.05)),          # C5 subset (3DE classic lens)
+]
+
+
+@pytest.mark.parametrize("idx,kw", SMALL_CONFIGS)
+def test_config_parity(idx, kw, oracle, gpu_ctx):
+    prob = S.make_config(idx, **kw)
+    opt = S.config_options(prob)
+    check_solve(prob, opt, oracle, gpu_ctx)
