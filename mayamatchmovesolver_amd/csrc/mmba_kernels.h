@@ -39,6 +39,19 @@ void launch_trsv_fwd(hipStream_t s, const double *S, const int *slot, int NT, in
                      const int *rows, int nrows, const double *Linv, double *r, double *y);
 void launch_trsv_bwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
                      const int *cols, int ncols, const double *Linv, double *y, double *x);
+void launch_trsv_fwd_all(hipStream_t s, const double *S, const int *slot, int NT,
+                         const int *rows_off, const int *rows, const double *Linv, double *r,
+                         double *y);
+void launch_trsv_bwd_all(hipStream_t s, const double *S, const int *slot, int NT,
+                         const int *cols_off, const int *cols, const double *Linv, double *y,
+                         double *x);
+void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
+                       const int *dest_off, int ndest, const int2 *pairs, double *S,
+                       const int *slot, int NT);
+void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
+                      const int *row_cf, double *rhs);
+void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                       const double *tb, double *S, const int *slot, int NT, double *rhs);
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                            const double *tb, const double *Lb, const double *xR, double *x);
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);

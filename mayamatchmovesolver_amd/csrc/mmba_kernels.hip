@@ -368,59 +368,77 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
                                                  const int *__restrict__ nloc,
                                                  const double *__restrict__ f,
                                                  double *partial, int chunk) {
-    __shared__ double acc[NGMAX * NGMAX + NGMAX];
+    // One observation per thread (grid-stride over the block's chunk); each
+    // thread scatters its global-parameter Jacobian entries into a dense
+    // register vector, products are reduced wave -> block in a fixed order
+    // (deterministic, no atomics).
+    __shared__ double wsum[4][NGMAX * NGMAX + NGMAX];
     const int nG = P.nG;
-    const int nent = nG * nG + nG;
-    for (int t = threadIdx.x; t < nent; t += blockDim.x) acc[t] = 0.;
-    __syncthreads();
-    const int i0 = blockIdx.x * chunk;
-    const int i1 = min(P.M, i0 + chunk);
+    const int nCF = P.nR - nG;
     const int M = P.M;
-    // thread t handles observations i0 + t, i0 + t + 256, ... and accumulates
-    // into LDS with per-entry ownership by (t % nent) rounds to stay deterministic:
-    // each observation's contributions are applied by one thread serially.
-    for (int t = 0; t < nent; ++t) {
-        // serialised over entries: entry t owned by thread (t % blockDim.x)
-        if ((int)threadIdx.x != (t % (int)blockDim.x)) continue;
-        const int ga = t < nG * nG ? t / nG : t - nG * nG;
-        const int gb = t < nG * nG ? t % nG : -1;
-        const int pa = P.g_param[ga];
-        const int pbp = gb >= 0 ? P.g_param[gb] : -1;
-        double s = 0.;
-        for (int i = i0; i < i1; ++i) {
-            const int nl = nloc[i];
-            int la = -1, lb = -1;
-            for (int l = 0; l < nl; ++l) {
-                const int p = jcol[(size_t)l * M + i];
-                if (p == pa) la = l;
-                if (p == pbp) lb = l;
-            }
-            if (la < 0) continue;
-            const double ax = J[(size_t)(2 * la) * M + i], ay = J[(size_t)(2 * la + 1) * M + i];
-            if (gb < 0) {
-                s += ax * f[2 * i] + ay * f[2 * i + 1];
-            } else if (lb >= 0) {
-                s += ax * J[(size_t)(2 * lb) * M + i] + ay * J[(size_t)(2 * lb + 1) * M + i];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double accv[NGMAX * NGMAX + NGMAX];
+#pragma unroll
+    for (int e = 0; e < NGMAX * NGMAX + NGMAX; ++e) accv[e] = 0.;
+    const int i0 = blockIdx.x * chunk;
+    const int i1 = min(M, i0 + chunk);
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += blockDim.x) {
+        double gx[NGMAX], gy[NGMAX];
+#pragma unroll
+        for (int q = 0; q < NGMAX; ++q) gx[q] = gy[q] = 0.;
+        const int nl = nloc[i];
+        for (int l = 0; l < nl; ++l) {
+            const int p = jcol[(size_t)l * M + i];
+            if (P.p_class[p] != PC_G) continue;
+            const int gi = P.p_pos[p] - nCF;
+            const double jx = J[(size_t)(2 * l) * M + i], jy = J[(size_t)(2 * l + 1) * M + i];
+#pragma unroll
+            for (int q = 0; q < NGMAX; ++q) {
+                gx[q] = (gi == q) ? jx : gx[q];
+                gy[q] = (gi == q) ? jy : gy[q];
             }
         }
-        acc[t] = s;
+        const double fx = f[2 * i], fy = f[2 * i + 1];
+#pragma unroll
+        for (int a = 0; a < NGMAX; ++a) {
+            if (a >= nG) break;
+#pragma unroll
+            for (int b = 0; b < NGMAX; ++b) {
+                if (b >= nG) break;
+                accv[a * NGMAX + b] += gx[a] * gx[b] + gy[a] * gy[b];
+            }
+            accv[NGMAX * NGMAX + a] += gx[a] * fx + gy[a] * fy;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NGMAX * NGMAX + NGMAX; ++e) {
+        const bool used = (e < NGMAX * NGMAX) ? ((e / NGMAX) < nG && (e % NGMAX) < nG)
+                                               : (e - NGMAX * NGMAX) < nG;
+        if (!used) continue;
+        double v = accv[e];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) wsum[wave][e] = v;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < nent; t += blockDim.x)
-        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = acc[t];
+    for (int e = threadIdx.x; e < NGMAX * NGMAX + NGMAX; e += blockDim.x) {
+        const double v = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
+        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + e] = v;
+    }
 }
 
 __global__ void k_ne_glob_reduce(DevProblem P, const double *__restrict__ partial, int nblk,
                                  double *Agg, double *g) {
     const int nG = P.nG;
-    const int nent = nG * nG + nG;
-    for (int t = threadIdx.x; t < nent; t += blockDim.x) {
+    for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
+        const bool mat = t < NGMAX * NGMAX;
+        if (mat ? ((t / NGMAX) >= nG || (t % NGMAX) >= nG) : (t - NGMAX * NGMAX) >= nG) continue;
         double s = 0.;
         for (int k = 0; k < nblk; ++k) s += partial[(size_t)k * (NGMAX * NGMAX + NGMAX) + t];
-        if (t < nG * nG)
-            Agg[(t / nG) * NGMAX + (t % nG)] = s;
+        if (mat)
+            Agg[t] = s;
         else
-            g[P.g_param[t - nG * nG]] = s;
+            g[P.g_param[t - NGMAX * NGMAX]] = s;
     }
 }
 
@@ -669,180 +687,91 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
     }
 }
 
-// -------------------------------------------------------------------------
-// Tiled Cholesky of S (64x64 tiles, right-looking).
-// -------------------------------------------------------------------------
-constexpr int LDP = TILE + 1;  // padded LDS row (conflict-free column walks)
+// Deterministic Schur accumulation: one wave per destination block
+// (cf_i >= cf_j); pairs of observations sharing a bundle are pre-sorted by
+// destination on the host, so every S entry has a single writer and a fixed
+// summation order (no atomics).
+__global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *__restrict__ W,
+                                                   const int2 *__restrict__ dest,
+                                                   const int *__restrict__ dest_off,
+                                                   const int2 *__restrict__ pairs, double *S,
+                                                   const int *__restrict__ slot, int NT) {
+    const int d = blockIdx.x;
+    const int2 cc = dest[d];
+    const int pci = P.cf_pc[cc.x], pcj = P.cf_pc[cc.y];
+    const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
+    const int M = P.M;
+    const int q0 = dest_off[d], q1 = dest_off[d + 1];
+    for (int e = threadIdx.x; e < pci * pcj; e += 64) {
+        const int a = e / pcj, c = e % pcj;
+        const int R = ri + a, C = rj + c;
+        if (R < C) continue;
+        double acc = 0.;
+        for (int q = q0; q < q1; ++q) {
+            const int2 pr = pairs[q];
+            acc += W[(size_t)(a * 3) * M + pr.x] * W[(size_t)(c * 3) * M + pr.y] +
+                   W[(size_t)(a * 3 + 1) * M + pr.x] * W[(size_t)(c * 3 + 1) * M + pr.y] +
+                   W[(size_t)(a * 3 + 2) * M + pr.x] * W[(size_t)(c * 3 + 2) * M + pr.y];
+        }
+        *s_at(S, slot, NT, R, C) -= acc;
+    }
+}
 
-// Factor a diagonal tile in LDS; returns false on a non-positive pivot.
-__device__ bool lds_potrf(double (*A)[LDP], int *bad) {
-    for (int j = 0; j < TILE; ++j) {
-        if (threadIdx.x == 0) {
-            double d = A[j][j];
-            if (!(d > 0.) || !isfinite(d)) {
-                *bad = 1;
-                d = 1.;
+// rhs_R -= sum_{i in cf} W_i t_b(i): one thread per reduced-system row of a
+// camera-frame block, looping over that block's contiguous observations.
+__global__ void k_schur_rhs(DevProblem P, const double *__restrict__ W,
+                            const double *__restrict__ tb, const int *__restrict__ row_cf,
+                            double *rhs) {
+    const int R = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nCF = P.nR - P.nG;
+    if (R >= nCF) return;
+    const int cf = row_cf[R];
+    const int a = R - P.cf_roff[cf];
+    const int M = P.M;
+    double acc = 0.;
+    for (int i = P.cf_obs_off[cf]; i < P.cf_obs_off[cf + 1]; ++i) {
+        const int b = P.obs_bnd[i];
+        if (P.bnd_pb[b] == 0) continue;
+        acc += W[(size_t)(a * 3) * M + i] * tb[(size_t)b * 3] +
+               W[(size_t)(a * 3 + 1) * M + i] * tb[(size_t)b * 3 + 1] +
+               W[(size_t)(a * 3 + 2) * M + i] * tb[(size_t)b * 3 + 2];
+    }
+    rhs[R] -= acc;
+}
+
+// Global-parameter rows of the Schur complement (atomics; nG is small).
+__global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
+                             const double *__restrict__ Wg, const double *__restrict__ tb,
+                             double *S, const int *__restrict__ slot, int NT, double *rhs) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int pb = P.bnd_pb[b];
+    const int nG = P.nG;
+    if (pb == 0 || nG == 0) return;
+    const int M = P.M;
+    const int nCF = P.nR - nG;
+    const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
+    const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1], t2 = tb[(size_t)b * 3 + 2];
+    for (int q = 0; q < nG; ++q) {
+        const double *wg = &Wg[((size_t)b * NGMAX + q) * 3];
+        atomicAdd(&rhs[nCF + q], -(wg[0] * t0 + wg[1] * t1 + wg[2] * t2));
+        for (int qj = q0; qj < q1; ++qj) {
+            const int j = P.bobs[qj];
+            const int cfj = P.obs_cf[j];
+            const int pcj = P.cf_pc[cfj];
+            const int rj = P.cf_roff[cfj];
+            for (int c = 0; c < pcj; ++c) {
+                const double v = wg[0] * W[(size_t)(c * 3) * M + j] +
+                                 wg[1] * W[(size_t)(c * 3 + 1) * M + j] +
+                                 wg[2] * W[(size_t)(c * 3 + 2) * M + j];
+                atomicAdd(s_at(S, slot, NT, nCF + q, rj + c), -v);
             }
-            A[j][j] = sqrt(d);
         }
-        __syncthreads();
-        const double piv = A[j][j];
-        for (int r = j + 1 + threadIdx.x; r < TILE; r += blockDim.x) A[r][j] /= piv;
-        __syncthreads();
-        const int m = TILE - j - 1;
-        for (int t = threadIdx.x; t < m * m; t += blockDim.x) {
-            const int r = j + 1 + t / m, c = j + 1 + t % m;
-            if (c <= r) A[r][c] -= A[r][j] * A[c][j];
+        for (int q2 = 0; q2 <= q; ++q2) {
+            const double *wh = &Wg[((size_t)b * NGMAX + q2) * 3];
+            atomicAdd(s_at(S, slot, NT, nCF + q, nCF + q2),
+                      -(wg[0] * wh[0] + wg[1] * wh[1] + wg[2] * wh[2]));
         }
-        __syncthreads();
-    }
-    return *bad == 0;
-}
-
-// Linv = L^-1 (lower), one column per thread.
-__device__ void lds_trtri(double (*L)[LDP], double (*Li)[LDP]) {
-    for (int c = threadIdx.x; c < TILE; c += blockDim.x) {
-        for (int r = 0; r < TILE; ++r) Li[r][c] = 0.;
-        for (int r = c; r < TILE; ++r) {
-            double s = (r == c) ? 1. : 0.;
-            for (int k = c; k < r; ++k) s -= L[r][k] * Li[k][c];
-            Li[r][c] = s / L[r][r];
-        }
-    }
-    __syncthreads();
-}
-
-// Panel k: block 0 factors the diagonal tile and stores L_kk and Linv_kk;
-// block j>0 factors it redundantly and solves L_Ik = S_Ik L_kk^-T.
-__global__ void __launch_bounds__(256) k_chol_panel(double *S, const int *__restrict__ slot,
-                                                    int NT, int k,
-                                                    const int *__restrict__ rows,
-                                                    double *Linv, int *fail) {
-    __shared__ double A[TILE][LDP];
-    __shared__ double Li[TILE][LDP];
-    __shared__ int bad;
-    if (threadIdx.x == 0) bad = 0;
-    const double *D = &S[(size_t)slot[k * NT + k] * TILE * TILE];
-    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) A[t / TILE][t % TILE] = D[t];
-    __syncthreads();
-    lds_potrf(A, &bad);
-    __syncthreads();
-    if (threadIdx.x == 0 && bad && blockIdx.x == 0) atomicOr(fail, 1);
-    lds_trtri(A, Li);
-    if (blockIdx.x == 0) {
-        double *Dw = &S[(size_t)slot[k * NT + k] * TILE * TILE];
-        for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) {
-            const int r = t / TILE, c = t % TILE;
-            Dw[t] = (c <= r) ? A[r][c] : 0.;
-            Linv[(size_t)k * TILE * TILE + t] = Li[r][c];
-        }
-        return;
-    }
-    const int I = rows[blockIdx.x - 1];
-    double *B = &S[(size_t)slot[I * NT + k] * TILE * TILE];
-    // reuse A as the row tile
-    __syncthreads();
-    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) A[t / TILE][t % TILE] = B[t];
-    __syncthreads();
-    // X = B * Linv^T : X[r][c] = sum_{t<=c} B[r][t] * Linv[c][t]
-    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) {
-        const int r = t / TILE, c = t % TILE;
-        double s = 0.;
-        for (int q = 0; q <= c; ++q) s += A[r][q] * Li[c][q];
-        B[t] = s;
-    }
-}
-
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-
-// Trailing update S_IJ -= L_Ik L_Jk^T for the listed (I, J) pairs of panel k,
-// fp64 MFMA 16x16x4: 4 waves, each owns a 16x64 row strip (4 MFMA tiles).
-__global__ void __launch_bounds__(256) k_chol_update(double *S, const int *__restrict__ slot,
-                                                     int NT, int k,
-                                                     const int2 *__restrict__ pairs) {
-    __shared__ double A[TILE][LDP];
-    __shared__ double B[TILE][LDP];
-    const int2 pr = pairs[blockIdx.x];
-    const int I = pr.x, Jt = pr.y;
-    const double *Lik = &S[(size_t)slot[I * NT + k] * TILE * TILE];
-    const double *Ljk = &S[(size_t)slot[Jt * NT + k] * TILE * TILE];
-    for (int t = threadIdx.x; t < TILE * TILE; t += blockDim.x) {
-        A[t / TILE][t % TILE] = Lik[t];
-        B[t / TILE][t % TILE] = Ljk[t];
-    }
-    __syncthreads();
-    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-    const int li = lane & 15, lk = lane >> 4;
-    dbl4 acc[4];
-    for (int tj = 0; tj < 4; ++tj) acc[tj] = (dbl4){0., 0., 0., 0.};
-    const int ti = wave;
-    for (int ks = 0; ks < TILE / 4; ++ks) {
-        const double a = A[ti * 16 + li][ks * 4 + lk];
-#pragma unroll
-        for (int tj = 0; tj < 4; ++tj) {
-            const double bv = B[tj * 16 + li][ks * 4 + lk];
-            acc[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[tj], 0, 0, 0);
-        }
-    }
-    double *C = &S[(size_t)slot[I * NT + Jt] * TILE * TILE];
-#pragma unroll
-    for (int tj = 0; tj < 4; ++tj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = ti * 16 + lk + 4 * r;
-            const int col = tj * 16 + li;
-            C[row * TILE + col] -= acc[tj][r];
-        }
-}
-
-// Forward substitution L y = r, panel k: y_k = Linv_kk r_k, r_I -= L_Ik y_k.
-__global__ void k_trsv_fwd(const double *__restrict__ S, const int *__restrict__ slot, int NT,
-                           int k, const int *__restrict__ rows, const double *__restrict__ Linv,
-                           double *r, double *y) {
-    __shared__ double yk[TILE];
-    const double *Li = &Linv[(size_t)k * TILE * TILE];
-    for (int row = threadIdx.x; row < TILE; row += blockDim.x) {
-        double s = 0.;
-        for (int t = 0; t <= row; ++t) s += Li[row * TILE + t] * r[k * TILE + t];
-        yk[row] = s;
-    }
-    __syncthreads();
-    if (blockIdx.x == 0) {
-        for (int row = threadIdx.x; row < TILE; row += blockDim.x) y[k * TILE + row] = yk[row];
-        return;
-    }
-    const int I = rows[blockIdx.x - 1];
-    const double *L = &S[(size_t)slot[I * NT + k] * TILE * TILE];
-    for (int row = threadIdx.x; row < TILE; row += blockDim.x) {
-        double s = 0.;
-        for (int c = 0; c < TILE; ++c) s += L[row * TILE + c] * yk[c];
-        r[I * TILE + row] -= s;
-    }
-}
-
-// Back substitution L^T x = y, panel k (descending): x_k = Linv_kk^T y_k,
-// y_J -= L_kJ^T x_k for every J < k with L_kJ structurally non-zero.
-__global__ void k_trsv_bwd(const double *__restrict__ S, const int *__restrict__ slot, int NT,
-                           int k, const int *__restrict__ cols, const double *__restrict__ Linv,
-                           double *y, double *x) {
-    __shared__ double xk[TILE];
-    const double *Li = &Linv[(size_t)k * TILE * TILE];
-    for (int row = threadIdx.x; row < TILE; row += blockDim.x) {
-        double s = 0.;
-        for (int t = row; t < TILE; ++t) s += Li[t * TILE + row] * y[k * TILE + t];
-        xk[row] = s;
-    }
-    __syncthreads();
-    if (blockIdx.x == 0) {
-        for (int row = threadIdx.x; row < TILE; row += blockDim.x) x[k * TILE + row] = xk[row];
-        return;
-    }
-    const int Jt = cols[blockIdx.x - 1];
-    const double *L = &S[(size_t)slot[k * NT + Jt] * TILE * TILE];
-    for (int c = threadIdx.x; c < TILE; c += blockDim.x) {
-        double s = 0.;
-        for (int rr = 0; rr < TILE; ++rr) s += L[rr * TILE + c] * xk[rr];
-        y[Jt * TILE + c] -= s;
     }
 }
 
@@ -1172,22 +1101,20 @@ void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, con
     if (P.nB == 0) return;
     k_schur_pairs<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, S, slot, NT, rhs);
 }
-void launch_chol_panel(hipStream_t s, double *S, const int *slot, int NT, int k, const int *rows,
-                       int nrows, double *Linv, int *fail) {
-    k_chol_panel<<<1 + nrows, 256, 0, s>>>(S, slot, NT, k, rows, Linv, fail);
+void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
+                       const int *dest_off, int ndest, const int2 *pairs, double *S,
+                       const int *slot, int NT) {
+    if (ndest > 0) k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, S, slot, NT);
 }
-void launch_chol_update(hipStream_t s, double *S, const int *slot, int NT, int k,
-                        const int2 *pairs, int npairs) {
-    if (npairs == 0) return;
-    k_chol_update<<<npairs, 256, 0, s>>>(S, slot, NT, k, pairs);
+void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
+                      const int *row_cf, double *rhs) {
+    const int nCF = P.nR - P.nG;
+    if (nCF > 0) k_schur_rhs<<<nblk(nCF, 128), 128, 0, s>>>(P, W, tb, row_cf, rhs);
 }
-void launch_trsv_fwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
-                     const int *rows, int nrows, const double *Linv, double *r, double *y) {
-    k_trsv_fwd<<<1 + nrows, 64, 0, s>>>(S, slot, NT, k, rows, Linv, r, y);
-}
-void launch_trsv_bwd(hipStream_t s, const double *S, const int *slot, int NT, int k,
-                     const int *cols, int ncols, const double *Linv, double *y, double *x) {
-    k_trsv_bwd<<<1 + ncols, 64, 0, s>>>(S, slot, NT, k, cols, Linv, y, x);
+void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                       const double *tb, double *S, const int *slot, int NT, double *rhs) {
+    if (P.nG > 0 && P.nB > 0)
+        k_schur_glob<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, S, slot, NT, rhs);
 }
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                            const double *tb, const double *Lb, const double *xR, double *x) {

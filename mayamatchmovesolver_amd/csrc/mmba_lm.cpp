@@ -97,7 +97,15 @@ bool Plan::solve_damped(double lam) {
     if (nR > 0) {
         MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, d_S, d_slot, NT, d_rhs);
-        if (nB_solved > 0) launch_schur_pairs(s, P, d_W, d_Wg, d_tb, d_S, d_slot, NT, d_rhs);
+        if (nB_solved > 0) {
+            if (use_dest) {
+                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, d_S, d_slot, NT);
+                launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
+                launch_schur_glob(s, P, d_W, d_Wg, d_tb, d_S, d_slot, NT, d_rhs);
+            } else {
+                launch_schur_pairs(s, P, d_W, d_Wg, d_tb, d_S, d_slot, NT, d_rhs);
+            }
+        }
         if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
         for (int k = 0; k < NT; ++k) {
             const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
@@ -113,13 +121,18 @@ bool Plan::solve_damped(double lam) {
             chol_ms += ms;
             chol_n++;
         }
-        for (int k = 0; k < NT; ++k) {
-            const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
-            launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_rhs, d_yR);
-        }
-        for (int k = NT - 1; k >= 0; --k) {
-            const int c0 = panel_cols_off[k], nc = panel_cols_off[k + 1] - c0;
-            launch_trsv_bwd(s, d_S, d_slot, NT, k, d_cols + c0, nc, d_Linv, d_yR, d_xR);
+        if (narrow) {
+            launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_rhs, d_yR);
+            launch_trsv_bwd_all(s, d_S, d_slot, NT, d_cols_off, d_cols, d_Linv, d_yR, d_xR);
+        } else {
+            for (int k = 0; k < NT; ++k) {
+                const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
+                launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_rhs, d_yR);
+            }
+            for (int k = NT - 1; k >= 0; --k) {
+                const int c0 = panel_cols_off[k], nc = panel_cols_off[k + 1] - c0;
+                launch_trsv_bwd(s, d_S, d_slot, NT, k, d_cols + c0, nc, d_Linv, d_yR, d_xR);
+            }
         }
         launch_scatter_xR(s, P, d_xR, d_xs);
     }
@@ -143,9 +156,13 @@ double Plan::newton_term(double dxnorm) {
         acc += read_scalar(2);
     }
     if (nR > 0) {
-        for (int k = 0; k < NT; ++k) {
-            const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
-            launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
+        if (narrow) {
+            launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_wR, d_yR);
+        } else {
+            for (int k = 0; k < NT; ++k) {
+                const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
+                launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
+            }
         }
         launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + 3);
         acc += read_scalar(3);

@@ -373,6 +373,65 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int J = 0; J <= I; ++J)
             if (nz[(size_t)I * NT + J]) slot[(size_t)I * NT + J] = nslots++;
 
+    // ---- Schur accumulation plan: observation pairs sharing a bundle, sorted
+    // by destination block (cf_i >= cf_j) ----
+    std::vector<int> row_cf(nCF > 0 ? nCF : 1, 0);
+    for (int cf = 0; cf < ncf; ++cf)
+        for (int a = 0; a < cf_pc[cf]; ++a) row_cf[cf_roff[cf] + a] = cf;
+    std::vector<int2> dest_h, dpairs_h;
+    std::vector<int> dest_off_h;
+    {
+        long long npairs = 0;
+        for (int b = 0; b < nB; ++b)
+            if (bnd_pb[b] > 0) {
+                const long long kb = bobs_off[b + 1] - bobs_off[b];
+                npairs += kb * kb;
+            }
+        use_dest = nB_solved > 0 && nR > 0 && npairs <= (32ll << 20);
+        if (use_dest) {
+            struct PairRec {
+                int cfi, cfj, i, j;
+            };
+            std::vector<PairRec> recs;
+            recs.reserve((size_t)npairs / 2 + 16);
+            for (int b = 0; b < nB; ++b) {
+                if (bnd_pb[b] == 0) continue;
+                for (int qi = bobs_off[b]; qi < bobs_off[b + 1]; ++qi) {
+                    const int i = bobs[qi], cfi = d_cf[i];
+                    if (cf_pc[cfi] == 0) continue;
+                    for (int qj = bobs_off[b]; qj < bobs_off[b + 1]; ++qj) {
+                        const int j = bobs[qj], cfj = d_cf[j];
+                        if (cf_pc[cfj] == 0 || cfi < cfj) continue;
+                        recs.push_back({cfi, cfj, i, j});
+                    }
+                }
+            }
+            std::sort(recs.begin(), recs.end(), [](const PairRec &x, const PairRec &y) {
+                if (x.cfi != y.cfi) return x.cfi < y.cfi;
+                if (x.cfj != y.cfj) return x.cfj < y.cfj;
+                if (x.i != y.i) return x.i < y.i;
+                return x.j < y.j;
+            });
+            for (size_t q = 0; q < recs.size(); ++q) {
+                if (q == 0 || recs[q].cfi != recs[q - 1].cfi || recs[q].cfj != recs[q - 1].cfj) {
+                    dest_h.push_back(make_int2(recs[q].cfi, recs[q].cfj));
+                    dest_off_h.push_back((int)q);
+                }
+                dpairs_h.push_back(make_int2(recs[q].i, recs[q].j));
+            }
+            dest_off_h.push_back((int)recs.size());
+            ndest = (int)dest_h.size();
+        }
+    }
+    {
+        int widest = 0;
+        for (int k = 0; k < NT; ++k) {
+            widest = std::max(widest, panel_rows_off[k + 1] - panel_rows_off[k]);
+            widest = std::max(widest, panel_cols_off[k + 1] - panel_cols_off[k]);
+        }
+        narrow = NT > 0 && widest <= 8;
+    }
+
     // ---- device upload ----
     size_t nvals = 0;
     for (int a = 0; a < nA; ++a)
@@ -452,6 +511,14 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_rows = upload(panel_rows);
     d_cols = upload(panel_cols);
     d_pairs = upload(pairs);
+    d_rows_off = upload(panel_rows_off);
+    d_cols_off = upload(panel_cols_off);
+    d_row_cf = upload(row_cf);
+    if (use_dest) {
+        d_dest = upload(dest_h);
+        d_dest_off = upload(dest_off_h);
+        d_dpairs = upload(dpairs_h);
+    }
     d_S = dalloc<double>((size_t)nslots * TILE * TILE);
     d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
 

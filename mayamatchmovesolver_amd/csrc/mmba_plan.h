@@ -63,6 +63,14 @@ struct Plan {
     double *d_S = nullptr, *d_Linv = nullptr;
     int *d_rows = nullptr, *d_cols = nullptr;
     int2 *d_pairs = nullptr;
+    // deterministic Schur accumulation (destination-sorted observation pairs)
+    bool use_dest = false;
+    int ndest = 0;
+    int2 *d_dest = nullptr, *d_dpairs = nullptr;
+    int *d_dest_off = nullptr, *d_row_cf = nullptr;
+    // single-workgroup triangular solves for narrow (banded) structures
+    bool narrow = false;
+    int *d_rows_off = nullptr, *d_cols_off = nullptr;
     int *d_var_cf = nullptr, *d_stale = nullptr, *d_ref_of_dev = nullptr;
     double *d_attr0 = nullptr;
     size_t attr_bytes = 0;
