@@ -30,6 +30,28 @@ constexpr int LMAX = 20;    // local Jacobian columns per observation
 constexpr int TILE = 64;    // reduced-system tile edge
 constexpr int CAMREC = 20;  // doubles per camera-frame record
 
+// Band + arrow layout of the reduced system (narrow structures): rows of
+// camera-frame parameters keep w+1 entries each (columns r-w .. r), the
+// global parameters are dense arrow rows.
+constexpr int BNB = 16;          // column block of the band factorisation
+constexpr int WBAND_MAX = 80;    // widest half bandwidth (BWR >= 3*BNB + w: the window
+                                 // also holds the rows entering and leaving)
+constexpr int BWR = 128;         // LDS window rows (>= BNB + WBAND_MAX, power of 2)
+
+// Where entry (R, C), R >= C, of the reduced system lives.
+struct SView {
+    int band;  // 0: 64x64 tiles, 1: band + arrow
+    // tiles
+    double *S;
+    const int *slot;
+    int NT;
+    // band + arrow
+    double *Bd;  // [nb][w+1]
+    int w, nb;   // half bandwidth, band rows (= camera-frame parameters)
+    double *Ga;  // [nG][nb]
+    double *Gd;  // [NGMAX][NGMAX] lower
+};
+
 // Parameter classes.
 enum ParamClass : int { PC_CF = 0, PC_B = 1, PC_G = 2 };
 
@@ -65,5 +87,15 @@ struct DevProblem {
     const double *p_min, *p_max, *p_off, *p_scale;
     const int *g_param;  // global index -> param id
 };
+
+__device__ __forceinline__ double *s_at(const SView &V, int R, int C) {
+    if (!V.band) {
+        const int s = V.slot[(R / TILE) * V.NT + (C / TILE)];
+        return &V.S[(size_t)s * TILE * TILE + (R % TILE) * TILE + (C % TILE)];
+    }
+    if (R < V.nb) return &V.Bd[(size_t)R * (V.w + 1) + (C - R + V.w)];
+    if (C < V.nb) return &V.Ga[(size_t)(R - V.nb) * V.nb + C];
+    return &V.Gd[(R - V.nb) * NGMAX + (C - V.nb)];
+}
 
 }  // namespace mmba

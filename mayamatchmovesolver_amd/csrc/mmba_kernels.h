@@ -28,9 +28,9 @@ void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const
                       double *W);
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
-                       double *S, const int *slot, int NT, double *rhs);
+                       const SView &V, int npad, double *rhs);
 void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                        const double *tb, double *S, const int *slot, int NT, double *rhs);
+                        const double *tb, const SView &V, double *rhs);
 void launch_chol_panel(hipStream_t s, double *S, const int *slot, int NT, int k, const int *rows,
                        int nrows, double *Linv, int *fail);
 void launch_chol_update(hipStream_t s, double *S, const int *slot, int NT, int k,
@@ -46,18 +46,26 @@ void launch_trsv_bwd_all(hipStream_t s, const double *S, const int *slot, int NT
                          const int *cols_off, const int *cols, const double *Linv, double *y,
                          double *x);
 void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
-                       const int *dest_off, int ndest, const int2 *pairs, double *S,
-                       const int *slot, int NT);
+                       const int *dest_off, int ndest, const int2 *pairs, const SView &V);
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs);
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                       const double *tb, double *S, const int *slot, int NT, double *rhs);
+                       const double *tb, const SView &V, double *rhs);
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                            const double *tb, const double *Lb, const double *xR, double *x);
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                           const double *Lb, const double *v, double *wR, double *usq);
 void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double *vR, int nRpad);
+// Band + arrow reduced system (mmba_band.hip).
+// nbk: column block of the factorisation (8 or 16); the solves must use the
+// same value (Dinv holds nbk x nbk blocks).
+void launch_band_potrf(hipStream_t s, const SView &V, int nG, double *Dinv, double *Gdinv,
+                       int *fail, long long *probe, int nbk);
+void launch_band_fwd(hipStream_t s, const SView &V, int nG, const double *Dinv,
+                     const double *Gdinv, const double *r, double *y, int nbk);
+void launch_band_bwd(hipStream_t s, const SView &V, int nG, const double *Dinv,
+                     const double *Gdinv, const double *y, double *x, int nbk);
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
                   int nparts, double *out);
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,

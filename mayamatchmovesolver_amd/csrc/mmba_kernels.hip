@@ -567,19 +567,12 @@ __global__ void k_schur_obs(DevProblem P, const double *__restrict__ J,
     }
 }
 
-__device__ __forceinline__ double *s_at(double *S, const int *__restrict__ slot, int NT, int R,
-                                        int C) {
-    const int s = slot[(R / TILE) * NT + (C / TILE)];
-    return &S[(size_t)s * TILE * TILE + (R % TILE) * TILE + (C % TILE)];
-}
-
 // S = (Acc + lam D^2 | Acg | Agg + lam D^2), lower triangle, plus identity
 // on the padded tail; rhs = g_R.
 __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
                              const double *__restrict__ Acg, const double *__restrict__ Agg,
                              const double *__restrict__ g, const double *__restrict__ diag,
-                             double lam, double *S, const int *__restrict__ slot, int NT,
-                             double *rhs) {
+                             double lam, const SView V, int npad, double *rhs) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int nG = P.nG;
     const int nCF = P.nR - nG;
@@ -597,13 +590,13 @@ __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
                     v += lam * (d * d);
                     if (v == 0.) v = 1.;
                 }
-                *s_at(S, slot, NT, r0 + a, r0 + c) = v;
+                *s_at(V, r0 + a, r0 + c) = v;
             }
             rhs[r0 + a] = (Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + a] == 0. && lam == 0.)
                               ? 0.
                               : g[pa];
             for (int q = 0; q < nG; ++q)
-                *s_at(S, slot, NT, nCF + q, r0 + a) = Acg[((size_t)cf * PCMAX + a) * NGMAX + q];
+                *s_at(V, nCF + q, r0 + a) = Acg[((size_t)cf * PCMAX + a) * NGMAX + q];
         }
     } else if (t < P.ncf + nG) {
         const int q = t - P.ncf;
@@ -615,13 +608,13 @@ __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
                 v += lam * (d * d);
                 if (v == 0.) v = 1.;
             }
-            *s_at(S, slot, NT, nCF + q, nCF + c) = v;
+            *s_at(V, nCF + q, nCF + c) = v;
         }
         rhs[nCF + q] = (Agg[q * NGMAX + q] == 0. && lam == 0.) ? 0. : g[p];
     } else {
         const int r = P.nR + (t - P.ncf - nG);
-        if (r < NT * TILE) {
-            *s_at(S, slot, NT, r, r) = 1.;
+        if (r < P.nR + npad) {
+            *s_at(V, r, r) = 1.;
             rhs[r] = 0.;
         }
     }
@@ -630,7 +623,7 @@ __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
 // Schur complement over bundles: S -= sum_b W_b W_b^T, rhs -= W_b tb.
 __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
                               const double *__restrict__ Wg, const double *__restrict__ tb,
-                              double *S, const int *__restrict__ slot, int NT, double *rhs) {
+                              const SView V, double *rhs) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
@@ -659,7 +652,7 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
                     const double v = wa0 * W[(size_t)(c * 3) * M + j] +
                                      wa1 * W[(size_t)(c * 3 + 1) * M + j] +
                                      wa2 * W[(size_t)(c * 3 + 2) * M + j];
-                    atomicAdd(s_at(S, slot, NT, R, C), -v);
+                    atomicAdd(s_at(V, R, C), -v);
                 }
             }
         }
@@ -676,12 +669,12 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
                 const double v = wg[0] * W[(size_t)(c * 3) * M + j] +
                                  wg[1] * W[(size_t)(c * 3 + 1) * M + j] +
                                  wg[2] * W[(size_t)(c * 3 + 2) * M + j];
-                atomicAdd(s_at(S, slot, NT, nCF + q, rj + c), -v);
+                atomicAdd(s_at(V, nCF + q, rj + c), -v);
             }
         }
         for (int q2 = 0; q2 <= q; ++q2) {
             const double *wh = &Wg[((size_t)b * NGMAX + q2) * 3];
-            atomicAdd(s_at(S, slot, NT, nCF + q, nCF + q2),
+            atomicAdd(s_at(V, nCF + q, nCF + q2),
                       -(wg[0] * wh[0] + wg[1] * wh[1] + wg[2] * wh[2]));
         }
     }
@@ -694,8 +687,8 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
 __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *__restrict__ W,
                                                    const int2 *__restrict__ dest,
                                                    const int *__restrict__ dest_off,
-                                                   const int2 *__restrict__ pairs, double *S,
-                                                   const int *__restrict__ slot, int NT) {
+                                                   const int2 *__restrict__ pairs,
+                                                   const SView V) {
     const int d = blockIdx.x;
     const int2 cc = dest[d];
     const int pci = P.cf_pc[cc.x], pcj = P.cf_pc[cc.y];
@@ -713,36 +706,47 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
                    W[(size_t)(a * 3 + 1) * M + pr.x] * W[(size_t)(c * 3 + 1) * M + pr.y] +
                    W[(size_t)(a * 3 + 2) * M + pr.x] * W[(size_t)(c * 3 + 2) * M + pr.y];
         }
-        *s_at(S, slot, NT, R, C) -= acc;
+        *s_at(V, R, C) -= acc;
     }
 }
 
-// rhs_R -= sum_{i in cf} W_i t_b(i): one thread per reduced-system row of a
-// camera-frame block, looping over that block's contiguous observations.
-__global__ void k_schur_rhs(DevProblem P, const double *__restrict__ W,
-                            const double *__restrict__ tb, const int *__restrict__ row_cf,
-                            double *rhs) {
-    const int R = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nCF = P.nR - P.nG;
-    if (R >= nCF) return;
-    const int cf = row_cf[R];
-    const int a = R - P.cf_roff[cf];
+// rhs_R -= sum_{i in cf} W_i t_b(i): one wave per camera-frame, lanes stride
+// over the cf's contiguous observations (coalesced W reads), fixed-order wave
+// reduction per row.
+__global__ void __launch_bounds__(64) k_schur_rhs(DevProblem P, const double *__restrict__ W,
+                                                  const double *__restrict__ tb, double *rhs) {
+    const int cf = blockIdx.x;
+    const int pc = P.cf_pc[cf];
+    if (pc == 0) return;
+    const int r0 = P.cf_roff[cf];
     const int M = P.M;
-    double acc = 0.;
-    for (int i = P.cf_obs_off[cf]; i < P.cf_obs_off[cf + 1]; ++i) {
+    double acc[PCMAX];
+#pragma unroll
+    for (int a = 0; a < PCMAX; ++a) acc[a] = 0.;
+    for (int i = P.cf_obs_off[cf] + (int)threadIdx.x; i < P.cf_obs_off[cf + 1]; i += 64) {
         const int b = P.obs_bnd[i];
         if (P.bnd_pb[b] == 0) continue;
-        acc += W[(size_t)(a * 3) * M + i] * tb[(size_t)b * 3] +
-               W[(size_t)(a * 3 + 1) * M + i] * tb[(size_t)b * 3 + 1] +
-               W[(size_t)(a * 3 + 2) * M + i] * tb[(size_t)b * 3 + 2];
+        const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1], t2 = tb[(size_t)b * 3 + 2];
+#pragma unroll
+        for (int a = 0; a < PCMAX; ++a)
+            if (a < pc)
+                acc[a] += W[(size_t)(a * 3) * M + i] * t0 + W[(size_t)(a * 3 + 1) * M + i] * t1 +
+                          W[(size_t)(a * 3 + 2) * M + i] * t2;
     }
-    rhs[R] -= acc;
+#pragma unroll
+    for (int a = 0; a < PCMAX; ++a) {
+        if (a >= pc) break;
+        double v = acc[a];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (threadIdx.x == 0) rhs[r0 + a] -= v;
+    }
 }
 
 // Global-parameter rows of the Schur complement (atomics; nG is small).
 __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
                              const double *__restrict__ Wg, const double *__restrict__ tb,
-                             double *S, const int *__restrict__ slot, int NT, double *rhs) {
+                             const SView V, double *rhs) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
@@ -764,12 +768,12 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
                 const double v = wg[0] * W[(size_t)(c * 3) * M + j] +
                                  wg[1] * W[(size_t)(c * 3 + 1) * M + j] +
                                  wg[2] * W[(size_t)(c * 3 + 2) * M + j];
-                atomicAdd(s_at(S, slot, NT, nCF + q, rj + c), -v);
+                atomicAdd(s_at(V, nCF + q, rj + c), -v);
             }
         }
         for (int q2 = 0; q2 <= q; ++q2) {
             const double *wh = &Wg[((size_t)b * NGMAX + q2) * 3];
-            atomicAdd(s_at(S, slot, NT, nCF + q, nCF + q2),
+            atomicAdd(s_at(V, nCF + q, nCF + q2),
                       -(wg[0] * wh[0] + wg[1] * wh[1] + wg[2] * wh[2]));
         }
     }
@@ -1092,29 +1096,28 @@ void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const
 }
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
-                       double *S, const int *slot, int NT, double *rhs) {
-    const int n = P.ncf + P.nG + (NT * TILE - P.nR);
-    k_schur_init<<<nblk(n, 64), 64, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, S, slot, NT, rhs);
+                       const SView &V, int npad, double *rhs) {
+    const int n = P.ncf + P.nG + npad;
+    k_schur_init<<<nblk(n, 64), 64, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs);
 }
 void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                        const double *tb, double *S, const int *slot, int NT, double *rhs) {
+                        const double *tb, const SView &V, double *rhs) {
     if (P.nB == 0) return;
-    k_schur_pairs<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, S, slot, NT, rhs);
+    k_schur_pairs<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, V, rhs);
 }
 void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
-                       const int *dest_off, int ndest, const int2 *pairs, double *S,
-                       const int *slot, int NT) {
-    if (ndest > 0) k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, S, slot, NT);
+                       const int *dest_off, int ndest, const int2 *pairs, const SView &V) {
+    if (ndest > 0) k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
 }
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs) {
-    const int nCF = P.nR - P.nG;
-    if (nCF > 0) k_schur_rhs<<<nblk(nCF, 128), 128, 0, s>>>(P, W, tb, row_cf, rhs);
+    (void)row_cf;
+    if (P.ncf > 0) k_schur_rhs<<<P.ncf, 64, 0, s>>>(P, W, tb, rhs);
 }
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                       const double *tb, double *S, const int *slot, int NT, double *rhs) {
+                       const double *tb, const SView &V, double *rhs) {
     if (P.nG > 0 && P.nB > 0)
-        k_schur_glob<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, S, slot, NT, rhs);
+        k_schur_glob<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, V, rhs);
 }
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                            const double *tb, const double *Lb, const double *xR, double *x) {

@@ -95,23 +95,35 @@ bool Plan::solve_damped(double lam) {
         launch_schur_obs(s, P, d_J, d_Lb, d_W);
     }
     if (nR > 0) {
-        MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
-        launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, d_S, d_slot, NT, d_rhs);
+        const SView V = sview();
+        if (band) {
+            const int nb = nR - nG;
+            MMBA_HIP(hipMemsetAsync(d_Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
+            if (nG > 0) MMBA_HIP(hipMemsetAsync(d_Ga, 0, sizeof(double) * (size_t)nG * nb, s));
+            MMBA_HIP(hipMemsetAsync(d_Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
+        } else {
+            MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
+        }
+        launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
         if (nB_solved > 0) {
             if (use_dest) {
-                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, d_S, d_slot, NT);
+                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V);
                 launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
-                launch_schur_glob(s, P, d_W, d_Wg, d_tb, d_S, d_slot, NT, d_rhs);
+                launch_schur_glob(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
-                launch_schur_pairs(s, P, d_W, d_Wg, d_tb, d_S, d_slot, NT, d_rhs);
+                launch_schur_pairs(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             }
         }
         if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
-        for (int k = 0; k < NT; ++k) {
-            const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
-            launch_chol_panel(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_fail);
-            const int q0 = panel_pairs_off[k], nq = panel_pairs_off[k + 1] - q0;
-            launch_chol_update(s, d_S, d_slot, NT, k, d_pairs + q0, nq);
+        if (band) {
+            launch_band_potrf(s, V, nG, d_Dinv, d_Gdinv, d_fail, d_probe, band_nb);
+        } else {
+            for (int k = 0; k < NT; ++k) {
+                const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
+                launch_chol_panel(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_fail);
+                const int q0 = panel_pairs_off[k], nq = panel_pairs_off[k + 1] - q0;
+                launch_chol_update(s, d_S, d_slot, NT, k, d_pairs + q0, nq);
+            }
         }
         if (timing) {
             MMBA_HIP(hipEventRecord(ev_b, s));
@@ -121,7 +133,10 @@ bool Plan::solve_damped(double lam) {
             chol_ms += ms;
             chol_n++;
         }
-        if (narrow) {
+        if (band) {
+            launch_band_fwd(s, V, nG, d_Dinv, d_Gdinv, d_rhs, d_yR, band_nb);
+            launch_band_bwd(s, V, nG, d_Dinv, d_Gdinv, d_yR, d_xR, band_nb);
+        } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_rhs, d_yR);
             launch_trsv_bwd_all(s, d_S, d_slot, NT, d_cols_off, d_cols, d_Linv, d_yR, d_xR);
         } else {
@@ -156,7 +171,9 @@ double Plan::newton_term(double dxnorm) {
         acc += read_scalar(2);
     }
     if (nR > 0) {
-        if (narrow) {
+        if (band) {
+            launch_band_fwd(s, sview(), nG, d_Dinv, d_Gdinv, d_wR, d_yR, band_nb);
+        } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_wR, d_yR);
         } else {
             for (int k = 0; k < NT; ++k) {

@@ -12,6 +12,8 @@
 //       transforms shared by several bundles/cameras) -> dense arrow rows
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -23,6 +25,14 @@
 namespace mmba {
 
 Plan::~Plan() {
+    if (d_probe) {
+        long long h[4] = {0, 0, 0, 0};
+        if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+            std::fprintf(stderr,
+                         "[mmba probe] band potrf cycles: diag+move %lld panel %lld update %lld "
+                         "tail %lld (nb=%d w=%d nG=%d, factorisations=%d)\n",
+                         h[0], h[1], h[2], h[3], nR - nG, bw, nG, chol_n);
+    }
     if (ev_a) (void)hipEventDestroy(ev_a);
     if (ev_b) (void)hipEventDestroy(ev_b);
     for (void *p : allocs) (void)hipFree(p);
@@ -133,11 +143,14 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             if (a >= 0) attr_bnds[a].push_back(b);
     }
 
-    // ---- camera-frame keys: every (camera, frame) with observations ----
+    // ---- camera-frame keys: every (camera, frame) with observations, keyed
+    // (frame, camera) so camera-frames are numbered frame-major: a bundle tracked
+    // over a window of frames then couples a contiguous band of the reduced
+    // system, for any number of cameras ----
     std::vector<int> obs_cam(M);
     for (int i = 0; i < M; ++i) obs_cam[i] = pr->mkr_cam[pr->obs_marker[i]];
     std::map<std::pair<int, int>, int> cf_id;
-    for (int i = 0; i < M; ++i) cf_id[{obs_cam[i], pr->obs_frame[i]}] = 0;
+    for (int i = 0; i < M; ++i) cf_id[{pr->obs_frame[i], obs_cam[i]}] = 0;
 
     // ---- classify parameters ----
     std::vector<int> p_class(n), p_blk(n, -1), p_pos(n, -1), p_both(n, 0);
@@ -152,8 +165,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         p_both[p] = (!cams.empty() && !bnds.empty()) ? 1 : 0;
         if (lc.empty() && bnds.empty() && cams.size() == 1 && fp >= 0) {
             p_class[p] = PC_CF;
-            p_cfkey[p] = {cams[0], fp};
-            cf_id[{cams[0], fp}] = 0;
+            p_cfkey[p] = {fp, cams[0]};
+            cf_id[{fp, cams[0]}] = 0;
         } else if (lc.empty() && cams.empty() && bnds.size() == 1 && fp < 0) {
             p_class[p] = PC_B;
             p_blk[p] = bnds[0];
@@ -166,8 +179,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     std::vector<int> cf_cam, cf_frame;
     for (auto &kv : cf_id) {
         kv.second = ncf++;
-        cf_cam.push_back(kv.first.first);
-        cf_frame.push_back(kv.first.second);
+        cf_frame.push_back(kv.first.first);
+        cf_cam.push_back(kv.first.second);
     }
     // CF blocks
     std::vector<std::vector<int>> cf_params(ncf);
@@ -254,7 +267,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
 
     // ---- observations in device order (by camera-frame) ----
     std::vector<int> obs_cf(M);
-    for (int i = 0; i < M; ++i) obs_cf[i] = cf_id[{obs_cam[i], pr->obs_frame[i]}];
+    for (int i = 0; i < M; ++i) obs_cf[i] = cf_id[{pr->obs_frame[i], obs_cam[i]}];
     ref_of_dev.resize(M);
     std::iota(ref_of_dev.begin(), ref_of_dev.end(), 0);
     std::stable_sort(ref_of_dev.begin(), ref_of_dev.end(),
@@ -305,11 +318,31 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             }
     }
 
+    // ---- reduced-system layout: band + arrow when the camera-frame band is
+    // narrow (every C2/C4/C5-like scene), 64x64 tiles otherwise ----
+    bw = 0;
+    for (int cf = 0; cf < ncf; ++cf)
+        if (cf_pc[cf] > 0) bw = std::max(bw, cf_pc[cf] - 1);
+    for (int b = 0; b < nB; ++b) {
+        if (bnd_pb[b] == 0) continue;
+        int lo = nCF, hi = -1;
+        for (int q = bobs_off[b]; q < bobs_off[b + 1]; ++q) {
+            const int cf = d_cf[bobs[q]];
+            if (cf_pc[cf] == 0) continue;
+            lo = std::min(lo, cf_roff[cf]);
+            hi = std::max(hi, cf_roff[cf] + cf_pc[cf] - 1);
+        }
+        if (hi >= 0) bw = std::max(bw, hi - lo);
+    }
+    band = nR > 0 && bw <= WBAND_MAX;
+    if (const char *e = std::getenv("MMBA_BAND_NB")) band_nb = std::atoi(e) == 16 ? 16 : 8;
+
     // ---- symbolic tile structure of the reduced system ----
-    NT = nR > 0 ? (nR + TILE - 1) / TILE : 0;
-    nRpad = NT * TILE;
+    NT = (nR > 0 && !band) ? (nR + TILE - 1) / TILE : 0;
+    nRpad = band ? nR : NT * TILE;
     std::vector<uint8_t> nz((size_t)NT * NT, 0);
     auto mark = [&](int R, int C) {
+        if (NT == 0) return;
         int I = R / TILE, J = C / TILE;
         if (I < J) std::swap(I, J);
         nz[(size_t)I * NT + J] = 1;
@@ -327,7 +360,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 int I = R / TILE;
                 if (J <= I) nz[(size_t)I * NT + J] = 1;
             }
-    for (int b = 0; b < nB; ++b) {
+    for (int b = 0; b < nB && NT > 0; ++b) {
         if (bnd_pb[b] == 0) continue;
         std::set<int> tiles;
         for (int q = bobs_off[b]; q < bobs_off[b + 1]; ++q) {
@@ -521,6 +554,17 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     d_S = dalloc<double>((size_t)nslots * TILE * TILE);
     d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
+    if (band) {
+        d_Bd = dalloc<double>((size_t)nCF * (bw + 1));
+        d_Ga = dalloc<double>((size_t)nG * nCF);
+        d_Gd = dalloc<double>(NGMAX * NGMAX);
+        d_Dinv = dalloc<double>((size_t)((nCF + BNB - 1) / BNB) * BNB * BNB);
+        d_Gdinv = dalloc<double>(NGMAX * NGMAX);
+        if (std::getenv("MMBA_PROBE")) {
+            d_probe = dalloc<long long>(4);
+            MMBA_HIP(hipMemsetAsync(d_probe, 0, 4 * sizeof(long long), s));
+        }
+    }
 
     d_x = dalloc<double>(n);
     d_ext = dalloc<double>(n);

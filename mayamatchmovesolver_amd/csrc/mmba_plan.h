@@ -68,6 +68,26 @@ struct Plan {
     int ndest = 0;
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
+    // band + arrow layout of the reduced system (mmba_band.hip)
+    bool band = false;
+    int bw = 0;
+    int band_nb = 8;  // column block of the band factorisation (8 or 16)
+    double *d_Bd = nullptr, *d_Ga = nullptr, *d_Gd = nullptr, *d_Dinv = nullptr,
+           *d_Gdinv = nullptr;
+    SView sview() const {
+        SView V{};
+        V.band = band ? 1 : 0;
+        V.S = d_S;
+        V.slot = d_slot;
+        V.NT = NT;
+        V.Bd = d_Bd;
+        V.w = bw;
+        V.nb = nR - nG;
+        V.Ga = d_Ga;
+        V.Gd = d_Gd;
+        return V;
+    }
+    long long *d_probe = nullptr;  // MMBA_PROBE=1: band-kernel phase cycles
     // single-workgroup triangular solves for narrow (banded) structures
     bool narrow = false;
     int *d_rows_off = nullptr, *d_cols_off = nullptr;
