@@ -293,6 +293,16 @@ typedef struct mmba_kernel_stats {
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);
 
+/* Test hook (not part of the solver seam): solve S x = r with the device
+ * band + arrow Cholesky for a dense symmetric positive-definite S of order
+ * nb + nG whose leading nb x nb block has half bandwidth w and whose last nG
+ * rows are dense ("arrow").  P > 0 forces the number of band partitions
+ * (nested dissection on the band rows), P <= 0 uses the solver's heuristic.
+ * S is row-major, only its lower triangle is read.  ynorm2 = ||L^-1 r||^2 (the
+ * quantity lmpar's Newton correction uses); parts_used = partitions run. */
+int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const double *S,
+                          const double *r, double *x, double *ynorm2, int *parts_used);
+
 #ifdef __cplusplus
 }
 #endif

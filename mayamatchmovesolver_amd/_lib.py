@@ -67,6 +67,9 @@ def lib():
                                  C.POINTER(abi.MmbaOptions), dp, dp, dp, dp,
                                  C.POINTER(abi.MmbaResult), C.POINTER(abi.MmbaCallbacks),
                                  C.POINTER(abi.MmbaTrace)]
+        L.mmba_debug_band_solve.restype = C.c_int
+        L.mmba_debug_band_solve.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, dp, dp,
+                                            dp, dp, C.POINTER(C.c_int)]
         L.mmba_plan_kernel_stats.restype = C.c_int
         L.mmba_plan_kernel_stats.argtypes = [C.c_void_p, C.c_int, C.POINTER(abi.MmbaKernelStats)]
         L.mmba_comm_unique_id.restype = C.c_int

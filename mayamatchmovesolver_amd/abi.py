@@ -191,4 +191,5 @@ EXPORTED_SYMBOLS = [
     "mmba_plan_solve",
     "mmba_solve",
     "mmba_plan_kernel_stats",
+    "mmba_debug_band_solve",
 ]

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "mmba_geom.h"
+#include "mmba_kernels.h"
 #include "mmba_plan.h"
 
 namespace mmba {
@@ -19,9 +20,9 @@ void set_error(const std::string &msg) { g_last_error = msg; }
 
 using namespace mmba;
 
-#define MMBA_GUARD(body)                              \
+#define MMBA_GUARD(...)                               \
     try {                                             \
-        body                                          \
+        __VA_ARGS__                                   \
     } catch (const DeviceError &) {                   \
         return MMBA_ERR_DEVICE;                       \
     } catch (const Unsupported &u) {                  \
@@ -205,6 +206,61 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         p.jac_ms = p.resid_ms = p.chol_ms = 0.;
         p.jac_n = p.resid_n = p.chol_n = 0;
     }
+    return MMBA_OK;
+}
+
+int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const double *S,
+                          const double *r, double *x, double *ynorm2, int *parts_used) {
+    if (!ctx || nb < 0 || w < 0 || w > WBAND_MAX || nG < 0 || nG > NGMAX || !S || !r || !x)
+        return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        MMBA_HIP(hipSetDevice(ctx->device));
+        Plan p;
+        p.ctx = ctx;
+        p.s = ctx->stream;
+        p.nG = nG;
+        p.nR = nb + nG;
+        p.bw = w;
+        p.band = true;
+        p.setup_band(P);
+        const int n = nb + nG, W1 = w + 1;
+        std::vector<double> hb((size_t)nb * W1, 0.), ha((size_t)nG * nb), hg(NGMAX * NGMAX, 0.);
+        for (int i = 0; i < nb; ++i)
+            for (int k = 0; k < W1; ++k) {
+                const int c = i - w + k;
+                if (c >= 0) hb[(size_t)i * W1 + k] = S[(size_t)i * n + c];
+            }
+        for (int q = 0; q < nG; ++q) {
+            for (int c = 0; c < nb; ++c) ha[(size_t)q * nb + c] = S[(size_t)(nb + q) * n + c];
+            for (int c = 0; c <= q; ++c) hg[q * NGMAX + c] = S[(size_t)(nb + q) * n + nb + c];
+        }
+        MMBA_HIP(hipMemcpyAsync(p.bs.Bd, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, p.s));
+        if (nG) MMBA_HIP(hipMemcpyAsync(p.bs.Ga, ha.data(), ha.size() * 8, hipMemcpyHostToDevice, p.s));
+        MMBA_HIP(hipMemcpyAsync(p.bs.Gd, hg.data(), hg.size() * 8, hipMemcpyHostToDevice, p.s));
+        double *dr = p.dalloc<double>(n), *dy = p.dalloc<double>(n), *dx = p.dalloc<double>(n);
+        int *dfail = p.dalloc<int>(1);
+        MMBA_HIP(hipMemsetAsync(dfail, 0, sizeof(int), p.s));
+        MMBA_HIP(hipMemcpyAsync(dr, r, (size_t)n * 8, hipMemcpyHostToDevice, p.s));
+        band_factor(p.s, p.bs, dfail, nullptr);
+        band_forward(p.s, p.bs, dr, dy);
+        band_backward(p.s, p.bs, dy, dx);
+        std::vector<double> hy(n);
+        int fail = 0;
+        MMBA_HIP(hipMemcpyAsync(x, dx, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
+        MMBA_HIP(hipMemcpyAsync(hy.data(), dy, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
+        MMBA_HIP(hipMemcpyAsync(&fail, dfail, sizeof(int), hipMemcpyDeviceToHost, p.s));
+        MMBA_HIP(hipStreamSynchronize(p.s));
+        if (ynorm2) {
+            double acc = 0.;
+            for (double v : hy) acc += v * v;
+            *ynorm2 = acc;
+        }
+        if (parts_used) *parts_used = p.bs.P;
+        if (fail) {
+            set_error("band factorisation: non-positive pivot");
+            return MMBA_ERR_INVALID;
+        }
+    });
     return MMBA_OK;
 }
 

@@ -5,24 +5,33 @@
 //   S = [ B   Gᵀ ]   B: nb x nb banded (half bandwidth w: a bundle couples the
 //       [ G   D  ]      camera-frames of the frames it is tracked in),
 //                    G: nG x nb dense arrow rows (lens, static camera attrs),
-// factors as L = [Lb 0; Ga Ld] with no fill outside the band and the arrow.
-// The factorisation is a chain: column j needs every update of columns < j,
-// so it runs as ONE workgroup that walks 16-column blocks through an LDS
-// window of BWR band rows (right-looking):
-//   A. wave 0 factors and inverts the 16x16 diagonal block in registers
-//      (lane = row, v_readlane broadcasts); meanwhile waves 1-3 move the rows
-//      the next block needs into the window and the finished rows out,
-//   B. the <= w panel rows below and the arrow rows: P = P Dinv^T,
-//   C. trailing update of the w x w window and the arrow (rank 16).
-// One launch replaces the ~2 NT launches of the tiled path; every LDS access
-// after the initial load is on-chip.  The solves use the stored block
-// inverses so each 16-row block costs two short reductions.
+// factors with no fill outside the band and the arrow.  A band factorisation
+// is a chain (column j needs every update of columns < j), so the rows are
+// split into P partitions (nested dissection on the frame axis):
+//
+//   partition p = interior rows I_p | separator rows S_p (its last w rows)
+//   I_p couples only to S_{p-1}, S_p and G, never to another interior.
+//
+// Stage 1 (one workgroup per partition, concurrently): factor B[I_p, I_p];
+// the separator and global rows that touch I_p are the partition's "arrow"
+// A_p (<= 2w + nG rows), reduced to Y_p = A_p L_p^-T, and Z_p = Y_p Y_p^T is
+// the partition's Schur term.  Stage 2: the separator system
+// T = S[seps + G] - sum_p Z_p (band 2w-1 + arrow) is assembled and factored
+// by the same kernel with P = 1 ("corner" mode: the global rows are factored
+// at the end).  With P = 1 stage 1 alone is the whole factorisation.
+//
+// Inside one workgroup the band rows stream through an LDS window of WR rows
+// in NB-column blocks (right-looking):
+//   A. wave 0 factors and inverts the NB x NB diagonal block in registers
+//      (lane = row, v_readlane broadcasts); waves 1-3 move the rows the next
+//      block needs into the window and the finished rows out,
+//   B. panel rows below and arrow rows: P <- P Dinv^T,
+//   C. trailing update of the window, the arrow rows and Z (rank NB).
+// The solves use the stored NB x NB block inverses: two short reductions per
+// block.
 #include "mmba_kernels.h"
 
 namespace mmba {
-
-constexpr int BW1 = WBAND_MAX + 1;
-constexpr int BMASK = BWR - 1;
 
 // Broadcast lane l's double to the whole wave (v_readlane: l is wave-uniform).
 __device__ __forceinline__ double rdlane(double v, int l) {
@@ -41,12 +50,20 @@ __device__ __forceinline__ double rsq_nr(double d) {
     return y;
 }
 
-// Factor a 16x16 SPD block held one row per lane (lane r = row r; lanes
-// 16..63 mirror 0..15) and invert the factor: on return a[c], c <= r, is row
-// r of L and x[] is column r of L^-1 (upper entries of a[] are scratch).
-// Rows >= nd must be identity padding.  Branch-free: every lane runs every
-// update, broadcasts are v_readlane of wave-uniform lanes, 1/L_jj comes from
-// the rsq of the pivot.  Returns non-zero if a pivot was replaced.
+// Row q of a packed lower triangle holding entry e (q(q+1)/2 <= e).
+__device__ __forceinline__ int tri_row(int e) {
+    int q = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
+    if ((q + 1) * (q + 2) / 2 <= e) ++q;
+    if (q * (q + 1) / 2 > e) --q;
+    return q;
+}
+
+// Factor an NB x NB SPD block held one row per lane (lane r = row r; lanes
+// >= NB mirror) and invert the factor: on return a[c], c <= r, is row r of L
+// and x[] is column r of L^-1 (upper entries of a[] are scratch).  Padding
+// rows must be identity.  Branch-free: every lane runs every update,
+// broadcasts are v_readlane of wave-uniform lanes, 1/L_jj is the rsq of the
+// pivot.  Returns non-zero if a pivot was replaced.
 template <int NB>
 __device__ __forceinline__ int potrf_inv(double (&a)[NB], double (&x)[NB]) {
     const int r = threadIdx.x & (NB - 1);
@@ -76,94 +93,110 @@ __device__ __forceinline__ int potrf_inv(double (&a)[NB], double (&x)[NB]) {
     return badl;
 }
 
-template <int NB>
-__global__ void __launch_bounds__(256) k_band_potrf(SView V, int nG, double *Dinv, double *Gdinv,
-                                                    int *fail, long long *probe) {
-    // probe (diagnostic builds of the bench only, MMBA_PROBE=1): thread 0
-    // accumulates s_memtime cycles per phase; never read by the solver.
-    long long pt[4] = {0, 0, 0, 0}, tprev = probe ? (long long)clock64() : 0;
+// ---------------------------------------------------------------------------
+// Stage-1 / corner factorisation, one workgroup per partition.  CORNER: the
+// arrow rows are the nG global rows, Z starts from Gd and is factored at the
+// end into Gd / Gdinv.  Otherwise -Z_p (packed lower, na rows) goes to zpool.
+// ---------------------------------------------------------------------------
+template <int NB, int WR, int WMAX, int NAMAX, bool CORNER>
+__global__ void __launch_bounds__(256)
+    k_band_factor(double *Bd, int w, const BandPart *__restrict__ parts, double *apool,
+                  double *zpool, double *Dinv, double *Gd, double *Gdinv, int *fail,
+                  long long *probe) {
+    constexpr int WM = WR - 1;
+    __shared__ double win[WR][WMAX + 1];
+    __shared__ double gwin[NAMAX][WR];
+    __shared__ double sX[NB][NB + 1];
+    __shared__ double sP[WMAX][NB + 1];
+    __shared__ double sPG[NAMAX][NB + 1];
+    __shared__ double sZ[NAMAX * (NAMAX + 1) / 2];
+    __shared__ int bad;
+    // probe (diagnostic, MMBA_PROBE=1): thread 0 of workgroup 0 accumulates
+    // s_memtime cycles per phase; never read by the solver.
+    const bool prb = probe && blockIdx.x == 0 && threadIdx.x == 0;
+    long long pt[4] = {0, 0, 0, 0}, tprev = prb ? (long long)clock64() : 0;
     auto stamp = [&](int ph) {
-        if (probe && threadIdx.x == 0) {
+        if (prb) {
             const long long t = (long long)clock64();
             pt[ph] += t - tprev;
             tprev = t;
         }
     };
-    __shared__ double win[BWR][BW1];
-    __shared__ double gwin[NGMAX][BWR];
-    __shared__ double sX[NB][NB + 1];
-    __shared__ double sP[WBAND_MAX][NB + 1];
-    __shared__ double sPG[NGMAX][NB + 1];
-    __shared__ double sGd[NGMAX][NGMAX + 1];
-    __shared__ int bad;
+    const BandPart pd = parts[blockIdx.x];
     const int tid = threadIdx.x;
-    const int w = V.w, nb = V.nb, W1 = w + 1;
+    const int r0 = pd.r0, r1 = pd.r1, na = pd.na, W1 = w + 1;
+    const int ast = r1 - r0;
+    const int nz = na * (na + 1) / 2;
+    double *A = apool + pd.aoff;
     if (tid == 0) bad = 0;
-    for (int e = tid; e < NGMAX * NGMAX; e += blockDim.x) {
-        const int q = e / NGMAX, q2 = e % NGMAX;
-        sGd[q][q2] = (q < nG && q2 <= q) ? V.Gd[q * NGMAX + q2] : 0.;
+    for (int e = tid; e < nz; e += blockDim.x) {
+        double v = 0.;
+        if (CORNER) {
+            const int q = tri_row(e);
+            v = Gd[q * NGMAX + (e - q * (q + 1) / 2)];
+        }
+        sZ[e] = v;
     }
-    // rows [r0, r1) enter the window; t0/nt: the participating threads
-    auto load_rows = [&](int r0, int r1, int t0, int nt) {
-        for (int e = t0; e < (r1 - r0) * W1; e += nt) {
-            const int row = r0 + e / W1, k = e % W1;
-            win[row & BMASK][k] = (row - w + k >= 0) ? V.Bd[(size_t)row * W1 + k] : 0.;
+    // rows [a, b) enter the window (band entries left of r0 belong to the
+    // arrow of this partition and are dropped); t0/nt: participating threads
+    auto load_rows = [&](int a, int b, int t0, int nt) {
+        for (int e = t0; e < (b - a) * W1; e += nt) {
+            const int row = a + e / W1, k = e % W1;
+            win[row & WM][k] = (row - w + k >= r0) ? Bd[(size_t)row * W1 + k] : 0.;
         }
-        for (int e = t0; e < nG * (r1 - r0); e += nt) {
-            const int q = e / (r1 - r0), row = r0 + e % (r1 - r0);
-            gwin[q][row & BMASK] = V.Ga[(size_t)q * nb + row];
-        }
-    };
-    // rows [r0, r1) are final: window -> HBM
-    auto store_rows = [&](int r0, int r1, int t0, int nt) {
-        for (int e = t0; e < (r1 - r0) * W1; e += nt) {
-            const int row = r0 + e / W1, k = e % W1;
-            V.Bd[(size_t)row * W1 + k] = win[row & BMASK][k];
-        }
-        for (int e = t0; e < nG * (r1 - r0); e += nt) {
-            const int q = e / (r1 - r0), row = r0 + e % (r1 - r0);
-            V.Ga[(size_t)q * nb + row] = gwin[q][row & BMASK];
+        for (int e = t0; e < na * (b - a); e += nt) {
+            const int q = e / (b - a), row = a + e % (b - a);
+            gwin[q][row & WM] = A[(size_t)q * ast + (row - r0)];
         }
     };
-    int loaded = min(nb, NB + w);
-    load_rows(0, loaded, tid, blockDim.x);
+    auto store_rows = [&](int a, int b, int t0, int nt) {
+        for (int e = t0; e < (b - a) * W1; e += nt) {
+            const int row = a + e / W1, k = e % W1;
+            Bd[(size_t)row * W1 + k] = win[row & WM][k];
+        }
+        for (int e = t0; e < na * (b - a); e += nt) {
+            const int q = e / (b - a), row = a + e % (b - a);
+            A[(size_t)q * ast + (row - r0)] = gwin[q][row & WM];
+        }
+    };
+    int loaded = min(r1, r0 + NB + w);
+    load_rows(r0, loaded, tid, blockDim.x);
     __syncthreads();
-    for (int j0 = 0, b = 0; j0 < nb; j0 += NB, ++b) {
-        const int nd = min(NB, nb - j0);
-        // A. wave 0: diagonal block factor + inverse (the serial chain);
-        //    waves 1-3: rows of the next block enter, the previous block leaves.
+    for (int j0 = r0, b = pd.doff; j0 < r1; j0 += NB, ++b) {
+        const int nd = min(NB, r1 - j0);
+        // A. diagonal block (wave 0) || window traffic (waves 1-3)
         if (tid < 64) {
             const int r = tid & (NB - 1);
             double a[NB], x[NB];
 #pragma unroll
             for (int c = 0; c < NB; ++c) {
                 a[c] = 0.;
-                if (c <= r && r < nd && r - c <= w) a[c] = win[(j0 + r) & BMASK][c - r + w];
+                if (c <= r && r < nd && r - c <= w) a[c] = win[(j0 + r) & WM][c - r + w];
             }
             if (r >= nd) a[r] = 1.;
             const int badl = potrf_inv<NB>(a, x);
             if (tid < NB) {
 #pragma unroll
                 for (int c = 0; c < NB; ++c) {
-                    if (c <= r && r < nd && r - c <= w) win[(j0 + r) & BMASK][c - r + w] = a[c];
+                    if (c <= r && r < nd && r - c <= w) win[(j0 + r) & WM][c - r + w] = a[c];
                     sX[c][r] = x[c];
                 }
             }
             if (tid == 0 && badl) bad = 1;
         } else {
-            const int want = min(nb, j0 + 2 * NB + w);
+            const int want = min(r1, j0 + 2 * NB + w);
             if (want > loaded) load_rows(loaded, want, tid - 64, blockDim.x - 64);
-            if (j0 > 0) store_rows(j0 - NB, j0, tid - 64, blockDim.x - 64);
+            if (j0 > r0) store_rows(j0 - NB, j0, tid - 64, blockDim.x - 64);
         }
-        loaded = max(loaded, min(nb, j0 + 2 * NB + w));
+        loaded = max(loaded, min(r1, j0 + 2 * NB + w));
         __syncthreads();
         stamp(0);
         // B. panel rows [j0+NB, pend) and arrow rows: P <- P Dinv^T
-        const int pend = min(nb, j0 + NB + w);
+        const int pend = min(r1, j0 + NB + w);
         const int npan = max(0, pend - (j0 + NB));
         for (int e = tid; e < npan * NB; e += blockDim.x) {
             const int li = e / NB, c = e % NB, i = j0 + NB + li;
-            const double *wr = &win[i & BMASK][0];
+            const double *wr = &win[i & WM][0];
             double pv[NB];
 #pragma unroll
             for (int t = 0; t < NB; ++t) {
@@ -175,86 +208,87 @@ __global__ void __launch_bounds__(256) k_band_potrf(SView V, int nG, double *Din
             for (int t = 0; t < NB; ++t) s = fma(pv[t], sX[c][t], s);  // sX upper = 0
             sP[li][c] = s;
         }
-        for (int e = tid; e < nG * NB; e += blockDim.x) {
+        for (int e = tid; e < na * NB; e += blockDim.x) {
             const int q = e / NB, c = e % NB;
             double s = 0.;
 #pragma unroll
             for (int t = 0; t < NB; ++t)
-                s = fma((t < nd) ? gwin[q][(j0 + t) & BMASK] : 0., sX[c][t], s);
+                s = fma((t < nd) ? gwin[q][(j0 + t) & WM] : 0., sX[c][t], s);
             sPG[q][c] = s;
         }
         __syncthreads();
         stamp(1);
-        // C. trailing update (rank NB), panel and arrow columns written back
+        // C. trailing update (rank NB), panel / arrow columns written back
         for (int e = tid; e < npan * W1; e += blockDim.x) {
             const int li = e / W1, kk = e % W1;
             const int i = j0 + NB + li, k = i - kk;
             if (k < j0 + NB) continue;
             const int lk = k - j0 - NB;
-            double s = win[i & BMASK][w - kk];
+            double s = win[i & WM][w - kk];
 #pragma unroll
             for (int t = 0; t < NB; ++t) s = fma(-sP[li][t], sP[lk][t], s);
-            win[i & BMASK][w - kk] = s;
+            win[i & WM][w - kk] = s;
         }
         for (int e = tid; e < npan * NB; e += blockDim.x) {
             const int li = e / NB, c = e % NB, i = j0 + NB + li, col = j0 + c;
-            if (i - col <= w) win[i & BMASK][col - i + w] = sP[li][c];
+            if (i - col <= w) win[i & WM][col - i + w] = sP[li][c];
         }
-        for (int e = tid; e < nG * npan; e += blockDim.x) {
+        for (int e = tid; e < na * npan; e += blockDim.x) {
             const int q = e / npan, li = e % npan, i = j0 + NB + li;
-            double s = gwin[q][i & BMASK];
+            double s = gwin[q][i & WM];
 #pragma unroll
             for (int t = 0; t < NB; ++t) s = fma(-sPG[q][t], sP[li][t], s);
-            gwin[q][i & BMASK] = s;
+            gwin[q][i & WM] = s;
         }
-        for (int e = tid; e < nG * nG; e += blockDim.x) {
-            const int q = e / nG, q2 = e % nG;
-            if (q2 > q) continue;
-            double s = sGd[q][q2];
+        for (int e = tid; e < nz; e += blockDim.x) {
+            const int q = tri_row(e), q2 = e - q * (q + 1) / 2;
+            double s = sZ[e];
 #pragma unroll
             for (int t = 0; t < NB; ++t) s = fma(-sPG[q][t], sPG[q2][t], s);
-            sGd[q][q2] = s;
+            sZ[e] = s;
         }
-        for (int e = tid; e < nG * nd; e += blockDim.x) {
+        for (int e = tid; e < na * nd; e += blockDim.x) {
             const int q = e / nd, c = e % nd;
-            gwin[q][(j0 + c) & BMASK] = sPG[q][c];
+            gwin[q][(j0 + c) & WM] = sPG[q][c];
         }
         for (int e = tid; e < NB * NB; e += blockDim.x)
             Dinv[(size_t)b * NB * NB + e] = sX[e / NB][e % NB];
         __syncthreads();
         stamp(2);
     }
-    {
-        const int jl = ((nb - 1) / NB) * NB;
-        if (nb > 0) store_rows(jl, nb, tid, blockDim.x);
+    if (r1 > r0) {
+        const int jl = r0 + ((r1 - r0 - 1) / NB) * NB;
+        store_rows(jl, r1, tid, blockDim.x);
     }
-    // arrow corner: Ld Ld^T = D - Ga Ga^T (already accumulated in sGd)
-    if (nG > 0) {
-        if (tid < 64) {
-            const int r = tid & (BNB - 1);
-            double a[BNB], x[BNB];
+    if (CORNER) {
+        // Ld Ld^T = D - Y Y^T (accumulated in sZ), na = nG <= 16
+        if (na > 0 && tid < 64) {
+            const int r = tid & 15;
+            double a[16], x[16];
 #pragma unroll
-            for (int c = 0; c < BNB; ++c) a[c] = (c <= r && r < nG) ? sGd[r][c] : 0.;
-            if (r >= nG) a[r] = 1.;
-            const int badl = potrf_inv<BNB>(a, x);
-            if (tid < BNB) {
+            for (int c = 0; c < 16; ++c) a[c] = (c <= r && r < na) ? sZ[r * (r + 1) / 2 + c] : 0.;
+            if (r >= na) a[r] = 1.;
+            const int badl = potrf_inv<16>(a, x);
+            if (tid < 16) {
 #pragma unroll
-                for (int c = 0; c < BNB; ++c) {
-                    V.Gd[r * NGMAX + c] = (c <= r) ? a[c] : 0.;
+                for (int c = 0; c < 16; ++c) {
+                    Gd[r * NGMAX + c] = (c <= r) ? a[c] : 0.;
                     Gdinv[c * NGMAX + r] = x[c];
                 }
             }
             if (tid == 0 && badl) bad = 1;
         }
+    } else {
+        for (int e = tid; e < nz; e += blockDim.x) zpool[pd.zoff + e] = sZ[e];
     }
     __syncthreads();
     stamp(3);
     if (tid == 0 && bad) atomicOr(fail, 1);
-    if (probe && tid == 0)
+    if (prb)
         for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long *)&probe[k], (unsigned long long)pt[k]);
 }
 
-// Sum over the 16 lanes of a lane group (rows of a block are 16-lane groups).
+// Sum over the 16 lanes of a lane group.
 __device__ __forceinline__ double sum16(double v) {
     v += __shfl_xor(v, 8, 16);
     v += __shfl_xor(v, 4, 16);
@@ -263,29 +297,39 @@ __device__ __forceinline__ double sum16(double v) {
     return v;
 }
 
-// L y = r.  Thread (i = tid/16, l = tid%16): row i of the current block.
-template <int NB>
-__global__ void __launch_bounds__(256) k_band_fwd(SView V, int nG, const double *__restrict__ Dinv,
-                                                  const double *__restrict__ Gdinv,
-                                                  const double *__restrict__ r, double *y) {
-    __shared__ double ywin[BWR];
+// ---------------------------------------------------------------------------
+// Forward solve of one partition: y_I = L_I^-1 r_I and the arrow sums
+// c_a = sum_c Y[a][c] y_c.  CORNER: y_G = Ld^-1 (r_G - c) into y[nb + q];
+// otherwise c goes to cpool.  Thread (i = tid/16, l = tid%16): row i of the
+// current block.  r and y are in reduced-system order (length nb + nG).
+// ---------------------------------------------------------------------------
+template <int NB, int WR, bool CORNER>
+__global__ void __launch_bounds__(256)
+    k_band_fwd(const double *__restrict__ Bd, int w, int nb, const BandPart *__restrict__ parts,
+               const double *__restrict__ apool, const double *__restrict__ Dinv,
+               const double *__restrict__ Gdinv, double *cpool, const double *__restrict__ r,
+               double *y) {
+    constexpr int WM = WR - 1;
+    __shared__ double ywin[WR];
     __shared__ double t[NB];
-    __shared__ double sumG[NGMAX];
+    __shared__ double csum[2 * WBAND_PART + NGMAX];
     __shared__ double tg[NGMAX];
+    const BandPart pd = parts[blockIdx.x];
     const int tid = threadIdx.x, i = tid >> 4, l = tid & 15;
-    const int w = V.w, nb = V.nb, W1 = w + 1;
-    if (tid < NGMAX) sumG[tid] = 0.;
+    const int r0 = pd.r0, r1 = pd.r1, na = pd.na, W1 = w + 1, ast = r1 - r0;
+    const double *A = apool + pd.aoff;
+    for (int a = tid; a < na; a += blockDim.x) csum[a] = 0.;
     __syncthreads();
-    for (int j0 = 0, b = 0; j0 < nb; j0 += NB, ++b) {
-        const int nd = min(NB, nb - j0);
+    for (int j0 = r0, b = pd.doff; j0 < r1; j0 += NB, ++b) {
+        const int nd = min(NB, r1 - j0);
         const int row = j0 + i;
         double s = 0.;
         if (i < nd) {
-            // columns k in [max(0, row - w), j0): kk = j0 - 1 - k < w - i
+            // columns k in [max(r0, row - w), j0): kk = j0 - 1 - k < w - i
             for (int kk = l; kk < w - i; kk += 16) {
                 const int k = j0 - 1 - kk;
-                if (k < 0) break;
-                s += V.Bd[(size_t)row * W1 + (k - row + w)] * ywin[k & BMASK];
+                if (k < r0) break;
+                s += Bd[(size_t)row * W1 + (k - row + w)] * ywin[k & WM];
             }
         }
         s = sum16(s);
@@ -294,92 +338,288 @@ __global__ void __launch_bounds__(256) k_band_fwd(SView V, int nG, const double 
         double s2 = (i < nd && l <= i) ? Dinv[(size_t)b * NB * NB + i * NB + l] * t[l] : 0.;
         s2 = sum16(s2);
         if (l == 0 && i < nd) {
-            ywin[row & BMASK] = s2;
+            ywin[row & WM] = s2;
             y[row] = s2;
         }
         __syncthreads();
-        if (nG > 0) {
-            // arrow: sumG[q] += sum_c Ga[q][j0+c] y_{j0+c}, q = i, c = l
-            double p = (i < nG && l < nd) ? V.Ga[(size_t)i * nb + j0 + l] * ywin[(j0 + l) & BMASK] : 0.;
+        // arrow sums: lane group i takes arrow rows i, i+16, ...; lane l = column
+        for (int a = i; a < na; a += 16) {
+            double p = (l < nd) ? A[(size_t)a * ast + (j0 - r0 + l)] * ywin[(j0 + l) & WM] : 0.;
             p = sum16(p);
-            if (l == 0 && i < nG) sumG[i] += p;
+            if (l == 0) csum[a] += p;
         }
     }
     __syncthreads();
-    if (nG > 0) {
-        if (tid < nG) tg[tid] = r[nb + tid] - sumG[tid];
+    if (CORNER) {
+        if (tid < na) tg[tid] = r[nb + tid] - csum[tid];
         __syncthreads();
-        if (tid < nG) {
+        if (tid < na) {
             double s = 0.;
             for (int q2 = 0; q2 <= tid; ++q2) s += Gdinv[tid * NGMAX + q2] * tg[q2];
             y[nb + tid] = s;
         }
+    } else {
+        for (int a = tid; a < na; a += blockDim.x) cpool[pd.coff + a] = csum[a];
     }
 }
 
-// L^T x = y.
-template <int NB>
-__global__ void __launch_bounds__(256) k_band_bwd(SView V, int nG, const double *__restrict__ Dinv,
-                                                  const double *__restrict__ Gdinv,
-                                                  const double *__restrict__ y, double *x) {
-    __shared__ double xwin[BWR];
+// ---------------------------------------------------------------------------
+// Backward solve of one partition: x_I = L_I^-T (y_I - Y^T x_A).  CORNER: x_A
+// = x_G = Ld^-T y_G (also written to x[nb + q]); otherwise x_A is read from x
+// at the separator / global positions (filled by the separator solve first).
+// ---------------------------------------------------------------------------
+template <int NB, int WR, bool CORNER>
+__global__ void __launch_bounds__(256)
+    k_band_bwd(const double *__restrict__ Bd, int w, int nb, const BandPart *__restrict__ parts,
+               const double *__restrict__ apool, const double *__restrict__ Dinv,
+               const double *__restrict__ Gdinv, const double *__restrict__ y, double *x) {
+    constexpr int WM = WR - 1;
+    __shared__ double xwin[WR];
     __shared__ double t[NB];
-    __shared__ double xG[NGMAX];
+    __shared__ double xA[2 * WBAND_PART + NGMAX];
+    const BandPart pd = parts[blockIdx.x];
     const int tid = threadIdx.x, i = tid >> 4, l = tid & 15;
-    const int w = V.w, nb = V.nb, W1 = w + 1;
-    if (tid < NGMAX) {
-        double s = 0.;
-        if (tid < nG)
-            for (int q2 = tid; q2 < nG; ++q2) s += Gdinv[q2 * NGMAX + tid] * y[nb + q2];
-        xG[tid] = s;
-        if (tid < nG) x[nb + tid] = s;
+    const int r0 = pd.r0, r1 = pd.r1, na = pd.na, W1 = w + 1, ast = r1 - r0;
+    const double *A = apool + pd.aoff;
+    if (CORNER) {
+        if (tid < na) {
+            double s = 0.;
+            for (int q2 = tid; q2 < na; ++q2) s += Gdinv[q2 * NGMAX + tid] * y[nb + q2];
+            xA[tid] = s;
+            x[nb + tid] = s;
+        }
+    } else {
+        for (int a = tid; a < na; a += blockDim.x) {
+            int src;
+            if (a < pd.nprev)
+                src = pd.sprev + a;
+            else if (a < pd.nprev + pd.nnext)
+                src = pd.snext + (a - pd.nprev);
+            else
+                src = nb + (a - pd.nprev - pd.nnext);
+            xA[a] = x[src];
+        }
     }
     __syncthreads();
-    const int nblkb = (nb + NB - 1) / NB;
-    for (int b = nblkb - 1; b >= 0; --b) {
-        const int j0 = b * NB;
-        const int nd = min(NB, nb - j0);
+    const int nblk = (r1 - r0 + NB - 1) / NB;
+    for (int bb = nblk - 1; bb >= 0; --bb) {
+        const int j0 = r0 + bb * NB, b = pd.doff + bb;
+        const int nd = min(NB, r1 - j0);
         const int col = j0 + i;
         double s = 0.;
         if (i < nd) {
-            // rows k in [j0+NB, min(nb, col+w+1))
-            for (int k = j0 + NB + l; k <= col + w && k < nb; k += 16)
-                s += V.Bd[(size_t)k * W1 + (col - k + w)] * xwin[k & BMASK];
-            if (l < nG) s += V.Ga[(size_t)l * nb + col] * xG[l];
+            for (int k = j0 + NB + l; k <= col + w && k < r1; k += 16)
+                s += Bd[(size_t)k * W1 + (col - k + w)] * xwin[k & WM];
+            for (int a = l; a < na; a += 16) s += A[(size_t)a * ast + (col - r0)] * xA[a];
         }
         s = sum16(s);
         if (l == 0 && i < nd) t[i] = y[col] - s;
         __syncthreads();
-        double s2 = (i < nd && l >= i && l < nd) ? Dinv[(size_t)b * NB * NB + l * NB + i] * t[l] : 0.;
+        double s2 =
+            (i < nd && l >= i && l < nd) ? Dinv[(size_t)b * NB * NB + l * NB + i] * t[l] : 0.;
         s2 = sum16(s2);
         if (l == 0 && i < nd) {
-            xwin[col & BMASK] = s2;
+            xwin[col & WM] = s2;
             x[col] = s2;
         }
         __syncthreads();
     }
 }
 
-void launch_band_potrf(hipStream_t s, const SView &V, int nG, double *Dinv, double *Gdinv,
-                       int *fail, long long *probe, int nbk) {
-    if (nbk == 8)
-        k_band_potrf<8><<<1, 256, 0, s>>>(V, nG, Dinv, Gdinv, fail, probe);
-    else
-        k_band_potrf<16><<<1, 256, 0, s>>>(V, nG, Dinv, Gdinv, fail, probe);
+// ---------------------------------------------------------------------------
+// Partition plumbing (P > 1).
+// ---------------------------------------------------------------------------
+// Arrow rows of every partition from the band / global rows; thread per
+// (arrow row, interior column), blockIdx.y = partition.
+__global__ void k_band_extract(const double *__restrict__ Bd, int w,
+                               const double *__restrict__ Ga, int nb,
+                               const BandPart *__restrict__ parts, int P, double *apool) {
+    const int p = blockIdx.y;
+    if (p >= P) return;
+    const BandPart pd = parts[p];
+    const int ast = pd.r1 - pd.r0;
+    const int W1 = w + 1;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < pd.na * ast;
+         e += gridDim.x * blockDim.x) {
+        const int a = e / ast, c = pd.r0 + e % ast;
+        double v = 0.;
+        if (a < pd.nprev) {
+            const int k = pd.sprev + a;  // k < c: S[c][k] lives in row c
+            if (c - k <= w) v = Bd[(size_t)c * W1 + (k - c + w)];
+        } else if (a < pd.nprev + pd.nnext) {
+            const int k = pd.snext + (a - pd.nprev);  // k > c: S[k][c] in row k
+            if (k - c <= w) v = Bd[(size_t)k * W1 + (c - k + w)];
+        } else {
+            v = Ga[(size_t)(a - pd.nprev - pd.nnext) * nb + c];
+        }
+        apool[pd.aoff + e] = v;
+    }
 }
-void launch_band_fwd(hipStream_t s, const SView &V, int nG, const double *Dinv,
-                     const double *Gdinv, const double *r, double *y, int nbk) {
-    if (nbk == 8)
-        k_band_fwd<8><<<1, 256, 0, s>>>(V, nG, Dinv, Gdinv, r, y);
-    else
-        k_band_fwd<16><<<1, 256, 0, s>>>(V, nG, Dinv, Gdinv, r, y);
+
+// zpool entry (a, b) of partition pd: -Z_p[a][b] (packed lower triangle).
+__device__ __forceinline__ double zget(const double *zp, const BandPart &pd, int a, int b) {
+    if (a < b) {
+        const int t = a;
+        a = b;
+        b = t;
+    }
+    return zp[pd.zoff + a * (a + 1) / 2 + b];
 }
-void launch_band_bwd(hipStream_t s, const SView &V, int nG, const double *Dinv,
-                     const double *Gdinv, const double *y, double *x, int nbk) {
-    if (nbk == 8)
-        k_band_bwd<8><<<1, 256, 0, s>>>(V, nG, Dinv, Gdinv, y, x);
-    else
-        k_band_bwd<16><<<1, 256, 0, s>>>(V, nG, Dinv, Gdinv, y, x);
+
+// Separator system T = S[seps + G] - sum_p Z_p (zpool holds -Z_p, the
+// partitions' Schur updates, so they are added).  Separator s (band rows
+// [parts[s].snext, +w)) -> T rows [s*w, (s+1)*w); half bandwidth wT = 2w-1.
+// Partition p has prev separator p-1 (arrow rows 0..w-1) and next separator
+// p (arrow rows nprev..nprev+w-1).  Thread per T entry, fixed summation order.
+__global__ void k_band_tassemble(const double *__restrict__ Bd, int w,
+                                 const double *__restrict__ Ga, const double *__restrict__ Gd,
+                                 int nb, int nG, const BandPart *__restrict__ parts, int P,
+                                 const double *__restrict__ zpool, double *TBd, double *TGa,
+                                 double *TGd) {
+    const int nsep = P - 1, nbT = nsep * w, wT = 2 * w - 1, W1T = wT + 1, W1 = w + 1;
+    const int nband = nbT * W1T, narrow = nG * nbT, ncorner = NGMAX * NGMAX;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nband) {
+        const int R = e / W1T, k = e % W1T, C = R - wT + k;
+        double v = 0.;
+        if (C >= 0) {
+            const int sR = R / w, uR = R % w, sC = C / w, uC = C % w;
+            const BandPart &pa = parts[sR];
+            const int gR = pa.snext + uR, gC = parts[sC].snext + uC;
+            if (gR - gC <= w) v = Bd[(size_t)gR * W1 + (gC - gR + w)];
+            if (sR == sC) {
+                const BandPart &pb = parts[sR + 1];
+                v += zget(zpool, pa, pa.nprev + uR, pa.nprev + uC);
+                v += zget(zpool, pb, uR, uC);
+            } else if (sR == sC + 1) {  // partition sR: prev = sC, next = sR
+                v += zget(zpool, pa, pa.nprev + uR, uC);
+            }  // sR == sC + 2 lies inside the T band but is structurally zero
+        }
+        TBd[e] = v;
+    } else if (e < nband + narrow) {
+        const int q = (e - nband) / nbT, C = (e - nband) % nbT;
+        const int sC = C / w, uC = C % w;
+        const BandPart &pa = parts[sC], &pb = parts[sC + 1];
+        double v = Ga[(size_t)q * nb + pa.snext + uC];
+        v += zget(zpool, pa, pa.nprev + pa.nnext + q, pa.nprev + uC);
+        v += zget(zpool, pb, pb.nprev + pb.nnext + q, uC);
+        TGa[(size_t)q * nbT + C] = v;
+    } else if (e < nband + narrow + ncorner) {
+        const int q = (e - nband - narrow) / NGMAX, q2 = (e - nband - narrow) % NGMAX;
+        double v = 0.;
+        if (q < nG && q2 <= q) {
+            v = Gd[q * NGMAX + q2];
+            for (int p = 0; p < P; ++p) {
+                const BandPart &pd = parts[p];
+                v += zget(zpool, pd, pd.nprev + pd.nnext + q, pd.nprev + pd.nnext + q2);
+            }
+        }
+        TGd[q * NGMAX + q2] = v;
+    }
+}
+
+// Separator right-hand side: rT = r[seps + G] - sum_p c_p.
+__global__ void k_band_trhs(const double *__restrict__ r, int w, int nb, int nG,
+                            const BandPart *__restrict__ parts, int P,
+                            const double *__restrict__ cpool, double *rT) {
+    const int nbT = (P - 1) * w;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nbT) {
+        const int s = e / w, u = e % w;
+        const BandPart &pa = parts[s], &pb = parts[s + 1];
+        rT[e] = r[pa.snext + u] - cpool[pa.coff + pa.nprev + u] - cpool[pb.coff + u];
+    } else if (e < nbT + nG) {
+        const int q = e - nbT;
+        double v = r[nb + q];
+        for (int p = 0; p < P; ++p)
+            v -= cpool[parts[p].coff + parts[p].nprev + parts[p].nnext + q];
+        rT[e] = v;
+    }
+}
+
+// T-order vector -> reduced-system order (separator rows and globals).
+__global__ void k_band_tscatter(const double *__restrict__ vT, int w, int nb, int nG,
+                                const BandPart *__restrict__ parts, int P, double *v) {
+    const int nbT = (P - 1) * w;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nbT)
+        v[parts[e / w].snext + e % w] = vT[e];
+    else if (e < nbT + nG)
+        v[nb + (e - nbT)] = vT[e];
+}
+
+// ---------------------------------------------------------------------------
+// Host side.
+// ---------------------------------------------------------------------------
+static inline int nblk_(long n, int bs) { return (int)((n + bs - 1) / bs); }
+
+void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe) {
+    if (B.P == 1) {
+        if (B.w <= WBAND_PART)
+            k_band_factor<8, 64, WBAND_PART, NGMAX, true><<<1, 256, 0, s>>>(
+                B.Bd, B.w, B.d_parts, B.Ga, nullptr, B.Dinv, B.Gd, B.Gdinv, fail, probe);
+        else
+            k_band_factor<8, 128, WBAND_MAX, NGMAX, true><<<1, 256, 0, s>>>(
+                B.Bd, B.w, B.d_parts, B.Ga, nullptr, B.Dinv, B.Gd, B.Gdinv, fail, probe);
+        return;
+    }
+    const int nbT = (B.P - 1) * B.w;
+    {
+        dim3 grid(nblk_(B.max_arrow, 256), B.P);
+        k_band_extract<<<grid, 256, 0, s>>>(B.Bd, B.w, B.Ga, B.nb, B.d_parts, B.P, B.apool);
+    }
+    k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGMAX, false><<<B.P, 256, 0, s>>>(
+        B.Bd, B.w, B.d_parts, B.apool, B.zpool, B.Dinv, nullptr, nullptr, fail, probe);
+    {
+        const int n = nbT * (2 * B.w) + B.nG * nbT + NGMAX * NGMAX;
+        k_band_tassemble<<<nblk_(n, 256), 256, 0, s>>>(B.Bd, B.w, B.Ga, B.Gd, B.nb, B.nG,
+                                                       B.d_parts, B.P, B.zpool, B.TBd, B.TGa,
+                                                       B.TGd);
+    }
+    k_band_factor<8, 128, WBAND_MAX, NGMAX, true><<<1, 256, 0, s>>>(
+        B.TBd, 2 * B.w - 1, B.d_tpart, B.TGa, nullptr, B.TDinv, B.TGd, B.TGdinv, fail, nullptr);
+}
+
+void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y) {
+    if (B.P == 1) {
+        if (B.w <= WBAND_PART)
+            k_band_fwd<8, 64, true><<<1, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.Ga, B.Dinv,
+                                                       B.Gdinv, nullptr, r, y);
+        else
+            k_band_fwd<8, 128, true><<<1, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.Ga, B.Dinv,
+                                                        B.Gdinv, nullptr, r, y);
+        return;
+    }
+    const int nbT = (B.P - 1) * B.w;
+    k_band_fwd<8, 64, false><<<B.P, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.apool, B.Dinv,
+                                                  nullptr, B.cpool, r, y);
+    k_band_trhs<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(r, B.w, B.nb, B.nG, B.d_parts, B.P,
+                                                       B.cpool, B.rT);
+    k_band_fwd<8, 128, true><<<1, 256, 0, s>>>(B.TBd, 2 * B.w - 1, nbT, B.d_tpart, B.TGa,
+                                                B.TDinv, B.TGdinv, nullptr, B.rT, B.yT);
+    k_band_tscatter<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(B.yT, B.w, B.nb, B.nG, B.d_parts,
+                                                           B.P, y);
+}
+
+void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *x) {
+    if (B.P == 1) {
+        if (B.w <= WBAND_PART)
+            k_band_bwd<8, 64, true><<<1, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.Ga, B.Dinv,
+                                                       B.Gdinv, y, x);
+        else
+            k_band_bwd<8, 128, true><<<1, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.Ga, B.Dinv,
+                                                        B.Gdinv, y, x);
+        return;
+    }
+    const int nbT = (B.P - 1) * B.w;
+    // the separator system first (its right-hand side is the yT band_forward
+    // left for this y), then every partition
+    k_band_bwd<8, 128, true><<<1, 256, 0, s>>>(B.TBd, 2 * B.w - 1, nbT, B.d_tpart, B.TGa,
+                                                B.TDinv, B.TGdinv, B.yT, B.xT);
+    k_band_tscatter<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(B.xT, B.w, B.nb, B.nG, B.d_parts,
+                                                           B.P, x);
+    k_band_bwd<8, 64, false><<<B.P, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.apool, B.Dinv,
+                                                  nullptr, y, x);
 }
 
 }  // namespace mmba

@@ -32,11 +32,34 @@ constexpr int CAMREC = 20;  // doubles per camera-frame record
 
 // Band + arrow layout of the reduced system (narrow structures): rows of
 // camera-frame parameters keep w+1 entries each (columns r-w .. r), the
-// global parameters are dense arrow rows.
-constexpr int BNB = 16;          // column block of the band factorisation
-constexpr int WBAND_MAX = 80;    // widest half bandwidth (BWR >= 3*BNB + w: the window
-                                 // also holds the rows entering and leaving)
-constexpr int BWR = 128;         // LDS window rows (>= BNB + WBAND_MAX, power of 2)
+// global parameters are dense arrow rows (mmba_band.hip).
+constexpr int WBAND_MAX = 80;    // widest half bandwidth of the band layout
+constexpr int WBAND_PART = 40;   // widest half bandwidth that is partitioned
+
+// One partition of the band rows: interior rows [r0, r1) plus its arrow
+// (previous separator rows, next separator rows, global rows).
+struct BandPart {
+    int r0, r1;
+    int na, nprev, nnext;  // arrow rows: nprev + nnext + nG
+    int sprev, snext;      // first band row of the prev / next separator (-1: none)
+    int zoff;              // packed lower Z_p (na rows) in zpool
+    int doff;              // first NB x NB block inverse
+    int coff;              // solve partial sums in cpool
+    long long aoff;        // arrow rows: apool[aoff + a*(r1-r0) + (c-r0)]
+};
+
+// Device buffers of the (partitioned) band factorisation.
+struct BandSolver {
+    int P = 1, w = 0, nb = 0, nG = 0;
+    long long max_arrow = 0;                 // max na*(r1-r0) over partitions
+    double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr, *Gdinv = nullptr, *Dinv = nullptr;
+    BandPart *d_parts = nullptr;             // P partitions (P == 1: arrow = Ga)
+    double *apool = nullptr, *zpool = nullptr, *cpool = nullptr;
+    // separator system (P > 1)
+    double *TBd = nullptr, *TGa = nullptr, *TGd = nullptr, *TGdinv = nullptr, *TDinv = nullptr;
+    BandPart *d_tpart = nullptr;
+    double *rT = nullptr, *yT = nullptr, *xT = nullptr;
+};
 
 // Where entry (R, C), R >= C, of the reduced system lives.
 struct SView {

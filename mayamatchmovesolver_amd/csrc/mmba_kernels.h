@@ -57,15 +57,12 @@ void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, dou
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                           const double *Lb, const double *v, double *wR, double *usq);
 void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double *vR, int nRpad);
-// Band + arrow reduced system (mmba_band.hip).
-// nbk: column block of the factorisation (8 or 16); the solves must use the
-// same value (Dinv holds nbk x nbk blocks).
-void launch_band_potrf(hipStream_t s, const SView &V, int nG, double *Dinv, double *Gdinv,
-                       int *fail, long long *probe, int nbk);
-void launch_band_fwd(hipStream_t s, const SView &V, int nG, const double *Dinv,
-                     const double *Gdinv, const double *r, double *y, int nbk);
-void launch_band_bwd(hipStream_t s, const SView &V, int nG, const double *Dinv,
-                     const double *Gdinv, const double *y, double *x, int nbk);
+// Band + arrow reduced system (mmba_band.hip): factorisation in place, then
+// L y = r (band_forward; keeps the separator part of y for band_backward) and
+// L^T x = y.  r, y, x are in reduced-system order (length nb + nG).
+void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe);
+void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
+void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
                   int nparts, double *out);
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,

@@ -98,9 +98,9 @@ bool Plan::solve_damped(double lam) {
         const SView V = sview();
         if (band) {
             const int nb = nR - nG;
-            MMBA_HIP(hipMemsetAsync(d_Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
-            if (nG > 0) MMBA_HIP(hipMemsetAsync(d_Ga, 0, sizeof(double) * (size_t)nG * nb, s));
-            MMBA_HIP(hipMemsetAsync(d_Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
+            MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
+            if (nG > 0) MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * (size_t)nG * nb, s));
+            MMBA_HIP(hipMemsetAsync(bs.Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
         } else {
             MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         }
@@ -116,7 +116,7 @@ bool Plan::solve_damped(double lam) {
         }
         if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
         if (band) {
-            launch_band_potrf(s, V, nG, d_Dinv, d_Gdinv, d_fail, d_probe, band_nb);
+            band_factor(s, bs, d_fail, d_probe);
         } else {
             for (int k = 0; k < NT; ++k) {
                 const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
@@ -134,8 +134,8 @@ bool Plan::solve_damped(double lam) {
             chol_n++;
         }
         if (band) {
-            launch_band_fwd(s, V, nG, d_Dinv, d_Gdinv, d_rhs, d_yR, band_nb);
-            launch_band_bwd(s, V, nG, d_Dinv, d_Gdinv, d_yR, d_xR, band_nb);
+            band_forward(s, bs, d_rhs, d_yR);
+            band_backward(s, bs, d_yR, d_xR);
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_rhs, d_yR);
             launch_trsv_bwd_all(s, d_S, d_slot, NT, d_cols_off, d_cols, d_Linv, d_yR, d_xR);
@@ -172,7 +172,7 @@ double Plan::newton_term(double dxnorm) {
     }
     if (nR > 0) {
         if (band) {
-            launch_band_fwd(s, sview(), nG, d_Dinv, d_Gdinv, d_wR, d_yR, band_nb);
+            band_forward(s, bs, d_wR, d_yR);
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_wR, d_yR);
         } else {

@@ -29,9 +29,9 @@ Plan::~Plan() {
         long long h[4] = {0, 0, 0, 0};
         if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
             std::fprintf(stderr,
-                         "[mmba probe] band potrf cycles: diag+move %lld panel %lld update %lld "
-                         "tail %lld (nb=%d w=%d nG=%d, factorisations=%d)\n",
-                         h[0], h[1], h[2], h[3], nR - nG, bw, nG, chol_n);
+                         "[mmba probe] band factor cycles (partition 0): diag+move %lld panel %lld "
+                         "update %lld tail %lld (nb=%d w=%d nG=%d P=%d)\n",
+                         h[0], h[1], h[2], h[3], nR - nG, bw, nG, bs.P);
     }
     if (ev_a) (void)hipEventDestroy(ev_a);
     if (ev_b) (void)hipEventDestroy(ev_b);
@@ -335,7 +335,6 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         if (hi >= 0) bw = std::max(bw, hi - lo);
     }
     band = nR > 0 && bw <= WBAND_MAX;
-    if (const char *e = std::getenv("MMBA_BAND_NB")) band_nb = std::atoi(e) == 16 ? 16 : 8;
 
     // ---- symbolic tile structure of the reduced system ----
     NT = (nR > 0 && !band) ? (nR + TILE - 1) / TILE : 0;
@@ -554,16 +553,10 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     d_S = dalloc<double>((size_t)nslots * TILE * TILE);
     d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
-    if (band) {
-        d_Bd = dalloc<double>((size_t)nCF * (bw + 1));
-        d_Ga = dalloc<double>((size_t)nG * nCF);
-        d_Gd = dalloc<double>(NGMAX * NGMAX);
-        d_Dinv = dalloc<double>((size_t)((nCF + BNB - 1) / BNB) * BNB * BNB);
-        d_Gdinv = dalloc<double>(NGMAX * NGMAX);
-        if (std::getenv("MMBA_PROBE")) {
-            d_probe = dalloc<long long>(4);
-            MMBA_HIP(hipMemsetAsync(d_probe, 0, 4 * sizeof(long long), s));
-        }
+    if (band) setup_band();
+    if (band && std::getenv("MMBA_PROBE")) {
+        d_probe = dalloc<long long>(4);
+        MMBA_HIP(hipMemsetAsync(d_probe, 0, 4 * sizeof(long long), s));
     }
 
     d_x = dalloc<double>(n);
@@ -614,6 +607,77 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipEventCreate(&ev_a));
     MMBA_HIP(hipEventCreate(&ev_b));
     MMBA_HIP(hipStreamSynchronize(s));
+}
+
+// Partitions of the band rows (nested dissection along the frame axis, see
+// mmba_band.hip) and the device buffers of the band factorisation.
+void Plan::setup_band(int Pforce) {
+    const int nb = nR - nG, w = bw;
+    int P = 1;
+    if (Pforce > 0 && w <= WBAND_PART) {
+        P = std::max(1, std::min(Pforce, nb / (w + 1)));
+    } else if (w > 0 && w <= WBAND_PART) {
+        // balance the interior chains (nb/P rows) against the separator chain
+        // ((P-1) w rows at bandwidth 2w-1); measured on C4 (nb 2994, w 23):
+        // P = 1/4/8/12/16/24 -> 1.20/0.70/0.44/0.40/0.41/0.48 ms per factorisation
+        P = (int)std::lround(std::sqrt((double)nb / w));
+        if (const char *e = std::getenv("MMBA_BAND_PARTS")) P = std::atoi(e);
+        P = std::max(1, std::min(P, nb / (2 * w + 8)));
+    }
+    std::vector<BandPart> parts(P);
+    long long aoff = 0;
+    int zoff = 0, doff = 0, coff = 0;
+    bs.max_arrow = 0;
+    for (int p = 0; p < P; ++p) {
+        BandPart &q = parts[p];
+        const int s0 = (int)((long long)p * nb / P), s1 = (int)((long long)(p + 1) * nb / P);
+        q.r0 = s0;
+        q.r1 = (p < P - 1) ? s1 - w : nb;
+        q.nprev = p > 0 ? w : 0;
+        q.nnext = p < P - 1 ? w : 0;
+        q.sprev = p > 0 ? s0 - w : -1;
+        q.snext = p < P - 1 ? s1 - w : -1;
+        q.na = q.nprev + q.nnext + nG;
+        q.aoff = P > 1 ? aoff : 0;
+        q.zoff = zoff;
+        q.doff = doff;
+        q.coff = coff;
+        aoff += (long long)q.na * (q.r1 - q.r0);
+        bs.max_arrow = std::max(bs.max_arrow, (long long)q.na * (q.r1 - q.r0));
+        zoff += q.na * (q.na + 1) / 2;
+        doff += (q.r1 - q.r0 + 7) / 8;
+        coff += q.na;
+    }
+    bs.P = P;
+    bs.w = w;
+    bs.nb = nb;
+    bs.nG = nG;
+    bs.Bd = dalloc<double>((size_t)nb * (w + 1));
+    bs.Ga = dalloc<double>((size_t)nG * nb);
+    bs.Gd = dalloc<double>(NGMAX * NGMAX);
+    bs.Gdinv = dalloc<double>(NGMAX * NGMAX);
+    bs.Dinv = dalloc<double>((size_t)doff * 64);
+    bs.d_parts = upload(parts);
+    if (P > 1) {
+        bs.apool = dalloc<double>((size_t)aoff);
+        bs.zpool = dalloc<double>((size_t)zoff);
+        bs.cpool = dalloc<double>((size_t)coff);
+        const int nbT = (P - 1) * w;
+        bs.TBd = dalloc<double>((size_t)nbT * 2 * w);
+        bs.TGa = dalloc<double>((size_t)nG * nbT);
+        bs.TGd = dalloc<double>(NGMAX * NGMAX);
+        bs.TGdinv = dalloc<double>(NGMAX * NGMAX);
+        bs.TDinv = dalloc<double>((size_t)((nbT + 7) / 8) * 64);
+        BandPart t{};
+        t.r0 = 0;
+        t.r1 = nbT;
+        t.na = nG;
+        t.sprev = t.snext = -1;
+        bs.d_tpart = upload(std::vector<BandPart>{t});
+        bs.rT = dalloc<double>(nbT + nG);
+        bs.yT = dalloc<double>(nbT + nG);
+        bs.xT = dalloc<double>(nbT + nG);
+    }
 }
 
 }  // namespace mmba

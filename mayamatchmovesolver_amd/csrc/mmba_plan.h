@@ -71,20 +71,19 @@ struct Plan {
     // band + arrow layout of the reduced system (mmba_band.hip)
     bool band = false;
     int bw = 0;
-    int band_nb = 8;  // column block of the band factorisation (8 or 16)
-    double *d_Bd = nullptr, *d_Ga = nullptr, *d_Gd = nullptr, *d_Dinv = nullptr,
-           *d_Gdinv = nullptr;
+    BandSolver bs;
+    void setup_band(int Pforce = 0);
     SView sview() const {
         SView V{};
         V.band = band ? 1 : 0;
         V.S = d_S;
         V.slot = d_slot;
         V.NT = NT;
-        V.Bd = d_Bd;
+        V.Bd = bs.Bd;
         V.w = bw;
         V.nb = nR - nG;
-        V.Ga = d_Ga;
-        V.Gd = d_Gd;
+        V.Ga = bs.Ga;
+        V.Gd = bs.Gd;
         return V;
     }
     long long *d_probe = nullptr;  // MMBA_PROBE=1: band-kernel phase cycles

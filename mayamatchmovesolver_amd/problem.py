@@ -212,12 +212,22 @@ class Problem:
         return p
 
     def external_params(self, x):
-        """Internal parameter vector -> attribute (external) values."""
-        return np.array([
-            param_internal_to_external(float(v), self.param_min[i], self.param_max[i],
-                                       self.param_offset[i], self.param_scale[i])
-            for i, v in enumerate(np.asarray(x, dtype=np.float64))
-        ])
+        """Internal parameter vector -> attribute (external) values
+        (``parameterBoundFromInternalToExternal`` vectorised over parameters)."""
+        v = np.asarray(x, dtype=np.float64)
+        lo, hi = self.param_min, self.param_max
+        off, sc = self.param_offset, self.param_scale
+        unb = (lo <= -FLOAT_MAX) & (hi >= FLOAT_MAX)
+        up_inf = ~unb & (hi >= FLOAT_MAX)
+        lo_inf = ~unb & ~up_inf & (lo <= -FLOAT_MAX)
+        both = ~unb & ~up_inf & ~lo_inf
+        out = np.where(unb, v, 0.0)
+        r = np.sqrt(v * v + 1.0)
+        out = np.where(up_inf, lo - (1.0 + r), out)
+        out = np.where(lo_inf, hi + (1.0 - r), out)
+        out = np.where(both, lo + ((hi - lo) / 2.0) * (np.sin(v) + 1.0), out)
+        out = out / sc - off
+        return np.minimum(np.maximum(out, lo), hi)
 
 
 class SceneBuilder:

@@ -39,9 +39,12 @@ class SolveResult:
     fnorm_trace: np.ndarray
     kernel_stats: Optional[Dict] = None
 
+    problem: Optional[Problem] = None
+
     @property
     def external(self):
-        return self._external
+        """Attribute values at the solution (what setParameters writes back)."""
+        return self.problem.external_params(self.x)
 
     def result_strings(self) -> List[str]:
         r = self.result
@@ -149,10 +152,8 @@ class Solver:
                                    C.byref(cbs) if cbs is not None else None, C.byref(tr))
         if rc not in (abi.MMBA_OK, abi.MMBA_ERR_INTERRUPTED):
             check(rc)
-        out = SolveResult(x=x, fvec=fvec, err_user=eu, err_dist=ed, result=res.as_dict(),
-                          fnorm_trace=tbuf[:min(tr.count, trace_capacity)].copy())
-        out._external = p.external_params(x)
-        return out
+        return SolveResult(x=x, fvec=fvec, err_user=eu, err_dist=ed, result=res.as_dict(),
+                           fnorm_trace=tbuf[:min(tr.count, trace_capacity)].copy(), problem=p)
 
 
 def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
@@ -166,3 +167,19 @@ def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
 
 def device_count() -> int:
     return int(lib().mmba_device_count())
+
+
+def debug_band_solve(ctx: "Context", S: np.ndarray, nb: int, w: int, nG: int, parts: int = 0):
+    """Test hook: solve S x = r-style systems with the device band + arrow
+    Cholesky (``mmba_debug_band_solve``).  Returns a function r -> (x, ||L^-1 r||^2, P)."""
+    S = np.ascontiguousarray(S, dtype=np.float64)
+
+    def solve(r):
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        x = np.empty_like(r)
+        yn = C.c_double(0.0)
+        pu = C.c_int(0)
+        check(lib().mmba_debug_band_solve(ctx.handle, int(nb), int(w), int(nG), int(parts),
+                                          _dp(S), _dp(r), _dp(x), C.byref(yn), C.byref(pu)))
+        return x, yn.value, pu.value
+    return solve

@@ -89,3 +89,23 @@ def test_bound_transforms(oracle):
                 param_internal_to_external(a, lo, hi, off, sc), rel=1e-15, abs=1e-15)
     # B2: lower-bound-only attributes are clamped to xmin by int->ext
     assert oracle.param_internal_to_external(3.0, -5.0, FLOAT_MAX, 0.0, 1.0) == -5.0
+
+
+def test_vectorised_external_params_match_scalar(oracle):
+    """Problem.external_params (vectorised) == adjust_base.cpp:194-220 per element."""
+    from mayamatchmovesolver_amd import synthetic as S
+    from mayamatchmovesolver_amd.problem import FLOAT_MAX
+    prob = S.known_scene("test1")
+    n = 40
+    rng = np.random.default_rng(3)
+    lo = np.where(rng.random(n) < 0.5, -FLOAT_MAX, rng.uniform(-5, 0, n))
+    hi = np.where(rng.random(n) < 0.5, FLOAT_MAX, rng.uniform(1, 5, n))
+    prob.param_min, prob.param_max = lo, hi
+    prob.param_offset = np.where(rng.random(n) < 0.3, 0.5, 0.0)
+    prob.param_scale = np.where(rng.random(n) < 0.3, 2.0, 1.0)
+    x = rng.uniform(-3, 3, n)
+    got = prob.external_params(x)
+    for i in range(n):
+        ref = oracle.param_internal_to_external(x[i], lo[i], hi[i], prob.param_offset[i],
+                                                prob.param_scale[i])
+        assert got[i] == pytest.approx(ref, rel=1e-15, abs=1e-15)
