@@ -229,6 +229,8 @@ double mmba_param_internal_to_external(double value, double xmin, double xmax,
 
 int mmba_context_create(int device, mmba_context **out);
 void mmba_context_destroy(mmba_context *ctx);
+/* Wait for all work on the context's device (bench timing brackets). */
+int mmba_context_synchronize(mmba_context *ctx);
 
 /* Upload a problem into HBM once; the plan can then be solved many times
  * (cached device context for the many small calls the Python standard solver
@@ -237,12 +239,32 @@ int mmba_plan_create(mmba_context *ctx, const mmba_problem *prob,
                      const mmba_options *opt, mmba_plan **out);
 void mmba_plan_destroy(mmba_plan *plan);
 
-/* Shard the plan's observations by frame range over `nranks` processes, one
- * per GPU, and reduce normal equations with RCCL.  `unique_id` is 128 bytes
- * from mmba_comm_unique_id on rank 0, broadcast by the caller. */
+/*
+ * Frame-sharded solve: one plan per shard (one process per GPU
+ * over RCCL, or one thread per shard in one process for tests).  Every shard
+ * passes the SAME full problem; the library partitions the frames by
+ * observation count and each shard evaluates the observations of its frames
+ * (plus the other observations of the bundles tracked in them), owns the
+ * reduced-system rows of its camera-frames and factors them; the shards
+ * all-reduce scalars, the global-parameter block, the small separator system
+ * of the partitioned band factorisation and the reduced step.  Every shard
+ * returns the same x, fvec and result.  No reference counterpart (the
+ * reference solver is single-threaded).
+ */
+typedef struct mmba_comm mmba_comm;
+/* 128-byte RCCL unique id, made on one rank and broadcast by the caller. */
 int mmba_comm_unique_id(unsigned char out_id[128]);
-int mmba_plan_set_comm(mmba_plan *plan, int rank, int nranks,
-                       const unsigned char unique_id[128]);
+/* RCCL communicator on ctx's device (ncclCommInitRank). */
+int mmba_comm_create_rccl(mmba_context *ctx, int rank, int nranks,
+                          const unsigned char unique_id[128], mmba_comm **out);
+/* nranks in-process communicators (out[0..nranks-1], nranks <= 8), each used
+ * by one host thread with its own context. */
+int mmba_comm_create_local(int nranks, mmba_comm **out);
+void mmba_comm_destroy(mmba_comm *comm);
+/* Like mmba_plan_create, for the shard `comm` stands for.  Collective: every
+ * shard calls it (and then every solve / measure) together. */
+int mmba_plan_create_sharded(mmba_context *ctx, const mmba_problem *prob,
+                             const mmba_options *opt, mmba_comm *comm, mmba_plan **out);
 
 /* One residual evaluation (measureErrors, adjust_measureErrors.cpp:523) at
  * internal parameters x.  Any output pointer may be NULL. */

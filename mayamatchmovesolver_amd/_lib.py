@@ -48,6 +48,8 @@ def lib():
             f.argtypes = [C.c_double] * 5
         L.mmba_context_create.restype = C.c_int
         L.mmba_context_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.mmba_context_synchronize.restype = C.c_int
+        L.mmba_context_synchronize.argtypes = [C.c_void_p]
         L.mmba_context_destroy.restype = None
         L.mmba_context_destroy.argtypes = [C.c_void_p]
         L.mmba_plan_create.restype = C.c_int
@@ -74,8 +76,17 @@ def lib():
         L.mmba_plan_kernel_stats.argtypes = [C.c_void_p, C.c_int, C.POINTER(abi.MmbaKernelStats)]
         L.mmba_comm_unique_id.restype = C.c_int
         L.mmba_comm_unique_id.argtypes = [C.c_char_p]
-        L.mmba_plan_set_comm.restype = C.c_int
-        L.mmba_plan_set_comm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+        L.mmba_comm_create_rccl.restype = C.c_int
+        L.mmba_comm_create_rccl.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p,
+                                            C.POINTER(C.c_void_p)]
+        L.mmba_comm_create_local.restype = C.c_int
+        L.mmba_comm_create_local.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.mmba_comm_destroy.restype = None
+        L.mmba_comm_destroy.argtypes = [C.c_void_p]
+        L.mmba_plan_create_sharded.restype = C.c_int
+        L.mmba_plan_create_sharded.argtypes = [C.c_void_p, C.POINTER(abi.MmbaProblem),
+                                               C.POINTER(abi.MmbaOptions), C.c_void_p,
+                                               C.POINTER(C.c_void_p)]
         _lib = L
     return _lib
 

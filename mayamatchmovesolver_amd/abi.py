@@ -182,10 +182,14 @@ EXPORTED_SYMBOLS = [
     "mmba_param_internal_to_external",
     "mmba_context_create",
     "mmba_context_destroy",
+    "mmba_context_synchronize",
     "mmba_plan_create",
     "mmba_plan_destroy",
     "mmba_comm_unique_id",
-    "mmba_plan_set_comm",
+    "mmba_comm_create_rccl",
+    "mmba_comm_create_local",
+    "mmba_comm_destroy",
+    "mmba_plan_create_sharded",
     "mmba_plan_measure",
     "mmba_plan_jacobian",
     "mmba_plan_solve",

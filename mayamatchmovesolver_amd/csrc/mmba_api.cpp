@@ -25,6 +25,8 @@ using namespace mmba;
         __VA_ARGS__                                   \
     } catch (const DeviceError &) {                   \
         return MMBA_ERR_DEVICE;                       \
+    } catch (const CommError &) {                     \
+        return MMBA_ERR_COMM;                         \
     } catch (const Unsupported &u) {                  \
         set_error("unsupported: " + u.what);          \
         return MMBA_ERR_UNSUPPORTED;                  \
@@ -108,6 +110,12 @@ int mmba_context_create(int device, mmba_context **out) {
     })
 }
 
+int mmba_context_synchronize(mmba_context *ctx) {
+    if (!ctx) return MMBA_ERR_INVALID;
+    if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;
+    return hipDeviceSynchronize() == hipSuccess ? MMBA_OK : MMBA_ERR_DEVICE;
+}
+
 void mmba_context_destroy(mmba_context *ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -116,6 +124,11 @@ void mmba_context_destroy(mmba_context *ctx) {
 
 int mmba_plan_create(mmba_context *ctx, const mmba_problem *prob, const mmba_options *opt,
                      mmba_plan **out) {
+    return mmba_plan_create_sharded(ctx, prob, opt, nullptr, out);
+}
+
+int mmba_plan_create_sharded(mmba_context *ctx, const mmba_problem *prob,
+                             const mmba_options *opt, mmba_comm *comm, mmba_plan **out) {
     if (!ctx || !prob || !opt || !out) return MMBA_ERR_INVALID;
     *out = nullptr;
     mmba_plan *p = new mmba_plan();
@@ -123,6 +136,7 @@ int mmba_plan_create(mmba_context *ctx, const mmba_problem *prob, const mmba_opt
         MMBA_GUARD({
             MMBA_HIP(hipSetDevice(ctx->device));
             p->impl.ctx = ctx;
+            p->impl.comm = reinterpret_cast<Comm *>(comm);
             p->impl.build(prob, opt);
             return MMBA_OK;
         })
@@ -264,7 +278,5 @@ int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const
     return MMBA_OK;
 }
 
-int mmba_comm_unique_id(unsigned char out_id[128]);
-int mmba_plan_set_comm(mmba_plan *plan, int rank, int nranks, const unsigned char unique_id[128]);
 
 }  // extern "C"

@@ -471,11 +471,14 @@ __device__ __forceinline__ double zget(const double *zp, const BandPart &pd, int
 // [parts[s].snext, +w)) -> T rows [s*w, (s+1)*w); half bandwidth wT = 2w-1.
 // Partition p has prev separator p-1 (arrow rows 0..w-1) and next separator
 // p (arrow rows nprev..nprev+w-1).  Thread per T entry, fixed summation order.
+// Sharded: only the partitions [plo, phi) of this shard (and the separator
+// rows they own) contribute; the shards' partial T are then summed.
 __global__ void k_band_tassemble(const double *__restrict__ Bd, int w,
                                  const double *__restrict__ Ga, const double *__restrict__ Gd,
                                  int nb, int nG, const BandPart *__restrict__ parts, int P,
-                                 const double *__restrict__ zpool, double *TBd, double *TGa,
-                                 double *TGd) {
+                                 int plo, int phi, const double *__restrict__ zpool, double *TBd,
+                                 double *TGa, double *TGd) {
+    auto loc = [&](int p) { return p >= plo && p < phi; };
     const int nsep = P - 1, nbT = nsep * w, wT = 2 * w - 1, W1T = wT + 1, W1 = w + 1;
     const int nband = nbT * W1T, narrow = nG * nbT, ncorner = NGMAX * NGMAX;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -486,13 +489,13 @@ __global__ void k_band_tassemble(const double *__restrict__ Bd, int w,
             const int sR = R / w, uR = R % w, sC = C / w, uC = C % w;
             const BandPart &pa = parts[sR];
             const int gR = pa.snext + uR, gC = parts[sC].snext + uC;
-            if (gR - gC <= w) v = Bd[(size_t)gR * W1 + (gC - gR + w)];
+            if (loc(sR) && gR - gC <= w) v = Bd[(size_t)gR * W1 + (gC - gR + w)];
             if (sR == sC) {
                 const BandPart &pb = parts[sR + 1];
-                v += zget(zpool, pa, pa.nprev + uR, pa.nprev + uC);
-                v += zget(zpool, pb, uR, uC);
+                if (loc(sR)) v += zget(zpool, pa, pa.nprev + uR, pa.nprev + uC);
+                if (loc(sR + 1)) v += zget(zpool, pb, uR, uC);
             } else if (sR == sC + 1) {  // partition sR: prev = sC, next = sR
-                v += zget(zpool, pa, pa.nprev + uR, uC);
+                if (loc(sR)) v += zget(zpool, pa, pa.nprev + uR, uC);
             }  // sR == sC + 2 lies inside the T band but is structurally zero
         }
         TBd[e] = v;
@@ -500,16 +503,19 @@ __global__ void k_band_tassemble(const double *__restrict__ Bd, int w,
         const int q = (e - nband) / nbT, C = (e - nband) % nbT;
         const int sC = C / w, uC = C % w;
         const BandPart &pa = parts[sC], &pb = parts[sC + 1];
-        double v = Ga[(size_t)q * nb + pa.snext + uC];
-        v += zget(zpool, pa, pa.nprev + pa.nnext + q, pa.nprev + uC);
-        v += zget(zpool, pb, pb.nprev + pb.nnext + q, uC);
+        double v = 0.;
+        if (loc(sC)) {
+            v = Ga[(size_t)q * nb + pa.snext + uC];
+            v += zget(zpool, pa, pa.nprev + pa.nnext + q, pa.nprev + uC);
+        }
+        if (loc(sC + 1)) v += zget(zpool, pb, pb.nprev + pb.nnext + q, uC);
         TGa[(size_t)q * nbT + C] = v;
     } else if (e < nband + narrow + ncorner) {
         const int q = (e - nband - narrow) / NGMAX, q2 = (e - nband - narrow) % NGMAX;
         double v = 0.;
         if (q < nG && q2 <= q) {
-            v = Gd[q * NGMAX + q2];
-            for (int p = 0; p < P; ++p) {
+            v = Gd[q * NGMAX + q2];  // this shard's partial global block
+            for (int p = plo; p < phi; ++p) {
                 const BandPart &pd = parts[p];
                 v += zget(zpool, pd, pd.nprev + pd.nnext + q, pd.nprev + pd.nnext + q2);
             }
@@ -520,18 +526,22 @@ __global__ void k_band_tassemble(const double *__restrict__ Bd, int w,
 
 // Separator right-hand side: rT = r[seps + G] - sum_p c_p.
 __global__ void k_band_trhs(const double *__restrict__ r, int w, int nb, int nG,
-                            const BandPart *__restrict__ parts, int P,
+                            const BandPart *__restrict__ parts, int P, int plo, int phi,
                             const double *__restrict__ cpool, double *rT) {
     const int nbT = (P - 1) * w;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    auto loc = [&](int p) { return p >= plo && p < phi; };
     if (e < nbT) {
         const int s = e / w, u = e % w;
         const BandPart &pa = parts[s], &pb = parts[s + 1];
-        rT[e] = r[pa.snext + u] - cpool[pa.coff + pa.nprev + u] - cpool[pb.coff + u];
+        double v = 0.;
+        if (loc(s)) v = r[pa.snext + u] - cpool[pa.coff + pa.nprev + u];
+        if (loc(s + 1)) v -= cpool[pb.coff + u];
+        rT[e] = v;
     } else if (e < nbT + nG) {
         const int q = e - nbT;
-        double v = r[nb + q];
-        for (int p = 0; p < P; ++p)
+        double v = r[nb + q];  // this shard's partial global rows
+        for (int p = plo; p < phi; ++p)
             v -= cpool[parts[p].coff + parts[p].nprev + parts[p].nnext + q];
         rT[e] = v;
     }
@@ -564,18 +574,21 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
         return;
     }
     const int nbT = (B.P - 1) * B.w;
+    const int nloc = B.p_hi - B.p_lo;
     {
-        dim3 grid(nblk_(B.max_arrow, 256), B.P);
-        k_band_extract<<<grid, 256, 0, s>>>(B.Bd, B.w, B.Ga, B.nb, B.d_parts, B.P, B.apool);
+        dim3 grid(nblk_(B.max_arrow, 256), nloc);
+        k_band_extract<<<grid, 256, 0, s>>>(B.Bd, B.w, B.Ga, B.nb, B.d_parts + B.p_lo, nloc,
+                                            B.apool);
     }
-    k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGMAX, false><<<B.P, 256, 0, s>>>(
-        B.Bd, B.w, B.d_parts, B.apool, B.zpool, B.Dinv, nullptr, nullptr, fail, probe);
+    k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGMAX, false><<<nloc, 256, 0, s>>>(
+        B.Bd, B.w, B.d_parts + B.p_lo, B.apool, B.zpool, B.Dinv, nullptr, nullptr, fail, probe);
     {
         const int n = nbT * (2 * B.w) + B.nG * nbT + NGMAX * NGMAX;
         k_band_tassemble<<<nblk_(n, 256), 256, 0, s>>>(B.Bd, B.w, B.Ga, B.Gd, B.nb, B.nG,
-                                                       B.d_parts, B.P, B.zpool, B.TBd, B.TGa,
-                                                       B.TGd);
+                                                       B.d_parts, B.P, B.p_lo, B.p_hi, B.zpool,
+                                                       B.TBd, B.TGa, B.TGd);
     }
+    if (B.comm) B.comm->allreduce(B.TBd, B.tcount, ReduceOp::Sum, s);
     k_band_factor<8, 128, WBAND_MAX, NGMAX, true><<<1, 256, 0, s>>>(
         B.TBd, 2 * B.w - 1, B.d_tpart, B.TGa, nullptr, B.TDinv, B.TGd, B.TGdinv, fail, nullptr);
 }
@@ -591,10 +604,12 @@ void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y
         return;
     }
     const int nbT = (B.P - 1) * B.w;
-    k_band_fwd<8, 64, false><<<B.P, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.apool, B.Dinv,
-                                                  nullptr, B.cpool, r, y);
+    const int nloc = B.p_hi - B.p_lo;
+    k_band_fwd<8, 64, false><<<nloc, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts + B.p_lo, B.apool,
+                                                   B.Dinv, nullptr, B.cpool, r, y);
     k_band_trhs<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(r, B.w, B.nb, B.nG, B.d_parts, B.P,
-                                                       B.cpool, B.rT);
+                                                       B.p_lo, B.p_hi, B.cpool, B.rT);
+    if (B.comm) B.comm->allreduce(B.rT, nbT + B.nG, ReduceOp::Sum, s);
     k_band_fwd<8, 128, true><<<1, 256, 0, s>>>(B.TBd, 2 * B.w - 1, nbT, B.d_tpart, B.TGa,
                                                 B.TDinv, B.TGdinv, nullptr, B.rT, B.yT);
     k_band_tscatter<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(B.yT, B.w, B.nb, B.nG, B.d_parts,
@@ -618,8 +633,8 @@ void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *
                                                 B.TDinv, B.TGdinv, B.yT, B.xT);
     k_band_tscatter<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(B.xT, B.w, B.nb, B.nG, B.d_parts,
                                                            B.P, x);
-    k_band_bwd<8, 64, false><<<B.P, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.apool, B.Dinv,
-                                                  nullptr, y, x);
+    k_band_bwd<8, 64, false><<<B.p_hi - B.p_lo, 256, 0, s>>>(
+        B.Bd, B.w, B.nb, B.d_parts + B.p_lo, B.apool, B.Dinv, nullptr, y, x);
 }
 
 }  // namespace mmba

@@ -1,27 +1,159 @@
-// mmba_comm.cpp -- multi-GPU (one process per GPU) communicator.
-//
-// Round 1: the entry points exist so the ABI is complete; frame-sharded
-// normal-equation reduction over RCCL is not wired yet and reports
-// MMBA_ERR_UNSUPPORTED ("Multi-GPU").
+// mmba_comm.cpp -- communicators of the frame-sharded solve (one process or
+// thread per shard).  Every collective is an in-place all-reduce of a device
+// buffer on the plan's stream:
+//   RcclComm   RCCL over xGMI, one process per GPU (torch.distributed.run);
+//   LocalComm  N shards driven by N host threads in one process (tests on a
+//              one-GPU box run the sharded code path against the unsharded
+//              one): every shard sums all shards' buffers in rank order, so
+//              all shards get bitwise identical results.
+#include <rccl/rccl.h>
+
+#include <condition_variable>
 #include <cstring>
+#include <memory>
+#include <mutex>
 
 #include "mmba_plan.h"
+
+namespace mmba {
+
+// ---- RCCL ----
+struct RcclComm : Comm {
+    ncclComm_t c = nullptr;
+    ~RcclComm() override {
+        if (c) (void)ncclCommDestroy(c);
+    }
+    void allreduce(double *buf, size_t count, ReduceOp op, hipStream_t s) override {
+        if (count == 0) return;
+        const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclDouble,
+                                             op == ReduceOp::Max ? ncclMax : ncclSum, c, s);
+        if (r != ncclSuccess) {
+            set_error(std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+            throw CommError();
+        }
+    }
+};
+
+// ---- in-process group ----
+constexpr int LOCAL_MAX = 8;
+
+struct LocalGroup {
+    int n = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    long gen = 0;
+    double *bufs[LOCAL_MAX] = {};
+    void barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        const long g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
+struct BufSet {
+    const double *p[LOCAL_MAX];
+};
+
+__global__ void k_group_reduce(BufSet b, int n, size_t count, int max_op, double *out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        double s = b.p[0][i];
+        for (int k = 1; k < n; ++k) s = max_op ? fmax(s, b.p[k][i]) : s + b.p[k][i];
+        out[i] = s;
+    }
+}
+
+struct LocalComm : Comm {
+    std::shared_ptr<LocalGroup> g;
+    double *tmp = nullptr;
+    size_t tmp_count = 0;
+    ~LocalComm() override {
+        if (tmp) (void)hipFree(tmp);
+    }
+    void allreduce(double *buf, size_t count, ReduceOp op, hipStream_t s) override {
+        if (count == 0) return;
+        if (count > tmp_count) {
+            if (tmp) MMBA_HIP(hipFree(tmp));
+            MMBA_HIP(hipMalloc(&tmp, count * sizeof(double)));
+            tmp_count = count;
+        }
+        MMBA_HIP(hipStreamSynchronize(s));
+        g->bufs[rank] = buf;
+        g->barrier();  // every shard's buffer is final
+        BufSet b{};
+        for (int k = 0; k < g->n; ++k) b.p[k] = g->bufs[k];
+        const int blocks = (int)std::min<size_t>((count + 255) / 256, 1024);
+        k_group_reduce<<<blocks, 256, 0, s>>>(b, g->n, count, op == ReduceOp::Max, tmp);
+        MMBA_HIP(hipStreamSynchronize(s));
+        g->barrier();  // nobody reads a shard's buffer any more
+        MMBA_HIP(hipMemcpyAsync(buf, tmp, count * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+};
+
+}  // namespace mmba
+
+using namespace mmba;
 
 extern "C" {
 
 int mmba_comm_unique_id(unsigned char out_id[128]) {
     if (!out_id) return MMBA_ERR_INVALID;
-    std::memset(out_id, 0, 128);
-    mmba::set_error("unsupported: RCCL sharding not wired in this build");
-    return MMBA_ERR_UNSUPPORTED;
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+        return MMBA_ERR_COMM;
+    }
+    std::memcpy(out_id, &id, 128);
+    return MMBA_OK;
 }
 
-int mmba_plan_set_comm(mmba_plan *plan, int rank, int nranks, const unsigned char unique_id[128]) {
-    (void)unique_id;
-    if (!plan || rank < 0 || nranks <= 0 || rank >= nranks) return MMBA_ERR_INVALID;
-    if (nranks == 1) return MMBA_OK;
-    mmba::set_error("unsupported: RCCL sharding not wired in this build");
-    return MMBA_ERR_UNSUPPORTED;
+int mmba_comm_create_rccl(mmba_context *ctx, int rank, int nranks,
+                          const unsigned char unique_id[128], mmba_comm **out) {
+    if (!ctx || !unique_id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+        return MMBA_ERR_INVALID;
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;
+    auto *c = new RcclComm();
+    c->rank = rank;
+    c->nranks = nranks;
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, 128);
+    const ncclResult_t r = ncclCommInitRank(&c->c, nranks, id, rank);
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        c->c = nullptr;
+        delete c;
+        return MMBA_ERR_COMM;
+    }
+    *out = reinterpret_cast<mmba_comm *>(static_cast<Comm *>(c));
+    return MMBA_OK;
+}
+
+int mmba_comm_create_local(int nranks, mmba_comm **out) {
+    if (!out || nranks < 1 || nranks > LOCAL_MAX) return MMBA_ERR_INVALID;
+    auto g = std::make_shared<LocalGroup>();
+    g->n = nranks;
+    for (int r = 0; r < nranks; ++r) {
+        auto *c = new LocalComm();
+        c->rank = r;
+        c->nranks = nranks;
+        c->g = g;
+        out[r] = reinterpret_cast<mmba_comm *>(static_cast<Comm *>(c));
+    }
+    return MMBA_OK;
+}
+
+void mmba_comm_destroy(mmba_comm *comm) {
+    delete reinterpret_cast<Comm *>(comm);
 }
 
 }  // extern "C"

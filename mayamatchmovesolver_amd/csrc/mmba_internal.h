@@ -30,6 +30,16 @@ constexpr int LMAX = 20;    // local Jacobian columns per observation
 constexpr int TILE = 64;    // reduced-system tile edge
 constexpr int CAMREC = 20;  // doubles per camera-frame record
 
+// In-place all-reduce of device buffers across the shards of a plan
+// (mmba_comm.cpp: RCCL, or an in-process group for tests).
+enum class ReduceOp { Sum, Max };
+struct CommError {};
+struct Comm {
+    int rank = 0, nranks = 1;
+    virtual ~Comm() {}
+    virtual void allreduce(double *buf, size_t count, ReduceOp op, hipStream_t s) = 0;
+};
+
 // Band + arrow layout of the reduced system (narrow structures): rows of
 // camera-frame parameters keep w+1 entries each (columns r-w .. r), the
 // global parameters are dense arrow rows (mmba_band.hip).
@@ -51,12 +61,15 @@ struct BandPart {
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
     int P = 1, w = 0, nb = 0, nG = 0;
+    int p_lo = 0, p_hi = 1;                  // partitions this shard factors
+    Comm *comm = nullptr;                    // sharded: T, rT are all-reduced
     long long max_arrow = 0;                 // max na*(r1-r0) over partitions
     double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr, *Gdinv = nullptr, *Dinv = nullptr;
     BandPart *d_parts = nullptr;             // P partitions (P == 1: arrow = Ga)
     double *apool = nullptr, *zpool = nullptr, *cpool = nullptr;
     // separator system (P > 1)
     double *TBd = nullptr, *TGa = nullptr, *TGd = nullptr, *TGdinv = nullptr, *TDinv = nullptr;
+    size_t tcount = 0;                       // TBd | TGa | TGd are contiguous
     BandPart *d_tpart = nullptr;
     double *rT = nullptr, *yT = nullptr, *xT = nullptr;
 };
@@ -109,6 +122,12 @@ struct DevProblem {
     const int *p_attr, *p_frame, *p_class, *p_pos, *p_both, *p_blk;
     const double *p_min, *p_max, *p_off, *p_scale;
     const int *g_param;  // global index -> param id
+    // frame sharding (nullptr / all-true when unsharded): this shard owns the
+    // observations of its frame range, the camera-frames in it (reduced-system
+    // rows [Ra, Rb)), the bundles whose first observation it holds, and, on
+    // the root shard, the global parameters.
+    const int *obs_own, *cf_own, *bnd_own;
+    int root, Ra, Rb;
 };
 
 __device__ __forceinline__ double *s_at(const SView &V, int R, int C) {

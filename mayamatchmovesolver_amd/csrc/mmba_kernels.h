@@ -17,10 +17,13 @@ void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, dou
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed);
+// aggbuf = [Agg (NGMAX^2) | g_G (NGMAX)]: the global-parameter normal
+// equations, all-reduced across shards before launch_colnorms.
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
-               double *Abg, double *Agg, double *g, double *glob_partial, int glob_chunk,
-               double *acnorm);
+               double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk);
+void launch_colnorms(hipStream_t s, const DevProblem &P, const double *Acc, const double *Abb,
+                     const double *aggbuf, double *acnorm, double *g);
 void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
                           const double *Abg, const double *g, const double *diag, double lam,
                           double *Lb, double *tb, double *Wg, int *fail);
@@ -61,25 +64,33 @@ void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double
 // L y = r (band_forward; keeps the separator part of y for band_backward) and
 // L^T x = y.  r, y, x are in reduced-system order (length nb + nG).
 void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe);
+// (sharded: the partitions p_lo..p_hi run here, the separator system and its
+// right-hand side are all-reduced over B.comm)
 void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
 void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
+// mask (nullable): entries this shard owns
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                  int nparts, double *out);
+                  int nparts, double *out, const int *mask = nullptr);
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                      int nparts, double *out);
+                      int nparts, double *out, const int *mask = nullptr);
 void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out);
 void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
-                  double *partial, int nparts, double *out);
+                  double *partial, int nparts, double *out, const int *mask = nullptr);
 void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                      const int *nloc, const double *p, double *partial, int nparts,
                      double *out);
+void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mask,
+                      double *partial, int nparts, double *out);
+void launch_keep_rows(hipStream_t s, double *v, int lo, int hi, int nCF, int nR, int root);
+void launch_keep_mask(hipStream_t s, const double *src, const int *mask, int n, double *dst);
 void launch_lm_step(hipStream_t s, int n, const double *xs, const double *x, const double *diag,
                     double *wa1, double *wa2, double *wa3);
 void launch_diag_init(hipStream_t s, int n, const double *acnorm, double *diag, int first,
                       int mode);
 void launch_newton_v(hipStream_t s, int n, const double *diag, const double *x, double dxnorm,
                      double *v);
-void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const double *f2,
+void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const int *obs_own,
+                      const double *f2,
                       const double *eu2, const double *ed, double *f2o, double *eu2o,
                       double *edo);
 

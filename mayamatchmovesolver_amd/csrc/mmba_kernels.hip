@@ -11,6 +11,12 @@
 
 namespace mmba {
 
+// Frame-sharding ownership (all-true when unsharded).
+MMBA_DEV bool own_obs(const DevProblem &P, int i) { return !P.obs_own || P.obs_own[i]; }
+MMBA_DEV bool own_cf(const DevProblem &P, int cf) { return !P.cf_own || P.cf_own[cf]; }
+MMBA_DEV bool own_bnd(const DevProblem &P, int b) { return !P.bnd_own || P.bnd_own[b]; }
+MMBA_DEV bool own_mask(const int *m, int i) { return !m || m[i]; }
+
 // -------------------------------------------------------------------------
 // Parameters: external values, FD perturbations (adjust_solveFunc.cpp:148-180,
 // cminpack fdjac2), setParameters (adjust_setParameters.cpp:174-250).
@@ -114,7 +120,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
             eu[2 * i + 1] = r.uy;
             ed[i] = r.dist;
         }
-        s = r.ex * r.ex + r.ey * r.ey;
+        if (own_obs(P, i)) s = r.ex * r.ex + r.ey * r.ey;
     }
     red[threadIdx.x] = s;
     __syncthreads();
@@ -240,6 +246,7 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
     __shared__ int sN[NE_CHUNK];
     __shared__ double sF[2][NE_CHUNK];
     const int cf = blockIdx.x;
+    if (!own_cf(P, cf)) return;  // another shard owns this camera-frame
     const int pc = P.cf_pc[cf];
     const int nG = P.nG;
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
@@ -383,6 +390,7 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
     const int i0 = blockIdx.x * chunk;
     const int i1 = min(M, i0 + chunk);
     for (int i = i0 + (int)threadIdx.x; i < i1; i += blockDim.x) {
+        if (!own_obs(P, i)) continue;
         double gx[NGMAX], gy[NGMAX];
 #pragma unroll
         for (int q = 0; q < NGMAX; ++q) gx[q] = gy[q] = 0.;
@@ -428,7 +436,7 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
 }
 
 __global__ void k_ne_glob_reduce(DevProblem P, const double *__restrict__ partial, int nblk,
-                                 double *Agg, double *g) {
+                                 double *Agg, double *gG) {
     const int nG = P.nG;
     for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
         const bool mat = t < NGMAX * NGMAX;
@@ -438,14 +446,14 @@ __global__ void k_ne_glob_reduce(DevProblem P, const double *__restrict__ partia
         if (mat)
             Agg[t] = s;
         else
-            g[P.g_param[t - NGMAX * NGMAX]] = s;
+            gG[t - NGMAX * NGMAX] = s;
     }
 }
 
 // Column norms acnorm_p = sqrt(A_pp) in parameter order.
 __global__ void k_colnorms(DevProblem P, const double *__restrict__ Acc,
                            const double *__restrict__ Abb, const double *__restrict__ Agg,
-                           double *acnorm) {
+                           const double *__restrict__ gG, double *acnorm, double *g) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
     const int cls = P.p_class[p];
@@ -462,6 +470,7 @@ __global__ void k_colnorms(DevProblem P, const double *__restrict__ Acc,
     } else {
         const int gi = P.p_pos[p] - (P.nR - P.nG);
         d = Agg[gi * NGMAX + gi];
+        g[p] = gG[gi];
     }
     acnorm[p] = sqrt(d);
 }
@@ -578,6 +587,7 @@ __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
     const int nCF = P.nR - nG;
     if (t < P.ncf) {
         const int cf = t;
+        if (!own_cf(P, cf)) return;
         const int pc = P.cf_pc[cf];
         const int r0 = P.cf_roff[cf];
         const int v0 = P.cf_var_off[cf] + 1;
@@ -601,6 +611,10 @@ __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
     } else if (t < P.ncf + nG) {
         const int q = t - P.ncf;
         const int p = P.g_param[q];
+        if (!P.root) {  // the global block and its rhs are added once
+            rhs[nCF + q] = 0.;
+            return;
+        }
         for (int c = 0; c <= q; ++c) {
             double v = Agg[q * NGMAX + c];
             if (c == q) {
@@ -717,7 +731,7 @@ __global__ void __launch_bounds__(64) k_schur_rhs(DevProblem P, const double *__
                                                   const double *__restrict__ tb, double *rhs) {
     const int cf = blockIdx.x;
     const int pc = P.cf_pc[cf];
-    if (pc == 0) return;
+    if (pc == 0 || !own_cf(P, cf)) return;
     const int r0 = P.cf_roff[cf];
     const int M = P.M;
     double acc[PCMAX];
@@ -754,14 +768,16 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
     if (pb == 0 || nG == 0) return;
     const int M = P.M;
     const int nCF = P.nR - nG;
+    const bool ownb = own_bnd(P, b);
     const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
     const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1], t2 = tb[(size_t)b * 3 + 2];
     for (int q = 0; q < nG; ++q) {
         const double *wg = &Wg[((size_t)b * NGMAX + q) * 3];
-        atomicAdd(&rhs[nCF + q], -(wg[0] * t0 + wg[1] * t1 + wg[2] * t2));
+        if (ownb) atomicAdd(&rhs[nCF + q], -(wg[0] * t0 + wg[1] * t1 + wg[2] * t2));
         for (int qj = q0; qj < q1; ++qj) {
             const int j = P.bobs[qj];
             const int cfj = P.obs_cf[j];
+            if (!own_cf(P, cfj)) continue;  // S rows/columns of own camera-frames
             const int pcj = P.cf_pc[cfj];
             const int rj = P.cf_roff[cfj];
             for (int c = 0; c < pcj; ++c) {
@@ -771,6 +787,7 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
                 atomicAdd(s_at(V, nCF + q, rj + c), -v);
             }
         }
+        if (!ownb) continue;
         for (int q2 = 0; q2 <= q; ++q2) {
             const double *wh = &Wg[((size_t)b * NGMAX + q2) * 3];
             atomicAdd(s_at(V, nCF + q, nCF + q2),
@@ -840,6 +857,7 @@ __global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
     const int M = P.M, nG = P.nG;
     const int nCF = P.nR - nG;
     const int po = P.bnd_par_off[b];
+    const bool ownb = own_bnd(P, b);
     double L[3][3];
     for (int a = 0; a < 3; ++a)
         for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
@@ -849,10 +867,11 @@ __global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
         for (int k = 0; k < a; ++k) t -= L[a][k] * u[k];
         u[a] = t / L[a][a];
     }
-    usq[b] = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+    usq[b] = ownb ? u[0] * u[0] + u[1] * u[1] + u[2] * u[2] : 0.;
     for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
         const int i = P.bobs[q];
         const int cf = P.obs_cf[i];
+        if (!own_cf(P, cf)) continue;
         const int pc = P.cf_pc[cf];
         const int r0 = P.cf_roff[cf];
         for (int a = 0; a < pc; ++a) {
@@ -861,6 +880,7 @@ __global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
             atomicAdd(&wR[r0 + a], -s);
         }
     }
+    if (!ownb) return;
     for (int q = 0; q < nG; ++q) {
         double s = 0.;
         for (int c = 0; c < 3; ++c) s += Wg[((size_t)b * NGMAX + q) * 3 + c] * u[c];
@@ -871,7 +891,12 @@ __global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
 // v (parameter order) -> R order (non-bundle parameters); padded tail zero.
 __global__ void k_gather_R(DevProblem P, const double *__restrict__ v, double *vR, int nRpad) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < P.n && P.p_class[p] != PC_B) vR[P.p_pos[p]] = v[p];
+    if (p < P.n && P.p_class[p] != PC_B) {
+        // this shard's rows, the global rows on the root shard, zero elsewhere
+        const int R = P.p_pos[p];
+        const bool mine = (R >= P.nR - P.nG) ? P.root != 0 : (R >= P.Ra && R < P.Rb);
+        vR[R] = mine ? v[p] : 0.;
+    }
     const int r = P.nR + p;
     if (r < nRpad && p < nRpad) vR[r] = 0.;
 }
@@ -881,10 +906,11 @@ __global__ void k_gather_R(DevProblem P, const double *__restrict__ v, double *v
 // -------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_sumsq(const double *__restrict__ a,
                                                const double *__restrict__ d, int n,
-                                               double *partial) {
+                                               const int *__restrict__ mask, double *partial) {
     __shared__ double red[256];
     double s = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (!own_mask(mask, i)) continue;
         double v = d ? d[i] * a[i] : a[i];
         s += v * v;
     }
@@ -899,10 +925,11 @@ __global__ void __launch_bounds__(256) k_sumsq(const double *__restrict__ a,
 
 __global__ void __launch_bounds__(256) k_sumsq_div(const double *__restrict__ a,
                                                    const double *__restrict__ d, int n,
-                                                   double *partial) {
+                                                   const int *__restrict__ mask, double *partial) {
     __shared__ double red[256];
     double s = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (!own_mask(mask, i)) continue;
         double v = a[i] / d[i];
         s += v * v;
     }
@@ -932,11 +959,12 @@ __global__ void __launch_bounds__(256) k_reduce_sum(const double *__restrict__ p
 // gnorm (lmder.c): max_l |g_l / fnorm| / acnorm_l over acnorm_l != 0.
 __global__ void __launch_bounds__(256) k_gnorm(const double *__restrict__ g,
                                                const double *__restrict__ acnorm, int n,
-                                               double fnorm, double *partial) {
+                                               double fnorm, const int *__restrict__ mask,
+                                               double *partial) {
     __shared__ double red[256];
     double m = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        if (acnorm[i] != 0.) m = fmax(m, fabs((g[i] / fnorm) / acnorm[i]));
+        if (own_mask(mask, i) && acnorm[i] != 0.) m = fmax(m, fabs((g[i] / fnorm) / acnorm[i]));
     }
     red[threadIdx.x] = m;
     __syncthreads();
@@ -970,6 +998,7 @@ __global__ void __launch_bounds__(256) k_jp_sumsq(DevProblem P, const double *__
     const int M = P.M;
     double s = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        if (!own_obs(P, i)) continue;
         double ax = 0., ay = 0.;
         const int nl = nloc[i];
         for (int l = 0; l < nl; ++l) {
@@ -986,6 +1015,39 @@ __global__ void __launch_bounds__(256) k_jp_sumsq(DevProblem P, const double *__
         __syncthreads();
     }
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// max over owned entries of [acnorm_j == 0] (MINPACK's rank test, nsing < n).
+__global__ void __launch_bounds__(256) k_zero_flag(const double *__restrict__ acnorm, int n,
+                                                   const int *__restrict__ mask,
+                                                   double *partial) {
+    __shared__ double red[256];
+    double m = 0.;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        if (own_mask(mask, i) && acnorm[i] == 0.) m = 1.;
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// Keep this shard's reduced-system rows [lo, hi) (and the global rows on the
+// root shard) before the rows are summed across shards.
+__global__ void k_keep_rows(double *v, int lo, int hi, int nCF, int nR, int root) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nR) return;
+    const bool keep = (r >= nCF) ? root != 0 : (r >= lo && r < hi);
+    if (!keep) v[r] = 0.;
+}
+
+// dst = mask ? src : 0
+__global__ void k_keep_mask(const double *__restrict__ src, const int *__restrict__ mask, int n,
+                            double *dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = own_mask(mask, i) ? src[i] : 0.;
 }
 
 // Elementwise LM vector updates.
@@ -1018,11 +1080,12 @@ __global__ void k_newton_v(int n, const double *__restrict__ diag, const double 
 
 // Device order -> reference (errorToMarkerList) order.
 __global__ void k_unpermute(int M, const int *__restrict__ ref_of_dev,
+                            const int *__restrict__ obs_own,
                             const double *__restrict__ f2, const double *__restrict__ eu2,
                             const double *__restrict__ ed, double *f2o, double *eu2o,
                             double *edo) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M) return;
+    if (i >= M || (obs_own && !obs_own[i])) return;
     const int r = ref_of_dev[i];
     if (f2) {
         f2o[2 * r] = f2[2 * i];
@@ -1073,16 +1136,20 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
 }
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
-               double *Abg, double *Agg, double *g, double *glob_partial, int glob_chunk,
-               double *acnorm) {
+               double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk) {
+    double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
     if (P.ncf > 0) k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
     if (P.nB > 0) k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
     if (P.nG > 0) {
         const int nb = nblk(P.M, glob_chunk);
         k_ne_glob<<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
-        k_ne_glob_reduce<<<1, 256, 0, s>>>(P, glob_partial, nb, Agg, g);
+        k_ne_glob_reduce<<<1, 256, 0, s>>>(P, glob_partial, nb, Agg, gG);
     }
-    k_colnorms<<<nblk(P.n, 256), 256, 0, s>>>(P, Acc, Abb, Agg, acnorm);
+}
+void launch_colnorms(hipStream_t s, const DevProblem &P, const double *Acc, const double *Abb,
+                     const double *aggbuf, double *acnorm, double *g) {
+    k_colnorms<<<nblk(P.n, 256), 256, 0, s>>>(P, Acc, Abb, aggbuf, aggbuf + NGMAX * NGMAX,
+                                               acnorm, g);
 }
 void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
                           const double *Abg, const double *g, const double *diag, double lam,
@@ -1137,21 +1204,21 @@ void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double
     k_gather_R<<<nblk(n, 256), 256, 0, s>>>(P, v, vR, nRpad);
 }
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                  int nparts, double *out) {
-    k_sumsq<<<nparts, 256, 0, s>>>(a, d, n, partial);
+                  int nparts, double *out, const int *mask) {
+    k_sumsq<<<nparts, 256, 0, s>>>(a, d, n, mask, partial);
     k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                      int nparts, double *out) {
-    k_sumsq_div<<<nparts, 256, 0, s>>>(a, d, n, partial);
+                      int nparts, double *out, const int *mask) {
+    k_sumsq_div<<<nparts, 256, 0, s>>>(a, d, n, mask, partial);
     k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out) {
     k_reduce_sum<<<1, 256, 0, s>>>(partial, n, out);
 }
 void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
-                  double *partial, int nparts, double *out) {
-    k_gnorm<<<nparts, 256, 0, s>>>(g, acnorm, n, fnorm, partial);
+                  double *partial, int nparts, double *out, const int *mask) {
+    k_gnorm<<<nparts, 256, 0, s>>>(g, acnorm, n, fnorm, mask, partial);
     k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
@@ -1159,6 +1226,17 @@ void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const 
                      double *out) {
     k_jp_sumsq<<<nparts, 256, 0, s>>>(P, J, jcol, nloc, p, partial);
     k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mask,
+                      double *partial, int nparts, double *out) {
+    k_zero_flag<<<nparts, 256, 0, s>>>(acnorm, n, mask, partial);
+    k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_keep_rows(hipStream_t s, double *v, int lo, int hi, int nCF, int nR, int root) {
+    if (nR > 0) k_keep_rows<<<nblk(nR, 256), 256, 0, s>>>(v, lo, hi, nCF, nR, root);
+}
+void launch_keep_mask(hipStream_t s, const double *src, const int *mask, int n, double *dst) {
+    if (n > 0) k_keep_mask<<<nblk(n, 256), 256, 0, s>>>(src, mask, n, dst);
 }
 void launch_lm_step(hipStream_t s, int n, const double *xs, const double *x, const double *diag,
                     double *wa1, double *wa2, double *wa3) {
@@ -1172,10 +1250,12 @@ void launch_newton_v(hipStream_t s, int n, const double *diag, const double *x, 
                      double *v) {
     k_newton_v<<<nblk(n, 256), 256, 0, s>>>(n, diag, x, dxnorm, v);
 }
-void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const double *f2,
+void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const int *obs_own,
+                      const double *f2,
                       const double *eu2, const double *ed, double *f2o, double *eu2o,
                       double *edo) {
-    k_unpermute<<<nblk(M, 256), 256, 0, s>>>(M, ref_of_dev, f2, eu2, ed, f2o, eu2o, edo);
+    k_unpermute<<<nblk(M, 256), 256, 0, s>>>(M, ref_of_dev, obs_own, f2, eu2, ed, f2o, eu2o,
+                                             edo);
 }
 
 }  // namespace mmba

@@ -35,9 +35,20 @@ double Plan::read_scalar(int slot) {
     return h_scalar[slot];
 }
 
+// Sharded: every shard holds a partial sum (or max); sum them in place.
+void Plan::allreduce(double *d, size_t count, ReduceOp op) {
+    if (comm && nranks > 1) comm->allreduce(d, count, op, s);
+}
+
+double Plan::reduce_read(int slot, ReduceOp op) {
+    allreduce(d_scalar + slot, 1, op);
+    return read_scalar(slot);
+}
+
+// ||D v|| over the parameters (each counted by the shard that owns it).
 double Plan::dnorm(const double *dv) {
-    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + 1);
-    return std::sqrt(read_scalar(1));
+    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + 1, d_p_own);
+    return std::sqrt(reduce_read(1));
 }
 
 // iflag = 1: setParameters + measureErrors.  Returns ||f||.
@@ -57,7 +68,7 @@ double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
         resid_n++;
     }
     launch_reduce_sum(s, d_partial, residual_blocks(P), d_scalar);
-    const double r = std::sqrt(read_scalar(0));
+    const double r = std::sqrt(reduce_read(0));
     t_func += wall_now() - t0;
     return r;
 }
@@ -72,8 +83,11 @@ void Plan::jac(const double *dx) {
     if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                     d_stale, d_eu, d_ed);
+    if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
-              d_glob_partial, glob_chunk, d_acnorm);
+              d_glob_partial, glob_chunk);
+    if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
+    launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
     if (timing) {
         MMBA_HIP(hipEventRecord(ev_b, s));
         MMBA_HIP(hipEventSynchronize(ev_b));
@@ -96,6 +110,7 @@ bool Plan::solve_damped(double lam) {
     }
     if (nR > 0) {
         const SView V = sview();
+        MMBA_HIP(hipMemsetAsync(d_rhs, 0, sizeof(double) * nRpad, s));
         if (band) {
             const int nb = nR - nG;
             MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
@@ -136,6 +151,10 @@ bool Plan::solve_damped(double lam) {
         if (band) {
             band_forward(s, bs, d_rhs, d_yR);
             band_backward(s, bs, d_yR, d_xR);
+            if (nranks > 1) {  // every shard needs the rows of its halo camera-frames
+                launch_keep_rows(s, d_xR, Ra, Rb, nR - nG, nR, rank == 0);
+                allreduce(d_xR, nR);
+            }
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_rhs, d_yR);
             launch_trsv_bwd_all(s, d_S, d_slot, NT, d_cols_off, d_cols, d_Linv, d_yR, d_xR);
@@ -154,8 +173,14 @@ bool Plan::solve_damped(double lam) {
     if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_xs);
     MMBA_HIP(hipMemcpyAsync(h_fail, d_fail, sizeof(int), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipStreamSynchronize(s));
+    bool ok = *h_fail == 0;
+    if (nranks > 1) {
+        h_scalar[5] = ok ? 0. : 1.;
+        MMBA_HIP(hipMemcpyAsync(d_scalar + 5, h_scalar + 5, sizeof(double), hipMemcpyHostToDevice, s));
+        ok = reduce_read(5, ReduceOp::Max) == 0.;
+    }
     t_linear += wall_now() - t0;
-    return *h_fail == 0;
+    return ok;
 }
 
 // sqrt(v^T (A + lam D^2)^-1 v) with v = D^2 xs / dxnorm, using the current
@@ -163,12 +188,11 @@ bool Plan::solve_damped(double lam) {
 double Plan::newton_term(double dxnorm) {
     const double t0 = wall_now();
     launch_newton_v(s, n, d_diag, d_xs, dxnorm, d_v);
-    double acc = 0.;
+    MMBA_HIP(hipMemsetAsync(d_scalar + 2, 0, 2 * sizeof(double), s));
     if (nR > 0) launch_gather_R(s, P, d_v, d_wR, nRpad);
     if (nB_solved > 0) {
         launch_newton_bundle(s, P, d_W, d_Wg, d_Lb, d_v, d_wR, d_usq);
         launch_reduce_sum(s, d_usq, nB, d_scalar + 2);
-        acc += read_scalar(2);
     }
     if (nR > 0) {
         if (band) {
@@ -181,11 +205,14 @@ double Plan::newton_term(double dxnorm) {
                 launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
             }
         }
-        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + 3);
-        acc += read_scalar(3);
+        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + 3, d_ymask);
     }
+    allreduce(d_scalar + 2, 2);
+    MMBA_HIP(hipMemcpyAsync(h_scalar + 2, d_scalar + 2, 2 * sizeof(double),
+                            hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
     t_linear += wall_now() - t0;
-    return std::sqrt(acc);
+    return std::sqrt(h_scalar[2] + h_scalar[3]);
 }
 
 // lmpar restated on normal equations (see oracle/refcpu.c lmpar).
@@ -205,8 +232,9 @@ static double lmpar_ne(Plan &pl, double delta, double *par) {
         const double temp = pl.newton_term(dxnorm);
         parl = fp / delta / temp / temp;
     }
-    launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts, pl.d_scalar + 4);
-    const double gnorm = std::sqrt(pl.read_scalar(4));
+    launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts, pl.d_scalar + 4,
+                     pl.d_p_own);
+    const double gnorm = std::sqrt(pl.reduce_read(4));
     double paru = gnorm / delta;
     if (paru == 0.) paru = dwarf / std::min(delta, p1);
     *par = std::max(*par, parl);
@@ -231,18 +259,34 @@ static double lmpar_ne(Plan &pl, double delta, double *par) {
     return dxnorm;
 }
 
+// Device order -> reference (errorToMarkerList) order on the host.  Sharded:
+// every shard scatters the observations it owns and the shards' buffers are
+// summed, so every shard returns the full vectors.
 void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
                               double *f_out, double *eu_out, double *ed_out) {
-    double *tf = f_out ? d_ftrial : nullptr;  // scratch buffers for the permutation
-    double *te = eu_out ? d_J : nullptr;
-    double *td = ed_out ? d_J + m : nullptr;
-    launch_unpermute(s, M, d_ref_of_dev, f_out ? d_f2 : nullptr, eu_out ? d_eu2 : nullptr,
-                     ed_out ? d_ed1 : nullptr, tf, te, td);
-    if (f_out) MMBA_HIP(hipMemcpyAsync(f_out, tf, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+    double *tf = d_gather, *te = d_gather + mg, *td = d_gather + 2 * (size_t)mg;
+    const size_t total = 2 * (size_t)mg + Mg;
+    if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_gather, 0, sizeof(double) * total, s));
+    launch_unpermute(s, M, d_ref_of_dev, P.obs_own, f_out ? d_f2 : nullptr,
+                     eu_out ? d_eu2 : nullptr, ed_out ? d_ed1 : nullptr, tf, te, td);
+    allreduce(d_gather, total);
+    if (f_out) MMBA_HIP(hipMemcpyAsync(f_out, tf, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
     if (eu_out)
-        MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+        MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
     if (ed_out)
-        MMBA_HIP(hipMemcpyAsync(ed_out, td, sizeof(double) * M, hipMemcpyDeviceToHost, s));
+        MMBA_HIP(hipMemcpyAsync(ed_out, td, sizeof(double) * Mg, hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+}
+
+// Parameter vector of the solve on the host (sharded: owners' entries summed).
+void Plan::download_params(const double *dx, double *x_out) {
+    if (nranks > 1) {
+        double *tx = d_gather + 2 * (size_t)mg + Mg;
+        launch_keep_mask(s, dx, d_p_own, n, tx);
+        allreduce(tx, n);
+        dx = tx;
+    }
+    MMBA_HIP(hipMemcpyAsync(x_out, dx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipStreamSynchronize(s));
 }
 
@@ -271,16 +315,17 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
     }
-    std::vector<double> ed(M);
+    std::vector<double> ed(Mg);
     download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed.data());
-    if (ed_out) std::memcpy(ed_out, ed.data(), sizeof(double) * M);
-    if (stats) error_stats(ed.data(), M, &stats[0], &stats[1], &stats[2]);
+    if (ed_out) std::memcpy(ed_out, ed.data(), sizeof(double) * Mg);
+    if (stats) error_stats(ed.data(), Mg, &stats[0], &stats[1], &stats[2]);
     return MMBA_OK;
 }
 
 // Dense reference-order Jacobian at x (column-major, ldfjac = m); for tests
 // and small problems only.
 int Plan::dense_jacobian(const double *x, double *fjac) {
+    if (nranks > 1) throw Unsupported{"dense Jacobian of a sharded plan"};
     MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
     MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
     fun(d_x, d_f, d_eu, d_ed);
@@ -318,14 +363,14 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     };
     // fresh attribute block (the scene's current values)
     MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
-    std::vector<double> ed_host(M);
+    std::vector<double> ed_host(Mg);
     double init_avg = 0., init_min = 0., init_max = 0.;
     if (opt.accept_only_better) {
         // measureErrors before any parameter is set (adjust_base.cpp:1080-1103)
         launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
         download_ref_order(nullptr, nullptr, d_ed, nullptr, nullptr, ed_host.data());
-        error_stats(ed_host.data(), M, &init_avg, &init_min, &init_max);
+        error_stats(ed_host.data(), Mg, &init_avg, &init_min, &init_max);
     }
     r.error_initial_avg = init_avg;
 
@@ -344,7 +389,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     bool interrupted = false;
     double delta = 0., xnorm = 0., par = 0., fnorm = 0., gnorm = 0., ratio = 0.;
 
-    if (n <= 0 || m < n || ftol < 0. || xtol < 0. || gtol < 0. || maxfev <= 0 || factor <= 0.)
+    if (n <= 0 || mg < n || ftol < 0. || xtol < 0. || gtol < 0. || maxfev <= 0 || factor <= 0.)
         goto TERMINATE;
     if (mode == 2) {
         // diag = paramWeightList = 1.0 (adjust_base.cpp: countUpNumberOfUnknownParameters)
@@ -368,16 +413,9 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             ++njev;
             jac_evals += n;
             if (lmdif) nfev += n;
-            {
-                // rank deficiency from exactly-zero columns (MINPACK nsing < n)
-                std::vector<double> acn(n);
-                MMBA_HIP(hipMemcpyAsync(acn.data(), d_acnorm, sizeof(double) * n,
-                                        hipMemcpyDeviceToHost, s));
-                MMBA_HIP(hipStreamSynchronize(s));
-                rank_deficient = false;
-                for (double v : acn)
-                    if (v == 0.) rank_deficient = true;
-            }
+            // rank deficiency from exactly-zero columns (MINPACK nsing < n)
+            launch_zero_flag(s, d_acnorm, n, d_p_own, d_partial, nparts, d_scalar + 5);
+            rank_deficient = reduce_read(5, ReduceOp::Max) != 0.;
             launch_diag_init(s, n, d_acnorm, d_diag, iter == 1, mode);
             if (iter == 1) {
                 // diag set from acnorm (mode 1) *before* the max() update in
@@ -389,8 +427,9 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             }
             gnorm = 0.;
             if (fnorm != 0.) {
-                launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + 6);
-                gnorm = read_scalar(6);
+                launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + 6,
+                             d_p_own);
+                gnorm = reduce_read(6, ReduceOp::Max);
             }
             if (gnorm <= gtol) info = 4;
             if (info != 0) goto TERMINATE;
@@ -398,8 +437,8 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 const double dxn = lmpar_ne(*this, delta, &par);
                 (void)dxn;
                 launch_lm_step(s, n, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3);
-                launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + 1);
-                const double pnorm = std::sqrt(read_scalar(1));
+                launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + 1, d_p_own);
+                const double pnorm = std::sqrt(reduce_read(1));
                 if (iter == 1) delta = std::min(delta, pnorm);
                 const double fnorm1 = fun(d_wa2, d_ftrial, d_eu, d_ed);
                 ++nfev;
@@ -411,7 +450,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     actred = 1. - d1 * d1;
                 }
                 launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, d_partial, nparts, d_scalar + 1);
-                const double temp1 = std::sqrt(read_scalar(1)) / fnorm;
+                const double temp1 = std::sqrt(reduce_read(1)) / fnorm;
                 const double temp2 = (std::sqrt(par) * pnorm) / fnorm;
                 const double prered = temp1 * temp1 + temp2 * temp2 / p5;
                 const double dirder = -(temp1 * temp1 + temp2 * temp2);
@@ -462,11 +501,11 @@ TERMINATE:
     r.error_final = fnorm;
     {
         std::vector<double> xh(n);
-        MMBA_HIP(hipMemcpyAsync(xh.data(), d_x, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+        download_params(d_x, xh.data());
         download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_host.data());
-        if (ed_out) std::memcpy(ed_out, ed_host.data(), sizeof(double) * M);
+        if (ed_out) std::memcpy(ed_out, ed_host.data(), sizeof(double) * Mg);
         double avg, mn, mx;
-        error_stats(ed_host.data(), M, &avg, &mn, &mx);
+        error_stats(ed_host.data(), Mg, &avg, &mn, &mx);
         r.error_avg = avg;
         r.error_min = mn;
         r.error_max = mx;
@@ -480,8 +519,8 @@ TERMINATE:
         // RMS at the returned parameters
         MMBA_HIP(hipMemcpyAsync(d_wa2, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_wa2, d_ftrial, d_J, d_J + m);  // scratch user buffers
-        launch_sumsq(s, d_J + m, nullptr, M, d_partial, nparts, d_scalar + 7);
-        r.error_rms = std::sqrt(read_scalar(7) / M);
+        launch_sumsq(s, d_J + m, nullptr, M, d_partial, nparts, d_scalar + 7, P.obs_own);
+        r.error_rms = std::sqrt(reduce_read(7) / Mg);
     }
     r.num_trace = trace ? trace->count : 0;
     r.time_solve_s = wall_now() - t_start;

@@ -52,9 +52,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     const int nA = pr->num_attrs, nT = pr->num_transforms, nC = pr->num_cameras;
     const int nL = pr->num_lenses, nK = pr->num_markers;
     nB = pr->num_bundles;
-    M = pr->num_obs;
+    Mg = pr->num_obs;
+    mg = 2 * Mg;
+    M = Mg;  // local observations: all of them unless sharded (below)
     n = pr->num_params;
     m = 2 * M;
+    rank = comm ? comm->rank : 0;
+    nranks = comm ? comm->nranks : 1;
     require(F > 0 && M > 0 && n > 0, "empty problem");
     require(n <= m, "more parameters than errors (adjust_base.cpp:864)");
     require(opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER ||
@@ -265,14 +269,97 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     cam_lpar_off[nC] = (int)cam_lpar.size();
 
-    // ---- observations in device order (by camera-frame) ----
-    std::vector<int> obs_cf(M);
-    for (int i = 0; i < M; ++i) obs_cf[i] = cf_id[{pr->obs_frame[i], obs_cam[i]}];
-    ref_of_dev.resize(M);
-    std::iota(ref_of_dev.begin(), ref_of_dev.end(), 0);
+    // ---- reduced-system layout: band + arrow when the camera-frame band is
+    // narrow (every C2/C4/C5-like scene), 64x64 tiles otherwise.  Computed from
+    // all observations so every shard sees the same structure. ----
+    std::vector<int> obs_cf(Mg);
+    for (int i = 0; i < Mg; ++i) obs_cf[i] = cf_id[{pr->obs_frame[i], obs_cam[i]}];
+    std::vector<int> obs_bnd_g(Mg);
+    for (int i = 0; i < Mg; ++i) obs_bnd_g[i] = pr->mkr_bnd[pr->obs_marker[i]];
+    bw = 0;
+    for (int cf = 0; cf < ncf; ++cf)
+        if (cf_pc[cf] > 0) bw = std::max(bw, cf_pc[cf] - 1);
+    {
+        std::vector<int> blo(nB, nCF), bhi(nB, -1);
+        for (int i = 0; i < Mg; ++i) {
+            const int b = obs_bnd_g[i], cf = obs_cf[i];
+            if (bnd_pb[b] == 0 || cf_pc[cf] == 0) continue;
+            blo[b] = std::min(blo[b], cf_roff[cf]);
+            bhi[b] = std::max(bhi[b], cf_roff[cf] + cf_pc[cf] - 1);
+        }
+        for (int b = 0; b < nB; ++b)
+            if (bhi[b] >= 0) bw = std::max(bw, bhi[b] - blo[b]);
+    }
+    band = nR > 0 && bw <= WBAND_MAX;
+
+    // ---- frame sharding: this shard's frames, camera-frame rows, observations
+    // (own = in its frames; halo = other observations of solved bundles seen in
+    // its frames, so those bundles' blocks are complete here) ----
+    std::vector<int> obs_own_g(Mg, 1), bnd_owner(nB, 0);
+    Ra = 0;
+    Rb = nCF;
+    Ra_all.assign(1, 0);
+    Rb_all.assign(1, nCF);
+    std::vector<int> local;  // global observation indices on this shard
+    std::vector<int> cf_own(ncf, 1);
+    if (nranks > 1) {
+        if (!band || bw > WBAND_PART)
+            throw Unsupported{"sharded solve needs a narrow camera-frame band (w <= 40)"};
+        std::vector<long long> per_frame(F + 1, 0);
+        for (int i = 0; i < Mg; ++i) per_frame[pr->obs_frame[i] + 1]++;
+        for (int f = 0; f < F; ++f) per_frame[f + 1] += per_frame[f];
+        std::vector<int> bf(nranks + 1, F);
+        bf[0] = 0;
+        for (int k = 1; k < nranks; ++k) {
+            const long long target = (long long)k * Mg / nranks;
+            int f = bf[k - 1];
+            while (f < F && per_frame[f] < target) ++f;
+            bf[k] = f;
+        }
+        // camera-frame rows of every shard's frame range (rows are frame-major)
+        std::vector<int> first_row(F + 1, nCF);
+        for (int cf = ncf - 1; cf >= 0; --cf) first_row[cf_frame[cf]] = cf_roff[cf];
+        for (int f = F - 1; f >= 0; --f) first_row[f] = std::min(first_row[f], first_row[f + 1]);
+        Ra_all.assign(nranks, 0);
+        Rb_all.assign(nranks, 0);
+        for (int k = 0; k < nranks; ++k) {
+            Ra_all[k] = first_row[bf[k]];
+            Rb_all[k] = first_row[bf[k + 1]];
+            if (Rb_all[k] - Ra_all[k] < 2 * bw + 8)
+                throw Unsupported{"too few camera-frame rows per shard"};
+        }
+        Ra = Ra_all[rank];
+        Rb = Rb_all[rank];
+        const int fa = bf[rank], fb = bf[rank + 1];
+        for (int cf = 0; cf < ncf; ++cf) cf_own[cf] = (cf_frame[cf] >= fa && cf_frame[cf] < fb);
+        std::vector<int> bnd_first(nB, F);
+        for (int i = 0; i < Mg; ++i) {
+            const int f = pr->obs_frame[i];
+            obs_own_g[i] = (f >= fa && f < fb) ? 1 : 0;
+            bnd_first[obs_bnd_g[i]] = std::min(bnd_first[obs_bnd_g[i]], f);
+        }
+        for (int b = 0; b < nB; ++b) {
+            int k = 0;
+            while (k + 1 < nranks && bf[k + 1] <= bnd_first[b]) ++k;
+            bnd_owner[b] = k;
+        }
+        std::vector<char> bnd_here(nB, 0);
+        for (int i = 0; i < Mg; ++i)
+            if (obs_own_g[i] && bnd_pb[obs_bnd_g[i]] > 0) bnd_here[obs_bnd_g[i]] = 1;
+        for (int i = 0; i < Mg; ++i)
+            if (obs_own_g[i] || bnd_here[obs_bnd_g[i]]) local.push_back(i);
+        M = (int)local.size();
+        m = 2 * M;
+    } else {
+        local.resize(Mg);
+        std::iota(local.begin(), local.end(), 0);
+    }
+
+    // ---- local observations in device order (by camera-frame) ----
+    ref_of_dev = local;
     std::stable_sort(ref_of_dev.begin(), ref_of_dev.end(),
                      [&](int a, int b) { return obs_cf[a] < obs_cf[b]; });
-    std::vector<int> d_cf(M), d_bnd(M), d_frame(M), d_cam(M);
+    std::vector<int> d_cf(M), d_bnd(M), d_frame(M), d_cam(M), d_own(M);
     std::vector<double> d_xy(2 * (size_t)M), d_sqrtw(M);
     std::vector<int> cf_obs_off(ncf + 1, 0);
     for (int i = 0; i < M; ++i) {
@@ -284,6 +371,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_xy[2 * i] = pr->obs_xy[2 * r];
         d_xy[2 * i + 1] = pr->obs_xy[2 * r + 1];
         d_sqrtw[i] = std::sqrt(pr->obs_weight[r]);
+        d_own[i] = obs_own_g[r];
         cf_obs_off[d_cf[i] + 1]++;
     }
     for (int cf = 0; cf < ncf; ++cf) cf_obs_off[cf + 1] += cf_obs_off[cf];
@@ -317,24 +405,6 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 break;
             }
     }
-
-    // ---- reduced-system layout: band + arrow when the camera-frame band is
-    // narrow (every C2/C4/C5-like scene), 64x64 tiles otherwise ----
-    bw = 0;
-    for (int cf = 0; cf < ncf; ++cf)
-        if (cf_pc[cf] > 0) bw = std::max(bw, cf_pc[cf] - 1);
-    for (int b = 0; b < nB; ++b) {
-        if (bnd_pb[b] == 0) continue;
-        int lo = nCF, hi = -1;
-        for (int q = bobs_off[b]; q < bobs_off[b + 1]; ++q) {
-            const int cf = d_cf[bobs[q]];
-            if (cf_pc[cf] == 0) continue;
-            lo = std::min(lo, cf_roff[cf]);
-            hi = std::max(hi, cf_roff[cf] + cf_pc[cf] - 1);
-        }
-        if (hi >= 0) bw = std::max(bw, hi - lo);
-    }
-    band = nR > 0 && bw <= WBAND_MAX;
 
     // ---- symbolic tile structure of the reduced system ----
     NT = (nR > 0 && !band) ? (nR + TILE - 1) / TILE : 0;
@@ -420,6 +490,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 npairs += kb * kb;
             }
         use_dest = nB_solved > 0 && nR > 0 && npairs <= (32ll << 20);
+        if (nranks > 1 && nB_solved > 0 && !use_dest)
+            throw Unsupported{"sharded solve: too many observation pairs per bundle"};
         if (use_dest) {
             struct PairRec {
                 int cfi, cfj, i, j;
@@ -433,7 +505,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                     if (cf_pc[cfi] == 0) continue;
                     for (int qj = bobs_off[b]; qj < bobs_off[b + 1]; ++qj) {
                         const int j = bobs[qj], cfj = d_cf[j];
-                        if (cf_pc[cfj] == 0 || cfi < cfj) continue;
+                        // destination rows must be this shard's camera-frames
+                        if (cf_pc[cfj] == 0 || cfi < cfj || !cf_own[cfi]) continue;
                         recs.push_back({cfi, cfj, i, j});
                     }
                 }
@@ -534,6 +607,23 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.p_off = upload(pr->param_offset, n);
     D.p_scale = upload(pr->param_scale, n);
     D.g_param = upload(g_param);
+    D.root = rank == 0 ? 1 : 0;
+    D.Ra = Ra;
+    D.Rb = Rb;
+    p_own.assign(n, 1);
+    if (nranks > 1) {
+        std::vector<int> bown(nB);
+        for (int b = 0; b < nB; ++b) bown[b] = bnd_owner[b] == rank ? 1 : 0;
+        for (int q = 0; q < n; ++q) {
+            if (p_class[q] == PC_CF) p_own[q] = cf_own[p_blk[q]];
+            else if (p_class[q] == PC_B) p_own[q] = bown[p_blk[q]];
+            else p_own[q] = rank == 0 ? 1 : 0;
+        }
+        D.obs_own = upload(d_own);
+        D.cf_own = upload(cf_own);
+        D.bnd_own = upload(bown);
+        d_p_own = upload(p_own);
+    }
     P = D;
 
     d_var_cf = upload(var_cf);
@@ -583,7 +673,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_Acg = dalloc<double>((size_t)ncf * PCMAX * NGMAX);
     d_Abb = dalloc<double>((size_t)nB * 9);
     d_Abg = dalloc<double>((size_t)nB * PBMAX * NGMAX);
-    d_Agg = dalloc<double>(NGMAX * NGMAX);
+    d_Agg = dalloc<double>(NGMAX * NGMAX + NGMAX);  // [Agg | g_G], see launch_ne
+    d_gather = dalloc<double>((size_t)2 * mg + Mg + n);
     d_glob_partial = dalloc<double>((size_t)((M + glob_chunk - 1) / glob_chunk) * (NGMAX * NGMAX + NGMAX));
     d_Lb = dalloc<double>((size_t)nB * 9);
     d_tb = dalloc<double>((size_t)nB * 3);
@@ -598,7 +689,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_scalar = dalloc<double>(8);
     d_fail = dalloc<int>(1);
     MMBA_HIP(hipMemsetAsync(d_Acg, 0, sizeof(double) * (size_t)ncf * PCMAX * NGMAX, s));
-    MMBA_HIP(hipMemsetAsync(d_Agg, 0, sizeof(double) * NGMAX * NGMAX, s));
+    MMBA_HIP(hipMemsetAsync(d_Agg, 0, sizeof(double) * (NGMAX * NGMAX + NGMAX), s));
     MMBA_HIP(hipMemsetAsync(d_Abg, 0, sizeof(double) * (size_t)nB * PBMAX * NGMAX, s));
     MMBA_HIP(hipMemsetAsync(d_Abb, 0, sizeof(double) * (size_t)nB * 9, s));
     MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
@@ -613,26 +704,45 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
 // mmba_band.hip) and the device buffers of the band factorisation.
 void Plan::setup_band(int Pforce) {
     const int nb = nR - nG, w = bw;
-    int P = 1;
-    if (Pforce > 0 && w <= WBAND_PART) {
-        P = std::max(1, std::min(Pforce, nb / (w + 1)));
-    } else if (w > 0 && w <= WBAND_PART) {
-        // balance the interior chains (nb/P rows) against the separator chain
-        // ((P-1) w rows at bandwidth 2w-1); measured on C4 (nb 2994, w 23):
-        // P = 1/4/8/12/16/24 -> 1.20/0.70/0.44/0.40/0.41/0.48 ms per factorisation
-        P = (int)std::lround(std::sqrt((double)nb / w));
-        if (const char *e = std::getenv("MMBA_BAND_PARTS")) P = std::atoi(e);
-        P = std::max(1, std::min(P, nb / (2 * w + 8)));
+    if (Ra_all.empty()) {
+        Ra_all.assign(1, 0);
+        Rb_all.assign(1, nb);
     }
+    // partitions per shard range [Ra_all[k], Rb_all[k]) (one range unsharded)
+    auto count_parts = [&](int len) {
+        int P = 1;
+        if (Pforce > 0 && w <= WBAND_PART) {
+            P = std::max(1, std::min(Pforce, len / (w + 1)));
+        } else if (w > 0 && w <= WBAND_PART) {
+            // balance the interior chains (len/P rows) against the separator
+            // chain ((P-1) w rows at bandwidth 2w-1); measured on C4 (nb 2994,
+            // w 23): P = 1/4/8/12/16/24 -> 1.20/0.70/0.44/0.40/0.41/0.48 ms
+            P = (int)std::lround(std::sqrt((double)len / w));
+            if (const char *e = std::getenv("MMBA_BAND_PARTS")) P = std::atoi(e);
+            P = std::max(1, std::min(P, len / (2 * w + 8)));
+        }
+        return P;
+    };
+    std::vector<std::pair<int, int>> spans;  // [s0, s1) of every partition
+    for (size_t k = 0; k < Ra_all.size(); ++k) {
+        const int a = Ra_all[k], len = Rb_all[k] - a;
+        const int Pk = count_parts(len);
+        if ((int)k == rank) bs.p_lo = (int)spans.size();
+        for (int p = 0; p < Pk; ++p)
+            spans.push_back({a + (int)((long long)p * len / Pk),
+                             a + (int)((long long)(p + 1) * len / Pk)});
+        if ((int)k == rank) bs.p_hi = (int)spans.size();
+    }
+    const int P = (int)spans.size();
     std::vector<BandPart> parts(P);
     long long aoff = 0;
     int zoff = 0, doff = 0, coff = 0;
     bs.max_arrow = 0;
     for (int p = 0; p < P; ++p) {
         BandPart &q = parts[p];
-        const int s0 = (int)((long long)p * nb / P), s1 = (int)((long long)(p + 1) * nb / P);
+        const int s0 = spans[p].first, s1 = spans[p].second;
         q.r0 = s0;
-        q.r1 = (p < P - 1) ? s1 - w : nb;
+        q.r1 = (p < P - 1) ? s1 - w : s1;
         q.nprev = p > 0 ? w : 0;
         q.nnext = p < P - 1 ? w : 0;
         q.sprev = p > 0 ? s0 - w : -1;
@@ -648,7 +758,21 @@ void Plan::setup_band(int Pforce) {
         doff += (q.r1 - q.r0 + 7) / 8;
         coff += q.na;
     }
+    // ||L^-1 v||^2 terms counted by this shard: its interior rows; the
+    // separator and global rows (replicated) on the root shard
+    {
+        std::vector<int> ym(nR, 0);
+        for (int p = bs.p_lo; p < bs.p_hi; ++p)
+            for (int r = parts[p].r0; r < parts[p].r1; ++r) ym[r] = 1;
+        if (rank == 0) {
+            for (int p = 0; p < P - 1; ++p)
+                for (int u = 0; u < w; ++u) ym[parts[p].snext + u] = 1;
+            for (int q = nb; q < nR; ++q) ym[q] = 1;
+        }
+        d_ymask = upload(ym);
+    }
     bs.P = P;
+    bs.comm = nranks > 1 ? comm : nullptr;
     bs.w = w;
     bs.nb = nb;
     bs.nG = nG;
@@ -663,9 +787,10 @@ void Plan::setup_band(int Pforce) {
         bs.zpool = dalloc<double>((size_t)zoff);
         bs.cpool = dalloc<double>((size_t)coff);
         const int nbT = (P - 1) * w;
-        bs.TBd = dalloc<double>((size_t)nbT * 2 * w);
-        bs.TGa = dalloc<double>((size_t)nG * nbT);
-        bs.TGd = dalloc<double>(NGMAX * NGMAX);
+        bs.tcount = (size_t)nbT * 2 * w + (size_t)nG * nbT + NGMAX * NGMAX;
+        bs.TBd = dalloc<double>(bs.tcount);
+        bs.TGa = bs.TBd + (size_t)nbT * 2 * w;
+        bs.TGd = bs.TGa + (size_t)nG * nbT;
         bs.TGdinv = dalloc<double>(NGMAX * NGMAX);
         bs.TDinv = dalloc<double>((size_t)((nbT + 7) / 8) * 64);
         BandPart t{};

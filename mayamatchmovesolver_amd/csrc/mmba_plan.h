@@ -34,16 +34,21 @@ struct Invalid {
     std::string what;
 };
 
-struct Comm;  // RCCL communicator (mmba_comm.cpp)
-
 struct Plan {
     mmba_context *ctx = nullptr;
     hipStream_t s = nullptr;
     mmba_options opt{};
     DevProblem P{};
 
-    // sizes
-    int n = 0, M = 0, m = 0, F = 0;
+    // sizes (M, m: observations / residuals on this shard; Mg, mg: all)
+    int n = 0, M = 0, m = 0, F = 0, Mg = 0, mg = 0;
+    // frame sharding (mmba_comm.cpp): shard rank of nranks owns reduced rows
+    // [Ra, Rb); every shard's range is known for the partition layout
+    int rank = 0, nranks = 1, Ra = 0, Rb = 0;
+    std::vector<int> Ra_all, Rb_all;
+    std::vector<int> p_own;        // parameters this shard owns (norms, gather)
+    int *d_p_own = nullptr;        // device copy (nullptr unsharded)
+    int *d_ymask = nullptr;        // rows of L^-1 v this shard counts
     int ncf = 0, nB = 0, nG = 0, nCF = 0, nR = 0, NT = 0, nRpad = 0, nvar = 0, nslots = 0;
     int nB_solved = 0;  // bundles with a B block
     bool rank_deficient = false;
@@ -108,6 +113,7 @@ struct Plan {
     double *d_rhs = nullptr, *d_yR = nullptr, *d_xR = nullptr, *d_wR = nullptr,
            *d_usq = nullptr;
     double *d_partial = nullptr, *d_scalar = nullptr;
+    double *d_gather = nullptr;  // outputs in reference order: f | eu | ed | x
     int *d_fail = nullptr;
     double *h_scalar = nullptr;  // pinned
     int *h_fail = nullptr;       // pinned
@@ -151,6 +157,8 @@ struct Plan {
 
     // LM building blocks
     double read_scalar(int slot = 0);
+    void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
+    double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
     double fun(const double *dx, double *df, double *eu, double *ed);
     void jac(const double *dx);
     bool solve_damped(double lam);
@@ -161,6 +169,7 @@ struct Plan {
     int dense_jacobian(const double *x, double *fjac);
     int measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
                 double *stats);
+    void download_params(const double *dx, double *x_out);
     void download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
                             double *f_out, double *eu_out, double *ed_out);
 };

@@ -71,6 +71,9 @@ class Context:
     def handle(self):
         return self._h
 
+    def synchronize(self):
+        check(lib().mmba_context_synchronize(self._h))
+
     def close(self):
         if self._h:
             lib().mmba_context_destroy(self._h)
@@ -83,18 +86,62 @@ class Context:
             pass
 
 
+class Comm:
+    """One shard's communicator for the frame-sharded solve (``mmba_comm``).
+
+    ``Comm.rccl(ctx, rank, nranks, uid)``: RCCL, one process per GPU; ``uid`` is
+    ``comm_unique_id()`` from one rank, broadcast by the caller.
+    ``Comm.local_group(n)``: n in-process shards (one host thread each)."""
+
+    def __init__(self, handle, rank, nranks):
+        self._h = handle
+        self.rank, self.nranks = rank, nranks
+
+    @classmethod
+    def rccl(cls, ctx: "Context", rank: int, nranks: int, unique_id: bytes) -> "Comm":
+        h = C.c_void_p()
+        check(lib().mmba_comm_create_rccl(ctx.handle, int(rank), int(nranks),
+                                          bytes(unique_id), C.byref(h)))
+        return cls(h, rank, nranks)
+
+    @classmethod
+    def local_group(cls, nranks: int) -> List["Comm"]:
+        hs = (C.c_void_p * nranks)()
+        check(lib().mmba_comm_create_local(int(nranks), hs))
+        return [cls(C.c_void_p(hs[r]), r, nranks) for r in range(nranks)]
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().mmba_comm_destroy(self._h)
+            self._h = C.c_void_p()
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    check(lib().mmba_comm_unique_id(buf))
+    return buf.raw
+
+
 class Solver:
-    """A problem uploaded to one MI355X (``mmba_plan``)."""
+    """A problem uploaded to one MI355X (``mmba_plan``); with ``comm``, this
+    shard of a frame-sharded plan (every shard passes the same problem)."""
 
     def __init__(self, problem: Problem, options, context: Optional[Context] = None,
-                 device: int = 0):
+                 device: int = 0, comm: Optional[Comm] = None):
         self.problem = problem
         self.options = options
         self.ctx = context or Context(device)
+        self.comm = comm
         self._prob_c, self._keep = problem.to_ctypes()
         self._h = C.c_void_p()
-        check(lib().mmba_plan_create(self.ctx.handle, C.byref(self._prob_c),
-                                     C.byref(self.options), C.byref(self._h)))
+        check(lib().mmba_plan_create_sharded(self.ctx.handle, C.byref(self._prob_c),
+                                             C.byref(self.options),
+                                             comm.handle if comm is not None else None,
+                                             C.byref(self._h)))
 
     def close(self):
         if self._h:
@@ -115,9 +162,6 @@ class Solver:
         st = abi.MmbaKernelStats()
         check(lib().mmba_plan_kernel_stats(self._h, 1, C.byref(st)))
         return st.as_dict()
-
-    def set_comm(self, rank: int, nranks: int, unique_id: bytes):
-        check(lib().mmba_plan_set_comm(self._h, rank, nranks, unique_id))
 
     def measure(self, x=None):
         p = self.problem

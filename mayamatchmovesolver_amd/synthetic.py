@@ -171,12 +171,16 @@ CONFIG_NAMES = {
 
 
 def make_config(index: int, frames: int | None = None, scale: float = 1.0,
-                scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH) -> Problem:
+                scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH, window: int = 4,
+                depth=(20.0, 200.0)) -> Problem:
     """Concrete synthetic input for BASELINE.json ``configs[index]``.
 
     ``frames`` / ``scale`` shrink a configuration (frame-window subsets and
     fewer markers) for parity tests and the bounded CPU-baseline sample;
-    the defaults give the full configuration.
+    the defaults give the full configuration.  ``window`` (track length in
+    frames) and ``depth`` (bundle depth range) apply to configs[3] only: the
+    defaults are the C4 spec; longer tracks / nearer bundles give the
+    well-conditioned variants the sharded-solve tests compare x on.
     """
     rng = np.random.Generator(np.random.PCG64(20241008 + index))
     if index == 0:
@@ -188,7 +192,8 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                           K=int(50000 * scale), window=20, per_cam_markers=True)
     if index == 3:
         return _config_ba(rng, index, n_cams=1, F=frames or 500, B=int(50000 * scale),
-                          K=int(50000 * scale), window=4, per_cam_markers=False)
+                          K=int(50000 * scale), window=window, per_cam_markers=False,
+                          depth=depth)
     if index == 4:
         return _config_c5(rng, frames or 240, scale)
     raise KeyError(index)
@@ -340,7 +345,7 @@ def _config_c2(rng, F, scale):
                          meta={"name": CONFIG_NAMES[1]})
 
 
-def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers):
+def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0, 200.0)):
     """Full BA: animated cameras (t, r per frame) + static bundles, gauge-locked.
 
     C3 (``per_cam_markers``): a 10-camera rig (2 units apart) moving slowly,
@@ -376,7 +381,7 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers):
         # bundle j placed relative to the camera at the middle of its window
         mid = np.minimum(start + length // 2, F - 1)
         P = np.empty((B, 3))
-        depth = rng.uniform(20.0, 200.0, size=B)
+        depth = rng.uniform(depth[0], depth[1], size=B)
         u = rng.uniform(-0.35, 0.35, size=B)
         v = rng.uniform(-0.22, 0.22, size=B)
         owner = np.full(B, -1)

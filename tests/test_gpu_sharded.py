@@ -1,0 +1,105 @@
+"""Frame-sharded solve on one MI355X: N shards in one process
+(mmba_comm_create_local, one host thread and one stream per shard) run the same
+code path as the one-process-per-GPU RCCL run.  Bar: every shard returns the
+same x and result, and they match the CPU oracle like the unsharded solve
+(1e-6 relative on x and on every ||f|| of the trace)."""
+import threading
+
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import synthetic as S
+from mayamatchmovesolver_amd.solver import Comm, Context, Solver
+
+pytestmark = pytest.mark.gpu
+
+
+def run_sharded(prob, opt, n):
+    comms = Comm.local_group(n)
+    ctxs = [Context(0) for _ in range(n)]
+    outs, errs = [None] * n, [None] * n
+
+    def work(r):
+        try:
+            s = Solver(prob, opt, context=ctxs[r], comm=comms[r])
+            try:
+                outs[r] = s.solve()
+            finally:
+                s.close()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs[r] = e
+
+    ths = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(n)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ths), "sharded solve hung"
+    for c in comms:
+        c.close()
+    for c in ctxs:
+        c.close()
+    assert errs == [None] * n, errs
+    return outs
+
+
+# C4-type scenes with 4-frame tracks at depth 20-200 are too weakly determined
+# at test sizes for an x comparison (the unsharded solve differs from the
+# oracle by 1e-4 there too; only ||f|| is pinned): the Schur cases use 6-frame
+# tracks at depth 4-10.  Changing only the band partition count moves x by up
+# to 5e-7 on the first case, so the sharded run is compared at the same 1e-6.
+WC = dict(window=6, depth=(4.0, 10.0))
+CASES = [
+    (3, dict(frames=40, scale=0.004, **WC), 2),   # bundle-Schur BA, 2 shards
+    (1, dict(frames=24, scale=0.05), 2),          # C2 subset: pose + focal, no Schur
+    (1, dict(frames=36, scale=0.05), 3),          # C2 subset, 3 shards (a middle shard)
+    (4, dict(frames=32, scale=0.05), 2),          # C5 subset: lens globals (arrow rows)
+]
+
+
+def check_shards_agree(outs):
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o.x, outs[0].x)
+        np.testing.assert_array_equal(o.fvec, outs[0].fvec)
+        assert o.result["iterations"] == outs[0].result["iterations"]
+
+
+@pytest.mark.parametrize("idx,kw,nshards", CASES)
+def test_sharded_matches_oracle(idx, kw, nshards, oracle):
+    prob = S.make_config(idx, **kw)
+    opt = S.config_options(prob)
+    xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt)
+    outs = run_sharded(prob, opt, nshards)
+    check_shards_agree(outs)
+    g = outs[0]
+    assert g.result["reason_number"] == rr.reason_number, (g.result, rr.as_dict())
+    assert g.result["outer_iterations"] == rr.outer_iterations
+    np.testing.assert_allclose(g.fnorm_trace, trr, rtol=1e-6, atol=1e-9 * trr[0])
+    assert np.max(np.abs(g.x - xr) / np.maximum(np.abs(xr), 1e-3)) <= 1e-6
+    assert abs(g.result["error_final"] - rr.error_final) <= 1e-6 * rr.error_final
+    # per-residual values move with the roundoff-determined last digits of x
+    # (x at 8e-7 -> residuals at 1e-5 px on the Schur case): checked loosely
+    np.testing.assert_allclose(g.fvec, fr, rtol=0, atol=1e-4 * np.max(np.abs(fr)))
+    np.testing.assert_allclose(g.err_dist, edr, rtol=0, atol=1e-4 * np.max(np.abs(edr)))
+
+
+def test_sharded_ba_three_shards_structure(gpu_ctx):
+    """3 shards (one with separators on both sides) on a bundle-Schur scene,
+    against the unsharded GPU solve.  This scene is not conditioned well
+    enough for a 1e-6 comparison (a rejected trial point moves by 1.4e-6), so
+    the check is structural: same reason and counts, trace within 1e-5, x
+    within 1e-4 (decomposition errors show up at 1e-2)."""
+    prob = S.make_config(3, frames=54, scale=0.006, **WC)
+    opt = S.config_options(prob)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        ref = s.solve()
+    finally:
+        s.close()
+    outs = run_sharded(prob, opt, 3)
+    check_shards_agree(outs)
+    g = outs[0]
+    for k in ("reason_number", "iterations", "outer_iterations", "function_evals"):
+        assert g.result[k] == ref.result[k], k
+    np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-5)
+    assert np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3)) <= 1e-4

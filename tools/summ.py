@@ -6,8 +6,9 @@ for f in sorted(glob.glob(d + "/bench_*.json")):
         j = json.load(open(f))
     except Exception as e:
         print(f, "unreadable", e); continue
-    print("%-38s val=%.1f %s ms/step=%.2f it=%d rms=%.4f frac=%.4f chol_ms=%.3f split=%s" % (
-        j["config"]["workload"], j["value"], j["unit"], j["ms_per_step"], j["lm_iterations_per_solve"],
+    print("%-38s val=%.4g %s lm/s=%.1f ms/step=%.2f it=%d rms=%.4f frac=%.4f chol_ms=%.3f split=%s" % (
+        j["config"]["workload"], j["value"], j["unit"], j.get("lm_iterations_per_s", 0),
+        j["ms_per_step"], j["lm_iterations_per_solve"],
         j["final_rms_px"], j["roofline"]["frac"], j["reduced_cholesky"]["avg_ms"],
         {k: round(v * 1e3, 2) for k, v in j["time_split_s"].items()}))
 for f in glob.glob(d + "/prof/*kernel_stats.csv"):
