@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/.
+
+Each fixture ``<case>.npz`` holds one complete solver input (the flat
+``mmba_problem`` arrays + the options, field for field) and the CPU oracle's
+outputs for it (oracle/refcpu.c: the restatement of solveFrames ->
+cminpack lmder/lmdif -> solveFunc/measureErrors): final internal
+parameter vector, fvec, errorList, errorDistanceList, the per-evaluation
+||f|| trace and the SolverResult counters.
+
+The oracle itself is pinned against scipy's MINPACK and the reference's own
+known answers (tests/test_oracle_*.py); these fixtures freeze its outputs so
+that (a) the GPU parity tests have inputs/outputs that do not depend on the
+oracle being rebuilt on the GPU box and (b) any later change to the oracle or
+to the synthetic generator shows up as a fixture diff.
+
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from mayamatchmovesolver_amd import abi, make_options, synthetic as S  # noqa: E402
+
+OPT_FIELDS = ["solver_type", "iter_max", "tau", "eps1", "eps2", "eps3", "delta",
+              "auto_diff_type", "auto_param_scale", "scene_graph_mode", "image_width",
+              "accept_only_better"]
+RES_FIELDS = ["success", "reason_number", "iterations", "function_evals", "jacobian_evals",
+              "outer_iterations", "error_final", "error_avg", "error_min", "error_max",
+              "error_rms"]
+
+
+def cases():
+    """(name, problem, options) of every fixture."""
+    out = []
+    for name in ("test1", "test3", "minmax_both", "weight_ratio"):
+        for mode, tag in ((abi.SCENE_GRAPH_MODE_MAYA_DAG, "dag"),
+                          (abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH, "mmsg")):
+            opt = make_options(scene_graph_mode=mode,
+                               iterations=1000 if name == "test1" else 100,
+                               delta=1e-5 if name == "test3" else 1e-4)
+            out.append(("known_%s_%s" % (name, tag), S.known_scene(name), opt))
+    subsets = [
+        ("c1_full_lmdif", 0, dict()),
+        ("c2_f12", 1, dict(frames=12, scale=0.05)),
+        ("c3_f8", 2, dict(frames=8, scale=0.002)),
+        ("c4_f8", 3, dict(frames=8, scale=0.001)),
+        ("c4_f16", 3, dict(frames=16, scale=0.002)),
+        ("c5_f8_lens", 4, dict(frames=8, scale=0.05)),
+    ]
+    for name, idx, kw in subsets:
+        p = S.make_config(idx, **kw)
+        out.append((name, p, S.config_options(p)))
+    return out
+
+
+def options_from_npz(d):
+    o = abi.MmbaOptions()
+    for f in OPT_FIELDS:
+        t = type(getattr(o, f))
+        setattr(o, f, t(d["opt_" + f]))
+    return o
+
+
+def load(name):
+    from mayamatchmovesolver_amd.problem import Problem
+    d = dict(np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False))
+    prob = Problem.from_npz_dict(d)
+    return prob, options_from_npz(d), d
+
+
+def fixture_names():
+    return sorted(f[:-4] for f in os.listdir(HERE) if f.endswith(".npz"))
+
+
+def main():
+    from oracle import refcpu as R
+    for name, prob, opt in cases():
+        x, fvec, eu, ed, res, tr = R.solve(prob, opt)
+        d = prob.to_npz_dict()
+        for f in OPT_FIELDS:
+            d["opt_" + f] = np.array(getattr(opt, f))
+        rd = res.as_dict()
+        for f in RES_FIELDS:
+            d["res_" + f] = np.array(rd[f])
+        d.update(exp_x=x, exp_fvec=fvec, exp_err_user=eu, exp_err_dist=ed, exp_trace=tr)
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **d)
+        print("%-24s n=%6d m=%7d iters=%3d reason=%d  %7.1f KB" % (
+            name, prob.num_params, prob.num_residuals, res.outer_iterations,
+            res.reason_number, os.path.getsize(path) / 1024))
+
+
+if __name__ == "__main__":
+    main()
