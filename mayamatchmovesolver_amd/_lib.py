@@ -13,7 +13,7 @@ from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(_HERE, "csrc")
-LIB_PATH = os.path.join(CSRC, "libmmba.so")
+LIB_PATH = os.environ.get("MMBA_LIB", os.path.join(CSRC, "libmmba.so"))  # override: diagnostics only
 _lib = None
 
 

@@ -564,6 +564,10 @@ __global__ void k_band_tscatter(const double *__restrict__ vT, int w, int nb, in
 static inline int nblk_(long n, int bs) { return (int)((n + bs - 1) / bs); }
 
 void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe) {
+    if (B.use_bcr) {
+        bcr_factor(s, B, fail, probe);
+        return;
+    }
     if (B.P == 1) {
         if (B.w <= WBAND_PART)
             k_band_factor<8, 64, WBAND_PART, NGMAX, true><<<1, 256, 0, s>>>(
@@ -594,6 +598,10 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
 }
 
 void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y) {
+    if (B.use_bcr) {
+        bcr_forward(s, B, r, y);
+        return;
+    }
     if (B.P == 1) {
         if (B.w <= WBAND_PART)
             k_band_fwd<8, 64, true><<<1, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.Ga, B.Dinv,
@@ -617,6 +625,10 @@ void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y
 }
 
 void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *x) {
+    if (B.use_bcr) {
+        bcr_backward(s, B, y, x);
+        return;
+    }
     if (B.P == 1) {
         if (B.w <= WBAND_PART)
             k_band_bwd<8, 64, true><<<1, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts, B.Ga, B.Dinv,

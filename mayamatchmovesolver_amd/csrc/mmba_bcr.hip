@@ -1,0 +1,592 @@
+// mmba_bcr.hip -- block cyclic reduction (BCR) Cholesky of the reduced
+// camera system for CDNA4 (gfx950), fp64.
+//
+// The band + arrow system of mmba_band.hip (half bandwidth w <= 32, nG <= 16
+// dense arrow rows) is viewed as block tridiagonal with K x K blocks, K = the
+// smallest multiple of 8 >= w, plus the arrow:
+//
+//   block b: diagonal D_b, coupling L_b = S[b, b-1] (K x K), arrow G_b (nG x K).
+//
+// A sequential band Cholesky is a chain of nb columns.  BCR factors the same
+// matrix in the odd-even (nested-dissection) order: at level l (stride s =
+// 2^l) every odd active block o is eliminated at once,
+//
+//   C_o C_o^T = D_o,  U_o = C_o^-1 L_o,  V_o = C_o^-1 L_{o+s}^T,  Y_o = C_o^-1 G_o^T,
+//   D_{o-s} -= U_o^T U_o,  D_{o+s} -= V_o^T V_o,  L'_{o+s} = -V_o^T U_o,
+//   G_{o-s} -= Y_o^T U_o,  G_{o+s} -= Y_o^T V_o,  D_G -= Y_o^T Y_o,
+//
+// which is exactly the Cholesky factor of the permuted matrix (its column o
+// holds C_o, U_o^T, V_o^T, Y_o^T), so ||L^-1 r|| and the solution are those of
+// any Cholesky of S.  The chain shrinks from nb columns to log2(nb / K) levels
+// of K columns each; C4 (nb = 2,994, w = 23): 125 blocks of 24, 7 levels.
+//
+// One launch per level.  Workgroup per even active block e ("even owner"):
+// waves 0 / 1 factor the two odd neighbours o1 = e - s / o2 = e + s
+// concurrently (lane = row, pivots and columns broadcast through LDS), every
+// wave then forms the products with the explicit inverses C^-1, and the
+// workgroup updates D_e, G_e and the new coupling of e in place.  o2 is owned
+// by e (its C^-1, U, V, Y are stored for the solves and its Y^T Y for the
+// corner); o1 is recomputed bit-identically by e and by its owner e - 2s, so a
+// level needs no second launch.  L is double-buffered across levels (the new
+// coupling of e + 2s is written while e still reads the old one).  The last
+// active block and the arrow corner are factored densely by one workgroup.
+//
+// Solves: forward, one launch per level (workgroup per even block, both odd
+// neighbours' y = C^-1 r by matrix-vector products, r_e updated in place in a
+// work copy); backward, one launch per level (workgroup per odd block).
+#include "mmba_kernels.h"
+#include "mmba_plan.h"
+
+namespace mmba {
+
+// 1/sqrt(d): v_rsq_f64 plus two Newton steps (full fp64 precision).
+__device__ __forceinline__ double bcr_rsq(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+__device__ __forceinline__ double *bcr_blk(double *base, int b, int K) {
+    return base + (size_t)b * K * K;
+}
+
+// ---------------------------------------------------------------------------
+// Band rows -> blocks.  Workgroup per block b.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ void __launch_bounds__(256) k_bcr_load(BcrDev B) {
+    const int b = blockIdx.x;
+    const int W1 = B.w + 1;
+    double *D = bcr_blk(B.Dk, b, K), *L = bcr_blk(B.Lk0, b, K);
+    for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
+        const int i = e / K, c = e % K;
+        const int R = b * K + i;
+        double dv = 0., lv = 0.;
+        if (R < B.nb) {
+            const int C = b * K + c;
+            if (c <= i && R - C <= B.w) dv = B.Bd[(size_t)R * W1 + (C - R + B.w)];
+            const int Cp = (b - 1) * K + c;  // previous block's column
+            if (b > 0 && R - Cp <= B.w) lv = B.Bd[(size_t)R * W1 + (Cp - R + B.w)];
+        } else if (i == c) {
+            dv = 1.;  // padding rows: identity, uncoupled
+        }
+        D[e] = dv;
+        L[e] = lv;
+    }
+    for (int e = threadIdx.x; e < B.nG * K; e += blockDim.x) {
+        const int q = e / K, c = e % K, C = b * K + c;
+        B.Gk[((size_t)b * B.nG + q) * K + c] = C < B.nb ? B.Ga[(size_t)q * B.nb + C] : 0.;
+    }
+}
+
+// Order this wave's LDS accesses (a wave's DS instructions execute in issue
+// order; the fence keeps the compiler from reordering them).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Cholesky + explicit inverse of one K x K block by ONE wave (no workgroup
+// barriers): lane r < K holds row r in registers; the pivot is broadcast with
+// v_readlane, column j through LDS.  The inverse is formed column-oriented
+// (lane = column of the identity, axpy updates: K short dependent steps).
+// M: lower, row stride KS -> C.  Ci: C^-1, lower.  col: 64 doubles, idg: K.
+template <int K, int KS>
+__device__ __forceinline__ void bcr_chol_inv_wave(double *M, double *Ci, double *col, int &bad) {
+    const int lane = threadIdx.x & 63;
+    double a[K], rsv[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) a[c] = (lane < K && c <= lane) ? M[lane * KS + c] : 0.;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const long long dv = __double_as_longlong(a[j]);
+        const int lo = __builtin_amdgcn_readlane((int)(dv & 0xffffffffll), j);
+        const int hi = __builtin_amdgcn_readlane((int)(dv >> 32), j);
+        double d = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+        if (!(d > 0.) || !isfinite(d)) {
+            bad = 1;
+            d = 1.;
+        }
+        const double rs = bcr_rsq(d);
+        rsv[j] = rs;  // wave-uniform: 1 / C_jj
+        const double l = (lane > j) ? a[j] * rs : 0.;
+        a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+        if (lane < K) col[lane] = l;
+        wave_lds_sync();
+        // rank-1 update of this lane's row; entries right of the diagonal
+        // (c > lane) are dead and updated unconditionally (no exec masking)
+#pragma unroll
+        for (int c = j + 1; c < K; ++c) a[c] = fma(-l, col[c], a[c]);
+        wave_lds_sync();
+    }
+    if (lane < K)
+#pragma unroll
+        for (int c = 0; c < K; ++c) M[lane * KS + c] = (c <= lane) ? a[c] : 0.;
+    wave_lds_sync();
+    // inverse, column-oriented: lane = column cc of the identity
+    if (lane < K) {
+        const int cc = lane;
+        double x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = (i == cc) ? 1. : 0.;
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+            x[t] *= rsv[t];  // zero above the diagonal stays zero
+#pragma unroll
+            for (int i = t + 1; i < K; ++i) x[i] = fma(-M[i * KS + t], x[t], x[i]);
+            wave_lds_sync();  // keeps the column loads of step t from being hoisted
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) Ci[i * KS + cc] = x[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One elimination level.  blockIdx.x = even index / 2 (t = 2 blockIdx.x).
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
+                                                   int *fail, long long *probe) {
+    constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
+    constexpr int CG = K / 4;     // columns per product task
+    constexpr int GS = NGMAX;     // row stride of the K x nG arrays
+    __shared__ double sD[2][K * KS], sCi[2][K * KS];
+    // B operands, row-contiguous: Lo1, Le^T, Lo2, Ln^T
+    __shared__ double sB[4][K * KS];
+    __shared__ double sP[4][K * KS];  // U1, V1, U2, V2
+    __shared__ double sGT[2][K * GS], sY[2][K * GS];
+    __shared__ double col[2][64];
+    __shared__ double sDe[K * KS], sGe[NGMAX * K];
+    __shared__ int bad_s;
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const int t = 2 * blockIdx.x;
+    const int e = t * s;
+    const bool h1 = t >= 2;                 // o1 = e - s exists (and so does its prev e - 2s)
+    const bool h2 = t + 1 < nact;           // o2 = e + s
+    const bool hn = t + 2 < nact;           // e + 2s (o2's next)
+    const int o1 = e - s, o2 = e + s, en = e + 2 * s;
+    const int nG = B.nG;
+    const double *Lin = ping ? B.Lk1 : B.Lk0;
+    double *Lout = ping ? B.Lk0 : B.Lk1;
+    if (tid == 0) bad_s = 0;
+    // probe (diagnostic, MMBA_PROBE=1): thread 0 of workgroup 0 accumulates
+    // clock64 cycles per phase; never read by the solver.
+    const bool prb = probe && blockIdx.x == 0 && tid == 0;
+    long long tprev = prb ? (long long)clock64() : 0;
+    auto stamp = [&](int ph) {
+        if (prb) {
+            const long long tn = (long long)clock64();
+            atomicAdd((unsigned long long *)&probe[ph], (unsigned long long)(tn - tprev));
+            tprev = tn;
+        }
+    };
+    // stage every operand (zeros where a neighbour does not exist); the loads
+    // of one pass are issued before any LDS store
+    for (int q = tid; q < K * K; q += blockDim.x) {
+        const int i = q / K, c = q % K, x = i * KS + c, xt = c * KS + i;
+        const double d0 = h1 ? bcr_blk(B.Dk, o1, K)[q] : 0.;
+        const double d1 = h2 ? bcr_blk(B.Dk, o2, K)[q] : 0.;
+        const double b0 = h1 ? bcr_blk((double *)Lin, o1, K)[q] : 0.;
+        const double b1 = h1 ? bcr_blk((double *)Lin, e, K)[q] : 0.;
+        const double b2 = h2 ? bcr_blk((double *)Lin, o2, K)[q] : 0.;
+        const double b3 = hn ? bcr_blk((double *)Lin, en, K)[q] : 0.;
+        sD[0][x] = d0;
+        sD[1][x] = d1;
+        sCi[0][x] = 0.;  // stays zero for a missing neighbour
+        sCi[1][x] = 0.;
+        sB[0][x] = b0;
+        sB[1][xt] = b1;  // Le^T
+        sB[2][x] = b2;
+        sB[3][xt] = b3;  // Ln^T
+        sDe[x] = bcr_blk(B.Dk, e, K)[q];
+    }
+    for (int q = tid; q < nG * K; q += blockDim.x) sGe[q] = B.Gk[(size_t)e * nG * K + q];
+    for (int q = tid; q < 2 * K * GS; q += blockDim.x) {
+        const int which = q / (K * GS), r = q % (K * GS), u = r / GS, qq = r % GS;
+        const int o = which ? o2 : o1;
+        const bool h = which ? h2 : h1;
+        sGT[which][r] = (h && qq < nG) ? B.Gk[((size_t)o * nG + qq) * K + u] : 0.;
+    }
+    __syncthreads();
+    stamp(0);
+    int bad = 0;
+    if (wv == 0 && h1) bcr_chol_inv_wave<K, KS>(sD[0], sCi[0], col[0], bad);
+    if (wv == 1 && h2) bcr_chol_inv_wave<K, KS>(sD[1], sCi[1], col[1], bad);
+    if (bad) atomicOr(&bad_s, 1);
+    __syncthreads();
+    stamp(1);
+    // products P_m = Ci * B_m (U1 = Ci1 Lo1, V1 = Ci1 Le^T, U2 = Ci2 Lo2,
+    // V2 = Ci2 Ln^T) and Y_w = Ci_w G_w^T; a task is one row x CG columns
+    // (x 4 arrow columns for Y), Ci lower so u <= i
+    const int ngg = (nG + 3) / 4;
+    for (int q = tid; q < 4 * K * 4 + 2 * K * ngg; q += blockDim.x) {
+        if (q < 16 * K) {
+            const int m = q / (4 * K), r = q % (4 * K), i = r / 4, c0 = (r % 4) * CG;
+            const double *Ci = sCi[m >> 1];
+            const double *Bm = sB[m];
+            double acc[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) acc[c] = 0.;
+#pragma unroll 2
+            for (int u = 0; u <= i; ++u) {
+                const double av = Ci[i * KS + u];
+#pragma unroll
+                for (int c = 0; c < CG; ++c) acc[c] = fma(av, Bm[u * KS + c0 + c], acc[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < CG; ++c) sP[m][i * KS + c0 + c] = acc[c];
+        } else {
+            const int r = q - 16 * K, w = r / (K * ngg), r2 = r % (K * ngg);
+            const int i = r2 / ngg, c0 = (r2 % ngg) * 4;
+            const double *Ci = sCi[w];
+            double acc[4] = {0., 0., 0., 0.};
+#pragma unroll 2
+            for (int u = 0; u <= i; ++u) {
+                const double av = Ci[i * KS + u];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[c] = fma(av, sGT[w][u * GS + c0 + c], acc[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sY[w][i * GS + c0 + c] = acc[c];
+        }
+    }
+    __syncthreads();
+    stamp(2);
+    // updates of the even block: D_e -= V1^T V1 + U2^T U2 (lower), new
+    // coupling -V1^T U1, G_e -= Y1^T V1 + Y2^T U2; stored factor columns of o2
+    const double *U1 = sP[0], *V1 = sP[1], *U2 = sP[2], *V2 = sP[3];
+    double *De = bcr_blk(B.Dk, e, K);
+    for (int q = tid; q < 2 * 4 * K; q += blockDim.x) {
+        const int m = q / (4 * K), r = q % (4 * K), i = r / 4, c0 = (r % 4) * CG;
+        if (m == 0) {
+            if (c0 > i) continue;
+            double acc[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) acc[c] = 0.;
+#pragma unroll 2
+            for (int u = 0; u < K; ++u) {
+                const double v = V1[u * KS + i], w2 = U2[u * KS + i];
+#pragma unroll
+                for (int c = 0; c < CG; ++c)
+                    acc[c] = fma(v, V1[u * KS + c0 + c], fma(w2, U2[u * KS + c0 + c], acc[c]));
+            }
+#pragma unroll
+            for (int c = 0; c < CG; ++c)
+                if (c0 + c <= i) De[i * K + c0 + c] = sDe[i * KS + c0 + c] - acc[c];
+        } else if (h1) {
+            double acc[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) acc[c] = 0.;
+#pragma unroll 2
+            for (int u = 0; u < K; ++u) {
+                const double v = V1[u * KS + i];
+#pragma unroll
+                for (int c = 0; c < CG; ++c) acc[c] = fma(v, U1[u * KS + c0 + c], acc[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < CG; ++c) bcr_blk(Lout, e, K)[i * K + c0 + c] = -acc[c];
+        }
+    }
+    for (int q = tid; q < nG * 4; q += blockDim.x) {
+        const int qq = q / 4, c0 = (q % 4) * CG;
+        double acc[CG];
+#pragma unroll
+        for (int c = 0; c < CG; ++c) acc[c] = 0.;
+#pragma unroll 2
+        for (int u = 0; u < K; ++u) {
+            const double y1 = sY[0][u * GS + qq], y2 = sY[1][u * GS + qq];
+#pragma unroll
+            for (int c = 0; c < CG; ++c)
+                acc[c] = fma(y1, V1[u * KS + c0 + c], fma(y2, U2[u * KS + c0 + c], acc[c]));
+        }
+#pragma unroll
+        for (int c = 0; c < CG; ++c)
+            B.Gk[((size_t)e * nG + qq) * K + c0 + c] = sGe[qq * K + c0 + c] - acc[c];
+    }
+    if (h2) {
+        for (int q = tid; q < K * K; q += blockDim.x) {
+            const int i = q / K, c = q % K;
+            bcr_blk(B.FC, o2, K)[q] = sCi[1][i * KS + c];
+            bcr_blk(B.FU, o2, K)[q] = U2[i * KS + c];
+            bcr_blk(B.FV, o2, K)[q] = V2[i * KS + c];
+        }
+        for (int q = tid; q < K * nG; q += blockDim.x) {
+            const int i = q / nG, qq = q % nG;
+            B.FY[(size_t)o2 * K * nG + q] = sY[1][i * GS + qq];
+        }
+        for (int q = tid; q < nG * nG; q += blockDim.x) {
+            const int a = q / nG, c = q % nG;
+            double acc = 0.;
+            for (int u = 0; u < K; ++u) acc = fma(sY[1][u * GS + a], sY[1][u * GS + c], acc);
+            B.Zc[(size_t)o2 * nG * nG + q] = acc;
+        }
+    }
+    stamp(3);
+    if (tid == 0 && bad_s) atomicOr(fail, 1);  // bad_s settled at the product barrier
+}
+
+// ---------------------------------------------------------------------------
+// Root: block 0 and the arrow corner, dense, one wave.  N = K + nG rounded up
+// to 8 (identity padding).  T = [D_0, G_0^T; G_0, Gd - sum_o Y_o^T Y_o] =
+// Ct Ct^T, FT = Ct^-1 (lower, N x N).
+// ---------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail) {
+    constexpr int NS = N + 2;
+    __shared__ double T[N * NS], Ti[N * NS], col[64];
+    const int lane = threadIdx.x;
+    const int K = B.K, nG = B.nG, n0 = K + nG;
+    const double *D0 = B.Dk;
+    for (int q = lane; q < N * N; q += 64) {
+        const int i = q / N, c = q % N;
+        double v = 0.;
+        if (i < K && c < K) {
+            v = c <= i ? D0[i * K + c] : 0.;
+        } else if (i >= K && i < n0 && c < K) {
+            v = B.Gk[(i - K) * K + c];  // block 0 arrow
+        } else if (i >= K && i < n0 && c >= K && c <= i) {
+            const int a = i - K, b = c - K;
+            v = B.Gd[a * NGMAX + b];
+            for (int o = 1; o < B.nblk; ++o) v -= B.Zc[(size_t)o * nG * nG + a * nG + b];
+        } else if (i == c) {
+            v = 1.;  // padding beyond n0
+        }
+        T[i * NS + c] = v;
+    }
+    __syncthreads();
+    int bad = 0;
+    bcr_chol_inv_wave<N, NS>(T, Ti, col, bad);
+    wave_lds_sync();
+    for (int q = lane; q < N * N; q += 64) B.FT[q] = Ti[(q / N) * NS + q % N];
+    if (bad && lane == 0) atomicOr(fail, 1);
+}
+
+// ---------------------------------------------------------------------------
+// Solves.  Vectors are in reduced-system order (nb band rows, then nG global
+// rows); block rows at or beyond nb are padding (value 0, never stored).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double bcr_get(const double *v, int R, int nb) {
+    return R < nb ? v[R] : 0.;
+}
+
+// Forward level: workgroup (64 lanes) per even block e; lanes 0..K-1 handle
+// o1 = e - s, lanes 32..32+K-1 handle o2 = e + s.  Every factor entry a lane
+// needs is loaded at entry (independent of r), so the only dependent global
+// load is r itself.
+template <int K>
+__global__ void __launch_bounds__(64) k_bcr_fwd(BcrDev B, int s, int nact, double *rw,
+                                                double *y) {
+    __shared__ double sr[2][K], sy[2][K], sp[2][K];
+    const int lane = threadIdx.x, h = lane >> 5, i = lane & 31;
+    const int t = 2 * blockIdx.x, e = t * s;
+    const bool h1 = t >= 2, h2 = t + 1 < nact;
+    const int o = h ? e + s : e - s;
+    const bool act = (h ? h2 : h1) && i < K;
+    const int nb = B.nb, nG = B.nG;
+    double ci[K], cv[K];  // row i of C_o^-1; column i of V_o1 (h = 0) / U_o2 (h = 1)
+    if (act) {
+        const double *Ci = bcr_blk(B.FC, o, K);
+        const double *Vc = bcr_blk(h ? B.FU : B.FV, o, K);
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            ci[u] = u <= i ? Ci[i * K + u] : 0.;
+            cv[u] = Vc[u * K + i];
+        }
+        sr[h][i] = bcr_get(rw, o * K + i, nb);
+    }
+    __syncthreads();
+    double yv = 0.;
+    if (act) {
+#pragma unroll
+        for (int u = 0; u < K; ++u) yv = fma(ci[u], sr[h][u], yv);
+        sy[h][i] = yv;
+    }
+    __syncthreads();
+    if (i < K) {
+        double acc = 0.;
+        if (act)
+#pragma unroll
+            for (int u = 0; u < K; ++u) acc = fma(cv[u], sy[h][u], acc);
+        sp[h][i] = acc;
+    }
+    __syncthreads();
+    if (lane < K) {  // r_e -= V1^T y1 + U2^T y2
+        const int R = e * K + lane;
+        if (R < nb) rw[R] -= sp[0][lane] + sp[1][lane];
+    }
+    if (h2) {  // owner of o2: y and the arrow partial Y2^T y2
+        if (h == 1 && i < K && (e + s) * K + i < nb) y[(e + s) * K + i] = yv;
+        for (int q = lane; q < nG; q += 64) {
+            const double *Y2 = B.FY + (size_t)(e + s) * K * nG;
+            double acc = 0.;
+            for (int u = 0; u < K; ++u) acc = fma(Y2[u * nG + q], sy[1][u], acc);
+            B.gpart[(size_t)(e + s) * nG + q] = acc;
+        }
+    }
+}
+
+// Forward root: y_T = FT [r_0; r_G - sum_o gpart_o].
+template <int K>
+__global__ void __launch_bounds__(64) k_bcr_fwd_root(BcrDev B, const double *rw, double *y) {
+    const int N = B.NR;
+    __shared__ double v[K + NGMAX];
+    const int lane = threadIdx.x, nb = B.nb, nG = B.nG;
+    if (lane < K) v[lane] = bcr_get(rw, lane, nb);
+    if (lane < NGMAX) {
+        double g = 0.;
+        if (lane < nG) {
+            g = rw[nb + lane];
+            for (int o = 1; o < B.nblk; ++o) g -= B.gpart[(size_t)o * nG + lane];
+        }
+        v[K + lane] = g;
+    }
+    __syncthreads();
+    if (lane < K + nG) {
+        double acc = 0.;
+        for (int u = 0; u <= lane; ++u) acc = fma(B.FT[lane * N + u], v[u], acc);
+        if (lane < K) {
+            if (lane < nb) y[lane] = acc;
+        } else {
+            y[nb + lane - K] = acc;
+        }
+    }
+}
+
+// Backward root: x_T = FT^T y_T.
+template <int K>
+__global__ void __launch_bounds__(64) k_bcr_bwd_root(BcrDev B, const double *y, double *x) {
+    const int N = B.NR;
+    __shared__ double v[K + NGMAX];
+    const int lane = threadIdx.x, nb = B.nb, nG = B.nG;
+    if (lane < K) v[lane] = bcr_get(y, lane, nb);
+    if (lane < NGMAX) v[K + lane] = lane < nG ? y[nb + lane] : 0.;
+    __syncthreads();
+    if (lane < K + nG) {
+        double acc = 0.;
+        for (int u = lane; u < K + nG; ++u) acc = fma(B.FT[u * N + lane], v[u], acc);
+        if (lane < K) {
+            if (lane < nb) x[lane] = acc;
+        } else {
+            x[nb + lane - K] = acc;
+        }
+    }
+}
+
+// Backward level: workgroup per odd block o (t = 2 blockIdx.x + 1):
+// x_o = C_o^-T (y_o - U_o x_{o-s} - V_o x_{o+s} - Y_o x_G).  Factor rows are
+// loaded at entry, before the (dependent) x loads.
+template <int K>
+__global__ void __launch_bounds__(64) k_bcr_bwd(BcrDev B, int s, int nact, const double *y,
+                                                double *x) {
+    __shared__ double sv[K], xg[NGMAX], xp[K], xn[K];
+    const int lane = threadIdx.x;
+    const int t = 2 * blockIdx.x + 1, o = t * s;
+    const bool hn = t + 1 < nact;
+    const int nb = B.nb, nG = B.nG;
+    double ur[K], vr[K], cc[K];  // row lane of U_o, V_o; column lane of C_o^-1
+    double yo = 0.;
+    if (lane < K) {
+        const double *U = bcr_blk(B.FU, o, K), *V = bcr_blk(B.FV, o, K);
+        const double *Ci = bcr_blk(B.FC, o, K);
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            ur[u] = U[lane * K + u];
+            vr[u] = hn ? V[lane * K + u] : 0.;
+            cc[u] = u >= lane ? Ci[u * K + lane] : 0.;
+        }
+        yo = bcr_get(y, o * K + lane, nb);
+        xp[lane] = bcr_get(x, (o - s) * K + lane, nb);
+        xn[lane] = hn ? bcr_get(x, (o + s) * K + lane, nb) : 0.;
+    }
+    if (lane < nG) xg[lane] = x[nb + lane];
+    __syncthreads();
+    if (lane < K) {
+        const double *Y = B.FY + (size_t)o * K * nG;
+        double acc = yo;
+#pragma unroll
+        for (int u = 0; u < K; ++u) acc = fma(-ur[u], xp[u], fma(-vr[u], xn[u], acc));
+        for (int q = 0; q < nG; ++q) acc = fma(-Y[lane * nG + q], xg[q], acc);
+        sv[lane] = acc;
+    }
+    __syncthreads();
+    if (lane < K) {
+        double acc = 0.;
+#pragma unroll
+        for (int u = 0; u < K; ++u) acc = fma(cc[u], sv[u], acc);
+        const int R = o * K + lane;
+        if (R < nb) x[R] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side.
+// ---------------------------------------------------------------------------
+template <int K>
+static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long long *probe) {
+    const BcrDev &D = B.bcr;
+    k_bcr_load<K><<<D.nblk, 256, 0, s>>>(D);
+    int ping = 0;
+    for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) {
+        k_bcr_level<K><<<(nact + 1) / 2, 256, 0, s>>>(D, st, nact, ping, fail, probe);
+        ping ^= 1;
+    }
+    switch (D.NR) {
+        case 8: k_bcr_root<8><<<1, 64, 0, s>>>(D, fail); break;
+        case 16: k_bcr_root<16><<<1, 64, 0, s>>>(D, fail); break;
+        case 24: k_bcr_root<24><<<1, 64, 0, s>>>(D, fail); break;
+        case 32: k_bcr_root<32><<<1, 64, 0, s>>>(D, fail); break;
+        case 40: k_bcr_root<40><<<1, 64, 0, s>>>(D, fail); break;
+        default: k_bcr_root<48><<<1, 64, 0, s>>>(D, fail); break;
+    }
+}
+
+template <int K>
+static void bcr_forward_k(hipStream_t s, const BandSolver &B, const double *r, double *y) {
+    const BcrDev &D = B.bcr;
+    MMBA_HIP(hipMemcpyAsync(D.rw, r, sizeof(double) * (size_t)(D.nb + D.nG),
+                                  hipMemcpyDeviceToDevice, s));
+    for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2)
+        k_bcr_fwd<K><<<(nact + 1) / 2, 64, 0, s>>>(D, st, nact, D.rw, y);
+    k_bcr_fwd_root<K><<<1, 64, 0, s>>>(D, D.rw, y);
+}
+
+template <int K>
+static void bcr_backward_k(hipStream_t s, const BandSolver &B, const double *y, double *x) {
+    const BcrDev &D = B.bcr;
+    k_bcr_bwd_root<K><<<1, 64, 0, s>>>(D, y, x);
+    std::vector<std::pair<int, int>> lv;  // (stride, nact) per level, coarse to fine
+    for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) lv.push_back({st, nact});
+    for (int l = (int)lv.size() - 1; l >= 0; --l)
+        k_bcr_bwd<K><<<lv[l].second / 2, 64, 0, s>>>(D, lv[l].first, lv[l].second, y, x);
+}
+
+void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe) {
+    switch (B.bcr.K) {
+        case 8: bcr_factor_k<8>(s, B, fail, probe); break;
+        case 16: bcr_factor_k<16>(s, B, fail, probe); break;
+        case 24: bcr_factor_k<24>(s, B, fail, probe); break;
+        default: bcr_factor_k<32>(s, B, fail, probe); break;
+    }
+}
+
+void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y) {
+    switch (B.bcr.K) {
+        case 8: bcr_forward_k<8>(s, B, r, y); break;
+        case 16: bcr_forward_k<16>(s, B, r, y); break;
+        case 24: bcr_forward_k<24>(s, B, r, y); break;
+        default: bcr_forward_k<32>(s, B, r, y); break;
+    }
+}
+
+void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x) {
+    switch (B.bcr.K) {
+        case 8: bcr_backward_k<8>(s, B, y, x); break;
+        case 16: bcr_backward_k<16>(s, B, y, x); break;
+        case 24: bcr_backward_k<24>(s, B, y, x); break;
+        default: bcr_backward_k<32>(s, B, y, x); break;
+    }
+}
+
+}  // namespace mmba

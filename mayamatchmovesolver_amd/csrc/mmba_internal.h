@@ -29,6 +29,7 @@ constexpr int NGMAX = 16;   // global parameters
 constexpr int LMAX = 20;    // local Jacobian columns per observation
 constexpr int TILE = 64;    // reduced-system tile edge
 constexpr int CAMREC = 20;  // doubles per camera-frame record
+constexpr int BREC = 16;    // doubles per bundle record (128 B: one L2 line)
 
 // In-place all-reduce of device buffers across the shards of a plan
 // (mmba_comm.cpp: RCCL, or an in-process group for tests).
@@ -58,8 +59,21 @@ struct BandPart {
     long long aoff;        // arrow rows: apool[aoff + a*(r1-r0) + (c-r0)]
 };
 
+// Block cyclic reduction of the band + arrow system (mmba_bcr.hip): K x K
+// blocks (K = 8/16/24/32 >= w), per-block factor columns for the solves.
+struct BcrDev {
+    int K = 0, nb = 0, nG = 0, nblk = 0, w = 0;
+    int NR = 0;  // root system size: K + nG rounded up to 8
+    const double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr;  // input (band layout)
+    double *Dk = nullptr, *Lk0 = nullptr, *Lk1 = nullptr, *Gk = nullptr;
+    double *FC = nullptr, *FU = nullptr, *FV = nullptr, *FY = nullptr, *Zc = nullptr;
+    double *FT = nullptr, *gpart = nullptr, *rw = nullptr;
+};
+
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
+    bool use_bcr = false;                    // unsharded, w <= 32: block cyclic reduction
+    BcrDev bcr;
     int P = 1, w = 0, nb = 0, nG = 0;
     int p_lo = 0, p_hi = 1;                  // partitions this shard factors
     Comm *comm = nullptr;                    // sharded: T, rT are all-reduced
@@ -111,11 +125,20 @@ struct DevProblem {
     // camera-frame structure
     const int *cf_cam, *cf_frame, *cf_obs_off, *cf_var_off, *cf_var_param, *cf_var_flags;
     const int *cf_pc, *cf_roff;  // CF-block size and offset in R
+    int pc_uniform;              // common CF-block size of solved camera-frames (0: mixed)
     // bundle-side parameter lists (B-class first, then bundle-side globals)
     const int *bnd_par_off, *bnd_par;
     const int *bnd_pb;     // B-block size
     const int *bnd_xoff;   // offset of the B block in x (param ids are contiguous? no: list)
     const int *bobs_off, *bobs;  // observations grouped by bundle
+    // frame-independent bundles with only B-class parameters ("fast" bundles):
+    // bnd_p4[b] = {p0, p1, p2, pb} (pb = -1: generic path).  brec[b*BREC]:
+    // world position (3), position with parameter a perturbed (3 x 3), FD step
+    // of parameter a (3); written by k_bnd_records once per evaluation so the
+    // per-observation kernels read one 128-B record instead of walking
+    // bundle -> transform -> attribute tables.
+    const int4 *bnd_p4;
+    const double *brec;
     // per camera lens parameter lists
     const int *cam_lpar_off, *cam_lpar;
     // parameters

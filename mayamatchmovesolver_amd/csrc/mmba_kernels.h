@@ -9,6 +9,8 @@ void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, doub
                        double *ext_pert, double *step, int solver_type, double delta,
                        double eps_dif);
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext);
+void launch_bnd_records(hipStream_t s, const DevProblem &P, const double *ext_pert,
+                        const double *step, double *brec, int base_only);
 void launch_cam_records(hipStream_t s, const DevProblem &P, const int *var_cf,
                         const double *ext_pert, double *recs, int nvar, int base_only);
 int residual_blocks(const DevProblem &P);
@@ -49,13 +51,15 @@ void launch_trsv_bwd_all(hipStream_t s, const double *S, const int *slot, int NT
                          const int *cols_off, const int *cols, const double *Linv, double *y,
                          double *x);
 void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
-                       const int *dest_off, int ndest, const int2 *pairs, const SView &V);
+                       const int *dest_off, int ndest, const int2 *pairs, const SView &V,
+                       int pc_uniform);
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs);
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                        const double *tb, const SView &V, double *rhs);
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                           const double *tb, const double *Lb, const double *xR, double *x);
+                           const double *tb, const double *Lb, const double *xR, double *U,
+                           double *x);
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                           const double *Lb, const double *v, double *wR, double *usq);
@@ -68,6 +72,11 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
 // right-hand side are all-reduced over B.comm)
 void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
 void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
+// Block cyclic reduction variant (mmba_bcr.hip), same contract; used by the
+// band_* entry points when B.use_bcr.
+void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe);
+void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
+void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
 // mask (nullable): entries this shard owns
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
                   int nparts, double *out, const int *mask = nullptr);

@@ -82,6 +82,48 @@ __global__ void k_cam_records(DevProblem P, const int *__restrict__ var_cf,
     camera_record(P, P.cf_cam[cf], P.cf_frame[cf], ov, &recs[(size_t)idx * CAMREC]);
 }
 
+// -------------------------------------------------------------------------
+// Bundle records (fast bundles, see DevProblem::bnd_p4): one thread per
+// bundle walks the bundle's transform/attribute tables once per evaluation.
+// -------------------------------------------------------------------------
+__global__ void k_bnd_records(DevProblem P, const double *__restrict__ ext_pert,
+                              const double *__restrict__ step, double *brec, int base_only) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int4 p4 = P.bnd_p4[b];
+    if (p4.w < 0) return;
+    double *br = &brec[(size_t)b * BREC];
+    const Override none{-1, 0.};
+    double bp[3];
+    bundle_position(P, b, 0, none, bp);  // frame-independent: any frame
+    br[0] = bp[0];
+    br[1] = bp[1];
+    br[2] = bp[2];
+    if (base_only) return;
+    for (int a = 0; a < p4.w; ++a) {
+        const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
+        const Override ov{P.p_attr[p], ext_pert[p]};
+        bundle_position(P, b, 0, ov, bp);
+        br[3 + 3 * a] = bp[0];
+        br[4 + 3 * a] = bp[1];
+        br[5 + 3 * a] = bp[2];
+        br[12 + a] = step[p];
+    }
+}
+
+// Unperturbed bundle position of observation (b, frame f).
+__device__ __forceinline__ void base_bundle(const DevProblem &P, int b, int f, double *bp) {
+    if (P.bnd_p4[b].w >= 0) {
+        const double *br = &P.brec[(size_t)b * BREC];
+        bp[0] = br[0];
+        bp[1] = br[1];
+        bp[2] = br[2];
+    } else {
+        const Override none{-1, 0.};
+        bundle_position(P, b, f, none, bp);
+    }
+}
+
 __device__ __forceinline__ bool obs_lens(const DevProblem &P, int cam, int &lens) {
     if (!P.cam_lens) return false;
     lens = P.cam_lens[cam];
@@ -105,7 +147,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         const int cam = P.obs_cam[i];
         const Override none{-1, 0.};
         double bp[3];
-        bundle_position(P, b, fr, none, bp);
+        base_bundle(P, b, fr, bp);
         double lc[5];
         int lens;
         const bool hl = obs_lens(P, cam, lens);
@@ -152,8 +194,9 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     const int cam = P.obs_cam[i];
     const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
     const Override none{-1, 0.};
+    const int4 p4 = P.bnd_p4[b];
     double bp0[3];
-    bundle_position(P, b, fr, none, bp0);
+    base_bundle(P, b, fr, bp0);
     double lc0[5];
     int lens = -1;
     const bool hl = obs_lens(P, cam, lens);
@@ -166,16 +209,14 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     const int pstale = stale_param[fr];
     Resid rs = r0;
     int l = 0;
-    auto emit = [&](int p, const Resid &r) {
+    auto emit_s = [&](int p, const Resid &r, double st) {
         double jx, jy;
-        if (lmder) {
-            const double inv = step[p];
-            jx = (r.ex - r0.ex) * inv;
-            jy = (r.ey - r0.ey) * inv;
-        } else {
-            const double h = step[p];
-            jx = (r.ex - r0.ex) / h;
-            jy = (r.ey - r0.ey) / h;
+        if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
+            jx = (r.ex - r0.ex) * st;
+            jy = (r.ey - r0.ey) * st;
+        } else {      // st = h, divided (fdjac2)
+            jx = (r.ex - r0.ex) / st;
+            jy = (r.ey - r0.ey) / st;
         }
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
@@ -183,6 +224,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
         if (p == pstale) rs = r;
         ++l;
     };
+    auto emit = [&](int p, const Resid &r) { emit_s(p, r, step[p]); };
     // camera-side parameters (variants 1..nvar-1)
     for (int v = 1; v < nvar && l < LMAX; ++v) {
         const int t = voff + v;
@@ -196,7 +238,17 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
         emit(p, residual(rec, bp, mx, my, sw, P.mode, P.image_width, hl, lc0));
     }
     // bundle-side parameters not already covered by a camera variant
-    for (int q = P.bnd_par_off[b]; q < P.bnd_par_off[b + 1] && l < LMAX; ++q) {
+    if (p4.w >= 0) {  // fast bundle: perturbed positions from the record
+        const double *br = &P.brec[(size_t)b * BREC];
+        for (int a = 0; a < p4.w && l < LMAX; ++a) {
+            const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
+            const double bp[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
+            emit_s(p, residual(rec0, bp, mx, my, sw, P.mode, P.image_width, hl, lc0),
+                   br[12 + a]);
+        }
+    }
+    for (int q = p4.w >= 0 ? P.bnd_par_off[b + 1] : P.bnd_par_off[b];
+         q < P.bnd_par_off[b + 1] && l < LMAX; ++q) {
         const int p = P.bnd_par[q];
         if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
         if (P.p_both[p]) {
@@ -318,6 +370,62 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
         g[P.cf_var_param[P.cf_var_off[cf] + 1 + ea]] = acc;
     } else if (kind == 2) {
         Acg[((size_t)cf * PCMAX + ea) * NGMAX + eb] = acc;
+    }
+}
+
+// Uniform block size PC and no global parameters: one wave per camera-frame,
+// lane o accumulates the upper triangle of Acc and gC over the observations
+// o, o + 64, ... of the (contiguous) segment in registers; the 64 partial
+// sums are added through LDS in a fixed order.
+template <int PC>
+__global__ void __launch_bounds__(64) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
+                                                const double *__restrict__ f, double *Acc,
+                                                double *g) {
+    constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC;
+    __shared__ double red[NE][65];
+    const int cf = blockIdx.x;
+    if (!own_cf(P, cf) || P.cf_pc[cf] != PC) return;
+    const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
+    const size_t M = P.M;
+    const int lane = threadIdx.x;
+    double acc[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = 0.;
+    for (int i = o0 + lane; i < o1; i += 64) {
+        double jx[PC], jy[PC];
+#pragma unroll
+        for (int a = 0; a < PC; ++a) {
+            jx[a] = J[(2 * a) * M + i];
+            jy[a] = J[(2 * a + 1) * M + i];
+        }
+        const double fx = f[2 * i], fy = f[2 * i + 1];
+        int e = 0;
+#pragma unroll
+        for (int a = 0; a < PC; ++a)
+#pragma unroll
+            for (int c = a; c < PC; ++c) acc[e++] += jx[a] * jx[c] + jy[a] * jy[c];
+#pragma unroll
+        for (int a = 0; a < PC; ++a) acc[NCC + a] += jx[a] * fx + jy[a] * fy;
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) red[e][lane] = acc[e];
+    __syncthreads();
+    double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
+    for (int e = lane; e < NE; e += 64) {
+        double v = 0.;
+        for (int l = 0; l < 64; ++l) v += red[e][l];
+        if (e < NCC) {
+            int a = 0, rem = e;
+            while (rem >= PC - a) {
+                rem -= PC - a;
+                ++a;
+            }
+            const int c = a + rem;
+            A[a * PCMAX + c] = v;
+            A[c * PCMAX + a] = v;
+        } else {
+            g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
+        }
     }
 }
 
@@ -490,53 +598,69 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
     const int pb = P.bnd_pb[b];
     if (pb == 0) return;
     const int po = P.bnd_par_off[b];
-    double A[3][3];
-    for (int a = 0; a < 3; ++a)
-        for (int c = 0; c < 3; ++c) A[a][c] = Abb[(size_t)b * 9 + a * 3 + c];
-    double rhs[3] = {0., 0., 0.};
-    for (int a = 0; a < pb; ++a) {
-        const int p = P.bnd_par[po + a];
-        const double d = diag[p];
-        A[a][a] += lam * (d * d);
-        rhs[a] = g[p];
-        if (A[a][a] == 0.) {
-            A[a][a] = 1.;
-            rhs[a] = 0.;
+    // every index static (no scratch); rows a >= pb are identity padding
+    double A[3][3], rhs[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            A[a][c] = (a < pb && c < pb) ? Abb[(size_t)b * 9 + a * 3 + c] : (a == c ? 1. : 0.);
+        rhs[a] = 0.;
+        if (a < pb) {
+            const int p = P.bnd_par[po + a];
+            const double d = diag[p];
+            A[a][a] += lam * (d * d);
+            rhs[a] = g[p];
+            if (A[a][a] == 0.) {
+                A[a][a] = 1.;
+                rhs[a] = 0.;
+            }
         }
     }
-    double L[3][3] = {};
+    double L[3][3] = {}, il[3];
     bool ok = true;
-    for (int j = 0; j < pb; ++j) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
         double s = A[j][j];
+#pragma unroll
         for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
         if (!(s > 0.)) {
             ok = false;
             s = 1.;
         }
         L[j][j] = sqrt(s);
-        for (int i = j + 1; i < pb; ++i) {
+        il[j] = 1.0 / L[j][j];
+#pragma unroll
+        for (int i = j + 1; i < 3; ++i) {
             double t = A[i][j];
+#pragma unroll
             for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
-            L[i][j] = t / L[j][j];
+            L[i][j] = t * il[j];
         }
     }
     if (!ok) atomicOr(fail, 1);
+#pragma unroll
     for (int a = 0; a < 3; ++a)
-        for (int c = 0; c < 3; ++c) Lb[(size_t)b * 9 + a * 3 + c] = L[a][c];
-    double t[3] = {0., 0., 0.};
-    for (int a = 0; a < pb; ++a) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Lb[(size_t)b * 9 + a * 3 + c] = (a < pb) ? L[a][c] : 0.;
+    double t[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
         double s = rhs[a];
+#pragma unroll
         for (int k = 0; k < a; ++k) s -= L[a][k] * t[k];
-        t[a] = s / L[a][a];
+        t[a] = s * il[a];  // zero on padding rows (rhs 0)
     }
     for (int a = 0; a < 3; ++a) tb[(size_t)b * 3 + a] = t[a];
     for (int q = 0; q < P.nG; ++q) {
         // row q of Abg^T, forward-solve against L: w L^T = a  ->  L w^T = a^T
-        double w[3] = {0., 0., 0.};
-        for (int a = 0; a < pb; ++a) {
-            double s = Abg[((size_t)b * PBMAX + a) * NGMAX + q];
+        double w[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            double s = a < pb ? Abg[((size_t)b * PBMAX + a) * NGMAX + q] : 0.;
+#pragma unroll
             for (int k = 0; k < a; ++k) s -= L[a][k] * w[k];
-            w[a] = s / L[a][a];
+            w[a] = s * il[a];
         }
         for (int a = 0; a < 3; ++a) Wg[((size_t)b * NGMAX + q) * 3 + a] = w[a];
     }
@@ -554,25 +678,37 @@ __global__ void k_schur_obs(DevProblem P, const double *__restrict__ J,
     const int cf = P.obs_cf[i];
     const int pc = P.cf_pc[cf];
     const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
-    double bx[3], by[3];
-    for (int a = 0; a < pb; ++a) {
-        bx[a] = J[(size_t)(2 * (s + a)) * M + i];
-        by[a] = J[(size_t)(2 * (s + a) + 1) * M + i];
-    }
-    double L[3][3];
-    for (int a = 0; a < 3; ++a)
+    // every index static (no scratch): bundle columns a < pb, camera rows r < pc
+    double bx[3], by[3], L[3][3], il[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        bx[a] = a < pb ? J[(size_t)(2 * (s + a)) * M + i] : 0.;
+        by[a] = a < pb ? J[(size_t)(2 * (s + a) + 1) * M + i] : 0.;
+#pragma unroll
         for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
-    for (int r = 0; r < pc; ++r) {
-        const double cx = J[(size_t)(2 * r) * M + i], cy = J[(size_t)(2 * r + 1) * M + i];
-        double e[3];
-        for (int a = 0; a < pb; ++a) e[a] = cx * bx[a] + cy * by[a];
-        double w[3] = {0., 0., 0.};
-        for (int a = 0; a < pb; ++a) {
-            double t = e[a];
-            for (int k = 0; k < a; ++k) t -= L[a][k] * w[k];
-            w[a] = t / L[a][a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) il[a] = a < pb ? 1.0 / L[a][a] : 0.;
+    double cx[PCMAX], cy[PCMAX];
+#pragma unroll
+    for (int r = 0; r < PCMAX; ++r) {  // every load issued before the solves
+        cx[r] = r < pc ? J[(size_t)(2 * r) * M + i] : 0.;
+        cy[r] = r < pc ? J[(size_t)(2 * r + 1) * M + i] : 0.;
+    }
+#pragma unroll
+    for (int r = 0; r < PCMAX; ++r) {
+        if (r < pc) {
+            double w[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                double t = cx[r] * bx[a] + cy[r] * by[a];
+#pragma unroll
+                for (int k = 0; k < a; ++k) t -= L[a][k] * w[k];
+                w[a] = t * il[a];  // zero for a >= pb
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) W[((size_t)(r * 3 + a)) * M + i] = w[a];
         }
-        for (int a = 0; a < 3; ++a) W[((size_t)(r * 3 + a)) * M + i] = w[a];
     }
 }
 
@@ -697,30 +833,104 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
 // Deterministic Schur accumulation: one wave per destination block
 // (cf_i >= cf_j); pairs of observations sharing a bundle are pre-sorted by
 // destination on the host, so every S entry has a single writer and a fixed
-// summation order (no atomics).
+// summation order (no atomics).  The pairs' W rows are staged through LDS 64
+// pairs at a time: lane q loads pair q (the i of one destination are one
+// camera-frame's contiguous observations, so the SoA loads coalesce), then
+// lane e accumulates entries e and e + 64 of the (pci x pcj) block.
 __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *__restrict__ W,
                                                    const int2 *__restrict__ dest,
                                                    const int *__restrict__ dest_off,
                                                    const int2 *__restrict__ pairs,
                                                    const SView V) {
+    __shared__ double sA[3 * PCMAX][65];
+    __shared__ double sB[3 * PCMAX][65];
     const int d = blockIdx.x;
     const int2 cc = dest[d];
     const int pci = P.cf_pc[cc.x], pcj = P.cf_pc[cc.y];
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
     const int M = P.M;
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
-    for (int e = threadIdx.x; e < pci * pcj; e += 64) {
-        const int a = e / pcj, c = e % pcj;
-        const int R = ri + a, C = rj + c;
-        if (R < C) continue;
-        double acc = 0.;
-        for (int q = q0; q < q1; ++q) {
-            const int2 pr = pairs[q];
-            acc += W[(size_t)(a * 3) * M + pr.x] * W[(size_t)(c * 3) * M + pr.y] +
-                   W[(size_t)(a * 3 + 1) * M + pr.x] * W[(size_t)(c * 3 + 1) * M + pr.y] +
-                   W[(size_t)(a * 3 + 2) * M + pr.x] * W[(size_t)(c * 3 + 2) * M + pr.y];
+    const int lane = threadIdx.x;
+    const int ne = pci * pcj;
+    const int e0 = lane, e1 = lane + 64;
+    const int a0 = e0 / max(pcj, 1), c0 = e0 % max(pcj, 1);
+    const int a1 = e1 / max(pcj, 1), c1 = e1 % max(pcj, 1);
+    const bool v0 = e0 < ne && ri + a0 >= rj + c0;
+    const bool v1 = e1 < ne && ri + a1 >= rj + c1;
+    double acc0 = 0., acc1 = 0.;
+    for (int qb = q0; qb < q1; qb += 64) {
+        const int cnt = min(64, q1 - qb);
+        const int2 pr = lane < cnt ? pairs[qb + lane] : make_int2(0, 0);
+        double ra[3 * PCMAX], rb[3 * PCMAX];
+#pragma unroll
+        for (int k = 0; k < 3 * PCMAX; ++k) {  // issue every load before the stores
+            ra[k] = (lane < cnt && k < 3 * pci) ? W[(size_t)k * M + pr.x] : 0.;
+            rb[k] = (lane < cnt && k < 3 * pcj) ? W[(size_t)k * M + pr.y] : 0.;
         }
-        *s_at(V, R, C) -= acc;
+#pragma unroll
+        for (int k = 0; k < 3 * PCMAX; ++k) {
+            sA[k][lane] = ra[k];
+            sB[k][lane] = rb[k];
+        }
+        __syncthreads();
+        if (v0)
+            for (int q = 0; q < cnt; ++q)
+                acc0 += sA[a0 * 3][q] * sB[c0 * 3][q] + sA[a0 * 3 + 1][q] * sB[c0 * 3 + 1][q] +
+                        sA[a0 * 3 + 2][q] * sB[c0 * 3 + 2][q];
+        if (v1)
+            for (int q = 0; q < cnt; ++q)
+                acc1 += sA[a1 * 3][q] * sB[c1 * 3][q] + sA[a1 * 3 + 1][q] * sB[c1 * 3 + 1][q] +
+                        sA[a1 * 3 + 2][q] * sB[c1 * 3 + 2][q];
+        __syncthreads();
+    }
+    if (v0) *s_at(V, ri + a0, rj + c0) -= acc0;
+    if (v1) *s_at(V, ri + a1, rj + c1) -= acc1;
+}
+
+// Uniform camera-frame block size PC (every solved camera-frame has PC
+// parameters, e.g. 6 for pose-only BA): lane q accumulates the full PC x PC
+// product of the pairs q, q + 64, ... in registers (coalesced SoA loads, no
+// LDS in the loop), then the 64 partial blocks are summed through LDS in a
+// fixed order (deterministic).
+template <int PC>
+__global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
+                                                     const int2 *__restrict__ dest,
+                                                     const int *__restrict__ dest_off,
+                                                     const int2 *__restrict__ pairs,
+                                                     const SView V) {
+    __shared__ double red[PC * PC][65];
+    const int d = blockIdx.x;
+    const int2 cc = dest[d];
+    const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
+    const size_t M = P.M;
+    const int q0 = dest_off[d], q1 = dest_off[d + 1];
+    const int lane = threadIdx.x;
+    double acc[PC * PC];
+#pragma unroll
+    for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
+    for (int q = q0 + lane; q < q1; q += 64) {
+        const int2 pr = pairs[q];
+        double wi[3 * PC], wj[3 * PC];
+#pragma unroll
+        for (int k = 0; k < 3 * PC; ++k) {
+            wi[k] = W[k * M + pr.x];
+            wj[k] = W[k * M + pr.y];
+        }
+#pragma unroll
+        for (int a = 0; a < PC; ++a)
+#pragma unroll
+            for (int c = 0; c < PC; ++c)
+                acc[a * PC + c] += wi[a * 3] * wj[c * 3] + wi[a * 3 + 1] * wj[c * 3 + 1] +
+                                   wi[a * 3 + 2] * wj[c * 3 + 2];
+    }
+#pragma unroll
+    for (int e = 0; e < PC * PC; ++e) red[e][lane] = acc[e];
+    __syncthreads();
+    for (int e = lane; e < PC * PC; e += 64) {
+        double v = 0.;
+        for (int l = 0; l < 64; ++l) v += red[e][l];
+        const int a = e / PC, c = e % PC;
+        if (ri + a >= rj + c) *s_at(V, ri + a, rj + c) -= v;
     }
 }
 
@@ -796,8 +1006,27 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
     }
 }
 
-// x_b = Lb^-T (tb - sum_i W_i^T x_cf(i) - Wg_b^T x_G), scatter to parameter order.
-__global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
+// u_i = W_i^T x_cf(i) per observation (3 SoA rows, coalesced over i), so the
+// per-bundle back substitution gathers 3 values per observation instead of
+// the 3 x pc of W_i.
+__global__ void __launch_bounds__(256) k_obs_wtx(DevProblem P, const double *__restrict__ W,
+                                                 const double *__restrict__ xR, double *U) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    const int M = P.M;
+    const int cf = P.obs_cf[i];
+    const int pc = P.cf_pc[cf];
+    const int r0 = P.cf_roff[cf];
+    double u[3] = {0., 0., 0.};
+    for (int a = 0; a < pc; ++a) {
+        const double xv = xR[r0 + a];
+        for (int c = 0; c < 3; ++c) u[c] += W[(size_t)(a * 3 + c) * M + i] * xv;
+    }
+    for (int c = 0; c < 3; ++c) U[(size_t)c * M + i] = u[c];
+}
+
+// x_b = Lb^-T (tb - sum_i u_i - Wg_b^T x_G), scatter to parameter order.
+__global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ U,
                                  const double *__restrict__ Wg, const double *__restrict__ tb,
                                  const double *__restrict__ Lb, const double *__restrict__ xR,
                                  double *x) {
@@ -810,13 +1039,7 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
     double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
     for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
         const int i = P.bobs[q];
-        const int cf = P.obs_cf[i];
-        const int pc = P.cf_pc[cf];
-        const int r0 = P.cf_roff[cf];
-        for (int a = 0; a < pc; ++a) {
-            const double xv = xR[r0 + a];
-            for (int c = 0; c < 3; ++c) s[c] -= W[(size_t)(a * 3 + c) * M + i] * xv;
-        }
+        for (int c = 0; c < 3; ++c) s[c] -= U[(size_t)c * M + i];
     }
     for (int q = 0; q < nG; ++q) {
         const double xv = xR[nCF + q];
@@ -1114,6 +1337,10 @@ void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, doub
     k_param_prep<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext, ext_pert, step, solver_type, delta,
                                                  eps_dif);
 }
+void launch_bnd_records(hipStream_t s, const DevProblem &P, const double *ext_pert,
+                        const double *step, double *brec, int base_only) {
+    if (P.nB > 0) k_bnd_records<<<nblk(P.nB, 256), 256, 0, s>>>(P, ext_pert, step, brec, base_only);
+}
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);
 }
@@ -1138,7 +1365,14 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
                double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk) {
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
-    if (P.ncf > 0) k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
+    if (P.ncf > 0) {
+        if (P.nG == 0 && P.pc_uniform == 6)
+            k_ne_cf_u<6><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
+        else if (P.nG == 0 && P.pc_uniform == 7)
+            k_ne_cf_u<7><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
+        else
+            k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
+    }
     if (P.nB > 0) k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
     if (P.nG > 0) {
         const int nb = nblk(P.M, glob_chunk);
@@ -1173,8 +1407,15 @@ void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, con
     k_schur_pairs<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, V, rhs);
 }
 void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
-                       const int *dest_off, int ndest, const int2 *pairs, const SView &V) {
-    if (ndest > 0) k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
+                       const int *dest_off, int ndest, const int2 *pairs, const SView &V,
+                       int pc_uniform) {
+    if (ndest <= 0) return;
+    if (pc_uniform == 6)
+        k_schur_dest_u<6><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
+    else if (pc_uniform == 7)
+        k_schur_dest_u<7><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
+    else
+        k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
 }
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs) {
@@ -1187,9 +1428,11 @@ void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, cons
         k_schur_glob<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, V, rhs);
 }
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                           const double *tb, const double *Lb, const double *xR, double *x) {
-    if (P.nB > 0)
-        k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, Lb, xR, x);
+                           const double *tb, const double *Lb, const double *xR, double *U,
+                           double *x) {
+    if (P.nB == 0) return;
+    k_obs_wtx<<<nblk(P.M, 256), 256, 0, s>>>(P, W, xR, U);
+    k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, U, Wg, tb, Lb, xR, x);
 }
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x) {
     k_scatter_xR<<<nblk(P.n, 256), 256, 0, s>>>(P, xR, x);

@@ -57,6 +57,7 @@ double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
     launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
     launch_set_attrs(s, P, d_ext);
     launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
+    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
     if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
     launch_residual(s, P, d_recs, df, eu, ed, d_partial);
     if (timing) {
@@ -80,6 +81,7 @@ void Plan::jac(const double *dx) {
     launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
     launch_set_attrs(s, P, d_ext);
     launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 0);
+    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 0);
     if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                     d_stale, d_eu, d_ed);
@@ -122,7 +124,7 @@ bool Plan::solve_damped(double lam) {
         launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
         if (nB_solved > 0) {
             if (use_dest) {
-                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V);
+                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V, pc_uniform);
                 launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
                 launch_schur_glob(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
@@ -170,7 +172,7 @@ bool Plan::solve_damped(double lam) {
         }
         launch_scatter_xR(s, P, d_xR, d_xs);
     }
-    if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_xs);
+    if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
     MMBA_HIP(hipMemcpyAsync(h_fail, d_fail, sizeof(int), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipStreamSynchronize(s));
     bool ok = *h_fail == 0;
@@ -313,6 +315,8 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         fun(d_x, d_f, d_eu, d_ed);
     } else {
         launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
+        launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
+    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
     }
     std::vector<double> ed(Mg);
@@ -368,6 +372,8 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     if (opt.accept_only_better) {
         // measureErrors before any parameter is set (adjust_base.cpp:1080-1103)
         launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
+        launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
+    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
         download_ref_order(nullptr, nullptr, d_ed, nullptr, nullptr, ed_host.data());
         error_stats(ed_host.data(), Mg, &init_avg, &init_min, &init_max);

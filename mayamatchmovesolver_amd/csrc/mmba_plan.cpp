@@ -25,7 +25,14 @@
 namespace mmba {
 
 Plan::~Plan() {
-    if (d_probe) {
+    if (d_probe && bs.use_bcr) {
+        long long h[4] = {0, 0, 0, 0};
+        if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+            std::fprintf(stderr,
+                         "[mmba probe] bcr level cycles (workgroup 0, all levels): stage %lld "
+                         "chol+inv %lld products %lld updates %lld (K=%d nblk=%d)\n",
+                         h[0], h[1], h[2], h[3], bs.bcr.K, bs.bcr.nblk);
+    } else if (d_probe) {
         long long h[4] = {0, 0, 0, 0};
         if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
             std::fprintf(stderr,
@@ -258,6 +265,21 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int p : bglob[b]) bnd_par.push_back(p);
     }
     bnd_par_off[nB] = (int)bnd_par.size();
+    // fast bundles: position independent of the frame (no animated attribute
+    // in the bundle's transform chain) and only B-class parameters
+    std::vector<int4> bnd_p4(nB);
+    for (int b = 0; b < nB; ++b) {
+        bool fast = bglob[b].empty();
+        const int t0 = pr->bnd_tfm[b];
+        for (size_t q = 0; q < chain[t0].size() && fast; ++q)
+            for (int k = 0; k < (q == 0 ? 3 : 9); ++k) {
+                const int a = pr->tfm_attrs[9 * chain[t0][q] + k];
+                if (a >= 0 && pr->attr_animated[a]) fast = false;
+            }
+        const auto &bp = bpar[b];
+        bnd_p4[b] = make_int4(bp.size() > 0 ? bp[0] : -1, bp.size() > 1 ? bp[1] : -1,
+                              bp.size() > 2 ? bp[2] : -1, fast ? (int)bp.size() : -1);
+    }
     // lens params per camera
     std::vector<int> cam_lpar_off(nC + 1, 0), cam_lpar;
     for (int c = 0; c < nC; ++c) {
@@ -475,6 +497,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int J = 0; J <= I; ++J)
             if (nz[(size_t)I * NT + J]) slot[(size_t)I * NT + J] = nslots++;
 
+    pc_uniform = 0;
+    for (int cf = 0; cf < ncf; ++cf) {
+        if (cf_pc[cf] == 0) continue;
+        if (pc_uniform == 0) pc_uniform = cf_pc[cf];
+        else if (pc_uniform != cf_pc[cf]) pc_uniform = -1;
+    }
+    if (pc_uniform < 0) pc_uniform = 0;
     // ---- Schur accumulation plan: observation pairs sharing a bundle, sorted
     // by destination block (cf_i >= cf_j) ----
     std::vector<int> row_cf(nCF > 0 ? nCF : 1, 0);
@@ -588,10 +617,14 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.cf_var_flags = upload(cf_var_flags);
     D.cf_pc = upload(cf_pc);
     D.cf_roff = upload(cf_roff);
+    D.pc_uniform = pc_uniform;
     D.bnd_par_off = upload(bnd_par_off);
     D.bnd_par = upload(bnd_par);
     D.bnd_pb = upload(bnd_pb);
     D.bnd_xoff = nullptr;
+    D.bnd_p4 = upload(bnd_p4);
+    d_brec = dalloc<double>((size_t)nB * BREC);
+    D.brec = d_brec;
     D.bobs_off = upload(bobs_off);
     D.bobs = upload(bobs);
     D.cam_lpar_off = upload(cam_lpar_off);
@@ -680,6 +713,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_tb = dalloc<double>((size_t)nB * 3);
     d_Wg = dalloc<double>((size_t)nB * NGMAX * 3);
     d_W = dalloc<double>((size_t)PCMAX * 3 * (nB_solved > 0 ? M : 1));
+    d_U = dalloc<double>((size_t)3 * (nB_solved > 0 ? M : 1));
     d_rhs = dalloc<double>(nRpad);
     d_yR = dalloc<double>(nRpad);
     d_xR = dalloc<double>(nRpad);
@@ -704,6 +738,49 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
 // mmba_band.hip) and the device buffers of the band factorisation.
 void Plan::setup_band(int Pforce) {
     const int nb = nR - nG, w = bw;
+    // Unsharded and w <= 32: block cyclic reduction (mmba_bcr.hip).  Pforce < 0
+    // forces it, Pforce > 0 forces the partitioned chain; MMBA_BAND_BCR=0
+    // disables it (A/B measurements).
+    {
+        const char *e = std::getenv("MMBA_BAND_BCR");
+        const bool env_off = e && std::atoi(e) == 0;
+        if (nranks == 1 && w <= 32 && (Pforce < 0 || (Pforce == 0 && !env_off))) {
+            bs.use_bcr = true;
+            bs.P = 1;
+            bs.comm = nullptr;
+            bs.w = w;
+            bs.nb = nb;
+            bs.nG = nG;
+            bs.Bd = dalloc<double>((size_t)nb * (w + 1));
+            bs.Ga = dalloc<double>((size_t)nG * nb);
+            bs.Gd = dalloc<double>(NGMAX * NGMAX);
+            BcrDev &B = bs.bcr;
+            B.K = std::max(8, (w + 7) / 8 * 8);
+            B.nb = nb;
+            B.nG = nG;
+            B.w = w;
+            B.nblk = std::max(1, (nb + B.K - 1) / B.K);
+            B.NR = B.K + (nG + 7) / 8 * 8;
+            B.Bd = bs.Bd;
+            B.Ga = bs.Ga;
+            B.Gd = bs.Gd;
+            const size_t kk = (size_t)B.nblk * B.K * B.K;
+            B.Dk = dalloc<double>(kk);
+            B.Lk0 = dalloc<double>(kk);
+            B.Lk1 = dalloc<double>(kk);
+            B.FC = dalloc<double>(kk);
+            B.FU = dalloc<double>(kk);
+            B.FV = dalloc<double>(kk);
+            B.Gk = dalloc<double>((size_t)B.nblk * nG * B.K);
+            B.FY = dalloc<double>((size_t)B.nblk * nG * B.K);
+            B.Zc = dalloc<double>((size_t)B.nblk * nG * nG);
+            B.FT = dalloc<double>((size_t)B.NR * B.NR);
+            B.gpart = dalloc<double>((size_t)B.nblk * nG);
+            B.rw = dalloc<double>((size_t)nb + nG);
+            d_ymask = upload(std::vector<int>(std::max(nR, 1), 1));
+            return;
+        }
+    }
     if (Ra_all.empty()) {
         Ra_all.assign(1, 0);
         Rb_all.assign(1, nb);

@@ -71,6 +71,7 @@ struct Plan {
     // deterministic Schur accumulation (destination-sorted observation pairs)
     bool use_dest = false;
     int ndest = 0;
+    int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
     // band + arrow layout of the reduced system (mmba_band.hip)
@@ -104,12 +105,12 @@ struct Plan {
     double *d_wa1 = nullptr, *d_wa2 = nullptr, *d_wa3 = nullptr, *d_xs = nullptr,
            *d_v = nullptr;
     double *d_f = nullptr, *d_ftrial = nullptr, *d_eu = nullptr, *d_ed = nullptr;
-    double *d_recs = nullptr;
+    double *d_recs = nullptr, *d_brec = nullptr;
     double *d_J = nullptr;
     int *d_jcol = nullptr, *d_nloc = nullptr;
     double *d_Acc = nullptr, *d_Acg = nullptr, *d_Abb = nullptr, *d_Abg = nullptr,
            *d_Agg = nullptr, *d_glob_partial = nullptr;
-    double *d_Lb = nullptr, *d_tb = nullptr, *d_Wg = nullptr, *d_W = nullptr;
+    double *d_Lb = nullptr, *d_tb = nullptr, *d_Wg = nullptr, *d_W = nullptr, *d_U = nullptr;
     double *d_rhs = nullptr, *d_yR = nullptr, *d_xR = nullptr, *d_wR = nullptr,
            *d_usq = nullptr;
     double *d_partial = nullptr, *d_scalar = nullptr;

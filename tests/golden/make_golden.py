@@ -91,11 +91,22 @@ def main():
         for f in RES_FIELDS:
             d["res_" + f] = np.array(rd[f])
         d.update(exp_x=x, exp_fvec=fvec, exp_err_user=eu, exp_err_dist=ed, exp_trace=tr)
+        # roundoff envelope: how far the oracle's own final x moves when x0 is
+        # perturbed by ~1 ulp (relative 1e-15, 3 seeds).  On ill-conditioned
+        # scenes (weak gauge / scale directions) this exceeds 1e-6, and no fp64
+        # implementation -- the reference included -- determines x closer.
+        env = 0.0
+        for seed in range(3):
+            rng = np.random.default_rng(seed)
+            x0p = prob.x0 * (1.0 + 1e-15 * rng.standard_normal(prob.x0.size))
+            xp = R.solve(prob, opt, x0=x0p)[0]
+            env = max(env, float(np.max(np.abs(xp - x) / np.maximum(np.abs(x), 1e-3))))
+        d["exp_x_envelope"] = np.array(env)
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **d)
-        print("%-24s n=%6d m=%7d iters=%3d reason=%d  %7.1f KB" % (
+        print("%-24s n=%6d m=%7d iters=%3d reason=%d x-envelope=%.1e  %7.1f KB" % (
             name, prob.num_params, prob.num_residuals, res.outer_iterations,
-            res.reason_number, os.path.getsize(path) / 1024))
+            res.reason_number, env, os.path.getsize(path) / 1024))
 
 
 if __name__ == "__main__":

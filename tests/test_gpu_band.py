@@ -1,7 +1,7 @@
 """Device band + arrow Cholesky (csrc/mmba_band.hip) against numpy on random
 symmetric positive-definite matrices of the reduced-system shape: nb band rows
 of half bandwidth w plus nG dense arrow rows, with and without the partitioned
-(nested-dissection) path.  Tolerance: fp64 direct solve, 1e-10 relative to
+(nested-dissection) path and with block cyclic reduction (P = -1).  Tolerance: fp64 direct solve, 1e-10 relative to
 max |x| on well-conditioned matrices."""
 import numpy as np
 import pytest
@@ -37,6 +37,11 @@ CASES = [
     (500, 23, 0, 1), (2994, 23, 0, 0), (2994, 23, 0, 11), (2994, 23, 0, 24),
     (1000, 23, 5, 6), (1000, 40, 16, 4), (640, 60, 3, 1), (777, 80, 1, 1),
     (10, 2, 16, 1), (0, 0, 4, 1), (90, 5, 0, 9),
+    # P = -1: block cyclic reduction (csrc/mmba_bcr.hip), K = 8/16/24/32
+    (84, 6, 0, -1), (300, 6, 2, -1), (2994, 23, 0, -1), (1000, 23, 5, -1),
+    (1000, 32, 16, -1), (10, 2, 16, -1), (0, 0, 4, -1), (90, 5, 0, -1),
+    (7, 3, 0, -1), (777, 31, 1, -1), (1000, 16, 3, -1), (17, 8, 2, -1),
+    (2880, 11, 2, -1), (840, 6, 0, -1), (4096, 24, 0, -1), (24 * 65, 24, 1, -1),
 ]
 
 

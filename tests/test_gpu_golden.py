@@ -28,7 +28,11 @@ def test_gpu_matches_fixture(name, gpu_ctx):
     tr = d["exp_trace"]
     assert len(out.fnorm_trace) == len(tr)
     np.testing.assert_allclose(out.fnorm_trace, tr, rtol=REL, atol=1e-9 * tr[0])
+    # final x: 1e-6 relative, or -- on ill-conditioned scenes -- the oracle's
+    # own roundoff envelope (how far its x moves under a 1-ulp change of x0,
+    # stored in the fixture by make_golden.py)
     xr = d["exp_x"]
-    assert np.max(np.abs(out.x - xr) / np.maximum(np.abs(xr), 1e-3)) <= REL
+    tol = max(REL, float(d["exp_x_envelope"]))
+    assert np.max(np.abs(out.x - xr) / np.maximum(np.abs(xr), 1e-3)) <= tol
     # final residual vector: norm of the difference against the initial ||f||
     assert np.linalg.norm(out.fvec - d["exp_fvec"]) <= REL * float(tr[0])
