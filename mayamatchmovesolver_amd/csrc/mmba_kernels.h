@@ -90,6 +90,8 @@ void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const 
                      double *out);
 void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mask,
                       double *partial, int nparts, double *out);
+// *out = (*flag != 0) as a double (fail flags joining the scalar reads)
+void launch_flag_to_scalar(hipStream_t s, const int *flag, double *out);
 void launch_keep_rows(hipStream_t s, double *v, int lo, int hi, int nCF, int nR, int root);
 void launch_keep_mask(hipStream_t s, const double *src, const int *mask, int n, double *dst);
 void launch_lm_step(hipStream_t s, int n, const double *xs, const double *x, const double *diag,

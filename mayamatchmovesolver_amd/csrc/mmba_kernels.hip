@@ -1475,6 +1475,12 @@ void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mas
     k_zero_flag<<<nparts, 256, 0, s>>>(acnorm, n, mask, partial);
     k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
 }
+__global__ void k_flag_to_scalar(const int *__restrict__ flag, double *out) {
+    if (threadIdx.x == 0) *out = *flag ? 1. : 0.;
+}
+void launch_flag_to_scalar(hipStream_t s, const int *flag, double *out) {
+    k_flag_to_scalar<<<1, 64, 0, s>>>(flag, out);
+}
 void launch_keep_rows(hipStream_t s, double *v, int lo, int hi, int nCF, int nR, int root) {
     if (nR > 0) k_keep_rows<<<nblk(nR, 256), 256, 0, s>>>(v, lo, hi, nCF, nR, root);
 }

@@ -28,10 +28,61 @@ static double wall_now() {
         .count();
 }
 
-double Plan::read_scalar(int slot) {
-    MMBA_HIP(hipMemcpyAsync(h_scalar + slot, d_scalar + slot, sizeof(double),
+// ---- timing spans: events recorded on the stream, read after the solve ----
+hipEvent_t Plan::next_event() {
+    if (ev_used == ev_pool.size()) {
+        hipEvent_t e = nullptr;
+        MMBA_HIP(hipEventCreate(&e));
+        ev_pool.push_back(e);
+    }
+    return ev_pool[ev_used++];
+}
+
+void Plan::span_begin() {
+    if (!timing) return;
+    span_a = next_event();
+    MMBA_HIP(hipEventRecord(span_a, s));
+}
+
+void Plan::span_end(int kind) {
+    if (!timing) return;
+    hipEvent_t b = next_event();
+    MMBA_HIP(hipEventRecord(b, s));
+    spans.push_back({span_a, b, kind});
+    if (ev_used > 8192) collect_spans();  // bounded pool (long solves)
+}
+
+void Plan::collect_spans() {
+    if (!spans.empty()) {
+        MMBA_HIP(hipStreamSynchronize(s));
+        for (const Span &sp : spans) {
+            float ms = 0.f;
+            MMBA_HIP(hipEventElapsedTime(&ms, sp.a, sp.b));
+            if (sp.kind == SPAN_RESID) {
+                resid_ms += ms;
+                resid_n++;
+            } else if (sp.kind == SPAN_JAC) {
+                jac_ms += ms;
+                jac_n++;
+            } else {
+                chol_ms += ms;
+                chol_n++;
+            }
+        }
+        spans.clear();
+    }
+    ev_used = 0;
+}
+
+// ---- scalar slots ----
+void Plan::read_slots(int lo, int hi) {
+    MMBA_HIP(hipMemcpyAsync(h_scalar + lo, d_scalar + lo, sizeof(double) * (hi - lo + 1),
                             hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipStreamSynchronize(s));
+}
+
+double Plan::read_scalar(int slot) {
+    read_slots(slot, slot);
     return h_scalar[slot];
 }
 
@@ -45,31 +96,34 @@ double Plan::reduce_read(int slot, ReduceOp op) {
     return read_scalar(slot);
 }
 
-// ||D v|| over the parameters (each counted by the shard that owns it).
-double Plan::dnorm(const double *dv) {
-    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + 1, d_p_own);
-    return std::sqrt(reduce_read(1));
+// ||D v||^2 over the parameters (each counted by the shard that owns it).
+void Plan::dnorm_enqueue(const double *dv, int slot) {
+    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + slot, d_p_own);
+    allreduce(d_scalar + slot, 1);
 }
 
-// iflag = 1: setParameters + measureErrors.  Returns ||f||.
-double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
-    const double t0 = wall_now();
+double Plan::dnorm(const double *dv) {
+    dnorm_enqueue(dv, SL_DNORM);
+    return std::sqrt(read_scalar(SL_DNORM));
+}
+
+// iflag = 1: setParameters + measureErrors; ||f||^2 -> SL_FNORM.
+void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed) {
     launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
     launch_set_attrs(s, P, d_ext);
     launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
     launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
-    if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
+    span_begin();
     launch_residual(s, P, d_recs, df, eu, ed, d_partial);
-    if (timing) {
-        MMBA_HIP(hipEventRecord(ev_b, s));
-        MMBA_HIP(hipEventSynchronize(ev_b));
-        float ms = 0.f;
-        MMBA_HIP(hipEventElapsedTime(&ms, ev_a, ev_b));
-        resid_ms += ms;
-        resid_n++;
-    }
-    launch_reduce_sum(s, d_partial, residual_blocks(P), d_scalar);
-    const double r = std::sqrt(reduce_read(0));
+    span_end(SPAN_RESID);
+    launch_reduce_sum(s, d_partial, residual_blocks(P), d_scalar + SL_FNORM);
+    allreduce(d_scalar + SL_FNORM, 1);
+}
+
+double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
+    const double t0 = wall_now();
+    fun_enqueue(dx, df, eu, ed);
+    const double r = std::sqrt(read_scalar(SL_FNORM));
     t_func += wall_now() - t0;
     return r;
 }
@@ -82,7 +136,7 @@ void Plan::jac(const double *dx) {
     launch_set_attrs(s, P, d_ext);
     launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 0);
     launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 0);
-    if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
+    span_begin();
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                     d_stale, d_eu, d_ed);
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
@@ -90,20 +144,12 @@ void Plan::jac(const double *dx) {
               d_glob_partial, glob_chunk);
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
     launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
-    if (timing) {
-        MMBA_HIP(hipEventRecord(ev_b, s));
-        MMBA_HIP(hipEventSynchronize(ev_b));
-        float ms = 0.f;
-        MMBA_HIP(hipEventElapsedTime(&ms, ev_a, ev_b));
-        jac_ms += ms;
-        jac_n++;
-    }
-    MMBA_HIP(hipStreamSynchronize(s));
+    span_end(SPAN_JAC);
     t_jac += wall_now() - t0;
 }
 
-// d_xs = (A + lam D^2)^-1 g.  Returns false if a factorisation failed.
-bool Plan::solve_damped(double lam) {
+// d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
+void Plan::solve_damped_enqueue(double lam) {
     const double t0 = wall_now();
     MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));
     if (nB_solved > 0) {
@@ -131,7 +177,7 @@ bool Plan::solve_damped(double lam) {
                 launch_schur_pairs(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             }
         }
-        if (timing) MMBA_HIP(hipEventRecord(ev_a, s));
+        span_begin();
         if (band) {
             band_factor(s, bs, d_fail, d_probe);
         } else {
@@ -142,14 +188,7 @@ bool Plan::solve_damped(double lam) {
                 launch_chol_update(s, d_S, d_slot, NT, k, d_pairs + q0, nq);
             }
         }
-        if (timing) {
-            MMBA_HIP(hipEventRecord(ev_b, s));
-            MMBA_HIP(hipEventSynchronize(ev_b));
-            float ms = 0.f;
-            MMBA_HIP(hipEventElapsedTime(&ms, ev_a, ev_b));
-            chol_ms += ms;
-            chol_n++;
-        }
+        span_end(SPAN_CHOL);
         if (band) {
             band_forward(s, bs, d_rhs, d_yR);
             band_backward(s, bs, d_yR, d_xR);
@@ -173,28 +212,27 @@ bool Plan::solve_damped(double lam) {
         launch_scatter_xR(s, P, d_xR, d_xs);
     }
     if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
-    MMBA_HIP(hipMemcpyAsync(h_fail, d_fail, sizeof(int), hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
-    bool ok = *h_fail == 0;
-    if (nranks > 1) {
-        h_scalar[5] = ok ? 0. : 1.;
-        MMBA_HIP(hipMemcpyAsync(d_scalar + 5, h_scalar + 5, sizeof(double), hipMemcpyHostToDevice, s));
-        ok = reduce_read(5, ReduceOp::Max) == 0.;
-    }
+    launch_flag_to_scalar(s, d_fail, d_scalar + SL_FAIL);
+    allreduce(d_scalar + SL_FAIL, 1, ReduceOp::Max);
     t_linear += wall_now() - t0;
-    return ok;
 }
 
-// sqrt(v^T (A + lam D^2)^-1 v) with v = D^2 xs / dxnorm, using the current
-// factorisation (lmpar's parl / parc denominators).
-double Plan::newton_term(double dxnorm) {
+bool Plan::solve_damped(double lam) {
+    solve_damped_enqueue(lam);
+    return read_scalar(SL_FAIL) == 0.;
+}
+
+// v^T (A + lam D^2)^-1 v with v = D^2 xs / dxnorm, using the current
+// factorisation (lmpar's parl / parc denominators): bundle part -> SL_NEWT_B,
+// reduced part -> SL_NEWT_R.
+void Plan::newton_enqueue(double dxnorm) {
     const double t0 = wall_now();
     launch_newton_v(s, n, d_diag, d_xs, dxnorm, d_v);
-    MMBA_HIP(hipMemsetAsync(d_scalar + 2, 0, 2 * sizeof(double), s));
+    MMBA_HIP(hipMemsetAsync(d_scalar + SL_NEWT_B, 0, 2 * sizeof(double), s));
     if (nR > 0) launch_gather_R(s, P, d_v, d_wR, nRpad);
     if (nB_solved > 0) {
         launch_newton_bundle(s, P, d_W, d_Wg, d_Lb, d_v, d_wR, d_usq);
-        launch_reduce_sum(s, d_usq, nB, d_scalar + 2);
+        launch_reduce_sum(s, d_usq, nB, d_scalar + SL_NEWT_B);
     }
     if (nR > 0) {
         if (band) {
@@ -207,36 +245,41 @@ double Plan::newton_term(double dxnorm) {
                 launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
             }
         }
-        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + 3, d_ymask);
+        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R, d_ymask);
     }
-    allreduce(d_scalar + 2, 2);
-    MMBA_HIP(hipMemcpyAsync(h_scalar + 2, d_scalar + 2, 2 * sizeof(double),
-                            hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    allreduce(d_scalar + SL_NEWT_B, 2);
     t_linear += wall_now() - t0;
-    return std::sqrt(h_scalar[2] + h_scalar[3]);
 }
 
-// lmpar restated on normal equations (see oracle/refcpu.c lmpar).
+// lmpar restated on normal equations (see oracle/refcpu.c lmpar).  Every
+// decision point reads its scalars with one synchronisation.
 static double lmpar_ne(Plan &pl, double delta, double *par) {
     const double p1 = .1, p001 = .001;
     const double dwarf = DBL_MIN;
+    double *h = pl.h_scalar;
     int iter = 0;
-    const bool ok0 = pl.solve_damped(0.0);
-    double dxnorm = ok0 ? pl.dnorm(pl.d_xs) : HUGE_VAL;
+    pl.solve_damped_enqueue(0.0);
+    pl.dnorm_enqueue(pl.d_xs, Plan::SL_DNORM);
+    pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+    const bool ok0 = h[Plan::SL_FAIL] == 0.;
+    double dxnorm = ok0 ? std::sqrt(h[Plan::SL_DNORM]) : HUGE_VAL;
     double fp = dxnorm - delta;
     if (fp <= p1 * delta) {
         if (iter == 0) *par = 0.;
         return dxnorm;
     }
     double parl = 0.;
-    if (!pl.rank_deficient && ok0) {
-        const double temp = pl.newton_term(dxnorm);
+    const bool newton0 = !pl.rank_deficient && ok0;
+    if (newton0) pl.newton_enqueue(dxnorm);
+    launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts,
+                     pl.d_scalar + Plan::SL_GDIV, pl.d_p_own);
+    pl.allreduce(pl.d_scalar + Plan::SL_GDIV, 1);
+    pl.read_slots(Plan::SL_NEWT_B, Plan::SL_GDIV);
+    if (newton0) {
+        const double temp = std::sqrt(h[Plan::SL_NEWT_B] + h[Plan::SL_NEWT_R]);
         parl = fp / delta / temp / temp;
     }
-    launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts, pl.d_scalar + 4,
-                     pl.d_p_own);
-    const double gnorm = std::sqrt(pl.reduce_read(4));
+    const double gnorm = std::sqrt(h[Plan::SL_GDIV]);
     double paru = gnorm / delta;
     if (paru == 0.) paru = dwarf / std::min(delta, p1);
     *par = std::max(*par, parl);
@@ -245,13 +288,17 @@ static double lmpar_ne(Plan &pl, double delta, double *par) {
     for (;;) {
         ++iter;
         if (*par == 0.) *par = std::max(dwarf, p001 * paru);
-        pl.solve_damped(*par);
-        dxnorm = pl.dnorm(pl.d_xs);
+        pl.solve_damped_enqueue(*par);
+        pl.dnorm_enqueue(pl.d_xs, Plan::SL_DNORM);
+        pl.read_slots(Plan::SL_DNORM, Plan::SL_DNORM);
+        dxnorm = std::sqrt(h[Plan::SL_DNORM]);
         double temp = fp;
         fp = dxnorm - delta;
         if (std::fabs(fp) <= p1 * delta || (parl == 0. && fp <= temp && temp < 0.) || iter == 10)
             break;
-        temp = pl.newton_term(dxnorm);
+        pl.newton_enqueue(dxnorm);
+        pl.read_slots(Plan::SL_NEWT_B, Plan::SL_NEWT_R);
+        temp = std::sqrt(h[Plan::SL_NEWT_B] + h[Plan::SL_NEWT_R]);
         const double parc = fp / delta / temp / temp;
         if (fp > 0.) parl = std::max(parl, *par);
         if (fp < 0.) paru = std::min(paru, *par);
@@ -316,13 +363,13 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
     } else {
         launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
         launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
-    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
     }
     std::vector<double> ed(Mg);
     download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed.data());
     if (ed_out) std::memcpy(ed_out, ed.data(), sizeof(double) * Mg);
     if (stats) error_stats(ed.data(), Mg, &stats[0], &stats[1], &stats[2]);
+    collect_spans();
     return MMBA_OK;
 }
 
@@ -340,6 +387,7 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
     MMBA_HIP(hipMemcpyAsync(jc.data(), d_jcol, sizeof(int) * jc.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(nl.data(), d_nloc, sizeof(int) * M, hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipStreamSynchronize(s));
+    collect_spans();
     std::memset(fjac, 0, sizeof(double) * (size_t)m * n);
     for (int i = 0; i < M; ++i) {
         const int r = ref_of_dev[i];
@@ -373,7 +421,6 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         // measureErrors before any parameter is set (adjust_base.cpp:1080-1103)
         launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
         launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
-    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
         download_ref_order(nullptr, nullptr, d_ed, nullptr, nullptr, ed_host.data());
         error_stats(ed_host.data(), Mg, &init_avg, &init_min, &init_max);
@@ -420,33 +467,54 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             jac_evals += n;
             if (lmdif) nfev += n;
             // rank deficiency from exactly-zero columns (MINPACK nsing < n)
-            launch_zero_flag(s, d_acnorm, n, d_p_own, d_partial, nparts, d_scalar + 5);
-            rank_deficient = reduce_read(5, ReduceOp::Max) != 0.;
+            launch_zero_flag(s, d_acnorm, n, d_p_own, d_partial, nparts, d_scalar + SL_ZERO);
+            allreduce(d_scalar + SL_ZERO, 1, ReduceOp::Max);
             launch_diag_init(s, n, d_acnorm, d_diag, iter == 1, mode);
+            // diag set from acnorm (mode 1) *before* the max() update in
+            // lmder; both happen before xnorm only on the first pass, and
+            // max(diag, acnorm) == acnorm there, so one kernel suffices.
+            if (iter == 1) dnorm_enqueue(d_x, SL_XN2);
+            if (fnorm != 0.) {
+                launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + SL_GNORM,
+                             d_p_own);
+                allreduce(d_scalar + SL_GNORM, 1, ReduceOp::Max);
+            }
+            {
+                const double t0 = wall_now();
+                read_slots(SL_ZERO, SL_XN2);
+                t_jac += wall_now() - t0;
+            }
+            rank_deficient = h_scalar[SL_ZERO] != 0.;
             if (iter == 1) {
-                // diag set from acnorm (mode 1) *before* the max() update in
-                // lmder; both happen before xnorm only on the first pass, and
-                // max(diag, acnorm) == acnorm there, so one kernel suffices.
-                xnorm = dnorm(d_x);
+                xnorm = std::sqrt(h_scalar[SL_XN2]);
                 delta = factor * xnorm;
                 if (delta == 0.) delta = factor;
             }
-            gnorm = 0.;
-            if (fnorm != 0.) {
-                launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + 6,
-                             d_p_own);
-                gnorm = reduce_read(6, ReduceOp::Max);
-            }
+            gnorm = fnorm != 0. ? h_scalar[SL_GNORM] : 0.;
             if (gnorm <= gtol) info = 4;
             if (info != 0) goto TERMINATE;
             do {
                 const double dxn = lmpar_ne(*this, delta, &par);
                 (void)dxn;
+                // trial point: ||D p||, f(x + p), ||J p|| and the candidate
+                // ||D x_new|| are independent -- one synchronisation
                 launch_lm_step(s, n, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3);
-                launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + 1, d_p_own);
-                const double pnorm = std::sqrt(reduce_read(1));
+                launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + SL_PNORM,
+                             d_p_own);
+                allreduce(d_scalar + SL_PNORM, 1);
+                fun_enqueue(d_wa2, d_ftrial, d_eu, d_ed);
+                launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, d_partial, nparts,
+                                d_scalar + SL_JP);
+                allreduce(d_scalar + SL_JP, 1);
+                dnorm_enqueue(d_wa2, SL_XN2);
+                {
+                    const double t0 = wall_now();
+                    read_slots(SL_FNORM, SL_XN2);
+                    t_func += wall_now() - t0;
+                }
+                const double pnorm = std::sqrt(h_scalar[SL_PNORM]);
                 if (iter == 1) delta = std::min(delta, pnorm);
-                const double fnorm1 = fun(d_wa2, d_ftrial, d_eu, d_ed);
+                const double fnorm1 = std::sqrt(h_scalar[SL_FNORM]);
                 ++nfev;
                 ++func_evals;
                 push_trace(fnorm1);
@@ -455,8 +523,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     const double d1 = fnorm1 / fnorm;
                     actred = 1. - d1 * d1;
                 }
-                launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, d_partial, nparts, d_scalar + 1);
-                const double temp1 = std::sqrt(reduce_read(1)) / fnorm;
+                const double temp1 = std::sqrt(h_scalar[SL_JP]) / fnorm;
                 const double temp2 = (std::sqrt(par) * pnorm) / fnorm;
                 const double prered = temp1 * temp1 + temp2 * temp2 / p5;
                 const double dirder = -(temp1 * temp1 + temp2 * temp2);
@@ -479,7 +546,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     MMBA_HIP(hipMemcpyAsync(d_x, d_wa2, sizeof(double) * n,
                                             hipMemcpyDeviceToDevice, s));
                     std::swap(d_f, d_ftrial);
-                    xnorm = dnorm(d_x);
+                    xnorm = std::sqrt(h_scalar[SL_XN2]);  // ||D wa2||, computed above
                     fnorm = fnorm1;
                     ++iter;
                 }
@@ -525,9 +592,10 @@ TERMINATE:
         // RMS at the returned parameters
         MMBA_HIP(hipMemcpyAsync(d_wa2, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_wa2, d_ftrial, d_J, d_J + m);  // scratch user buffers
-        launch_sumsq(s, d_J + m, nullptr, M, d_partial, nparts, d_scalar + 7, P.obs_own);
-        r.error_rms = std::sqrt(reduce_read(7) / Mg);
+        launch_sumsq(s, d_J + m, nullptr, M, d_partial, nparts, d_scalar + SL_RMS, P.obs_own);
+        r.error_rms = std::sqrt(reduce_read(SL_RMS) / Mg);
     }
+    collect_spans();
     r.num_trace = trace ? trace->count : 0;
     r.time_solve_s = wall_now() - t_start;
     r.time_func_s = t_func;

@@ -40,8 +40,7 @@ Plan::~Plan() {
                          "update %lld tail %lld (nb=%d w=%d nG=%d P=%d)\n",
                          h[0], h[1], h[2], h[3], nR - nG, bw, nG, bs.P);
     }
-    if (ev_a) (void)hipEventDestroy(ev_a);
-    if (ev_b) (void)hipEventDestroy(ev_b);
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     for (void *p : allocs) (void)hipFree(p);
     if (h_scalar) (void)hipHostFree(h_scalar);
     if (h_fail) (void)hipHostFree(h_fail);
@@ -720,17 +719,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_wR = dalloc<double>(nRpad);
     d_usq = dalloc<double>(nB);
     d_partial = dalloc<double>(std::max(nparts, residual_blocks(P)));
-    d_scalar = dalloc<double>(8);
+    d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
     MMBA_HIP(hipMemsetAsync(d_Acg, 0, sizeof(double) * (size_t)ncf * PCMAX * NGMAX, s));
     MMBA_HIP(hipMemsetAsync(d_Agg, 0, sizeof(double) * (NGMAX * NGMAX + NGMAX), s));
     MMBA_HIP(hipMemsetAsync(d_Abg, 0, sizeof(double) * (size_t)nB * PBMAX * NGMAX, s));
     MMBA_HIP(hipMemsetAsync(d_Abb, 0, sizeof(double) * (size_t)nB * 9, s));
     MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
-    MMBA_HIP(hipHostMalloc(&h_scalar, 8 * sizeof(double)));
+    MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
-    MMBA_HIP(hipEventCreate(&ev_a));
-    MMBA_HIP(hipEventCreate(&ev_b));
     MMBA_HIP(hipStreamSynchronize(s));
 }
 

@@ -119,9 +119,22 @@ struct Plan {
     double *h_scalar = nullptr;  // pinned
     int *h_fail = nullptr;       // pinned
 
-    // timing (HIP events on the plan stream)
+    // timing (HIP events on the plan stream, read back only at the end of a
+    // solve so the hot path never waits on them)
     bool timing = false;
-    hipEvent_t ev_a = nullptr, ev_b = nullptr;
+    enum SpanKind { SPAN_RESID = 0, SPAN_JAC = 1, SPAN_CHOL = 2 };
+    struct Span {
+        hipEvent_t a, b;
+        int kind;
+    };
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<Span> spans;
+    hipEvent_t span_a = nullptr;
+    hipEvent_t next_event();
+    void span_begin();
+    void span_end(int kind);
+    void collect_spans();
     double jac_ms = 0., resid_ms = 0., chol_ms = 0.;
     int jac_n = 0, resid_n = 0, chol_n = 0;
     double t_func = 0., t_jac = 0., t_linear = 0.;
@@ -156,14 +169,35 @@ struct Plan {
 
     void build(const mmba_problem *prob, const mmba_options *o);
 
-    // LM building blocks
+    // LM building blocks.  *_enqueue functions only launch work; results land
+    // in device scalar slots (all-reduced across shards) and are fetched with
+    // one read_slots() per decision point of the MINPACK control flow.
+    enum Slot {
+        SL_FNORM = 0,   // ||f||^2 of the last fun_enqueue
+        SL_DNORM = 1,   // ||D v||^2
+        SL_NEWT_B = 2,  // lmpar Newton term, bundle part
+        SL_NEWT_R = 3,  //                    reduced-system part
+        SL_GDIV = 4,    // ||D^-1 g||^2 (lmpar gnorm)
+        SL_ZERO = 5,    // any exactly-zero Jacobian column (max)
+        SL_GNORM = 6,   // lmder gnorm (max)
+        SL_RMS = 7,
+        SL_FAIL = 8,    // factorisation failed (max)
+        SL_PNORM = 9,   // ||D p||^2 of the trial step
+        SL_JP = 10,     // ||J p||^2
+        SL_XN2 = 11,    // ||D x||^2 (current or candidate x)
+        NSLOT = 16
+    };
+    void read_slots(int lo, int hi);  // [lo, hi] inclusive, one D2H copy + sync
     double read_scalar(int slot = 0);
     void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
     double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
+    void fun_enqueue(const double *dx, double *df, double *eu, double *ed);
     double fun(const double *dx, double *df, double *eu, double *ed);
     void jac(const double *dx);
+    void solve_damped_enqueue(double lam);
     bool solve_damped(double lam);
-    double newton_term(double dxnorm);
+    void newton_enqueue(double dxnorm);
+    void dnorm_enqueue(const double *dv, int slot);
     double dnorm(const double *dv);
     int solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
               mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace);
