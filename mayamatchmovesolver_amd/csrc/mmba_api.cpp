@@ -255,13 +255,16 @@ int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const
         int *dfail = p.dalloc<int>(1);
         MMBA_HIP(hipMemsetAsync(dfail, 0, sizeof(int), p.s));
         MMBA_HIP(hipMemcpyAsync(dr, r, (size_t)n * 8, hipMemcpyHostToDevice, p.s));
-        band_factor(p.s, p.bs, dfail, nullptr);
-        band_forward(p.s, p.bs, dr, dy);
+        // x through the fused factor + forward path; ||L^-1 r||^2 through the
+        // standalone forward solve (the lmpar Newton-term path)
+        band_factor_forward(p.s, p.bs, dfail, nullptr, dr, dy);
         band_backward(p.s, p.bs, dy, dx);
+        double *dy2 = p.dalloc<double>(n);
+        band_forward(p.s, p.bs, dr, dy2);
         std::vector<double> hy(n);
         int fail = 0;
         MMBA_HIP(hipMemcpyAsync(x, dx, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
-        MMBA_HIP(hipMemcpyAsync(hy.data(), dy, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
+        MMBA_HIP(hipMemcpyAsync(hy.data(), dy2, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
         MMBA_HIP(hipMemcpyAsync(&fail, dfail, sizeof(int), hipMemcpyDeviceToHost, p.s));
         MMBA_HIP(hipStreamSynchronize(p.s));
         if (ynorm2) {

@@ -29,6 +29,8 @@
 //   C. trailing update of the window, the arrow rows and Z (rank NB).
 // The solves use the stored NB x NB block inverses: two short reductions per
 // block.
+#include <cstdlib>
+
 #include "mmba_kernels.h"
 
 namespace mmba {
@@ -595,6 +597,20 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
     if (B.comm) B.comm->allreduce(B.TBd, B.tcount, ReduceOp::Sum, s);
     k_band_factor<8, 128, WBAND_MAX, NGMAX, true><<<1, 256, 0, s>>>(
         B.TBd, 2 * B.w - 1, B.d_tpart, B.TGa, nullptr, B.TDinv, B.TGd, B.TGdinv, fail, nullptr);
+}
+
+void band_factor_forward(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
+                         const double *r, double *y) {
+    static const bool fused = [] {
+        const char *e = std::getenv("MMBA_BCR_FUSED");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (B.use_bcr && fused) {
+        bcr_factor(s, B, fail, probe, r, y);
+        return;
+    }
+    band_factor(s, B, fail, probe);
+    band_forward(s, B, r, y);
 }
 
 void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y) {

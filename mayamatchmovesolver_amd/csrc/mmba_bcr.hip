@@ -52,12 +52,25 @@ __device__ __forceinline__ double *bcr_blk(double *base, int b, int K) {
     return base + (size_t)b * K * K;
 }
 
+// Vector entry R of a reduced-order vector; block rows at or beyond nb are
+// padding (value 0, never stored).
+__device__ __forceinline__ double bcr_get(const double *v, int R, int nb) {
+    return R < nb ? v[R] : 0.;
+}
+
+
 // ---------------------------------------------------------------------------
 // Band rows -> blocks.  Workgroup per block b.
 // ---------------------------------------------------------------------------
 template <int K>
-__global__ void __launch_bounds__(256) k_bcr_load(BcrDev B) {
+__global__ void __launch_bounds__(256) k_bcr_load(BcrDev B, const double *r) {
     const int b = blockIdx.x;
+    if (r) {  // fused forward solve: work copy of the right-hand side
+        for (int i = threadIdx.x; i < K; i += blockDim.x)
+            if (b * K + i < B.nb) B.rw[b * K + i] = r[b * K + i];
+        if (b == 0)
+            for (int q = threadIdx.x; q < B.nG; q += blockDim.x) B.rw[B.nb + q] = r[B.nb + q];
+    }
     const int W1 = B.w + 1;
     double *D = bcr_blk(B.Dk, b, K), *L = bcr_blk(B.Lk0, b, K);
     for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
@@ -148,7 +161,7 @@ __device__ __forceinline__ void bcr_chol_inv_wave(double *M, double *Ci, double 
 // ---------------------------------------------------------------------------
 template <int K>
 __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
-                                                   int *fail, long long *probe) {
+                                                   int *fail, long long *probe, double *y) {
     constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
     constexpr int CG = K / 4;     // columns per product task
     constexpr int GS = NGMAX;     // row stride of the K x nG arrays
@@ -159,6 +172,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     __shared__ double sGT[2][K * GS], sY[2][K * GS];
     __shared__ double col[2][64];
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
+    __shared__ double sR[3][K], sYv[2][K];  // fused forward solve: r_o1, r_o2, r_e; y_o1, y_o2
     __shared__ int bad_s;
     const int tid = threadIdx.x, wv = tid >> 6;
     const int t = 2 * blockIdx.x;
@@ -203,6 +217,13 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         sDe[x] = bcr_blk(B.Dk, e, K)[q];
     }
     for (int q = tid; q < nG * K; q += blockDim.x) sGe[q] = B.Gk[(size_t)e * nG * K + q];
+    const bool fwd = y != nullptr;
+    if (fwd && tid < 3 * K) {
+        const int w = tid / K, i = tid % K;
+        const int blk = w == 0 ? o1 : (w == 1 ? o2 : e);
+        const bool hv = w == 0 ? h1 : (w == 1 ? h2 : true);
+        sR[w][i] = hv ? bcr_get(B.rw, blk * K + i, B.nb) : 0.;
+    }
     for (int q = tid; q < 2 * K * GS; q += blockDim.x) {
         const int which = q / (K * GS), r = q % (K * GS), u = r / GS, qq = r % GS;
         const int o = which ? o2 : o1;
@@ -214,6 +235,19 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     int bad = 0;
     if (wv == 0 && h1) bcr_chol_inv_wave<K, KS>(sD[0], sCi[0], col[0], bad);
     if (wv == 1 && h2) bcr_chol_inv_wave<K, KS>(sD[1], sCi[1], col[1], bad);
+    if (fwd && wv < 2) {  // fused forward solve: y_o = C_o^-1 r_o by the same wave
+        wave_lds_sync();
+        const int i = tid & 63;
+        if (i < K) {
+            double acc0 = 0., acc1 = 0.;  // C^-1 is lower: the upper entries are zero
+#pragma unroll
+            for (int u = 0; u < K; u += 2) {
+                acc0 = fma(sCi[wv][i * KS + u], sR[wv][u], acc0);
+                acc1 = fma(sCi[wv][i * KS + u + 1], sR[wv][u + 1], acc1);
+            }
+            sYv[wv][i] = acc0 + acc1;
+        }
+    }
     if (bad) atomicOr(&bad_s, 1);
     __syncthreads();
     stamp(1);
@@ -230,7 +264,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
 #pragma unroll
             for (int c = 0; c < CG; ++c) acc[c] = 0.;
 #pragma unroll 2
-            for (int u = 0; u <= i; ++u) {
+            for (int u = 0; u <= i; ++u) {  // C^-1 lower: entries u > i are zero
                 const double av = Ci[i * KS + u];
 #pragma unroll
                 for (int c = 0; c < CG; ++c) acc[c] = fma(av, Bm[u * KS + c0 + c], acc[c]);
@@ -289,6 +323,27 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             for (int c = 0; c < CG; ++c) bcr_blk(Lout, e, K)[i * K + c0 + c] = -acc[c];
         }
     }
+    if (fwd) {  // r_e -= V1^T y1 + U2^T y2; the owner of o2 stores y2 and Y2^T y2
+        const int ft = (tid + 256 - ((8 * K) & 255)) & 255;  // threads idle in the loop above first
+        if (ft < K) {
+            double acc0 = 0., acc1 = 0.;
+#pragma unroll
+            for (int u = 0; u < K; ++u) {
+                acc0 = fma(V1[u * KS + ft], sYv[0][u], acc0);
+                acc1 = fma(U2[u * KS + ft], sYv[1][u], acc1);
+            }
+            const int R = e * K + ft;
+            if (R < B.nb) B.rw[R] = sR[2][ft] - (acc0 + acc1);
+        } else if (h2 && ft >= 32 && ft < 32 + K) {
+            const int i = ft - 32, R = o2 * K + i;
+            if (R < B.nb) y[R] = sYv[1][i];
+        } else if (h2 && ft >= 64 && ft < 64 + nG) {
+            const int q = ft - 64;
+            double acc = 0.;
+            for (int u = 0; u < K; ++u) acc = fma(sY[1][u * GS + q], sYv[1][u], acc);
+            B.gpart[(size_t)o2 * nG + q] = acc;
+        }
+    }
     for (int q = tid; q < nG * 4; q += blockDim.x) {
         const int qq = q / 4, c0 = (q % 4) * CG;
         double acc[CG];
@@ -333,7 +388,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
 // Ct Ct^T, FT = Ct^-1 (lower, N x N).
 // ---------------------------------------------------------------------------
 template <int N>
-__global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail) {
+__global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y) {
     constexpr int NS = N + 2;
     __shared__ double T[N * NS], Ti[N * NS], col[64];
     const int lane = threadIdx.x;
@@ -361,15 +416,32 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail) {
     wave_lds_sync();
     for (int q = lane; q < N * N; q += 64) B.FT[q] = Ti[(q / N) * NS + q % N];
     if (bad && lane == 0) atomicOr(fail, 1);
+    if (y) {  // fused forward root: y_T = FT [r_0; r_G - sum_o gpart_o]
+        const int nb = B.nb;
+        if (lane < K) col[lane] = bcr_get(B.rw, lane, nb);
+        if (lane >= K && lane < n0) {
+            const int q = lane - K;
+            double g = B.rw[nb + q];
+            for (int o = 1; o < B.nblk; ++o) g -= B.gpart[(size_t)o * nG + q];
+            col[lane] = g;
+        }
+        wave_lds_sync();
+        if (lane < n0) {
+            double acc = 0.;
+            for (int u = 0; u <= lane; ++u) acc = fma(Ti[lane * NS + u], col[u], acc);
+            if (lane < K) {
+                if (lane < nb) y[lane] = acc;
+            } else {
+                y[nb + lane - K] = acc;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
 // Solves.  Vectors are in reduced-system order (nb band rows, then nG global
 // rows); block rows at or beyond nb are padding (value 0, never stored).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double bcr_get(const double *v, int R, int nb) {
-    return R < nb ? v[R] : 0.;
-}
 
 // Forward level: workgroup (64 lanes) per even block e; lanes 0..K-1 handle
 // o1 = e - s, lanes 32..32+K-1 handle o2 = e + s.  Every factor entry a lane
@@ -523,22 +595,26 @@ __global__ void __launch_bounds__(64) k_bcr_bwd(BcrDev B, int s, int nact, const
 // ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
+// Factorisation; with r != nullptr the forward solve y = L^-1 r runs inside
+// the same launches (r is copied to the work vector by the load kernel).
 template <int K>
-static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long long *probe) {
+static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
+                         const double *r, double *y) {
     const BcrDev &D = B.bcr;
-    k_bcr_load<K><<<D.nblk, 256, 0, s>>>(D);
+    k_bcr_load<K><<<D.nblk, 256, 0, s>>>(D, r);
+    double *yy = r ? y : nullptr;
     int ping = 0;
     for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) {
-        k_bcr_level<K><<<(nact + 1) / 2, 256, 0, s>>>(D, st, nact, ping, fail, probe);
+        k_bcr_level<K><<<(nact + 1) / 2, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
         ping ^= 1;
     }
     switch (D.NR) {
-        case 8: k_bcr_root<8><<<1, 64, 0, s>>>(D, fail); break;
-        case 16: k_bcr_root<16><<<1, 64, 0, s>>>(D, fail); break;
-        case 24: k_bcr_root<24><<<1, 64, 0, s>>>(D, fail); break;
-        case 32: k_bcr_root<32><<<1, 64, 0, s>>>(D, fail); break;
-        case 40: k_bcr_root<40><<<1, 64, 0, s>>>(D, fail); break;
-        default: k_bcr_root<48><<<1, 64, 0, s>>>(D, fail); break;
+        case 8: k_bcr_root<8><<<1, 64, 0, s>>>(D, fail, yy); break;
+        case 16: k_bcr_root<16><<<1, 64, 0, s>>>(D, fail, yy); break;
+        case 24: k_bcr_root<24><<<1, 64, 0, s>>>(D, fail, yy); break;
+        case 32: k_bcr_root<32><<<1, 64, 0, s>>>(D, fail, yy); break;
+        case 40: k_bcr_root<40><<<1, 64, 0, s>>>(D, fail, yy); break;
+        default: k_bcr_root<48><<<1, 64, 0, s>>>(D, fail, yy); break;
     }
 }
 
@@ -562,12 +638,13 @@ static void bcr_backward_k(hipStream_t s, const BandSolver &B, const double *y, 
         k_bcr_bwd<K><<<lv[l].second / 2, 64, 0, s>>>(D, lv[l].first, lv[l].second, y, x);
 }
 
-void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe) {
+void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
+                const double *r, double *y) {
     switch (B.bcr.K) {
-        case 8: bcr_factor_k<8>(s, B, fail, probe); break;
-        case 16: bcr_factor_k<16>(s, B, fail, probe); break;
-        case 24: bcr_factor_k<24>(s, B, fail, probe); break;
-        default: bcr_factor_k<32>(s, B, fail, probe); break;
+        case 8: bcr_factor_k<8>(s, B, fail, probe, r, y); break;
+        case 16: bcr_factor_k<16>(s, B, fail, probe, r, y); break;
+        case 24: bcr_factor_k<24>(s, B, fail, probe, r, y); break;
+        default: bcr_factor_k<32>(s, B, fail, probe, r, y); break;
     }
 }
 

@@ -68,13 +68,18 @@ void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double
 // L y = r (band_forward; keeps the separator part of y for band_backward) and
 // L^T x = y.  r, y, x are in reduced-system order (length nb + nG).
 void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe);
+// Factorisation followed by the forward solve y = L^-1 r (fused into the
+// factorisation launches when B.use_bcr).
+void band_factor_forward(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
+                         const double *r, double *y);
 // (sharded: the partitions p_lo..p_hi run here, the separator system and its
 // right-hand side are all-reduced over B.comm)
 void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
 void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
 // Block cyclic reduction variant (mmba_bcr.hip), same contract; used by the
 // band_* entry points when B.use_bcr.
-void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe);
+void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
+                const double *r = nullptr, double *y = nullptr);
 void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
 void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
 // mask (nullable): entries this shard owns

@@ -179,7 +179,7 @@ void Plan::solve_damped_enqueue(double lam) {
         }
         span_begin();
         if (band) {
-            band_factor(s, bs, d_fail, d_probe);
+            band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
         } else {
             for (int k = 0; k < NT; ++k) {
                 const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
@@ -190,7 +190,6 @@ void Plan::solve_damped_enqueue(double lam) {
         }
         span_end(SPAN_CHOL);
         if (band) {
-            band_forward(s, bs, d_rhs, d_yR);
             band_backward(s, bs, d_yR, d_xR);
             if (nranks > 1) {  // every shard needs the rows of its halo camera-frames
                 launch_keep_rows(s, d_xR, Ra, Rb, nR - nG, nR, rank == 0);
