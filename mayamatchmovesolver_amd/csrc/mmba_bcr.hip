@@ -156,6 +156,64 @@ __device__ __forceinline__ void bcr_chol_inv_wave(double *M, double *Ci, double 
     }
 }
 
+// Broadcast lane l's double to the wave (l wave-uniform).
+__device__ __forceinline__ double bcr_rdlane(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Cholesky of one K x K block by ONE wave (as bcr_chol_inv_wave, without the
+// inverse): M (lower, row stride KS) -> C, rs[j] = 1 / C_jj.
+template <int K, int KS>
+__device__ __forceinline__ void bcr_chol_wave(double *M, double *rs_out, double *col, int &bad) {
+    const int lane = threadIdx.x & 63;
+    double a[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) a[c] = (lane < K && c <= lane) ? M[lane * KS + c] : 0.;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double d = bcr_rdlane(a[j], j);
+        if (!(d > 0.) || !isfinite(d)) {
+            bad = 1;
+            d = 1.;
+        }
+        const double rs = bcr_rsq(d);
+        const double l = (lane > j) ? a[j] * rs : 0.;
+        a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+        if (lane < K) col[lane] = l;
+        if (lane == 0) rs_out[j] = rs;
+        wave_lds_sync();
+#pragma unroll
+        for (int c = j + 1; c < K; ++c) a[c] = fma(-l, col[c], a[c]);
+        wave_lds_sync();
+    }
+    if (lane < K)
+#pragma unroll
+        for (int c = 0; c < K; ++c) M[lane * KS + c] = (c <= lane) ? a[c] : 0.;
+}
+
+// In-place forward substitution X <- C^-1 X for the column this lane owns
+// (x points at its first entry, stride xs between rows); column-oriented
+// (axpy) steps so the K dependent steps are short.
+template <int K, int KS>
+__device__ __forceinline__ void bcr_trsv_col(const double *C, const double *rs, double *x0,
+                                             int xs) {
+    double x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = x0[i * xs];
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+        x[t] *= rs[t];
+#pragma unroll
+        for (int i = t + 1; i < K; ++i) x[i] = fma(-C[i * KS + t], x[t], x[i]);
+        wave_lds_sync();  // keeps the column loads of step t from being hoisted
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) x0[i * xs] = x[i];
+}
+
 // ---------------------------------------------------------------------------
 // One elimination level.  blockIdx.x = even index / 2 (t = 2 blockIdx.x).
 // ---------------------------------------------------------------------------
@@ -163,18 +221,18 @@ template <int K>
 __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
                                                    int *fail, long long *probe, double *y) {
     constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
-    constexpr int CG = K / 4;     // columns per product task
+    constexpr int CG = K / 4;     // columns per update task
     constexpr int GS = NGMAX;     // row stride of the K x nG arrays
-    __shared__ double sD[2][K * KS], sCi[2][K * KS];
-    // B operands, row-contiguous: Lo1, Le^T, Lo2, Ln^T
+    __shared__ double sD[2][K * KS];   // D_o1, D_o2 -> C_o1, C_o2
+    // right-hand sides, solved in place: Lo1 -> U1, Le^T -> V1, Lo2 -> U2, Ln^T -> V2
     __shared__ double sB[4][K * KS];
-    __shared__ double sP[4][K * KS];  // U1, V1, U2, V2
-    __shared__ double sGT[2][K * GS], sY[2][K * GS];
+    __shared__ double sGT[2][K * GS];  // G_o^T -> Y_o
+    __shared__ double sR[3][K];        // r_o1 -> y1, r_o2 -> y2, r_e (fused forward solve)
+    __shared__ double sRs[2][K];       // 1 / C_jj
     __shared__ double col[2][64];
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
-    __shared__ double sR[3][K], sYv[2][K];  // fused forward solve: r_o1, r_o2, r_e; y_o1, y_o2
     __shared__ int bad_s;
-    const int tid = threadIdx.x, wv = tid >> 6;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int t = 2 * blockIdx.x;
     const int e = t * s;
     const bool h1 = t >= 2;                 // o1 = e - s exists (and so does its prev e - 2s)
@@ -182,6 +240,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     const bool hn = t + 2 < nact;           // e + 2s (o2's next)
     const int o1 = e - s, o2 = e + s, en = e + 2 * s;
     const int nG = B.nG;
+    const bool fwd = y != nullptr;
     const double *Lin = ping ? B.Lk1 : B.Lk0;
     double *Lout = ping ? B.Lk0 : B.Lk1;
     if (tid == 0) bad_s = 0;
@@ -196,8 +255,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             tprev = tn;
         }
     };
-    // stage every operand (zeros where a neighbour does not exist); the loads
-    // of one pass are issued before any LDS store
+    // stage every operand (zeros where a neighbour does not exist)
     for (int q = tid; q < K * K; q += blockDim.x) {
         const int i = q / K, c = q % K, x = i * KS + c, xt = c * KS + i;
         const double d0 = h1 ? bcr_blk(B.Dk, o1, K)[q] : 0.;
@@ -206,23 +264,14 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         const double b1 = h1 ? bcr_blk((double *)Lin, e, K)[q] : 0.;
         const double b2 = h2 ? bcr_blk((double *)Lin, o2, K)[q] : 0.;
         const double b3 = hn ? bcr_blk((double *)Lin, en, K)[q] : 0.;
+        const double de = bcr_blk(B.Dk, e, K)[q];
         sD[0][x] = d0;
         sD[1][x] = d1;
-        sCi[0][x] = 0.;  // stays zero for a missing neighbour
-        sCi[1][x] = 0.;
         sB[0][x] = b0;
         sB[1][xt] = b1;  // Le^T
         sB[2][x] = b2;
         sB[3][xt] = b3;  // Ln^T
-        sDe[x] = bcr_blk(B.Dk, e, K)[q];
-    }
-    for (int q = tid; q < nG * K; q += blockDim.x) sGe[q] = B.Gk[(size_t)e * nG * K + q];
-    const bool fwd = y != nullptr;
-    if (fwd && tid < 3 * K) {
-        const int w = tid / K, i = tid % K;
-        const int blk = w == 0 ? o1 : (w == 1 ? o2 : e);
-        const bool hv = w == 0 ? h1 : (w == 1 ? h2 : true);
-        sR[w][i] = hv ? bcr_get(B.rw, blk * K + i, B.nb) : 0.;
+        sDe[x] = de;
     }
     for (int q = tid; q < 2 * K * GS; q += blockDim.x) {
         const int which = q / (K * GS), r = q % (K * GS), u = r / GS, qq = r % GS;
@@ -230,67 +279,45 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         const bool h = which ? h2 : h1;
         sGT[which][r] = (h && qq < nG) ? B.Gk[((size_t)o * nG + qq) * K + u] : 0.;
     }
+    for (int q = tid; q < nG * K; q += blockDim.x) sGe[q] = B.Gk[(size_t)e * nG * K + q];
+    if (tid < 3 * K) {
+        const int w = tid / K, i = tid % K;
+        const int blk = w == 0 ? o1 : (w == 1 ? o2 : e);
+        const bool hv = fwd && (w == 0 ? h1 : (w == 1 ? h2 : true));
+        sR[w][i] = hv ? bcr_get(B.rw, blk * K + i, B.nb) : 0.;
+    }
     __syncthreads();
     stamp(0);
+    // A. Cholesky of the two odd neighbours, one wave each
     int bad = 0;
-    if (wv == 0 && h1) bcr_chol_inv_wave<K, KS>(sD[0], sCi[0], col[0], bad);
-    if (wv == 1 && h2) bcr_chol_inv_wave<K, KS>(sD[1], sCi[1], col[1], bad);
-    if (fwd && wv < 2) {  // fused forward solve: y_o = C_o^-1 r_o by the same wave
-        wave_lds_sync();
-        const int i = tid & 63;
-        if (i < K) {
-            double acc0 = 0., acc1 = 0.;  // C^-1 is lower: the upper entries are zero
-#pragma unroll
-            for (int u = 0; u < K; u += 2) {
-                acc0 = fma(sCi[wv][i * KS + u], sR[wv][u], acc0);
-                acc1 = fma(sCi[wv][i * KS + u + 1], sR[wv][u + 1], acc1);
-            }
-            sYv[wv][i] = acc0 + acc1;
-        }
-    }
+    if (wv == 0 && h1) bcr_chol_wave<K, KS>(sD[0], sRs[0], col[0], bad);
+    if (wv == 1 && h2) bcr_chol_wave<K, KS>(sD[1], sRs[1], col[1], bad);
     if (bad) atomicOr(&bad_s, 1);
     __syncthreads();
     stamp(1);
-    // products P_m = Ci * B_m (U1 = Ci1 Lo1, V1 = Ci1 Le^T, U2 = Ci2 Lo2,
-    // V2 = Ci2 Ln^T) and Y_w = Ci_w G_w^T; a task is one row x CG columns
-    // (x 4 arrow columns for Y), Ci lower so u <= i
-    const int ngg = (nG + 3) / 4;
-    for (int q = tid; q < 4 * K * 4 + 2 * K * ngg; q += blockDim.x) {
-        if (q < 16 * K) {
-            const int m = q / (4 * K), r = q % (4 * K), i = r / 4, c0 = (r % 4) * CG;
-            const double *Ci = sCi[m >> 1];
-            const double *Bm = sB[m];
-            double acc[CG];
-#pragma unroll
-            for (int c = 0; c < CG; ++c) acc[c] = 0.;
-#pragma unroll 2
-            for (int u = 0; u <= i; ++u) {  // C^-1 lower: entries u > i are zero
-                const double av = Ci[i * KS + u];
-#pragma unroll
-                for (int c = 0; c < CG; ++c) acc[c] = fma(av, Bm[u * KS + c0 + c], acc[c]);
+    // B. triangular solves, lane = right-hand-side column: wave 0 U1 | V1,
+    // wave 1 U2 | V2, wave 2 Y1 | y1, wave 3 Y2 | y2 (C^-1 never formed)
+    {
+        const int w = wv & 1;  // which neighbour
+        if (w == 0 ? h1 : h2) {
+            if (wv < 2) {
+                if (lane < 2 * K) {
+                    const int m = 2 * w + lane / K, c = lane % K;
+                    bcr_trsv_col<K, KS>(sD[w], sRs[w], &sB[m][c], KS);
+                }
+            } else if (lane < nG) {
+                bcr_trsv_col<K, KS>(sD[w], sRs[w], &sGT[w][lane], GS);
+            } else if (lane == 32 && fwd) {
+                bcr_trsv_col<K, KS>(sD[w], sRs[w], &sR[w][0], 1);
             }
-#pragma unroll
-            for (int c = 0; c < CG; ++c) sP[m][i * KS + c0 + c] = acc[c];
-        } else {
-            const int r = q - 16 * K, w = r / (K * ngg), r2 = r % (K * ngg);
-            const int i = r2 / ngg, c0 = (r2 % ngg) * 4;
-            const double *Ci = sCi[w];
-            double acc[4] = {0., 0., 0., 0.};
-#pragma unroll 2
-            for (int u = 0; u <= i; ++u) {
-                const double av = Ci[i * KS + u];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[c] = fma(av, sGT[w][u * GS + c0 + c], acc[c]);
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) sY[w][i * GS + c0 + c] = acc[c];
         }
     }
     __syncthreads();
     stamp(2);
-    // updates of the even block: D_e -= V1^T V1 + U2^T U2 (lower), new
+    // C. updates of the even block: D_e -= V1^T V1 + U2^T U2 (lower), new
     // coupling -V1^T U1, G_e -= Y1^T V1 + Y2^T U2; stored factor columns of o2
-    const double *U1 = sP[0], *V1 = sP[1], *U2 = sP[2], *V2 = sP[3];
+    const double *U1 = sB[0], *V1 = sB[1], *U2 = sB[2], *V2 = sB[3];
+    const double *Y1 = sGT[0], *Y2 = sGT[1];
     double *De = bcr_blk(B.Dk, e, K);
     for (int q = tid; q < 2 * 4 * K; q += blockDim.x) {
         const int m = q / (4 * K), r = q % (4 * K), i = r / 4, c0 = (r % 4) * CG;
@@ -329,18 +356,18 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             double acc0 = 0., acc1 = 0.;
 #pragma unroll
             for (int u = 0; u < K; ++u) {
-                acc0 = fma(V1[u * KS + ft], sYv[0][u], acc0);
-                acc1 = fma(U2[u * KS + ft], sYv[1][u], acc1);
+                acc0 = fma(V1[u * KS + ft], sR[0][u], acc0);
+                acc1 = fma(U2[u * KS + ft], sR[1][u], acc1);
             }
             const int R = e * K + ft;
             if (R < B.nb) B.rw[R] = sR[2][ft] - (acc0 + acc1);
         } else if (h2 && ft >= 32 && ft < 32 + K) {
             const int i = ft - 32, R = o2 * K + i;
-            if (R < B.nb) y[R] = sYv[1][i];
+            if (R < B.nb) y[R] = sR[1][i];
         } else if (h2 && ft >= 64 && ft < 64 + nG) {
             const int q = ft - 64;
             double acc = 0.;
-            for (int u = 0; u < K; ++u) acc = fma(sY[1][u * GS + q], sYv[1][u], acc);
+            for (int u = 0; u < K; ++u) acc = fma(Y2[u * GS + q], sR[1][u], acc);
             B.gpart[(size_t)o2 * nG + q] = acc;
         }
     }
@@ -351,7 +378,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         for (int c = 0; c < CG; ++c) acc[c] = 0.;
 #pragma unroll 2
         for (int u = 0; u < K; ++u) {
-            const double y1 = sY[0][u * GS + qq], y2 = sY[1][u * GS + qq];
+            const double y1 = Y1[u * GS + qq], y2 = Y2[u * GS + qq];
 #pragma unroll
             for (int c = 0; c < CG; ++c)
                 acc[c] = fma(y1, V1[u * KS + c0 + c], fma(y2, U2[u * KS + c0 + c], acc[c]));
@@ -361,25 +388,27 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             B.Gk[((size_t)e * nG + qq) * K + c0 + c] = sGe[qq * K + c0 + c] - acc[c];
     }
     if (h2) {
+        // factor column of o2 for the solves: C with its diagonal replaced by
+        // 1 / C_jj, U2, V2 (K x K), Y2 (K x nG), and the corner term Y2^T Y2
         for (int q = tid; q < K * K; q += blockDim.x) {
             const int i = q / K, c = q % K;
-            bcr_blk(B.FC, o2, K)[q] = sCi[1][i * KS + c];
+            bcr_blk(B.FC, o2, K)[q] = (c == i) ? sRs[1][i] : sD[1][i * KS + c];
             bcr_blk(B.FU, o2, K)[q] = U2[i * KS + c];
             bcr_blk(B.FV, o2, K)[q] = V2[i * KS + c];
         }
         for (int q = tid; q < K * nG; q += blockDim.x) {
             const int i = q / nG, qq = q % nG;
-            B.FY[(size_t)o2 * K * nG + q] = sY[1][i * GS + qq];
+            B.FY[(size_t)o2 * K * nG + q] = Y2[i * GS + qq];
         }
         for (int q = tid; q < nG * nG; q += blockDim.x) {
             const int a = q / nG, c = q % nG;
             double acc = 0.;
-            for (int u = 0; u < K; ++u) acc = fma(sY[1][u * GS + a], sY[1][u * GS + c], acc);
+            for (int u = 0; u < K; ++u) acc = fma(Y2[u * GS + a], Y2[u * GS + c], acc);
             B.Zc[(size_t)o2 * nG * nG + q] = acc;
         }
     }
     stamp(3);
-    if (tid == 0 && bad_s) atomicOr(fail, 1);  // bad_s settled at the product barrier
+    if (tid == 0 && bad_s) atomicOr(fail, 1);  // bad_s settled at the solve barrier
 }
 
 // ---------------------------------------------------------------------------
@@ -444,43 +473,47 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
 // ---------------------------------------------------------------------------
 
 // Forward level: workgroup (64 lanes) per even block e; lanes 0..K-1 handle
-// o1 = e - s, lanes 32..32+K-1 handle o2 = e + s.  Every factor entry a lane
-// needs is loaded at entry (independent of r), so the only dependent global
-// load is r itself.
+// o1 = e - s, lanes 32..32+K-1 handle o2 = e + s.  y_o = C_o^-1 r_o by
+// substitution (row i of C in lane i's registers, y_t broadcast by
+// v_readlane); every factor entry is loaded at entry, so the only dependent
+// global load is r itself.
 template <int K>
 __global__ void __launch_bounds__(64) k_bcr_fwd(BcrDev B, int s, int nact, double *rw,
                                                 double *y) {
-    __shared__ double sr[2][K], sy[2][K], sp[2][K];
+    __shared__ double sy[2][K], sp[2][K];
     const int lane = threadIdx.x, h = lane >> 5, i = lane & 31;
     const int t = 2 * blockIdx.x, e = t * s;
     const bool h1 = t >= 2, h2 = t + 1 < nact;
     const int o = h ? e + s : e - s;
     const bool act = (h ? h2 : h1) && i < K;
     const int nb = B.nb, nG = B.nG;
-    double ci[K], cv[K];  // row i of C_o^-1; column i of V_o1 (h = 0) / U_o2 (h = 1)
+    double cr[K], cv[K];  // row i of C_o (diagonal 1/C_ii); column i of V_o1 / U_o2
+    double r = 0.;
     if (act) {
-        const double *Ci = bcr_blk(B.FC, o, K);
+        const double *Cf = bcr_blk(B.FC, o, K);
         const double *Vc = bcr_blk(h ? B.FU : B.FV, o, K);
 #pragma unroll
         for (int u = 0; u < K; ++u) {
-            ci[u] = u <= i ? Ci[i * K + u] : 0.;
+            cr[u] = u <= i ? Cf[i * K + u] : 0.;
             cv[u] = Vc[u * K + i];
         }
-        sr[h][i] = bcr_get(rw, o * K + i, nb);
-    }
-    __syncthreads();
-    double yv = 0.;
-    if (act) {
+        r = bcr_get(rw, o * K + i, nb);
+    } else {
 #pragma unroll
-        for (int u = 0; u < K; ++u) yv = fma(ci[u], sr[h][u], yv);
-        sy[h][i] = yv;
+        for (int u = 0; u < K; ++u) cr[u] = cv[u] = 0.;
     }
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        if (i == u) r *= cr[u];
+        const double y0 = bcr_rdlane(r, u), y1 = bcr_rdlane(r, 32 + u);
+        if (i > u) r = fma(-cr[u], h ? y1 : y0, r);
+    }
+    if (i < K) sy[h][i] = act ? r : 0.;
     __syncthreads();
     if (i < K) {
         double acc = 0.;
-        if (act)
 #pragma unroll
-            for (int u = 0; u < K; ++u) acc = fma(cv[u], sy[h][u], acc);
+        for (int u = 0; u < K; ++u) acc = fma(cv[u], sy[h][u], acc);
         sp[h][i] = acc;
     }
     __syncthreads();
@@ -489,7 +522,7 @@ __global__ void __launch_bounds__(64) k_bcr_fwd(BcrDev B, int s, int nact, doubl
         if (R < nb) rw[R] -= sp[0][lane] + sp[1][lane];
     }
     if (h2) {  // owner of o2: y and the arrow partial Y2^T y2
-        if (h == 1 && i < K && (e + s) * K + i < nb) y[(e + s) * K + i] = yv;
+        if (h == 1 && i < K && (e + s) * K + i < nb) y[(e + s) * K + i] = r;
         for (int q = lane; q < nG; q += 64) {
             const double *Y2 = B.FY + (size_t)(e + s) * K * nG;
             double acc = 0.;
@@ -547,48 +580,54 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_root(BcrDev B, const double *y, 
 }
 
 // Backward level: workgroup per odd block o (t = 2 blockIdx.x + 1):
-// x_o = C_o^-T (y_o - U_o x_{o-s} - V_o x_{o+s} - Y_o x_G).  Factor rows are
-// loaded at entry, before the (dependent) x loads.
+// x_o = C_o^-T (y_o - U_o x_{o-s} - V_o x_{o+s} - Y_o x_G), the last step by
+// back substitution (column i of C in lane i's registers).  Factor entries
+// are loaded at entry, before the (dependent) x loads.
 template <int K>
 __global__ void __launch_bounds__(64) k_bcr_bwd(BcrDev B, int s, int nact, const double *y,
                                                 double *x) {
-    __shared__ double sv[K], xg[NGMAX], xp[K], xn[K];
+    __shared__ double xg[NGMAX], xp[K], xn[K];
     const int lane = threadIdx.x;
     const int t = 2 * blockIdx.x + 1, o = t * s;
     const bool hn = t + 1 < nact;
     const int nb = B.nb, nG = B.nG;
-    double ur[K], vr[K], cc[K];  // row lane of U_o, V_o; column lane of C_o^-1
+    double ur[K], vr[K], cc[K];  // row lane of U_o, V_o; column lane of C_o (diag 1/C_ii)
     double yo = 0.;
     if (lane < K) {
         const double *U = bcr_blk(B.FU, o, K), *V = bcr_blk(B.FV, o, K);
-        const double *Ci = bcr_blk(B.FC, o, K);
+        const double *Cf = bcr_blk(B.FC, o, K);
 #pragma unroll
         for (int u = 0; u < K; ++u) {
             ur[u] = U[lane * K + u];
             vr[u] = hn ? V[lane * K + u] : 0.;
-            cc[u] = u >= lane ? Ci[u * K + lane] : 0.;
+            cc[u] = u >= lane ? Cf[u * K + lane] : 0.;
         }
         yo = bcr_get(y, o * K + lane, nb);
         xp[lane] = bcr_get(x, (o - s) * K + lane, nb);
         xn[lane] = hn ? bcr_get(x, (o + s) * K + lane, nb) : 0.;
+    } else {
+#pragma unroll
+        for (int u = 0; u < K; ++u) ur[u] = vr[u] = cc[u] = 0.;
     }
     if (lane < nG) xg[lane] = x[nb + lane];
     __syncthreads();
+    double v = 0.;
     if (lane < K) {
         const double *Y = B.FY + (size_t)o * K * nG;
-        double acc = yo;
+        v = yo;
 #pragma unroll
-        for (int u = 0; u < K; ++u) acc = fma(-ur[u], xp[u], fma(-vr[u], xn[u], acc));
-        for (int q = 0; q < nG; ++q) acc = fma(-Y[lane * nG + q], xg[q], acc);
-        sv[lane] = acc;
+        for (int u = 0; u < K; ++u) v = fma(-ur[u], xp[u], fma(-vr[u], xn[u], v));
+        for (int q = 0; q < nG; ++q) v = fma(-Y[lane * nG + q], xg[q], v);
     }
-    __syncthreads();
-    if (lane < K) {
-        double acc = 0.;
 #pragma unroll
-        for (int u = 0; u < K; ++u) acc = fma(cc[u], sv[u], acc);
+    for (int u = K - 1; u >= 0; --u) {
+        if (lane == u) v *= cc[u];
+        const double xu = bcr_rdlane(v, u);
+        if (lane < u) v = fma(-cc[u], xu, v);
+    }
+    if (lane < K) {
         const int R = o * K + lane;
-        if (R < nb) x[R] = acc;
+        if (R < nb) x[R] = v;
     }
 }
 

@@ -139,6 +139,11 @@ struct DevProblem {
     // bundle -> transform -> attribute tables.
     const int4 *bnd_p4;
     const double *brec;
+    // position of each observation in bundle order (bobs) and the bundle
+    // block records JB[8 * i] = [jx_a, jy_a] (a < 3), f_x, f_y written by
+    // k_jacobian (nullptr unless every solved bundle is fast and nG == 0)
+    const int *obs_bpos;
+    double *JB;
     // per camera lens parameter lists
     const int *cam_lpar_off, *cam_lpar;
     // parameters

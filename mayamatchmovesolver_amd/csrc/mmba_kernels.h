@@ -9,13 +9,17 @@ void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, doub
                        double *ext_pert, double *step, int solver_type, double delta,
                        double eps_dif);
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext);
-void launch_bnd_records(hipStream_t s, const DevProblem &P, const double *ext_pert,
-                        const double *step, double *brec, int base_only);
-void launch_cam_records(hipStream_t s, const DevProblem &P, const int *var_cf,
-                        const double *ext_pert, double *recs, int nvar, int base_only);
+// Camera-frame records (variant 0 only when base_only) and bundle records,
+// one launch.
+void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
+                    const double *ext_pert, const double *step, double *recs, int nvar,
+                    double *brec, int base_only);
 int residual_blocks(const DevProblem &P);
+// Reductions: with a ticket (a zero-initialised device counter) the partial
+// sums are combined inside the same launch, otherwise by a second kernel.
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
-                     double *ed, double *partial);
+                     double *ed, double *partial, double *out = nullptr,
+                     unsigned int *ticket = nullptr);
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed);
@@ -52,7 +56,7 @@ void launch_trsv_bwd_all(hipStream_t s, const double *S, const int *slot, int NT
                          double *x);
 void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
-                       int pc_uniform);
+                       int pc_uniform, int assign_off);
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs);
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
@@ -84,19 +88,23 @@ void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y)
 void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
 // mask (nullable): entries this shard owns
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                  int nparts, double *out, const int *mask = nullptr);
+                  int nparts, double *out, const int *mask = nullptr,
+                  unsigned int *ticket = nullptr);
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                      int nparts, double *out, const int *mask = nullptr);
+                      int nparts, double *out, const int *mask = nullptr,
+                      unsigned int *ticket = nullptr);
 void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out);
 void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
-                  double *partial, int nparts, double *out, const int *mask = nullptr);
+                  double *partial, int nparts, double *out, const int *mask = nullptr,
+                  unsigned int *ticket = nullptr);
 void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                      const int *nloc, const double *p, double *partial, int nparts,
-                     double *out);
+                     double *out, unsigned int *ticket = nullptr);
 void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mask,
-                      double *partial, int nparts, double *out);
-// *out = (*flag != 0) as a double (fail flags joining the scalar reads)
-void launch_flag_to_scalar(hipStream_t s, const int *flag, double *out);
+                      double *partial, int nparts, double *out, unsigned int *ticket = nullptr);
+// *out = (*flag != 0) as a double (fail flags joining the scalar reads);
+// the flag is cleared for the next use
+void launch_flag_to_scalar(hipStream_t s, int *flag, double *out);
 void launch_keep_rows(hipStream_t s, double *v, int lo, int hi, int nCF, int nR, int root);
 void launch_keep_mask(hipStream_t s, const double *src, const int *mask, int n, double *dst);
 void launch_lm_step(hipStream_t s, int n, const double *xs, const double *x, const double *diag,

@@ -17,6 +17,45 @@ MMBA_DEV bool own_cf(const DevProblem &P, int cf) { return !P.cf_own || P.cf_own
 MMBA_DEV bool own_bnd(const DevProblem &P, int b) { return !P.bnd_own || P.bnd_own[b]; }
 MMBA_DEV bool own_mask(const int *m, int i) { return !m || m[i]; }
 
+// Deterministic single-launch reduction epilogue (see the reductions section).
+template <bool MAX>
+__device__ __forceinline__ void finish_blocks(double v, double *partial, double *out,
+                                              unsigned int *ticket) {
+    __shared__ int last;
+    __shared__ double red[256];
+    if (threadIdx.x == 0) {
+        if (!ticket) {
+            partial[blockIdx.x] = v;
+        } else {
+            __hip_atomic_store(&partial[blockIdx.x], v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence();  // release the partial before the ticket
+            last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+        }
+    }
+    if (!ticket) return;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // acquire the other blocks' partials
+    double a = 0.;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
+        const double q = __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a = MAX ? fmax(a, q) : a + q;
+    }
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            red[threadIdx.x] = MAX ? fmax(red[threadIdx.x], red[threadIdx.x + w])
+                                   : red[threadIdx.x] + red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        *out = red[0];
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // -------------------------------------------------------------------------
 // Parameters: external values, FD perturbations (adjust_solveFunc.cpp:148-180,
 // cminpack fdjac2), setParameters (adjust_setParameters.cpp:174-250).
@@ -59,10 +98,10 @@ __global__ void k_set_attrs(DevProblem P, const double *__restrict__ ext) {
 // Camera-frame records: variant 0 = base, variant v = one cam-side parameter
 // perturbed (K0 in SURVEY 7).
 // -------------------------------------------------------------------------
-__global__ void k_cam_records(DevProblem P, const int *__restrict__ var_cf,
-                              const double *__restrict__ ext_pert, double *recs, int nvar,
-                              int base_only) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void cam_record_thread(const DevProblem &P, int t,
+                                                  const int *__restrict__ var_cf,
+                                                  const double *__restrict__ ext_pert,
+                                                  double *recs, int nvar, int base_only) {
     int cf, idx;
     if (base_only) {
         if (t >= P.ncf) return;
@@ -86,9 +125,10 @@ __global__ void k_cam_records(DevProblem P, const int *__restrict__ var_cf,
 // Bundle records (fast bundles, see DevProblem::bnd_p4): one thread per
 // bundle walks the bundle's transform/attribute tables once per evaluation.
 // -------------------------------------------------------------------------
-__global__ void k_bnd_records(DevProblem P, const double *__restrict__ ext_pert,
-                              const double *__restrict__ step, double *brec, int base_only) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void bnd_record_thread(const DevProblem &P, int b,
+                                                  const double *__restrict__ ext_pert,
+                                                  const double *__restrict__ step, double *brec,
+                                                  int base_only) {
     if (b >= P.nB) return;
     const int4 p4 = P.bnd_p4[b];
     if (p4.w < 0) return;
@@ -109,6 +149,20 @@ __global__ void k_bnd_records(DevProblem P, const double *__restrict__ ext_pert,
         br[5 + 3 * a] = bp[2];
         br[12 + a] = step[p];
     }
+}
+
+// Camera-frame and bundle records in one launch (both are short, latency-
+// bound chains; blocks [0, ncb) are camera records, the rest bundle records).
+__global__ void __launch_bounds__(64) k_records(DevProblem P, const int *__restrict__ var_cf,
+                                                const double *__restrict__ ext_pert,
+                                                const double *__restrict__ step, double *recs,
+                                                int nvar, double *brec, int base_only, int ncb) {
+    if ((int)blockIdx.x < ncb)
+        cam_record_thread(P, blockIdx.x * 64 + threadIdx.x, var_cf, ext_pert, recs, nvar,
+                          base_only);
+    else
+        bnd_record_thread(P, (blockIdx.x - ncb) * 64 + threadIdx.x, ext_pert, step, brec,
+                          base_only);
 }
 
 // Unperturbed bundle position of observation (b, frame f).
@@ -136,7 +190,8 @@ __device__ __forceinline__ bool obs_lens(const DevProblem &P, int cam, int &lens
 // -------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__restrict__ recs,
                                                   double *f, double *eu, double *ed,
-                                                  double *partial) {
+                                                  double *partial, double *out,
+                                                  unsigned int *ticket) {
     __shared__ double red[256];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double s = 0.;
@@ -170,7 +225,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    finish_blocks<false>(red[0], partial, out, ticket);
 }
 
 // -------------------------------------------------------------------------
@@ -209,6 +264,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     const int pstale = stale_param[fr];
     Resid rs = r0;
     int l = 0;
+    double ljx = 0., ljy = 0.;  // last emitted column (bundle block record)
     auto emit_s = [&](int p, const Resid &r, double st) {
         double jx, jy;
         if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
@@ -221,6 +277,8 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
         jcol[(size_t)l * M + i] = p;
+        ljx = jx;
+        ljy = jy;
         if (p == pstale) rs = r;
         ++l;
     };
@@ -240,11 +298,22 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     // bundle-side parameters not already covered by a camera variant
     if (p4.w >= 0) {  // fast bundle: perturbed positions from the record
         const double *br = &P.brec[(size_t)b * BREC];
+        double jb[8] = {0., 0., 0., 0., 0., 0., r0.ex, r0.ey};
         for (int a = 0; a < p4.w && l < LMAX; ++a) {
             const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
             const double bp[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
             emit_s(p, residual(rec0, bp, mx, my, sw, P.mode, P.image_width, hl, lc0),
                    br[12 + a]);
+            jb[2 * a] = ljx;
+            jb[2 * a + 1] = ljy;
+        }
+        // bundle block record, one 64-B record per observation (coalesced
+        // store; k_ne_bnd_jb gathers one record per observation of a bundle
+        // instead of 8 SoA rows): [jx_a, jy_a]_a, f_x, f_y
+        if (P.JB) {
+            double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)i * 8]);
+            dst[0] = make_double4(jb[0], jb[1], jb[2], jb[3]);
+            dst[1] = make_double4(jb[4], jb[5], jb[6], jb[7]);
         }
     }
     for (int q = p4.w >= 0 ? P.bnd_par_off[b + 1] : P.bnd_par_off[b];
@@ -427,6 +496,38 @@ __global__ void __launch_bounds__(64) k_ne_cf_u(DevProblem P, const double *__re
             g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
         }
     }
+}
+
+// Fast bundles, no global parameters: Abb and gB from the per-observation
+// block records, same summation order as k_ne_bnd.
+__global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, double *g) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.nB) return;
+    const int4 p4 = P.bnd_p4[b];
+    const int pb = p4.w;
+    if (pb <= 0) return;
+    double A[PBMAX][PBMAX] = {};
+    double gb[PBMAX] = {};
+    for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
+        const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)P.bobs[q] * 8]);
+        const double4 u = src[0], v = src[1];
+        const double jx[3] = {u.x, u.z, v.x}, jy[3] = {u.y, u.w, v.y};
+        const double fx = v.z, fy = v.w;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) A[a][c] += jx[a] * jx[c] + jy[a] * jy[c];
+            gb[a] += jx[a] * fx + jy[a] * fy;
+        }
+    }
+    double *Ab = &Abb[(size_t)b * 9];
+#pragma unroll
+    for (int a = 0; a < PBMAX; ++a)
+#pragma unroll
+        for (int c = 0; c < PBMAX; ++c) Ab[a * 3 + c] = (a < pb && c < pb) ? A[a][c] : 0.;
+    g[p4.x] = gb[0];
+    if (pb > 1) g[p4.y] = gb[1];
+    if (pb > 2) g[p4.z] = gb[2];
 }
 
 // Per bundle: Abb (pb x pb), gB, Abg (pb x nG).  One thread per bundle.
@@ -841,7 +942,7 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
                                                    const int2 *__restrict__ dest,
                                                    const int *__restrict__ dest_off,
                                                    const int2 *__restrict__ pairs,
-                                                   const SView V) {
+                                                   const SView V, int assign_off) {
     __shared__ double sA[3 * PCMAX][65];
     __shared__ double sB[3 * PCMAX][65];
     const int d = blockIdx.x;
@@ -883,8 +984,17 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
                         sA[a1 * 3 + 2][q] * sB[c1 * 3 + 2][q];
         __syncthreads();
     }
-    if (v0) *s_at(V, ri + a0, rj + c0) -= acc0;
-    if (v1) *s_at(V, ri + a1, rj + c1) -= acc1;
+    // off-diagonal camera-frame blocks have this single writer: with
+    // assign_off they are assigned (no zeroing of S needed between solves)
+    const bool asg = assign_off && cc.x != cc.y;
+    if (v0) {
+        double *d = s_at(V, ri + a0, rj + c0);
+        *d = asg ? -acc0 : *d - acc0;
+    }
+    if (v1) {
+        double *d = s_at(V, ri + a1, rj + c1);
+        *d = asg ? -acc1 : *d - acc1;
+    }
 }
 
 // Uniform camera-frame block size PC (every solved camera-frame has PC
@@ -897,7 +1007,7 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
                                                      const int2 *__restrict__ dest,
                                                      const int *__restrict__ dest_off,
                                                      const int2 *__restrict__ pairs,
-                                                     const SView V) {
+                                                     const SView V, int assign_off) {
     __shared__ double red[PC * PC][65];
     const int d = blockIdx.x;
     const int2 cc = dest[d];
@@ -930,7 +1040,10 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
         double v = 0.;
         for (int l = 0; l < 64; ++l) v += red[e][l];
         const int a = e / PC, c = e % PC;
-        if (ri + a >= rj + c) *s_at(V, ri + a, rj + c) -= v;
+        if (ri + a >= rj + c) {
+            double *d = s_at(V, ri + a, rj + c);
+            *d = (assign_off && cc.x != cc.y) ? -v : *d - v;  // see k_schur_dest
+        }
     }
 }
 
@@ -1022,7 +1135,8 @@ __global__ void __launch_bounds__(256) k_obs_wtx(DevProblem P, const double *__r
         const double xv = xR[r0 + a];
         for (int c = 0; c < 3; ++c) u[c] += W[(size_t)(a * 3 + c) * M + i] * xv;
     }
-    for (int c = 0; c < 3; ++c) U[(size_t)c * M + i] = u[c];
+    // one 32-B record per observation (coalesced; gathered per bundle)
+    reinterpret_cast<double4 *>(U)[i] = make_double4(u[0], u[1], u[2], 0.);
 }
 
 // x_b = Lb^-T (tb - sum_i u_i - Wg_b^T x_G), scatter to parameter order.
@@ -1038,8 +1152,10 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ U,
     const int nCF = P.nR - nG;
     double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
     for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-        const int i = P.bobs[q];
-        for (int c = 0; c < 3; ++c) s[c] -= U[(size_t)c * M + i];
+        const double4 u = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
+        s[0] -= u.x;
+        s[1] -= u.y;
+        s[2] -= u.z;
     }
     for (int q = 0; q < nG; ++q) {
         const double xv = xR[nCF + q];
@@ -1125,11 +1241,17 @@ __global__ void k_gather_R(DevProblem P, const double *__restrict__ v, double *v
 }
 
 // -------------------------------------------------------------------------
-// Vector helpers and deterministic two-pass reductions.
+// Vector helpers and deterministic reductions.  With a ticket the reduction
+// finishes in the same launch: every block publishes its partial (release),
+// takes a ticket, and the last block to arrive (acquire) combines all
+// partials in the same fixed order as the separate k_reduce_* kernel, then
+// resets the ticket (so the result is bit-identical to the two-launch form).
 // -------------------------------------------------------------------------
+
 __global__ void __launch_bounds__(256) k_sumsq(const double *__restrict__ a,
                                                const double *__restrict__ d, int n,
-                                               const int *__restrict__ mask, double *partial) {
+                                               const int *__restrict__ mask, double *partial,
+                                               double *out, unsigned int *ticket) {
     __shared__ double red[256];
     double s = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1143,12 +1265,13 @@ __global__ void __launch_bounds__(256) k_sumsq(const double *__restrict__ a,
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    finish_blocks<false>(red[0], partial, out, ticket);
 }
 
 __global__ void __launch_bounds__(256) k_sumsq_div(const double *__restrict__ a,
                                                    const double *__restrict__ d, int n,
-                                                   const int *__restrict__ mask, double *partial) {
+                                                   const int *__restrict__ mask, double *partial,
+                                                   double *out, unsigned int *ticket) {
     __shared__ double red[256];
     double s = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1162,7 +1285,7 @@ __global__ void __launch_bounds__(256) k_sumsq_div(const double *__restrict__ a,
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    finish_blocks<false>(red[0], partial, out, ticket);
 }
 
 __global__ void __launch_bounds__(256) k_reduce_sum(const double *__restrict__ partial, int n,
@@ -1183,7 +1306,8 @@ __global__ void __launch_bounds__(256) k_reduce_sum(const double *__restrict__ p
 __global__ void __launch_bounds__(256) k_gnorm(const double *__restrict__ g,
                                                const double *__restrict__ acnorm, int n,
                                                double fnorm, const int *__restrict__ mask,
-                                               double *partial) {
+                                               double *partial, double *out,
+                                               unsigned int *ticket) {
     __shared__ double red[256];
     double m = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1195,7 +1319,7 @@ __global__ void __launch_bounds__(256) k_gnorm(const double *__restrict__ g,
         if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    finish_blocks<true>(red[0], partial, out, ticket);
 }
 
 __global__ void k_reduce_max(const double *__restrict__ partial, int n, double *out) {
@@ -1216,7 +1340,8 @@ __global__ void __launch_bounds__(256) k_jp_sumsq(DevProblem P, const double *__
                                                   const int *__restrict__ jcol,
                                                   const int *__restrict__ nloc,
                                                   const double *__restrict__ p,
-                                                  double *partial) {
+                                                  double *partial, double *out,
+                                                  unsigned int *ticket) {
     __shared__ double red[256];
     const int M = P.M;
     double s = 0.;
@@ -1237,13 +1362,14 @@ __global__ void __launch_bounds__(256) k_jp_sumsq(DevProblem P, const double *__
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    finish_blocks<false>(red[0], partial, out, ticket);
 }
 
 // max over owned entries of [acnorm_j == 0] (MINPACK's rank test, nsing < n).
 __global__ void __launch_bounds__(256) k_zero_flag(const double *__restrict__ acnorm, int n,
                                                    const int *__restrict__ mask,
-                                                   double *partial) {
+                                                   double *partial, double *out,
+                                                   unsigned int *ticket) {
     __shared__ double red[256];
     double m = 0.;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
@@ -1254,7 +1380,7 @@ __global__ void __launch_bounds__(256) k_zero_flag(const double *__restrict__ ac
         if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    finish_blocks<true>(red[0], partial, out, ticket);
 }
 
 // Keep this shard's reduced-system rows [lo, hi) (and the global rows on the
@@ -1337,23 +1463,23 @@ void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, doub
     k_param_prep<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext, ext_pert, step, solver_type, delta,
                                                  eps_dif);
 }
-void launch_bnd_records(hipStream_t s, const DevProblem &P, const double *ext_pert,
-                        const double *step, double *brec, int base_only) {
-    if (P.nB > 0) k_bnd_records<<<nblk(P.nB, 256), 256, 0, s>>>(P, ext_pert, step, brec, base_only);
+void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
+                    const double *ext_pert, const double *step, double *recs, int nvar,
+                    double *brec, int base_only) {
+    const int ncb = nblk(base_only ? P.ncf : nvar, 64);
+    const int nbb = nblk(P.nB, 64);
+    if (ncb + nbb > 0)
+        k_records<<<ncb + nbb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
+                                           ncb);
 }
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);
 }
-void launch_cam_records(hipStream_t s, const DevProblem &P, const int *var_cf,
-                        const double *ext_pert, double *recs, int nvar, int base_only) {
-    const int n = base_only ? P.ncf : nvar;
-    if (n == 0) return;
-    k_cam_records<<<nblk(n, 64), 64, 0, s>>>(P, var_cf, ext_pert, recs, nvar, base_only);
-}
 int residual_blocks(const DevProblem &P) { return nblk(P.M, 256); }
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
-                     double *ed, double *partial) {
-    k_residual<<<nblk(P.M, 256), 256, 0, s>>>(P, recs, f, eu, ed, partial);
+                     double *ed, double *partial, double *out, unsigned int *ticket) {
+    k_residual<<<nblk(P.M, 256), 256, 0, s>>>(P, recs, f, eu, ed, partial, out, ticket);
+    if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, nblk(P.M, 256), out);
 }
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
@@ -1373,7 +1499,12 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
         else
             k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
     }
-    if (P.nB > 0) k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
+    if (P.nB > 0) {
+        if (P.JB)  // every solved bundle fast and no global parameters
+            k_ne_bnd_jb<<<nblk(P.nB, 256), 256, 0, s>>>(P, Abb, g);
+        else
+            k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
+    }
     if (P.nG > 0) {
         const int nb = nblk(P.M, glob_chunk);
         k_ne_glob<<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
@@ -1408,14 +1539,14 @@ void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, con
 }
 void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
-                       int pc_uniform) {
+                       int pc_uniform, int assign_off) {
     if (ndest <= 0) return;
     if (pc_uniform == 6)
-        k_schur_dest_u<6><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
+        k_schur_dest_u<6><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
     else if (pc_uniform == 7)
-        k_schur_dest_u<7><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
+        k_schur_dest_u<7><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
     else
-        k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V);
+        k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
 }
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs) {
@@ -1447,38 +1578,42 @@ void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double
     k_gather_R<<<nblk(n, 256), 256, 0, s>>>(P, v, vR, nRpad);
 }
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                  int nparts, double *out, const int *mask) {
-    k_sumsq<<<nparts, 256, 0, s>>>(a, d, n, mask, partial);
-    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+                  int nparts, double *out, const int *mask, unsigned int *ticket) {
+    k_sumsq<<<nparts, 256, 0, s>>>(a, d, n, mask, partial, out, ticket);
+    if (!ticket) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
-                      int nparts, double *out, const int *mask) {
-    k_sumsq_div<<<nparts, 256, 0, s>>>(a, d, n, mask, partial);
-    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+                      int nparts, double *out, const int *mask, unsigned int *ticket) {
+    k_sumsq_div<<<nparts, 256, 0, s>>>(a, d, n, mask, partial, out, ticket);
+    if (!ticket) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out) {
     k_reduce_sum<<<1, 256, 0, s>>>(partial, n, out);
 }
 void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
-                  double *partial, int nparts, double *out, const int *mask) {
-    k_gnorm<<<nparts, 256, 0, s>>>(g, acnorm, n, fnorm, mask, partial);
-    k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
+                  double *partial, int nparts, double *out, const int *mask,
+                  unsigned int *ticket) {
+    k_gnorm<<<nparts, 256, 0, s>>>(g, acnorm, n, fnorm, mask, partial, out, ticket);
+    if (!ticket) k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                      const int *nloc, const double *p, double *partial, int nparts,
-                     double *out) {
-    k_jp_sumsq<<<nparts, 256, 0, s>>>(P, J, jcol, nloc, p, partial);
-    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+                     double *out, unsigned int *ticket) {
+    k_jp_sumsq<<<nparts, 256, 0, s>>>(P, J, jcol, nloc, p, partial, out, ticket);
+    if (!ticket) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mask,
-                      double *partial, int nparts, double *out) {
-    k_zero_flag<<<nparts, 256, 0, s>>>(acnorm, n, mask, partial);
-    k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
+                      double *partial, int nparts, double *out, unsigned int *ticket) {
+    k_zero_flag<<<nparts, 256, 0, s>>>(acnorm, n, mask, partial, out, ticket);
+    if (!ticket) k_reduce_max<<<1, 256, 0, s>>>(partial, nparts, out);
 }
-__global__ void k_flag_to_scalar(const int *__restrict__ flag, double *out) {
-    if (threadIdx.x == 0) *out = *flag ? 1. : 0.;
+__global__ void k_flag_to_scalar(int *flag, double *out) {
+    if (threadIdx.x == 0) {
+        *out = *flag ? 1. : 0.;
+        *flag = 0;  // read-and-clear: ready for the next factorisation
+    }
 }
-void launch_flag_to_scalar(hipStream_t s, const int *flag, double *out) {
+void launch_flag_to_scalar(hipStream_t s, int *flag, double *out) {
     k_flag_to_scalar<<<1, 64, 0, s>>>(flag, out);
 }
 void launch_keep_rows(hipStream_t s, double *v, int lo, int hi, int nCF, int nR, int root) {

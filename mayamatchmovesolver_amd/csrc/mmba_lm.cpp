@@ -98,7 +98,7 @@ double Plan::reduce_read(int slot, ReduceOp op) {
 
 // ||D v||^2 over the parameters (each counted by the shard that owns it).
 void Plan::dnorm_enqueue(const double *dv, int slot) {
-    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + slot, d_p_own);
+    launch_sumsq(s, dv, d_diag, n, d_partial, nparts, d_scalar + slot, d_p_own, d_ticket);
     allreduce(d_scalar + slot, 1);
 }
 
@@ -111,12 +111,10 @@ double Plan::dnorm(const double *dv) {
 void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed) {
     launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
     launch_set_attrs(s, P, d_ext);
-    launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
-    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
+    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin();
-    launch_residual(s, P, d_recs, df, eu, ed, d_partial);
+    launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + SL_FNORM, d_ticket);
     span_end(SPAN_RESID);
-    launch_reduce_sum(s, d_partial, residual_blocks(P), d_scalar + SL_FNORM);
     allreduce(d_scalar + SL_FNORM, 1);
 }
 
@@ -134,8 +132,7 @@ void Plan::jac(const double *dx) {
     const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
     launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
     launch_set_attrs(s, P, d_ext);
-    launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 0);
-    launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 0);
+    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
     span_begin();
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                     d_stale, d_eu, d_ed);
@@ -151,26 +148,32 @@ void Plan::jac(const double *dx) {
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
 void Plan::solve_damped_enqueue(double lam) {
     const double t0 = wall_now();
-    MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));
+    // d_fail is zero here: launch_flag_to_scalar clears it after every use
     if (nB_solved > 0) {
         launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
         launch_schur_obs(s, P, d_J, d_Lb, d_W);
     }
     if (nR > 0) {
         const SView V = sview();
-        MMBA_HIP(hipMemsetAsync(d_rhs, 0, sizeof(double) * nRpad, s));
-        if (band) {
+        // unsharded, every rhs row is written by k_schur_init
+        if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_rhs, 0, sizeof(double) * nRpad, s));
+        // BCR leaves the band input untouched and every structural entry is
+        // rewritten (diagonal blocks by k_schur_init, off-diagonal blocks
+        // assigned by k_schur_dest, arrow rows by k_schur_init), so S is only
+        // zeroed once at plan build; the partitioned path factors in place
+        if (band && !bs.use_bcr) {
             const int nb = nR - nG;
             MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
             if (nG > 0) MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * (size_t)nG * nb, s));
             MMBA_HIP(hipMemsetAsync(bs.Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
-        } else {
+        } else if (!band) {
             MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         }
         launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
         if (nB_solved > 0) {
             if (use_dest) {
-                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V, pc_uniform);
+                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V, pc_uniform,
+                                  band && bs.use_bcr);
                 launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
                 launch_schur_glob(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
@@ -244,7 +247,8 @@ void Plan::newton_enqueue(double dxnorm) {
                 launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
             }
         }
-        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R, d_ymask);
+        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R, d_ymask,
+                     d_ticket);
     }
     allreduce(d_scalar + SL_NEWT_B, 2);
     t_linear += wall_now() - t0;
@@ -271,7 +275,7 @@ static double lmpar_ne(Plan &pl, double delta, double *par) {
     const bool newton0 = !pl.rank_deficient && ok0;
     if (newton0) pl.newton_enqueue(dxnorm);
     launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts,
-                     pl.d_scalar + Plan::SL_GDIV, pl.d_p_own);
+                     pl.d_scalar + Plan::SL_GDIV, pl.d_p_own, pl.d_ticket);
     pl.allreduce(pl.d_scalar + Plan::SL_GDIV, 1);
     pl.read_slots(Plan::SL_NEWT_B, Plan::SL_GDIV);
     if (newton0) {
@@ -360,8 +364,7 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_x, d_f, d_eu, d_ed);
     } else {
-        launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
-        launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
+        launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
     }
     std::vector<double> ed(Mg);
@@ -418,8 +421,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     double init_avg = 0., init_min = 0., init_max = 0.;
     if (opt.accept_only_better) {
         // measureErrors before any parameter is set (adjust_base.cpp:1080-1103)
-        launch_cam_records(s, P, d_var_cf, d_ext_pert, d_recs, nvar, 1);
-        launch_bnd_records(s, P, d_ext_pert, d_step, d_brec, 1);
+        launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
         download_ref_order(nullptr, nullptr, d_ed, nullptr, nullptr, ed_host.data());
         error_stats(ed_host.data(), Mg, &init_avg, &init_min, &init_max);
@@ -466,7 +468,8 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             jac_evals += n;
             if (lmdif) nfev += n;
             // rank deficiency from exactly-zero columns (MINPACK nsing < n)
-            launch_zero_flag(s, d_acnorm, n, d_p_own, d_partial, nparts, d_scalar + SL_ZERO);
+            launch_zero_flag(s, d_acnorm, n, d_p_own, d_partial, nparts, d_scalar + SL_ZERO,
+                             d_ticket);
             allreduce(d_scalar + SL_ZERO, 1, ReduceOp::Max);
             launch_diag_init(s, n, d_acnorm, d_diag, iter == 1, mode);
             // diag set from acnorm (mode 1) *before* the max() update in
@@ -475,7 +478,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             if (iter == 1) dnorm_enqueue(d_x, SL_XN2);
             if (fnorm != 0.) {
                 launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + SL_GNORM,
-                             d_p_own);
+                             d_p_own, d_ticket);
                 allreduce(d_scalar + SL_GNORM, 1, ReduceOp::Max);
             }
             {
@@ -499,11 +502,11 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 // ||D x_new|| are independent -- one synchronisation
                 launch_lm_step(s, n, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3);
                 launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + SL_PNORM,
-                             d_p_own);
+                             d_p_own, d_ticket);
                 allreduce(d_scalar + SL_PNORM, 1);
                 fun_enqueue(d_wa2, d_ftrial, d_eu, d_ed);
                 launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, d_partial, nparts,
-                                d_scalar + SL_JP);
+                                d_scalar + SL_JP, d_ticket);
                 allreduce(d_scalar + SL_JP, 1);
                 dnorm_enqueue(d_wa2, SL_XN2);
                 {

@@ -622,6 +622,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_pb = upload(bnd_pb);
     D.bnd_xoff = nullptr;
     D.bnd_p4 = upload(bnd_p4);
+    {
+        std::vector<int> bpos(M);
+        for (int q = 0; q < M; ++q) bpos[bobs[q]] = q;
+        D.obs_bpos = upload(bpos);
+        bool all_fast = nG == 0 && nB_solved > 0;
+        for (int b = 0; b < nB && all_fast; ++b)
+            if (bnd_pb[b] > 0 && bnd_p4[b].w < 0) all_fast = false;
+        D.JB = all_fast ? dalloc<double>((size_t)8 * M) : nullptr;
+    }
     d_brec = dalloc<double>((size_t)nB * BREC);
     D.brec = d_brec;
     D.bobs_off = upload(bobs_off);
@@ -712,7 +721,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_tb = dalloc<double>((size_t)nB * 3);
     d_Wg = dalloc<double>((size_t)nB * NGMAX * 3);
     d_W = dalloc<double>((size_t)PCMAX * 3 * (nB_solved > 0 ? M : 1));
-    d_U = dalloc<double>((size_t)3 * (nB_solved > 0 ? M : 1));
+    d_U = dalloc<double>((size_t)4 * (nB_solved > 0 ? M : 1));
     d_rhs = dalloc<double>(nRpad);
     d_yR = dalloc<double>(nRpad);
     d_xR = dalloc<double>(nRpad);
@@ -721,6 +730,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_partial = dalloc<double>(std::max(nparts, residual_blocks(P)));
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
+    MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));
+    // Single-launch reductions (finish_blocks) measured slower than the
+    // two-launch form on C4 (the 256-782 arrivals on one ticket plus the
+    // release fences cost more than the second launch), so they stay off.
+    d_ticket = nullptr;
     MMBA_HIP(hipMemsetAsync(d_Acg, 0, sizeof(double) * (size_t)ncf * PCMAX * NGMAX, s));
     MMBA_HIP(hipMemsetAsync(d_Agg, 0, sizeof(double) * (NGMAX * NGMAX + NGMAX), s));
     MMBA_HIP(hipMemsetAsync(d_Abg, 0, sizeof(double) * (size_t)nB * PBMAX * NGMAX, s));
@@ -751,6 +765,10 @@ void Plan::setup_band(int Pforce) {
             bs.Bd = dalloc<double>((size_t)nb * (w + 1));
             bs.Ga = dalloc<double>((size_t)nG * nb);
             bs.Gd = dalloc<double>(NGMAX * NGMAX);
+            // zeroed once: structural zeros of the band are never written
+            MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (w + 1), s));
+            MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * std::max<size_t>(1, (size_t)nG * nb), s));
+            MMBA_HIP(hipMemsetAsync(bs.Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
             BcrDev &B = bs.bcr;
             B.K = std::max(8, (w + 7) / 8 * 8);
             B.nb = nb;

@@ -116,6 +116,7 @@ struct Plan {
     double *d_partial = nullptr, *d_scalar = nullptr;
     double *d_gather = nullptr;  // outputs in reference order: f | eu | ed | x
     int *d_fail = nullptr;
+    unsigned int *d_ticket = nullptr;  // single-launch reduction ticket (zero between uses)
     double *h_scalar = nullptr;  // pinned
     int *h_fail = nullptr;       // pinned
 
