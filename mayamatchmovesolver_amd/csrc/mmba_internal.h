@@ -126,6 +126,11 @@ struct DevProblem {
     const int *cf_cam, *cf_frame, *cf_obs_off, *cf_var_off, *cf_var_param, *cf_var_flags;
     const int *cf_pc, *cf_roff;  // CF-block size and offset in R
     int pc_uniform;              // common CF-block size of solved camera-frames (0: mixed)
+    // Schur factors W_i (pc x 3 per observation) are stored per observation
+    // (AoS, wst doubles each: 3 * pc_uniform, else 3 * PCMAX) so the
+    // destination-sorted gathers of k_schur_dest read 2-3 cache lines per
+    // observation instead of one line per entry
+    int wst;
     // bundle-side parameter lists (B-class first, then bundle-side globals)
     const int *bnd_par_off, *bnd_par;
     const int *bnd_pb;     // B-block size
@@ -157,6 +162,10 @@ struct DevProblem {
     const int *obs_own, *cf_own, *bnd_own;
     int root, Ra, Rb;
 };
+
+__device__ __forceinline__ size_t widx(const DevProblem &P, int k, int i) {
+    return (size_t)i * P.wst + k;
+}
 
 __device__ __forceinline__ double *s_at(const SView &V, int R, int C) {
     if (!V.band) {

@@ -808,7 +808,7 @@ __global__ void k_schur_obs(DevProblem P, const double *__restrict__ J,
                 w[a] = t * il[a];  // zero for a >= pb
             }
 #pragma unroll
-            for (int a = 0; a < 3; ++a) W[((size_t)(r * 3 + a)) * M + i] = w[a];
+            for (int a = 0; a < 3; ++a) W[widx(P, r * 3 + a, i)] = w[a];
         }
     }
 }
@@ -889,8 +889,8 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
         const int pci = P.cf_pc[cfi];
         const int ri = P.cf_roff[cfi];
         for (int a = 0; a < pci; ++a) {
-            const double wa0 = W[(size_t)(a * 3) * M + i], wa1 = W[(size_t)(a * 3 + 1) * M + i],
-                         wa2 = W[(size_t)(a * 3 + 2) * M + i];
+            const double wa0 = W[widx(P, a * 3, i)], wa1 = W[widx(P, a * 3 + 1, i)],
+                         wa2 = W[widx(P, a * 3 + 2, i)];
             atomicAdd(&rhs[ri + a], -(wa0 * t0 + wa1 * t1 + wa2 * t2));
             for (int qj = q0; qj < q1; ++qj) {
                 const int j = P.bobs[qj];
@@ -900,9 +900,9 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
                 for (int c = 0; c < pcj; ++c) {
                     const int R = ri + a, C = rj + c;
                     if (R < C) continue;
-                    const double v = wa0 * W[(size_t)(c * 3) * M + j] +
-                                     wa1 * W[(size_t)(c * 3 + 1) * M + j] +
-                                     wa2 * W[(size_t)(c * 3 + 2) * M + j];
+                    const double v = wa0 * W[widx(P, c * 3, j)] +
+                                     wa1 * W[widx(P, c * 3 + 1, j)] +
+                                     wa2 * W[widx(P, c * 3 + 2, j)];
                     atomicAdd(s_at(V, R, C), -v);
                 }
             }
@@ -917,9 +917,9 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
             const int pcj = P.cf_pc[cfj];
             const int rj = P.cf_roff[cfj];
             for (int c = 0; c < pcj; ++c) {
-                const double v = wg[0] * W[(size_t)(c * 3) * M + j] +
-                                 wg[1] * W[(size_t)(c * 3 + 1) * M + j] +
-                                 wg[2] * W[(size_t)(c * 3 + 2) * M + j];
+                const double v = wg[0] * W[widx(P, c * 3, j)] +
+                                 wg[1] * W[widx(P, c * 3 + 1, j)] +
+                                 wg[2] * W[widx(P, c * 3 + 2, j)];
                 atomicAdd(s_at(V, nCF + q, rj + c), -v);
             }
         }
@@ -965,8 +965,8 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
         double ra[3 * PCMAX], rb[3 * PCMAX];
 #pragma unroll
         for (int k = 0; k < 3 * PCMAX; ++k) {  // issue every load before the stores
-            ra[k] = (lane < cnt && k < 3 * pci) ? W[(size_t)k * M + pr.x] : 0.;
-            rb[k] = (lane < cnt && k < 3 * pcj) ? W[(size_t)k * M + pr.y] : 0.;
+            ra[k] = (lane < cnt && k < 3 * pci) ? W[widx(P, k, pr.x)] : 0.;
+            rb[k] = (lane < cnt && k < 3 * pcj) ? W[widx(P, k, pr.y)] : 0.;
         }
 #pragma unroll
         for (int k = 0; k < 3 * PCMAX; ++k) {
@@ -1021,10 +1021,23 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
     for (int q = q0 + lane; q < q1; q += 64) {
         const int2 pr = pairs[q];
         double wi[3 * PC], wj[3 * PC];
+        if constexpr ((3 * PC) % 2 == 0) {  // wst = 3 PC: 16-B aligned records
+            const double2 *pi = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.x)]);
+            const double2 *pj = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.y)]);
 #pragma unroll
-        for (int k = 0; k < 3 * PC; ++k) {
-            wi[k] = W[k * M + pr.x];
-            wj[k] = W[k * M + pr.y];
+            for (int k = 0; k < 3 * PC / 2; ++k) {
+                const double2 a = pi[k], b = pj[k];
+                wi[2 * k] = a.x;
+                wi[2 * k + 1] = a.y;
+                wj[2 * k] = b.x;
+                wj[2 * k + 1] = b.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3 * PC; ++k) {
+                wi[k] = W[widx(P, k, pr.x)];
+                wj[k] = W[widx(P, k, pr.y)];
+            }
         }
 #pragma unroll
         for (int a = 0; a < PC; ++a)
@@ -1067,8 +1080,8 @@ __global__ void __launch_bounds__(64) k_schur_rhs(DevProblem P, const double *__
 #pragma unroll
         for (int a = 0; a < PCMAX; ++a)
             if (a < pc)
-                acc[a] += W[(size_t)(a * 3) * M + i] * t0 + W[(size_t)(a * 3 + 1) * M + i] * t1 +
-                          W[(size_t)(a * 3 + 2) * M + i] * t2;
+                acc[a] += W[widx(P, a * 3, i)] * t0 + W[widx(P, a * 3 + 1, i)] * t1 +
+                          W[widx(P, a * 3 + 2, i)] * t2;
     }
 #pragma unroll
     for (int a = 0; a < PCMAX; ++a) {
@@ -1104,9 +1117,9 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
             const int pcj = P.cf_pc[cfj];
             const int rj = P.cf_roff[cfj];
             for (int c = 0; c < pcj; ++c) {
-                const double v = wg[0] * W[(size_t)(c * 3) * M + j] +
-                                 wg[1] * W[(size_t)(c * 3 + 1) * M + j] +
-                                 wg[2] * W[(size_t)(c * 3 + 2) * M + j];
+                const double v = wg[0] * W[widx(P, c * 3, j)] +
+                                 wg[1] * W[widx(P, c * 3 + 1, j)] +
+                                 wg[2] * W[widx(P, c * 3 + 2, j)];
                 atomicAdd(s_at(V, nCF + q, rj + c), -v);
             }
         }
@@ -1133,7 +1146,7 @@ __global__ void __launch_bounds__(256) k_obs_wtx(DevProblem P, const double *__r
     double u[3] = {0., 0., 0.};
     for (int a = 0; a < pc; ++a) {
         const double xv = xR[r0 + a];
-        for (int c = 0; c < 3; ++c) u[c] += W[(size_t)(a * 3 + c) * M + i] * xv;
+        for (int c = 0; c < 3; ++c) u[c] += W[widx(P, a * 3 + c, i)] * xv;
     }
     // one 32-B record per observation (coalesced; gathered per bundle)
     reinterpret_cast<double4 *>(U)[i] = make_double4(u[0], u[1], u[2], 0.);
@@ -1215,7 +1228,7 @@ __global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
         const int r0 = P.cf_roff[cf];
         for (int a = 0; a < pc; ++a) {
             double s = 0.;
-            for (int c = 0; c < 3; ++c) s += W[(size_t)(a * 3 + c) * M + i] * u[c];
+            for (int c = 0; c < 3; ++c) s += W[widx(P, a * 3 + c, i)] * u[c];
             atomicAdd(&wR[r0 + a], -s);
         }
     }

@@ -617,6 +617,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.cf_pc = upload(cf_pc);
     D.cf_roff = upload(cf_roff);
     D.pc_uniform = pc_uniform;
+    D.wst = 3 * (pc_uniform > 0 ? pc_uniform : PCMAX);
     D.bnd_par_off = upload(bnd_par_off);
     D.bnd_par = upload(bnd_par);
     D.bnd_pb = upload(bnd_pb);
@@ -720,7 +721,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_Lb = dalloc<double>((size_t)nB * 9);
     d_tb = dalloc<double>((size_t)nB * 3);
     d_Wg = dalloc<double>((size_t)nB * NGMAX * 3);
-    d_W = dalloc<double>((size_t)PCMAX * 3 * (nB_solved > 0 ? M : 1));
+    d_W = dalloc<double>((size_t)P.wst * (nB_solved > 0 ? M : 1));
     d_U = dalloc<double>((size_t)4 * (nB_solved > 0 ? M : 1));
     d_rhs = dalloc<double>(nRpad);
     d_yR = dalloc<double>(nRpad);
