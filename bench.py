@@ -94,7 +94,7 @@ def broadcast_bytes(dist, data: bytes | None, n: int) -> bytes:
 
 # Kernels inside the K2 span (Plan::jac: span_begin .. span_end), i.e. the
 # launches whose HIP-event time is roofline.avg_ms.
-K2_REGEX = "k_jacobian|k_ne_|k_colnorms"
+K2_REGEX = "k_jacobian|k_ne_|k_colnorms|k_jac_epilogue"
 
 
 def pmc_traffic(args):

@@ -9,6 +9,36 @@ void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, doub
                        double *ext_pert, double *step, int solver_type, double delta,
                        double eps_dif);
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext);
+// launch_param_prep + launch_set_attrs in one launch
+void launch_param_set(hipStream_t s, const DevProblem &P, const double *x, double *ext,
+                      double *ext_pert, double *step, int solver_type, double delta,
+                      double eps_dif);
+// Partial rows -> scalar slots in one launch (row r: partial[off, off + n),
+// sum or max, -> scalar[slot]); flag (nullable) -> scalar[flag_slot], cleared.
+struct RedRow {
+    int off, n, is_max, slot;
+};
+struct RedSpec {
+    int nrows;
+    int flag_slot;
+    RedRow row[8];
+};
+void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
+                         double *scalar, int *flag = nullptr);
+// lmder bookkeeping after the normal equations (column norms, rank test, diag
+// update, ||D x||, gnorm): partial rows 0 / 1 / 2 (rstride apart, nparts each)
+void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
+                         const double *Abb, const double *aggbuf, double *acnorm, double *g,
+                         double *diag, const double *x, int first, int mode, double fnorm,
+                         int do_xn, int do_gn, const int *mask, double *partial, int nparts,
+                         int rstride);
+// lmder trial point x - xs with setParameters at it; partial rows 0 (pnorm^2)
+// and 1 (||D x_new||^2)
+void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
+                       const double *diag, double *wa1, double *wa2, double *wa3, double *ext,
+                       double *ext_pert, double *step, int solver_type, double delta,
+                       double eps_dif, const int *mask, double *partial, int nparts,
+                       int rstride);
 // Camera-frame records (variant 0 only when base_only) and bundle records,
 // one launch.
 void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,

@@ -60,13 +60,10 @@ __device__ __forceinline__ void finish_blocks(double v, double *partial, double 
 // Parameters: external values, FD perturbations (adjust_solveFunc.cpp:148-180,
 // cminpack fdjac2), setParameters (adjust_setParameters.cpp:174-250).
 // -------------------------------------------------------------------------
-__global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double *ext,
-                             double *ext_pert, double *step, int solver_type, double delta,
-                             double eps_dif) {
-    int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P.n) return;
+__device__ __forceinline__ void param_prep_one(const DevProblem &P, int p, double v, double *ext,
+                                               double *ext_pert, double *step, int solver_type,
+                                               double delta, double eps_dif) {
     const double xmin = P.p_min[p], xmax = P.p_max[p], off = P.p_off[p], sc = P.p_scale[p];
-    const double v = x[p];
     ext[p] = int_to_ext(v, xmin, xmax, off, sc);
     double xp;
     if (solver_type == MMBA_SOLVER_CMINPACK_LMDER) {
@@ -85,13 +82,36 @@ __global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double 
     ext_pert[p] = int_to_ext(xp, xmin, xmax, off, sc);
 }
 
-__global__ void k_set_attrs(DevProblem P, const double *__restrict__ ext) {
-    int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P.n) return;
+__device__ __forceinline__ void set_attr_one(const DevProblem &P, int p, double value) {
     const int a = P.p_attr[p];
     const int f = P.p_frame[p];
     const int64_t idx = P.attr_off[a] + (P.attr_anim[a] ? (f < 0 ? 0 : f) : 0);
-    P.attr_val[idx] = ext[p];
+    P.attr_val[idx] = value;
+}
+
+__global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double *ext,
+                             double *ext_pert, double *step, int solver_type, double delta,
+                             double eps_dif) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    param_prep_one(P, p, x[p], ext, ext_pert, step, solver_type, delta, eps_dif);
+}
+
+__global__ void k_set_attrs(DevProblem P, const double *__restrict__ ext) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    set_attr_one(P, p, ext[p]);
+}
+
+// setParameters in one launch: external value, FD perturbation and the
+// attribute write of each parameter (k_param_prep + k_set_attrs).
+__global__ void k_param_set(DevProblem P, const double *__restrict__ x, double *ext,
+                            double *ext_pert, double *step, int solver_type, double delta,
+                            double eps_dif) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    param_prep_one(P, p, x[p], ext, ext_pert, step, solver_type, delta, eps_dif);
+    set_attr_one(P, p, ext[p]);
 }
 
 // -------------------------------------------------------------------------
@@ -684,6 +704,145 @@ __global__ void k_colnorms(DevProblem P, const double *__restrict__ Acc,
     acnorm[p] = sqrt(d);
 }
 
+// Block tree reduction of one value per thread into partial[blockIdx.x]
+// (the order of k_sumsq / k_gnorm / k_zero_flag: bit-identical partials).
+template <bool MAX>
+__device__ __forceinline__ void block_partial(double v, double *red, double *partial) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            red[threadIdx.x] = MAX ? fmax(red[threadIdx.x], red[threadIdx.x + w])
+                                   : red[threadIdx.x] + red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// lmder bookkeeping after a Jacobian evaluation in one pass over the
+// parameters (lmder.c after qrfac; MINPACK's rank test):
+//   acnorm_p = sqrt(A_pp) and g_p of global parameters (k_colnorms);
+//   partial row 0: max over owned p of [acnorm_p == 0]           (k_zero_flag)
+//   diag update: mode 1, first pass diag = acnorm (1 where 0), then
+//   diag = max(diag, acnorm)                                      (k_diag_init)
+//   partial row 1: sum over owned p of (diag_p x_p)^2, do_xn      (xnorm)
+//   partial row 2: max over owned p with acnorm_p != 0 of
+//   |g_p / fnorm| / acnorm_p, do_gn                               (k_gnorm)
+// Rows are rstride apart, nparts = gridDim.x blocks each; every thread
+// accumulates in the grid-stride order of the separate kernels.
+__global__ void __launch_bounds__(256) k_jac_epilogue(
+    DevProblem P, const double *__restrict__ Acc, const double *__restrict__ Abb,
+    const double *__restrict__ Agg, const double *__restrict__ gG, double *acnorm, double *g,
+    double *diag, const double *__restrict__ x, int first, int mode, double fnorm, int do_xn,
+    int do_gn, const int *__restrict__ mask, double *partial, int rstride) {
+    __shared__ double red[256];
+    double zf = 0., xn = 0., gm = 0.;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.n; p += gridDim.x * blockDim.x) {
+        const int cls = P.p_class[p];
+        double d = 0.;
+        double gp;
+        if (cls == PC_CF) {
+            const int cf = P.p_blk[p];
+            const int a = P.p_pos[p] - P.cf_roff[cf];
+            d = Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + a];
+            gp = g[p];
+        } else if (cls == PC_B) {
+            const int b = P.p_blk[p];
+            const int a = P.p_pos[p];
+            d = Abb[(size_t)b * 9 + a * 3 + a];
+            gp = g[p];
+        } else {
+            const int gi = P.p_pos[p] - (P.nR - P.nG);
+            d = Agg[gi * NGMAX + gi];
+            gp = gG[gi];
+            g[p] = gp;
+        }
+        const double an = sqrt(d);
+        acnorm[p] = an;
+        double dg = diag[p];
+        if (mode != 2) {
+            if (first) dg = an == 0. ? 1. : an;
+            dg = fmax(dg, an);
+            diag[p] = dg;
+        }
+        if (own_mask(mask, p)) {
+            if (an == 0.) zf = 1.;
+            if (do_xn) {
+                const double v = dg * x[p];
+                xn += v * v;
+            }
+            if (do_gn && an != 0.) gm = fmax(gm, fabs((gp / fnorm) / an));
+        }
+    }
+    block_partial<true>(zf, red, partial);
+    __syncthreads();
+    block_partial<false>(xn, red, partial + rstride);
+    __syncthreads();
+    block_partial<true>(gm, red, partial + 2 * rstride);
+}
+
+// lmder trial point in one pass over the parameters: p = -xs,
+// wa1 = p, wa2 = x + p, wa3 = diag p (k_lm_step); setParameters at wa2
+// (k_param_prep + k_set_attrs); partial rows: 0 = sum (diag p)^2 (pnorm),
+// 1 = sum (diag wa2)^2 (the candidate ||D x||), over owned p.
+__global__ void __launch_bounds__(256) k_trial_prep(
+    DevProblem P, const double *__restrict__ xs, const double *__restrict__ x,
+    const double *__restrict__ diag, double *wa1, double *wa2, double *wa3, double *ext,
+    double *ext_pert, double *step, int solver_type, double delta, double eps_dif,
+    const int *__restrict__ mask, double *partial, int rstride) {
+    __shared__ double red[256];
+    double pn = 0., xn = 0.;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < P.n; j += gridDim.x * blockDim.x) {
+        const double st = -xs[j];
+        const double dj = diag[j];
+        const double xj = x[j] + st;
+        const double w3 = dj * st;
+        wa1[j] = st;
+        wa2[j] = xj;
+        wa3[j] = w3;
+        param_prep_one(P, j, xj, ext, ext_pert, step, solver_type, delta, eps_dif);
+        set_attr_one(P, j, ext[j]);
+        if (own_mask(mask, j)) {
+            pn += w3 * w3;
+            const double v = dj * xj;
+            xn += v * v;
+        }
+    }
+    block_partial<false>(pn, red, partial);
+    __syncthreads();
+    block_partial<false>(xn, red, partial + rstride);
+}
+
+// Several partial rows reduced in one launch, block r for row r, in the
+// order of k_reduce_sum / k_reduce_max; block 0 also converts the
+// factorisation fail flag to a scalar and clears it (k_flag_to_scalar).
+__global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__ partial,
+                                                      RedSpec spec, double *scalar, int *flag) {
+    __shared__ double red[256];
+    const RedRow rw = spec.row[blockIdx.x];
+    const bool mx = rw.is_max != 0;
+    double s = 0.;
+    for (int i = threadIdx.x; i < rw.n; i += blockDim.x) {
+        const double q = partial[rw.off + i];
+        s = mx ? fmax(s, q) : s + q;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            red[threadIdx.x] = mx ? fmax(red[threadIdx.x], red[threadIdx.x + w])
+                                  : red[threadIdx.x] + red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        scalar[rw.slot] = red[0];
+        if (blockIdx.x == 0 && flag && spec.flag_slot >= 0) {
+            scalar[spec.flag_slot] = *flag ? 1. : 0.;
+            *flag = 0;
+        }
+    }
+}
+
 // -------------------------------------------------------------------------
 // Damped system, bundle blocks: Abb + lam D^2 = Lb Lb^T (3x3), tb = Lb^-1 gb,
 // Wg_b = Abg^T Lb^-T (nG x pb).  At lam == 0 an exactly-zero diagonal (zero
@@ -879,7 +1038,7 @@ __global__ void k_schur_pairs(DevProblem P, const double *__restrict__ W,
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
     if (pb == 0) return;
-    const int M = P.M, nG = P.nG;
+    const int nG = P.nG;
     const int nCF = P.nR - nG;
     const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
     const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1], t2 = tb[(size_t)b * 3 + 2];
@@ -949,7 +1108,6 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
     const int2 cc = dest[d];
     const int pci = P.cf_pc[cc.x], pcj = P.cf_pc[cc.y];
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
-    const int M = P.M;
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
     const int lane = threadIdx.x;
     const int ne = pci * pcj;
@@ -1012,7 +1170,6 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
     const int d = blockIdx.x;
     const int2 cc = dest[d];
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
-    const size_t M = P.M;
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
     const int lane = threadIdx.x;
     double acc[PC * PC];
@@ -1069,7 +1226,6 @@ __global__ void __launch_bounds__(64) k_schur_rhs(DevProblem P, const double *__
     const int pc = P.cf_pc[cf];
     if (pc == 0 || !own_cf(P, cf)) return;
     const int r0 = P.cf_roff[cf];
-    const int M = P.M;
     double acc[PCMAX];
 #pragma unroll
     for (int a = 0; a < PCMAX; ++a) acc[a] = 0.;
@@ -1102,7 +1258,6 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
     const int pb = P.bnd_pb[b];
     const int nG = P.nG;
     if (pb == 0 || nG == 0) return;
-    const int M = P.M;
     const int nCF = P.nR - nG;
     const bool ownb = own_bnd(P, b);
     const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
@@ -1139,7 +1294,6 @@ __global__ void __launch_bounds__(256) k_obs_wtx(DevProblem P, const double *__r
                                                  const double *__restrict__ xR, double *U) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.M) return;
-    const int M = P.M;
     const int cf = P.obs_cf[i];
     const int pc = P.cf_pc[cf];
     const int r0 = P.cf_roff[cf];
@@ -1161,7 +1315,7 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ U,
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
     if (pb == 0) return;
-    const int M = P.M, nG = P.nG;
+    const int nG = P.nG;
     const int nCF = P.nR - nG;
     double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
     for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
@@ -1206,7 +1360,7 @@ __global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
         usq[b] = 0.;
         return;
     }
-    const int M = P.M, nG = P.nG;
+    const int nG = P.nG;
     const int nCF = P.nR - nG;
     const int po = P.bnd_par_off[b];
     const bool ownb = own_bnd(P, b);
@@ -1485,6 +1639,34 @@ void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
         k_records<<<ncb + nbb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
                                            ncb);
 }
+void launch_param_set(hipStream_t s, const DevProblem &P, const double *x, double *ext,
+                      double *ext_pert, double *step, int solver_type, double delta,
+                      double eps_dif) {
+    if (P.n == 0) return;
+    k_param_set<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext, ext_pert, step, solver_type, delta,
+                                                eps_dif);
+}
+void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
+                         const double *Abb, const double *aggbuf, double *acnorm, double *g,
+                         double *diag, const double *x, int first, int mode, double fnorm,
+                         int do_xn, int do_gn, const int *mask, double *partial, int nparts,
+                         int rstride) {
+    k_jac_epilogue<<<nparts, 256, 0, s>>>(P, Acc, Abb, aggbuf, aggbuf + NGMAX * NGMAX, acnorm,
+                                          g, diag, x, first, mode, fnorm, do_xn, do_gn, mask,
+                                          partial, rstride);
+}
+void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
+                       const double *diag, double *wa1, double *wa2, double *wa3, double *ext,
+                       double *ext_pert, double *step, int solver_type, double delta,
+                       double eps_dif, const int *mask, double *partial, int nparts,
+                       int rstride) {
+    k_trial_prep<<<nparts, 256, 0, s>>>(P, xs, x, diag, wa1, wa2, wa3, ext, ext_pert, step,
+                                        solver_type, delta, eps_dif, mask, partial, rstride);
+}
+void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
+                         double *scalar, int *flag) {
+    if (spec.nrows > 0) k_reduce_multi<<<spec.nrows, 256, 0, s>>>(partial, spec, scalar, flag);
+}
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);
 }
@@ -1593,7 +1775,7 @@ void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
                   int nparts, double *out, const int *mask, unsigned int *ticket) {
     k_sumsq<<<nparts, 256, 0, s>>>(a, d, n, mask, partial, out, ticket);
-    if (!ticket) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+    if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
                       int nparts, double *out, const int *mask, unsigned int *ticket) {
@@ -1613,7 +1795,7 @@ void launch_jp_sumsq(hipStream_t s, const DevProblem &P, const double *J, const 
                      const int *nloc, const double *p, double *partial, int nparts,
                      double *out, unsigned int *ticket) {
     k_jp_sumsq<<<nparts, 256, 0, s>>>(P, J, jcol, nloc, p, partial, out, ticket);
-    if (!ticket) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+    if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mask,
                       double *partial, int nparts, double *out, unsigned int *ticket) {

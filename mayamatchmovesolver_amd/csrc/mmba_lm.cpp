@@ -109,8 +109,7 @@ double Plan::dnorm(const double *dv) {
 
 // iflag = 1: setParameters + measureErrors; ||f||^2 -> SL_FNORM.
 void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed) {
-    launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
-    launch_set_attrs(s, P, d_ext);
+    launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin();
     launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + SL_FNORM, d_ticket);
@@ -127,11 +126,10 @@ double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
 }
 
 // iflag = 2: FD Jacobian blocks + normal equations + column norms at x.
-void Plan::jac(const double *dx) {
+void Plan::jac(const double *dx, const JacLM *lm) {
     const double t0 = wall_now();
     const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
-    launch_param_prep(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
-    launch_set_attrs(s, P, d_ext);
+    launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
     span_begin();
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
@@ -140,9 +138,51 @@ void Plan::jac(const double *dx) {
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
               d_glob_partial, glob_chunk);
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
-    launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
-    span_end(SPAN_JAC);
+    if (!lm) {
+        launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
+        span_end(SPAN_JAC);
+    } else {
+        const int do_xn = lm->first, do_gn = lm->fnorm != 0.;
+        launch_jac_epilogue(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g, d_diag, dx, lm->first,
+                            lm->mode, lm->fnorm, do_xn, do_gn, d_p_own, d_partial, nparts, pw);
+        span_end(SPAN_JAC);
+        RedSpec rs{};
+        rs.flag_slot = -1;
+        rs.row[rs.nrows++] = {0, nparts, 1, SL_ZERO};
+        if (do_xn) rs.row[rs.nrows++] = {pw, nparts, 0, SL_XN2};
+        if (do_gn) rs.row[rs.nrows++] = {2 * pw, nparts, 1, SL_GNORM};
+        launch_reduce_multi(s, d_partial, rs, d_scalar);
+        allreduce(d_scalar + SL_ZERO, 1, ReduceOp::Max);
+        if (do_xn) allreduce(d_scalar + SL_XN2, 1);
+        if (do_gn) allreduce(d_scalar + SL_GNORM, 1, ReduceOp::Max);
+    }
     t_jac += wall_now() - t0;
+}
+
+// Trial point x + p, p = -xs (lmder): one parameter pass (step, norms,
+// setParameters), measureErrors, ||J p||, one reduction launch.
+void Plan::trial_enqueue(double *eu, double *ed) {
+    const double t0 = wall_now();
+    double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
+    launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
+                      opt.solver_type, opt.delta, 1.0, d_p_own, pr, nparts, pw);
+    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+    span_begin();
+    launch_residual(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw);
+    span_end(SPAN_RESID);
+    launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, pr + 3 * (size_t)pw, nparts, nullptr);
+    RedSpec rs{};
+    rs.flag_slot = -1;
+    rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_PNORM};
+    rs.row[rs.nrows++] = {4 * pw, nparts, 0, SL_XN2T};
+    rs.row[rs.nrows++] = {5 * pw, residual_blocks(P), 0, SL_FNORM};
+    rs.row[rs.nrows++] = {6 * pw, nparts, 0, SL_JP};
+    launch_reduce_multi(s, d_partial, rs, d_scalar);
+    allreduce(d_scalar + SL_PNORM, 1);
+    allreduce(d_scalar + SL_XN2T, 1);
+    allreduce(d_scalar + SL_FNORM, 1);
+    allreduce(d_scalar + SL_JP, 1);
+    t_func += wall_now() - t0;
 }
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
@@ -256,19 +296,29 @@ void Plan::newton_enqueue(double dxnorm) {
 
 // lmpar restated on normal equations (see oracle/refcpu.c lmpar).  Every
 // decision point reads its scalars with one synchronisation.
-static double lmpar_ne(Plan &pl, double delta, double *par) {
+// pre: the undamped solve and its ||D x|| were enqueued and read already
+// (lmpar_first_enqueue); *undamped is set when lmpar returns that step.
+static void lmpar_first_enqueue(Plan &pl) {
+    pl.solve_damped_enqueue(0.0);
+    pl.dnorm_enqueue(pl.d_xs, Plan::SL_DNORM);
+}
+
+static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *undamped) {
     const double p1 = .1, p001 = .001;
     const double dwarf = DBL_MIN;
     double *h = pl.h_scalar;
     int iter = 0;
-    pl.solve_damped_enqueue(0.0);
-    pl.dnorm_enqueue(pl.d_xs, Plan::SL_DNORM);
-    pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+    *undamped = false;
+    if (!pre) {
+        lmpar_first_enqueue(pl);
+        pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+    }
     const bool ok0 = h[Plan::SL_FAIL] == 0.;
     double dxnorm = ok0 ? std::sqrt(h[Plan::SL_DNORM]) : HUGE_VAL;
     double fp = dxnorm - delta;
     if (fp <= p1 * delta) {
         if (iter == 0) *par = 0.;
+        *undamped = true;
         return dxnorm;
     }
     double parl = 0.;
@@ -463,27 +513,27 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 goto TERMINATE;
             }
             if (cb && cb->progress) cb->progress(cb->user, njev);
-            jac(d_x);
+            {
+                const JacLM lm{iter == 1, mode, fnorm};
+                jac(d_x, &lm);
+            }
             ++njev;
             jac_evals += n;
             if (lmdif) nfev += n;
-            // rank deficiency from exactly-zero columns (MINPACK nsing < n)
-            launch_zero_flag(s, d_acnorm, n, d_p_own, d_partial, nparts, d_scalar + SL_ZERO,
-                             d_ticket);
-            allreduce(d_scalar + SL_ZERO, 1, ReduceOp::Max);
-            launch_diag_init(s, n, d_acnorm, d_diag, iter == 1, mode);
-            // diag set from acnorm (mode 1) *before* the max() update in
-            // lmder; both happen before xnorm only on the first pass, and
-            // max(diag, acnorm) == acnorm there, so one kernel suffices.
-            if (iter == 1) dnorm_enqueue(d_x, SL_XN2);
-            if (fnorm != 0.) {
-                launch_gnorm(s, d_g, d_acnorm, n, fnorm, d_partial, nparts, d_scalar + SL_GNORM,
-                             d_p_own, d_ticket);
-                allreduce(d_scalar + SL_GNORM, 1, ReduceOp::Max);
-            }
+            // lmpar always starts from the undamped (Gauss-Newton) step of
+            // the new Jacobian, and when that step lies inside the trust
+            // region (the common case: spec_ok says the last lmpar took it)
+            // the trial point is x - xs0.  Both are enqueued behind the
+            // Jacobian before the host has seen gnorm / delta, so the whole
+            // outer iteration needs one synchronisation; a speculative
+            // trial that lmpar does not take is discarded (its errorList /
+            // errorDistanceList went to d_eu_s / d_ed_s).
+            lmpar_first_enqueue(*this);
+            const bool spec = spec_ok;
+            if (spec) trial_enqueue(d_eu_s, d_ed_s);
             {
                 const double t0 = wall_now();
-                read_slots(SL_ZERO, SL_XN2);
+                read_slots(SL_FNORM, SL_XN2T);
                 t_jac += wall_now() - t0;
             }
             rank_deficient = h_scalar[SL_ZERO] != 0.;
@@ -495,25 +545,25 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             gnorm = fnorm != 0. ? h_scalar[SL_GNORM] : 0.;
             if (gnorm <= gtol) info = 4;
             if (info != 0) goto TERMINATE;
+            bool pre = true;
             do {
-                const double dxn = lmpar_ne(*this, delta, &par);
+                bool undamped = false;
+                const double dxn = lmpar_ne(*this, delta, &par, pre, &undamped);
                 (void)dxn;
-                // trial point: ||D p||, f(x + p), ||J p|| and the candidate
-                // ||D x_new|| are independent -- one synchronisation
-                launch_lm_step(s, n, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3);
-                launch_sumsq(s, d_wa3, nullptr, n, d_partial, nparts, d_scalar + SL_PNORM,
-                             d_p_own, d_ticket);
-                allreduce(d_scalar + SL_PNORM, 1);
-                fun_enqueue(d_wa2, d_ftrial, d_eu, d_ed);
-                launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, d_partial, nparts,
-                                d_scalar + SL_JP, d_ticket);
-                allreduce(d_scalar + SL_JP, 1);
-                dnorm_enqueue(d_wa2, SL_XN2);
-                {
+                if (pre) spec_ok = undamped;
+                if (pre && spec && undamped) {
+                    // the speculative trial is lmder's trial point
+                    std::swap(d_eu, d_eu_s);
+                    std::swap(d_ed, d_ed_s);
+                } else {
+                    // trial point: ||D p||, f(x + p), ||J p|| and the
+                    // candidate ||D x_new|| -- one synchronisation
+                    trial_enqueue(d_eu, d_ed);
                     const double t0 = wall_now();
-                    read_slots(SL_FNORM, SL_XN2);
+                    read_slots(SL_FNORM, SL_XN2T);
                     t_func += wall_now() - t0;
                 }
+                pre = false;
                 const double pnorm = std::sqrt(h_scalar[SL_PNORM]);
                 if (iter == 1) delta = std::min(delta, pnorm);
                 const double fnorm1 = std::sqrt(h_scalar[SL_FNORM]);
@@ -548,7 +598,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     MMBA_HIP(hipMemcpyAsync(d_x, d_wa2, sizeof(double) * n,
                                             hipMemcpyDeviceToDevice, s));
                     std::swap(d_f, d_ftrial);
-                    xnorm = std::sqrt(h_scalar[SL_XN2]);  // ||D wa2||, computed above
+                    xnorm = std::sqrt(h_scalar[SL_XN2T]);  // ||D wa2||, computed above
                     fnorm = fnorm1;
                     ++iter;
                 }

@@ -707,6 +707,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_ftrial = dalloc<double>(m);
     d_eu = dalloc<double>(m);
     d_ed = dalloc<double>(M);
+    d_eu_s = dalloc<double>(m);
+    d_ed_s = dalloc<double>(M);
     d_recs = dalloc<double>((size_t)nvar * CAMREC);
     d_J = dalloc<double>((size_t)2 * LMAX * M);
     d_jcol = dalloc<int>((size_t)LMAX * M);
@@ -728,7 +730,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_xR = dalloc<double>(nRpad);
     d_wR = dalloc<double>(nRpad);
     d_usq = dalloc<double>(nB);
-    d_partial = dalloc<double>(std::max(nparts, residual_blocks(P)));
+    pw = std::max(nparts, residual_blocks(P));
+    d_partial = dalloc<double>((size_t)8 * pw);
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
     MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));

@@ -185,7 +185,8 @@ struct Plan {
         SL_FAIL = 8,    // factorisation failed (max)
         SL_PNORM = 9,   // ||D p||^2 of the trial step
         SL_JP = 10,     // ||J p||^2
-        SL_XN2 = 11,    // ||D x||^2 (current or candidate x)
+        SL_XN2 = 11,    // ||D x||^2 (first pass)
+        SL_XN2T = 12,   // ||D x_new||^2 of the trial point
         NSLOT = 16
     };
     void read_slots(int lo, int hi);  // [lo, hi] inclusive, one D2H copy + sync
@@ -194,7 +195,23 @@ struct Plan {
     double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
     void fun_enqueue(const double *dx, double *df, double *eu, double *ed);
     double fun(const double *dx, double *df, double *eu, double *ed);
-    void jac(const double *dx);
+    // with lm: the lmder bookkeeping after the normal equations is fused
+    // into the column-norm launch (k_jac_epilogue); scalars -> SL_ZERO,
+    // SL_XN2 (first pass), SL_GNORM (fnorm != 0)
+    struct JacLM {
+        int first, mode;
+        double fnorm;
+    };
+    void jac(const double *dx, const JacLM *lm = nullptr);
+    // trial point x - xs: setParameters, measureErrors into (d_ftrial, eu,
+    // ed), ||J p||; scalars -> SL_PNORM, SL_XN2T, SL_FNORM, SL_JP
+    void trial_enqueue(double *eu, double *ed);
+    // speculative trial (lmpar's first, undamped, step taken before the
+    // host has read it): its errorList / errorDistanceList land here and are
+    // swapped in when lmpar accepts that step
+    double *d_eu_s = nullptr, *d_ed_s = nullptr;
+    bool spec_ok = true;  // last lmpar accepted its undamped step
+    int pw = 0;           // partial-row stride of d_partial (8 rows)
     void solve_damped_enqueue(double lam);
     bool solve_damped(double lam);
     void newton_enqueue(double dxnorm);
