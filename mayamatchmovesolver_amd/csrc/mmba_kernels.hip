@@ -926,49 +926,68 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
     }
 }
 
-// W_i = (J_c(i)^T J_b(i)) Lb^-T per observation (PCMAX x 3, SoA over i).
-__global__ void k_schur_obs(DevProblem P, const double *__restrict__ J,
-                            const double *__restrict__ Lb, double *W) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.M) return;
-    const int M = P.M;
-    const int b = P.obs_bnd[i];
-    const int pb = P.bnd_pb[b];
-    if (pb == 0) return;
-    const int cf = P.obs_cf[i];
-    const int pc = P.cf_pc[cf];
-    const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
-    // every index static (no scratch): bundle columns a < pb, camera rows r < pc
-    double bx[3], by[3], L[3][3], il[3];
+// W_i = (J_c(i)^T J_b(i)) Lb^-T per observation (pc x 3, AoS rows of wst
+// doubles).  One wave per 64 consecutive observations: the rows are built in
+// LDS and the wave's contiguous 64 wst-double chunk is stored coalesced
+// (zeros where a row has no bundle block / no camera block).
+__global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__restrict__ J,
+                                                  const double *__restrict__ Lb, double *W) {
+    __shared__ double sw[64 * 3 * PCMAX];
+    const int lane = threadIdx.x;
+    const int i0 = blockIdx.x * 64;
+    const int i = i0 + lane;
+    const int M = P.M, wst = P.wst;
+    double *row = &sw[lane * wst];
+    for (int k = 0; k < wst; ++k) row[k] = 0.;
+    const int b = i < M ? P.obs_bnd[i] : 0;
+    const int pb = i < M ? P.bnd_pb[b] : 0;
+    if (pb > 0) {
+        const int cf = P.obs_cf[i];
+        const int pc = min(P.cf_pc[cf], wst / 3);
+        const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
+        // every index static (no scratch): bundle columns a < pb, camera rows r < pc
+        double bx[3], by[3], L[3][3], il[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        bx[a] = a < pb ? J[(size_t)(2 * (s + a)) * M + i] : 0.;
-        by[a] = a < pb ? J[(size_t)(2 * (s + a) + 1) * M + i] : 0.;
+        for (int a = 0; a < 3; ++a) {
+            bx[a] = a < pb ? J[(size_t)(2 * (s + a)) * M + i] : 0.;
+            by[a] = a < pb ? J[(size_t)(2 * (s + a) + 1) * M + i] : 0.;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) il[a] = a < pb ? 1.0 / L[a][a] : 0.;
-    double cx[PCMAX], cy[PCMAX];
-#pragma unroll
-    for (int r = 0; r < PCMAX; ++r) {  // every load issued before the solves
-        cx[r] = r < pc ? J[(size_t)(2 * r) * M + i] : 0.;
-        cy[r] = r < pc ? J[(size_t)(2 * r + 1) * M + i] : 0.;
-    }
-#pragma unroll
-    for (int r = 0; r < PCMAX; ++r) {
-        if (r < pc) {
-            double w[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                double t = cx[r] * bx[a] + cy[r] * by[a];
-#pragma unroll
-                for (int k = 0; k < a; ++k) t -= L[a][k] * w[k];
-                w[a] = t * il[a];  // zero for a >= pb
-            }
-#pragma unroll
-            for (int a = 0; a < 3; ++a) W[widx(P, r * 3 + a, i)] = w[a];
+            for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
         }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) il[a] = a < pb ? 1.0 / L[a][a] : 0.;
+        double cx[PCMAX], cy[PCMAX];
+#pragma unroll
+        for (int r = 0; r < PCMAX; ++r) {  // every load issued before the solves
+            cx[r] = r < pc ? J[(size_t)(2 * r) * M + i] : 0.;
+            cy[r] = r < pc ? J[(size_t)(2 * r + 1) * M + i] : 0.;
+        }
+#pragma unroll
+        for (int r = 0; r < PCMAX; ++r) {
+            if (r < pc) {
+                double w[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    double t = cx[r] * bx[a] + cy[r] * by[a];
+#pragma unroll
+                    for (int k = 0; k < a; ++k) t -= L[a][k] * w[k];
+                    w[a] = t * il[a];  // zero for a >= pb
+                }
+#pragma unroll
+                for (int a = 0; a < 3; ++a) row[r * 3 + a] = w[a];
+            }
+        }
+    }
+    __syncthreads();
+    const int nrow = min(64, M - i0);
+    const size_t base = (size_t)i0 * wst;
+    if (wst % 2 == 0) {
+        const int nv = nrow * wst / 2;
+        double2 *dst = reinterpret_cast<double2 *>(&W[base]);
+        const double2 *src = reinterpret_cast<const double2 *>(sw);
+        for (int k = lane; k < nv; k += 64) dst[k] = src[k];
+    } else {
+        for (int k = lane; k < nrow * wst; k += 64) W[base + k] = sw[k];
     }
 }
 
@@ -1156,26 +1175,28 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
 }
 
 // Uniform camera-frame block size PC (every solved camera-frame has PC
-// parameters, e.g. 6 for pose-only BA): lane q accumulates the full PC x PC
-// product of the pairs q, q + 64, ... in registers (coalesced SoA loads, no
-// LDS in the loop), then the 64 partial blocks are summed through LDS in a
-// fixed order (deterministic).
-template <int PC>
-__global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
-                                                     const int2 *__restrict__ dest,
-                                                     const int *__restrict__ dest_off,
-                                                     const int2 *__restrict__ pairs,
-                                                     const SView V, int assign_off) {
-    __shared__ double red[PC * PC][65];
+// parameters, e.g. 6 for pose-only BA): NW waves per destination block; lane
+// q of the workgroup accumulates the full PC x PC product of the pairs q,
+// q + 64 NW, ... in registers (the W records are 16-B aligned AoS rows), each
+// wave folds its 64 partial blocks with a fixed xor-shuffle tree and the NW
+// wave results are summed in wave order (deterministic).
+template <int PC, int NW>
+__global__ void __launch_bounds__(64 * NW) k_schur_dest_u(DevProblem P,
+                                                          const double *__restrict__ W,
+                                                          const int2 *__restrict__ dest,
+                                                          const int *__restrict__ dest_off,
+                                                          const int2 *__restrict__ pairs,
+                                                          const SView V, int assign_off) {
+    __shared__ double red[PC * PC][NW];
     const int d = blockIdx.x;
     const int2 cc = dest[d];
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double acc[PC * PC];
 #pragma unroll
     for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
-    for (int q = q0 + lane; q < q1; q += 64) {
+    for (int q = q0 + tid; q < q1; q += 64 * NW) {
         const int2 pr = pairs[q];
         double wi[3 * PC], wj[3 * PC];
         if constexpr ((3 * PC) % 2 == 0) {  // wst = 3 PC: 16-B aligned records
@@ -1204,15 +1225,22 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
                                    wi[a * 3 + 2] * wj[c * 3 + 2];
     }
 #pragma unroll
-    for (int e = 0; e < PC * PC; ++e) red[e][lane] = acc[e];
+    for (int e = 0; e < PC * PC; ++e) {
+        double v = acc[e];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[e][wv] = v;
+    }
     __syncthreads();
-    for (int e = lane; e < PC * PC; e += 64) {
-        double v = 0.;
-        for (int l = 0; l < 64; ++l) v += red[e][l];
+    if (tid < PC * PC) {
+        const int e = tid;
+        double v = red[e][0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v += red[e][w];
         const int a = e / PC, c = e % PC;
         if (ri + a >= rj + c) {
-            double *d = s_at(V, ri + a, rj + c);
-            *d = (assign_off && cc.x != cc.y) ? -v : *d - v;  // see k_schur_dest
+            double *dd = s_at(V, ri + a, rj + c);
+            *dd = (assign_off && cc.x != cc.y) ? -v : *dd - v;  // see k_schur_dest
         }
     }
 }
@@ -1287,20 +1315,37 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
     }
 }
 
-// u_i = W_i^T x_cf(i) per observation (3 SoA rows, coalesced over i), so the
-// per-bundle back substitution gathers 3 values per observation instead of
-// the 3 x pc of W_i.
-__global__ void __launch_bounds__(256) k_obs_wtx(DevProblem P, const double *__restrict__ W,
-                                                 const double *__restrict__ xR, double *U) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.M) return;
+// u_i = W_i^T x_cf(i) per observation, so the per-bundle back substitution
+// gathers 3 values per observation instead of the 3 x pc of W_i.  One wave
+// per 64 consecutive observations: their contiguous W rows are loaded
+// coalesced into LDS first.
+__global__ void __launch_bounds__(64) k_obs_wtx(DevProblem P, const double *__restrict__ W,
+                                                const double *__restrict__ xR, double *U) {
+    __shared__ double sw[64 * 3 * PCMAX];
+    const int lane = threadIdx.x;
+    const int i0 = blockIdx.x * 64;
+    const int i = i0 + lane;
+    const int M = P.M, wst = P.wst;
+    const int nrow = min(64, M - i0);
+    const size_t base = (size_t)i0 * wst;
+    if (wst % 2 == 0) {
+        const int nv = nrow * wst / 2;
+        const double2 *src = reinterpret_cast<const double2 *>(&W[base]);
+        double2 *dst = reinterpret_cast<double2 *>(sw);
+        for (int k = lane; k < nv; k += 64) dst[k] = src[k];
+    } else {
+        for (int k = lane; k < nrow * wst; k += 64) sw[k] = W[base + k];
+    }
+    __syncthreads();
+    if (i >= M) return;
     const int cf = P.obs_cf[i];
-    const int pc = P.cf_pc[cf];
+    const int pc = min(P.cf_pc[cf], wst / 3);
     const int r0 = P.cf_roff[cf];
+    const double *row = &sw[lane * wst];
     double u[3] = {0., 0., 0.};
     for (int a = 0; a < pc; ++a) {
         const double xv = xR[r0 + a];
-        for (int c = 0; c < 3; ++c) u[c] += W[widx(P, a * 3 + c, i)] * xv;
+        for (int c = 0; c < 3; ++c) u[c] += row[a * 3 + c] * xv;
     }
     // one 32-B record per observation (coalesced; gathered per bundle)
     reinterpret_cast<double4 *>(U)[i] = make_double4(u[0], u[1], u[2], 0.);
@@ -1719,7 +1764,7 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
 }
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
                       double *W) {
-    k_schur_obs<<<nblk(P.M, 128), 128, 0, s>>>(P, J, Lb, W);
+    k_schur_obs<<<nblk(P.M, 64), 64, 0, s>>>(P, J, Lb, W);
 }
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
@@ -1737,9 +1782,9 @@ void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, cons
                        int pc_uniform, int assign_off) {
     if (ndest <= 0) return;
     if (pc_uniform == 6)
-        k_schur_dest_u<6><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
+        k_schur_dest_u<6, 4><<<ndest, 256, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
     else if (pc_uniform == 7)
-        k_schur_dest_u<7><<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
+        k_schur_dest_u<7, 4><<<ndest, 256, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
     else
         k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
 }
@@ -1757,7 +1802,7 @@ void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, 
                            const double *tb, const double *Lb, const double *xR, double *U,
                            double *x) {
     if (P.nB == 0) return;
-    k_obs_wtx<<<nblk(P.M, 256), 256, 0, s>>>(P, W, xR, U);
+    k_obs_wtx<<<nblk(P.M, 64), 64, 0, s>>>(P, W, xR, U);
     k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, U, Wg, tb, Lb, xR, x);
 }
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x) {
