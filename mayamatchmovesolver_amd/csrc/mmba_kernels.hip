@@ -370,6 +370,99 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     }
 }
 
+// Uniform fast case of k_jacobian (every camera-frame has at most NCV
+// camera-side variants, no bundle-side variants, every solved bundle is a
+// fast bundle, no lens): the same residuals and differences, but every
+// index and record load is issued up front and the NCV + 3 perturbed
+// residuals are independent straight-line code, so their fp64 latency
+// chains overlap (the generic loop serialises them behind its dependent
+// variant-table loads).  Emits columns in the generic kernel's order.
+template <int NCV>
+__global__ void __launch_bounds__(128) k_jacobian_u(DevProblem P, const double *__restrict__ recs,
+                                                    const double *__restrict__ step,
+                                                    int solver_type, double *J, int *jcol,
+                                                    int *nloc, const int *__restrict__ stale_param,
+                                                    double *eu, double *ed) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    const int M = P.M;
+    const int cf = P.obs_cf[i];
+    const int b = P.obs_bnd[i];
+    const int fr = P.obs_frame[i];
+    const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
+    const int4 p4 = P.bnd_p4[b];
+    const int voff = P.cf_var_off[cf];
+    const int nv = min(P.cf_var_off[cf + 1] - voff - 1, NCV);
+    const int pstale = stale_param[fr];
+    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
+    int pv[NCV];
+    double st[NCV + 3];
+#pragma unroll
+    for (int v = 0; v < NCV; ++v) pv[v] = v < nv ? P.cf_var_param[voff + 1 + v] : -1;
+#pragma unroll
+    for (int v = 0; v < NCV; ++v) st[v] = v < nv ? step[pv[v]] : 1.;
+    double bp0[3], bq[3][3];
+    base_bundle(P, b, fr, bp0);
+    const int nb = p4.w > 0 ? p4.w : 0;
+    const double *br = &P.brec[(size_t)b * BREC];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const bool h = a < nb;
+        bq[a][0] = h ? br[3 + 3 * a] : bp0[0];
+        bq[a][1] = h ? br[4 + 3 * a] : bp0[1];
+        bq[a][2] = h ? br[5 + 3 * a] : bp0[2];
+        st[NCV + a] = h ? br[12 + a] : 1.;
+    }
+    const double *rec0 = &recs[(size_t)voff * CAMREC];
+    const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr);
+    Resid rr[NCV + 3];
+#pragma unroll
+    for (int v = 0; v < NCV; ++v) {
+        const double *rec = &recs[(size_t)(voff + 1 + (v < nv ? v : 0)) * CAMREC];
+        rr[v] = residual(rec, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        rr[NCV + a] = residual(rec0, bq[a], mx, my, sw, P.mode, P.image_width, false, nullptr);
+    int l = 0;
+    Resid rs = r0;
+    double jb[8] = {0., 0., 0., 0., 0., 0., r0.ex, r0.ey};
+#pragma unroll
+    for (int c = 0; c < NCV + 3; ++c) {
+        const bool cam = c < NCV;
+        if (cam ? c >= nv : c - NCV >= nb) continue;
+        const int p = cam ? pv[c] : (c == NCV ? p4.x : (c == NCV + 1 ? p4.y : p4.z));
+        double jx, jy;
+        if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
+            jx = (rr[c].ex - r0.ex) * st[c];
+            jy = (rr[c].ey - r0.ey) * st[c];
+        } else {      // st = h, divided (fdjac2)
+            jx = (rr[c].ex - r0.ex) / st[c];
+            jy = (rr[c].ey - r0.ey) / st[c];
+        }
+        J[(size_t)(2 * l) * M + i] = jx;
+        J[(size_t)(2 * l + 1) * M + i] = jy;
+        jcol[(size_t)l * M + i] = p;
+        if (!cam) {
+            jb[2 * (c - NCV)] = jx;
+            jb[2 * (c - NCV) + 1] = jy;
+        }
+        if (p == pstale) rs = rr[c];
+        ++l;
+    }
+    if (p4.w >= 0 && P.JB) {
+        double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)i * 8]);
+        dst[0] = make_double4(jb[0], jb[1], jb[2], jb[3]);
+        dst[1] = make_double4(jb[4], jb[5], jb[6], jb[7]);
+    }
+    nloc[i] = l;
+    if (eu) {
+        eu[2 * i] = rs.ux;
+        eu[2 * i + 1] = rs.uy;
+        ed[i] = rs.dist;
+    }
+}
+
 // -------------------------------------------------------------------------
 // Normal equations.  Per camera-frame segment (contiguous observations):
 // Acc (pc x pc), gC (pc), Acg (pc x nG).  One workgroup per cf; each thread
@@ -1175,28 +1268,32 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
 }
 
 // Uniform camera-frame block size PC (every solved camera-frame has PC
-// parameters, e.g. 6 for pose-only BA): NW waves per destination block; lane
-// q of the workgroup accumulates the full PC x PC product of the pairs q,
-// q + 64 NW, ... in registers (the W records are 16-B aligned AoS rows), each
-// wave folds its 64 partial blocks with a fixed xor-shuffle tree and the NW
-// wave results are summed in wave order (deterministic).
-template <int PC, int NW>
-__global__ void __launch_bounds__(64 * NW) k_schur_dest_u(DevProblem P,
-                                                          const double *__restrict__ W,
-                                                          const int2 *__restrict__ dest,
-                                                          const int *__restrict__ dest_off,
-                                                          const int2 *__restrict__ pairs,
-                                                          const SView V, int assign_off) {
-    __shared__ double red[PC * PC][NW];
-    const int d = blockIdx.x;
+// parameters, e.g. 6 for pose-only BA): one wave per destination block; lane
+// q accumulates the full PC x PC product of the pairs q, q + 64, ... in
+// registers (16-B vector loads of the AoS W rows, no LDS in the loop), then
+// the 64 partial blocks are summed through LDS in a fixed order
+// (deterministic).  XCD-aware order: consecutive workgroups are dealt round
+// robin to the 8 XCDs, so workgroup w takes destination
+// (w % 8) * ceil(ndest / 8) + w / 8 -- each XCD sweeps one contiguous band of
+// destinations and the W rows of its camera-frames stay in that XCD's L2.
+template <int PC>
+__global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
+                                                     const int2 *__restrict__ dest,
+                                                     const int *__restrict__ dest_off,
+                                                     const int2 *__restrict__ pairs,
+                                                     const SView V, int assign_off, int ndest) {
+    __shared__ double red[PC * PC][65];
+    const int per = (ndest + 7) / 8;
+    const int d = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (d >= ndest) return;
     const int2 cc = dest[d];
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int lane = threadIdx.x;
     double acc[PC * PC];
 #pragma unroll
     for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
-    for (int q = q0 + tid; q < q1; q += 64 * NW) {
+    for (int q = q0 + lane; q < q1; q += 64) {
         const int2 pr = pairs[q];
         double wi[3 * PC], wj[3 * PC];
         if constexpr ((3 * PC) % 2 == 0) {  // wst = 3 PC: 16-B aligned records
@@ -1225,18 +1322,11 @@ __global__ void __launch_bounds__(64 * NW) k_schur_dest_u(DevProblem P,
                                    wi[a * 3 + 2] * wj[c * 3 + 2];
     }
 #pragma unroll
-    for (int e = 0; e < PC * PC; ++e) {
-        double v = acc[e];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) red[e][wv] = v;
-    }
+    for (int e = 0; e < PC * PC; ++e) red[e][lane] = acc[e];
     __syncthreads();
-    if (tid < PC * PC) {
-        const int e = tid;
-        double v = red[e][0];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) v += red[e][w];
+    for (int e = lane; e < PC * PC; e += 64) {
+        double v = 0.;
+        for (int l = 0; l < 64; ++l) v += red[e][l];
         const int a = e / PC, c = e % PC;
         if (ri + a >= rj + c) {
             double *dd = s_at(V, ri + a, rj + c);
@@ -1723,7 +1813,18 @@ void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, dou
 }
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
-                     int *jcol, int *nloc, const int *stale_param, double *eu, double *ed) {
+                     int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
+                     int ncv) {
+    if (ncv == 6) {
+        k_jacobian_u<6><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc,
+                                                        stale_param, eu, ed);
+        return;
+    }
+    if (ncv == 7) {
+        k_jacobian_u<7><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc,
+                                                        stale_param, eu, ed);
+        return;
+    }
     k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
                                                 nloc, stale_param, eu, ed);
 }
@@ -1782,9 +1883,11 @@ void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, cons
                        int pc_uniform, int assign_off) {
     if (ndest <= 0) return;
     if (pc_uniform == 6)
-        k_schur_dest_u<6, 4><<<ndest, 256, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
+        k_schur_dest_u<6><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
+                                                                assign_off, ndest);
     else if (pc_uniform == 7)
-        k_schur_dest_u<7, 4><<<ndest, 256, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
+        k_schur_dest_u<7><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
+                                                                assign_off, ndest);
     else
         k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
 }

@@ -631,6 +631,18 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int b = 0; b < nB && all_fast; ++b)
             if (bnd_pb[b] > 0 && bnd_p4[b].w < 0) all_fast = false;
         D.JB = all_fast ? dalloc<double>((size_t)8 * M) : nullptr;
+        // uniform fast Jacobian kernel: fast bundles, no lens, no bundle-side
+        // camera variants, at most pc_uniform (6 or 7) variants per camera-frame
+        bool fast = all_fast && (pc_uniform == 6 || pc_uniform == 7);
+        for (int c = 0; c < nC && fast; ++c)
+            if (pr->cam_lens && pr->cam_lens[c] >= 0) fast = false;
+        for (size_t t = 0; t < cf_var_flags.size() && fast; ++t)
+            if (cf_var_flags[t] != 0) fast = false;
+        for (int cf = 0; cf < ncf && fast; ++cf)
+            if (cf_var_off[cf + 1] - cf_var_off[cf] - 1 > pc_uniform) fast = false;
+        jac_ncv = fast ? pc_uniform : 0;
+        if (const char *e = std::getenv("MMBA_JAC_GENERIC"))
+            if (std::atoi(e)) jac_ncv = 0;
     }
     d_brec = dalloc<double>((size_t)nB * BREC);
     D.brec = d_brec;

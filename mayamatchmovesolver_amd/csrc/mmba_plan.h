@@ -71,6 +71,7 @@ struct Plan {
     // deterministic Schur accumulation (destination-sorted observation pairs)
     bool use_dest = false;
     int ndest = 0;
+    int jac_ncv = 0;     // uniform fast Jacobian kernel (k_jacobian_u<jac_ncv>), 0: generic
     int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
