@@ -50,6 +50,12 @@ int residual_blocks(const DevProblem &P);
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out = nullptr,
                      unsigned int *ticket = nullptr);
+// launch_residual (partials only) plus ||J p||^2 partials of the same blocks
+// into partial_jp (k_jp_sumsq's sum, one launch)
+void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
+                        double *eu, double *ed, double *partial, const double *J,
+                        const int *jcol, const int *nloc, const double *pstep,
+                        double *partial_jp);
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,

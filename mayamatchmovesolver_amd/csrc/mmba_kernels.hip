@@ -6,6 +6,8 @@
 //   k_chol_update                    fp64 MFMA (v_mfma_f64_16x16x4_f64),
 //                                    64x64 tiles staged in LDS.
 //   everything else                  small O(n) vector work.
+#include <cstdlib>
+
 #include "mmba_geom.h"
 #include "mmba_kernels.h"
 
@@ -208,13 +210,22 @@ __device__ __forceinline__ bool obs_lens(const DevProblem &P, int cam, int &lens
 // Residuals (measureErrors).  Writes f (device order), user deviation and
 // distance, and one partial sum of squares per block.
 // -------------------------------------------------------------------------
+// JP: the trial-point evaluation also forms (J p)_obs = sum_l J_l p[jcol_l]
+// from the Jacobian blocks of the current x (lmder's ||J p|| for prered,
+// k_jp_sumsq) into a second partial row.
+template <bool JP>
 __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__restrict__ recs,
                                                   double *f, double *eu, double *ed,
                                                   double *partial, double *out,
-                                                  unsigned int *ticket) {
+                                                  unsigned int *ticket,
+                                                  const double *__restrict__ J,
+                                                  const int *__restrict__ jcol,
+                                                  const int *__restrict__ nloc,
+                                                  const double *__restrict__ pstep,
+                                                  double *partial_jp) {
     __shared__ double red[256];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    double s = 0.;
+    double s = 0., sj = 0.;
     if (i < P.M) {
         const int cf = P.obs_cf[i];
         const int b = P.obs_bnd[i];
@@ -237,7 +248,30 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
             eu[2 * i + 1] = r.uy;
             ed[i] = r.dist;
         }
-        if (own_obs(P, i)) s = r.ex * r.ex + r.ey * r.ey;
+        if (own_obs(P, i)) {
+            s = r.ex * r.ex + r.ey * r.ey;
+            if constexpr (JP) {
+                const int M = P.M;
+                double ax = 0., ay = 0.;
+                const int nl = nloc[i];
+                for (int l = 0; l < nl; ++l) {
+                    const double pv = pstep[jcol[(size_t)l * M + i]];
+                    ax += J[(size_t)(2 * l) * M + i] * pv;
+                    ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+                }
+                sj = ax * ax + ay * ay;
+            }
+        }
+    }
+    if constexpr (JP) {
+        red[threadIdx.x] = sj;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) partial_jp[blockIdx.x] = red[0];
+        __syncthreads();
     }
     red[threadIdx.x] = s;
     __syncthreads();
@@ -378,11 +412,10 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
 // chains overlap (the generic loop serialises them behind its dependent
 // variant-table loads).  Emits columns in the generic kernel's order.
 template <int NCV>
-__global__ void __launch_bounds__(128) k_jacobian_u(DevProblem P, const double *__restrict__ recs,
-                                                    const double *__restrict__ step,
-                                                    int solver_type, double *J, int *jcol,
-                                                    int *nloc, const int *__restrict__ stale_param,
-                                                    double *eu, double *ed) {
+__global__ void __launch_bounds__(128) k_jacobian_u(
+    DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
+    int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
+    const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.M) return;
     const int M = P.M;
@@ -396,59 +429,59 @@ __global__ void __launch_bounds__(128) k_jacobian_u(DevProblem P, const double *
     const int pstale = stale_param[fr];
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     int pv[NCV];
-    double st[NCV + 3];
+    double st[NCV];
 #pragma unroll
     for (int v = 0; v < NCV; ++v) pv[v] = v < nv ? P.cf_var_param[voff + 1 + v] : -1;
 #pragma unroll
     for (int v = 0; v < NCV; ++v) st[v] = v < nv ? step[pv[v]] : 1.;
-    double bp0[3], bq[3][3];
+    double bp0[3];
     base_bundle(P, b, fr, bp0);
     const int nb = p4.w > 0 ? p4.w : 0;
-    const double *br = &P.brec[(size_t)b * BREC];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const bool h = a < nb;
-        bq[a][0] = h ? br[3 + 3 * a] : bp0[0];
-        bq[a][1] = h ? br[4 + 3 * a] : bp0[1];
-        bq[a][2] = h ? br[5 + 3 * a] : bp0[2];
-        st[NCV + a] = h ? br[12 + a] : 1.;
-    }
-    const double *rec0 = &recs[(size_t)voff * CAMREC];
+    const double *__restrict__ br = &P.brec[(size_t)b * BREC];
+    const double *__restrict__ rec0 = &recs[(size_t)voff * CAMREC];
     const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr);
-    Resid rr[NCV + 3];
-#pragma unroll
-    for (int v = 0; v < NCV; ++v) {
-        const double *rec = &recs[(size_t)(voff + 1 + (v < nv ? v : 0)) * CAMREC];
-        rr[v] = residual(rec, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr);
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-        rr[NCV + a] = residual(rec0, bq[a], mx, my, sw, P.mode, P.image_width, false, nullptr);
     int l = 0;
-    Resid rs = r0;
+    double rsx = r0.ux, rsy = r0.uy, rsd = r0.dist;  // errorList of the stale column
     double jb[8] = {0., 0., 0., 0., 0., 0., r0.ex, r0.ey};
-#pragma unroll
-    for (int c = 0; c < NCV + 3; ++c) {
-        const bool cam = c < NCV;
-        if (cam ? c >= nv : c - NCV >= nb) continue;
-        const int p = cam ? pv[c] : (c == NCV ? p4.x : (c == NCV + 1 ? p4.y : p4.z));
+    auto emit = [&](int p, const Resid &r, double s) {
         double jx, jy;
-        if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
-            jx = (rr[c].ex - r0.ex) * st[c];
-            jy = (rr[c].ey - r0.ey) * st[c];
-        } else {      // st = h, divided (fdjac2)
-            jx = (rr[c].ex - r0.ex) / st[c];
-            jy = (rr[c].ey - r0.ey) / st[c];
+        if (lmder) {  // s = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
+            jx = (r.ex - r0.ex) * s;
+            jy = (r.ey - r0.ey) * s;
+        } else {      // s = h, divided (fdjac2)
+            jx = (r.ex - r0.ex) / s;
+            jy = (r.ey - r0.ey) / s;
         }
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
         jcol[(size_t)l * M + i] = p;
-        if (!cam) {
-            jb[2 * (c - NCV)] = jx;
-            jb[2 * (c - NCV) + 1] = jy;
+        if (p == pstale) {
+            rsx = r.ux;
+            rsy = r.uy;
+            rsd = r.dist;
         }
-        if (p == pstale) rs = rr[c];
         ++l;
+        return make_double2(jx, jy);
+    };
+#pragma unroll
+    for (int v = 0; v < NCV; ++v) {
+        if (v < nv) {
+            const double *__restrict__ rec = &recs[(size_t)(voff + 1 + v) * CAMREC];
+            emit(pv[v], residual(rec, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr),
+                 st[v]);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (a < nb) {
+            const double bq[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
+            const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
+            const double2 j = emit(
+                p, residual(rec0, bq, mx, my, sw, P.mode, P.image_width, false, nullptr),
+                br[12 + a]);
+            jb[2 * a] = j.x;
+            jb[2 * a + 1] = j.y;
+        }
     }
     if (p4.w >= 0 && P.JB) {
         double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)i * 8]);
@@ -457,9 +490,9 @@ __global__ void __launch_bounds__(128) k_jacobian_u(DevProblem P, const double *
     }
     nloc[i] = l;
     if (eu) {
-        eu[2 * i] = rs.ux;
-        eu[2 * i + 1] = rs.uy;
-        ed[i] = rs.dist;
+        eu[2 * i] = rsx;
+        eu[2 * i + 1] = rsy;
+        ed[i] = rsd;
     }
 }
 
@@ -1770,6 +1803,19 @@ void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
                     double *brec, int base_only) {
     const int ncb = nblk(base_only ? P.ncf : nvar, 64);
     const int nbb = nblk(P.nB, 64);
+    static const bool split = [] {
+        const char *e = std::getenv("MMBA_REC_SPLIT");
+        return e && std::atoi(e) != 0;
+    }();
+    if (split) {  // diagnostic: camera and bundle records as separate launches
+        if (ncb > 0)
+            k_records<<<ncb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
+                                         ncb);
+        if (nbb > 0)
+            k_records<<<nbb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
+                                         0);
+        return;
+    }
     if (ncb + nbb > 0)
         k_records<<<ncb + nbb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
                                            ncb);
@@ -1808,8 +1854,16 @@ void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
 int residual_blocks(const DevProblem &P) { return nblk(P.M, 256); }
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out, unsigned int *ticket) {
-    k_residual<<<nblk(P.M, 256), 256, 0, s>>>(P, recs, f, eu, ed, partial, out, ticket);
+    k_residual<false><<<nblk(P.M, 256), 256, 0, s>>>(P, recs, f, eu, ed, partial, out, ticket,
+                                                      nullptr, nullptr, nullptr, nullptr, nullptr);
     if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, nblk(P.M, 256), out);
+}
+void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
+                        double *eu, double *ed, double *partial, const double *J,
+                        const int *jcol, const int *nloc, const double *pstep,
+                        double *partial_jp) {
+    k_residual<true><<<nblk(P.M, 256), 256, 0, s>>>(P, recs, f, eu, ed, partial, nullptr,
+                                                     nullptr, J, jcol, nloc, pstep, partial_jp);
 }
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,

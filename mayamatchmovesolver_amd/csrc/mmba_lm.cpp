@@ -168,15 +168,15 @@ void Plan::trial_enqueue(double *eu, double *ed) {
                       opt.solver_type, opt.delta, 1.0, d_p_own, pr, nparts, pw);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin();
-    launch_residual(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw);
+    launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
+                       d_wa1, pr + 3 * (size_t)pw);
     span_end(SPAN_RESID);
-    launch_jp_sumsq(s, P, d_J, d_jcol, d_nloc, d_wa1, pr + 3 * (size_t)pw, nparts, nullptr);
     RedSpec rs{};
     rs.flag_slot = -1;
     rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_PNORM};
     rs.row[rs.nrows++] = {4 * pw, nparts, 0, SL_XN2T};
     rs.row[rs.nrows++] = {5 * pw, residual_blocks(P), 0, SL_FNORM};
-    rs.row[rs.nrows++] = {6 * pw, nparts, 0, SL_JP};
+    rs.row[rs.nrows++] = {6 * pw, residual_blocks(P), 0, SL_JP};
     launch_reduce_multi(s, d_partial, rs, d_scalar);
     allreduce(d_scalar + SL_PNORM, 1);
     allreduce(d_scalar + SL_XN2T, 1);
@@ -186,7 +186,7 @@ void Plan::trial_enqueue(double *eu, double *ed) {
 }
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
-void Plan::solve_damped_enqueue(double lam) {
+void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
     const double t0 = wall_now();
     // d_fail is zero here: launch_flag_to_scalar clears it after every use
     if (nB_solved > 0) {
@@ -254,7 +254,17 @@ void Plan::solve_damped_enqueue(double lam) {
         launch_scatter_xR(s, P, d_xR, d_xs);
     }
     if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
-    launch_flag_to_scalar(s, d_fail, d_scalar + SL_FAIL);
+    if (dnorm_slot < 0) {
+        launch_flag_to_scalar(s, d_fail, d_scalar + SL_FAIL);
+    } else {  // ||D xs||^2 and the fail flag in one reduction launch
+        double *pr = d_partial + 7 * (size_t)pw;
+        launch_sumsq(s, d_xs, d_diag, n, pr, nparts, nullptr, d_p_own);
+        RedSpec rs{};
+        rs.flag_slot = SL_FAIL;
+        rs.row[rs.nrows++] = {7 * pw, nparts, 0, dnorm_slot};
+        launch_reduce_multi(s, d_partial, rs, d_scalar, d_fail);
+        allreduce(d_scalar + dnorm_slot, 1);
+    }
     allreduce(d_scalar + SL_FAIL, 1, ReduceOp::Max);
     t_linear += wall_now() - t0;
 }
@@ -299,8 +309,7 @@ void Plan::newton_enqueue(double dxnorm) {
 // pre: the undamped solve and its ||D x|| were enqueued and read already
 // (lmpar_first_enqueue); *undamped is set when lmpar returns that step.
 static void lmpar_first_enqueue(Plan &pl) {
-    pl.solve_damped_enqueue(0.0);
-    pl.dnorm_enqueue(pl.d_xs, Plan::SL_DNORM);
+    pl.solve_damped_enqueue(0.0, Plan::SL_DNORM);
 }
 
 static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *undamped) {
@@ -341,8 +350,7 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *unda
     for (;;) {
         ++iter;
         if (*par == 0.) *par = std::max(dwarf, p001 * paru);
-        pl.solve_damped_enqueue(*par);
-        pl.dnorm_enqueue(pl.d_xs, Plan::SL_DNORM);
+        pl.solve_damped_enqueue(*par, Plan::SL_DNORM);
         pl.read_slots(Plan::SL_DNORM, Plan::SL_DNORM);
         dxnorm = std::sqrt(h[Plan::SL_DNORM]);
         double temp = fp;

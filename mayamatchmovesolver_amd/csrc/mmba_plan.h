@@ -213,7 +213,9 @@ struct Plan {
     double *d_eu_s = nullptr, *d_ed_s = nullptr;
     bool spec_ok = true;  // last lmpar accepted its undamped step
     int pw = 0;           // partial-row stride of d_partial (8 rows)
-    void solve_damped_enqueue(double lam);
+    // dnorm_slot >= 0: also ||D xs||^2 -> that slot (one reduction launch
+    // with the fail flag)
+    void solve_damped_enqueue(double lam, int dnorm_slot = -1);
     bool solve_damped(double lam);
     void newton_enqueue(double dxnorm);
     void dnorm_enqueue(const double *dv, int slot);
