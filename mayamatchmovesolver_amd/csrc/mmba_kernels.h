@@ -91,9 +91,12 @@ void launch_trsv_fwd_all(hipStream_t s, const double *S, const int *slot, int NT
 void launch_trsv_bwd_all(hipStream_t s, const double *S, const int *slot, int NT,
                          const int *cols_off, const int *cols, const double *Linv, double *y,
                          double *x);
-void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
+// Returns true when the right-hand side update rhs_R -= sum W_i t_b(i) was
+// fused into the diagonal destinations (uniform path; else launch_schur_rhs).
+bool launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
-                       int pc_uniform, int assign_off);
+                       int pc_uniform, int assign_off, const double *tb = nullptr,
+                       double *rhs = nullptr);
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs);
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,

@@ -1119,38 +1119,44 @@ __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__
 
 // S = (Acc + lam D^2 | Acg | Agg + lam D^2), lower triangle, plus identity
 // on the padded tail; rhs = g_R.
-__global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
-                             const double *__restrict__ Acg, const double *__restrict__ Agg,
-                             const double *__restrict__ g, const double *__restrict__ diag,
-                             double lam, const SView V, int npad, double *rhs) {
+__global__ void __launch_bounds__(256) k_schur_init(
+    DevProblem P, const double *__restrict__ Acc, const double *__restrict__ Acg,
+    const double *__restrict__ Agg, const double *__restrict__ g,
+    const double *__restrict__ diag, double lam, const SView V, int npad,
+    double *__restrict__ rhs) {
+    // one thread per reduced row: (camera-frame, row a) for t < ncf * PCMAX,
+    // then the global rows, then the padding rows
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int nG = P.nG;
     const int nCF = P.nR - nG;
-    if (t < P.ncf) {
-        const int cf = t;
-        if (!own_cf(P, cf)) return;
+    const int ncr = P.ncf * PCMAX;
+    if (t < ncr) {
+        const int cf = t / PCMAX, a = t % PCMAX;
         const int pc = P.cf_pc[cf];
+        if (a >= pc || !own_cf(P, cf)) return;
         const int r0 = P.cf_roff[cf];
         const int v0 = P.cf_var_off[cf] + 1;
-        for (int a = 0; a < pc; ++a) {
-            const int pa = P.cf_var_param[v0 + a];
-            for (int c = 0; c <= a; ++c) {
-                double v = Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + c];
-                if (a == c) {
-                    const double d = diag[pa];
-                    v += lam * (d * d);
-                    if (v == 0.) v = 1.;
-                }
-                *s_at(V, r0 + a, r0 + c) = v;
+        const double *Arow = &Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX];
+        double av[PCMAX];
+#pragma unroll
+        for (int c = 0; c < PCMAX; ++c) av[c] = c <= a ? Arow[c] : 0.;
+        const int pa = P.cf_var_param[v0 + a];
+        const double d = diag[pa], ga = g[pa];
+#pragma unroll
+        for (int c = 0; c < PCMAX; ++c) {
+            if (c > a) break;
+            double v = av[c];
+            if (c == a) {
+                v += lam * (d * d);
+                if (v == 0.) v = 1.;
             }
-            rhs[r0 + a] = (Acc[(size_t)cf * PCMAX * PCMAX + a * PCMAX + a] == 0. && lam == 0.)
-                              ? 0.
-                              : g[pa];
-            for (int q = 0; q < nG; ++q)
-                *s_at(V, nCF + q, r0 + a) = Acg[((size_t)cf * PCMAX + a) * NGMAX + q];
+            *s_at(V, r0 + a, r0 + c) = v;
         }
-    } else if (t < P.ncf + nG) {
-        const int q = t - P.ncf;
+        rhs[r0 + a] = (av[a] == 0. && lam == 0.) ? 0. : ga;
+        for (int q = 0; q < nG; ++q)
+            *s_at(V, nCF + q, r0 + a) = Acg[((size_t)cf * PCMAX + a) * NGMAX + q];
+    } else if (t < ncr + nG) {
+        const int q = t - ncr;
         const int p = P.g_param[q];
         if (!P.root) {  // the global block and its rhs are added once
             rhs[nCF + q] = 0.;
@@ -1167,7 +1173,7 @@ __global__ void k_schur_init(DevProblem P, const double *__restrict__ Acc,
         }
         rhs[nCF + q] = (Agg[q * NGMAX + q] == 0. && lam == 0.) ? 0. : g[p];
     } else {
-        const int r = P.nR + (t - P.ncf - nG);
+        const int r = P.nR + (t - ncr - nG);
         if (r < P.nR + npad) {
             *s_at(V, r, r) = 1.;
             rhs[r] = 0.;
@@ -1314,8 +1320,12 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
                                                      const int2 *__restrict__ dest,
                                                      const int *__restrict__ dest_off,
                                                      const int2 *__restrict__ pairs,
-                                                     const SView V, int assign_off, int ndest) {
-    __shared__ double red[PC * PC][65];
+                                                     const SView V, int assign_off, int ndest,
+                                                     const double *__restrict__ tb, double *rhs) {
+    // diagonal destinations (cf, cf) hold exactly the pairs (i, i) of the
+    // camera-frame's observations with a bundle block, so they also form
+    // rhs_R -= sum_i W_i t_b(i) (k_schur_rhs) in the same loop
+    __shared__ double red[PC * PC + PC][65];
     const int per = (ndest + 7) / 8;
     const int d = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (d >= ndest) return;
@@ -1323,9 +1333,12 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
     const int lane = threadIdx.x;
-    double acc[PC * PC];
+    const bool diag = rhs && cc.x == cc.y && own_cf(P, cc.x);
+    double acc[PC * PC], accr[PC];
 #pragma unroll
     for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
+#pragma unroll
+    for (int a = 0; a < PC; ++a) accr[a] = 0.;
     for (int q = q0 + lane; q < q1; q += 64) {
         const int2 pr = pairs[q];
         double wi[3 * PC], wj[3 * PC];
@@ -1353,13 +1366,28 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
             for (int c = 0; c < PC; ++c)
                 acc[a * PC + c] += wi[a * 3] * wj[c * 3] + wi[a * 3 + 1] * wj[c * 3 + 1] +
                                    wi[a * 3 + 2] * wj[c * 3 + 2];
+        if (diag) {
+            const int b = P.obs_bnd[pr.x];
+            const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1],
+                         t2 = tb[(size_t)b * 3 + 2];
+#pragma unroll
+            for (int a = 0; a < PC; ++a)
+                accr[a] += wi[a * 3] * t0 + wi[a * 3 + 1] * t1 + wi[a * 3 + 2] * t2;
+        }
     }
 #pragma unroll
     for (int e = 0; e < PC * PC; ++e) red[e][lane] = acc[e];
+    if (diag)
+#pragma unroll
+        for (int a = 0; a < PC; ++a) red[PC * PC + a][lane] = accr[a];
     __syncthreads();
-    for (int e = lane; e < PC * PC; e += 64) {
+    for (int e = lane; e < PC * PC + (diag ? PC : 0); e += 64) {
         double v = 0.;
         for (int l = 0; l < 64; ++l) v += red[e][l];
+        if (e >= PC * PC) {
+            rhs[ri + e - PC * PC] -= v;
+            continue;
+        }
         const int a = e / PC, c = e % PC;
         if (ri + a >= rj + c) {
             double *dd = s_at(V, ri + a, rj + c);
@@ -1924,26 +1952,30 @@ void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
                        const SView &V, int npad, double *rhs) {
-    const int n = P.ncf + P.nG + npad;
-    k_schur_init<<<nblk(n, 64), 64, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs);
+    const int n = P.ncf * PCMAX + P.nG + npad;
+    k_schur_init<<<nblk(n, 256), 256, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs);
 }
 void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                         const double *tb, const SView &V, double *rhs) {
     if (P.nB == 0) return;
     k_schur_pairs<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, tb, V, rhs);
 }
-void launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
+bool launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
-                       int pc_uniform, int assign_off) {
-    if (ndest <= 0) return;
-    if (pc_uniform == 6)
+                       int pc_uniform, int assign_off, const double *tb, double *rhs) {
+    if (ndest <= 0) return false;
+    if (pc_uniform == 6) {
         k_schur_dest_u<6><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
-                                                                assign_off, ndest);
-    else if (pc_uniform == 7)
+                                                                assign_off, ndest, tb, rhs);
+        return rhs != nullptr;
+    }
+    if (pc_uniform == 7) {
         k_schur_dest_u<7><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
-                                                                assign_off, ndest);
-    else
-        k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
+                                                                assign_off, ndest, tb, rhs);
+        return rhs != nullptr;
+    }
+    k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);
+    return false;
 }
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs) {

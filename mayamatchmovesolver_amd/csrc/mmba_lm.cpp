@@ -212,9 +212,13 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
         if (nB_solved > 0) {
             if (use_dest) {
-                launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V, pc_uniform,
-                                  band && bs.use_bcr);
-                launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
+                // unsharded uniform plans fold the rhs update into the
+                // diagonal destinations
+                const bool rhs_done =
+                    launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V,
+                                      pc_uniform, band && bs.use_bcr, d_tb,
+                                      nranks > 1 ? nullptr : d_rhs);
+                if (!rhs_done) launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
                 launch_schur_glob(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
                 launch_schur_pairs(s, P, d_W, d_Wg, d_tb, V, d_rhs);
