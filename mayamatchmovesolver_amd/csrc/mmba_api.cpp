@@ -219,6 +219,7 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
     if (enable_timing) {
         p.jac_ms = p.resid_ms = p.chol_ms = 0.;
         p.jac_n = p.resid_n = p.chol_n = 0;
+        p.span_ctr[0] = p.span_ctr[1] = p.span_ctr[2] = 0;
     }
     return MMBA_OK;
 }

@@ -38,14 +38,19 @@ hipEvent_t Plan::next_event() {
     return ev_pool[ev_used++];
 }
 
-void Plan::span_begin() {
-    if (!timing) return;
+// Spans are sampled: every span_stride-th span of each kind is timed (an
+// event pair costs ~6 us of stream time, more than some of the kernels it
+// brackets), so the timed region is barely perturbed.
+void Plan::span_begin(int kind) {
+    span_on = timing && (span_ctr[kind]++ % span_stride) == 0;
+    if (!span_on) return;
     span_a = next_event();
     MMBA_HIP(hipEventRecord(span_a, s));
 }
 
 void Plan::span_end(int kind) {
-    if (!timing) return;
+    if (!span_on) return;
+    span_on = false;
     hipEvent_t b = next_event();
     MMBA_HIP(hipEventRecord(b, s));
     spans.push_back({span_a, b, kind});
@@ -111,7 +116,7 @@ double Plan::dnorm(const double *dv) {
 void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed) {
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
-    span_begin();
+    span_begin(SPAN_RESID);
     launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + SL_FNORM, d_ticket);
     span_end(SPAN_RESID);
     allreduce(d_scalar + SL_FNORM, 1);
@@ -131,7 +136,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
-    span_begin();
+    span_begin(SPAN_JAC);
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                     d_stale, d_eu, d_ed, jac_ncv);
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
@@ -167,7 +172,7 @@ void Plan::trial_enqueue(double *eu, double *ed) {
     launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
                       opt.solver_type, opt.delta, 1.0, d_p_own, pr, nparts, pw);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
-    span_begin();
+    span_begin(SPAN_RESID);
     launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
                        d_wa1, pr + 3 * (size_t)pw);
     span_end(SPAN_RESID);
@@ -224,7 +229,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
                 launch_schur_pairs(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             }
         }
-        span_begin();
+        span_begin(SPAN_CHOL);
         if (band) {
             band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
         } else {

@@ -134,7 +134,10 @@ struct Plan {
     std::vector<Span> spans;
     hipEvent_t span_a = nullptr;
     hipEvent_t next_event();
-    void span_begin();
+    int span_ctr[3] = {0, 0, 0};
+    int span_stride = 4;
+    bool span_on = false;
+    void span_begin(int kind);
     void span_end(int kind);
     void collect_spans();
     double jac_ms = 0., resid_ms = 0., chol_ms = 0.;
