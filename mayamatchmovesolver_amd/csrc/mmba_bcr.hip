@@ -34,6 +34,9 @@
 // Solves: forward, one launch per level (workgroup per even block, both odd
 // neighbours' y = C^-1 r by matrix-vector products, r_e updated in place in a
 // work copy); backward, one launch per level (workgroup per odd block).
+#include <algorithm>
+#include <atomic>
+
 #include "mmba_kernels.h"
 #include "mmba_plan.h"
 
@@ -632,6 +635,134 @@ __global__ void __launch_bounds__(64) k_bcr_bwd(BcrDev B, int s, int nact, const
 }
 
 // ---------------------------------------------------------------------------
+// Backward solve in ONE launch (dataflow): the root and every level's blocks
+// are items of a list in dependency order (root, coarsest level, ...,
+// level 0; B.ord), dealt round robin to G <= 256 one-wave workgroups (all
+// resident, so a wait always ends).  Block o = t 2^l (t odd) needs x of o - s
+// and o + s (s = 2^l, both finished earlier in the list) and of the root
+// when there is an arrow.  Hand-off per MI355X guide G16 (R1): x rows are
+// stored write-through (agent-scope relaxed atomic stores), the storing
+// wave drains (vmcnt 0) and one lane stores the block's flag = epoch; a
+// consumer polls the producers' flags relaxed (s_sleep), takes ONE
+// agent-scope acquire, then loads x.  Factor rows and y (written by earlier
+// launches) are loaded before the wait.  Every spin is bounded: a timeout
+// sets bit 1 of *fail (the solve then counts as failed) instead of hanging.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned int bcr_gu32;
+typedef __attribute__((address_space(1))) unsigned long long bcr_gu64;
+
+__device__ __forceinline__ void bcr_put(double *x, int R, double v) {
+    __hip_atomic_store((bcr_gu64 *)(x + R), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void bcr_publish(int *flags, int o, unsigned epoch, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+        __hip_atomic_store((bcr_gu32 *)(flags + o), epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true when flags[a] (and flags[b], b >= 0) == epoch; false after the bound
+__device__ __forceinline__ bool bcr_wait(const int *flags, int a, int b, unsigned epoch) {
+    for (unsigned spins = 0;; ++spins) {
+        unsigned fa = __hip_atomic_load((bcr_gu32 *)(flags + a), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        unsigned fb = b >= 0 ? __hip_atomic_load((bcr_gu32 *)(flags + b), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : epoch;
+        fa = __builtin_amdgcn_readfirstlane(fa);
+        fb = __builtin_amdgcn_readfirstlane(fb);
+        if (fa == epoch && fb == epoch) break;
+        if (spins > (1u << 22)) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return true;
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, double *x,
+                                                    unsigned epoch, int *fail) {
+    __shared__ double xg[NGMAX], xp[K], xn[K], v0[K + NGMAX];
+    const int lane = threadIdx.x;
+    const int nb = B.nb, nG = B.nG, nblk = B.nblk;
+    for (int k = blockIdx.x; k < nblk; k += gridDim.x) {
+        const int o = B.ord[k];
+        if (o == 0) {  // root: x_T = FT^T y_T (k_bcr_bwd_root)
+            const int N = B.NR;
+            if (lane < K) v0[lane] = bcr_get(y, lane, nb);
+            if (lane < NGMAX) v0[K + lane] = lane < nG ? y[nb + lane] : 0.;
+            __syncthreads();
+            if (lane < K + nG) {
+                double acc = 0.;
+                for (int u = lane; u < K + nG; ++u) acc = fma(B.FT[u * N + lane], v0[u], acc);
+                if (lane < K) {
+                    if (lane < nb) bcr_put(x, lane, acc);
+                } else {
+                    bcr_put(x, nb + lane - K, acc);
+                }
+            }
+            bcr_publish(B.flags, 0, epoch, lane);
+            __syncthreads();
+            continue;
+        }
+        const int s = 1 << __builtin_ctz(o);
+        const bool hn = o + s < nblk;
+        // factor rows and y_o first (written by earlier launches)
+        double ur[K], vr[K], cc[K];  // row lane of U_o, V_o; column lane of C_o (diag 1/C_ii)
+        double yo = 0.;
+        if (lane < K) {
+            const double *U = bcr_blk(B.FU, o, K), *V = bcr_blk(B.FV, o, K);
+            const double *Cf = bcr_blk(B.FC, o, K);
+#pragma unroll
+            for (int u = 0; u < K; ++u) {
+                ur[u] = U[lane * K + u];
+                vr[u] = hn ? V[lane * K + u] : 0.;
+                cc[u] = u >= lane ? Cf[u * K + lane] : 0.;
+            }
+            yo = bcr_get(y, o * K + lane, nb);
+        } else {
+#pragma unroll
+            for (int u = 0; u < K; ++u) ur[u] = vr[u] = cc[u] = 0.;
+        }
+        // producers: o - s, o + s (if any), the root (arrow rows)
+        bool ok = bcr_wait(B.flags, o - s, hn ? o + s : -1, epoch);
+        if (ok && nG > 0 && o - s != 0) ok = bcr_wait(B.flags, 0, -1, epoch);
+        if (!ok) {
+            if (lane == 0) atomicOr(fail, 2);
+            continue;
+        }
+        if (lane < K) {
+            xp[lane] = bcr_get(x, (o - s) * K + lane, nb);
+            xn[lane] = hn ? bcr_get(x, (o + s) * K + lane, nb) : 0.;
+        }
+        if (lane < nG) xg[lane] = x[nb + lane];
+        __syncthreads();
+        double v = 0.;
+        if (lane < K) {
+            const double *Y = B.FY + (size_t)o * K * nG;
+            v = yo;
+#pragma unroll
+            for (int u = 0; u < K; ++u) v = fma(-ur[u], xp[u], fma(-vr[u], xn[u], v));
+            for (int q = 0; q < nG; ++q) v = fma(-Y[lane * nG + q], xg[q], v);
+        }
+#pragma unroll
+        for (int u = K - 1; u >= 0; --u) {
+            if (lane == u) v *= cc[u];
+            const double xu = bcr_rdlane(v, u);
+            if (lane < u) v = fma(-cc[u], xu, v);
+        }
+        if (lane < K) {
+            const int R = o * K + lane;
+            if (R < nb) bcr_put(x, R, v);
+        }
+        bcr_publish(B.flags, o, epoch, lane);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
 // Factorisation; with r != nullptr the forward solve y = L^-1 r runs inside
@@ -667,9 +798,17 @@ static void bcr_forward_k(hipStream_t s, const BandSolver &B, const double *r, d
     k_bcr_fwd_root<K><<<1, 64, 0, s>>>(D, D.rw, y);
 }
 
+static std::atomic<unsigned> g_bcr_epoch{0};
+
 template <int K>
 static void bcr_backward_k(hipStream_t s, const BandSolver &B, const double *y, double *x) {
     const BcrDev &D = B.bcr;
+    if (D.flags && D.fail) {  // one dataflow launch
+        unsigned ep = ++g_bcr_epoch;
+        if (ep == 0) ep = ++g_bcr_epoch;  // flags start at 0: never use epoch 0
+        k_bcr_bwd_all<K><<<std::min(D.nblk, 256), 64, 0, s>>>(D, y, x, ep, D.fail);
+        return;
+    }
     k_bcr_bwd_root<K><<<1, 64, 0, s>>>(D, y, x);
     std::vector<std::pair<int, int>> lv;  // (stride, nact) per level, coarse to fine
     for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) lv.push_back({st, nact});

@@ -68,6 +68,11 @@ struct BcrDev {
     double *Dk = nullptr, *Lk0 = nullptr, *Lk1 = nullptr, *Gk = nullptr;
     double *FC = nullptr, *FU = nullptr, *FV = nullptr, *FY = nullptr, *Zc = nullptr;
     double *FT = nullptr, *gpart = nullptr, *rw = nullptr;
+    // dataflow backward solve (k_bcr_bwd_all): per-block flags (epochs),
+    // blocks in dependency order, the plan's fail flag (nullptr: per-level launches)
+    int *flags = nullptr;
+    const int *ord = nullptr;
+    int *fail = nullptr;
 };
 
 // Device buffers of the (partitioned) band factorisation.

@@ -746,6 +746,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_partial = dalloc<double>((size_t)8 * pw);
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
+    if (bs.use_bcr && bs.bcr.flags) bs.bcr.fail = d_fail;
     MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));
     // Single-launch reductions (finish_blocks) measured slower than the
     // two-launch form on C4 (the 256-782 arrivals on one ticket plus the
@@ -808,6 +809,23 @@ void Plan::setup_band(int Pforce) {
             B.FT = dalloc<double>((size_t)B.NR * B.NR);
             B.gpart = dalloc<double>((size_t)B.nblk * nG);
             B.rw = dalloc<double>((size_t)nb + nG);
+            {
+                // dataflow backward solve: blocks in dependency order (root,
+                // then levels coarse to fine); MMBA_BCR_BWD_LEVELS=1 keeps the
+                // per-level launches (A/B)
+                const char *e2 = std::getenv("MMBA_BCR_BWD_LEVELS");
+                if (!(e2 && std::atoi(e2) != 0)) {
+                    std::vector<int> ord{0};
+                    int L = 0;
+                    while ((1 << L) < B.nblk) ++L;
+                    for (int l = L; l >= 0; --l)
+                        for (int o = 1 << l; o < B.nblk; o += 2 << l) ord.push_back(o);
+                    if ((int)ord.size() != B.nblk) throw Invalid{"bcr order"};
+                    B.ord = upload(ord);
+                    B.flags = dalloc<int>(B.nblk);
+                    MMBA_HIP(hipMemsetAsync(B.flags, 0, sizeof(int) * B.nblk, s));
+                }
+            }
             d_ymask = upload(std::vector<int>(std::max(nR, 1), 1));
             return;
         }
