@@ -265,6 +265,13 @@ void mmba_comm_destroy(mmba_comm *comm);
  * shard calls it (and then every solve / measure) together. */
 int mmba_plan_create_sharded(mmba_context *ctx, const mmba_problem *prob,
                              const mmba_options *opt, mmba_comm *comm, mmba_plan **out);
+/* The frame partition a sharded plan uses (host only, no device needed):
+ * shard k owns frames [bounds[k], bounds[k+1]) (balanced by observation
+ * count) and the bundles whose earliest observation lies in them
+ * (bundle_owner, nullable).  obs_bundle[i] = bundle of observation i. */
+int mmba_shard_layout(int32_t num_frames, int32_t num_obs, const int32_t *obs_frame,
+                      const int32_t *obs_bundle, int32_t num_bundles, int32_t nranks,
+                      int32_t *bounds_out /* nranks + 1 */, int32_t *bundle_owner_out);
 
 /* One residual evaluation (measureErrors, adjust_measureErrors.cpp:523) at
  * internal parameters x.  Any output pointer may be NULL. */

@@ -6,6 +6,8 @@ device is visible, every compute entry point raises.
 from __future__ import annotations
 
 import ctypes as C
+
+import numpy as np
 import os
 import subprocess
 
@@ -87,6 +89,10 @@ def lib():
         L.mmba_plan_create_sharded.argtypes = [C.c_void_p, C.POINTER(abi.MmbaProblem),
                                                C.POINTER(abi.MmbaOptions), C.c_void_p,
                                                C.POINTER(C.c_void_p)]
+        ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+        L.mmba_shard_layout.restype = C.c_int
+        L.mmba_shard_layout.argtypes = [C.c_int32, C.c_int32, ip, ip, C.c_int32, C.c_int32, ip,
+                                        ip]
         _lib = L
     return _lib
 

@@ -186,6 +186,7 @@ EXPORTED_SYMBOLS = [
     "mmba_plan_create",
     "mmba_plan_destroy",
     "mmba_comm_unique_id",
+    "mmba_shard_layout",
     "mmba_comm_create_rccl",
     "mmba_comm_create_local",
     "mmba_comm_destroy",

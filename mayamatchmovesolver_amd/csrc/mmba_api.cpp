@@ -42,6 +42,22 @@ extern "C" {
 
 int mmba_abi_version(void) { return MMBA_ABI_VERSION; }
 
+int mmba_shard_layout(int32_t num_frames, int32_t num_obs, const int32_t *obs_frame,
+                      const int32_t *obs_bundle, int32_t num_bundles, int32_t nranks,
+                      int32_t *bounds_out, int32_t *bundle_owner_out) {
+    if (num_frames <= 0 || num_obs < 0 || nranks <= 0 || !bounds_out ||
+        (num_obs > 0 && !obs_frame) || (bundle_owner_out && (!obs_bundle || num_bundles < 0)))
+        return MMBA_ERR_INVALID;
+    for (int i = 0; i < num_obs; ++i) {
+        if (obs_frame[i] < 0 || obs_frame[i] >= num_frames) return MMBA_ERR_INVALID;
+        if (bundle_owner_out && (obs_bundle[i] < 0 || obs_bundle[i] >= num_bundles))
+            return MMBA_ERR_INVALID;
+    }
+    mmba::shard_layout(num_frames, num_obs, obs_frame, obs_bundle, num_bundles, nranks,
+                       bounds_out, bundle_owner_out);
+    return MMBA_OK;
+}
+
 const char *mmba_last_error(void) { return g_last_error.c_str(); }
 
 int mmba_device_count(void) {

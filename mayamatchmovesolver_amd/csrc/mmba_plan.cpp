@@ -50,6 +50,35 @@ static void require(bool c, const char *what) {
     if (!c) throw Invalid{what};
 }
 
+// Frame partition of a sharded solve, shared with the host-only
+// ABI entry mmba_shard_layout: shard k owns frames [bounds[k], bounds[k+1]),
+// the first frame whose cumulative observation count reaches k * M / nranks
+// starting shard k; a bundle belongs to the shard holding its first
+// (earliest-frame) observation.
+void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd, int nB,
+                  int nranks, int32_t *bounds, int32_t *bnd_owner) {
+    std::vector<long long> per_frame(F + 1, 0);
+    for (int i = 0; i < M; ++i) per_frame[obs_frame[i] + 1]++;
+    for (int f = 0; f < F; ++f) per_frame[f + 1] += per_frame[f];
+    for (int k = 0; k <= nranks; ++k) bounds[k] = F;
+    bounds[0] = 0;
+    for (int k = 1; k < nranks; ++k) {
+        const long long target = (long long)k * M / nranks;
+        int f = bounds[k - 1];
+        while (f < F && per_frame[f] < target) ++f;
+        bounds[k] = f;
+    }
+    if (!bnd_owner) return;
+    std::vector<int> bnd_first(nB, F);
+    for (int i = 0; i < M; ++i)
+        bnd_first[obs_bnd[i]] = std::min(bnd_first[obs_bnd[i]], (int)obs_frame[i]);
+    for (int b = 0; b < nB; ++b) {
+        int k = 0;
+        while (k + 1 < nranks && bounds[k + 1] <= bnd_first[b]) ++k;
+        bnd_owner[b] = k;
+    }
+}
+
 void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     require(pr && o, "null problem/options");
     opt = *o;
@@ -326,17 +355,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     if (nranks > 1) {
         if (!band || bw > WBAND_PART)
             throw Unsupported{"sharded solve needs a narrow camera-frame band (w <= 40)"};
-        std::vector<long long> per_frame(F + 1, 0);
-        for (int i = 0; i < Mg; ++i) per_frame[pr->obs_frame[i] + 1]++;
-        for (int f = 0; f < F; ++f) per_frame[f + 1] += per_frame[f];
-        std::vector<int> bf(nranks + 1, F);
-        bf[0] = 0;
-        for (int k = 1; k < nranks; ++k) {
-            const long long target = (long long)k * Mg / nranks;
-            int f = bf[k - 1];
-            while (f < F && per_frame[f] < target) ++f;
-            bf[k] = f;
-        }
+        std::vector<int> bf(nranks + 1, F), bnd_owner_all(nB, 0);
+        shard_layout(F, Mg, pr->obs_frame, obs_bnd_g.data(), nB, nranks, bf.data(),
+                     bnd_owner_all.data());
         // camera-frame rows of every shard's frame range (rows are frame-major)
         std::vector<int> first_row(F + 1, nCF);
         for (int cf = ncf - 1; cf >= 0; --cf) first_row[cf_frame[cf]] = cf_roff[cf];
@@ -353,17 +374,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         Rb = Rb_all[rank];
         const int fa = bf[rank], fb = bf[rank + 1];
         for (int cf = 0; cf < ncf; ++cf) cf_own[cf] = (cf_frame[cf] >= fa && cf_frame[cf] < fb);
-        std::vector<int> bnd_first(nB, F);
         for (int i = 0; i < Mg; ++i) {
             const int f = pr->obs_frame[i];
             obs_own_g[i] = (f >= fa && f < fb) ? 1 : 0;
-            bnd_first[obs_bnd_g[i]] = std::min(bnd_first[obs_bnd_g[i]], f);
         }
-        for (int b = 0; b < nB; ++b) {
-            int k = 0;
-            while (k + 1 < nranks && bf[k + 1] <= bnd_first[b]) ++k;
-            bnd_owner[b] = k;
-        }
+        bnd_owner = bnd_owner_all;
         std::vector<char> bnd_here(nB, 0);
         for (int i = 0; i < Mg; ++i)
             if (obs_own_g[i] && bnd_pb[obs_bnd_g[i]] > 0) bnd_here[obs_bnd_g[i]] = 1;

@@ -34,6 +34,9 @@ struct Invalid {
     std::string what;
 };
 
+void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd, int nB,
+                  int nranks, int32_t *bounds, int32_t *bnd_owner);
+
 struct Plan {
     mmba_context *ctx = nullptr;
     hipStream_t s = nullptr;

@@ -209,6 +209,20 @@ def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
         s.close()
 
 
+def shard_layout(problem: Problem, nranks: int):
+    """Frame partition a sharded plan of `problem` uses (host only): returns
+    (bounds[nranks + 1], bundle_owner[num_bundles]); shard k owns frames
+    [bounds[k], bounds[k + 1]) and the bundles whose first observation is there."""
+    p = problem
+    frames = np.ascontiguousarray(p.obs_frame, dtype=np.int32)
+    bnd = np.ascontiguousarray(np.asarray(p.mkr_bnd)[np.asarray(p.obs_marker)], dtype=np.int32)
+    bounds = np.zeros(nranks + 1, dtype=np.int32)
+    owner = np.zeros(max(p.num_bundles, 1), dtype=np.int32)
+    check(lib().mmba_shard_layout(p.num_frames, p.num_obs, frames, bnd, p.num_bundles, nranks,
+                                  bounds, owner))
+    return bounds, owner[:p.num_bundles]
+
+
 def device_count() -> int:
     return int(lib().mmba_device_count())
 
