@@ -59,7 +59,8 @@ void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, 
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
-                     int ncv = 0);  // ncv 6 / 7: uniform fast kernel (Plan::jac_ncv)
+                     int ncv = 0,  // ncv 6 / 7: uniform fast kernels (Plan::jac_ncv)
+                     const double *f = nullptr);  // residuals at x (column-parallel kernel)
 // aggbuf = [Agg (NGMAX^2) | g_G (NGMAX)]: the global-parameter normal
 // equations, all-reduced across shards before launch_colnorms.
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,

@@ -138,7 +138,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
     span_begin(SPAN_JAC);
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
-                    d_stale, d_eu, d_ed, jac_ncv);
+                    d_stale, d_eu, d_ed, jac_ncv, d_f);
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
               d_glob_partial, glob_chunk);

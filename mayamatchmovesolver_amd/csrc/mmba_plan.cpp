@@ -638,6 +638,12 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_pb = upload(bnd_pb);
     D.bnd_xoff = nullptr;
     D.bnd_p4 = upload(bnd_p4);
+    D.all_bnd_fast = 1;
+    for (int b = 0; b < nB; ++b)
+        if (bnd_p4[b].w < 0) D.all_bnd_fast = 0;
+    D.no_lens = 1;
+    for (int c = 0; c < nC; ++c)
+        if (pr->cam_lens && pr->cam_lens[c] >= 0) D.no_lens = 0;
     {
         std::vector<int> bpos(M);
         for (int q = 0; q < M; ++q) bpos[bobs[q]] = q;
