@@ -420,7 +420,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
 // residuals are independent straight-line code, so their fp64 latency
 // chains overlap (the generic loop serialises them behind its dependent
 // variant-table loads).  Emits columns in the generic kernel's order.
-template <int NCV>
+template <int NCV, bool GEN>  // GEN: some bundle needs the transform-chain path
 __global__ void __launch_bounds__(128) k_jacobian_u(
     DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
     int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
@@ -444,7 +444,14 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
 #pragma unroll
     for (int v = 0; v < NCV; ++v) st[v] = v < nv ? step[pv[v]] : 1.;
     double bp0[3];
-    base_bundle(P, b, fr, bp0);
+    if (GEN) {
+        base_bundle(P, b, fr, bp0);
+    } else {
+        const double *br0 = &P.brec[(size_t)b * BREC];
+        bp0[0] = br0[0];
+        bp0[1] = br0[1];
+        bp0[2] = br0[2];
+    }
     const int nb = p4.w > 0 ? p4.w : 0;
     const double *__restrict__ br = &P.brec[(size_t)b * BREC];
     const double *__restrict__ rec0 = &recs[(size_t)voff * CAMREC];
@@ -502,99 +509,6 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
         eu[2 * i] = rsx;
         eu[2 * i + 1] = rsy;
         ed[i] = rsd;
-    }
-}
-
-// Column-parallel form of the uniform fast case: one thread per (column
-// slot c, observation i), t = c M + i, slots 0..NCV-1 = camera variants,
-// NCV..NCV+2 = bundle parameters.  Each thread evaluates ONE perturbed
-// residual and differences it against f = the residual vector at x (the
-// last accepted evaluation, bitwise the r0 the per-observation kernels
-// recompute: same records, same bundle position, same code).  Every store
-// of a column is coalesced over i.  errorList / errorDistanceList are
-// only written by the stale column (the other observations already hold
-// their values at x, which is what the reference leaves there).
-template <int NCV, bool GEN>  // GEN: some bundle needs the transform-chain path
-__global__ void __launch_bounds__(256) k_jacobian_c(
-    DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
-    const double *__restrict__ f, int solver_type, double *__restrict__ J,
-    int *__restrict__ jcol, int *__restrict__ nloc, const int *__restrict__ stale_param,
-    double *__restrict__ eu, double *__restrict__ ed) {
-    const int M = P.M;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long long)(NCV + 3) * M) return;
-    const int c = (int)(t / M), i = (int)(t - (long long)c * M);
-    const int cf = P.obs_cf[i];
-    const int b = P.obs_bnd[i];
-    const int4 p4 = P.bnd_p4[b];
-    const int voff = P.cf_var_off[cf];
-    const int nv = min(P.cf_var_off[cf + 1] - voff - 1, NCV);
-    const int nb = p4.w > 0 ? p4.w : 0;
-    if (c == 0) nloc[i] = nv + nb;
-    const bool cam = c < NCV;
-    const int a = c - NCV;
-    double *jb = (!cam && p4.w >= 0 && P.JB) ? &P.JB[(size_t)i * 8] : nullptr;
-    const double f0 = f[2 * i], f1 = f[2 * i + 1];
-    if (jb && a == 0) {
-        jb[6] = f0;
-        jb[7] = f1;
-    }
-    if (cam ? c >= nv : a >= nb) {
-        if (jb) {
-            jb[2 * a] = 0.;
-            jb[2 * a + 1] = 0.;
-        }
-        return;
-    }
-    const int fr = P.obs_frame[i];
-    const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
-    int p, l;
-    double st, bp[3];
-    const double *rec;
-    if (cam) {
-        const int tv = voff + 1 + c;
-        p = P.cf_var_param[tv];
-        st = step[p];
-        rec = &recs[(size_t)tv * CAMREC];
-        if (!GEN || p4.w >= 0) {
-            const double *br0 = &P.brec[(size_t)b * BREC];
-            bp[0] = br0[0];
-            bp[1] = br0[1];
-            bp[2] = br0[2];
-        } else {
-            base_bundle(P, b, fr, bp);
-        }
-        l = c;
-    } else {
-        const double *br = &P.brec[(size_t)b * BREC];
-        p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
-        st = br[12 + a];
-        bp[0] = br[3 + 3 * a];
-        bp[1] = br[4 + 3 * a];
-        bp[2] = br[5 + 3 * a];
-        rec = &recs[(size_t)voff * CAMREC];
-        l = nv + a;
-    }
-    const Resid r = residual(rec, bp, mx, my, sw, P.mode, P.image_width, false, nullptr);
-    double jx, jy;
-    if (solver_type == MMBA_SOLVER_CMINPACK_LMDER) {  // st = 1/delta, multiplied
-        jx = (r.ex - f0) * st;
-        jy = (r.ey - f1) * st;
-    } else {  // st = h, divided (fdjac2)
-        jx = (r.ex - f0) / st;
-        jy = (r.ey - f1) / st;
-    }
-    J[(size_t)(2 * l) * M + i] = jx;
-    J[(size_t)(2 * l + 1) * M + i] = jy;
-    jcol[(size_t)l * M + i] = p;
-    if (jb) {
-        jb[2 * a] = jx;
-        jb[2 * a + 1] = jy;
-    }
-    if (eu && p == stale_param[fr]) {
-        eu[2 * i] = r.ux;
-        eu[2 * i + 1] = r.uy;
-        ed[i] = r.dist;
     }
 }
 
@@ -2007,32 +1921,19 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
                      int ncv, const double *f) {
-    static const bool per_obs = [] {
-        const char *e = std::getenv("MMBA_JAC_U");
-        return e && std::atoi(e) != 0;
-    }();
-#define MMBA_JAC_C(NCV, GEN)                                                                \
-    k_jacobian_c<NCV, GEN><<<nblk((long)(NCV + 3) * P.M, 256), 256, 0, s>>>(                  \
-        P, recs, step, f, solver_type, J, jcol, nloc, stale_param, eu, ed)
-    if ((ncv == 6 || ncv == 7) && !per_obs && f) {
+    (void)f;
+#define MMBA_JAC_U(NCV, GEN)                                                                \
+    k_jacobian_u<NCV, GEN><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, \
+                                                           nloc, stale_param, eu, ed)
+    if (ncv == 6 || ncv == 7) {
         if (ncv == 6) {
-            if (P.all_bnd_fast) MMBA_JAC_C(6, false); else MMBA_JAC_C(6, true);
+            if (P.all_bnd_fast) MMBA_JAC_U(6, false); else MMBA_JAC_U(6, true);
         } else {
-            if (P.all_bnd_fast) MMBA_JAC_C(7, false); else MMBA_JAC_C(7, true);
+            if (P.all_bnd_fast) MMBA_JAC_U(7, false); else MMBA_JAC_U(7, true);
         }
         return;
     }
-#undef MMBA_JAC_C
-    if (ncv == 6) {
-        k_jacobian_u<6><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc,
-                                                        stale_param, eu, ed);
-        return;
-    }
-    if (ncv == 7) {
-        k_jacobian_u<7><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc,
-                                                        stale_param, eu, ed);
-        return;
-    }
+#undef MMBA_JAC_U
     k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
                                                 nloc, stale_param, eu, ed);
 }
