@@ -697,10 +697,10 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
             if (lane < K + nG) {
                 double acc = 0.;
                 for (int u = lane; u < K + nG; ++u) acc = fma(B.FT[u * N + lane], v0[u], acc);
-                if (lane < K) {
-                    if (lane < nb) bcr_put(x, lane, acc);
-                } else {
-                    bcr_put(x, nb + lane - K, acc);
+                const int R = lane < K ? lane : nb + lane - K;
+                if (lane >= K || lane < nb) {
+                    bcr_put(x, R, acc);
+                    if (B.xs && B.row_param[R] >= 0) B.xs[B.row_param[R]] = acc;
                 }
             }
             bcr_publish(B.flags, 0, epoch, lane);
@@ -755,7 +755,10 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
         }
         if (lane < K) {
             const int R = o * K + lane;
-            if (R < nb) bcr_put(x, R, v);
+            if (R < nb) {
+                bcr_put(x, R, v);
+                if (B.xs && B.row_param[R] >= 0) B.xs[B.row_param[R]] = v;  // k_scatter_xR
+            }
         }
         bcr_publish(B.flags, o, epoch, lane);
         __syncthreads();

@@ -73,6 +73,10 @@ struct BcrDev {
     int *flags = nullptr;
     const int *ord = nullptr;
     int *fail = nullptr;
+    // with xs: the backward solve also scatters x_R to parameter order
+    // (xs[row_param[R]] = x_R, k_scatter_xR's job)
+    const int *row_param = nullptr;
+    double *xs = nullptr;
 };
 
 // Device buffers of the (partitioned) band factorisation.

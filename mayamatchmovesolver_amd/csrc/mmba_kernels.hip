@@ -1355,8 +1355,21 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
     for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
 #pragma unroll
     for (int a = 0; a < PC; ++a) accr[a] = 0.;
-    for (int q = q0 + lane; q < q1; q += 64) {
-        const int2 pr = pairs[q];
+    // pair indices of up to 8 rounds are loaded first (independent loads);
+    // the unrolled rounds then let the W gathers of round k + 1 overlap the
+    // products of round k
+    constexpr int NPF = 8;
+    for (int qb = q0; qb < q1; qb += 64 * NPF) {
+        int2 prk[NPF];
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) {
+            const int q = qb + lane + 64 * k;
+            prk[k] = q < q1 ? pairs[q] : make_int2(-1, -1);
+        }
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) {
+        const int2 pr = prk[k];
+        if (pr.x < 0) continue;
         double wi[3 * PC], wj[3 * PC];
         if constexpr ((3 * PC) % 2 == 0) {  // wst = 3 PC: 16-B aligned records
             const double2 *pi = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.x)]);
@@ -1389,6 +1402,7 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
 #pragma unroll
             for (int a = 0; a < PC; ++a)
                 accr[a] += wi[a * 3] * t0 + wi[a * 3 + 1] * t1 + wi[a * 3 + 2] * t2;
+        }
         }
     }
 #pragma unroll
@@ -1519,7 +1533,8 @@ __global__ void __launch_bounds__(64) k_obs_wtx(DevProblem P, const double *__re
 }
 
 // x_b = Lb^-T (tb - sum_i u_i - Wg_b^T x_G), scatter to parameter order.
-__global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ U,
+__global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
+                                 const double *__restrict__ U,
                                  const double *__restrict__ Wg, const double *__restrict__ tb,
                                  const double *__restrict__ Lb, const double *__restrict__ xR,
                                  double *x) {
@@ -1531,10 +1546,27 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ U,
     const int nCF = P.nR - nG;
     double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
     for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-        const double4 u = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
-        s[0] -= u.x;
-        s[1] -= u.y;
-        s[2] -= u.z;
+        double u[3];
+        if (W) {  // u_i = W_i^T x_cf(i) here (k_obs_wtx's arithmetic), no U round trip
+            const int i = P.bobs[q];
+            const int cf = P.obs_cf[i];
+            const int pc = min(P.cf_pc[cf], P.wst / 3);
+            const int r0 = P.cf_roff[cf];
+            const double *row = &W[widx(P, 0, i)];
+            u[0] = u[1] = u[2] = 0.;
+            for (int a = 0; a < pc; ++a) {
+                const double xv = xR[r0 + a];
+                for (int c = 0; c < 3; ++c) u[c] += row[a * 3 + c] * xv;
+            }
+        } else {
+            const double4 uu = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
+            u[0] = uu.x;
+            u[1] = uu.y;
+            u[2] = uu.z;
+        }
+        s[0] -= u[0];
+        s[1] -= u[1];
+        s[2] -= u[2];
     }
     for (int q = 0; q < nG; ++q) {
         const double xv = xR[nCF + q];
@@ -2018,8 +2050,16 @@ void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, 
                            const double *tb, const double *Lb, const double *xR, double *U,
                            double *x) {
     if (P.nB == 0) return;
-    k_obs_wtx<<<nblk(P.M, 64), 64, 0, s>>>(P, W, xR, U);
-    k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, U, Wg, tb, Lb, xR, x);
+    static const bool two_pass = [] {
+        const char *e = std::getenv("MMBA_BACKSUB_WTX");
+        return e && std::atoi(e) != 0;
+    }();
+    if (two_pass) {  // A/B: per-observation u_i pass, then the bundle gather
+        k_obs_wtx<<<nblk(P.M, 64), 64, 0, s>>>(P, W, xR, U);
+        k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, nullptr, U, Wg, tb, Lb, xR, x);
+    } else {
+        k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, nullptr, Wg, tb, Lb, xR, x);
+    }
 }
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x) {
     k_scatter_xR<<<nblk(P.n, 256), 256, 0, s>>>(P, xR, x);

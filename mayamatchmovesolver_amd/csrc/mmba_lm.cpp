@@ -260,7 +260,8 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
                 launch_trsv_bwd(s, d_S, d_slot, NT, k, d_cols + c0, nc, d_Linv, d_yR, d_xR);
             }
         }
-        launch_scatter_xR(s, P, d_xR, d_xs);
+        if (!(band && bs.use_bcr && bs.bcr.xs))  // else done by the BCR backward solve
+            launch_scatter_xR(s, P, d_xR, d_xs);
     }
     if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
     if (dnorm_slot < 0) {

@@ -767,7 +767,16 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_partial = dalloc<double>((size_t)8 * pw);
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
-    if (bs.use_bcr && bs.bcr.flags) bs.bcr.fail = d_fail;
+    if (bs.use_bcr && bs.bcr.flags) {
+        bs.bcr.fail = d_fail;
+        if (nranks == 1) {
+            std::vector<int> row_param(std::max(nR, 1), -1);
+            for (int p = 0; p < n; ++p)
+                if (p_class[p] != PC_B && p_pos[p] >= 0 && p_pos[p] < nR) row_param[p_pos[p]] = p;
+            bs.bcr.row_param = upload(row_param);
+            bs.bcr.xs = d_xs;
+        }
+    }
     MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));
     // Single-launch reductions (finish_blocks) measured slower than the
     // two-launch form on C4 (the 256-782 arrivals on one ticket plus the
