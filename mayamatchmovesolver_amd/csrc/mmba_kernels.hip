@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
 // chains overlap (the generic loop serialises them behind its dependent
 // variant-table loads).  Emits columns in the generic kernel's order.
 template <int NCV, bool GEN>  // GEN: some bundle needs the transform-chain path
-__global__ void __launch_bounds__(128) k_jacobian_u(
+__global__ void __launch_bounds__(128, 4) k_jacobian_u(
     DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
     int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
     const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed) {
@@ -1074,7 +1074,7 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
 // (zeros where a row has no bundle block / no camera block).
 __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__restrict__ J,
                                                   const double *__restrict__ Lb, double *W) {
-    __shared__ double sw[64 * 3 * PCMAX];
+    extern __shared__ double sw[];  // 64 x wst doubles (9 KB for pose-only BA)
     const int lane = threadIdx.x;
     const int i0 = blockIdx.x * 64;
     const int i = i0 + lane;
@@ -1332,7 +1332,7 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
 // (w % 8) * ceil(ndest / 8) + w / 8 -- each XCD sweeps one contiguous band of
 // destinations and the W rows of its camera-frames stay in that XCD's L2.
 template <int PC>
-__global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
+__global__ void __launch_bounds__(64, 3) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
                                                      const int2 *__restrict__ dest,
                                                      const int *__restrict__ dest_off,
                                                      const int2 *__restrict__ pairs,
@@ -1341,7 +1341,11 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
     // diagonal destinations (cf, cf) hold exactly the pairs (i, i) of the
     // camera-frame's observations with a bundle block, so they also form
     // rhs_R -= sum_i W_i t_b(i) (k_schur_rhs) in the same loop
-    __shared__ double red[PC * PC + PC][65];
+    // two-step lane reduction through a half-width buffer: 11 KB of LDS per
+    // one-wave workgroup (a 64-wide buffer, 22 KB, capped residency at 7
+    // workgroups per CU -- 1,792 < 1,992 destinations for C4 -- and ran the
+    // grid in two rounds)
+    __shared__ double red[PC * PC + PC][33];
     const int per = (ndest + 7) / 8;
     const int d = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (d >= ndest) return;
@@ -1358,7 +1362,7 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
     // pair indices of up to 8 rounds are loaded first (independent loads);
     // the unrolled rounds then let the W gathers of round k + 1 overlap the
     // products of round k
-    constexpr int NPF = 8;
+    constexpr int NPF = 4;
     for (int qb = q0; qb < q1; qb += 64 * NPF) {
         int2 prk[NPF];
 #pragma unroll
@@ -1405,15 +1409,25 @@ __global__ void __launch_bounds__(64) k_schur_dest_u(DevProblem P, const double 
         }
         }
     }
+    if (lane >= 32) {
 #pragma unroll
-    for (int e = 0; e < PC * PC; ++e) red[e][lane] = acc[e];
-    if (diag)
+        for (int e = 0; e < PC * PC; ++e) red[e][lane - 32] = acc[e];
+        if (diag)
 #pragma unroll
-        for (int a = 0; a < PC; ++a) red[PC * PC + a][lane] = accr[a];
+            for (int a = 0; a < PC; ++a) red[PC * PC + a][lane - 32] = accr[a];
+    }
+    __syncthreads();
+    if (lane < 32) {
+#pragma unroll
+        for (int e = 0; e < PC * PC; ++e) red[e][lane] += acc[e];
+        if (diag)
+#pragma unroll
+            for (int a = 0; a < PC; ++a) red[PC * PC + a][lane] += accr[a];
+    }
     __syncthreads();
     for (int e = lane; e < PC * PC + (diag ? PC : 0); e += 64) {
         double v = 0.;
-        for (int l = 0; l < 64; ++l) v += red[e][l];
+        for (int l = 0; l < 32; ++l) v += red[e][l];
         if (e >= PC * PC) {
             rhs[ri + e - PC * PC] -= v;
             continue;
@@ -1502,7 +1516,7 @@ __global__ void k_schur_glob(DevProblem P, const double *__restrict__ W,
 // coalesced into LDS first.
 __global__ void __launch_bounds__(64) k_obs_wtx(DevProblem P, const double *__restrict__ W,
                                                 const double *__restrict__ xR, double *U) {
-    __shared__ double sw[64 * 3 * PCMAX];
+    extern __shared__ double sw[];  // 64 x wst doubles
     const int lane = threadIdx.x;
     const int i0 = blockIdx.x * 64;
     const int i = i0 + lane;
@@ -2006,7 +2020,7 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
 }
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
                       double *W) {
-    k_schur_obs<<<nblk(P.M, 64), 64, 0, s>>>(P, J, Lb, W);
+    k_schur_obs<<<nblk(P.M, 64), 64, sizeof(double) * 64 * P.wst, s>>>(P, J, Lb, W);
 }
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
@@ -2055,7 +2069,7 @@ void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, 
         return e && std::atoi(e) != 0;
     }();
     if (two_pass) {  // A/B: per-observation u_i pass, then the bundle gather
-        k_obs_wtx<<<nblk(P.M, 64), 64, 0, s>>>(P, W, xR, U);
+        k_obs_wtx<<<nblk(P.M, 64), 64, sizeof(double) * 64 * P.wst, s>>>(P, W, xR, U);
         k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, nullptr, U, Wg, tb, Lb, xR, x);
     } else {
         k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, nullptr, Wg, tb, Lb, xR, x);
