@@ -83,7 +83,20 @@ void Plan::collect_spans() {
 void Plan::read_slots(int lo, int hi) {
     MMBA_HIP(hipMemcpyAsync(h_scalar + lo, d_scalar + lo, sizeof(double) * (hi - lo + 1),
                             hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    if (!spin_wait) {
+        MMBA_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    // The LM control thread has nothing else to do: poll an event instead of
+    // a blocking stream synchronisation (whose wake-up adds tens of us per
+    // decision point).
+    if (!ev_sync) MMBA_HIP(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
+    MMBA_HIP(hipEventRecord(ev_sync, s));
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev_sync);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) MMBA_HIP(e);
+    }
 }
 
 double Plan::read_scalar(int slot) {

@@ -41,6 +41,7 @@ Plan::~Plan() {
                          h[0], h[1], h[2], h[3], nR - nG, bw, nG, bs.P);
     }
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    if (ev_sync) (void)hipEventDestroy(ev_sync);
     for (void *p : allocs) (void)hipFree(p);
     if (h_scalar) (void)hipHostFree(h_scalar);
     if (h_fail) (void)hipHostFree(h_fail);
@@ -788,6 +789,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipMemsetAsync(d_Abb, 0, sizeof(double) * (size_t)nB * 9, s));
     MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
     MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
+    if (const char *e = std::getenv("MMBA_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
     MMBA_HIP(hipStreamSynchronize(s));
 }

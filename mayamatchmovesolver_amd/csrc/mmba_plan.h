@@ -196,7 +196,9 @@ struct Plan {
         SL_XN2T = 12,   // ||D x_new||^2 of the trial point
         NSLOT = 16
     };
-    void read_slots(int lo, int hi);  // [lo, hi] inclusive, one D2H copy + sync
+    void read_slots(int lo, int hi);
+    bool spin_wait = true;  // MMBA_SPIN_WAIT=0: blocking synchronisation
+    hipEvent_t ev_sync = nullptr;  // [lo, hi] inclusive, one D2H copy + sync
     double read_scalar(int slot = 0);
     void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
     double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
