@@ -99,7 +99,8 @@ struct BandSolver {
 
 // Where entry (R, C), R >= C, of the reduced system lives.
 struct SView {
-    int band;  // 0: 64x64 tiles, 1: band + arrow
+    int band;  // 0: 64x64 tiles (or dense), 1: band + arrow
+    int dense, ld;  // dense: column-major lower triangle, leading dimension ld
     // tiles
     double *S;
     const int *slot;
@@ -179,6 +180,7 @@ __device__ __forceinline__ size_t widx(const DevProblem &P, int k, int i) {
 }
 
 __device__ __forceinline__ double *s_at(const SView &V, int R, int C) {
+    if (V.dense) return &V.S[(size_t)C * V.ld + R];
     if (!V.band) {
         const int s = V.slot[(R / TILE) * V.NT + (C / TILE)];
         return &V.S[(size_t)s * TILE * TILE + (R % TILE) * TILE + (C % TILE)];

@@ -224,6 +224,8 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
             MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
             if (nG > 0) MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * (size_t)nG * nb, s));
             MMBA_HIP(hipMemsetAsync(bs.Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
+        } else if (dense) {
+            MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nRpad * dld, s));
         } else if (!band) {
             MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         }
@@ -245,6 +247,8 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         span_begin(SPAN_CHOL);
         if (band) {
             band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
+        } else if (dense) {
+            ds.factor(s, d_S, nRpad, dld, d_fail);
         } else {
             for (int k = 0; k < NT; ++k) {
                 const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
@@ -260,6 +264,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
                 launch_keep_rows(s, d_xR, Ra, Rb, nR - nG, nR, rank == 0);
                 allreduce(d_xR, nR);
             }
+        } else if (dense) {
+            ds.forward(s, d_S, nRpad, dld, d_rhs, d_yR);
+            ds.backward(s, d_S, nRpad, dld, d_yR, d_xR);
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_rhs, d_yR);
             launch_trsv_bwd_all(s, d_S, d_slot, NT, d_cols_off, d_cols, d_Linv, d_yR, d_xR);
@@ -312,6 +319,8 @@ void Plan::newton_enqueue(double dxnorm) {
     if (nR > 0) {
         if (band) {
             band_forward(s, bs, d_wR, d_yR);
+        } else if (dense) {
+            ds.forward(s, d_S, nRpad, dld, d_wR, d_yR);
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_wR, d_yR);
         } else {

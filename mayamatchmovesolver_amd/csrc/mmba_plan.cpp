@@ -533,34 +533,47 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 const long long kb = bobs_off[b + 1] - bobs_off[b];
                 npairs += kb * kb;
             }
-        use_dest = nB_solved > 0 && nR > 0 && npairs <= (32ll << 20);
+        use_dest = nB_solved > 0 && nR > 0 && npairs <= (1ll << 30);
         if (nranks > 1 && nB_solved > 0 && !use_dest)
             throw Unsupported{"sharded solve: too many observation pairs per bundle"};
         if (use_dest) {
             struct PairRec {
                 int cfi, cfj, i, j;
             };
-            std::vector<PairRec> recs;
-            recs.reserve((size_t)npairs / 2 + 16);
-            for (int b = 0; b < nB; ++b) {
-                if (bnd_pb[b] == 0) continue;
-                for (int qi = bobs_off[b]; qi < bobs_off[b + 1]; ++qi) {
-                    const int i = bobs[qi], cfi = d_cf[i];
-                    if (cf_pc[cfi] == 0) continue;
-                    for (int qj = bobs_off[b]; qj < bobs_off[b + 1]; ++qj) {
-                        const int j = bobs[qj], cfj = d_cf[j];
-                        // destination rows must be this shard's camera-frames
-                        if (cf_pc[cfj] == 0 || cfi < cfj || !cf_own[cfi]) continue;
-                        recs.push_back({cfi, cfj, i, j});
+            // bucket by destination row cfi (counting pass), then sort each
+            // bucket by (cfj, i, j): O(pairs) grouping instead of one global
+            // sort (C3: ~50M pairs)
+            std::vector<long long> cnt(ncf + 1, 0);
+            auto for_pairs = [&](auto &&fn) {
+                for (int b = 0; b < nB; ++b) {
+                    if (bnd_pb[b] == 0) continue;
+                    for (int qi = bobs_off[b]; qi < bobs_off[b + 1]; ++qi) {
+                        const int i = bobs[qi], cfi = d_cf[i];
+                        if (cf_pc[cfi] == 0 || !cf_own[cfi]) continue;
+                        for (int qj = bobs_off[b]; qj < bobs_off[b + 1]; ++qj) {
+                            const int j = bobs[qj], cfj = d_cf[j];
+                            // destination rows must be this shard's camera-frames
+                            if (cf_pc[cfj] == 0 || cfi < cfj) continue;
+                            fn(cfi, cfj, i, j);
+                        }
                     }
                 }
+            };
+            for_pairs([&](int cfi, int, int, int) { cnt[cfi + 1]++; });
+            for (int cf = 0; cf < ncf; ++cf) cnt[cf + 1] += cnt[cf];
+            std::vector<PairRec> recs((size_t)cnt[ncf]);
+            {
+                std::vector<long long> pos(cnt.begin(), cnt.end() - 1);
+                for_pairs([&](int cfi, int cfj, int i, int j) { recs[pos[cfi]++] = {cfi, cfj, i, j}; });
             }
-            std::sort(recs.begin(), recs.end(), [](const PairRec &x, const PairRec &y) {
-                if (x.cfi != y.cfi) return x.cfi < y.cfi;
-                if (x.cfj != y.cfj) return x.cfj < y.cfj;
-                if (x.i != y.i) return x.i < y.i;
-                return x.j < y.j;
-            });
+            for (int cf = 0; cf < ncf; ++cf)
+                std::sort(recs.begin() + cnt[cf], recs.begin() + cnt[cf + 1],
+                          [](const PairRec &x, const PairRec &y) {
+                              if (x.cfj != y.cfj) return x.cfj < y.cfj;
+                              if (x.i != y.i) return x.i < y.i;
+                              return x.j < y.j;
+                          });
+            dpairs_h.reserve(recs.size());
             for (size_t q = 0; q < recs.size(); ++q) {
                 if (q == 0 || recs[q].cfi != recs[q - 1].cfi || recs[q].cfj != recs[q - 1].cfj) {
                     dest_h.push_back(make_int2(recs[q].cfi, recs[q].cfj));
@@ -717,8 +730,22 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_dest_off = upload(dest_off_h);
         d_dpairs = upload(dpairs_h);
     }
-    d_S = dalloc<double>((size_t)nslots * TILE * TILE);
-    d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
+    {
+        // dense reduced system: at least 30 % of the lower tiles non-zero
+        // after fill (MMBA_DENSE=0 keeps the tiled path, =1 forces dense)
+        const long long full = (long long)NT * (NT + 1) / 2;
+        dense = !band && nranks == 1 && NT >= 8 && (long long)nslots * 10 >= full * 3;
+        if (const char *e = std::getenv("MMBA_DENSE"))
+            dense = !band && nranks == 1 && NT > 0 && std::atoi(e) != 0;
+    }
+    if (dense) {
+        dld = nRpad;
+        d_S = dalloc<double>((size_t)nRpad * nRpad);
+        d_Linv = nullptr;
+    } else {
+        d_S = dalloc<double>((size_t)nslots * TILE * TILE);
+        d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
+    }
     if (band) setup_band();
     if (band && std::getenv("MMBA_PROBE")) {
         d_probe = dalloc<long long>(4);

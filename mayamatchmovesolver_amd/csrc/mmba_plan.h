@@ -37,6 +37,17 @@ struct Invalid {
 void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd, int nB,
                   int nranks, int32_t *bounds, int32_t *bnd_owner);
 
+// Dense reduced system (mmba_dense.hip): blocked Cholesky with rocBLAS
+// trsm/syrk/gemm trailing updates and a one-wave panel kernel.
+struct DenseSolver {
+    void *handle = nullptr;  // rocblas_handle
+    ~DenseSolver();
+    void init(hipStream_t s);
+    void factor(hipStream_t s, double *A, int n, int ld, int *fail);
+    void forward(hipStream_t s, const double *A, int n, int ld, const double *r, double *y);
+    void backward(hipStream_t s, const double *A, int n, int ld, const double *y, double *x);
+};
+
 struct Plan {
     mmba_context *ctx = nullptr;
     hipStream_t s = nullptr;
@@ -86,6 +97,8 @@ struct Plan {
     SView sview() const {
         SView V{};
         V.band = band ? 1 : 0;
+        V.dense = dense ? 1 : 0;
+        V.ld = dld;
         V.S = d_S;
         V.slot = d_slot;
         V.NT = NT;
@@ -96,6 +109,10 @@ struct Plan {
         V.Gd = bs.Gd;
         return V;
     }
+    // dense reduced system (most tiles structurally non-zero)
+    bool dense = false;
+    int dld = 0;
+    DenseSolver ds;
     long long *d_probe = nullptr;  // MMBA_PROBE=1: band-kernel phase cycles
     // single-workgroup triangular solves for narrow (banded) structures
     bool narrow = false;

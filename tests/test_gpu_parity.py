@@ -95,3 +95,15 @@ def test_config_parity(idx, kw, oracle, gpu_ctx):
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
     check_solve(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_reduced_system_dense_and_tiled(dense, oracle, gpu_ctx, monkeypatch):
+    """The C3 structure (bundles tracked by several cameras across the whole
+    shot: an almost dense reduced system) through both reduced-system solvers:
+    the tiled Cholesky and the dense blocked Cholesky (rocBLAS trsm/syrk
+    trailing updates, one-wave panel kernel), each against the oracle."""
+    monkeypatch.setenv("MMBA_DENSE", dense)
+    prob = S.make_config(2, frames=10, scale=0.004)
+    opt = S.config_options(prob)
+    check_solve(prob, opt, oracle, gpu_ctx)

@@ -1,0 +1,7 @@
+# Kernel stats of one full-size C3 solve.
+set -o pipefail
+OUT=${1:-gpurun_out/c3}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof -o c3 --output-format csv -- python3 bench.py --config 2 --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > $OUT/prof.json 2> $OUT/prof.err || exit 1
+echo done
