@@ -104,6 +104,6 @@ def test_reduced_system_dense_and_tiled(dense, oracle, gpu_ctx, monkeypatch):
     the tiled Cholesky and the dense blocked Cholesky (rocBLAS trsm/syrk
     trailing updates, one-wave panel kernel), each against the oracle."""
     monkeypatch.setenv("MMBA_DENSE", dense)
-    prob = S.make_config(2, frames=10, scale=0.004)
+    prob = S.make_config(2, frames=8, scale=0.002)
     opt = S.config_options(prob)
     check_solve(prob, opt, oracle, gpu_ctx)
