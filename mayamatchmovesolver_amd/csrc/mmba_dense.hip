@@ -3,19 +3,24 @@
 // When the bundles tie most camera-frames together (C3: every bundle is
 // tracked by five cameras over windows spread across the whole shot) the
 // reduced system S has almost no zero tiles and its Cholesky factor is
-// dense.  S is then held as one column-major lower triangle (ld = nRpad) and
-// factored by a right-looking blocked Cholesky:
+// dense.  S is then held as one column-major lower triangle A (n = nRpad
+// columns, ld = n + 64 rows) and factored right-looking in 64-column panels
+// grouped into 256-column blocks:
 //
-//   for each 64-column panel k:  L_kk = chol(S_kk)       k_dense_potf64 (one wave)
-//                                L_ik = S_ik L_kk^-T      rocblas_dtrsm (MFMA)
-//                                S_ii -= L_ik L_ik^T      rocblas_dsyrk (MFMA)
+//   panel k:  L_kk = chol(A_kk), Linv_kk = L_kk^-1     k_dense_potf64 (one wave)
+//             L_ik = A_ik Linv_kk^T                    rocblas_dgemm (MFMA fp64)
+//             in-block trailing columns                 rocblas_dsyrk / dgemm
+//   block:    A_22 -= L_21 L_21^T (rank 256)            rocblas_dsyrk (MFMA fp64)
 //
-// grouped so the trailing updates run as large rank-256 SYRK/GEMM calls
-// (the 64-column panels inside a 256-column block are factored with small
-// trsm/syrk calls on the block only).  The flops are the n^3/3 of a dense
-// Cholesky, in fp64 MFMA library GEMMs; the panel factorisation is a
-// hand-written one-wave register kernel (the latency-bound part).
-// Solves L y = r and L^T x = y are rocblas_dtrsv.
+// The right-hand side rides along as row n of A (A[n, j] = r_j): the panel
+// GEMMs and trailing updates that produce L also produce row n of the
+// factor of [S r; r^T .], which is y = L^-1 r -- the forward solve costs
+// nothing extra.  The backward solve x = L^-T y (and a stand-alone forward
+// solve for lmpar's Newton term) walk the 64-row blocks with two GEMVs per
+// block (the diagonal block through the stored Linv_kk, then the update of
+// the rest), rocblas_dgemv.  The flops are those of a dense Cholesky, n^3/3,
+// in MFMA library GEMMs; the panel factorisation is the hand-written,
+// latency-bound part.
 #include <rocblas/rocblas.h>
 
 #include "mmba_kernels.h"
@@ -30,13 +35,30 @@ __device__ __forceinline__ double dn_rdlane(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// In-place Cholesky of the 64 x 64 diagonal block at A (column-major, ld):
-// lane r holds row r in registers, the pivot is broadcast with v_readlane and
-// column j through LDS.  A non-positive or non-finite pivot sets *fail and is
-// replaced by 1 (the factorisation continues; the LM treats the solve as
-// failed).  Only the lower triangle is read and written.
-__global__ void __launch_bounds__(64) k_dense_potf64(double *A, int ld, int *fail) {
+__device__ __forceinline__ double dn_rsq(double d) {  // 1/sqrt(d), full fp64
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+__device__ __forceinline__ void dn_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// In-place Cholesky of the 64 x 64 diagonal block at A (column-major, ld)
+// and its inverse Linv (column-major 64 x 64, lower, ld 64): lane r holds row
+// r in registers, the pivot is broadcast with v_readlane and column j
+// through LDS; the inverse is formed column-oriented (lane = column of the
+// identity).  A non-positive or non-finite pivot sets *fail and is replaced
+// by 1 (the factorisation continues; the LM treats the solve as failed).
+__global__ void __launch_bounds__(64) k_dense_potf64(double *A, int ld, double *Linv,
+                                                     int *fail) {
     __shared__ double col[64];
+    __shared__ double Ls[64][65];
+    __shared__ double rsv[64];
     const int lane = threadIdx.x;
     double a[64];
 #pragma unroll
@@ -49,21 +71,50 @@ __global__ void __launch_bounds__(64) k_dense_potf64(double *A, int ld, int *fai
             bad = 1;
             d = 1.;
         }
-        const double sd = sqrt(d);
-        const double l = lane > j ? a[j] / sd : 0.;
-        a[j] = lane == j ? sd : (lane > j ? l : a[j]);
+        const double rs = dn_rsq(d);
+        const double l = lane > j ? a[j] * rs : 0.;
+        a[j] = lane == j ? d * rs : (lane > j ? l : a[j]);
         col[lane] = l;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) rsv[j] = rs;
+        dn_wave_sync();
 #pragma unroll
         for (int c = j + 1; c < 64; ++c) a[c] = fma(-l, col[c], a[c]);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        dn_wave_sync();
     }
 #pragma unroll
-    for (int c = 0; c < 64; ++c)
-        if (c <= lane) A[(size_t)c * ld + lane] = a[c];
+    for (int c = 0; c < 64; ++c) {
+        const double v = c <= lane ? a[c] : 0.;
+        Ls[lane][c] = v;
+        if (c <= lane) A[(size_t)c * ld + lane] = v;
+    }
+    dn_wave_sync();
+    // inverse, column cc = lane of the identity: x <- L^-1 e_cc
+    {
+        const int cc = lane;
+        double x[64];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) x[i] = (i == cc) ? 1. : 0.;
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+            x[t] *= rsv[t];
+#pragma unroll
+            for (int i = t + 1; i < 64; ++i) x[i] = fma(-Ls[i][t], x[t], x[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 64; ++i) Linv[(size_t)cc * 64 + i] = x[i];  // column cc
+    }
     if (bad && lane == 0) atomicOr(fail, 1);
+}
+
+// A[n, j] = r[j] (the right-hand side as row n of the factored matrix) and
+// y[j] = A[n, j] after the factorisation.
+__global__ void k_dense_row_put(double *A, int ld, int n, const double *r) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) A[(size_t)j * ld + n] = r[j];
+}
+__global__ void k_dense_row_get(const double *A, int ld, int n, double *y) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) y[j] = A[(size_t)j * ld + n];
 }
 
 #define MMBA_RB(call)                                                                    \
@@ -89,25 +140,27 @@ void DenseSolver::init(hipStream_t s) {
     MMBA_RB(rocblas_set_pointer_mode((rocblas_handle)handle, rocblas_pointer_mode_host));
 }
 
-// Factor rows/columns [k0, k0 + nb) of the trailing matrix: 64-column panels,
-// each followed by the trsm/syrk of the rows below it up to row `end`.
-static void dense_block(rocblas_handle h, double *A, int ld, int k0, int nb, int end,
-                        int *fail, hipStream_t s) {
-    const double one = 1.0, mone = -1.0;
+// Panels of the block of columns [k0, k0 + nb); rows below the diagonal run
+// to `end` (exclusive; includes the right-hand-side row).
+void DenseSolver::block(hipStream_t s, double *A, int ld, int k0, int nb, int end, int *fail) {
+    rocblas_handle h = (rocblas_handle)handle;
+    const double one = 1.0, mone = -1.0, zero = 0.0;
     for (int p = k0; p < k0 + nb; p += 64) {
         double *App = A + (size_t)p * ld + p;
-        k_dense_potf64<<<1, 64, 0, s>>>(App, ld, fail);
+        double *Li = Linv + (size_t)(p / 64) * 64 * 64;
+        k_dense_potf64<<<1, 64, 0, s>>>(App, ld, Li, fail);
         const int m = end - (p + 64);
         if (m <= 0) continue;
         double *Aip = App + 64;
-        MMBA_RB(rocblas_dtrsm(h, rocblas_side_right, rocblas_fill_lower,
-                              rocblas_operation_transpose, rocblas_diagonal_non_unit, m, 64,
-                              &one, App, ld, Aip, ld));
-        // update only the rest of this block's columns [p + 64, k0 + nb)
+        // L_ip = A_ip Linv^T, out of place, then back into A
+        MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, 64, 64,
+                              &one, Aip, ld, Li, 64, &zero, ws, m));
+        MMBA_HIP(hipMemcpy2DAsync(Aip, sizeof(double) * ld, ws, sizeof(double) * m,
+                                  sizeof(double) * m, 64, hipMemcpyDeviceToDevice, s));
+        // the rest of this block's columns [p + 64, k0 + nb)
         const int mb = k0 + nb - (p + 64);
         if (mb > 0) {
             double *Aqq = A + (size_t)(p + 64) * ld + (p + 64);
-            // S[p+64 .. end, p+64 .. k0+nb) -= L[p+64 .. end, p] L[p+64 .. k0+nb, p]^T
             MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mb, 64, &mone,
                                   Aip, ld, &one, Aqq, ld));
             const int mr = end - (k0 + nb);
@@ -119,40 +172,71 @@ static void dense_block(rocblas_handle h, double *A, int ld, int k0, int nb, int
     }
 }
 
-void DenseSolver::factor(hipStream_t s, double *A, int n, int ld, int *fail) {
+void DenseSolver::setup(Plan &pl, int n) {
+    this->n = n;
+    ld = n + 64;
+    A = pl.dalloc<double>((size_t)ld * (n + 1));  // column n: the unused A[n][n]
+    Linv = pl.dalloc<double>((size_t)n * 64);
+    ws = pl.dalloc<double>((size_t)(n + 64) * 64);
+}
+
+void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int *fail) {
     init(s);
     rocblas_handle h = (rocblas_handle)handle;
     const double one = 1.0, mone = -1.0;
+    k_dense_row_put<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, r);
+    const int end = n + 1;  // rows 0..n-1 and the right-hand-side row n
     constexpr int NB = 256;
     for (int k0 = 0; k0 < n; k0 += NB) {
         const int nb = std::min(NB, n - k0);
-        // panels of this block (their trsm covers every row below)
-        dense_block(h, A, ld, k0, nb, n, fail, s);
-        const int m = n - (k0 + nb);
-        if (m <= 0) break;
-        // trailing update with the whole block: S22 -= L21 L21^T (rank nb)
+        block(s, A, ld, k0, nb, end, fail);
+        const int m = end - (k0 + nb);
+        if (k0 + nb >= n) break;
+        // trailing update with the whole block, rhs row included (it also
+        // updates the unused A[n][n])
         double *L21 = A + (size_t)k0 * ld + k0 + nb;
         double *S22 = A + (size_t)(k0 + nb) * ld + (k0 + nb);
         MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, nb, &mone, L21,
                               ld, &one, S22, ld));
     }
+    k_dense_row_get<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, y);
 }
 
-void DenseSolver::forward(hipStream_t s, const double *A, int n, int ld, const double *r,
-                          double *y) {
+// y = L^-1 r: per 64-row block, y_k = Linv_kk t_k, then t_(k+1..) -= L_(k+1..),k y_k.
+void DenseSolver::forward(hipStream_t s, const double *r, double *y) {
     init(s);
-    if (y != r) MMBA_HIP(hipMemcpyAsync(y, r, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-    MMBA_RB(rocblas_dtrsv((rocblas_handle)handle, rocblas_fill_lower, rocblas_operation_none,
-                          rocblas_diagonal_non_unit, n, A, ld, y, 1));
+    rocblas_handle h = (rocblas_handle)handle;
+    const double one = 1.0, mone = -1.0, zero = 0.0;
+    double *t = ws;
+    MMBA_HIP(hipMemcpyAsync(t, r, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    for (int k = 0; k < n; k += 64) {
+        const double *Li = Linv + (size_t)(k / 64) * 64 * 64;
+        MMBA_RB(rocblas_dgemv(h, rocblas_operation_none, 64, 64, &one, Li, 64, t + k, 1, &zero,
+                              y + k, 1));
+        const int m = n - (k + 64);
+        if (m > 0)
+            MMBA_RB(rocblas_dgemv(h, rocblas_operation_none, m, 64, &mone,
+                                  A + (size_t)k * ld + k + 64, ld, y + k, 1, &one, t + k + 64,
+                                  1));
+    }
 }
 
-void DenseSolver::backward(hipStream_t s, const double *A, int n, int ld, const double *y,
-                           double *x) {
+// x = L^-T y: per 64-row block from the last, x_k = Linv_kk^T t_k, then
+// t_(0..k) -= L_k,(0..k)^T x_k.
+void DenseSolver::backward(hipStream_t s, const double *y, double *x) {
     init(s);
-    if (x != y) MMBA_HIP(hipMemcpyAsync(x, y, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-    MMBA_RB(rocblas_dtrsv((rocblas_handle)handle, rocblas_fill_lower,
-                          rocblas_operation_transpose, rocblas_diagonal_non_unit, n, A, ld, x,
-                          1));
+    rocblas_handle h = (rocblas_handle)handle;
+    const double one = 1.0, mone = -1.0, zero = 0.0;
+    double *t = ws;
+    MMBA_HIP(hipMemcpyAsync(t, y, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    for (int k = n - 64; k >= 0; k -= 64) {
+        const double *Li = Linv + (size_t)(k / 64) * 64 * 64;
+        MMBA_RB(rocblas_dgemv(h, rocblas_operation_transpose, 64, 64, &one, Li, 64, t + k, 1,
+                              &zero, x + k, 1));
+        if (k > 0)
+            MMBA_RB(rocblas_dgemv(h, rocblas_operation_transpose, 64, k, &mone, A + k, ld,
+                                  x + k, 1, &one, t, 1));
+    }
 }
 
 }  // namespace mmba

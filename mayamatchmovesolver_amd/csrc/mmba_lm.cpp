@@ -225,7 +225,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
             if (nG > 0) MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * (size_t)nG * nb, s));
             MMBA_HIP(hipMemsetAsync(bs.Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
         } else if (dense) {
-            MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nRpad * dld, s));
+            MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)(nRpad + 1) * dld, s));
         } else if (!band) {
             MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         }
@@ -248,7 +248,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         if (band) {
             band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
         } else if (dense) {
-            ds.factor(s, d_S, nRpad, dld, d_fail);
+            ds.factor_forward(s, d_rhs, d_yR, d_fail);  // y = L^-1 rhs rides along
         } else {
             for (int k = 0; k < NT; ++k) {
                 const int r0 = panel_rows_off[k], nr = panel_rows_off[k + 1] - r0;
@@ -265,8 +265,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
                 allreduce(d_xR, nR);
             }
         } else if (dense) {
-            ds.forward(s, d_S, nRpad, dld, d_rhs, d_yR);
-            ds.backward(s, d_S, nRpad, dld, d_yR, d_xR);
+            ds.backward(s, d_yR, d_xR);
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_rhs, d_yR);
             launch_trsv_bwd_all(s, d_S, d_slot, NT, d_cols_off, d_cols, d_Linv, d_yR, d_xR);
@@ -320,7 +319,7 @@ void Plan::newton_enqueue(double dxnorm) {
         if (band) {
             band_forward(s, bs, d_wR, d_yR);
         } else if (dense) {
-            ds.forward(s, d_S, nRpad, dld, d_wR, d_yR);
+            ds.forward(s, d_wR, d_yR);
         } else if (narrow) {
             launch_trsv_fwd_all(s, d_S, d_slot, NT, d_rows_off, d_rows, d_Linv, d_wR, d_yR);
         } else {

@@ -739,8 +739,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             dense = !band && nranks == 1 && NT > 0 && std::atoi(e) != 0;
     }
     if (dense) {
-        dld = nRpad;
-        d_S = dalloc<double>((size_t)nRpad * nRpad);
+        ds.setup(*this, nRpad);
+        d_S = ds.A;
+        dld = ds.ld;
         d_Linv = nullptr;
     } else {
         d_S = dalloc<double>((size_t)nslots * TILE * TILE);

@@ -37,15 +37,21 @@ struct Invalid {
 void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd, int nB,
                   int nranks, int32_t *bounds, int32_t *bnd_owner);
 
-// Dense reduced system (mmba_dense.hip): blocked Cholesky with rocBLAS
-// trsm/syrk/gemm trailing updates and a one-wave panel kernel.
+// Dense reduced system (mmba_dense.hip): blocked right-looking Cholesky,
+// one-wave panel kernel + rocBLAS GEMM/SYRK trailing updates, right-hand
+// side carried as an extra row (fused forward solve), GEMV block solves.
+struct Plan;
 struct DenseSolver {
     void *handle = nullptr;  // rocblas_handle
+    int n = 0, ld = 0;       // columns (nRpad), leading dimension (n + 64)
+    double *A = nullptr, *Linv = nullptr, *ws = nullptr;
     ~DenseSolver();
+    void setup(Plan &pl, int n);
     void init(hipStream_t s);
-    void factor(hipStream_t s, double *A, int n, int ld, int *fail);
-    void forward(hipStream_t s, const double *A, int n, int ld, const double *r, double *y);
-    void backward(hipStream_t s, const double *A, int n, int ld, const double *y, double *x);
+    void block(hipStream_t s, double *A, int ld, int k0, int nb, int end, int *fail);
+    void factor_forward(hipStream_t s, const double *r, double *y, int *fail);
+    void forward(hipStream_t s, const double *r, double *y);
+    void backward(hipStream_t s, const double *y, double *x);
 };
 
 struct Plan {
