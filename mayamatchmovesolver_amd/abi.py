@@ -164,11 +164,11 @@ class MmbaKernelStats(C.Structure):
         ("chol_flops", C.c_double),
         ("chol_launches", C.c_int32),
         ("reduced_dim", C.c_int32),
-        ("pad1", C.c_int32),
+        ("reduced_kind", C.c_int32),
     ]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_ if name != "pad1"}
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 # Functions exported by libmmba.so (checked by tests/test_abi.py against
