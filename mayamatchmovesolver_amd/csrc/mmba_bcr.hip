@@ -175,21 +175,34 @@ __device__ __forceinline__ void bcr_chol_wave(double *M, double *rs_out, double 
     double a[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) a[c] = (lane < K && c <= lane) ? M[lane * KS + c] : 0.;
+    // Look-ahead: the next pivot only needs column j + 1, whose multiplier
+    // l_(j+1) is lane j + 1's own l (broadcast by v_readlane, no LDS), so
+    // column j + 1 is updated and the next pivot and its reciprocal root are
+    // formed before the LDS round trip of the remaining columns -- the
+    // pivot chain overlaps the bulk update.  Same operations and operands as
+    // the plain loop (a[j+1] = fma(-l, col[j+1], a[j+1]) with col[j+1] = l_(j+1)).
+    double d = bcr_rdlane(a[0], 0);
+    bool dbad = !(d > 0.) || !isfinite(d);
+    if (dbad) d = 1.;
+    double rs = bcr_rsq(d);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        double d = bcr_rdlane(a[j], j);
-        if (!(d > 0.) || !isfinite(d)) {
-            bad = 1;
-            d = 1.;
-        }
-        const double rs = bcr_rsq(d);
+        if (dbad) bad = 1;
         const double l = (lane > j) ? a[j] * rs : 0.;
         a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
         if (lane < K) col[lane] = l;
         if (lane == 0) rs_out[j] = rs;
+        if (j + 1 < K) {
+            const double lj1 = bcr_rdlane(l, j + 1);
+            a[j + 1] = fma(-l, lj1, a[j + 1]);
+            d = bcr_rdlane(a[j + 1], j + 1);
+            dbad = !(d > 0.) || !isfinite(d);
+            if (dbad) d = 1.;
+            rs = bcr_rsq(d);
+        }
         wave_lds_sync();
 #pragma unroll
-        for (int c = j + 1; c < K; ++c) a[c] = fma(-l, col[c], a[c]);
+        for (int c = j + 2; c < K; ++c) a[c] = fma(-l, col[c], a[c]);
         wave_lds_sync();
     }
     if (lane < K)
