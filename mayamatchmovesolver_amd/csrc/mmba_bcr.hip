@@ -436,9 +436,31 @@ template <int N>
 __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y) {
     constexpr int NS = N + 2;
     __shared__ double T[N * NS], Ti[N * NS], col[64];
+    __shared__ double zsum[NGMAX * NGMAX], gsum[NGMAX];
     const int lane = threadIdx.x;
     const int K = B.K, nG = B.nG, n0 = K + nG;
     const double *D0 = B.Dk;
+    // sum_o Y_o^T Y_o and sum_o gpart_o over the eliminated blocks: lanes
+    // stride over o, then a fixed xor-shuffle tree (a serial loop over the
+    // blocks was a chain of nblk dependent loads: 78 us at nblk = 360)
+    for (int e = 0; e < nG * nG + (y ? nG : 0); ++e) {
+        double v = 0.;
+        if (e < nG * nG) {
+            for (int o = 1 + lane; o < B.nblk; o += 64) v += B.Zc[(size_t)o * nG * nG + e];
+        } else {
+            const int q = e - nG * nG;
+            for (int o = 1 + lane; o < B.nblk; o += 64) v += B.gpart[(size_t)o * nG + q];
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) {
+            if (e < nG * nG)
+                zsum[e] = v;
+            else
+                gsum[e - nG * nG] = v;
+        }
+    }
+    __syncthreads();
     for (int q = lane; q < N * N; q += 64) {
         const int i = q / N, c = q % N;
         double v = 0.;
@@ -448,8 +470,7 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
             v = B.Gk[(i - K) * K + c];  // block 0 arrow
         } else if (i >= K && i < n0 && c >= K && c <= i) {
             const int a = i - K, b = c - K;
-            v = B.Gd[a * NGMAX + b];
-            for (int o = 1; o < B.nblk; ++o) v -= B.Zc[(size_t)o * nG * nG + a * nG + b];
+            v = B.Gd[a * NGMAX + b] - zsum[a * nG + b];
         } else if (i == c) {
             v = 1.;  // padding beyond n0
         }
@@ -466,9 +487,7 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
         if (lane < K) col[lane] = bcr_get(B.rw, lane, nb);
         if (lane >= K && lane < n0) {
             const int q = lane - K;
-            double g = B.rw[nb + q];
-            for (int o = 1; o < B.nblk; ++o) g -= B.gpart[(size_t)o * nG + q];
-            col[lane] = g;
+            col[lane] = B.rw[nb + q] - gsum[q];
         }
         wave_lds_sync();
         if (lane < n0) {
@@ -555,13 +574,13 @@ __global__ void __launch_bounds__(64) k_bcr_fwd_root(BcrDev B, const double *rw,
     __shared__ double v[K + NGMAX];
     const int lane = threadIdx.x, nb = B.nb, nG = B.nG;
     if (lane < K) v[lane] = bcr_get(rw, lane, nb);
-    if (lane < NGMAX) {
-        double g = 0.;
-        if (lane < nG) {
-            g = rw[nb + lane];
-            for (int o = 1; o < B.nblk; ++o) g -= B.gpart[(size_t)o * nG + lane];
-        }
-        v[K + lane] = g;
+    if (lane < NGMAX) v[K + lane] = 0.;
+    for (int q = 0; q < nG; ++q) {  // lanes stride over the blocks (see k_bcr_root)
+        double gs = 0.;
+        for (int o = 1 + lane; o < B.nblk; o += 64) gs += B.gpart[(size_t)o * nG + q];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) gs += __shfl_xor(gs, off);
+        if (lane == 0) v[K + q] = rw[nb + q] - gs;
     }
     __syncthreads();
     if (lane < K + nG) {

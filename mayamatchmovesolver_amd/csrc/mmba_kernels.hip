@@ -525,13 +525,14 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
                                                const double *__restrict__ f, double *Acc,
                                                double *Acg, double *g) {
     __shared__ double sJ[2 * LMAX][NE_CHUNK];
-    __shared__ int sC[LMAX][NE_CHUNK];
-    __shared__ int sN[NE_CHUNK];
+    __shared__ int sG[NGMAX][NE_CHUNK];  // local column of global q in observation o (-1)
     __shared__ double sF[2][NE_CHUNK];
     const int cf = blockIdx.x;
     if (!own_cf(P, cf)) return;  // another shard owns this camera-frame
     const int pc = P.cf_pc[cf];
     const int nG = P.nG;
+    const int nCF = P.nR - nG;
+    const int lm = P.lmax;  // widest observation: only these J rows are staged
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const int M = P.M;
     const int ncc = pc * (pc + 1) / 2;
@@ -556,22 +557,28 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
         eb = (e - ncc - pc) % nG;
         kind = 2;
     }
-    const int gp = (kind == 2) ? P.g_param[eb] : -1;
     double acc = 0.;
     for (int c0 = o0; c0 < o1; c0 += NE_CHUNK) {
         const int cnt = min(NE_CHUNK, o1 - c0);
         __syncthreads();
-        for (int t = threadIdx.x; t < 2 * LMAX * NE_CHUNK; t += blockDim.x) {
+        for (int t = threadIdx.x; t < 2 * lm * NE_CHUNK; t += blockDim.x) {
             const int row = t / NE_CHUNK, o = t % NE_CHUNK;
             sJ[row][o] = (o < cnt) ? J[(size_t)row * M + c0 + o] : 0.;
         }
-        if (nG > 0)
-            for (int t = threadIdx.x; t < LMAX * NE_CHUNK; t += blockDim.x) {
-                const int row = t / NE_CHUNK, o = t % NE_CHUNK;
-                sC[row][o] = (o < cnt) ? jcol[(size_t)row * M + c0 + o] : -1;
+        if (nG > 0) {
+            for (int t = threadIdx.x; t < NGMAX * NE_CHUNK; t += blockDim.x)
+                sG[t / NE_CHUNK][t % NE_CHUNK] = -1;
+            __syncthreads();
+            // columns l >= pc of every observation: which global parameter
+            // (the camera block's own columns come first, l < pc)
+            for (int t = threadIdx.x; t < lm * NE_CHUNK; t += blockDim.x) {
+                const int l = t / NE_CHUNK, o = t % NE_CHUNK;
+                if (o >= cnt || l < pc || l >= nloc[c0 + o]) continue;
+                const int p = jcol[(size_t)l * M + c0 + o];
+                if (P.p_class[p] == PC_G) sG[P.p_pos[p] - nCF][o] = l;
             }
+        }
         for (int t = threadIdx.x; t < NE_CHUNK; t += blockDim.x) {
-            sN[t] = (t < cnt) ? nloc[c0 + t] : 0;
             sF[0][t] = (t < cnt) ? f[2 * (c0 + t)] : 0.;
             sF[1][t] = (t < cnt) ? f[2 * (c0 + t) + 1] : 0.;
         }
@@ -584,12 +591,9 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
                 acc += sJ[2 * ea][o] * sF[0][o] + sJ[2 * ea + 1][o] * sF[1][o];
         } else if (kind == 2) {
             for (int o = 0; o < cnt; ++o) {
-                for (int l = pc; l < sN[o]; ++l) {
-                    if (sC[l][o] == gp) {
-                        acc += sJ[2 * ea][o] * sJ[2 * l][o] + sJ[2 * ea + 1][o] * sJ[2 * l + 1][o];
-                        break;
-                    }
-                }
+                const int l = sG[eb][o];
+                if (l >= 0)
+                    acc += sJ[2 * ea][o] * sJ[2 * l][o] + sJ[2 * ea + 1][o] * sJ[2 * l + 1][o];
             }
         }
     }
@@ -741,6 +745,11 @@ __global__ void k_ne_bnd(DevProblem P, const double *__restrict__ J,
 }
 
 // Globals: partial sums of Agg (nG x nG) and gG per block of observations.
+// NG: compile-time bound on the number of global parameters (2, 4, 8 or
+// NGMAX): the per-thread accumulators are NG^2 + NG registers (a 272-double
+// NGMAX array spilled 2 KB per lane to scratch).  Partial rows keep the
+// NGMAX layout.
+template <int NG>
 __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__restrict__ J,
                                                  const int *__restrict__ jcol,
                                                  const int *__restrict__ nloc,
@@ -750,21 +759,22 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
     // thread scatters its global-parameter Jacobian entries into a dense
     // register vector, products are reduced wave -> block in a fixed order
     // (deterministic, no atomics).
-    __shared__ double wsum[4][NGMAX * NGMAX + NGMAX];
+    constexpr int NA = NG * NG + NG;
+    __shared__ double wsum[4][NA];
     const int nG = P.nG;
     const int nCF = P.nR - nG;
     const int M = P.M;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double accv[NGMAX * NGMAX + NGMAX];
+    double accv[NA];
 #pragma unroll
-    for (int e = 0; e < NGMAX * NGMAX + NGMAX; ++e) accv[e] = 0.;
+    for (int e = 0; e < NA; ++e) accv[e] = 0.;
     const int i0 = blockIdx.x * chunk;
     const int i1 = min(M, i0 + chunk);
     for (int i = i0 + (int)threadIdx.x; i < i1; i += blockDim.x) {
         if (!own_obs(P, i)) continue;
-        double gx[NGMAX], gy[NGMAX];
+        double gx[NG], gy[NG];
 #pragma unroll
-        for (int q = 0; q < NGMAX; ++q) gx[q] = gy[q] = 0.;
+        for (int q = 0; q < NG; ++q) gx[q] = gy[q] = 0.;
         const int nl = nloc[i];
         for (int l = 0; l < nl; ++l) {
             const int p = jcol[(size_t)l * M + i];
@@ -772,37 +782,36 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
             const int gi = P.p_pos[p] - nCF;
             const double jx = J[(size_t)(2 * l) * M + i], jy = J[(size_t)(2 * l + 1) * M + i];
 #pragma unroll
-            for (int q = 0; q < NGMAX; ++q) {
+            for (int q = 0; q < NG; ++q) {
                 gx[q] = (gi == q) ? jx : gx[q];
                 gy[q] = (gi == q) ? jy : gy[q];
             }
         }
         const double fx = f[2 * i], fy = f[2 * i + 1];
 #pragma unroll
-        for (int a = 0; a < NGMAX; ++a) {
-            if (a >= nG) break;
+        for (int a = 0; a < NG; ++a) {
 #pragma unroll
-            for (int b = 0; b < NGMAX; ++b) {
-                if (b >= nG) break;
-                accv[a * NGMAX + b] += gx[a] * gx[b] + gy[a] * gy[b];
-            }
-            accv[NGMAX * NGMAX + a] += gx[a] * fx + gy[a] * fy;
+            for (int b = 0; b < NG; ++b) accv[a * NG + b] += gx[a] * gx[b] + gy[a] * gy[b];
+            accv[NG * NG + a] += gx[a] * fx + gy[a] * fy;
         }
     }
 #pragma unroll
-    for (int e = 0; e < NGMAX * NGMAX + NGMAX; ++e) {
-        const bool used = (e < NGMAX * NGMAX) ? ((e / NGMAX) < nG && (e % NGMAX) < nG)
-                                               : (e - NGMAX * NGMAX) < nG;
-        if (!used) continue;
+    for (int e = 0; e < NA; ++e) {
         double v = accv[e];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0) wsum[wave][e] = v;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < NGMAX * NGMAX + NGMAX; e += blockDim.x) {
-        const double v = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
-        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + e] = v;
+    for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
+        const bool mat = t < NGMAX * NGMAX;
+        const int a = mat ? t / NGMAX : t - NGMAX * NGMAX, b = mat ? t % NGMAX : 0;
+        double v = 0.;
+        if (a < NG && b < NG) {
+            const int e = mat ? a * NG + b : NG * NG + a;
+            v = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
+        }
+        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = v;
     }
 }
 
@@ -2003,7 +2012,14 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
     }
     if (P.nG > 0) {
         const int nb = nblk(P.M, glob_chunk);
-        k_ne_glob<<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+        if (P.nG <= 2)
+            k_ne_glob<2><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+        else if (P.nG <= 4)
+            k_ne_glob<4><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+        else if (P.nG <= 8)
+            k_ne_glob<8><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+        else
+            k_ne_glob<NGMAX><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
         k_ne_glob_reduce<<<1, 256, 0, s>>>(P, glob_partial, nb, Agg, gG);
     }
 }

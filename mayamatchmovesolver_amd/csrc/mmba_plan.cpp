@@ -685,6 +685,19 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bobs = upload(bobs);
     D.cam_lpar_off = upload(cam_lpar_off);
     D.cam_lpar = upload(cam_lpar);
+    {
+        // widest observation (local Jacobian columns): camera variants +
+        // bundle-side parameters + the camera's lens parameters
+        int lm = 1;
+        for (int i = 0; i < M; ++i) {
+            const int cf = d_cf[i], b = d_bnd[i], cam = d_cam[i];
+            const int w = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
+                          (bnd_par_off[b + 1] - bnd_par_off[b]) +
+                          (cam_lpar_off[cam + 1] - cam_lpar_off[cam]);
+            lm = std::max(lm, w);
+        }
+        D.lmax = std::min(lm, LMAX);
+    }
     D.p_attr = upload(pr->param_attr, n);
     D.p_frame = upload(pr->param_frame, n);
     D.p_class = upload(p_class);

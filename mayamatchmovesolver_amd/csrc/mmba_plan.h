@@ -73,7 +73,7 @@ struct Plan {
     int nB_solved = 0;  // bundles with a B block
     bool rank_deficient = false;
     int nparts = 256;
-    int glob_chunk = 4096;
+    int glob_chunk = 512;
 
     // host structure
     std::vector<int> ref_of_dev;
