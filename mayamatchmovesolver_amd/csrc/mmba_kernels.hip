@@ -612,21 +612,25 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
 // lane o accumulates the upper triangle of Acc and gC over the observations
 // o, o + 64, ... of the (contiguous) segment in registers; the 64 partial
 // sums are added through LDS in a fixed order.
-template <int PC>
-__global__ void __launch_bounds__(64) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
-                                                const double *__restrict__ f, double *Acc,
-                                                double *g) {
+template <int PC, int NW>
+__global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
+                                                     const double *__restrict__ f, double *Acc,
+                                                     double *g) {
+    // NW waves per camera-frame (long segments: C2 has ~1,700 observations
+    // per camera-frame): thread t takes observations t, t + 64 NW, ...;
+    // each wave folds its partial sums with a fixed xor-shuffle tree, the NW
+    // wave sums are added in wave order (deterministic)
     constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC;
-    __shared__ double red[NE][65];
+    __shared__ double wsum[NW][NE];
     const int cf = blockIdx.x;
     if (!own_cf(P, cf) || P.cf_pc[cf] != PC) return;
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const size_t M = P.M;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double acc[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) acc[e] = 0.;
-    for (int i = o0 + lane; i < o1; i += 64) {
+    for (int i = o0 + tid; i < o1; i += 64 * NW) {
         double jx[PC], jy[PC];
 #pragma unroll
         for (int a = 0; a < PC; ++a) {
@@ -643,12 +647,18 @@ __global__ void __launch_bounds__(64) k_ne_cf_u(DevProblem P, const double *__re
         for (int a = 0; a < PC; ++a) acc[NCC + a] += jx[a] * fx + jy[a] * fy;
     }
 #pragma unroll
-    for (int e = 0; e < NE; ++e) red[e][lane] = acc[e];
+    for (int e = 0; e < NE; ++e) {
+        double v = acc[e];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) wsum[wv][e] = v;
+    }
     __syncthreads();
     double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
-    for (int e = lane; e < NE; e += 64) {
-        double v = 0.;
-        for (int l = 0; l < 64; ++l) v += red[e][l];
+    for (int e = tid; e < NE; e += 64 * NW) {
+        double v = wsum[0][e];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v += wsum[w][e];
         if (e < NCC) {
             int a = 0, rem = e;
             while (rem >= PC - a) {
@@ -815,18 +825,26 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
     }
 }
 
-__global__ void k_ne_glob_reduce(DevProblem P, const double *__restrict__ partial, int nblk,
-                                 double *Agg, double *gG) {
+// Sum of the per-block partial rows: one wave per entry (entries dealt to
+// the 4 waves), lanes stride over the blocks, fixed xor-shuffle tree.
+__global__ void __launch_bounds__(256) k_ne_glob_reduce(DevProblem P,
+                                                        const double *__restrict__ partial,
+                                                        int nblk, double *Agg, double *gG) {
     const int nG = P.nG;
-    for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int t = wave; t < NGMAX * NGMAX + NGMAX; t += 4) {
         const bool mat = t < NGMAX * NGMAX;
         if (mat ? ((t / NGMAX) >= nG || (t % NGMAX) >= nG) : (t - NGMAX * NGMAX) >= nG) continue;
         double s = 0.;
-        for (int k = 0; k < nblk; ++k) s += partial[(size_t)k * (NGMAX * NGMAX + NGMAX) + t];
-        if (mat)
-            Agg[t] = s;
-        else
-            gG[t - NGMAX * NGMAX] = s;
+        for (int k = lane; k < nblk; k += 64) s += partial[(size_t)k * (NGMAX * NGMAX + NGMAX) + t];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        if (lane == 0) {
+            if (mat)
+                Agg[t] = s;
+            else
+                gG[t - NGMAX * NGMAX] = s;
+        }
     }
 }
 
@@ -1997,10 +2015,18 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
                double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk) {
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
     if (P.ncf > 0) {
-        if (P.nG == 0 && P.pc_uniform == 6)
-            k_ne_cf_u<6><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
-        else if (P.nG == 0 && P.pc_uniform == 7)
-            k_ne_cf_u<7><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
+        const bool wide = P.M > 256 * P.ncf;  // long camera-frame segments: 4 waves
+        if (P.nG == 0 && P.pc_uniform == 6) {
+            if (wide)
+                k_ne_cf_u<6, 4><<<P.ncf, 256, 0, s>>>(P, J, f, Acc, g);
+            else
+                k_ne_cf_u<6, 1><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
+        } else if (P.nG == 0 && P.pc_uniform == 7) {
+            if (wide)
+                k_ne_cf_u<7, 4><<<P.ncf, 256, 0, s>>>(P, J, f, Acc, g);
+            else
+                k_ne_cf_u<7, 1><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
+        }
         else
             k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
     }

@@ -668,7 +668,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         D.JB = all_fast ? dalloc<double>((size_t)8 * M) : nullptr;
         // uniform fast Jacobian kernel: fast bundles, no lens, no bundle-side
         // camera variants, at most pc_uniform (6 or 7) variants per camera-frame
-        bool fast = all_fast && (pc_uniform == 6 || pc_uniform == 7);
+        bool fast = nG == 0 && (pc_uniform == 6 || pc_uniform == 7);
+        for (int b = 0; b < nB && fast; ++b)
+            if (bnd_pb[b] > 0 && bnd_p4[b].w < 0) fast = false;
         for (int c = 0; c < nC && fast; ++c)
             if (pr->cam_lens && pr->cam_lens[c] >= 0) fast = false;
         for (size_t t = 0; t < cf_var_flags.size() && fast; ++t)
