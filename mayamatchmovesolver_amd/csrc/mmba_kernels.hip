@@ -2015,7 +2015,7 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
                double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk) {
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
     if (P.ncf > 0) {
-        const bool wide = P.M > 256 * P.ncf;  // long camera-frame segments: 4 waves
+        const bool wide = P.M > 1024 * P.ncf;  // long camera-frame segments (C2): 4 waves
         if (P.nG == 0 && P.pc_uniform == 6) {
             if (wide)
                 k_ne_cf_u<6, 4><<<P.ncf, 256, 0, s>>>(P, J, f, Acc, g);
