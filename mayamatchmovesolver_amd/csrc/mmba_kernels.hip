@@ -612,24 +612,29 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
 // lane o accumulates the upper triangle of Acc and gC over the observations
 // o, o + 64, ... of the (contiguous) segment in registers; the 64 partial
 // sums are added through LDS in a fixed order.
-template <int PC, int NW>
+template <int PC, int NW, int NG>
 __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
+                                                     const int *__restrict__ jcol,
+                                                     const int *__restrict__ nloc,
                                                      const double *__restrict__ f, double *Acc,
-                                                     double *g) {
+                                                     double *Acg, double *g) {
     // NW waves per camera-frame (long segments: C2 has ~1,700 observations
     // per camera-frame): thread t takes observations t, t + 64 NW, ...;
     // each wave folds its partial sums with a fixed xor-shuffle tree, the NW
-    // wave sums are added in wave order (deterministic)
-    constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC;
-    __shared__ double wsum[NW][NE];
+    // wave sums are added in wave order (deterministic).  NG > 0: the
+    // couplings Acg with up to NG global parameters (lens), whose columns
+    // follow the camera block in each observation (found through jcol).
+    constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC, NT = NE + PC * NG;
+    __shared__ double wsum[NW][NT];
     const int cf = blockIdx.x;
     if (!own_cf(P, cf) || P.cf_pc[cf] != PC) return;
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const size_t M = P.M;
+    const int nCF = P.nR - P.nG;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    double acc[NE];
+    double acc[NT];
 #pragma unroll
-    for (int e = 0; e < NE; ++e) acc[e] = 0.;
+    for (int e = 0; e < NT; ++e) acc[e] = 0.;
     for (int i = o0 + tid; i < o1; i += 64 * NW) {
         double jx[PC], jy[PC];
 #pragma unroll
@@ -645,9 +650,31 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
             for (int c = a; c < PC; ++c) acc[e++] += jx[a] * jx[c] + jy[a] * jy[c];
 #pragma unroll
         for (int a = 0; a < PC; ++a) acc[NCC + a] += jx[a] * fx + jy[a] * fy;
+        if constexpr (NG > 0) {
+            double gx[NG], gy[NG];
+#pragma unroll
+            for (int q = 0; q < NG; ++q) gx[q] = gy[q] = 0.;
+            const int nl = nloc[i];
+            for (int l = PC; l < nl; ++l) {
+                const int p = jcol[(size_t)l * M + i];
+                if (P.p_class[p] != PC_G) continue;
+                const int gi = P.p_pos[p] - nCF;
+                const double ux = J[(size_t)(2 * l) * M + i], uy = J[(size_t)(2 * l + 1) * M + i];
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    gx[q] = (gi == q) ? ux : gx[q];
+                    gy[q] = (gi == q) ? uy : gy[q];
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < PC; ++a)
+#pragma unroll
+                for (int q = 0; q < NG; ++q)
+                    acc[NE + a * NG + q] += jx[a] * gx[q] + jy[a] * gy[q];
+        }
     }
 #pragma unroll
-    for (int e = 0; e < NE; ++e) {
+    for (int e = 0; e < NT; ++e) {
         double v = acc[e];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -655,7 +682,7 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
     }
     __syncthreads();
     double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
-    for (int e = tid; e < NE; e += 64 * NW) {
+    for (int e = tid; e < NT; e += 64 * NW) {
         double v = wsum[0][e];
 #pragma unroll
         for (int w = 1; w < NW; ++w) v += wsum[w][e];
@@ -668,8 +695,11 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
             const int c = a + rem;
             A[a * PCMAX + c] = v;
             A[c * PCMAX + a] = v;
-        } else {
+        } else if (e < NE) {
             g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
+        } else {
+            const int a = (e - NE) / NG, q = (e - NE) % NG;
+            if (q < P.nG) Acg[((size_t)cf * PCMAX + a) * NGMAX + q] = v;
         }
     }
 }
@@ -2016,19 +2046,27 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
     if (P.ncf > 0) {
         const bool wide = P.M > 1024 * P.ncf;  // long camera-frame segments (C2): 4 waves
-        if (P.nG == 0 && P.pc_uniform == 6) {
-            if (wide)
-                k_ne_cf_u<6, 4><<<P.ncf, 256, 0, s>>>(P, J, f, Acc, g);
-            else
-                k_ne_cf_u<6, 1><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
-        } else if (P.nG == 0 && P.pc_uniform == 7) {
-            if (wide)
-                k_ne_cf_u<7, 4><<<P.ncf, 256, 0, s>>>(P, J, f, Acc, g);
-            else
-                k_ne_cf_u<7, 1><<<P.ncf, 64, 0, s>>>(P, J, f, Acc, g);
-        }
-        else
+#define MMBA_NE_U(PC, NW, NG)                                                              \
+    k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g)
+        const int pcu = P.pc_uniform;
+        if ((pcu == 6 || pcu == 7) && (P.nG == 0 || P.nG <= 2)) {
+            if (P.nG == 0) {
+                if (pcu == 6) {
+                    if (wide) MMBA_NE_U(6, 4, 0); else MMBA_NE_U(6, 1, 0);
+                } else {
+                    if (wide) MMBA_NE_U(7, 4, 0); else MMBA_NE_U(7, 1, 0);
+                }
+            } else {
+                if (pcu == 6) {
+                    if (wide) MMBA_NE_U(6, 4, 2); else MMBA_NE_U(6, 1, 2);
+                } else {
+                    if (wide) MMBA_NE_U(7, 4, 2); else MMBA_NE_U(7, 1, 2);
+                }
+            }
+        } else {
             k_ne_cf<<<P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g);
+        }
+#undef MMBA_NE_U
     }
     if (P.nB > 0) {
         if (P.JB)  // every solved bundle fast and no global parameters
