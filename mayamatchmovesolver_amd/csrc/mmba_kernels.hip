@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
 // chains overlap (the generic loop serialises them behind its dependent
 // variant-table loads).  Emits columns in the generic kernel's order.
 template <int NCV, bool GEN>  // GEN: some bundle needs the transform-chain path
-__global__ void __launch_bounds__(128, 4) k_jacobian_u(
+__global__ void __launch_bounds__(128) k_jacobian_u(
     DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
     int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
     const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed) {
