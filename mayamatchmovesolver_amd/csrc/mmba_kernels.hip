@@ -263,10 +263,26 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
                 const int M = P.M;
                 double ax = 0., ay = 0.;
                 const int nl = nloc[i];
-                for (int l = 0; l < nl; ++l) {
-                    const double pv = pstep[jcol[(size_t)l * M + i]];
-                    ax += J[(size_t)(2 * l) * M + i] * pv;
-                    ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+                if (P.jcol_implicit) {
+                    // uniform plans: column l is camera variant l (l < nv), then
+                    // the bundle's parameters (k_jacobian_u's order)
+                    const int voff = P.cf_var_off[cf];
+                    const int nv = P.cf_var_off[cf + 1] - voff - 1;
+                    const int4 p4 = P.bnd_p4[b];
+                    for (int l = 0; l < nl; ++l) {
+                        const int a = l - nv;
+                        const int p = l < nv ? P.cf_var_param[voff + 1 + l]
+                                             : (a == 0 ? p4.x : (a == 1 ? p4.y : p4.z));
+                        const double pv = pstep[p];
+                        ax += J[(size_t)(2 * l) * M + i] * pv;
+                        ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+                    }
+                } else {
+                    for (int l = 0; l < nl; ++l) {
+                        const double pv = pstep[jcol[(size_t)l * M + i]];
+                        ax += J[(size_t)(2 * l) * M + i] * pv;
+                        ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+                    }
                 }
                 sj = ax * ax + ay * ay;
             }
@@ -458,6 +474,8 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr);
     int l = 0;
     double rsx = r0.ux, rsy = r0.uy, rsd = r0.dist;  // errorList of the stale column
+    bool hit = false;
+    const bool wcol = !P.jcol_implicit;
     double jb[8] = {0., 0., 0., 0., 0., 0., r0.ex, r0.ey};
     auto emit = [&](int p, const Resid &r, double s) {
         double jx, jy;
@@ -470,11 +488,12 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
         }
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
-        jcol[(size_t)l * M + i] = p;
+        if (wcol) jcol[(size_t)l * M + i] = p;
         if (p == pstale) {
             rsx = r.ux;
             rsy = r.uy;
             rsd = r.dist;
+            hit = true;
         }
         ++l;
         return make_double2(jx, jy);
@@ -505,7 +524,10 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
         dst[1] = make_double4(jb[4], jb[5], jb[6], jb[7]);
     }
     nloc[i] = l;
-    if (eu) {
+    // errorList / errorDistanceList as left by the last FD column: only the
+    // observations that column moves change; the others keep their values at
+    // x (what d_eu / d_ed already hold from the evaluation that accepted x)
+    if (eu && (hit || !P.jcol_implicit)) {
         eu[2 * i] = rsx;
         eu[2 * i + 1] = rsy;
         ed[i] = rsd;

@@ -471,7 +471,10 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
     MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
     MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
     fun(d_x, d_f, d_eu, d_ed);
+    const int implicit = P.jcol_implicit;
+    P.jcol_implicit = 0;  // this host-side reassembly reads jcol
     jac(d_x);
+    P.jcol_implicit = implicit;
     std::vector<double> J((size_t)2 * LMAX * M);
     std::vector<int> jc((size_t)LMAX * M), nl(M);
     MMBA_HIP(hipMemcpyAsync(J.data(), d_J, sizeof(double) * J.size(), hipMemcpyDeviceToHost, s));

@@ -680,6 +680,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         jac_ncv = fast ? pc_uniform : 0;
         if (const char *e = std::getenv("MMBA_JAC_GENERIC"))
             if (std::atoi(e)) jac_ncv = 0;
+        D.jcol_implicit = jac_ncv > 0 ? 1 : 0;
+        if (const char *e = std::getenv("MMBA_JCOL"))
+            if (std::atoi(e)) D.jcol_implicit = 0;
     }
     d_brec = dalloc<double>((size_t)nB * BREC);
     D.brec = d_brec;
