@@ -63,9 +63,26 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *f = nullptr);  // residuals at x (column-parallel kernel)
 // aggbuf = [Agg (NGMAX^2) | g_G (NGMAX)]: the global-parameter normal
 // equations, all-reduced across shards before launch_colnorms.
+// lmder's bookkeeping after the normal equations (k_jac_epilogue's column
+// norms, rank test, diag update, ||D x||, gnorm) fused into the uniform
+// normal-equation kernels: each camera-frame / bundle block writes one
+// partial per quantity at column cf_base + cf / bnd_base + block of the rows
+// partial[0 | rstride | 2 rstride] (max, sum, max).
+struct NeEpi {
+    int on = 0;
+    int first = 0, mode = 1, do_xn = 0, do_gn = 0;
+    double fnorm = 0.;
+    const double *x = nullptr;
+    double *diag = nullptr, *acnorm = nullptr, *partial = nullptr;
+    int rstride = 0, cf_base = 0, bnd_base = 0;
+};
+// Whether launch_ne can fuse the bookkeeping (uniform camera blocks, fast
+// bundles, no global parameters).
+bool ne_epilogue_fusable(const DevProblem &P);
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
-               double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk);
+               double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk,
+               const NeEpi &epi = NeEpi());
 void launch_colnorms(hipStream_t s, const DevProblem &P, const double *Acc, const double *Abb,
                      const double *aggbuf, double *acnorm, double *g);
 void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,

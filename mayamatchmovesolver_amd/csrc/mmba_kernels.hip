@@ -634,12 +634,40 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
 // lane o accumulates the upper triangle of Acc and gC over the observations
 // o, o + 64, ... of the (contiguous) segment in registers; the 64 partial
 // sums are added through LDS in a fixed order.
+// One parameter's share of the lmder bookkeeping (k_jac_epilogue, same
+// operations): acnorm, diag update, and its contributions to the rank flag,
+// ||D x||^2 and gnorm.
+__device__ __forceinline__ void epi_param(const NeEpi &E, int p, double d, double gp, double &zf,
+                                          double &xn, double &gm) {
+    const double an = sqrt(d);
+    E.acnorm[p] = an;
+    double dg = E.diag[p];
+    if (E.mode != 2) {
+        if (E.first) dg = an == 0. ? 1. : an;
+        dg = fmax(dg, an);
+        E.diag[p] = dg;
+    }
+    if (an == 0.) zf = 1.;
+    if (E.do_xn) {
+        const double v = dg * E.x[p];
+        xn += v * v;
+    }
+    if (E.do_gn && an != 0.) gm = fmax(gm, fabs((gp / E.fnorm) / an));
+}
+
+__device__ __forceinline__ void epi_store(const NeEpi &E, int col, double zf, double xn,
+                                          double gm) {
+    E.partial[col] = zf;
+    E.partial[E.rstride + col] = xn;
+    E.partial[2 * E.rstride + col] = gm;
+}
+
 template <int PC, int NW, int NG>
 __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
                                                      const int *__restrict__ jcol,
                                                      const int *__restrict__ nloc,
                                                      const double *__restrict__ f, double *Acc,
-                                                     double *Acg, double *g) {
+                                                     double *Acg, double *g, NeEpi E) {
     // NW waves per camera-frame (long segments: C2 has ~1,700 observations
     // per camera-frame): thread t takes observations t, t + 64 NW, ...;
     // each wave folds its partial sums with a fixed xor-shuffle tree, the NW
@@ -649,7 +677,10 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
     constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC, NT = NE + PC * NG;
     __shared__ double wsum[NW][NT];
     const int cf = blockIdx.x;
-    if (!own_cf(P, cf) || P.cf_pc[cf] != PC) return;
+    if (!own_cf(P, cf) || P.cf_pc[cf] != PC) {
+        if (E.on && threadIdx.x == 0) epi_store(E, E.cf_base + cf, 0., 0., 0.);
+        return;
+    }
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const size_t M = P.M;
     const int nCF = P.nR - P.nG;
@@ -724,38 +755,76 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
             if (q < P.nG) Acg[((size_t)cf * PCMAX + a) * NGMAX + q] = v;
         }
     }
+    if (E.on && tid == 0) {
+        // the block's parameters (sums re-formed in the same order as above)
+        double zf = 0., xn = 0., gm = 0.;
+        const int v0 = P.cf_var_off[cf] + 1;
+        for (int a = 0; a < PC; ++a) {
+            const int ed = a * PC - a * (a - 1) / 2;  // upper-triangle index of (a, a)
+            double d = wsum[0][ed], gp = wsum[0][NCC + a];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) {
+                d += wsum[w][ed];
+                gp += wsum[w][NCC + a];
+            }
+            epi_param(E, P.cf_var_param[v0 + a], d, gp, zf, xn, gm);
+        }
+        epi_store(E, E.cf_base + cf, zf, xn, gm);
+    }
 }
 
 // Fast bundles, no global parameters: Abb and gB from the per-observation
 // block records, same summation order as k_ne_bnd.
-__global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, double *g) {
+__global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, double *g,
+                                                   NeEpi E) {
+    __shared__ double red[3][256];
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= P.nB) return;
-    const int4 p4 = P.bnd_p4[b];
+    const int4 p4 = b < P.nB ? P.bnd_p4[b] : make_int4(-1, -1, -1, 0);
     const int pb = p4.w;
-    if (pb <= 0) return;
-    double A[PBMAX][PBMAX] = {};
-    double gb[PBMAX] = {};
-    for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-        const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)P.bobs[q] * 8]);
-        const double4 u = src[0], v = src[1];
-        const double jx[3] = {u.x, u.z, v.x}, jy[3] = {u.y, u.w, v.y};
-        const double fx = v.z, fy = v.w;
+    double zf = 0., xn = 0., gm = 0.;
+    if (pb > 0) {
+        double A[PBMAX][PBMAX] = {};
+        double gb[PBMAX] = {};
+        for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
+            const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)P.bobs[q] * 8]);
+            const double4 u = src[0], v = src[1];
+            const double jx[3] = {u.x, u.z, v.x}, jy[3] = {u.y, u.w, v.y};
+            const double fx = v.z, fy = v.w;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
+            for (int a = 0; a < 3; ++a) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) A[a][c] += jx[a] * jx[c] + jy[a] * jy[c];
-            gb[a] += jx[a] * fx + jy[a] * fy;
+                for (int c = 0; c < 3; ++c) A[a][c] += jx[a] * jx[c] + jy[a] * jy[c];
+                gb[a] += jx[a] * fx + jy[a] * fy;
+            }
+        }
+        double *Ab = &Abb[(size_t)b * 9];
+#pragma unroll
+        for (int a = 0; a < PBMAX; ++a)
+#pragma unroll
+            for (int c = 0; c < PBMAX; ++c) Ab[a * 3 + c] = (a < pb && c < pb) ? A[a][c] : 0.;
+        g[p4.x] = gb[0];
+        if (pb > 1) g[p4.y] = gb[1];
+        if (pb > 2) g[p4.z] = gb[2];
+        if (E.on) {
+            epi_param(E, p4.x, A[0][0], gb[0], zf, xn, gm);
+            if (pb > 1) epi_param(E, p4.y, A[1][1], gb[1], zf, xn, gm);
+            if (pb > 2) epi_param(E, p4.z, A[2][2], gb[2], zf, xn, gm);
         }
     }
-    double *Ab = &Abb[(size_t)b * 9];
-#pragma unroll
-    for (int a = 0; a < PBMAX; ++a)
-#pragma unroll
-        for (int c = 0; c < PBMAX; ++c) Ab[a * 3 + c] = (a < pb && c < pb) ? A[a][c] : 0.;
-    g[p4.x] = gb[0];
-    if (pb > 1) g[p4.y] = gb[1];
-    if (pb > 2) g[p4.z] = gb[2];
+    if (!E.on) return;
+    red[0][threadIdx.x] = zf;
+    red[1][threadIdx.x] = xn;
+    red[2][threadIdx.x] = gm;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            red[0][threadIdx.x] = fmax(red[0][threadIdx.x], red[0][threadIdx.x + w]);
+            red[1][threadIdx.x] += red[1][threadIdx.x + w];
+            red[2][threadIdx.x] = fmax(red[2][threadIdx.x], red[2][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) epi_store(E, E.bnd_base + blockIdx.x, red[0][0], red[1][0], red[2][0]);
 }
 
 // Per bundle: Abb (pb x pb), gB, Abg (pb x nG).  One thread per bundle.
@@ -2062,14 +2131,19 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
     k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
                                                 nloc, stale_param, eu, ed);
 }
+bool ne_epilogue_fusable(const DevProblem &P) {
+    return P.nG == 0 && P.JB && (P.pc_uniform == 6 || P.pc_uniform == 7) && !P.obs_own;
+}
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
-               double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk) {
+               double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk,
+               const NeEpi &epi) {
+    const NeEpi E = ne_epilogue_fusable(P) ? epi : NeEpi();
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
     if (P.ncf > 0) {
         const bool wide = P.M > 1024 * P.ncf;  // long camera-frame segments (C2): 4 waves
 #define MMBA_NE_U(PC, NW, NG)                                                              \
-    k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g)
+    k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E)
         const int pcu = P.pc_uniform;
         if ((pcu == 6 || pcu == 7) && (P.nG == 0 || P.nG <= 2)) {
             if (P.nG == 0) {
@@ -2092,7 +2166,7 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
     }
     if (P.nB > 0) {
         if (P.JB)  // every solved bundle fast and no global parameters
-            k_ne_bnd_jb<<<nblk(P.nB, 256), 256, 0, s>>>(P, Abb, g);
+            k_ne_bnd_jb<<<nblk(P.nB, 256), 256, 0, s>>>(P, Abb, g, E);
         else
             k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
     }

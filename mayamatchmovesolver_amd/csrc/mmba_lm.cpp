@@ -153,10 +153,38 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                     d_stale, d_eu, d_ed, jac_ncv, d_f);
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
+    // uniform unsharded plans: the lmder bookkeeping rides in the
+    // normal-equation kernels (no k_jac_epilogue launch)
+    const bool fuse = lm && ne_epilogue_fusable(P);
+    NeEpi epi;
+    if (fuse) {
+        epi.on = 1;
+        epi.first = lm->first;
+        epi.mode = lm->mode;
+        epi.fnorm = lm->fnorm;
+        epi.do_xn = lm->first;
+        epi.do_gn = lm->fnorm != 0.;
+        epi.x = dx;
+        epi.diag = d_diag;
+        epi.acnorm = d_acnorm;
+        epi.partial = d_partial;
+        epi.rstride = pw;
+        epi.cf_base = 0;
+        epi.bnd_base = ncf;
+    }
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
-              d_glob_partial, glob_chunk);
+              d_glob_partial, glob_chunk, epi);
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
-    if (!lm) {
+    if (fuse) {
+        span_end(SPAN_JAC);
+        const int ncol = ncf + (nB + 255) / 256;
+        RedSpec rs{};
+        rs.flag_slot = -1;
+        rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
+        if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, SL_XN2};
+        if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
+        launch_reduce_multi(s, d_partial, rs, d_scalar);
+    } else if (!lm) {
         launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
         span_end(SPAN_JAC);
     } else {

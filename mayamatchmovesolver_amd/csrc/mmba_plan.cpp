@@ -810,7 +810,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_xR = dalloc<double>(nRpad);
     d_wR = dalloc<double>(nRpad);
     d_usq = dalloc<double>(nB);
-    pw = std::max(nparts, residual_blocks(P));
+    pw = std::max(std::max(nparts, residual_blocks(P)), ncf + (nB + 255) / 256);
     d_partial = dalloc<double>((size_t)8 * pw);
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
