@@ -264,6 +264,17 @@ MMBA_DEV void projection_matrix(int mode, double focal_mm, double fbw_inch,
 // normalised forward direction (3), marker film-fit factors (2).
 MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &ov,
                             double *rec) {
+    // MMBA_REC_PROBE=1 (diagnostic): thread 0 of block 0 accumulates the
+    // cycles of each phase; never read by the solver
+    const bool prb = P.rec_probe && blockIdx.x == 0 && threadIdx.x == 0;
+    long long tp = prb ? (long long)clock64() : 0;
+    auto stamp = [&](int k) {
+        if (prb) {
+            const long long tn = (long long)clock64();
+            atomicAdd((unsigned long long *)&P.rec_probe[k], (unsigned long long)(tn - tp));
+            tp = tn;
+        }
+    };
     const int *ca = &P.cam_attrs[MMBA_CAM_NUM_ATTRS * c];
     double w = attr_get(P, ca[MMBA_CAM_FILM_BACK_W_INCH], f, 36.0 / 25.4, ov);
     double h = attr_get(P, ca[MMBA_CAM_FILM_BACK_H_INCH], f, 24.0 / 25.4, ov);
@@ -292,10 +303,13 @@ MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &o
     double Pm[16];
     const int fit = P.cam_fit[c];
     projection_matrix(P.mode, focal, fbw, fbh, offx, offy, iw, ih, fit, far_clip, cscale, Pm);
+    stamp(0);
     double ra = iw / ih;
     double W[16], Ci[16], PV[16];
     world_matrix(P, P.cam_tfm[c], f, ov, W);
+    stamp(1);
     mat4_inverse(W, Ci);
+    stamp(2);
     mat4_mul(Pm, Ci, PV);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -326,6 +340,7 @@ MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &o
     }
     rec[18] = sx;
     rec[19] = sy;
+    stamp(3);
 }
 
 // ---- LDPK classic 3DE model (undistort polynomial + fixed-point inverse) ----

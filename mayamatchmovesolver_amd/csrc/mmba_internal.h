@@ -157,6 +157,7 @@ struct DevProblem {
     int all_bnd_fast;  // every bundle is fast (bnd_p4[b].w >= 0)
     int lmax;          // most local Jacobian columns of any observation (<= LMAX)
     int jcol_implicit; // uniform fast plans: jcol not stored (derived from the structure)
+    long long *rec_probe;  // MMBA_REC_PROBE=1: camera-record phase cycles (diagnostic)
     int no_lens;       // no camera has a (3DE classic) lens
     // position of each observation in bundle order (bobs) and the bundle
     // block records JB[8 * i] = [jx_a, jy_a] (a < 3), f_x, f_y written by

@@ -40,6 +40,14 @@ Plan::~Plan() {
                          "update %lld tail %lld (nb=%d w=%d nG=%d P=%d)\n",
                          h[0], h[1], h[2], h[3], nR - nG, bw, nG, bs.P);
     }
+    if (P.rec_probe) {
+        long long h[4] = {0, 0, 0, 0};
+        if (hipMemcpy(h, P.rec_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+            std::fprintf(stderr,
+                         "[mmba probe] camera record cycles (thread 0, all calls): attrs+projection "
+                         "%lld world %lld inverse %lld rest %lld\n",
+                         h[0], h[1], h[2], h[3]);
+    }
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (ev_sync) (void)hipEventDestroy(ev_sync);
     for (void *p : allocs) (void)hipFree(p);
@@ -652,6 +660,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_pb = upload(bnd_pb);
     D.bnd_xoff = nullptr;
     D.bnd_p4 = upload(bnd_p4);
+    D.rec_probe = nullptr;
+    if (std::getenv("MMBA_REC_PROBE")) {
+        D.rec_probe = dalloc<long long>(4);
+        MMBA_HIP(hipMemsetAsync(D.rec_probe, 0, 4 * sizeof(long long), s));
+    }
     D.all_bnd_fast = 1;
     for (int b = 0; b < nB; ++b)
         if (bnd_p4[b].w < 0) D.all_bnd_fast = 0;
