@@ -260,26 +260,12 @@ MMBA_DEV void projection_matrix(int mode, double focal_mm, double fbw_inch,
     }
 }
 
-// Camera-frame record: rows 0,1,3 of P*C^-1 (12), camera position (3),
-// normalised forward direction (3), marker film-fit factors (2).
-MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &ov,
-                            double *rec) {
-    // MMBA_REC_PROBE=1 (diagnostic): thread 0 of block 0 accumulates the
-    // cycles of each phase; never read by the solver
-    const bool prb = P.rec_probe && blockIdx.x == 0 && threadIdx.x == 0;
-    long long tp = prb ? (long long)clock64() : 0;
-    auto stamp = [&](int k) {
-        if (prb) {
-            const long long tn = (long long)clock64();
-            atomicAdd((unsigned long long *)&P.rec_probe[k], (unsigned long long)(tn - tp));
-            tp = tn;
-        }
-    };
-    const int *ca = &P.cam_attrs[MMBA_CAM_NUM_ATTRS * c];
-    double w = attr_get(P, ca[MMBA_CAM_FILM_BACK_W_INCH], f, 36.0 / 25.4, ov);
-    double h = attr_get(P, ca[MMBA_CAM_FILM_BACK_H_INCH], f, 24.0 / 25.4, ov);
-    double ox = attr_get(P, ca[MMBA_CAM_FILM_OFFSET_X_INCH], f, 0., ov);
-    double oy = attr_get(P, ca[MMBA_CAM_FILM_OFFSET_Y_INCH], f, 0., ov);
+// Camera-frame record from the camera's attribute values (cv: film back w/h,
+// film offset x/y in inches, focal mm, far clip, camera scale) and its world
+// matrix W.
+MMBA_DEV void camera_record_tail(const DevProblem &P, int c, double w, double h, double ox,
+                                 double oy, double focal, double far_clip, double cscale,
+                                 const double *W, double *rec) {
     double fbw, fbh, offx, offy, fa;
     if (P.mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
         double w_mm = w * 25.4, h_mm = h * 25.4;
@@ -295,21 +281,14 @@ MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &o
         offy = oy;
         fa = w / h;
     }
-    double focal = attr_get(P, ca[MMBA_CAM_FOCAL_MM], f, 35.0, ov);
-    double far_clip = attr_get(P, ca[MMBA_CAM_FAR_CLIP], f, 10000.0, ov);
-    double cscale = attr_get(P, ca[MMBA_CAM_SCALE], f, 1.0, ov);
     double iw = (double)P.cam_size[2 * c];
     double ih = (double)P.cam_size[2 * c + 1];
     double Pm[16];
     const int fit = P.cam_fit[c];
     projection_matrix(P.mode, focal, fbw, fbh, offx, offy, iw, ih, fit, far_clip, cscale, Pm);
-    stamp(0);
     double ra = iw / ih;
-    double W[16], Ci[16], PV[16];
-    world_matrix(P, P.cam_tfm[c], f, ov, W);
-    stamp(1);
+    double Ci[16], PV[16];
     mat4_inverse(W, Ci);
-    stamp(2);
     mat4_mul(Pm, Ci, PV);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -340,7 +319,46 @@ MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &o
     }
     rec[18] = sx;
     rec[19] = sy;
-    stamp(3);
+}
+
+// Camera-frame record: rows 0,1,3 of P*C^-1 (12), camera position (3),
+// normalised forward direction (3), marker film-fit factors (2).
+MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &ov,
+                            double *rec) {
+    const int *ca = &P.cam_attrs[MMBA_CAM_NUM_ATTRS * c];
+    const double w = attr_get(P, ca[MMBA_CAM_FILM_BACK_W_INCH], f, 36.0 / 25.4, ov);
+    const double h = attr_get(P, ca[MMBA_CAM_FILM_BACK_H_INCH], f, 24.0 / 25.4, ov);
+    const double ox = attr_get(P, ca[MMBA_CAM_FILM_OFFSET_X_INCH], f, 0., ov);
+    const double oy = attr_get(P, ca[MMBA_CAM_FILM_OFFSET_Y_INCH], f, 0., ov);
+    const double focal = attr_get(P, ca[MMBA_CAM_FOCAL_MM], f, 35.0, ov);
+    const double far_clip = attr_get(P, ca[MMBA_CAM_FAR_CLIP], f, 10000.0, ov);
+    const double cscale = attr_get(P, ca[MMBA_CAM_SCALE], f, 1.0, ov);
+    double W[16];
+    world_matrix(P, P.cam_tfm[c], f, ov, W);
+    camera_record_tail(P, c, w, h, ox, oy, focal, far_clip, cscale, W, rec);
+}
+
+// Same record for a camera transform without parent, gathered through the
+// plan's per-camera-frame table of attribute-value indices
+// (P.cf_aidx[17 cf + k]: 7 camera attributes, then tx ty tz rx ry rz sx sy sz;
+// -1 = default): one dependent load level instead of the attribute-table walk.
+// ov_idx is the perturbed attribute's value index (-1: none).
+MMBA_DEV void camera_record_fast(const DevProblem &P, int cf, long long ov_idx, double ov_val,
+                                 double *rec) {
+    const int *ix = &P.cf_aidx[(size_t)CF_AIDX * cf];
+    const double dflt[CF_AIDX] = {36.0 / 25.4, 24.0 / 25.4, 0., 0., 35.0, 10000.0, 1.0,
+                                  0., 0., 0., 0., 0., 0., 1., 1., 1.};
+    double v[CF_AIDX];
+#pragma unroll
+    for (int k = 0; k < CF_AIDX; ++k) {
+        const int a = ix[k];
+        v[k] = a < 0 ? dflt[k] : (a == ov_idx ? ov_val : P.attr_val[a]);
+    }
+    const int c = P.cf_cam[cf];
+    double W[16];
+    trs_matrix(v[7], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15],
+               P.tfm_roo[P.cam_tfm[c]], W);
+    camera_record_tail(P, c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], W, rec);
 }
 
 // ---- LDPK classic 3DE model (undistort polynomial + fixed-point inverse) ----

@@ -26,7 +26,8 @@ namespace mmba {
 constexpr int PCMAX = 10;   // params per camera-frame block
 constexpr int PBMAX = 3;    // params per bundle block
 constexpr int NGMAX = 16;   // global parameters
-constexpr int LMAX = 20;    // local Jacobian columns per observation
+constexpr int LMAX = 20;
+constexpr int CF_AIDX = 16;  // camera-frame attribute table: 7 camera + 9 TRS    // local Jacobian columns per observation
 constexpr int TILE = 64;    // reduced-system tile edge
 constexpr int CAMREC = 20;  // doubles per camera-frame record
 constexpr int BREC = 16;    // doubles per bundle record (128 B: one L2 line)
@@ -157,7 +158,9 @@ struct DevProblem {
     int all_bnd_fast;  // every bundle is fast (bnd_p4[b].w >= 0)
     int lmax;          // most local Jacobian columns of any observation (<= LMAX)
     int jcol_implicit; // uniform fast plans: jcol not stored (derived from the structure)
-    long long *rec_probe;  // MMBA_REC_PROBE=1: camera-record phase cycles (diagnostic)
+    // camera records through a per-camera-frame table of attribute-value
+    // indices (every camera transform without a parent; nullptr otherwise)
+    const int *cf_aidx;
     int no_lens;       // no camera has a (3DE classic) lens
     // position of each observation in bundle order (bobs) and the bundle
     // block records JB[8 * i] = [jx_a, jy_a] (a < 3), f_x, f_y written by

@@ -140,6 +140,15 @@ __device__ __forceinline__ void cam_record_thread(const DevProblem &P, int t,
         ov.attr = P.p_attr[p];
         ov.value = ext_pert[p];
     }
+    if (P.cf_aidx) {
+        long long ov_idx = -1;
+        if (p >= 0) {
+            const int f = P.cf_frame[cf];
+            ov_idx = P.attr_off[ov.attr] + (P.attr_anim[ov.attr] ? (f < 0 ? 0 : f) : 0);
+        }
+        camera_record_fast(P, cf, ov_idx, ov.value, &recs[(size_t)idx * CAMREC]);
+        return;
+    }
     camera_record(P, P.cf_cam[cf], P.cf_frame[cf], ov, &recs[(size_t)idx * CAMREC]);
 }
 

@@ -40,14 +40,6 @@ Plan::~Plan() {
                          "update %lld tail %lld (nb=%d w=%d nG=%d P=%d)\n",
                          h[0], h[1], h[2], h[3], nR - nG, bw, nG, bs.P);
     }
-    if (P.rec_probe) {
-        long long h[4] = {0, 0, 0, 0};
-        if (hipMemcpy(h, P.rec_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
-            std::fprintf(stderr,
-                         "[mmba probe] camera record cycles (thread 0, all calls): attrs+projection "
-                         "%lld world %lld inverse %lld rest %lld\n",
-                         h[0], h[1], h[2], h[3]);
-    }
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (ev_sync) (void)hipEventDestroy(ev_sync);
     for (void *p : allocs) (void)hipFree(p);
@@ -660,10 +652,37 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_pb = upload(bnd_pb);
     D.bnd_xoff = nullptr;
     D.bnd_p4 = upload(bnd_p4);
-    D.rec_probe = nullptr;
-    if (std::getenv("MMBA_REC_PROBE")) {
-        D.rec_probe = dalloc<long long>(4);
-        MMBA_HIP(hipMemsetAsync(D.rec_probe, 0, 4 * sizeof(long long), s));
+    {
+        // per-camera-frame attribute-value indices for the camera records
+        // (cameras whose transform has no parent; MMBA_CAM_TABLE=0 disables)
+        bool ok = true;
+        for (int c = 0; c < nC && ok; ++c)
+            if (pr->tfm_parent[pr->cam_tfm[c]] >= 0) ok = false;
+        if (const char *e = std::getenv("MMBA_CAM_TABLE"))
+            if (std::atoi(e) == 0) ok = false;
+        D.cf_aidx = nullptr;
+        if (ok && ncf > 0) {
+            static const int cam_k[7] = {MMBA_CAM_FILM_BACK_W_INCH, MMBA_CAM_FILM_BACK_H_INCH,
+                                         MMBA_CAM_FILM_OFFSET_X_INCH, MMBA_CAM_FILM_OFFSET_Y_INCH,
+                                         MMBA_CAM_FOCAL_MM, MMBA_CAM_FAR_CLIP, MMBA_CAM_SCALE};
+            std::vector<int> tab((size_t)CF_AIDX * ncf, -1);
+            auto vidx = [&](int a, int f) -> int {
+                if (a < 0) return -1;
+                const long long ix = pr->attr_offset[a] + (pr->attr_animated[a] ? f : 0);
+                if (ix > INT32_MAX) throw Unsupported{"attribute block over 2^31 values"};
+                return (int)ix;
+            };
+            for (int cf = 0; cf < ncf; ++cf) {
+                const int c = cf_cam[cf], f = cf_frame[cf];
+                for (int k = 0; k < 7; ++k)
+                    tab[(size_t)CF_AIDX * cf + k] =
+                        vidx(pr->cam_attrs[MMBA_CAM_NUM_ATTRS * c + cam_k[k]], f);
+                const int t = pr->cam_tfm[c];
+                for (int k = 0; k < 9; ++k)
+                    tab[(size_t)CF_AIDX * cf + 7 + k] = vidx(pr->tfm_attrs[9 * t + k], f);
+            }
+            D.cf_aidx = upload(tab);
+        }
     }
     D.all_bnd_fast = 1;
     for (int b = 0; b < nB; ++b)
