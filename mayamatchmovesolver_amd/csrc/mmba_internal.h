@@ -82,8 +82,12 @@ struct BcrDev {
 
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
-    bool use_bcr = false;                    // unsharded, w <= 32: block cyclic reduction
+    bool use_bcr = false;                    // w <= 32: block cyclic reduction
     BcrDev bcr;
+    // sharded BCR: Bd | Ga | Gd | rhs contiguous; every shard writes its own
+    // Schur terms, one all-reduce (sum) assembles S, every shard factors it
+    double *red = nullptr, *red_rhs = nullptr;
+    size_t red_count = 0;
     int P = 1, w = 0, nb = 0, nG = 0;
     int p_lo = 0, p_hi = 1;                  // partitions this shard factors
     Comm *comm = nullptr;                    // sharded: T, rT are all-reduced

@@ -198,8 +198,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         if (do_xn) rs.row[rs.nrows++] = {pw, nparts, 0, SL_XN2};
         if (do_gn) rs.row[rs.nrows++] = {2 * pw, nparts, 1, SL_GNORM};
         launch_reduce_multi(s, d_partial, rs, d_scalar);
-        allreduce(d_scalar + SL_ZERO, 1, ReduceOp::Max);
-        if (do_xn) allreduce(d_scalar + SL_XN2, 1);
+        allreduce(d_scalar + SL_ZERO, do_xn ? 2 : 1);  // [ZERO, XN2]
         if (do_gn) allreduce(d_scalar + SL_GNORM, 1, ReduceOp::Max);
     }
     t_jac += wall_now() - t0;
@@ -224,10 +223,7 @@ void Plan::trial_enqueue(double *eu, double *ed) {
     rs.row[rs.nrows++] = {5 * pw, residual_blocks(P), 0, SL_FNORM};
     rs.row[rs.nrows++] = {6 * pw, residual_blocks(P), 0, SL_JP};
     launch_reduce_multi(s, d_partial, rs, d_scalar);
-    allreduce(d_scalar + SL_PNORM, 1);
-    allreduce(d_scalar + SL_XN2T, 1);
-    allreduce(d_scalar + SL_FNORM, 1);
-    allreduce(d_scalar + SL_JP, 1);
+    allreduce(d_scalar + SL_PNORM, 4);  // [PNORM, XN2T, FNORM, JP]
     t_func += wall_now() - t0;
 }
 
@@ -247,7 +243,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         // rewritten (diagonal blocks by k_schur_init, off-diagonal blocks
         // assigned by k_schur_dest, arrow rows by k_schur_init), so S is only
         // zeroed once at plan build; the partitioned path factors in place
-        if (band && !bs.use_bcr) {
+        if (band && bs.red) {  // d_rhs is the tail of the block, zeroed above
+            MMBA_HIP(hipMemsetAsync(bs.red, 0, sizeof(double) * (bs.red_count - nRpad), s));
+        } else if (band && !bs.use_bcr) {
             const int nb = nR - nG;
             MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
             if (nG > 0) MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * (size_t)nG * nb, s));
@@ -274,6 +272,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         }
         span_begin(SPAN_CHOL);
         if (band) {
+            if (bs.red) allreduce(bs.red, bs.red_count);
             band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
         } else if (dense) {
             ds.factor_forward(s, d_rhs, d_yR, d_fail);  // y = L^-1 rhs rides along
@@ -288,7 +287,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         span_end(SPAN_CHOL);
         if (band) {
             band_backward(s, bs, d_yR, d_xR);
-            if (nranks > 1) {  // every shard needs the rows of its halo camera-frames
+            if (nranks > 1 && !bs.use_bcr) {  // every shard needs its halo camera-frame rows
                 launch_keep_rows(s, d_xR, Ra, Rb, nR - nG, nR, rank == 0);
                 allreduce(d_xR, nR);
             }
@@ -320,9 +319,13 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         rs.flag_slot = SL_FAIL;
         rs.row[rs.nrows++] = {7 * pw, nparts, 0, dnorm_slot};
         launch_reduce_multi(s, d_partial, rs, d_scalar, d_fail);
-        allreduce(d_scalar + dnorm_slot, 1);
     }
-    allreduce(d_scalar + SL_FAIL, 1, ReduceOp::Max);
+    if (dnorm_slot == SL_DNORM) {
+        allreduce(d_scalar + SL_DNORM, 2);  // [DNORM, FAIL]
+    } else {
+        if (dnorm_slot >= 0) allreduce(d_scalar + dnorm_slot, 1);
+        allreduce(d_scalar + SL_FAIL, 1);
+    }
     t_linear += wall_now() - t0;
 }
 
@@ -603,7 +606,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             if (spec) trial_enqueue(d_eu_s, d_ed_s);
             {
                 const double t0 = wall_now();
-                read_slots(SL_FNORM, SL_XN2T);
+                read_slots(0, SL_LAST);
                 t_jac += wall_now() - t0;
             }
             rank_deficient = h_scalar[SL_ZERO] != 0.;
@@ -630,7 +633,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     // candidate ||D x_new|| -- one synchronisation
                     trial_enqueue(d_eu, d_ed);
                     const double t0 = wall_now();
-                    read_slots(SL_FNORM, SL_XN2T);
+                    read_slots(0, SL_LAST);
                     t_func += wall_now() - t0;
                 }
                 pre = false;

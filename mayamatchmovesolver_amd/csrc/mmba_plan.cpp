@@ -837,7 +837,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_Wg = dalloc<double>((size_t)nB * NGMAX * 3);
     d_W = dalloc<double>((size_t)P.wst * (nB_solved > 0 ? M : 1));
     d_U = dalloc<double>((size_t)4 * (nB_solved > 0 ? M : 1));
-    d_rhs = dalloc<double>(nRpad);
+    d_rhs = bs.red_rhs ? bs.red_rhs : dalloc<double>(nRpad);
     d_yR = dalloc<double>(nRpad);
     d_xR = dalloc<double>(nRpad);
     d_wR = dalloc<double>(nRpad);
@@ -882,16 +882,32 @@ void Plan::setup_band(int Pforce) {
     {
         const char *e = std::getenv("MMBA_BAND_BCR");
         const bool env_off = e && std::atoi(e) == 0;
-        if (nranks == 1 && w <= 32 && (Pforce < 0 || (Pforce == 0 && !env_off))) {
+        // Sharded: the partitioned chain's separator system grows with the
+        // shard count (one workgroup, (P-1) w rows at bandwidth 2w-1), so the
+        // shards all-reduce S instead and each runs the log-depth BCR on it;
+        // MMBA_SHARD_BCR=0 keeps the partitioned chain (A/B).
+        const char *es = std::getenv("MMBA_SHARD_BCR");
+        const bool shard_ok = nranks == 1 || !(es && std::atoi(es) == 0);
+        if (shard_ok && w <= 32 && (Pforce < 0 || (Pforce == 0 && !env_off))) {
             bs.use_bcr = true;
             bs.P = 1;
-            bs.comm = nullptr;
+            bs.comm = nranks > 1 ? comm : nullptr;
             bs.w = w;
             bs.nb = nb;
             bs.nG = nG;
-            bs.Bd = dalloc<double>((size_t)nb * (w + 1));
-            bs.Ga = dalloc<double>((size_t)nG * nb);
-            bs.Gd = dalloc<double>(NGMAX * NGMAX);
+            if (nranks > 1) {
+                const size_t nbd = (size_t)nb * (w + 1), nga = (size_t)nG * nb;
+                bs.red_count = nbd + nga + NGMAX * NGMAX + (size_t)nRpad;
+                bs.red = dalloc<double>(bs.red_count);
+                bs.Bd = bs.red;
+                bs.Ga = bs.Bd + nbd;
+                bs.Gd = bs.Ga + nga;
+                bs.red_rhs = bs.Gd + NGMAX * NGMAX;
+            } else {
+                bs.Bd = dalloc<double>((size_t)nb * (w + 1));
+                bs.Ga = dalloc<double>((size_t)nG * nb);
+                bs.Gd = dalloc<double>(NGMAX * NGMAX);
+            }
             // zeroed once: structural zeros of the band are never written
             MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (w + 1), s));
             MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * std::max<size_t>(1, (size_t)nG * nb), s));
@@ -936,7 +952,8 @@ void Plan::setup_band(int Pforce) {
                     MMBA_HIP(hipMemsetAsync(B.flags, 0, sizeof(int) * B.nblk, s));
                 }
             }
-            d_ymask = upload(std::vector<int>(std::max(nR, 1), 1));
+            // every shard holds the whole y = L^-1 v: rank 0 counts it
+            d_ymask = upload(std::vector<int>(std::max(nR, 1), rank == 0 ? 1 : 0));
             return;
         }
     }

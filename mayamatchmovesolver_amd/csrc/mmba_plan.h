@@ -204,19 +204,24 @@ struct Plan {
     // in device scalar slots (all-reduced across shards) and are fetched with
     // one read_slots() per decision point of the MINPACK control flow.
     enum Slot {
-        SL_FNORM = 0,   // ||f||^2 of the last fun_enqueue
-        SL_DNORM = 1,   // ||D v||^2
-        SL_NEWT_B = 2,  // lmpar Newton term, bundle part
-        SL_NEWT_R = 3,  //                    reduced-system part
-        SL_GDIV = 4,    // ||D^-1 g||^2 (lmpar gnorm)
-        SL_ZERO = 5,    // any exactly-zero Jacobian column (max)
-        SL_GNORM = 6,   // lmder gnorm (max)
-        SL_RMS = 7,
-        SL_FAIL = 8,    // factorisation failed (max)
-        SL_PNORM = 9,   // ||D p||^2 of the trial step
-        SL_JP = 10,     // ||J p||^2
-        SL_XN2 = 11,    // ||D x||^2 (first pass)
-        SL_XN2T = 12,   // ||D x_new||^2 of the trial point
+        // grouped so that each sharded exchange is one all-reduce:
+        // trial point [PNORM..JP], damped solve [DNORM, FAIL], lmpar Newton
+        // [NEWT_B, NEWT_R], Jacobian [ZERO, XN2] (sums; the flags are 0/1
+        // per shard, so a sum is nonzero exactly when the max is)
+        SL_PNORM = 0,   // ||D p||^2 of the trial step
+        SL_XN2T = 1,    // ||D x_new||^2 of the trial point
+        SL_FNORM = 2,   // ||f||^2 of the last fun_enqueue
+        SL_JP = 3,      // ||J p||^2
+        SL_DNORM = 4,   // ||D v||^2
+        SL_FAIL = 5,    // factorisation failed (flag)
+        SL_NEWT_B = 6,  // lmpar Newton term, bundle part
+        SL_NEWT_R = 7,  //                    reduced-system part
+        SL_GDIV = 8,    // ||D^-1 g||^2 (lmpar gnorm)
+        SL_ZERO = 9,    // any exactly-zero Jacobian column (flag)
+        SL_XN2 = 10,    // ||D x||^2 (first pass)
+        SL_GNORM = 11,  // lmder gnorm (max)
+        SL_RMS = 12,
+        SL_LAST = 12,
         NSLOT = 16
     };
     void read_slots(int lo, int hi);

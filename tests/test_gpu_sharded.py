@@ -64,8 +64,16 @@ def check_shards_agree(outs):
         assert o.result["iterations"] == outs[0].result["iterations"]
 
 
+# reduced-system solve of a sharded plan: S all-reduced and factored by block
+# cyclic reduction on every shard (default), or the partitioned band chain
+# with an all-reduced separator system (MMBA_SHARD_BCR=0)
+SOLVES = {"bcr": "1", "partitioned": "0"}
+
+
+@pytest.mark.parametrize("solve", list(SOLVES))
 @pytest.mark.parametrize("idx,kw,nshards", CASES)
-def test_sharded_matches_oracle(idx, kw, nshards, oracle):
+def test_sharded_matches_oracle(idx, kw, nshards, solve, oracle, monkeypatch):
+    monkeypatch.setenv("MMBA_SHARD_BCR", SOLVES[solve])
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
     xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt)
@@ -83,12 +91,14 @@ def test_sharded_matches_oracle(idx, kw, nshards, oracle):
     np.testing.assert_allclose(g.err_dist, edr, rtol=0, atol=1e-4 * np.max(np.abs(edr)))
 
 
-def test_sharded_ba_three_shards_structure(gpu_ctx):
+@pytest.mark.parametrize("solve", list(SOLVES))
+def test_sharded_ba_three_shards_structure(solve, gpu_ctx, monkeypatch):
     """3 shards (one with separators on both sides) on a bundle-Schur scene,
     against the unsharded GPU solve.  This scene is not conditioned well
     enough for a 1e-6 comparison (a rejected trial point moves by 1.4e-6), so
     the check is structural: same reason and counts, trace within 1e-5, x
     within 1e-4 (decomposition errors show up at 1e-2)."""
+    monkeypatch.setenv("MMBA_SHARD_BCR", SOLVES[solve])
     prob = S.make_config(3, frames=54, scale=0.006, **WC)
     opt = S.config_options(prob)
     s = Solver(prob, opt, context=gpu_ctx)
