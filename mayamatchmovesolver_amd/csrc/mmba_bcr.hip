@@ -210,6 +210,43 @@ __device__ __forceinline__ void bcr_chol_wave(double *M, double *rs_out, double 
         for (int c = 0; c < K; ++c) M[lane * KS + c] = (c <= lane) ? a[c] : 0.;
 }
 
+// Augmented Cholesky by ONE wave: lanes 0..K-1 hold the rows of the K x K
+// block (lower part of a), lanes K..63 hold right-hand-side columns b
+// (a = b^T, all K entries).  Factoring [D, B; B^T, *] leaves C in the block
+// rows and (C^-1 b)^T in every right-hand-side lane: the forward
+// substitutions ride on the pivot chain (same operations as bcr_trsv_col:
+// x_j *= 1 / C_jj, x_c -= C_cj x_j).  The caller loads a[] and stores it
+// back (so two waves can factor the same block without an LDS race).
+template <int K>
+__device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out, double *col,
+                                                  int &bad) {
+    const int lane = threadIdx.x & 63;
+    double d = bcr_rdlane(a[0], 0);
+    bool dbad = !(d > 0.) || !isfinite(d);
+    if (dbad) d = 1.;
+    double rs = bcr_rsq(d);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (dbad) bad = 1;
+        const double l = (lane > j) ? a[j] * rs : 0.;
+        a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+        if (lane < K) col[lane] = l;
+        if (rs_out && lane == 0) rs_out[j] = rs;
+        if (j + 1 < K) {
+            const double lj1 = bcr_rdlane(l, j + 1);
+            a[j + 1] = fma(-l, lj1, a[j + 1]);
+            d = bcr_rdlane(a[j + 1], j + 1);
+            dbad = !(d > 0.) || !isfinite(d);
+            if (dbad) d = 1.;
+            rs = bcr_rsq(d);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int c = j + 2; c < K; ++c) a[c] = fma(-l, col[c], a[c]);
+        wave_lds_sync();
+    }
+}
+
 // In-place forward substitution X <- C^-1 X for the column this lane owns
 // (x points at its first entry, stride xs between rows); column-oriented
 // (axpy) steps so the K dependent steps are short.
@@ -245,7 +282,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     __shared__ double sGT[2][K * GS];  // G_o^T -> Y_o
     __shared__ double sR[3][K];        // r_o1 -> y1, r_o2 -> y2, r_e (fused forward solve)
     __shared__ double sRs[2][K];       // 1 / C_jj
-    __shared__ double col[2][64];
+    __shared__ double col[4][64];
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
     __shared__ int bad_s;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -271,8 +308,12 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             tprev = tn;
         }
     };
-    // stage every operand (zeros where a neighbour does not exist)
-    for (int q = tid; q < K * K; q += blockDim.x) {
+    // stage every operand (zeros where a neighbour does not exist); fixed
+    // trip count so every round's loads are issued before the first store
+#pragma unroll
+    for (int q0 = 0; q0 < K * K; q0 += 256) {
+        const int q = q0 + tid;
+        if (q >= K * K) break;
         const int i = q / K, c = q % K, x = i * KS + c, xt = c * KS + i;
         const double d0 = h1 ? bcr_blk(B.Dk, o1, K)[q] : 0.;
         const double d1 = h2 ? bcr_blk(B.Dk, o2, K)[q] : 0.;
@@ -304,8 +345,51 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     }
     __syncthreads();
     stamp(0);
-    // A. Cholesky of the two odd neighbours, one wave each
     int bad = 0;
+    if constexpr (2 * K + NGMAX <= 64) {
+        // A+B. Cholesky of the two odd neighbours with their triangular
+        // solves fused into the pivot chain (bcr_chol_aug_wave): wave w
+        // factors neighbour w & 1; waves 0/1 carry U (and y) in lanes K..,
+        // waves 2/3 carry V and Y^T.  Both waves of a neighbour form the
+        // same C bit for bit; waves 0/1 store it.
+        const int w = wv & 1, half = wv >> 1;
+        const bool act = w == 0 ? h1 : h2;
+        double *xp = nullptr;
+        int xs = 0;
+        if (lane >= K && lane < 2 * K) {
+            xp = &sB[2 * w + half][lane - K];
+            xs = KS;
+        } else if (lane >= 2 * K) {
+            if (half == 0 && lane == 2 * K && fwd) {
+                xp = &sR[w][0];
+                xs = 1;
+            } else if (half == 1 && lane - 2 * K < nG) {
+                xp = &sGT[w][lane - 2 * K];
+                xs = GS;
+            }
+        }
+        double a[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+            a[c] = lane < K ? (c <= lane ? sD[w][lane * KS + c] : 0.) : (xp ? xp[c * xs] : 0.);
+        __syncthreads();  // every wave holds its operands: stores below may overwrite them
+        if (act) bcr_chol_aug_wave<K>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
+        if (act) {
+            if (lane < K) {
+                if (half == 0)
+#pragma unroll
+                    for (int c = 0; c < K; ++c) sD[w][lane * KS + c] = (c <= lane) ? a[c] : 0.;
+            } else if (xp) {
+#pragma unroll
+                for (int c = 0; c < K; ++c) xp[c * xs] = a[c];
+            }
+        }
+        if (bad) atomicOr(&bad_s, 1);
+        __syncthreads();
+        stamp(1);
+        stamp(2);
+    } else {
+    // A. Cholesky of the two odd neighbours, one wave each
     if (wv == 0 && h1) bcr_chol_wave<K, KS>(sD[0], sRs[0], col[0], bad);
     if (wv == 1 && h2) bcr_chol_wave<K, KS>(sD[1], sRs[1], col[1], bad);
     if (bad) atomicOr(&bad_s, 1);
@@ -330,6 +414,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     }
     __syncthreads();
     stamp(2);
+    }
     // C. updates of the even block: D_e -= V1^T V1 + U2^T U2 (lower), new
     // coupling -V1^T U1, G_e -= Y1^T V1 + Y2^T U2; stored factor columns of o2
     const double *U1 = sB[0], *V1 = sB[1], *U2 = sB[2], *V2 = sB[3];
