@@ -232,6 +232,12 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
         a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
         if (lane < K) col[lane] = l;
         if (rs_out && lane == 0) rs_out[j] = rs;
+        // column j is published before the pivot look-ahead, so its LDS
+        // reads are in flight while the next reciprocal root is formed
+        wave_lds_sync();
+        double cv[K];
+#pragma unroll
+        for (int c = j + 2; c < K; ++c) cv[c] = col[c];
         if (j + 1 < K) {
             const double lj1 = bcr_rdlane(l, j + 1);
             a[j + 1] = fma(-l, lj1, a[j + 1]);
@@ -240,9 +246,8 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
             if (dbad) d = 1.;
             rs = bcr_rsq(d);
         }
-        wave_lds_sync();
 #pragma unroll
-        for (int c = j + 2; c < K; ++c) a[c] = fma(-l, col[c], a[c]);
+        for (int c = j + 2; c < K; ++c) a[c] = fma(-l, cv[c], a[c]);
         wave_lds_sync();
     }
 }
