@@ -221,17 +221,21 @@ template <int K>
 __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out, double *col,
                                                   int &bad) {
     const int lane = threadIdx.x & 63;
+    // per-step bookkeeping stays in one register each: lane j keeps 1 / C_jj
+    // (stored once after the chain), the pivot checks fold into one flag
+    double rsl = 0.;
+    bool anybad = false;
     double d = bcr_rdlane(a[0], 0);
     bool dbad = !(d > 0.) || !isfinite(d);
     if (dbad) d = 1.;
     double rs = bcr_rsq(d);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        if (dbad) bad = 1;
+        anybad |= dbad;
         const double l = (lane > j) ? a[j] * rs : 0.;
         a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+        if (lane == j) rsl = rs;
         if (lane < K) col[lane] = l;
-        if (rs_out && lane == 0) rs_out[j] = rs;
         // column j is published before the pivot look-ahead, so its LDS
         // reads are in flight while the next reciprocal root is formed
         wave_lds_sync();
@@ -250,6 +254,8 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
         for (int c = j + 2; c < K; ++c) a[c] = fma(-l, cv[c], a[c]);
         wave_lds_sync();
     }
+    if (anybad) bad = 1;
+    if (rs_out && lane < K) rs_out[lane] = rsl;
 }
 
 // In-place forward substitution X <- C^-1 X for the column this lane owns

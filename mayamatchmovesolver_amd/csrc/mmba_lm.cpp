@@ -668,8 +668,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     par = p5 * par;
                 }
                 if (ratio >= p0001) {
-                    MMBA_HIP(hipMemcpyAsync(d_x, d_wa2, sizeof(double) * n,
-                                            hipMemcpyDeviceToDevice, s));
+                    std::swap(d_x, d_wa2);  // x <- wa2 (both plain n-vectors: no copy)
                     std::swap(d_f, d_ftrial);
                     xnorm = std::sqrt(h_scalar[SL_XN2T]);  // ||D wa2||, computed above
                     fnorm = fnorm1;
