@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--config", type=int, default=3, help="BASELINE.json configs index")
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--lens-model", default="classic", choices=["classic", "radial"],
+                    help="configs[4] lens: 3DE classic (the C5 spec) or 3DE radial std deg 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-traffic", action="store_true",
@@ -208,7 +210,8 @@ def main():
         frames = (frames or BASE_FRAMES.get(args.config, 500)) * world
         scale = scale * world
     t0 = time.perf_counter()
-    prob = S.make_config(args.config, frames=frames, scale=scale)
+    kw = {"lens_model": args.lens_model} if args.config == 4 else {}
+    prob = S.make_config(args.config, frames=frames, scale=scale, **kw)
     opt = S.config_options(prob)
     gen_s = time.perf_counter() - t0
     ctx = Context(local)
@@ -294,7 +297,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY 8(d) generator, seed 20241008+i)",
-            "config": {"workload": S.CONFIG_NAMES[args.config], "frames": prob.num_frames,
+            "config": {"workload": prob.meta.get("name", S.CONFIG_NAMES[args.config]),
+                       "frames": prob.num_frames,
                        "cameras": prob.num_cameras, "bundles": prob.num_bundles,
                        "markers": prob.num_markers, "observations": prob.num_obs,
                        "parameters": prob.num_params, "residuals": prob.num_residuals,

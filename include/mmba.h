@@ -70,9 +70,11 @@ extern "C" {
 #define MMBA_ROO_YXZ 4
 #define MMBA_ROO_ZYX 5
 
-/* Lens model types (mmlens LensModelType); only 3DE Classic is mapped. */
+/* Lens model types (mmlens LensModelType, lib/cppbind/mmlens/include/mmlens/
+ * _cxxbridge.h:414-421: k3deClassic, k3deRadialStdDeg4). */
 #define MMBA_LENS_NONE 0
 #define MMBA_LENS_3DE_CLASSIC 1
+#define MMBA_LENS_3DE_RADIAL_STD_DEG4 2
 
 /* Camera attribute slots in `cam_attrs` (8 per camera). */
 #define MMBA_CAM_FILM_BACK_W_INCH 0
@@ -85,8 +87,17 @@ extern "C" {
 #define MMBA_CAM_SCALE 7
 #define MMBA_CAM_NUM_ATTRS 8
 
-/* Lens attribute slots in `lens_attrs` (5 per lens; LDPK classic order). */
-#define MMBA_LENS_NUM_ATTRS 5
+/* Lens attribute slots in `lens_attrs` (8 per lens; -1 = attribute absent,
+ * the model's default is used).
+ *   3DE classic (LDPK classic order, lens_model_3de_classic.cpp:75-113):
+ *     0 distortion, 1 anamorphic squeeze (default 1), 2 curvature x,
+ *     3 curvature y, 4 quartic distortion; 5-7 unused.
+ *   3DE radial decentered deg 4 cylindric
+ *   (lens_model_3de_radial_decentered_deg_4_cylindric.cpp:70-80):
+ *     0 degree-2 distortion, 1 degree-2 u, 2 degree-2 v, 3 degree-4 distortion,
+ *     4 degree-4 u, 5 degree-4 v, 6 cylindric direction (degrees),
+ *     7 cylindric bending.  All default 0. */
+#define MMBA_LENS_NUM_ATTRS 8
 
 /*
  * Flattened problem.  Units are Maya UI units, exactly as the reference
@@ -123,7 +134,7 @@ typedef struct mmba_problem {
 
     int32_t num_lenses;
     const int32_t *lens_type;  /* [num_lenses] MMBA_LENS_*     */
-    const int32_t *lens_attrs; /* [5*num_lenses] attribute ids */
+    const int32_t *lens_attrs; /* [8*num_lenses] attribute ids */
 
     int32_t num_bundles;
     const int32_t *bnd_tfm; /* [num_bundles] transform index */

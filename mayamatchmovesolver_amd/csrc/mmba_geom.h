@@ -373,18 +373,34 @@ MMBA_DEV void lens_eval(const double *c, double px, double py, double &qx, doubl
     qy = py * (1 + cyx * p0_2 + cyy * p1_2 + cyxx * p0_4 + cyyx * p01_2 + cyyy * p1_4);
 }
 
-MMBA_DEV void lens_distort(const double *coeff, double x, double y, double &ox, double &oy) {
-    const double w = 3.6, h = 2.4;  // LensModel defaults (lens_model.h:42)
-    const double r = sqrt(w * w + h * h) / 2.0;
-    double ux = x + 0.5, uy = y + 0.5;
-    double qx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
-    double qy = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+// ---- LDPK radial decentered deg 4 + cylindric extender (3DE radial std
+// deg 4; mmlens distortion_structs.h:108-150; ldpk_radial_decentered_
+// distortion.h operator(), ldpk_cylindric_extender.h cylindric_extender_2)
+// c: c2 u2 v2 c4 u4 v4 phi(degrees) b ----
+MMBA_DEV void radial_eval(const double *c, double x, double y, double &qx, double &qy) {
+    const double c2 = c[0], u2 = c[1], v2 = c[2], c4 = c[3], u4 = c[4], v4 = c[5];
+    double x2 = x * x;
+    double y2 = y * y;
+    double xy = x * y;
+    double r2 = x2 + y2;
+    double r4 = r2 * r2;
+    qx = x * (1.0 + c2 * r2 + c4 * r4) + (r2 + 2.0 * x2) * (u2 + u4 * r2) +
+         2.0 * xy * (v2 + v4 * r2);
+    qy = y * (1.0 + c2 * r2 + c4 * r4) + (r2 + 2.0 * y2) * (v2 + v4 * r2) +
+         2.0 * xy * (u2 + u4 * r2);
+}
+
+// p <- q - (f(q) - q), then p <- p + q - f(p): <= 20 iterations until
+// ||f(p) - q|| < 1e-6, then 2 more (ldpk_generic_distortion_base.h map_inverse)
+template <typename EVAL>
+MMBA_DEV void fixed_point_inverse(EVAL f, double qx, double qy, double &px, double &py) {
     double fx, fy;
-    lens_eval(coeff, qx, qy, fx, fy);
-    double px = qx - (fx - qx), py = qy - (fy - qy);
+    f(qx, qy, fx, fy);
+    px = qx - (fx - qx);
+    py = qy - (fy - qy);
     for (int i = 0; i < 20; ++i) {
         double ix, iy;
-        lens_eval(coeff, px, py, ix, iy);
+        f(px, py, ix, iy);
         px = px + qx - ix;
         py = py + qy - iy;
         double dx = ix - qx, dy = iy - qy;
@@ -392,9 +408,37 @@ MMBA_DEV void lens_distort(const double *coeff, double x, double y, double &ox, 
     }
     for (int i = 0; i < 2; ++i) {
         double ix, iy;
-        lens_eval(coeff, px, py, ix, iy);
+        f(px, py, ix, iy);
         px = px + qx - ix;
         py = py + qy - iy;
+    }
+}
+
+MMBA_DEV void lens_distort(int type, const double *coeff, double x, double y, double &ox,
+                           double &oy) {
+    const double w = 3.6, h = 2.4;  // LensModel defaults (lens_model.h:42)
+    const double r = sqrt(w * w + h * h) / 2.0;
+    double ux = x + 0.5, uy = y + 0.5;
+    double qx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
+    double qy = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+    double px, py;
+    if (type == MMBA_LENS_3DE_RADIAL_STD_DEG4) {
+        // cylindric^-1 (invert(_m) * q, calc_m with M_PI), then the radial inverse
+        const double pi = 3.14159265358979323846;
+        const double phi = coeff[6], b = coeff[7];
+        double q = sqrt(1.0 + b), cs = cos(phi * pi / 180.0), sn = sin(phi * pi / 180.0);
+        const double m00 = cs * cs * q + sn * sn / q, m01 = (q - 1.0 / q) * cs * sn;
+        const double m10 = (q - 1.0 / q) * cs * sn, m11 = cs * cs / q + sn * sn * q;
+        const double det = m00 * m11 - m01 * m10;
+        const double i00 = m11 / det, i01 = -m01 / det, i10 = -m10 / det, i11 = m00 / det;
+        const double tx = i00 * qx + i01 * qy, ty = i10 * qx + i11 * qy;
+        fixed_point_inverse(
+            [&](double a, double bb, double &fa, double &fb) { radial_eval(coeff, a, bb, fa, fb); },
+            tx, ty, px, py);
+    } else {
+        fixed_point_inverse(
+            [&](double a, double bb, double &fa, double &fb) { lens_eval(coeff, a, bb, fa, fb); },
+            qx, qy, px, py);
     }
     double cxm = px * r + ((w / 2) + 0.0);
     double cym = py * r + ((h / 2) + 0.0);
@@ -410,7 +454,7 @@ struct Resid {
 
 // One observation's residual from a camera record and a bundle position.
 MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, double mkr_y,
-                        double sqrtw, int mode, double image_width, bool has_lens,
+                        double sqrtw, int mode, double image_width, int lens_type,
                         const double *lens) {
     double sp0 = rec[0] * bp[0] + rec[1] * bp[1] + rec[2] * bp[2] + rec[3];
     double sp1 = rec[4] * bp[0] + rec[5] * bp[1] + rec[6] * bp[2] + rec[7];
@@ -426,9 +470,9 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
         double dot = rec[15] * (bd0 / bl) + rec[16] * (bd1 / bl) + rec[17] * (bd2 / bl);
         if (dot < 0.0) factor = 1e+6;
     }
-    if (has_lens) {
+    if (lens_type != MMBA_LENS_NONE) {
         double ox, oy;
-        lens_distort(lens, point_x, point_y, ox, oy);
+        lens_distort(lens_type, lens, point_x, point_y, ox, oy);
         if (isfinite(ox)) point_x = ox;
         if (isfinite(oy)) point_y = oy;
     }
@@ -446,11 +490,10 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
 MMBA_DEV void lens_coeffs(const DevProblem &P, int lens, int f, const Override &ov,
                           double *c) {
     const int *la = &P.lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
-    c[0] = attr_get(P, la[0], f, 0., ov);
-    c[1] = attr_get(P, la[1], f, 1., ov);
-    c[2] = attr_get(P, la[2], f, 0., ov);
-    c[3] = attr_get(P, la[3], f, 0., ov);
-    c[4] = attr_get(P, la[4], f, 0., ov);
+    const bool classic = P.lens_type[lens] == MMBA_LENS_3DE_CLASSIC;
+#pragma unroll
+    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
+        c[k] = attr_get(P, la[k], f, (classic && k == 1) ? 1. : 0., ov);  // squeeze: 1
 }
 
 // Box-constraint reparametrisation (adjust_base.cpp:194-220).

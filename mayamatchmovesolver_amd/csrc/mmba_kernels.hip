@@ -209,10 +209,11 @@ __device__ __forceinline__ void base_bundle(const DevProblem &P, int b, int f, d
     }
 }
 
-__device__ __forceinline__ bool obs_lens(const DevProblem &P, int cam, int &lens) {
-    if (!P.cam_lens) return false;
+// Lens model type of the camera's lens (MMBA_LENS_*), 0 without one.
+__device__ __forceinline__ int obs_lens(const DevProblem &P, int cam, int &lens) {
+    if (!P.cam_lens) return MMBA_LENS_NONE;
     lens = P.cam_lens[cam];
-    return lens >= 0 && P.lens_type[lens] == MMBA_LENS_3DE_CLASSIC;
+    return lens >= 0 ? P.lens_type[lens] : MMBA_LENS_NONE;
 }
 
 // -------------------------------------------------------------------------
@@ -252,9 +253,9 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         } else {
             base_bundle(P, b, fr, bp);
         }
-        double lc[5];
+        double lc[MMBA_LENS_NUM_ATTRS];
         int lens = -1;
-        const bool hl = !FAST && obs_lens(P, cam, lens);
+        const int hl = FAST ? MMBA_LENS_NONE : obs_lens(P, cam, lens);
         if (hl) lens_coeffs(P, lens, fr, none, lc);
         const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
         Resid r = residual(rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i], P.mode,
@@ -340,9 +341,9 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     const int4 p4 = P.bnd_p4[b];
     double bp0[3];
     base_bundle(P, b, fr, bp0);
-    double lc0[5];
+    double lc0[MMBA_LENS_NUM_ATTRS];
     int lens = -1;
-    const bool hl = obs_lens(P, cam, lens);
+    const int hl = obs_lens(P, cam, lens);
     if (hl) lens_coeffs(P, lens, fr, none, lc0);
     const int voff = P.cf_var_off[cf];
     const int nvar = P.cf_var_off[cf + 1] - voff;
@@ -424,7 +425,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
             const int p = P.cam_lpar[q];
             if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
             const Override ov{P.p_attr[p], ext_pert[p]};
-            double lc[5];
+            double lc[MMBA_LENS_NUM_ATTRS];
             lens_coeffs(P, lens, fr, ov, lc);
             emit(p, residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, hl, lc));
         }
@@ -480,7 +481,7 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     const int nb = p4.w > 0 ? p4.w : 0;
     const double *__restrict__ br = &P.brec[(size_t)b * BREC];
     const double *__restrict__ rec0 = &recs[(size_t)voff * CAMREC];
-    const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr);
+    const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr);
     int l = 0;
     double rsx = r0.ux, rsy = r0.uy, rsd = r0.dist;  // errorList of the stale column
     bool hit = false;
@@ -511,7 +512,7 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     for (int v = 0; v < NCV; ++v) {
         if (v < nv) {
             const double *__restrict__ rec = &recs[(size_t)(voff + 1 + v) * CAMREC];
-            emit(pv[v], residual(rec, bp0, mx, my, sw, P.mode, P.image_width, false, nullptr),
+            emit(pv[v], residual(rec, bp0, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr),
                  st[v]);
         }
     }
@@ -521,7 +522,7 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
             const double bq[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
             const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
             const double2 j = emit(
-                p, residual(rec0, bq, mx, my, sw, P.mode, P.image_width, false, nullptr),
+                p, residual(rec0, bq, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr),
                 br[12 + a]);
             jb[2 * a] = j.x;
             jb[2 * a + 1] = j.y;

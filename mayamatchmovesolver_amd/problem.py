@@ -202,6 +202,12 @@ class Problem:
     @classmethod
     def from_npz_dict(cls, d):
         kw = {name: np.asarray(d[name]) for name in _FIELDS_I32 + _FIELDS_I64 + _FIELDS_F64}
+        nl = int(np.asarray(kw["lens_type"]).size)
+        la = np.asarray(kw["lens_attrs"], dtype=np.int32).reshape(-1)
+        if nl and la.size == 5 * nl:  # fixtures written with the 5-slot (classic-only) stride
+            la = np.concatenate([la.reshape(nl, 5), -np.ones((nl, abi.LENS_NUM_ATTRS - 5),
+                                                             np.int32)], axis=1).reshape(-1)
+            kw["lens_attrs"] = la
         return cls(num_frames=int(d["num_frames"]), **kw)
 
     def with_x0(self, x0):
@@ -332,6 +338,19 @@ class SceneBuilder:
                self._as_attr(quartic_distortion, 0.0)]
         idx = len(self._lens_type)
         self._lens_type.append(abi.LENS_3DE_CLASSIC)
+        self._lens_attrs.append(ids + [-1] * (abi.LENS_NUM_ATTRS - len(ids)))
+        return idx, ids
+
+    def lens_3de_radial_std_deg4(self, degree2_distortion=0.0, degree2_u=0.0, degree2_v=0.0,
+                                 degree4_distortion=0.0, degree4_u=0.0, degree4_v=0.0,
+                                 cylindric_direction=0.0, cylindric_bending=0.0):
+        """3DE radial decentered deg 4 cylindric lens (mmlens
+        LensModel3deRadialDecenteredDeg4Cylindric).  Returns (lens index, [8 attr ids])."""
+        vals = (degree2_distortion, degree2_u, degree2_v, degree4_distortion, degree4_u,
+                degree4_v, cylindric_direction, cylindric_bending)
+        ids = [self._as_attr(v, 0.0) for v in vals]
+        idx = len(self._lens_type)
+        self._lens_type.append(abi.LENS_3DE_RADIAL_STD_DEG4)
         self._lens_attrs.append(ids)
         return idx, ids
 

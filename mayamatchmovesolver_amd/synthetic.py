@@ -161,6 +161,37 @@ def _lens_distort_truth(c, x, y):
     return px * r / w, py * r / h
 
 
+def _radial_distort_truth(c, x, y):
+    """Forward model used only to synthesise markers through a 3DE radial
+    decentered deg 4 cylindric lens: cylindric^-1 then the fixed-point inverse
+    of the radial decentered polynomial (LDPK radial_decentered_distortion,
+    cylindric_extender_2)."""
+    c2, u2, v2, c4, u4, v4, phi, bend = c
+    w, h = 3.6, 2.4
+    r = math.sqrt(w * w + h * h) / 2.0
+    q = math.sqrt(1.0 + bend)
+    cs, sn = math.cos(math.radians(phi)), math.sin(math.radians(phi))
+    m = np.array([[cs * cs * q + sn * sn / q, (q - 1 / q) * cs * sn],
+                  [(q - 1 / q) * cs * sn, cs * cs / q + sn * sn * q]])
+    mi = np.linalg.inv(m)
+    dx, dy = x * w / r, y * h / r
+    qx, qy = mi[0, 0] * dx + mi[0, 1] * dy, mi[1, 0] * dx + mi[1, 1] * dy
+
+    def ev(px, py):
+        x2, y2, xy = px * px, py * py, px * py
+        r2 = x2 + y2
+        rad = 1.0 + c2 * r2 + c4 * r2 * r2
+        return (px * rad + (r2 + 2 * x2) * (u2 + u4 * r2) + 2 * xy * (v2 + v4 * r2),
+                py * rad + (r2 + 2 * y2) * (v2 + v4 * r2) + 2 * xy * (u2 + u4 * r2))
+
+    fx, fy = ev(qx, qy)
+    px, py = qx - (fx - qx), qy - (fy - qy)
+    for _ in range(40):
+        ix, iy = ev(px, py)
+        px, py = px + qx - ix, py + qy - iy
+    return px * r / w, py * r / h
+
+
 CONFIG_NAMES = {
     0: "c1_1cam_20bnd_50mkr_10f_lmdif",
     1: "c2_1cam_1kbnd_5kmkr_120f_pose_focal",
@@ -172,7 +203,7 @@ CONFIG_NAMES = {
 
 def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                 scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH, window: int = 4,
-                depth=(20.0, 200.0)) -> Problem:
+                depth=(20.0, 200.0), lens_model: str = "classic") -> Problem:
     """Concrete synthetic input for BASELINE.json ``configs[index]``.
 
     ``frames`` / ``scale`` shrink a configuration (frame-window subsets and
@@ -181,6 +212,9 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
     frames) and ``depth`` (bundle depth range) apply to configs[3] only: the
     defaults are the C4 spec; longer tracks / nearer bundles give the
     well-conditioned variants the sharded-solve tests compare x on.
+    ``lens_model`` (configs[4] only): "classic" (the C5 spec) or "radial" (the
+    same scene through a 3DE radial decentered deg 4 cylindric lens, degree-2
+    and degree-4 distortion solved: SURVEY 8(f) row 2).
     """
     rng = np.random.Generator(np.random.PCG64(20241008 + index))
     if index == 0:
@@ -195,7 +229,7 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                           K=int(50000 * scale), window=window, per_cam_markers=False,
                           depth=depth)
     if index == 4:
-        return _config_c5(rng, frames or 240, scale)
+        return _config_c5(rng, frames or 240, scale, lens_model)
     raise KeyError(index)
 
 
@@ -261,7 +295,10 @@ def _bulk_problem(F, cams_t, cams_r, cams_focal, cam_solve, bnd_init, bnd_solved
     lens_ids = []
     lens_idx = -1
     if lens is not None:
-        lens_idx, lens_ids = b.lens_3de_classic(*lens["init"])
+        if lens.get("model") == "radial":
+            lens_idx, lens_ids = b.lens_3de_radial_std_deg4(*lens["init"])
+        else:
+            lens_idx, lens_ids = b.lens_3de_classic(*lens["init"])
     cam_attr_ids = []
     for c in range(len(cams_t)):
         tfm, tids = b.transform(t=[cams_t[c][:, 0], cams_t[c][:, 1], cams_t[c][:, 2]],
@@ -425,7 +462,7 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0
                          meta={"name": CONFIG_NAMES[index]})
 
 
-def _config_c5(rng, F, scale):
+def _config_c5(rng, F, scale, lens_model="classic"):
     """2 cams, 1k locked bundles, 2k markers (1k per cam), windows mean 60,
     one shared 3DE-classic lens with distortion + quartic solved (lens attrs first)."""
     B, K = max(1, int(1000 * scale)), max(2, int(2000 * scale))
@@ -435,7 +472,15 @@ def _config_c5(rng, F, scale):
     K = mkr_cam.size
     mkr_bnd = np.arange(K) % B
     start, length = _windows(rng, K, F, 60)
-    lens_true = (0.05, 1.0, 0.0, 0.0, 0.01)
+    if lens_model == "radial":
+        lens_true = (0.05, 0.002, -0.002, 0.01, 0.0, 0.0, 20.0, 0.05)
+        distort = _radial_distort_truth
+        lens = {"model": "radial", "init": (0.0,) + lens_true[1:3] + (0.0,) + lens_true[4:],
+                "solve_slots": (0, 3)}
+    else:
+        lens_true = (0.05, 1.0, 0.0, 0.0, 0.01)
+        distort = _lens_distort_truth
+        lens = {"init": (0.0, 1.0, 0.0, 0.0, 0.0), "solve_slots": (0, 4)}
 
     def proj(ks, fs):
         mx = np.empty(ks.size)
@@ -448,16 +493,17 @@ def _config_c5(rng, F, scale):
         ra = RENDER[0] / RENDER[1]
         fa = FILM_W_MM / FILM_H_MM
         py = my * (ra / fa)
-        dx, dy = _lens_distort_truth(lens_true, mx, py)
+        dx, dy = distort(lens_true, mx, py)
         return dx, dy / (ra / fa)
 
     ks, fs, xy = _obs_from_windows(rng, start, length, proj)
     t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
     r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
-    lens = {"init": (0.0, 1.0, 0.0, 0.0, 0.0), "solve_slots": (0, 4)}
     return _bulk_problem(F, t0, r0, [FOCAL_MM, FOCAL_MM], lambda tids, cids: list(tids[:6]),
                          P, np.zeros(B, bool), mkr_cam, mkr_bnd, ks, fs, xy, lens=lens,
-                         lens_first=True, meta={"name": CONFIG_NAMES[4]})
+                         lens_first=True,
+                         meta={"name": CONFIG_NAMES[4] + ("_radial" if lens_model == "radial"
+                                                          else "")})
 
 
 def config_options(prob: Problem, scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH,

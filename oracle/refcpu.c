@@ -792,6 +792,105 @@ void ref_lens_3de_classic_undistort(const double coeff[5], double x, double y,
     *out_y = cym / h - 0.5;
 }
 
+/* 3DE radial decentered deg 4 cylindric (mmlens
+ * lens_model_3de_radial_decentered_deg_4_cylindric.cpp:58-92 ->
+ * distortion_structs.h:108-150 Distortion3deRadialStdDeg4): undistort =
+ * cylindric(radial(p)); distort = radial.map_inverse(cylindric^-1(q)), the
+ * fixed-point inverse of ldpk_generic_distortion_base.h (20 + 2 iterations,
+ * 1e-6).  Restated from the LDPK 2.8 header text
+ * (ldpk_radial_decentered_distortion.h operator(), ldpk_cylindric_extender.h
+ * cylindric_extender_2::calc_m / eval / eval_inv, ldpk_vec2d.h invert / mat*vec).
+ * c: degree-2 c2 u2 v2, degree-4 c4 u4 v4, phi (degrees), b. */
+static void radial_eval(const double c[8], double x, double y, double *qx, double *qy) {
+    const double c2 = c[0], u2 = c[1], v2 = c[2], c4 = c[3], u4 = c[4], v4 = c[5];
+    double x2 = x * x;
+    double y2 = y * y;
+    double xy = x * y;
+    double r2 = x2 + y2;
+    double r4 = r2 * r2;
+    *qx = x * (1.0 + c2 * r2 + c4 * r4) + (r2 + 2.0 * x2) * (u2 + u4 * r2) +
+          2.0 * xy * (v2 + v4 * r2);
+    *qy = y * (1.0 + c2 * r2 + c4 * r4) + (r2 + 2.0 * y2) * (v2 + v4 * r2) +
+          2.0 * xy * (u2 + u4 * r2);
+}
+
+static void cylindric_mats(const double c[8], double m[4], double mi[4]) {
+    const double phi = c[6], b = c[7];
+    const double pi = 3.14159265358979323846; /* M_PI, as ldpk_cylindric_extender.h */
+    double q = sqrt(1.0 + b), cs = cos(phi * pi / 180.0), sn = sin(phi * pi / 180.0);
+    m[0] = cs * cs * q + sn * sn / q;
+    m[1] = (q - 1.0 / q) * cs * sn;
+    m[2] = (q - 1.0 / q) * cs * sn;
+    m[3] = cs * cs / q + sn * sn * q;
+    double det = m[0] * m[3] - m[1] * m[2];
+    mi[0] = m[3] / det;
+    mi[1] = -m[1] / det;
+    mi[2] = -m[2] / det;
+    mi[3] = m[0] / det;
+}
+
+static void radial_map_inverse(const double c[8], double qx, double qy, double *px_out,
+                               double *py_out) {
+    double fx, fy;
+    radial_eval(c, qx, qy, &fx, &fy);
+    double px = qx - (fx - qx), py = qy - (fy - qy);
+    for (int i = 0; i < 20; ++i) {
+        double ix, iy;
+        radial_eval(c, px, py, &ix, &iy);
+        px = px + qx - ix;
+        py = py + qy - iy;
+        double dx = ix - qx, dy = iy - qy;
+        double diff = sqrt(dx * dx + dy * dy);
+        if (diff < 1e-6) break;
+    }
+    for (int i = 0; i < 2; ++i) {
+        double ix, iy;
+        radial_eval(c, px, py, &ix, &iy);
+        px = px + qx - ix;
+        py = py + qy - iy;
+    }
+    *px_out = px;
+    *py_out = py;
+}
+
+void ref_lens_3de_radial_distort(const double coeff[8], double x, double y, double *out_x,
+                                 double *out_y) {
+    const double w = LENS_FB_W_CM, h = LENS_FB_H_CM;
+    const double r = sqrt(w * w + h * h) / 2.0;
+    double ux = x + 0.5, uy = y + 0.5;
+    double dnx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
+    double dny = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+    double m[4], mi[4];
+    cylindric_mats(coeff, m, mi);
+    double tx = mi[0] * dnx + mi[1] * dny;
+    double ty = mi[2] * dnx + mi[3] * dny;
+    double px, py;
+    radial_map_inverse(coeff, tx, ty, &px, &py);
+    double cxm = px * r + ((w / 2) + 0.0);
+    double cym = py * r + ((h / 2) + 0.0);
+    *out_x = cxm / w - 0.5;
+    *out_y = cym / h - 0.5;
+}
+
+void ref_lens_3de_radial_undistort(const double coeff[8], double x, double y, double *out_x,
+                                   double *out_y) {
+    const double w = LENS_FB_W_CM, h = LENS_FB_H_CM;
+    const double r = sqrt(w * w + h * h) / 2.0;
+    double ux = x + 0.5, uy = y + 0.5;
+    double dnx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
+    double dny = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+    double m[4], mi[4];
+    cylindric_mats(coeff, m, mi);
+    double qx, qy;
+    radial_eval(coeff, dnx, dny, &qx, &qy);
+    double px = m[0] * qx + m[1] * qy;
+    double py = m[2] * qx + m[3] * qy;
+    double cxm = px * r + ((w / 2) + 0.0);
+    double cym = py * r + ((h / 2) + 0.0);
+    *out_x = cxm / w - 0.5;
+    *out_y = cym / h - 0.5;
+}
+
 /* ======================================================================
  * Scene state + measureErrors.
  * ====================================================================== */
@@ -910,13 +1009,12 @@ static void film_fit_marker(int film_fit, double film_aspect,
     }
 }
 
-static void lens_coeffs(const ref_scene *s, int lens, int f, double c[5]) {
+/* Lens attribute values (absent slots: the model's defaults, mmba.h). */
+static void lens_coeffs(const ref_scene *s, int lens, int f, double c[MMBA_LENS_NUM_ATTRS]) {
     const int *la = &s->p->lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
-    c[0] = attr_value(s, la[0], f, 0.);
-    c[1] = attr_value(s, la[1], f, 1.);
-    c[2] = attr_value(s, la[2], f, 0.);
-    c[3] = attr_value(s, la[3], f, 0.);
-    c[4] = attr_value(s, la[4], f, 0.);
+    const int classic = s->p->lens_type[lens] == MMBA_LENS_3DE_CLASSIC;
+    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
+        c[k] = attr_value(s, la[k], f, (classic && k == 1) ? 1. : 0.);
 }
 
 static void apply_lens(const ref_scene *s, int cam, int f, double *px,
@@ -924,10 +1022,15 @@ static void apply_lens(const ref_scene *s, int cam, int f, double *px,
     const mmba_problem *p = s->p;
     if (!p->cam_lens) return;
     int lens = p->cam_lens[cam];
-    if (lens < 0 || p->lens_type[lens] != MMBA_LENS_3DE_CLASSIC) return;
-    double c[5], ox = *px, oy = *py;
+    if (lens < 0) return;
+    const int type = p->lens_type[lens];
+    if (type != MMBA_LENS_3DE_CLASSIC && type != MMBA_LENS_3DE_RADIAL_STD_DEG4) return;
+    double c[MMBA_LENS_NUM_ATTRS], ox = *px, oy = *py;
     lens_coeffs(s, lens, f, c);
-    ref_lens_3de_classic_distort(c, *px, *py, &ox, &oy);
+    if (type == MMBA_LENS_3DE_CLASSIC)
+        ref_lens_3de_classic_distort(c, *px, *py, &ox, &oy);
+    else
+        ref_lens_3de_radial_distort(c, *px, *py, &ox, &oy);
     if (isfinite(ox)) *px = ox; /* adjust_measureErrors.cpp:466-472 */
     if (isfinite(oy)) *py = oy;
 }

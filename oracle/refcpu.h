@@ -68,6 +68,11 @@ void ref_lens_3de_classic_distort(const double coeff[5], double x, double y,
                                   double *out_x, double *out_y);
 void ref_lens_3de_classic_undistort(const double coeff[5], double x, double y,
                                     double *out_x, double *out_y);
+/* 3DE radial decentered deg 4 cylindric: coeff = c2 u2 v2 c4 u4 v4 phi(deg) b */
+void ref_lens_3de_radial_distort(const double coeff[8], double x, double y,
+                                 double *out_x, double *out_y);
+void ref_lens_3de_radial_undistort(const double coeff[8], double x, double y,
+                                   double *out_x, double *out_y);
 
 /* ---- full solve through the same mmba_problem layout ---- */
 int ref_measure(const mmba_problem *prob, const mmba_options *opt,

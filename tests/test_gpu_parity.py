@@ -81,12 +81,38 @@ def test_measure_and_jacobian_small(mode, oracle, gpu_ctx):
         s.close()
 
 
+@pytest.mark.parametrize("lens_model", ["classic", "radial"])
+def test_measure_and_jacobian_lens(lens_model, oracle, gpu_ctx):
+    """Residuals (1e-12) and FD Jacobian (1e-7 of its max entry) through each
+    lens model, lens coefficients solved (SURVEY 8(f) row 2 for "radial")."""
+    prob = S.make_config(4, frames=8, scale=0.05, lens_model=lens_model)
+    opt = S.config_options(prob)
+    f_ref, eu_ref, ed_ref, _ = oracle.measure(prob, opt)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        f, eu, ed, _ = s.measure()
+        np.testing.assert_allclose(f, f_ref, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(ed, ed_ref, rtol=1e-12, atol=1e-12)
+        x1 = prob.x0 + 0.01
+        f1, _, _, _ = s.measure(x1)
+        f1_ref, _, _, _ = oracle.measure(prob, opt, x1)
+        np.testing.assert_allclose(f1, f1_ref, rtol=1e-12, atol=1e-12)
+        J = s.jacobian(x1)
+        _, J_ref = oracle.jacobian(prob, opt, x1)
+        scale = np.max(np.abs(J_ref))
+        assert np.max(np.abs(J - J_ref)) <= 1e-7 * scale
+    finally:
+        s.close()
+
+
 SMALL_CONFIGS = [
     (0, dict()),                              # C1 full (lmdif, 90 params)
     (1, dict(frames=12, scale=0.05)),         # C2 subset (pose + focal per frame)
     (2, dict(frames=8, scale=0.002)),         # C3 subset (10 cams, Schur)
     (3, dict(frames=8, scale=0.001)),         # C4 subset (Schur BA)
     (4, dict(frames=8, scale=0.05)),          # C5 subset (3DE classic lens)
+    (4, dict(frames=8, scale=0.05, lens_model="radial")),  # C5 subset, 3DE radial std deg 4
+    (4, dict(frames=24, scale=0.2, lens_model="radial")),
 ]
 
 

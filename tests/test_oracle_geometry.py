@@ -75,6 +75,50 @@ def test_lens_3de_classic_round_trip(oracle):
     assert oracle.lens_distort([0, 1, 0, 0, 0], 0.3, -0.2) == pytest.approx((0.3, -0.2), abs=1e-15)
 
 
+RADIAL_TEST_COEFF = [0.1, 0.01, -0.01, 0.05, -0.02, 0.02, 45.0, 0.5]
+
+
+def test_lens_3de_radial_round_trip(oracle):
+    """mmlens test_once_3de_radial_std_deg4.cpp:40-67 (the coefficients of that
+    test, its order: undistort, then redistort).  The reference test prints and
+    asserts nothing; the fixed-point inverse (20 + 2 iterations,
+    ldpk_generic_distortion_base.h) is not converged at the far corner
+    (-0.5, 0.5) with this strong bending (1.2e-3 there), so the bound is 1e-5
+    inside |x|, |y| <= 0.45 and 2e-3 on the whole frame."""
+    for x in np.linspace(-0.5, 0.5, 9):
+        for y in np.linspace(-0.5, 0.5, 9):
+            ux, uy = oracle.lens_radial_undistort(RADIAL_TEST_COEFF, x, y)
+            dx, dy = oracle.lens_radial_distort(RADIAL_TEST_COEFF, ux, uy)
+            tol = 1e-5 if max(abs(x), abs(y)) <= 0.45 else 2e-3
+            assert abs(dx - x) < tol and abs(dy - y) < tol
+    zero = [0.0] * 8
+    assert oracle.lens_radial_distort(zero, 0.3, -0.2) == pytest.approx((0.3, -0.2), abs=1e-15)
+    assert oracle.lens_radial_undistort(zero, 0.3, -0.2) == pytest.approx((0.3, -0.2), abs=1e-15)
+
+
+def test_lens_3de_radial_undistort_model(oracle):
+    """The undistort map restated independently in numpy from the LDPK text:
+    cylindric M (ldpk_cylindric_extender.h calc_m) applied to the radial
+    decentered polynomial (ldpk_radial_decentered_distortion.h operator()),
+    in diagonal-normalised coordinates (mmlens lib.h:45-58, back 3.6 x 2.4)."""
+    c2, u2, v2, c4, u4, v4, phi, b = RADIAL_TEST_COEFF
+    w, h = 3.6, 2.4
+    r = np.hypot(w, h) / 2
+    q = np.sqrt(1 + b)
+    cs, sn = np.cos(np.radians(phi)), np.sin(np.radians(phi))
+    M = np.array([[cs * cs * q + sn * sn / q, (q - 1 / q) * cs * sn],
+                  [(q - 1 / q) * cs * sn, cs * cs / q + sn * sn * q]])
+    for x, y in [(0.3, -0.2), (-0.45, 0.4), (0.01, 0.02), (0.5, 0.5)]:
+        px, py = x * w / r, y * h / r
+        r2 = px * px + py * py
+        rad = 1 + c2 * r2 + c4 * r2 * r2
+        qx = px * rad + (r2 + 2 * px * px) * (u2 + u4 * r2) + 2 * px * py * (v2 + v4 * r2)
+        qy = py * rad + (r2 + 2 * py * py) * (v2 + v4 * r2) + 2 * px * py * (u2 + u4 * r2)
+        ox, oy = M @ [qx, qy]
+        got = oracle.lens_radial_undistort(RADIAL_TEST_COEFF, x, y)
+        assert got == pytest.approx((ox * r / w, oy * r / h), abs=1e-13)
+
+
 def test_bound_transforms(oracle):
     from mayamatchmovesolver_amd.problem import (FLOAT_MAX, param_external_to_internal,
                                                  param_internal_to_external)

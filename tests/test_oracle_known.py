@@ -31,3 +31,19 @@ def test_behind_camera_penalty_only_in_maya_dag(oracle):
     f_dag = oracle.measure(prob, make_options(scene_graph_mode=abi.SCENE_GRAPH_MODE_MAYA_DAG))[0]
     f_sg = oracle.measure(prob, make_options(scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH))[0]
     np.testing.assert_allclose(f_dag, f_sg * 1e6, rtol=1e-12)
+
+
+def test_radial_lens_scene_recovers_coefficients(oracle):
+    """the C5 scene through a 3DE radial decentered deg 4
+    cylindric lens (truth c2 = 0.05, c4 = 0.01; u/v/phi/b fixed at truth):
+    the oracle lmder solve converges and recovers both solved coefficients
+    to within the 0.5 px marker noise."""
+    from mayamatchmovesolver_amd import synthetic as S
+    prob = S.make_config(4, frames=24, scale=0.2, lens_model="radial")
+    assert list(prob.lens_type) == [abi.LENS_3DE_RADIAL_STD_DEG4]
+    opt = S.config_options(prob)
+    x, f, eu, ed, res, trace = oracle.solve(prob, opt)
+    assert 1 <= res.reason_number <= 4
+    ext = prob.external_params(x)
+    assert abs(ext[0] - 0.05) < 2e-3 and abs(ext[1] - 0.01) < 3e-3, ext[:2]
+    assert trace[-1] < 0.02 * trace[0]
