@@ -50,8 +50,9 @@ def parse():
     ap.add_argument("--config", type=int, default=3, help="BASELINE.json configs index")
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--lens-model", default="classic", choices=["classic", "radial"],
-                    help="configs[4] lens: 3DE classic (the C5 spec) or 3DE radial std deg 4")
+    ap.add_argument("--lens-model", default="classic",
+                    choices=["classic", "radial", "anamorphic", "anamorphic_rescaled"],
+                    help="configs[4] lens model (classic = the C5 spec)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-traffic", action="store_true",

@@ -75,6 +75,8 @@ extern "C" {
 #define MMBA_LENS_NONE 0
 #define MMBA_LENS_3DE_CLASSIC 1
 #define MMBA_LENS_3DE_RADIAL_STD_DEG4 2
+#define MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 3
+#define MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED 4
 
 /* Camera attribute slots in `cam_attrs` (8 per camera). */
 #define MMBA_CAM_FILM_BACK_W_INCH 0
@@ -87,7 +89,7 @@ extern "C" {
 #define MMBA_CAM_SCALE 7
 #define MMBA_CAM_NUM_ATTRS 8
 
-/* Lens attribute slots in `lens_attrs` (8 per lens; -1 = attribute absent,
+/* Lens attribute slots in `lens_attrs` (14 per lens; -1 = attribute absent,
  * the model's default is used).
  *   3DE classic (LDPK classic order, lens_model_3de_classic.cpp:75-113):
  *     0 distortion, 1 anamorphic squeeze (default 1), 2 curvature x,
@@ -96,8 +98,13 @@ extern "C" {
  *   (lens_model_3de_radial_decentered_deg_4_cylindric.cpp:70-80):
  *     0 degree-2 distortion, 1 degree-2 u, 2 degree-2 v, 3 degree-4 distortion,
  *     4 degree-4 u, 5 degree-4 v, 6 cylindric direction (degrees),
- *     7 cylindric bending.  All default 0. */
-#define MMBA_LENS_NUM_ATTRS 8
+ *     7 cylindric bending.  All default 0.
+ *   3DE anamorphic deg 4 rotate squeeze xy (+ rescaled)
+ *   (lens_model_3de_anamorphic_deg_4_rotate_squeeze_xy[_rescaled].cpp:53-66):
+ *     0 cx02, 1 cy02, 2 cx22, 3 cy22, 4 cx04, 5 cy04, 6 cx24, 7 cy24, 8 cx44,
+ *     9 cy44 (default 0), 10 lens rotation (degrees, default 0), 11 squeeze x,
+ *     12 squeeze y, 13 rescale (rescaled model only; defaults 1). */
+#define MMBA_LENS_NUM_ATTRS 14
 
 /*
  * Flattened problem.  Units are Maya UI units, exactly as the reference
@@ -134,7 +141,7 @@ typedef struct mmba_problem {
 
     int32_t num_lenses;
     const int32_t *lens_type;  /* [num_lenses] MMBA_LENS_*     */
-    const int32_t *lens_attrs; /* [8*num_lenses] attribute ids */
+    const int32_t *lens_attrs; /* [14*num_lenses] attribute ids */
 
     int32_t num_bundles;
     const int32_t *bnd_tfm; /* [num_bundles] transform index */

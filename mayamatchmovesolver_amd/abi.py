@@ -30,6 +30,8 @@ ROO_XYZ, ROO_YZX, ROO_ZXY, ROO_XZY, ROO_YXZ, ROO_ZYX = range(6)
 LENS_NONE = 0
 LENS_3DE_CLASSIC = 1
 LENS_3DE_RADIAL_STD_DEG4 = 2
+LENS_3DE_ANAMORPHIC_STD_DEG4 = 3
+LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED = 4
 
 CAM_FILM_BACK_W_INCH = 0
 CAM_FILM_BACK_H_INCH = 1
@@ -40,7 +42,7 @@ CAM_NEAR_CLIP = 5
 CAM_FAR_CLIP = 6
 CAM_SCALE = 7
 CAM_NUM_ATTRS = 8
-LENS_NUM_ATTRS = 8
+LENS_NUM_ATTRS = 14
 
 _i32p = C.POINTER(C.c_int32)
 _i64p = C.POINTER(C.c_int64)

@@ -390,6 +390,35 @@ MMBA_DEV void radial_eval(const double *c, double x, double y, double &qx, doubl
          2.0 * xy * (u2 + u4 * r2);
 }
 
+// ---- LDPK anamorphic deg 4 (degree-4 specialisation of
+// ldpk_generic_anamorphic_distortion.h: prepare() + operator()) ----
+// c: cx02 cy02 cx22 cy22 cx04 cy04 cx24 cy24 cx44 cy44 rot(deg) sqx sqy rescale
+MMBA_DEV void anam_eval(const double *c, double x, double y, double &qx, double &qy) {
+    const double cx02 = c[0], cy02 = c[1], cx22 = c[2], cy22 = c[3], cx04 = c[4],
+                 cy04 = c[5], cx24 = c[6], cy24 = c[7], cx44 = c[8], cy44 = c[9];
+    double cx_x2 = cx02 + cx22, cx_y2 = cx02 - cx22, cx_x4 = cx04 + cx24 + cx44;
+    double cx_x2y2 = 2.0 * cx04 - 6.0 * cx44, cx_y4 = cx04 - cx24 + cx44;
+    double cy_x2 = cy02 + cy22, cy_y2 = cy02 - cy22, cy_x4 = cy04 + cy24 + cy44;
+    double cy_x2y2 = 2.0 * cy04 - 6.0 * cy44, cy_y4 = cy04 - cy24 + cy44;
+    double x2 = x * x, x4 = x2 * x2;
+    double y2 = y * y, y4 = y2 * y2;
+    qx = x * (1.0 + x2 * cx_x2 + y2 * cx_y2 + x4 * cx_x4 + x2 * y2 * cx_x2y2 + y4 * cx_y4);
+    qy = y * (1.0 + x2 * cy_x2 + y2 * cy_y2 + x4 * cy_x4 + x2 * y2 * cy_x2y2 + y4 * cy_y4);
+}
+
+struct Mat2 {
+    double a00, a01, a10, a11;
+};
+// LDPK mat2d product and inverse (ldpk_vec2d.h: row-major, invert = adj / det)
+MMBA_DEV Mat2 m2_mul(const Mat2 &t, const Mat2 &a) {
+    return Mat2{t.a00 * a.a00 + t.a01 * a.a10, t.a00 * a.a01 + t.a01 * a.a11,
+                t.a10 * a.a00 + t.a11 * a.a10, t.a10 * a.a01 + t.a11 * a.a11};
+}
+MMBA_DEV Mat2 m2_inv(const Mat2 &a) {
+    const double det = a.a00 * a.a11 - a.a01 * a.a10;
+    return Mat2{a.a11 / det, -a.a01 / det, -a.a10 / det, a.a00 / det};
+}
+
 // p <- q - (f(q) - q), then p <- p + q - f(p): <= 20 iterations until
 // ||f(p) - q|| < 1e-6, then 2 more (ldpk_generic_distortion_base.h map_inverse)
 template <typename EVAL>
@@ -435,6 +464,26 @@ MMBA_DEV void lens_distort(int type, const double *coeff, double x, double y, do
         fixed_point_inverse(
             [&](double a, double bb, double &fa, double &fb) { radial_eval(coeff, a, bb, fa, fb); },
             tx, ty, px, py);
+    } else if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 ||
+               type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED) {
+        // PAR * anamorphic^-1(RSP^-1 q): RSP = R Sx Sy Rs PA, PAR = PA Rs R
+        // (linear_extender::set, left-to-right products; PA = pixel aspect 1,
+        // Rs = identity for the non-rescaled model: both leave products exact)
+        const double pi = 3.14159265358979323846;
+        const double phi = coeff[10] / 180.0 * pi;
+        const Mat2 R{cos(phi), -sin(phi), sin(phi), cos(phi)};
+        const Mat2 Sx{coeff[11], 0.0, 0.0, 1.0}, Sy{1.0, 0.0, 0.0, coeff[12]};
+        const Mat2 Rs{coeff[13], 0.0, 0.0, 1.0}, PA{1.0, 0.0, 0.0, 1.0};
+        const Mat2 rsp = m2_mul(m2_mul(m2_mul(m2_mul(R, Sx), Sy), Rs), PA);
+        const Mat2 par = m2_mul(m2_mul(PA, Rs), R);
+        const Mat2 ri = m2_inv(rsp);
+        const double tx = ri.a00 * qx + ri.a01 * qy, ty = ri.a10 * qx + ri.a11 * qy;
+        double ax, ay;
+        fixed_point_inverse(
+            [&](double a, double bb, double &fa, double &fb) { anam_eval(coeff, a, bb, fa, fb); },
+            tx, ty, ax, ay);
+        px = par.a00 * ax + par.a01 * ay;
+        py = par.a10 * ax + par.a11 * ay;
     } else {
         fixed_point_inverse(
             [&](double a, double bb, double &fa, double &fb) { lens_eval(coeff, a, bb, fa, fb); },
@@ -490,10 +539,16 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
 MMBA_DEV void lens_coeffs(const DevProblem &P, int lens, int f, const Override &ov,
                           double *c) {
     const int *la = &P.lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
-    const bool classic = P.lens_type[lens] == MMBA_LENS_3DE_CLASSIC;
+    const int type = P.lens_type[lens];
+    const bool classic = type == MMBA_LENS_3DE_CLASSIC;
+    const bool anam = type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 ||
+                      type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED;
+    // absent slots take the model default (mmba.h): classic squeeze,
+    // anamorphic squeeze x / y and rescale are 1, the rest 0
 #pragma unroll
     for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
-        c[k] = attr_get(P, la[k], f, (classic && k == 1) ? 1. : 0., ov);  // squeeze: 1
+        c[k] = attr_get(P, la[k], f, ((classic && k == 1) || (anam && k >= 11)) ? 1. : 0., ov);
+    if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.;  // no rescale slot
 }
 
 // Box-constraint reparametrisation (adjust_base.cpp:194-220).

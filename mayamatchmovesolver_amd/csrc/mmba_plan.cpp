@@ -143,9 +143,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     int lens_owner = -2;
     for (int c = 0; c < nC; ++c) {
         const int l = pr->cam_lens ? pr->cam_lens[c] : -1;
-        if (l >= 0 && pr->lens_type[l] != MMBA_LENS_3DE_CLASSIC &&
-            pr->lens_type[l] != MMBA_LENS_3DE_RADIAL_STD_DEG4)
-            throw Unsupported{"lens model not mapped (3DE classic, 3DE radial std deg 4)"};
+        if (l >= 0 && (pr->lens_type[l] < MMBA_LENS_3DE_CLASSIC ||
+                       pr->lens_type[l] > MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED))
+            throw Unsupported{"unknown lens model type"};
         // B3: the reference mixes per-marker/per-attr lens indices; it is only
         // well defined when every camera shares one lens (or none has one).
         if (lens_owner == -2) lens_owner = l;

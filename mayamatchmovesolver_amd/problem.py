@@ -351,7 +351,26 @@ class SceneBuilder:
         ids = [self._as_attr(v, 0.0) for v in vals]
         idx = len(self._lens_type)
         self._lens_type.append(abi.LENS_3DE_RADIAL_STD_DEG4)
-        self._lens_attrs.append(ids)
+        self._lens_attrs.append(ids + [-1] * (abi.LENS_NUM_ATTRS - len(ids)))
+        return idx, ids
+
+    def lens_3de_anamorphic_std_deg4(self, cx02=0.0, cy02=0.0, cx22=0.0, cy22=0.0, cx04=0.0,
+                                     cy04=0.0, cx24=0.0, cy24=0.0, cx44=0.0, cy44=0.0,
+                                     lens_rotation=0.0, squeeze_x=1.0, squeeze_y=1.0,
+                                     rescale=None):
+        """3DE anamorphic deg 4 rotate squeeze xy lens (mmlens
+        LensModel3deAnamorphicDeg4RotateSqueezeXY); with ``rescale`` the
+        "Rescaled" variant.  Returns (lens index, [13 or 14 attr ids])."""
+        vals = (cx02, cy02, cx22, cy22, cx04, cy04, cx24, cy24, cx44, cy44, lens_rotation)
+        ids = [self._as_attr(v, 0.0) for v in vals]
+        ids += [self._as_attr(squeeze_x, 1.0), self._as_attr(squeeze_y, 1.0)]
+        kind = abi.LENS_3DE_ANAMORPHIC_STD_DEG4
+        if rescale is not None:
+            ids.append(self._as_attr(rescale, 1.0))
+            kind = abi.LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED
+        idx = len(self._lens_type)
+        self._lens_type.append(kind)
+        self._lens_attrs.append(ids + [-1] * (abi.LENS_NUM_ATTRS - len(ids)))
         return idx, ids
 
     def bundle(self, tfm: int) -> int:

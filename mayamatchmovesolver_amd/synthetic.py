@@ -192,6 +192,40 @@ def _radial_distort_truth(c, x, y):
     return px * r / w, py * r / h
 
 
+def _anamorphic_distort_truth(c, x, y):
+    """Forward model used only to synthesise markers through a 3DE anamorphic
+    deg 4 rotate squeeze xy (rescaled) lens: PAR * fixed-point inverse of the
+    anamorphic polynomial at RSP^-1 q (LDPK generic_anamorphic_distortion<4>,
+    rotation / squeeze extenders)."""
+    cx02, cy02, cx22, cy22, cx04, cy04, cx24, cy24, cx44, cy44, rot, sqx, sqy, rs = c
+    w, h = 3.6, 2.4
+    r = math.sqrt(w * w + h * h) / 2.0
+    ph = math.radians(rot)
+    R = np.array([[math.cos(ph), -math.sin(ph)], [math.sin(ph), math.cos(ph)]])
+    rsp = R @ np.diag([sqx, 1.0]) @ np.diag([1.0, sqy]) @ np.diag([rs, 1.0])
+    par = np.diag([rs, 1.0]) @ R
+    ri = np.linalg.inv(rsp)
+    dx, dy = x * w / r, y * h / r
+    qx, qy = ri[0, 0] * dx + ri[0, 1] * dy, ri[1, 0] * dx + ri[1, 1] * dy
+    kx = (cx02 + cx22, cx02 - cx22, cx04 + cx24 + cx44, 2 * cx04 - 6 * cx44, cx04 - cx24 + cx44)
+    ky = (cy02 + cy22, cy02 - cy22, cy04 + cy24 + cy44, 2 * cy04 - 6 * cy44, cy04 - cy24 + cy44)
+
+    def ev(px, py):
+        x2, y2 = px * px, py * py
+        return (px * (1 + x2 * kx[0] + y2 * kx[1] + x2 * x2 * kx[2] + x2 * y2 * kx[3]
+                      + y2 * y2 * kx[4]),
+                py * (1 + x2 * ky[0] + y2 * ky[1] + x2 * x2 * ky[2] + x2 * y2 * ky[3]
+                      + y2 * y2 * ky[4]))
+
+    fx, fy = ev(qx, qy)
+    px, py = qx - (fx - qx), qy - (fy - qy)
+    for _ in range(40):
+        ix, iy = ev(px, py)
+        px, py = px + qx - ix, py + qy - iy
+    ox, oy = par[0, 0] * px + par[0, 1] * py, par[1, 0] * px + par[1, 1] * py
+    return ox * r / w, oy * r / h
+
+
 CONFIG_NAMES = {
     0: "c1_1cam_20bnd_50mkr_10f_lmdif",
     1: "c2_1cam_1kbnd_5kmkr_120f_pose_focal",
@@ -212,9 +246,11 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
     frames) and ``depth`` (bundle depth range) apply to configs[3] only: the
     defaults are the C4 spec; longer tracks / nearer bundles give the
     well-conditioned variants the sharded-solve tests compare x on.
-    ``lens_model`` (configs[4] only): "classic" (the C5 spec) or "radial" (the
+    ``lens_model`` (configs[4] only): "classic" (the C5 spec), "radial" (the
     same scene through a 3DE radial decentered deg 4 cylindric lens, degree-2
-    and degree-4 distortion solved: SURVEY 8(f) row 2).
+    and degree-4 distortion solved), "anamorphic" / "anamorphic_rescaled"
+    (3DE anamorphic deg 4 rotate squeeze xy [rescaled], cx02 / cy02 solved):
+    SURVEY 8(f) row 2.
     """
     rng = np.random.Generator(np.random.PCG64(20241008 + index))
     if index == 0:
@@ -297,6 +333,8 @@ def _bulk_problem(F, cams_t, cams_r, cams_focal, cam_solve, bnd_init, bnd_solved
     if lens is not None:
         if lens.get("model") == "radial":
             lens_idx, lens_ids = b.lens_3de_radial_std_deg4(*lens["init"])
+        elif lens.get("model") == "anamorphic":
+            lens_idx, lens_ids = b.lens_3de_anamorphic_std_deg4(*lens["init"])
         else:
             lens_idx, lens_ids = b.lens_3de_classic(*lens["init"])
     cam_attr_ids = []
@@ -472,7 +510,15 @@ def _config_c5(rng, F, scale, lens_model="classic"):
     K = mkr_cam.size
     mkr_bnd = np.arange(K) % B
     start, length = _windows(rng, K, F, 60)
-    if lens_model == "radial":
+    if lens_model in ("anamorphic", "anamorphic_rescaled"):
+        resc = lens_model == "anamorphic_rescaled"
+        lens_true = (0.03, 0.02, -0.01, 0.01, 0.005, 0.005, 0.0, 0.0, 0.0, 0.0, 5.0, 1.05, 1.0,
+                     1.2 if resc else 1.0)
+        distort = _anamorphic_distort_truth
+        init = (0.0, 0.0) + lens_true[2:13]
+        lens = {"model": "anamorphic", "init": init + ((lens_true[13],) if resc else ()),
+                "solve_slots": (0, 1)}
+    elif lens_model == "radial":
         lens_true = (0.05, 0.002, -0.002, 0.01, 0.0, 0.0, 20.0, 0.05)
         distort = _radial_distort_truth
         lens = {"model": "radial", "init": (0.0,) + lens_true[1:3] + (0.0,) + lens_true[4:],
@@ -502,8 +548,8 @@ def _config_c5(rng, F, scale, lens_model="classic"):
     return _bulk_problem(F, t0, r0, [FOCAL_MM, FOCAL_MM], lambda tids, cids: list(tids[:6]),
                          P, np.zeros(B, bool), mkr_cam, mkr_bnd, ks, fs, xy, lens=lens,
                          lens_first=True,
-                         meta={"name": CONFIG_NAMES[4] + ("_radial" if lens_model == "radial"
-                                                          else "")})
+                         meta={"name": CONFIG_NAMES[4] + ("" if lens_model == "classic"
+                                                          else "_" + lens_model)})
 
 
 def config_options(prob: Problem, scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH,

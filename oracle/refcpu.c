@@ -891,6 +891,129 @@ void ref_lens_3de_radial_undistort(const double coeff[8], double x, double y, do
     *out_y = cym / h - 0.5;
 }
 
+/* 3DE anamorphic deg 4 rotate squeeze xy (+ rescaled) (mmlens
+ * lens_model_3de_anamorphic_deg_4_rotate_squeeze_xy[_rescaled].cpp ->
+ * distortion_structs.h:152-301 Distortion3deAnamorphicStdDeg4[Rescaled]):
+ *   undistort = RSP * anamorphic(PAR^-1 * p),
+ *   distort   = PAR * anamorphic.map_inverse(RSP^-1 * q),
+ * RSP = R Sx Sy [Rs] PA and PAR = PA [Rs] R (ldpk_linear_extender.h set(),
+ * left-to-right 2x2 products), R = rotation by value / 180 * pi
+ * (ldpk_rotation_extender.h), Sx / Sy / Rs / PA squeeze-x / squeeze-y
+ * extenders (ldpk_squeeze_extender.h; PA = the LensModel pixel aspect 1.0,
+ * lens_model.h:41), the anamorphic polynomial of the degree-4
+ * specialisation of ldpk_generic_anamorphic_distortion.h (prepare(),
+ * operator()).  A missing rescale factor (non-rescaled model) is the
+ * identity, which leaves every product exactly unchanged.
+ * c: cx02 cy02 cx22 cy22 cx04 cy04 cx24 cy24 cx44 cy44 rot(deg) sqx sqy rescale */
+typedef struct {
+    double a00, a01, a10, a11;
+} ref_m2;
+
+static ref_m2 m2_mul(ref_m2 t, ref_m2 a) {
+    ref_m2 r = {t.a00 * a.a00 + t.a01 * a.a10, t.a00 * a.a01 + t.a01 * a.a11,
+                t.a10 * a.a00 + t.a11 * a.a10, t.a10 * a.a01 + t.a11 * a.a11};
+    return r;
+}
+
+static ref_m2 m2_inv(ref_m2 a) {
+    double det = a.a00 * a.a11 - a.a01 * a.a10;
+    ref_m2 r = {a.a11 / det, -a.a01 / det, -a.a10 / det, a.a00 / det};
+    return r;
+}
+
+static void anam_mats(const double c[14], ref_m2 *rsp, ref_m2 *par) {
+    const double pi = 3.14159265358979323846;
+    double phi = c[10] / 180.0 * pi;
+    ref_m2 R = {cos(phi), -sin(phi), sin(phi), cos(phi)};
+    ref_m2 Sx = {c[11], 0.0, 0.0, 1.0};
+    ref_m2 Sy = {1.0, 0.0, 0.0, c[12]};
+    ref_m2 Rs = {c[13], 0.0, 0.0, 1.0};
+    ref_m2 PA = {1.0, 0.0, 0.0, 1.0};
+    *rsp = m2_mul(m2_mul(m2_mul(m2_mul(R, Sx), Sy), Rs), PA);
+    *par = m2_mul(m2_mul(PA, Rs), R);
+}
+
+static void anam_eval(const double c[14], double x, double y, double *qx, double *qy) {
+    const double cx02 = c[0], cy02 = c[1], cx22 = c[2], cy22 = c[3], cx04 = c[4],
+                 cy04 = c[5], cx24 = c[6], cy24 = c[7], cx44 = c[8], cy44 = c[9];
+    double cx_x2 = cx02 + cx22, cx_y2 = cx02 - cx22, cx_x4 = cx04 + cx24 + cx44;
+    double cx_x2y2 = 2.0 * cx04 - 6.0 * cx44, cx_y4 = cx04 - cx24 + cx44;
+    double cy_x2 = cy02 + cy22, cy_y2 = cy02 - cy22, cy_x4 = cy04 + cy24 + cy44;
+    double cy_x2y2 = 2.0 * cy04 - 6.0 * cy44, cy_y4 = cy04 - cy24 + cy44;
+    double x2 = x * x, x4 = x2 * x2;
+    double y2 = y * y, y4 = y2 * y2;
+    *qx = x * (1.0 + x2 * cx_x2 + y2 * cx_y2 + x4 * cx_x4 + x2 * y2 * cx_x2y2 + y4 * cx_y4);
+    *qy = y * (1.0 + x2 * cy_x2 + y2 * cy_y2 + x4 * cy_x4 + x2 * y2 * cy_x2y2 + y4 * cy_y4);
+}
+
+static void anam_map_inverse(const double c[14], double qx, double qy, double *px_out,
+                             double *py_out) {
+    double fx, fy;
+    anam_eval(c, qx, qy, &fx, &fy);
+    double px = qx - (fx - qx), py = qy - (fy - qy);
+    for (int i = 0; i < 20; ++i) {
+        double ix, iy;
+        anam_eval(c, px, py, &ix, &iy);
+        px = px + qx - ix;
+        py = py + qy - iy;
+        double dx = ix - qx, dy = iy - qy;
+        double diff = sqrt(dx * dx + dy * dy);
+        if (diff < 1e-6) break;
+    }
+    for (int i = 0; i < 2; ++i) {
+        double ix, iy;
+        anam_eval(c, px, py, &ix, &iy);
+        px = px + qx - ix;
+        py = py + qy - iy;
+    }
+    *px_out = px;
+    *py_out = py;
+}
+
+void ref_lens_3de_anamorphic_distort(const double coeff[14], double x, double y,
+                                     double *out_x, double *out_y) {
+    const double w = LENS_FB_W_CM, h = LENS_FB_H_CM;
+    const double r = sqrt(w * w + h * h) / 2.0;
+    double ux = x + 0.5, uy = y + 0.5;
+    double dnx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
+    double dny = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+    ref_m2 rsp, par;
+    anam_mats(coeff, &rsp, &par);
+    ref_m2 ri = m2_inv(rsp);
+    double tx = ri.a00 * dnx + ri.a01 * dny;
+    double ty = ri.a10 * dnx + ri.a11 * dny;
+    double px, py;
+    anam_map_inverse(coeff, tx, ty, &px, &py);
+    double ox = par.a00 * px + par.a01 * py;
+    double oy = par.a10 * px + par.a11 * py;
+    double cxm = ox * r + ((w / 2) + 0.0);
+    double cym = oy * r + ((h / 2) + 0.0);
+    *out_x = cxm / w - 0.5;
+    *out_y = cym / h - 0.5;
+}
+
+void ref_lens_3de_anamorphic_undistort(const double coeff[14], double x, double y,
+                                       double *out_x, double *out_y) {
+    const double w = LENS_FB_W_CM, h = LENS_FB_H_CM;
+    const double r = sqrt(w * w + h * h) / 2.0;
+    double ux = x + 0.5, uy = y + 0.5;
+    double dnx = ((ux - 1.0 / 2.0) * w - 0.0) / r;
+    double dny = ((uy - 1.0 / 2.0) * h - 0.0) / r;
+    ref_m2 rsp, par;
+    anam_mats(coeff, &rsp, &par);
+    ref_m2 pi_ = m2_inv(par);
+    double tx = pi_.a00 * dnx + pi_.a01 * dny;
+    double ty = pi_.a10 * dnx + pi_.a11 * dny;
+    double qx, qy;
+    anam_eval(coeff, tx, ty, &qx, &qy);
+    double ox = rsp.a00 * qx + rsp.a01 * qy;
+    double oy = rsp.a10 * qx + rsp.a11 * qy;
+    double cxm = ox * r + ((w / 2) + 0.0);
+    double cym = oy * r + ((h / 2) + 0.0);
+    *out_x = cxm / w - 0.5;
+    *out_y = cym / h - 0.5;
+}
+
 /* ======================================================================
  * Scene state + measureErrors.
  * ====================================================================== */
@@ -1009,12 +1132,23 @@ static void film_fit_marker(int film_fit, double film_aspect,
     }
 }
 
+/* Default of lens attribute slot k (mmba.h): classic squeeze, anamorphic
+ * squeeze x / y and rescale are 1, everything else 0. */
+static double lens_default(int type, int k) {
+    if (type == MMBA_LENS_3DE_CLASSIC) return k == 1 ? 1. : 0.;
+    if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 ||
+        type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED)
+        return k >= 11 ? 1. : 0.;
+    return 0.;
+}
+
 /* Lens attribute values (absent slots: the model's defaults, mmba.h). */
 static void lens_coeffs(const ref_scene *s, int lens, int f, double c[MMBA_LENS_NUM_ATTRS]) {
     const int *la = &s->p->lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
-    const int classic = s->p->lens_type[lens] == MMBA_LENS_3DE_CLASSIC;
+    const int type = s->p->lens_type[lens];
     for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
-        c[k] = attr_value(s, la[k], f, (classic && k == 1) ? 1. : 0.);
+        c[k] = attr_value(s, la[k], f, lens_default(type, k));
+    if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.; /* no rescale slot */
 }
 
 static void apply_lens(const ref_scene *s, int cam, int f, double *px,
@@ -1024,13 +1158,15 @@ static void apply_lens(const ref_scene *s, int cam, int f, double *px,
     int lens = p->cam_lens[cam];
     if (lens < 0) return;
     const int type = p->lens_type[lens];
-    if (type != MMBA_LENS_3DE_CLASSIC && type != MMBA_LENS_3DE_RADIAL_STD_DEG4) return;
+    if (type < MMBA_LENS_3DE_CLASSIC || type > MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED) return;
     double c[MMBA_LENS_NUM_ATTRS], ox = *px, oy = *py;
     lens_coeffs(s, lens, f, c);
     if (type == MMBA_LENS_3DE_CLASSIC)
         ref_lens_3de_classic_distort(c, *px, *py, &ox, &oy);
-    else
+    else if (type == MMBA_LENS_3DE_RADIAL_STD_DEG4)
         ref_lens_3de_radial_distort(c, *px, *py, &ox, &oy);
+    else
+        ref_lens_3de_anamorphic_distort(c, *px, *py, &ox, &oy);
     if (isfinite(ox)) *px = ox; /* adjust_measureErrors.cpp:466-472 */
     if (isfinite(oy)) *py = oy;
 }

@@ -73,6 +73,13 @@ void ref_lens_3de_radial_distort(const double coeff[8], double x, double y,
                                  double *out_x, double *out_y);
 void ref_lens_3de_radial_undistort(const double coeff[8], double x, double y,
                                    double *out_x, double *out_y);
+/* 3DE anamorphic deg 4 rotate squeeze xy (+ rescaled): coeff = cx02 cy02 cx22
+ * cy22 cx04 cy04 cx24 cy24 cx44 cy44 rotation(deg) squeeze_x squeeze_y rescale
+ * (rescale 1 for the non-rescaled model) */
+void ref_lens_3de_anamorphic_distort(const double coeff[14], double x, double y,
+                                     double *out_x, double *out_y);
+void ref_lens_3de_anamorphic_undistort(const double coeff[14], double x, double y,
+                                       double *out_x, double *out_y);
 
 /* ---- full solve through the same mmba_problem layout ---- */
 int ref_measure(const mmba_problem *prob, const mmba_options *opt,

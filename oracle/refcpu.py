@@ -54,7 +54,8 @@ def lib():
         L.ref_reproject.restype = None
         L.ref_reproject.argtypes = [dp, dp, dp, dp]
         for name in ("ref_lens_3de_classic_distort", "ref_lens_3de_classic_undistort",
-                     "ref_lens_3de_radial_distort", "ref_lens_3de_radial_undistort"):
+                     "ref_lens_3de_radial_distort", "ref_lens_3de_radial_undistort",
+                     "ref_lens_3de_anamorphic_distort", "ref_lens_3de_anamorphic_undistort"):
             f = getattr(L, name)
             f.restype = None
             f.argtypes = [dp, C.c_double, C.c_double, dp, dp]
@@ -190,6 +191,20 @@ def lens_radial_undistort(coeff, x, y):
     c = np.ascontiguousarray(coeff, dtype=np.float64)
     ox, oy = C.c_double(), C.c_double()
     lib().ref_lens_3de_radial_undistort(_dp(c), x, y, C.byref(ox), C.byref(oy))
+    return ox.value, oy.value
+
+
+def lens_anamorphic_distort(coeff, x, y):
+    c = np.ascontiguousarray(coeff, dtype=np.float64)
+    ox, oy = C.c_double(), C.c_double()
+    lib().ref_lens_3de_anamorphic_distort(_dp(c), x, y, C.byref(ox), C.byref(oy))
+    return ox.value, oy.value
+
+
+def lens_anamorphic_undistort(coeff, x, y):
+    c = np.ascontiguousarray(coeff, dtype=np.float64)
+    ox, oy = C.c_double(), C.c_double()
+    lib().ref_lens_3de_anamorphic_undistort(_dp(c), x, y, C.byref(ox), C.byref(oy))
     return ox.value, oy.value
 
 

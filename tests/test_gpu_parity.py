@@ -81,7 +81,8 @@ def test_measure_and_jacobian_small(mode, oracle, gpu_ctx):
         s.close()
 
 
-@pytest.mark.parametrize("lens_model", ["classic", "radial"])
+@pytest.mark.parametrize("lens_model", ["classic", "radial", "anamorphic",
+                                        "anamorphic_rescaled"])
 def test_measure_and_jacobian_lens(lens_model, oracle, gpu_ctx):
     """Residuals (1e-12) and FD Jacobian (1e-7 of its max entry) through each
     lens model, lens coefficients solved (SURVEY 8(f) row 2 for "radial")."""
@@ -113,6 +114,8 @@ SMALL_CONFIGS = [
     (4, dict(frames=8, scale=0.05)),          # C5 subset (3DE classic lens)
     (4, dict(frames=8, scale=0.05, lens_model="radial")),  # C5 subset, 3DE radial std deg 4
     (4, dict(frames=24, scale=0.2, lens_model="radial")),
+    (4, dict(frames=8, scale=0.05, lens_model="anamorphic")),  # 3DE anamorphic std deg 4
+    (4, dict(frames=24, scale=0.2, lens_model="anamorphic_rescaled")),
 ]
 
 

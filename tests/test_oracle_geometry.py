@@ -119,6 +119,54 @@ def test_lens_3de_radial_undistort_model(oracle):
         assert got == pytest.approx((ox * r / w, oy * r / h), abs=1e-13)
 
 
+ANAM_TEST_COEFF = [0.05, 0.05, -0.05, -0.05, 0.05, 0.05, -0.05, -0.05, 0.15, 0.15,
+                   45.0, 1.1, 1.0]
+
+
+@pytest.mark.parametrize("rescale", [1.0, 2.0])
+def test_lens_3de_anamorphic_round_trip(oracle, rescale):
+    """mmlens test_once_3de_anamorphic_std_deg4[_rescaled].cpp:58-74 (its
+    coefficients; rescale 1.0 is the non-rescaled model): undistort, then
+    redistort, returns the input (the reference test prints, asserts nothing)."""
+    c = ANAM_TEST_COEFF + [rescale]
+    worst = 0.0
+    for x in np.linspace(-0.4, 0.4, 9):
+        for y in np.linspace(-0.4, 0.4, 9):
+            ux, uy = oracle.lens_anamorphic_undistort(c, x, y)
+            dx, dy = oracle.lens_anamorphic_distort(c, ux, uy)
+            worst = max(worst, abs(dx - x), abs(dy - y))
+    assert worst < 1e-5, worst
+    ident = [0.0] * 10 + [0.0, 1.0, 1.0, 1.0]
+    assert oracle.lens_anamorphic_distort(ident, 0.3, -0.2) == pytest.approx((0.3, -0.2), abs=1e-15)
+
+
+@pytest.mark.parametrize("rescale", [1.0, 2.0])
+def test_lens_3de_anamorphic_undistort_generic_form(oracle, rescale):
+    """The oracle's undistort uses the degree-4 specialisation (prepare()'s
+    combined coefficients); restate it here from the GENERIC r / phi form of
+    ldpk_generic_anamorphic_distortion.h operator() (sum of
+    c(i_phi, i_r) cos(i_phi phi) r^i_r), with the extender matrices built
+    independently (rotation, squeeze x / y, rescale; pixel aspect 1)."""
+    c = ANAM_TEST_COEFF + [rescale]
+    cx = {(0, 0): 1.0, (0, 2): c[0], (2, 2): c[2], (0, 4): c[4], (2, 4): c[6], (4, 4): c[8]}
+    cy = {(0, 0): 1.0, (0, 2): c[1], (2, 2): c[3], (0, 4): c[5], (2, 4): c[7], (4, 4): c[9]}
+    ph = np.radians(c[10])
+    R = np.array([[np.cos(ph), -np.sin(ph)], [np.sin(ph), np.cos(ph)]])
+    Sx, Sy, Rs = np.diag([c[11], 1.0]), np.diag([1.0, c[12]]), np.diag([c[13], 1.0])
+    rsp = R @ Sx @ Sy @ Rs
+    par = Rs @ R
+    w, h = 3.6, 2.4
+    rr = np.hypot(w, h) / 2
+    for x, y in [(0.3, -0.2), (-0.35, 0.25), (0.01, 0.02), (0.4, 0.4)]:
+        p = np.linalg.solve(par, [x * w / rr, y * h / rr])
+        r, phi = np.hypot(*p), np.arctan2(p[1], p[0])
+        qx = sum(v * np.cos(k[0] * phi) * r ** k[1] for k, v in cx.items())
+        qy = sum(v * np.cos(k[0] * phi) * r ** k[1] for k, v in cy.items())
+        o = rsp @ [p[0] * qx, p[1] * qy]
+        got = oracle.lens_anamorphic_undistort(c, x, y)
+        assert got == pytest.approx((o[0] * rr / w, o[1] * rr / h), abs=1e-12)
+
+
 def test_bound_transforms(oracle):
     from mayamatchmovesolver_amd.problem import (FLOAT_MAX, param_external_to_internal,
                                                  param_internal_to_external)
