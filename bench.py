@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--lens-model", default="classic",
-                    choices=["classic", "radial", "anamorphic", "anamorphic_rescaled"],
+                    choices=["classic", "classic_animated", "radial", "anamorphic",
+                             "anamorphic_rescaled"],
                     help="configs[4] lens model (classic = the C5 spec)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)

@@ -249,7 +249,9 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
     ``lens_model`` (configs[4] only): "classic" (the C5 spec), "radial" (the
     same scene through a 3DE radial decentered deg 4 cylindric lens, degree-2
     and degree-4 distortion solved), "anamorphic" / "anamorphic_rescaled"
-    (3DE anamorphic deg 4 rotate squeeze xy [rescaled], cx02 / cy02 solved):
+    (3DE anamorphic deg 4 rotate squeeze xy [rescaled], cx02 / cy02 solved),
+    "classic_animated" (the classic lens with its distortion animated, one
+    parameter per frame):
     SURVEY 8(f) row 2.
     """
     rng = np.random.Generator(np.random.PCG64(20241008 + index))
@@ -527,6 +529,8 @@ def _config_c5(rng, F, scale, lens_model="classic"):
         lens_true = (0.05, 1.0, 0.0, 0.0, 0.01)
         distort = _lens_distort_truth
         lens = {"init": (0.0, 1.0, 0.0, 0.0, 0.0), "solve_slots": (0, 4)}
+        if lens_model == "classic_animated":  # distortion keyed per frame (F params)
+            lens["init"] = (np.zeros(F),) + lens["init"][1:]
 
     def proj(ks, fs):
         mx = np.empty(ks.size)

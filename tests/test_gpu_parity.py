@@ -81,8 +81,8 @@ def test_measure_and_jacobian_small(mode, oracle, gpu_ctx):
         s.close()
 
 
-@pytest.mark.parametrize("lens_model", ["classic", "radial", "anamorphic",
-                                        "anamorphic_rescaled"])
+@pytest.mark.parametrize("lens_model", ["classic", "classic_animated", "radial",
+                                        "anamorphic", "anamorphic_rescaled"])
 def test_measure_and_jacobian_lens(lens_model, oracle, gpu_ctx):
     """Residuals (1e-12) and FD Jacobian (1e-7 of its max entry) through each
     lens model, lens coefficients solved (SURVEY 8(f) row 2 for "radial")."""
@@ -116,6 +116,7 @@ SMALL_CONFIGS = [
     (4, dict(frames=24, scale=0.2, lens_model="radial")),
     (4, dict(frames=8, scale=0.05, lens_model="anamorphic")),  # 3DE anamorphic std deg 4
     (4, dict(frames=24, scale=0.2, lens_model="anamorphic_rescaled")),
+    (4, dict(frames=8, scale=0.05, lens_model="classic_animated")),  # animated lens attr
 ]
 
 
