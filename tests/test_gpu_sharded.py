@@ -113,3 +113,25 @@ def test_sharded_ba_three_shards_structure(solve, gpu_ctx, monkeypatch):
         assert g.result[k] == ref.result[k], k
     np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-5)
     assert np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3)) <= 1e-4
+
+
+@pytest.mark.parametrize("nshards", [4, 8])
+def test_sharded_ba_many_shards(nshards, gpu_ctx):
+    """The shard counts the 1/2/4/8-GPU bench runs (default BCR reduced solve),
+    on a bundle-Schur scene with 12 frames per shard, against the unsharded
+    GPU solve: every shard agrees bit for bit, same reason, trace within 1e-5,
+    x within 1e-4 (the structural bar of the three-shard test above)."""
+    prob = S.make_config(3, frames=12 * nshards, scale=0.0015 * nshards, **WC)
+    opt = S.config_options(prob)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        ref = s.solve()
+    finally:
+        s.close()
+    outs = run_sharded(prob, opt, nshards)
+    check_shards_agree(outs)
+    g = outs[0]
+    assert g.result["reason_number"] == ref.result["reason_number"]
+    n = min(len(g.fnorm_trace), len(ref.fnorm_trace))
+    np.testing.assert_allclose(g.fnorm_trace[:n], ref.fnorm_trace[:n], rtol=1e-5)
+    assert np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3)) <= 1e-4
