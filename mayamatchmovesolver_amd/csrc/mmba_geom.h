@@ -101,12 +101,11 @@ MMBA_DEV void trs_matrix(double tx, double ty, double tz, double rx, double ry,
                          double rz, double sx, double sy, double sz, int roo,
                          double *out) {
     double srx, crx, sry, cry, srz, crz;
-    srx = sin(rx * DEG2RAD);
-    crx = cos(rx * DEG2RAD);
-    sry = sin(ry * DEG2RAD);
-    cry = cos(ry * DEG2RAD);
-    srz = sin(rz * DEG2RAD);
-    crz = cos(rz * DEG2RAD);
+    // one shared argument reduction per angle (the camera-record chain is
+    // one thread's serial fp64 stream: k_records is latency-bound)
+    sincos(rx * DEG2RAD, &srx, &crx);
+    sincos(ry * DEG2RAD, &sry, &cry);
+    sincos(rz * DEG2RAD, &srz, &crz);
     const double RX[16] = {1, 0, 0, 0, 0, crx, -srx, 0, 0, srx, crx, 0, 0, 0, 0, 1};
     const double RY[16] = {cry, 0, sry, 0, 0, 1, 0, 0, -sry, 0, cry, 0, 0, 0, 0, 1};
     const double RZ[16] = {crz, -srz, 0, 0, srz, crz, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
