@@ -297,6 +297,16 @@ int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out,
                       double *err_user_out, double *err_dist_out,
                       double *avg_min_max_out /* [3] */);
 
+/* Per-observation reprojection at internal parameters x (NULL: the problem's
+ * x0): the lens-distorted reprojected point and the film-fit corrected
+ * marker, [2*num_obs] each in observation order -- the out_point_list /
+ * out_marker_list pair FlatScene::evaluate produces
+ * (lib/rust/mmscenegraph/src/scene/flat.rs:271-356) and measureErrors
+ * compares (adjust_measureErrors.cpp:444-472); |marker - point| * imageWidth
+ * is err_user of mmba_plan_measure.  Either output may be NULL. */
+int mmba_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
+                        double *marker_xy_out);
+
 /* Reference-layout Jacobian at internal parameters x (the fjac the reference
  * builds in solveFunc_calculateJacobianMatrix, adjust_solveFunc.cpp:482-525):
  * column-major num_residuals x num_params, ldfjac = num_residuals.  Dense

@@ -61,6 +61,8 @@ def lib():
         L.mmba_plan_destroy.argtypes = [C.c_void_p]
         L.mmba_plan_measure.restype = C.c_int
         L.mmba_plan_measure.argtypes = [C.c_void_p, dp, dp, dp, dp, dp]
+        L.mmba_plan_reproject.restype = C.c_int
+        L.mmba_plan_reproject.argtypes = [C.c_void_p, dp, dp, dp]
         L.mmba_plan_jacobian.restype = C.c_int
         L.mmba_plan_jacobian.argtypes = [C.c_void_p, dp, dp]
         L.mmba_plan_solve.restype = C.c_int

@@ -195,6 +195,7 @@ EXPORTED_SYMBOLS = [
     "mmba_comm_destroy",
     "mmba_plan_create_sharded",
     "mmba_plan_measure",
+    "mmba_plan_reproject",
     "mmba_plan_jacobian",
     "mmba_plan_solve",
     "mmba_solve",

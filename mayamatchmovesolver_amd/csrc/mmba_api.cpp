@@ -176,6 +176,15 @@ int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out, double
     })
 }
 
+int mmba_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
+                        double *marker_xy_out) {
+    if (!plan) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        return plan->impl.reproject(x, point_xy_out, marker_xy_out);
+    })
+}
+
 int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac) {
     if (!plan || !x || !fjac) return MMBA_ERR_INVALID;
     MMBA_GUARD({

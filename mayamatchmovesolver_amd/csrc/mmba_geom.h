@@ -500,15 +500,35 @@ struct Resid {
     double dist;      // errorDistanceList
 };
 
+// Reprojected point of a bundle position through a camera record
+// (reprojection.rs:28-63: P C^-1 b, / w, x 0.5), before the lens.
+MMBA_DEV void project_point(const double *rec, const double *bp, double &point_x,
+                            double &point_y) {
+    double sp0 = rec[0] * bp[0] + rec[1] * bp[1] + rec[2] * bp[2] + rec[3];
+    double sp1 = rec[4] * bp[0] + rec[5] * bp[1] + rec[6] * bp[2] + rec[7];
+    double sp3 = rec[8] * bp[0] + rec[9] * bp[1] + rec[10] * bp[2] + rec[11];
+    point_x = (sp0 / sp3) * 0.5;
+    point_y = (sp1 / sp3) * 0.5;
+}
+
+// Lens distortion of a reprojected point; a non-finite result keeps the
+// undistorted coordinate (adjust_measureErrors.cpp:466-472).
+MMBA_DEV void distort_point(int lens_type, const double *lens, double &point_x,
+                            double &point_y) {
+    if (lens_type != MMBA_LENS_NONE) {
+        double ox, oy;
+        lens_distort(lens_type, lens, point_x, point_y, ox, oy);
+        if (isfinite(ox)) point_x = ox;
+        if (isfinite(oy)) point_y = oy;
+    }
+}
+
 // One observation's residual from a camera record and a bundle position.
 MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, double mkr_y,
                         double sqrtw, int mode, double image_width, int lens_type,
                         const double *lens) {
-    double sp0 = rec[0] * bp[0] + rec[1] * bp[1] + rec[2] * bp[2] + rec[3];
-    double sp1 = rec[4] * bp[0] + rec[5] * bp[1] + rec[6] * bp[2] + rec[7];
-    double sp3 = rec[8] * bp[0] + rec[9] * bp[1] + rec[10] * bp[2] + rec[11];
-    double point_x = (sp0 / sp3) * 0.5;
-    double point_y = (sp1 / sp3) * 0.5;
+    double point_x, point_y;
+    project_point(rec, bp, point_x, point_y);
     mkr_x *= rec[18];
     mkr_y *= rec[19];
     double factor = 1.0;
@@ -518,12 +538,7 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
         double dot = rec[15] * (bd0 / bl) + rec[16] * (bd1 / bl) + rec[17] * (bd2 / bl);
         if (dot < 0.0) factor = 1e+6;
     }
-    if (lens_type != MMBA_LENS_NONE) {
-        double ox, oy;
-        lens_distort(lens_type, lens, point_x, point_y, ox, oy);
-        if (isfinite(ox)) point_x = ox;
-        if (isfinite(oy)) point_y = oy;
-    }
+    distort_point(lens_type, lens, point_x, point_y);
     double dx = fabs(mkr_x - point_x), dy = fabs(mkr_y - point_y);
     double dxp = dx * image_width, dyp = dy * image_width;
     Resid r;

@@ -47,6 +47,8 @@ void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
 int residual_blocks(const DevProblem &P);
 // Reductions: with a ticket (a zero-initialised device counter) the partial
 // sums are combined inside the same launch, otherwise by a second kernel.
+void launch_reproject(hipStream_t s, const DevProblem &P, const double *recs, double *pts,
+                      double *mkr);
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out = nullptr,
                      unsigned int *ticket = nullptr);

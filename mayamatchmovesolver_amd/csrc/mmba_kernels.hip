@@ -2110,6 +2110,34 @@ void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, dou
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr);
     if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, nblk(P.M, 256), out);
 }
+// Per-observation reprojection (FlatScene::evaluate's out_point_list /
+// out_marker_list, the pair measureErrors compares): the lens-distorted point
+// and the film-fit corrected marker, device order.  Records must be current.
+__global__ void __launch_bounds__(256) k_reproject(DevProblem P, const double *__restrict__ recs,
+                                                   double *pts, double *mkr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    const int cf = P.obs_cf[i], b = P.obs_bnd[i], fr = P.obs_frame[i], cam = P.obs_cam[i];
+    const Override none{-1, 0.};
+    double bp[3];
+    base_bundle(P, b, fr, bp);
+    double lc[MMBA_LENS_NUM_ATTRS];
+    int lens = -1;
+    const int hl = obs_lens(P, cam, lens);
+    if (hl) lens_coeffs(P, lens, fr, none, lc);
+    const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
+    double px, py;
+    project_point(rec, bp, px, py);
+    distort_point(hl, lc, px, py);
+    pts[2 * i] = px;
+    pts[2 * i + 1] = py;
+    mkr[2 * i] = P.obs_xy[2 * i] * rec[18];
+    mkr[2 * i + 1] = P.obs_xy[2 * i + 1] * rec[19];
+}
+void launch_reproject(hipStream_t s, const DevProblem &P, const double *recs, double *pts,
+                      double *mkr) {
+    if (P.M > 0) k_reproject<<<nblk(P.M, 256), 256, 0, s>>>(P, recs, pts, mkr);
+}
 void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,

@@ -495,6 +495,21 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
     return MMBA_OK;
 }
 
+// Per-observation reprojected point and corrected marker at x (caller's
+// observation order); the scratch trial buffers carry them (no solve runs).
+int Plan::reproject(const double *x, double *point_out, double *marker_out) {
+    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    if (x) {
+        MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
+        fun(d_x, d_f, d_eu, d_ed);  // parameters set, records current
+    } else {
+        launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+    }
+    launch_reproject(s, P, d_recs, d_ftrial, d_eu_s);
+    download_ref_order(d_ftrial, d_eu_s, d_ed_s, point_out, marker_out, nullptr);
+    return MMBA_OK;
+}
+
 // Dense reference-order Jacobian at x (column-major, ldfjac = m); for tests
 // and small problems only.
 int Plan::dense_jacobian(const double *x, double *fjac) {

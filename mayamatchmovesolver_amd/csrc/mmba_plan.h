@@ -259,6 +259,7 @@ struct Plan {
     int solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
               mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace);
     int dense_jacobian(const double *x, double *fjac);
+    int reproject(const double *x, double *point_out, double *marker_out);
     int measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
                 double *stats);
     void download_params(const double *dx, double *x_out);

@@ -171,6 +171,16 @@ class Solver:
         check(lib().mmba_plan_measure(self._h, _dp(xx), _dp(fvec), _dp(eu), _dp(ed), _dp(st)))
         return fvec, eu, ed, st
 
+    def reproject(self, x=None):
+        """Per-observation reprojected (lens-distorted) point and film-fit
+        corrected marker at internal parameters x (``mmba_plan_reproject``):
+        two [2M] arrays in observation order."""
+        M = self.problem.num_obs
+        pts, mkr = np.zeros(2 * M), np.zeros(2 * M)
+        xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+        check(lib().mmba_plan_reproject(self._h, _dp(xx), _dp(pts), _dp(mkr)))
+        return pts, mkr
+
     def jacobian(self, x):
         """Dense reference-layout Jacobian (m x n) at internal parameters x."""
         p = self.problem

@@ -1032,6 +1032,7 @@ typedef struct {
     double *xa, *xb, *ea, *eb; /* FD scratch */
     mmba_trace *trace;
     int interrupted;
+    double *obs_pts, *obs_mkr; /* optional: reprojected point / corrected marker [2M] */
 } ref_scene;
 
 static double attr_value(const ref_scene *s, int a, int f, double dflt) {
@@ -1233,6 +1234,12 @@ static void measure(ref_scene *s, const char *frame_mask, double *errors) {
             if (dot < 0.0) factor = 1e+6;
         }
         apply_lens(s, c, f, &point_x, &point_y);
+        if (s->obs_pts) {
+            s->obs_pts[2 * i] = point_x;
+            s->obs_pts[2 * i + 1] = point_y;
+            s->obs_mkr[2 * i] = mkr_x;
+            s->obs_mkr[2 * i + 1] = mkr_y;
+        }
         double w = sqrt(p->obs_weight[i]);
         double dx = fabs(mkr_x - point_x), dy = fabs(mkr_y - point_y);
         double dxp = dx * image_width, dyp = dy * image_width;
@@ -1444,6 +1451,27 @@ int ref_measure(const mmba_problem *prob, const mmba_options *opt,
     if (avg_min_max)
         error_stats(s.err_dist, prob->num_obs, &avg_min_max[0], &avg_min_max[1], &avg_min_max[2]);
     free(f);
+    scene_free(&s);
+    return MMBA_OK;
+}
+
+/* Per-observation reprojection (the out_point_list / out_marker_list of
+ * FlatScene::evaluate, flat.rs:271-356, and the point / marker pair
+ * measureErrors compares, adjust_measureErrors.cpp:444-472), lens applied. */
+int ref_reproject_obs(const mmba_problem *prob, const mmba_options *opt, const double *x,
+                      double *point_xy, double *marker_xy) {
+    int rc = validate(prob, opt);
+    if (rc) return rc;
+    ref_scene s;
+    scene_init(&s, prob, opt);
+    const int m = 2 * prob->num_obs;
+    double *f = (double *)malloc(sizeof(double) * m);
+    s.obs_pts = point_xy;
+    s.obs_mkr = marker_xy;
+    if (x) set_parameters(&s, x);
+    measure(&s, NULL, f);
+    free(f);
+    s.obs_pts = s.obs_mkr = NULL;
     scene_free(&s);
     return MMBA_OK;
 }

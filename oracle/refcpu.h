@@ -82,6 +82,8 @@ void ref_lens_3de_anamorphic_undistort(const double coeff[14], double x, double 
                                        double *out_x, double *out_y);
 
 /* ---- full solve through the same mmba_problem layout ---- */
+int ref_reproject_obs(const mmba_problem *prob, const mmba_options *opt, const double *x,
+                      double *point_xy, double *marker_xy);
 int ref_measure(const mmba_problem *prob, const mmba_options *opt,
                 const double *x /* NULL = initial attr values */,
                 double *fvec, double *err_user, double *err_dist,

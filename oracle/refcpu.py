@@ -62,6 +62,9 @@ def lib():
         L.ref_measure.restype = C.c_int
         L.ref_measure.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions), dp, dp,
                                   dp, dp, dp]
+        L.ref_reproject_obs.restype = C.c_int
+        L.ref_reproject_obs.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions),
+                                        dp, dp, dp]
         L.ref_solve.restype = C.c_int
         L.ref_solve.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions), dp, dp,
                                 dp, dp, C.POINTER(abi.MmbaResult), C.POINTER(abi.MmbaTrace)]
@@ -230,6 +233,20 @@ def measure(problem, options, x=None):
     if rc != 0:
         raise RuntimeError("ref_measure failed rc=%d" % rc)
     return fvec, eu, ed, st
+
+
+def reproject_obs(problem, options, x=None):
+    """Per-observation reprojected point and film-fit corrected marker
+    (each [2M], observation order)."""
+    p, keep = problem.to_ctypes()
+    M = problem.num_obs
+    pts, mkr = np.zeros(2 * M), np.zeros(2 * M)
+    xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+    rc = lib().ref_reproject_obs(C.byref(p), C.byref(options), None if xx is None else _dp(xx),
+                                 _dp(pts), _dp(mkr))
+    if rc != 0:
+        raise RuntimeError("ref_reproject_obs failed rc=%d" % rc)
+    return pts, mkr
 
 
 def jacobian(problem, options, x):

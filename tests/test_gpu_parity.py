@@ -137,3 +137,27 @@ def test_reduced_system_dense_and_tiled(dense, oracle, gpu_ctx, monkeypatch):
     prob = S.make_config(2, frames=8, scale=0.002)
     opt = S.config_options(prob)
     check_solve(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("mode", [abi.SCENE_GRAPH_MODE_MAYA_DAG,
+                                  abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH])
+@pytest.mark.parametrize("idx,kw", [(3, dict(frames=8, scale=0.001)),
+                                    (4, dict(frames=8, scale=0.05)),
+                                    (4, dict(frames=8, scale=0.05, lens_model="radial")),
+                                    (4, dict(frames=8, scale=0.05,
+                                             lens_model="anamorphic_rescaled"))])
+def test_reproject_matches_oracle(idx, kw, mode, oracle, gpu_ctx):
+    """mmba_plan_reproject (SURVEY 8(f) row 4, the FlatScene::evaluate point /
+    marker lists): reprojected point and corrected marker per observation,
+    1e-12, at x0 and at a moved x."""
+    prob = S.make_config(idx, **kw)
+    opt = S.config_options(prob, scene_graph_mode=mode)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        for x in (None, prob.x0 + 0.002):
+            pts, mkr = s.reproject(x)
+            pr, mr = oracle.reproject_obs(prob, opt, x)
+            np.testing.assert_allclose(pts, pr, rtol=1e-12, atol=1e-14)
+            np.testing.assert_allclose(mkr, mr, rtol=1e-15, atol=0)
+    finally:
+        s.close()

@@ -52,3 +52,17 @@ def test_lens_scene_recovers_coefficients(oracle, lens_model, kind, truth):
     ext = prob.external_params(x)
     assert abs(ext[0] - truth[0]) < 2e-3 and abs(ext[1] - truth[1]) < 3e-3, ext[:2]
     assert trace[-1] < 0.02 * trace[0]
+
+
+@pytest.mark.parametrize("mode", [abi.SCENE_GRAPH_MODE_MAYA_DAG,
+                                  abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH])
+@pytest.mark.parametrize("lens_model", ["classic", "anamorphic"])
+def test_reproject_is_the_measured_pair(oracle, mode, lens_model):
+    """ref_reproject_obs returns the point / marker pair measureErrors compares:
+    |marker - point| * imageWidth is errorList (behind-camera factor 1 here)."""
+    prob = S.make_config(4, frames=8, scale=0.05, lens_model=lens_model)
+    opt = S.config_options(prob, scene_graph_mode=mode)
+    x = prob.x0 + 0.003
+    pts, mkr = oracle.reproject_obs(prob, opt, x)
+    _, eu, _, _ = oracle.measure(prob, opt, x)
+    np.testing.assert_allclose(np.abs(mkr - pts) * opt.image_width, eu, rtol=1e-15, atol=0)
