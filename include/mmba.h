@@ -325,6 +325,18 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out,
                     mmba_result *res, const mmba_callbacks *cb,
                     mmba_trace *trace);
 
+/* Per-frame solve mode (FrameSolveMode::kPerFrame, adjust_base.cpp:1430-1484):
+ * one LM solve per frame over that frame's observations and the parameters
+ * keyed at it plus every static parameter, x_inout updated frame by frame;
+ * results[num_frames] gets each frame's SolverResult.  Without static
+ * parameters the frames are independent and up to max_concurrency of them
+ * run at once (one stream each); with one they run in order, as in the
+ * reference.  The first frame with no parameters or fewer residuals than
+ * parameters stops the sequence (later frames: success = 0). */
+int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
+                         const mmba_options *opt, double *x_inout,
+                         mmba_result *results /* [num_frames] */, int32_t max_concurrency);
+
 /* One-shot convenience: plan_create + plan_solve + plan_destroy. */
 int mmba_solve(mmba_context *ctx, const mmba_problem *prob,
                const mmba_options *opt, double *x_inout, double *fvec_out,

@@ -1,0 +1,140 @@
+// mmba_perframe.cpp -- per-frame solve mode (FrameSolveMode::kPerFrame,
+// src/mmSolver/adjust/adjust_base.cpp:1430-1484): one solveFrames call per
+// frame, each over that frame's observations and the parameters of that frame
+// (animated attributes keyed at it) plus every static parameter.
+//
+// The reference runs the frames one after another.  When no static parameter
+// is solved the frames share nothing, so here they run concurrently: a pool
+// of host threads, each with its own context (stream) and one plan per frame,
+// all on the caller's device -- many small launch-bound LM solves overlap on
+// the GPU instead of queueing behind each other.  With a static parameter the
+// frames are chained exactly as in the reference (frame i starts from the
+// static values frame i - 1 left), so they run in order.
+//
+// Like the reference loop (":1471-1476 Failed to solve frame, stopping
+// solve"), the first frame that cannot be solved (fewer residuals than
+// parameters, no parameters) stops the sequence: later frames are left
+// untouched and report success = 0, reason_number = 0.
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
+#include "mmba_plan.h"
+
+namespace {
+
+// The sub-problem of one frame: the caller's arrays except the observation
+// and parameter lists, which are filtered (order kept: observations stay
+// marker-major, parameters attr-major).
+struct FrameProblem {
+    std::vector<int32_t> obs_marker, obs_frame, param_attr, param_frame;
+    std::vector<double> obs_xy, obs_weight, pmin, pmax, poff, pscale;
+    std::vector<int> params;  // indices into the full parameter vector
+    mmba_problem p{};
+
+    void build(const mmba_problem &full, int f) {
+        p = full;
+        for (int i = 0; i < full.num_obs; ++i) {
+            if (full.obs_frame[i] != f) continue;
+            obs_marker.push_back(full.obs_marker[i]);
+            obs_frame.push_back(f);
+            obs_xy.push_back(full.obs_xy[2 * i]);
+            obs_xy.push_back(full.obs_xy[2 * i + 1]);
+            obs_weight.push_back(full.obs_weight[i]);
+        }
+        for (int j = 0; j < full.num_params; ++j) {
+            if (full.param_frame[j] != f && full.param_frame[j] != -1) continue;
+            params.push_back(j);
+            param_attr.push_back(full.param_attr[j]);
+            param_frame.push_back(full.param_frame[j]);
+            pmin.push_back(full.param_min[j]);
+            pmax.push_back(full.param_max[j]);
+            poff.push_back(full.param_offset[j]);
+            pscale.push_back(full.param_scale[j]);
+        }
+        p.num_obs = (int32_t)obs_marker.size();
+        p.obs_marker = obs_marker.data();
+        p.obs_frame = obs_frame.data();
+        p.obs_xy = obs_xy.data();
+        p.obs_weight = obs_weight.data();
+        p.num_params = (int32_t)params.size();
+        p.param_attr = param_attr.data();
+        p.param_frame = param_frame.data();
+        p.param_min = pmin.data();
+        p.param_max = pmax.data();
+        p.param_offset = poff.data();
+        p.param_scale = pscale.data();
+    }
+    bool solvable() const { return p.num_params > 0 && p.num_params <= 2 * p.num_obs; }
+};
+
+// One frame: plan, solve from the current x, write the frame's parameters back.
+int solve_frame(mmba_context *ctx, FrameProblem &fp, const mmba_options *opt, double *x,
+                mmba_result *res) {
+    const int n = fp.p.num_params, m = 2 * fp.p.num_obs;
+    std::vector<double> xs(n), fvec(m), eu(m), ed(fp.p.num_obs);
+    for (int k = 0; k < n; ++k) xs[k] = x[fp.params[k]];
+    mmba_plan *plan = nullptr;
+    int rc = mmba_plan_create(ctx, &fp.p, opt, &plan);
+    if (rc != MMBA_OK) return rc;
+    rc = mmba_plan_solve(plan, xs.data(), fvec.data(), eu.data(), ed.data(), res, nullptr,
+                         nullptr);
+    mmba_plan_destroy(plan);
+    if (rc != MMBA_OK && rc != MMBA_ERR_INTERRUPTED) return rc;
+    for (int k = 0; k < n; ++k) x[fp.params[k]] = xs[k];
+    return rc;
+}
+
+}  // namespace
+
+extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
+                                    const mmba_options *opt, double *x_inout,
+                                    mmba_result *results, int32_t max_concurrency) {
+    if (!ctx || !prob || !opt || !x_inout || !results || prob->num_frames <= 0)
+        return MMBA_ERR_INVALID;
+    const int F = prob->num_frames;
+    std::vector<FrameProblem> fr(F);
+    bool chained = false;
+    for (int j = 0; j < prob->num_params; ++j) chained |= prob->param_frame[j] < 0;
+    int nf = F;  // frames before the first unsolvable one
+    for (int f = 0; f < F; ++f) {
+        results[f] = mmba_result{};
+        if (f < nf) {
+            fr[f].build(*prob, f);
+            if (!fr[f].solvable()) nf = f;
+        }
+    }
+    const int workers = chained ? 1 : std::max(1, std::min<int>(max_concurrency, nf));
+    if (workers == 1) {
+        for (int f = 0; f < nf; ++f) {
+            const int rc = solve_frame(ctx, fr[f], opt, x_inout, &results[f]);
+            if (rc != MMBA_OK) return rc;
+        }
+        return MMBA_OK;
+    }
+    // independent frames: disjoint parameter sets, so the threads write
+    // disjoint entries of x_inout
+    std::atomic<int> next{0}, first_err{MMBA_OK};
+    auto work = [&]() {
+        mmba_context *c = nullptr;
+        int rc = mmba_context_create(ctx->device, &c);
+        if (rc != MMBA_OK) {
+            int ok = MMBA_OK;
+            first_err.compare_exchange_strong(ok, rc);
+            return;
+        }
+        for (int f; (f = next.fetch_add(1)) < nf && first_err.load() == MMBA_OK;) {
+            rc = solve_frame(c, fr[f], opt, x_inout, &results[f]);
+            if (rc != MMBA_OK) {
+                int ok = MMBA_OK;
+                first_err.compare_exchange_strong(ok, rc);
+            }
+        }
+        mmba_context_destroy(c);
+    };
+    std::vector<std::thread> pool;
+    for (int w = 0; w < workers; ++w) pool.emplace_back(work);
+    for (auto &t : pool) t.join();
+    return first_err.load();
+}

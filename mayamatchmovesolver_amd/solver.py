@@ -219,6 +219,23 @@ def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
         s.close()
 
 
+def solve_per_frame(problem: Problem, options, x0=None, device: int = 0,
+                    max_concurrency: int = 8):
+    """Per-frame solve mode (``mmba_solve_per_frame``; FrameSolveMode::kPerFrame,
+    adjust_base.cpp:1430-1484).  Returns (x, [per-frame result dicts])."""
+    p, keep = problem.to_ctypes()
+    x = np.array(problem.x0 if x0 is None else x0, dtype=np.float64)
+    F = problem.num_frames
+    res = (abi.MmbaResult * F)()
+    ctx = Context(device)
+    try:
+        check(lib().mmba_solve_per_frame(ctx.handle, C.byref(p), C.byref(options), _dp(x),
+                                         res, int(max_concurrency)))
+    finally:
+        ctx.close()
+    return x, [r.as_dict() for r in res]
+
+
 def shard_layout(problem: Problem, nranks: int):
     """Frame partition a sharded plan of `problem` uses (host only): returns
     (bounds[nranks + 1], bundle_owner[num_bundles]); shard k owns frames
