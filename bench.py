@@ -54,6 +54,9 @@ def parse():
                     choices=["classic", "classic_animated", "radial", "anamorphic",
                              "anamorphic_rescaled"],
                     help="configs[4] lens model (classic = the C5 spec)")
+    ap.add_argument("--per-frame", type=int, default=0, metavar="CONC",
+                    help="per-frame solve mode (mmba_solve_per_frame) with CONC frames at "
+                         "once; prints its own JSON line (not the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-traffic", action="store_true",
@@ -195,8 +198,40 @@ def cpu_baseline(cfg_index, budget_s):
             "sample": desc, "t_iter_s_extrapolated": t_iter_full}
 
 
+def per_frame_line(args):
+    """Per-frame solve mode (FrameSolveMode::kPerFrame) over the config's
+    frames, CONC frame solves in flight: residuals/s over all frame solves."""
+    from mayamatchmovesolver_amd import synthetic as S
+    from mayamatchmovesolver_amd.solver import solve_per_frame
+    kw = {"lens_model": args.lens_model} if args.config == 4 else {}
+    prob = S.make_config(args.config, frames=args.frames, scale=args.scale, **kw)
+    opt = S.config_options(prob)
+    obs_per_frame = np.bincount(np.asarray(prob.obs_frame), minlength=prob.num_frames)
+    for _ in range(args.warmup):
+        solve_per_frame(prob, opt, max_concurrency=args.per_frame)
+    t0 = time.perf_counter()
+    resid = iters = 0
+    for _ in range(args.steps):
+        _, res = solve_per_frame(prob, opt, max_concurrency=args.per_frame)
+        for f, r in enumerate(res):
+            resid += int(obs_per_frame[f]) * (r["function_evals"] + r["outer_iterations"])
+            iters += r["outer_iterations"]
+    dt = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "per-frame solve mode residuals/s", "value": resid / dt,
+        "unit": "residuals/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "dtype": "f64",
+        "data": "synthetic", "config": {"workload": prob.meta.get("name"),
+                                        "frames": prob.num_frames,
+                                        "concurrent_frames": args.per_frame},
+        "lm_iterations_per_s": iters / dt, "frames_per_s": prob.num_frames * args.steps / dt}),
+        flush=True)
+
+
 def main():
     args = parse()
+    if args.per_frame:
+        return per_frame_line(args)
     world, rank, local, dist = dist_setup()
     # PMC passes first, as child processes, before this process initialises
     # the GPU (rank 0 of a 1-GPU run only)

@@ -220,7 +220,7 @@ def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
 
 
 def solve_per_frame(problem: Problem, options, x0=None, device: int = 0,
-                    max_concurrency: int = 8):
+                    max_concurrency: int = 1):
     """Per-frame solve mode (``mmba_solve_per_frame``; FrameSolveMode::kPerFrame,
     adjust_base.cpp:1430-1484).  Returns (x, [per-frame result dicts])."""
     p, keep = problem.to_ctypes()
