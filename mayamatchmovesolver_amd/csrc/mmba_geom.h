@@ -106,11 +106,14 @@ MMBA_DEV void trs_matrix(double tx, double ty, double tz, double rx, double ry,
     sincos(rx * DEG2RAD, &srx, &crx);
     sincos(ry * DEG2RAD, &sry, &cry);
     sincos(rz * DEG2RAD, &srz, &crz);
-    const double RX[16] = {1, 0, 0, 0, 0, crx, -srx, 0, 0, srx, crx, 0, 0, 0, 0, 1};
-    const double RY[16] = {cry, 0, sry, 0, 0, 1, 0, 0, -sry, 0, cry, 0, 0, 0, 0, 1};
-    const double RZ[16] = {crz, -srz, 0, 0, srz, crz, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    const double S[16] = {sx, 0, 0, 0, 0, sy, 0, 0, 0, 0, sz, 0, 0, 0, 0, 1};
-    const double T[16] = {1, 0, 0, tx, 0, 1, 0, ty, 0, 0, 1, tz, 0, 0, 0, 1};
+    // The reference forms T * (a * b * c) * S as 4x4 products. Every term that
+    // 4x4 form adds beyond the 3x3 rotation block is an exact zero (x * 0,
+    // added last), and T, S only place t and scale columns, so the 3x3
+    // rotation products below, then column scaling, give the same doubles for
+    // finite inputs at a quarter of the arithmetic.
+    const double RX[9] = {1, 0, 0, 0, crx, -srx, 0, srx, crx};
+    const double RY[9] = {cry, 0, sry, 0, 1, 0, -sry, 0, cry};
+    const double RZ[9] = {crz, -srz, 0, srz, crz, 0, 0, 0, 1};
     const double *a, *b, *c;
     switch (roo) {
         default:
@@ -121,11 +124,31 @@ MMBA_DEV void trs_matrix(double tx, double ty, double tz, double rx, double ry,
         case MMBA_ROO_YXZ: a = RZ; b = RX; c = RY; break;
         case MMBA_ROO_ZYX: a = RX; b = RY; c = RZ; break;
     }
-    double R[16];
-    mat4_mul(a, b, R);
-    mat4_mul(R, c, R);
-    mat4_mul(T, R, out);
-    mat4_mul(out, S, out);
+    double AB[9], R[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            AB[r * 3 + k] = a[r * 3 + 0] * b[0 * 3 + k] + a[r * 3 + 1] * b[1 * 3 + k] +
+                            a[r * 3 + 2] * b[2 * 3 + k];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            R[r * 3 + k] = AB[r * 3 + 0] * c[0 * 3 + k] + AB[r * 3 + 1] * c[1 * 3 + k] +
+                           AB[r * 3 + 2] * c[2 * 3 + k];
+    const double s[3] = {sx, sy, sz};
+    const double t[3] = {tx, ty, tz};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) out[r * 4 + k] = R[r * 3 + k] * s[k];
+        out[r * 4 + 3] = t[r];
+    }
+    out[12] = 0.;
+    out[13] = 0.;
+    out[14] = 0.;
+    out[15] = 1.;
 }
 
 MMBA_DEV void local_matrix(const DevProblem &P, int t, int f, const Override &ov,
