@@ -97,6 +97,23 @@ MMBA_DEV void mat4_inverse(const double *m, double *out) {
     for (int i = 0; i < 16; ++i) out[i] = inv[i] * inv_det;
 }
 
+// R = (a * b) * c for 3x3 row-major rotation factors.
+MMBA_DEV void rot3_chain(const double *a, const double *b, const double *c, double *R) {
+    double AB[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            AB[r * 3 + k] = a[r * 3 + 0] * b[0 * 3 + k] + a[r * 3 + 1] * b[1 * 3 + k] +
+                            a[r * 3 + 2] * b[2 * 3 + k];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            R[r * 3 + k] = AB[r * 3 + 0] * c[0 * 3 + k] + AB[r * 3 + 1] * c[1 * 3 + k] +
+                           AB[r * 3 + 2] * c[2 * 3 + k];
+}
+
 MMBA_DEV void trs_matrix(double tx, double ty, double tz, double rx, double ry,
                          double rz, double sx, double sy, double sz, int roo,
                          double *out) {
@@ -114,29 +131,18 @@ MMBA_DEV void trs_matrix(double tx, double ty, double tz, double rx, double ry,
     const double RX[9] = {1, 0, 0, 0, crx, -srx, 0, srx, crx};
     const double RY[9] = {cry, 0, sry, 0, 1, 0, -sry, 0, cry};
     const double RZ[9] = {crz, -srz, 0, srz, crz, 0, 0, 0, 1};
-    const double *a, *b, *c;
+    // Each rotation order names its factors at compile time, so the factor
+    // arrays stay in registers (a runtime-selected pointer put them in scratch).
+    double R[9];
     switch (roo) {
         default:
-        case MMBA_ROO_XYZ: a = RZ; b = RY; c = RX; break;
-        case MMBA_ROO_YZX: a = RX; b = RZ; c = RY; break;
-        case MMBA_ROO_ZXY: a = RY; b = RX; c = RZ; break;
-        case MMBA_ROO_XZY: a = RY; b = RZ; c = RX; break;
-        case MMBA_ROO_YXZ: a = RZ; b = RX; c = RY; break;
-        case MMBA_ROO_ZYX: a = RX; b = RY; c = RZ; break;
+        case MMBA_ROO_XYZ: rot3_chain(RZ, RY, RX, R); break;
+        case MMBA_ROO_YZX: rot3_chain(RX, RZ, RY, R); break;
+        case MMBA_ROO_ZXY: rot3_chain(RY, RX, RZ, R); break;
+        case MMBA_ROO_XZY: rot3_chain(RY, RZ, RX, R); break;
+        case MMBA_ROO_YXZ: rot3_chain(RZ, RX, RY, R); break;
+        case MMBA_ROO_ZYX: rot3_chain(RX, RY, RZ, R); break;
     }
-    double AB[9], R[9];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            AB[r * 3 + k] = a[r * 3 + 0] * b[0 * 3 + k] + a[r * 3 + 1] * b[1 * 3 + k] +
-                            a[r * 3 + 2] * b[2 * 3 + k];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            R[r * 3 + k] = AB[r * 3 + 0] * c[0 * 3 + k] + AB[r * 3 + 1] * c[1 * 3 + k] +
-                           AB[r * 3 + 2] * c[2 * 3 + k];
     const double s[3] = {sx, sy, sz};
     const double t[3] = {tx, ty, tz};
 #pragma unroll
