@@ -1489,8 +1489,10 @@ __global__ void __launch_bounds__(64) k_schur_dest(DevProblem P, const double *_
 // robin to the 8 XCDs, so workgroup w takes destination
 // (w % 8) * ceil(ndest / 8) + w / 8 -- each XCD sweeps one contiguous band of
 // destinations and the W rows of its camera-frames stay in that XCD's L2.
+// Two waves per SIMD: C4's 1,992 destinations are ~2 waves per SIMD anyway, and
+// the 3-wave register cap spilled the prefetched W rows to scratch.
 template <int PC>
-__global__ void __launch_bounds__(64, 3) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
+__global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const double *__restrict__ W,
                                                      const int2 *__restrict__ dest,
                                                      const int *__restrict__ dest_off,
                                                      const int2 *__restrict__ pairs,
@@ -1747,14 +1749,22 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
     double L[3][3];
     for (int a = 0; a < 3; ++a)
         for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+    // compile-time indices under pb guards (same operation order): s, L and
+    // xb stay in registers instead of scratch
     double xb[3] = {0., 0., 0.};
-    for (int a = pb - 1; a >= 0; --a) {
+#pragma unroll
+    for (int a = 2; a >= 0; --a) {
+        if (a >= pb) continue;
         double t = s[a];
-        for (int k = a + 1; k < pb; ++k) t -= L[k][a] * xb[k];
+#pragma unroll
+        for (int k = a + 1; k < 3; ++k)
+            if (k < pb) t -= L[k][a] * xb[k];
         xb[a] = t / L[a][a];
     }
     const int po = P.bnd_par_off[b];
-    for (int a = 0; a < pb; ++a) x[P.bnd_par[po + a]] = xb[a];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        if (a < pb) x[P.bnd_par[po + a]] = xb[a];
 }
 
 // Reduced-system solution (R order) -> parameter order.
