@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out/r1_s7f
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r1_s7f/smoke.txt 2>&1 && \
+timeout -k 10 400 python -u bench.py > gpurun_out/r1_s7f/bench_default.json 2> gpurun_out/r1_s7f/bench_default.err
+echo "exit=$?"
