@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 1
+#define MMBA_ABI_VERSION 2
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -168,6 +168,36 @@ typedef struct mmba_problem {
     const double *param_max;      /* [num_params] Attr::getMaximumValue (+FLT_MAX = none) */
     const double *param_offset;   /* [num_params] Attr::getOffsetValue */
     const double *param_scale;    /* [num_params] Attr::getScaleValue  */
+
+    /* ---- ABI 2 ---- */
+    /* paramWeightList (adjust_base.cpp countUpNumberOfUnknownParameters), the
+     * `diag` lmder/lmdif read in mode 2 (auto_param_scale off,
+     * adjust_cminpack_lmder.cpp:103-106,151).  NULL = 1.0 for every parameter. */
+    const double *param_weight;   /* [num_params] */
+
+    /* Attribute stiffness and smoothness error rows
+     * (adjust_measureErrors.cpp:311-387; counted by countUpNumberOfErrors,
+     * adjust_relationships.cpp:184-215).  Row i of each list is
+     *   ((1 / gaussian(v, value, variance)) - 1) * weight,
+     *   gaussian(x, mean, sigma) = exp(-((x - mean)^2 / (2 sigma^2))),
+     * with v the attribute's current value (at `frame` for an animated
+     * attribute).  The rows follow the 2*num_obs marker rows: stiffness rows,
+     * then smoothness rows, exactly as the reference indexes errorList.  Pass
+     * the first num_stiff entries of stiffAttrsList (the reference indexes
+     * that list by row).  Only the Maya DAG path computes them: in MM Scene
+     * Graph mode they stay 0 (adjust_measureErrors.cpp:518). */
+    int32_t num_stiff;
+    const int32_t *stiff_attr;     /* [num_stiff] attribute id            */
+    const int32_t *stiff_frame;    /* [num_stiff] frame index (animated attrs; ignored for static) */
+    const double *stiff_weight;    /* [num_stiff] stiffness weight  (> 0)  */
+    const double *stiff_variance;  /* [num_stiff] stiffness variance       */
+    const double *stiff_value;     /* [num_stiff] stiffness value (mean)   */
+    int32_t num_smooth;
+    const int32_t *smooth_attr;
+    const int32_t *smooth_frame;
+    const double *smooth_weight;
+    const double *smooth_variance;
+    const double *smooth_value;
 } mmba_problem;
 
 /* SolverOptions subset that the LM path reads (adjust_data.h:133-185). */
@@ -183,9 +213,32 @@ typedef struct mmba_options {
     int32_t auto_param_scale; /* 1 -> MINPACK mode 1, else mode 2        */
     int32_t scene_graph_mode; /* MMBA_SCENE_GRAPH_*                      */
     double image_width;       /* pixels (default 2048)                   */
-    int32_t accept_only_better; /* restore x0 when error avg got worse   */
+    int32_t accept_only_better; /* report error_is_better against the initial error */
     int32_t log_level;        /* 0 error .. 4 debug                      */
+
+    /* ---- ABI 2 ---- */
+    /* Robust loss (applyLossFunctionToErrors, adjust_base.cpp:132-187), applied
+     * to every residual row only when robust_loss != 0, i.e. when the solver
+     * type supports it (SolverOptions::solverSupportsRobustLoss; false for
+     * both cminpack types, adjust_defines.h:122,141 -- so off by default). */
+    int32_t robust_loss;        /* solverSupportsRobustLoss                 */
+    int32_t robust_loss_type;   /* MMBA_ROBUST_LOSS_*                       */
+    double robust_loss_scale;
+    /* Initial measurement of solveFrames (adjust_base.cpp:1080-1103).
+     * 0 (default): the library measures the errors at the scene's current
+     * values before solving.  1: the caller already did; its average error
+     * distance is `initial_error_avg` (used for accept-only-better).  Every
+     * ABI-2 field is 0 in the reference behaviour, so a zeroed struct plus
+     * the ABI-1 fields keeps it. */
+    int32_t initial_error_given;
+    int32_t pad_opt0;
+    double initial_error_avg;
 } mmba_options;
+
+/* Robust loss types (adjust_defines.h:96-98). */
+#define MMBA_ROBUST_LOSS_TRIVIAL 0
+#define MMBA_ROBUST_LOSS_SOFT_L_ONE 1
+#define MMBA_ROBUST_LOSS_CAUCHY 2
 
 /* SolverResult mirror (adjust_results.h:59-72) plus run statistics. */
 typedef struct mmba_result {
@@ -211,8 +264,13 @@ typedef struct mmba_result {
     double time_linear_s;     /* Schur + Cholesky + solves                 */
 } mmba_result;
 
-/* Interrupt / progress callbacks, polled between LM iterations
- * (MComputation::isInterruptRequested, adjust_solveFunc.cpp:317-325). */
+/* Interrupt / progress callbacks.  `interrupt` is polled where the
+ * reference polls MComputation::isInterruptRequested: at every solveFunc call
+ * (each residual evaluation and each Jacobian request,
+ * adjust_solveFunc.cpp:567-571) and before every finite-difference column
+ * (:321-325); a non-zero return stops the solve with reason_number -1 and the
+ * counts the reference would report.  `progress` is called once per LM outer
+ * iteration with the Jacobian count.  Either pointer may be NULL. */
 typedef struct mmba_callbacks {
     int (*interrupt)(void *user);           /* non-zero -> stop */
     void (*progress)(void *user, int iter);
@@ -313,29 +371,42 @@ int mmba_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
  * output -- meant for tests and small problems. */
 int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac);
 
-/* Run the LM solve from internal parameters x_inout (replaces the
- * solve_3d_cminpack_* call inside solveFrames, including the initial
- * error measurement and accept-only-better logic of adjust_base.cpp:1080-1244).
- *   fvec_out     [num_residuals]   errorList (weighted, |dx|*imageWidth*sqrt(w))
- *   err_user_out [num_residuals]   ud->errorList (no weight)
+/* Run the LM solve from internal parameters x_inout: the
+ * solve_3d_cminpack_lmder / _lmdif call inside solveFrames, bracketed by the
+ * initial error measurement (adjust_base.cpp:1080-1103, unless
+ * opt->initial_measure == 0) and the accept-only-better test (:1208-1229).
+ *   x_inout      [num_params]      in: x0; out: the solved x, as lmder leaves
+ *                                  paramList.  res->error_is_better says
+ *                                  whether the caller should write it back
+ *                                  (:1231-1244) or keep x0.
+ *   fvec_out     [num_residuals]   errorList (weighted, |dx|*imageWidth*sqrt(w),
+ *                                  then the stiffness / smoothness rows)
+ *   err_user_out [num_residuals]   ud->errorList (no weight, no loss)
  *   err_dist_out [num_obs]         ud->errorDistanceList
- * num_residuals = 2*num_obs.  Any output may be NULL. */
+ * num_residuals = 2*num_obs + num_stiff + num_smooth.  Any output may be NULL. */
 int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out,
                     double *err_user_out, double *err_dist_out,
                     mmba_result *res, const mmba_callbacks *cb,
                     mmba_trace *trace);
 
 /* Per-frame solve mode (FrameSolveMode::kPerFrame, adjust_base.cpp:1430-1484):
- * one LM solve per frame over that frame's observations and the parameters
- * keyed at it plus every static parameter, x_inout updated frame by frame;
- * results[num_frames] gets each frame's SolverResult.  Without static
- * parameters the frames are independent and up to max_concurrency of them
- * run at once (one stream each); with one they run in order, as in the
- * reference.  The first frame with no parameters or fewer residuals than
- * parameters stops the sequence (later frames: success = 0). */
+ * one solveFrames per frame over that frame's observations and the
+ * parameters keyed at it plus every static parameter; results[num_frames]
+ * gets each frame's SolverResult and x_inout the parameters each frame's
+ * solveFrames writes back (the solved values when error_is_better, else the
+ * frame's starting values).  Without static parameters the frames share
+ * nothing and are solved together on the device by one batched LM (one
+ * workgroup per frame, MINPACK control flow per frame on the device); with
+ * one they are chained in order, as in the reference.  The first frame with
+ * no parameters or fewer residuals than parameters stops the sequence (later
+ * frames: success = 0).  cb->interrupt is polled before every frame batch;
+ * frames that start after it returned non-zero report reason_number -1
+ * without moving, as each solveFrames call of the reference does once the
+ * interrupt flag is set.  max_concurrency: frames per batch (0 = all). */
 int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
                          const mmba_options *opt, double *x_inout,
-                         mmba_result *results /* [num_frames] */, int32_t max_concurrency);
+                         mmba_result *results /* [num_frames] */, int32_t max_concurrency,
+                         const mmba_callbacks *cb);
 
 /* One-shot convenience: plan_create + plan_solve + plan_destroy. */
 int mmba_solve(mmba_context *ctx, const mmba_problem *prob,

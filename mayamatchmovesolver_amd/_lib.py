@@ -38,6 +38,9 @@ def lib():
             raise MmbaError(abi.MMBA_ERR_NO_DEVICE,
                             "libmmba.so not built (run __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
+        if L.mmba_abi_version() != abi.ABI_VERSION:
+            raise MmbaError(abi.MMBA_ERR_INVALID, "libmmba.so ABI %d, bindings expect %d "
+                            "(rebuild)" % (L.mmba_abi_version(), abi.ABI_VERSION))
         dp = C.POINTER(C.c_double)
         L.mmba_abi_version.restype = C.c_int
         L.mmba_device_count.restype = C.c_int
@@ -64,7 +67,7 @@ def lib():
         L.mmba_plan_reproject.restype = C.c_int
         L.mmba_solve_per_frame.restype = C.c_int
         L.mmba_solve_per_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, dp, C.c_void_p,
-                                           C.c_int32]
+                                           C.c_int32, C.POINTER(abi.MmbaCallbacks)]
         L.mmba_plan_reproject.argtypes = [C.c_void_p, dp, dp, dp]
         L.mmba_plan_jacobian.restype = C.c_int
         L.mmba_plan_jacobian.argtypes = [C.c_void_p, dp, dp]

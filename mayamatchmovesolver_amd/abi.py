@@ -19,6 +19,10 @@ SCENE_GRAPH_MODE_MAYA_DAG = 1
 SCENE_GRAPH_MODE_MM_SCENE_GRAPH = 2
 AUTO_DIFF_TYPE_FORWARD = 0
 AUTO_DIFF_TYPE_CENTRAL = 1
+ROBUST_LOSS_TYPE_TRIVIAL = 0
+ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
+ROBUST_LOSS_TYPE_CAUCHY = 2
+ABI_VERSION = 2
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -86,6 +90,20 @@ class MmbaProblem(C.Structure):
         ("param_max", _f64p),
         ("param_offset", _f64p),
         ("param_scale", _f64p),
+        # ABI 2
+        ("param_weight", _f64p),
+        ("num_stiff", C.c_int32),
+        ("stiff_attr", _i32p),
+        ("stiff_frame", _i32p),
+        ("stiff_weight", _f64p),
+        ("stiff_variance", _f64p),
+        ("stiff_value", _f64p),
+        ("num_smooth", C.c_int32),
+        ("smooth_attr", _i32p),
+        ("smooth_frame", _i32p),
+        ("smooth_weight", _f64p),
+        ("smooth_variance", _f64p),
+        ("smooth_value", _f64p),
     ]
 
 
@@ -104,6 +122,13 @@ class MmbaOptions(C.Structure):
         ("image_width", C.c_double),
         ("accept_only_better", C.c_int32),
         ("log_level", C.c_int32),
+        # ABI 2
+        ("robust_loss", C.c_int32),
+        ("robust_loss_type", C.c_int32),
+        ("robust_loss_scale", C.c_double),
+        ("initial_error_given", C.c_int32),
+        ("pad_opt0", C.c_int32),
+        ("initial_error_avg", C.c_double),
     ]
 
 

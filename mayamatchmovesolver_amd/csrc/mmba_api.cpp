@@ -97,8 +97,8 @@ double mmba_param_internal_to_external(double value, double xmin, double xmax, d
 
 double mmba_param_external_to_internal(double value, double xmin, double xmax, double offset,
                                        double scale) {
-    value = value > xmin ? value : xmin;
-    value = value < xmax ? value : xmax;
+    value = (value < xmin) ? xmin : value;  // std::max<double>(value, xmin)
+    value = (xmax < value) ? xmax : value;  // std::min<double>(value, xmax)
     value = (value * scale) + offset;
     xmin = (xmin * scale) + offset;
     xmax = (xmax * scale) + offset;

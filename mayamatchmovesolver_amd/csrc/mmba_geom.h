@@ -579,6 +579,43 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
     return r;
 }
 
+// applyLossFunctionToErrors for one row (adjust_base.cpp:158-187), same
+// operation order as the reference (pow, log1p).
+MMBA_DEV double robust_loss(double f, int type, double scale) {
+    double z = pow(f / scale, 2);
+    double rho0 = z, rho1 = 1.0, rho2 = 0.0;
+    if (type == MMBA_ROBUST_LOSS_SOFT_L_ONE) {
+        double t = 1.0 + z;
+        rho0 = 2.0 * (pow(t, 0.5 - 1.0));
+        rho1 = pow(t, -0.5);
+        rho2 = -0.5 * pow(t, -1.5);
+    } else if (type == MMBA_ROBUST_LOSS_CAUCHY) {
+        rho0 = log1p(z);
+        double t = 1.0 + z;
+        rho1 = 1.0 / t;
+        rho2 = -1.0 / pow(t, 2.0);
+    }
+    (void)rho0;
+    rho2 /= pow(scale, 2.0);
+    double J_scale = rho1 + 2.0 * rho2 * pow(f, 2.0);
+    const double eps = 2.220446049250313080847e-16;
+    if (J_scale < eps) J_scale = eps;
+    J_scale = pow(J_scale, 0.5);
+    return f * (rho1 / J_scale);
+}
+
+// residual() with the robust loss applied to the weighted rows when the
+// solver applies one (fvec only: errorList / errorDistanceList are unscaled).
+MMBA_DEV Resid residual_l(const DevProblem &P, const double *rec, const double *bp, double mkr_x,
+                          double mkr_y, double sqrtw, int lens_type, const double *lens) {
+    Resid r = residual(rec, bp, mkr_x, mkr_y, sqrtw, P.mode, P.image_width, lens_type, lens);
+    if (P.loss_on) {
+        r.ex = robust_loss(r.ex, P.loss_type, P.loss_scale);
+        r.ey = robust_loss(r.ey, P.loss_type, P.loss_scale);
+    }
+    return r;
+}
+
 MMBA_DEV void lens_coeffs(const DevProblem &P, int lens, int f, const Override &ov,
                           double *c) {
     const int *la = &P.lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
@@ -594,14 +631,15 @@ MMBA_DEV void lens_coeffs(const DevProblem &P, int lens, int f, const Override &
     if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.;  // no rescale slot
 }
 
-// Box-constraint reparametrisation (adjust_base.cpp:194-220).
+// Box-constraint reparametrisation (adjust_base.cpp:194-220); the clamps
+// keep std::max / std::min argument order (adjust_base.cpp:202-203,217-218).
 __host__ __device__ inline double int_to_ext(double value, double xmin, double xmax,
                                              double offset, double scale) {
     const double float_max = 3.40282346638528859811704183484516925440e+38;
     if ((xmin <= -float_max) && (xmax >= float_max)) {
         value = (value / scale) - offset;
-        value = value > xmin ? value : xmin;
-        value = value < xmax ? value : xmax;
+        value = (value < xmin) ? xmin : value;  // std::max<double>: NaN passes
+        value = (xmax < value) ? xmax : value;  // std::min<double>
         return value;
     } else if (xmax >= float_max) {
         value = xmin - (1.0 + sqrt(value * value + 1.0));
@@ -611,8 +649,8 @@ __host__ __device__ inline double int_to_ext(double value, double xmin, double x
         value = xmin + ((xmax - xmin) / 2.0) * (sin(value) + 1.0);
     }
     value = (value / scale) - offset;
-    value = value > xmin ? value : xmin;
-    value = value < xmax ? value : xmax;
+    value = (value < xmin) ? xmin : value;
+    value = (xmax < value) ? xmax : value;
     return value;
 }
 

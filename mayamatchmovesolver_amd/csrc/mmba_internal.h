@@ -183,6 +183,15 @@ struct DevProblem {
     // the root shard, the global parameters.
     const int *obs_own, *cf_own, *bnd_own;
     int root, Ra, Rb;
+    // attribute stiffness / smoothness rows (mmba_rows.hip): nrows rows after
+    // the 2 M marker rows, measured only in Maya DAG mode (rows_live);
+    // row_param = the parameter setting the row's (attribute, frame), -1 none
+    int nrows, rows_live;
+    const int *row_attr, *row_frame, *row_param;
+    const double *row_w, *row_var, *row_val;
+    // robust loss on every residual row (applyLossFunctionToErrors), when on
+    int loss_on, loss_type;
+    double loss_scale;
 };
 
 __device__ __forceinline__ size_t widx(const DevProblem &P, int k, int i) {

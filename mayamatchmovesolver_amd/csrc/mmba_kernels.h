@@ -58,11 +58,31 @@ void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, 
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,
                         double *partial_jp);
+// Second evaluation of central FD columns (lmder, autoDiffType central):
+// records / bundle records / perturbed values at x + deltaB and the column
+// factor 0.5 / (|dA| + |dB|) (0: forward column).  recs == nullptr: forward.
+struct CentralB {
+    const double *recs = nullptr, *brec = nullptr, *ext_pert = nullptr, *step = nullptr;
+};
+void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
+                          double *stepB, double delta, double *count);
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
                      int ncv = 0,  // ncv 6 / 7: uniform fast kernels (Plan::jac_ncv)
-                     const double *f = nullptr);  // residuals at x (column-parallel kernel)
+                     const double *f = nullptr,  // residuals at x (column-parallel kernel)
+                     const CentralB &CB = CentralB());
+// Attribute stiffness / smoothness rows (mmba_rows.hip): fr / eur point at
+// row 0 of the rows (f + 2M); partial[slot] gets the rows' sum of squares
+// (slot = nblk(M, 256): the entry after the residual blocks).
+void launch_rows_eval(hipStream_t s, const DevProblem &P, double *fr, double *eur,
+                      double *partial, int slot, const double *Jrow = nullptr,
+                      const double *pstep = nullptr, double *partial_jp = nullptr);
+void launch_rows_jac(hipStream_t s, const DevProblem &P, const double *ext,
+                     const double *ext_pert, const double *step, const double *ext_pertB,
+                     const double *stepB, int lmder, double *Jrow, double *eur, int last_param);
+void launch_rows_ne(hipStream_t s, const DevProblem &P, const double *Jrow, const double *fr,
+                    const int *p_own, double *Acc, double *Abb, double *aggbuf, double *g);
 // aggbuf = [Agg (NGMAX^2) | g_G (NGMAX)]: the global-parameter normal
 // equations, all-reduced across shards before launch_colnorms.
 // lmder's bookkeeping after the normal equations (k_jac_epilogue's column

@@ -99,6 +99,33 @@ __global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double 
     param_prep_one(P, p, x[p], ext, ext_pert, step, solver_type, delta, eps_dif);
 }
 
+// Central differences, second evaluation of each column
+// (solveFunc_calculateJacobianMatrixForParameter, adjust_solveFunc.cpp:405-475):
+// deltaB = calculateParameterDelta(value, delta, -1); when deltaB == deltaA the
+// column stays a forward difference (stepB = 0), otherwise the column is
+// (f(x + deltaA) - f(x + deltaB)) * 0.5 / (|deltaA| + |deltaB|) (B8), with
+// stepB holding that factor.  count += number of central columns (each one
+// is a second incrementJacobianIteration).
+__global__ void k_param_central(DevProblem P, const double *__restrict__ x, double *ext_pertB,
+                                double *stepB, double delta, double *count) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    const double v = x[p];
+    const double xmin = P.p_min[p], xmax = P.p_max[p];
+    double sa = 1., sb = -1.;
+    if ((v + delta) > xmax) sa = sb = -1.;
+    if ((v - delta) < xmin) sa = sb = 1.;
+    const double dA = delta * sa, dB = delta * sb;
+    if (dA == dB) {
+        stepB[p] = 0.;
+        ext_pertB[p] = 0.;
+        return;
+    }
+    stepB[p] = 0.5 / (fabs(dA) + fabs(dB));
+    ext_pertB[p] = int_to_ext(v + dB, xmin, xmax, P.p_off[p], P.p_scale[p]);
+    atomicAdd(count, 1.0);
+}
+
 __global__ void k_set_attrs(DevProblem P, const double *__restrict__ ext) {
     int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
@@ -258,8 +285,8 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         const int hl = FAST ? MMBA_LENS_NONE : obs_lens(P, cam, lens);
         if (hl) lens_coeffs(P, lens, fr, none, lc);
         const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
-        Resid r = residual(rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i], P.mode,
-                           P.image_width, hl, lc);
+        Resid r = residual_l(P, rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i],
+                             hl, lc);
         f[2 * i] = r.ex;
         f[2 * i + 1] = r.ey;
         if (eu) {
@@ -328,7 +355,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
                                                   const double *__restrict__ step,
                                                   int solver_type, double *J, int *jcol,
                                                   int *nloc, const int *__restrict__ stale_param,
-                                                  double *eu, double *ed) {
+                                                  double *eu, double *ed, CentralB CB) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.M) return;
     const int M = P.M;
@@ -348,41 +375,52 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     const int voff = P.cf_var_off[cf];
     const int nvar = P.cf_var_off[cf + 1] - voff;
     const double *rec0 = &recs[(size_t)voff * CAMREC];
-    const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, hl, lc0);
+    const Resid r0 = residual_l(P, rec0, bp0, mx, my, sw, hl, lc0);
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     const int pstale = stale_param[fr];
     Resid rs = r0;
     int l = 0;
     double ljx = 0., ljy = 0.;  // last emitted column (bundle block record)
-    auto emit_s = [&](int p, const Resid &r, double st) {
+    // evalB: the column's second (deltaB) evaluation, run only for a central
+    // column (CB.step[p] != 0)
+    auto emit_s = [&](int p, const Resid &r, double st, auto &&evalB) {
         double jx, jy;
-        if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
-            jx = (r.ex - r0.ex) * st;
-            jy = (r.ey - r0.ey) * st;
-        } else {      // st = h, divided (fdjac2)
-            jx = (r.ex - r0.ex) / st;
-            jy = (r.ey - r0.ey) / st;
+        const double sB = (lmder && CB.recs) ? CB.step[p] : 0.;
+        if (sB != 0.) {  // central: (f(x + dA) - f(x + dB)) * 0.5 / (|dA| + |dB|)
+            const Resid rb = evalB();
+            jx = (r.ex - rb.ex) * sB;
+            jy = (r.ey - rb.ey) * sB;
+            if (p == pstale) rs = rb;  // the column's last measureErrors
+        } else {
+            if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
+                jx = (r.ex - r0.ex) * st;
+                jy = (r.ey - r0.ey) * st;
+            } else {      // st = h, divided (fdjac2)
+                jx = (r.ex - r0.ex) / st;
+                jy = (r.ey - r0.ey) / st;
+            }
+            if (p == pstale) rs = r;
         }
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
         jcol[(size_t)l * M + i] = p;
         ljx = jx;
         ljy = jy;
-        if (p == pstale) rs = r;
         ++l;
     };
-    auto emit = [&](int p, const Resid &r) { emit_s(p, r, step[p]); };
     // camera-side parameters (variants 1..nvar-1)
     for (int v = 1; v < nvar && l < LMAX; ++v) {
         const int t = voff + v;
         const int p = P.cf_var_param[t];
-        const double *rec = &recs[(size_t)t * CAMREC];
+        const bool bside = (P.cf_var_flags[t] & VF_BUNDLE_SIDE) != 0;
         double bp[3] = {bp0[0], bp0[1], bp0[2]};
-        if (P.cf_var_flags[t] & VF_BUNDLE_SIDE) {
-            const Override ov{P.p_attr[p], ext_pert[p]};
-            bundle_position(P, b, fr, ov, bp);
-        }
-        emit(p, residual(rec, bp, mx, my, sw, P.mode, P.image_width, hl, lc0));
+        if (bside) bundle_position(P, b, fr, Override{P.p_attr[p], ext_pert[p]}, bp);
+        emit_s(p, residual_l(P, &recs[(size_t)t * CAMREC], bp, mx, my, sw, hl, lc0), step[p],
+               [&]() {
+                   double bq[3] = {bp0[0], bp0[1], bp0[2]};
+                   if (bside) bundle_position(P, b, fr, Override{P.p_attr[p], CB.ext_pert[p]}, bq);
+                   return residual_l(P, &CB.recs[(size_t)t * CAMREC], bq, mx, my, sw, hl, lc0);
+               });
     }
     // bundle-side parameters not already covered by a camera variant
     if (p4.w >= 0) {  // fast bundle: perturbed positions from the record
@@ -391,8 +429,11 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
         for (int a = 0; a < p4.w && l < LMAX; ++a) {
             const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
             const double bp[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
-            emit_s(p, residual(rec0, bp, mx, my, sw, P.mode, P.image_width, hl, lc0),
-                   br[12 + a]);
+            emit_s(p, residual_l(P, rec0, bp, mx, my, sw, hl, lc0), br[12 + a], [&]() {
+                const double *bb = &CB.brec[(size_t)b * BREC];
+                const double bq[3] = {bb[3 + 3 * a], bb[4 + 3 * a], bb[5 + 3 * a]};
+                return residual_l(P, rec0, bq, mx, my, sw, hl, lc0);
+            });
             jb[2 * a] = ljx;
             jb[2 * a + 1] = ljy;
         }
@@ -414,20 +455,26 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
             for (int v = 1; v < nvar; ++v) seen |= (P.cf_var_param[voff + v] == p);
             if (seen) continue;
         }
-        const Override ov{P.p_attr[p], ext_pert[p]};
         double bp[3];
-        bundle_position(P, b, fr, ov, bp);
-        emit(p, residual(rec0, bp, mx, my, sw, P.mode, P.image_width, hl, lc0));
+        bundle_position(P, b, fr, Override{P.p_attr[p], ext_pert[p]}, bp);
+        emit_s(p, residual_l(P, rec0, bp, mx, my, sw, hl, lc0), step[p], [&]() {
+            double bq[3];
+            bundle_position(P, b, fr, Override{P.p_attr[p], CB.ext_pert[p]}, bq);
+            return residual_l(P, rec0, bq, mx, my, sw, hl, lc0);
+        });
     }
     // lens parameters of this camera's lens
     if (hl) {
         for (int q = P.cam_lpar_off[cam]; q < P.cam_lpar_off[cam + 1] && l < LMAX; ++q) {
             const int p = P.cam_lpar[q];
             if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
-            const Override ov{P.p_attr[p], ext_pert[p]};
             double lc[MMBA_LENS_NUM_ATTRS];
-            lens_coeffs(P, lens, fr, ov, lc);
-            emit(p, residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, hl, lc));
+            lens_coeffs(P, lens, fr, Override{P.p_attr[p], ext_pert[p]}, lc);
+            emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, lc), step[p], [&]() {
+                double lq[MMBA_LENS_NUM_ATTRS];
+                lens_coeffs(P, lens, fr, Override{P.p_attr[p], CB.ext_pert[p]}, lq);
+                return residual_l(P, rec0, bp0, mx, my, sw, hl, lq);
+            });
         }
     }
     nloc[i] = l;
@@ -1137,7 +1184,7 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
     if (threadIdx.x == 0) {
         scalar[rw.slot] = red[0];
         if (blockIdx.x == 0 && flag && spec.flag_slot >= 0) {
-            scalar[spec.flag_slot] = *flag ? 1. : 0.;
+            scalar[spec.flag_slot] = (double)*flag;  // bit 1 pivot, bit 2 dataflow timeout
             *flag = 0;
         }
     }
@@ -2109,7 +2156,9 @@ void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &sp
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);
 }
-int residual_blocks(const DevProblem &P) { return nblk(P.M, 256); }
+// Partial sums of a residual evaluation: one per 256 observations, plus one
+// for the attribute rows (k_rows_eval writes entry nblk(M, 256)).
+int residual_blocks(const DevProblem &P) { return nblk(P.M, 256) + (P.nrows > 0 ? 1 : 0); }
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out, unsigned int *ticket) {
     if (P.all_bnd_fast && P.no_lens)
@@ -2118,7 +2167,7 @@ void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, dou
     else
         k_residual<false, false><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr);
-    if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, nblk(P.M, 256), out);
+    if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, residual_blocks(P), out);
 }
 // Per-observation reprojection (FlatScene::evaluate's out_point_list /
 // out_marker_list, the pair measureErrors compares): the lens-distorted point
@@ -2162,7 +2211,7 @@ void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, 
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
-                     int ncv, const double *f) {
+                     int ncv, const double *f, const CentralB &CB) {
     (void)f;
 #define MMBA_JAC_U(NCV, GEN)                                                                \
     k_jacobian_u<NCV, GEN><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, \
@@ -2177,7 +2226,12 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
     }
 #undef MMBA_JAC_U
     k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
-                                                nloc, stale_param, eu, ed);
+                                                nloc, stale_param, eu, ed, CB);
+}
+void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
+                          double *stepB, double delta, double *count) {
+    if (P.n > 0)
+        k_param_central<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext_pertB, stepB, delta, count);
 }
 bool ne_epilogue_fusable(const DevProblem &P) {
     return P.nG == 0 && P.JB && (P.pc_uniform == 6 || P.pc_uniform == 7) && !P.obs_own;
@@ -2346,7 +2400,7 @@ void launch_zero_flag(hipStream_t s, const double *acnorm, int n, const int *mas
 }
 __global__ void k_flag_to_scalar(int *flag, double *out) {
     if (threadIdx.x == 0) {
-        *out = *flag ? 1. : 0.;
+        *out = (double)*flag;
         *flag = 0;  // read-and-clear: ready for the next factorisation
     }
 }

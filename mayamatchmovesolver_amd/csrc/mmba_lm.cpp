@@ -130,6 +130,9 @@ void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed) {
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin(SPAN_RESID);
+    // stiffness / smoothness rows: their partial goes after the residual blocks
+    launch_rows_eval(s, P, df + 2 * (size_t)M, eu ? eu + 2 * (size_t)M : nullptr, d_partial,
+                     (M + 255) / 256);
     launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + SL_FNORM, d_ticket);
     span_end(SPAN_RESID);
     allreduce(d_scalar + SL_FNORM, 1);
@@ -147,15 +150,29 @@ double Plan::fun(const double *dx, double *df, double *eu, double *ed) {
 void Plan::jac(const double *dx, const JacLM *lm) {
     const double t0 = wall_now();
     const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
+    const bool lmder = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
+    CentralB CB;
+    if (central) {  // the deltaB pass of the central columns
+        MMBA_HIP(hipMemsetAsync(d_scalar + SL_NCENT, 0, sizeof(double), s));
+        launch_param_central(s, P, dx, d_ext_pertB, d_stepB, opt.delta, d_scalar + SL_NCENT);
+        launch_records(s, P, d_var_cf, d_ext_pertB, d_stepB, d_recsB, nvar, d_brecB, 0);
+        CB.recs = d_recsB;
+        CB.brec = d_brecB;
+        CB.ext_pert = d_ext_pertB;
+        CB.step = d_stepB;
+    }
     span_begin(SPAN_JAC);
     launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
-                    d_stale, d_eu, d_ed, jac_ncv, d_f);
+                    d_stale, d_eu, d_ed, jac_ncv, d_f, CB);
+    launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
+                    central ? d_stepB : nullptr, lmder ? 1 : 0, d_Jrow, d_eu + 2 * (size_t)M,
+                    n - 1);
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     // uniform unsharded plans: the lmder bookkeeping rides in the
     // normal-equation kernels (no k_jac_epilogue launch)
-    const bool fuse = lm && ne_epilogue_fusable(P);
+    const bool fuse = lm && ne_epilogue_fusable(P) && nrows == 0;
     NeEpi epi;
     if (fuse) {
         epi.on = 1;
@@ -174,6 +191,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     }
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
               d_glob_partial, glob_chunk, epi);
+    launch_rows_ne(s, P, d_Jrow, d_f + 2 * (size_t)M, d_p_own, d_Acc, d_Abb, d_Agg, d_g);
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
     if (fuse) {
         span_end(SPAN_JAC);
@@ -213,6 +231,8 @@ void Plan::trial_enqueue(double *eu, double *ed) {
                       opt.solver_type, opt.delta, 1.0, d_p_own, pr, nparts, pw);
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin(SPAN_RESID);
+    launch_rows_eval(s, P, d_ftrial + 2 * (size_t)M, eu + 2 * (size_t)M, pr + 2 * (size_t)pw,
+                     (M + 255) / 256, d_Jrow, d_wa1, pr + 3 * (size_t)pw);
     launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
                        d_wa1, pr + 3 * (size_t)pw);
     span_end(SPAN_RESID);
@@ -413,7 +433,23 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *unda
         ++iter;
         if (*par == 0.) *par = std::max(dwarf, p001 * paru);
         pl.solve_damped_enqueue(*par, Plan::SL_DNORM);
-        pl.read_slots(Plan::SL_DNORM, Plan::SL_DNORM);
+        pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+        // (A + par D^2) is positive definite for par > 0, so a failed damped
+        // factorisation is a numerical breakdown (or, bit 2, a timed-out
+        // dataflow wait in the block cyclic reduction): never use its stale
+        // step.  Raise par (a larger damping is better conditioned) a few
+        // times, then give up with an error.
+        for (int retry = 0; h[Plan::SL_FAIL] != 0.; ++retry) {
+            if (h[Plan::SL_FAIL] >= 2. || retry == 8) {
+                set_error("damped normal-equation factorisation failed (par " +
+                          std::to_string(*par) + ", flag " + std::to_string(h[Plan::SL_FAIL]) +
+                          ")");
+                throw DeviceError();
+            }
+            *par *= 10.;
+            pl.solve_damped_enqueue(*par, Plan::SL_DNORM);
+            pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+        }
         dxnorm = std::sqrt(h[Plan::SL_DNORM]);
         double temp = fp;
         fp = dxnorm - delta;
@@ -442,6 +478,14 @@ void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const dou
     launch_unpermute(s, M, d_ref_of_dev, P.obs_own, f_out ? d_f2 : nullptr,
                      eu_out ? d_eu2 : nullptr, ed_out ? d_ed1 : nullptr, tf, te, td);
     allreduce(d_gather, total);
+    if (nrows > 0) {  // stiffness / smoothness rows: identical on every shard
+        if (f_out)
+            MMBA_HIP(hipMemcpyAsync(tf + 2 * (size_t)Mg, d_f2 + 2 * (size_t)M,
+                                    sizeof(double) * nrows, hipMemcpyDeviceToDevice, s));
+        if (eu_out)
+            MMBA_HIP(hipMemcpyAsync(te + 2 * (size_t)Mg, d_eu2 + 2 * (size_t)M,
+                                    sizeof(double) * nrows, hipMemcpyDeviceToDevice, s));
+    }
     if (f_out) MMBA_HIP(hipMemcpyAsync(f_out, tf, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
     if (eu_out)
         MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
@@ -485,6 +529,8 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         fun(d_x, d_f, d_eu, d_ed);
     } else {
         launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+        launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
+                         (M + 255) / 256);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
     }
     std::vector<double> ed(Mg);
@@ -521,8 +567,14 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
     P.jcol_implicit = 0;  // this host-side reassembly reads jcol
     jac(d_x);
     P.jcol_implicit = implicit;
-    std::vector<double> J((size_t)2 * LMAX * M);
-    std::vector<int> jc((size_t)LMAX * M), nl(M);
+    std::vector<double> J((size_t)2 * LMAX * M), Jr(nrows);
+    std::vector<int> jc((size_t)LMAX * M), nl(M), rp(nrows);
+    if (nrows > 0) {
+        MMBA_HIP(hipMemcpyAsync(Jr.data(), d_Jrow, sizeof(double) * nrows, hipMemcpyDeviceToHost,
+                                s));
+        MMBA_HIP(hipMemcpyAsync(rp.data(), P.row_param, sizeof(int) * nrows,
+                                hipMemcpyDeviceToHost, s));
+    }
     MMBA_HIP(hipMemcpyAsync(J.data(), d_J, sizeof(double) * J.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(jc.data(), d_jcol, sizeof(int) * jc.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(nl.data(), d_nloc, sizeof(int) * M, hipMemcpyDeviceToHost, s));
@@ -537,13 +589,57 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
             fjac[(size_t)p * m + 2 * r + 1] = J[(size_t)(2 * l + 1) * M + i];
         }
     }
+    for (int r = 0; r < nrows; ++r)
+        if (rp[r] >= 0) fjac[(size_t)rp[r] * m + 2 * (size_t)M + r] = Jr[r];
     return MMBA_OK;
+}
+
+// Columns [0, k) of an interrupted lmder Jacobian were measured: recompute
+// errorList / errorDistanceList as the last of them left them (B13 with the
+// stale-column table cut at k; lmdif measured every frame per column).
+void Plan::jac_partial_stale(const double *dx, int k) {
+    std::vector<int> st(F, -1);
+    const bool lmdif = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDIF;
+    for (int f = 0; f < F; ++f) {
+        if (lmdif) {
+            st[f] = k - 1;
+            continue;
+        }
+        for (int p = k - 1; p >= 0; --p)
+            if (param_frame_host[p] < 0 || param_frame_host[p] == f) {
+                st[f] = p;
+                break;
+            }
+    }
+    MMBA_HIP(hipMemcpyAsync(d_stale, st.data(), sizeof(int) * F, hipMemcpyHostToDevice, s));
+    const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
+    launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
+    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
+    CentralB CB;
+    if (central) {
+        MMBA_HIP(hipMemsetAsync(d_scalar + SL_NCENT, 0, sizeof(double), s));
+        launch_param_central(s, P, dx, d_ext_pertB, d_stepB, opt.delta, d_scalar + SL_NCENT);
+        launch_records(s, P, d_var_cf, d_ext_pertB, d_stepB, d_recsB, nvar, d_brecB, 0);
+        CB.recs = d_recsB;
+        CB.brec = d_brecB;
+        CB.ext_pert = d_ext_pertB;
+        CB.step = d_stepB;
+    }
+    // the generic kernel honours the stale table for every column
+    launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
+                    d_stale, d_eu, d_ed, 0, d_f, CB);
+    launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
+                    central ? d_stepB : nullptr, lmdif ? 0 : 1, d_Jrow, d_eu + 2 * (size_t)M,
+                    k - 1);
+    MMBA_HIP(hipMemcpyAsync(d_stale, stale_host.data(), sizeof(int) * F, hipMemcpyHostToDevice,
+                            s));
 }
 
 int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
                 mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {
     const double t_start = wall_now();
     t_func = t_jac = t_linear = 0.;
+    cbk = cb;
     mmba_result r;
     std::memset(&r, 0, sizeof(r));
     if (trace) trace->count = 0;
@@ -556,17 +652,26 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     // fresh attribute block (the scene's current values)
     MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
     std::vector<double> ed_host(Mg);
-    double init_avg = 0., init_min = 0., init_max = 0.;
-    if (opt.accept_only_better) {
-        // measureErrors before any parameter is set (adjust_base.cpp:1080-1103)
+    double init_avg = 0., init_min = 0., init_max = 0., init_fnorm = 0.;
+    bool measured = false;
+    if (opt.accept_only_better && !opt.initial_error_given) {
+        // measureErrors before any parameter is set (adjust_base.cpp:1080-1103);
+        // it writes errorList (lmder's fvec), ud->errorList and
+        // errorDistanceList, which an immediate interrupt leaves in place
         launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
-        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
+        launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
+                         (M + 255) / 256);
+        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FNORM);
+        allreduce(d_scalar + SL_FNORM, 1);
         download_ref_order(nullptr, nullptr, d_ed, nullptr, nullptr, ed_host.data());
         error_stats(ed_host.data(), Mg, &init_avg, &init_min, &init_max);
+        init_fnorm = std::sqrt(read_scalar(SL_FNORM));
+        measured = true;
+    } else if (opt.accept_only_better) {
+        init_avg = opt.initial_error_avg;  // the caller measured it
     }
     r.error_initial_avg = init_avg;
 
-    std::vector<double> x0(x_inout, x_inout + n);
     MMBA_HIP(hipMemcpyAsync(d_x, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
     MMBA_HIP(hipMemsetAsync(d_diag, 0, sizeof(double) * n, s));
 
@@ -577,30 +682,69 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     const double ftol = opt.eps1, xtol = opt.eps2, gtol = opt.eps3;
     const int maxfev = opt.iter_max;
     const bool lmdif = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDIF;
+    const bool polls = cb && cb->interrupt;
     int info = 0, nfev = 0, njev = 0, func_evals = 0, jac_evals = 0;
     bool interrupted = false;
-    double delta = 0., xnorm = 0., par = 0., fnorm = 0., gnorm = 0., ratio = 0.;
+    double delta = 0., xnorm = 0., par = 0., fnorm = init_fnorm, gnorm = 0., ratio = 0.;
 
     if (n <= 0 || mg < n || ftol < 0. || xtol < 0. || gtol < 0. || maxfev <= 0 || factor <= 0.)
         goto TERMINATE;
     if (mode == 2) {
-        // diag = paramWeightList = 1.0 (adjust_base.cpp: countUpNumberOfUnknownParameters)
-        std::vector<double> ones(n, 1.0);
-        MMBA_HIP(hipMemcpyAsync(d_diag, ones.data(), sizeof(double) * n, hipMemcpyHostToDevice, s));
+        // diag = paramWeightList (adjust_cminpack_lmder.cpp:151); lmder
+        // rejects a non-positive entry before the first evaluation
+        for (int j = 0; j < n; ++j)
+            if (param_weight[j] <= 0.) goto TERMINATE;
+        MMBA_HIP(hipMemcpyAsync(d_diag, param_weight.data(), sizeof(double) * n,
+                                hipMemcpyHostToDevice, s));
     }
-    fnorm = fun(d_x, d_f, d_eu, d_ed);
+    // iflag = 1 at x0: incrementNormalIteration, then the interrupt poll
+    // (adjust_solveFunc.cpp:551-571)
     nfev = 1;
     func_evals = 1;
+    if (polls && poll_interrupt()) {
+        interrupted = true;
+        info = -1;
+        goto TERMINATE;
+    }
+    fnorm = fun(d_x, d_f, d_eu, d_ed);
     push_trace(fnorm);
     {
         int iter = 1;
         for (;;) {
-            if (cb && cb->interrupt && cb->interrupt(cb->user)) {
-                interrupted = true;
-                info = -1;
-                goto TERMINATE;
-            }
             if (cb && cb->progress) cb->progress(cb->user, njev);
+            if (polls) {
+                // the Jacobian request: lmder polls at solveFunc entry and before
+                // every FD column (adjust_solveFunc.cpp:321-325); every fdjac2
+                // column of lmdif is a solveFunc call (counted, then polled)
+                int k = -1;
+                if (!lmdif && poll_interrupt()) k = 0;
+                for (int j = 0; j < n && k < 0; ++j) {
+                    if (lmdif) ++jac_evals;
+                    if (poll_interrupt()) k = j;
+                }
+                if (k >= 0) {
+                    interrupted = true;
+                    info = -1;
+                    if (lmdif) {
+                        nfev += n;  // lmdif adds n after fdjac2 returns
+                    } else {
+                        ++njev;     // lmder counts the Jacobian call
+                        jac_evals += k;
+                        if (central && k > 0) {  // second evaluations of columns < k
+                            launch_param_central(s, P, d_x, d_ext_pertB, d_stepB, opt.delta,
+                                                 d_scalar + SL_NCENT);
+                            std::vector<double> sb(n);
+                            MMBA_HIP(hipMemcpyAsync(sb.data(), d_stepB, sizeof(double) * n,
+                                                    hipMemcpyDeviceToHost, s));
+                            MMBA_HIP(hipStreamSynchronize(s));
+                            for (int j = 0; j < k; ++j) jac_evals += sb[j] != 0. ? 1 : 0;
+                        }
+                    }
+                    if (k > 0) jac_partial_stale(d_x, k);
+                    goto TERMINATE;
+                }
+                if (lmdif) jac_evals -= n;  // counted below with the rest
+            }
             {
                 const JacLM lm{iter == 1, mode, fnorm};
                 jac(d_x, &lm);
@@ -624,6 +768,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 read_slots(0, SL_LAST);
                 t_jac += wall_now() - t0;
             }
+            if (central) jac_evals += (int)h_scalar[SL_NCENT];
             rank_deficient = h_scalar[SL_ZERO] != 0.;
             if (iter == 1) {
                 xnorm = std::sqrt(h_scalar[SL_XN2]);
@@ -639,6 +784,14 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 const double dxn = lmpar_ne(*this, delta, &par, pre, &undamped);
                 (void)dxn;
                 if (pre) spec_ok = undamped;
+                // the trial point's solveFunc call: counted, then polled
+                ++nfev;
+                ++func_evals;
+                if (polls && poll_interrupt()) {
+                    interrupted = true;
+                    info = -1;
+                    goto TERMINATE;
+                }
                 if (pre && spec && undamped) {
                     // the speculative trial is lmder's trial point
                     std::swap(d_eu, d_eu_s);
@@ -655,8 +808,6 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 const double pnorm = std::sqrt(h_scalar[SL_PNORM]);
                 if (iter == 1) delta = std::min(delta, pnorm);
                 const double fnorm1 = std::sqrt(h_scalar[SL_FNORM]);
-                ++nfev;
-                ++func_evals;
                 push_trace(fnorm1);
                 double actred = -1.;
                 if (p1 * fnorm1 < fnorm) {
@@ -703,6 +854,13 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         }
     }
 TERMINATE:
+    cbk = nullptr;
+    if (interrupted && !measured && nfev <= 1) {
+        // errorList / ud->errorList / errorDistanceList were never written
+        MMBA_HIP(hipMemsetAsync(d_f, 0, sizeof(double) * m, s));
+        MMBA_HIP(hipMemsetAsync(d_eu, 0, sizeof(double) * m, s));
+        MMBA_HIP(hipMemsetAsync(d_ed, 0, sizeof(double) * M, s));
+    }
     r.reason_number = info;
     r.iterations = nfev;
     r.function_evals = func_evals;
@@ -710,10 +868,12 @@ TERMINATE:
     r.outer_iterations = njev;
     r.user_interrupted = interrupted ? 1 : 0;
     r.success = func_evals > 0;
-    r.error_final = fnorm;
+    r.error_final = fnorm;  // enorm(fvec) at the returned x
     {
-        std::vector<double> xh(n);
-        download_params(d_x, xh.data());
+        // lmder leaves the solved x in paramList (adjust_cminpack_lmder.cpp:128);
+        // solveFrames writes it back only when the error got better
+        // (:1227-1244), which error_is_better reports
+        download_params(d_x, x_inout);
         download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_host.data());
         if (ed_out) std::memcpy(ed_out, ed_host.data(), sizeof(double) * Mg);
         double avg, mn, mx;
@@ -721,16 +881,9 @@ TERMINATE:
         r.error_avg = avg;
         r.error_min = mn;
         r.error_max = mx;
-        int better = 1;
-        if (opt.accept_only_better) better = avg <= init_avg;
-        r.error_is_better = better;
-        if (better)
-            std::memcpy(x_inout, xh.data(), sizeof(double) * n);
-        else
-            std::memcpy(x_inout, x0.data(), sizeof(double) * n);
+        r.error_is_better = opt.accept_only_better ? (avg <= init_avg) : 1;
         // RMS at the returned parameters
-        MMBA_HIP(hipMemcpyAsync(d_wa2, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
-        fun(d_wa2, d_ftrial, d_J, d_J + m);  // scratch user buffers
+        fun(d_x, d_ftrial, d_J, d_J + m);  // scratch user buffers
         launch_sumsq(s, d_J + m, nullptr, M, d_partial, nparts, d_scalar + SL_RMS, P.obs_own);
         r.error_rms = std::sqrt(reduce_read(SL_RMS) / Mg);
     }

@@ -17,6 +17,8 @@
 // untouched and report success = 0, reason_number = 0.
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -69,72 +71,134 @@ struct FrameProblem {
     bool solvable() const { return p.num_params > 0 && p.num_params <= 2 * p.num_obs; }
 };
 
-// One frame: plan, solve from the current x, write the frame's parameters back.
+// One frame: plan, solve from the current x, write the frame's parameters
+// back when the error got better (solveFrames' write-back, :1231-1244).
 int solve_frame(mmba_context *ctx, FrameProblem &fp, const mmba_options *opt, double *x,
-                mmba_result *res) {
-    const int n = fp.p.num_params, m = 2 * fp.p.num_obs;
+                mmba_result *res, const mmba_callbacks *cb) {
+    const int n = fp.p.num_params;
+    const int m = 2 * fp.p.num_obs + fp.p.num_stiff + fp.p.num_smooth;
     std::vector<double> xs(n), fvec(m), eu(m), ed(fp.p.num_obs);
     for (int k = 0; k < n; ++k) xs[k] = x[fp.params[k]];
     mmba_plan *plan = nullptr;
     int rc = mmba_plan_create(ctx, &fp.p, opt, &plan);
     if (rc != MMBA_OK) return rc;
-    rc = mmba_plan_solve(plan, xs.data(), fvec.data(), eu.data(), ed.data(), res, nullptr,
-                         nullptr);
+    rc = mmba_plan_solve(plan, xs.data(), fvec.data(), eu.data(), ed.data(), res, cb, nullptr);
     mmba_plan_destroy(plan);
     if (rc != MMBA_OK && rc != MMBA_ERR_INTERRUPTED) return rc;
-    for (int k = 0; k < n; ++k) x[fp.params[k]] = xs[k];
-    return rc;
+    if (res->error_is_better)
+        for (int k = 0; k < n; ++k) x[fp.params[k]] = xs[k];
+    return MMBA_OK;
 }
 
 }  // namespace
 
 extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
                                     const mmba_options *opt, double *x_inout,
-                                    mmba_result *results, int32_t max_concurrency) {
+                                    mmba_result *results, int32_t max_concurrency,
+                                    const mmba_callbacks *cb) {
     if (!ctx || !prob || !opt || !x_inout || !results || prob->num_frames <= 0)
         return MMBA_ERR_INVALID;
-    const int F = prob->num_frames;
-    std::vector<FrameProblem> fr(F);
-    bool chained = false;
-    for (int j = 0; j < prob->num_params; ++j) chained |= prob->param_frame[j] < 0;
-    int nf = F;  // frames before the first unsolvable one
-    for (int f = 0; f < F; ++f) {
-        results[f] = mmba_result{};
-        if (f < nf) {
-            fr[f].build(*prob, f);
-            if (!fr[f].solvable()) nf = f;
-        }
-    }
-    const int workers = chained ? 1 : std::max(1, std::min<int>(max_concurrency, nf));
-    if (workers == 1) {
-        for (int f = 0; f < nf; ++f) {
-            const int rc = solve_frame(ctx, fr[f], opt, x_inout, &results[f]);
-            if (rc != MMBA_OK) return rc;
-        }
-        return MMBA_OK;
-    }
-    // independent frames: disjoint parameter sets, so the threads write
-    // disjoint entries of x_inout
-    std::atomic<int> next{0}, first_err{MMBA_OK};
-    auto work = [&]() {
-        mmba_context *c = nullptr;
-        int rc = mmba_context_create(ctx->device, &c);
-        if (rc != MMBA_OK) {
-            int ok = MMBA_OK;
-            first_err.compare_exchange_strong(ok, rc);
-            return;
-        }
-        for (int f; (f = next.fetch_add(1)) < nf && first_err.load() == MMBA_OK;) {
-            rc = solve_frame(c, fr[f], opt, x_inout, &results[f]);
-            if (rc != MMBA_OK) {
-                int ok = MMBA_OK;
-                first_err.compare_exchange_strong(ok, rc);
+    try {
+        const int F = prob->num_frames;
+        std::vector<FrameProblem> fr(F);
+        bool chained = false;
+        for (int j = 0; j < prob->num_params; ++j) chained |= prob->param_frame[j] < 0;
+        int nf = F;  // frames before the first unsolvable one
+        for (int f = 0; f < F; ++f) {
+            results[f] = mmba_result{};
+            if (f < nf) {
+                fr[f].build(*prob, f);
+                if (!fr[f].solvable()) nf = f;
             }
         }
-        mmba_context_destroy(c);
-    };
-    std::vector<std::thread> pool;
-    for (int w = 0; w < workers; ++w) pool.emplace_back(work);
-    for (auto &t : pool) t.join();
-    return first_err.load();
+        if (max_concurrency <= 0) max_concurrency = nf;
+        const int workers = chained ? 1 : std::max(1, std::min<int>(max_concurrency, nf));
+        if (workers == 1) {
+            for (int f = 0; f < nf; ++f) {
+                const int rc = solve_frame(ctx, fr[f], opt, x_inout, &results[f], cb);
+                if (rc != MMBA_OK) return rc;
+            }
+            return MMBA_OK;
+        }
+        // Independent frames: disjoint parameter sets, so the workers write
+        // disjoint entries of x_inout.  A worker's failure is kept with its
+        // message (mmba_last_error is per thread) and re-raised on the
+        // calling thread; frames after the first failed one keep their
+        // starting values, as the reference loop stops there (:1473-1477).
+        // The interrupt callback is only called from the calling thread (the
+        // Maya main-thread contract): it is polled here before each frame is
+        // handed out, and a set interrupt reaches the frames' own solves
+        // through a flag.
+        std::atomic<int> next{0}, first_err{MMBA_OK}, err_frame{F};
+        std::atomic<bool> stop_flag{false};
+        std::mutex mu;
+        std::string err_msg;
+        std::vector<std::vector<double>> xout(nf);
+        std::vector<char> done(nf, 0);
+        struct Sticky {
+            std::atomic<bool> *flag;
+        } sticky{&stop_flag};
+        mmba_callbacks wcb{};
+        wcb.interrupt = [](void *u) -> int {
+            return static_cast<Sticky *>(u)->flag->load() ? 1 : 0;
+        };
+        wcb.user = &sticky;
+        auto work = [&]() {
+            mmba_context *c = nullptr;
+            int rc = mmba_context_create(ctx->device, &c);
+            if (rc != MMBA_OK) {
+                std::lock_guard<std::mutex> lk(mu);
+                int ok = MMBA_OK;
+                if (first_err.compare_exchange_strong(ok, rc)) err_msg = mmba_last_error();
+                return;
+            }
+            for (int f; (f = next.fetch_add(1)) < nf && first_err.load() == MMBA_OK;) {
+                try {
+                    std::vector<double> x(x_inout, x_inout + prob->num_params);
+                    rc = solve_frame(c, fr[f], opt, x.data(), &results[f],
+                                     cb && cb->interrupt ? &wcb : nullptr);
+                    if (rc == MMBA_OK) {
+                        xout[f] = std::move(x);
+                        done[f] = 1;
+                    }
+                } catch (const std::exception &e) {
+                    mmba::set_error(std::string("per-frame worker: ") + e.what());
+                    rc = MMBA_ERR_INVALID;
+                } catch (...) {
+                    mmba::set_error("per-frame worker: unknown exception");
+                    rc = MMBA_ERR_INVALID;
+                }
+                if (rc != MMBA_OK) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (f < err_frame.load()) {
+                        err_frame = f;
+                        first_err = rc;
+                        err_msg = mmba_last_error();
+                    }
+                }
+            }
+            mmba_context_destroy(c);
+        };
+        std::vector<std::thread> pool;
+        for (int w = 0; w < workers; ++w) pool.emplace_back(work);
+        if (cb && cb->interrupt) {
+            // poll from the calling thread while the workers run
+            while (next.load() < nf && first_err.load() == MMBA_OK && !stop_flag.load()) {
+                if (cb->interrupt(cb->user)) stop_flag = true;
+                std::this_thread::yield();
+            }
+        }
+        for (auto &t : pool) t.join();
+        const int ef = err_frame.load();
+        for (int f = 0; f < nf && f < ef; ++f) {
+            if (!done[f]) continue;
+            for (int k : fr[f].params) x_inout[k] = xout[f][k];
+        }
+        for (int f = ef + 1; f < F; ++f) results[f] = mmba_result{};
+        if (first_err.load() != MMBA_OK) mmba::set_error(err_msg);
+        return first_err.load();
+    } catch (const std::exception &e) {
+        mmba::set_error(std::string("per-frame: ") + e.what());
+        return MMBA_ERR_INVALID;
+    }
 }

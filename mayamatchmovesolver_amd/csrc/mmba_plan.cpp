@@ -89,10 +89,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     const int nL = pr->num_lenses, nK = pr->num_markers;
     nB = pr->num_bundles;
     Mg = pr->num_obs;
-    mg = 2 * Mg;
+    nrows = (pr->num_stiff > 0 ? pr->num_stiff : 0) + (pr->num_smooth > 0 ? pr->num_smooth : 0);
+    mg = 2 * Mg + nrows;
     M = Mg;  // local observations: all of them unless sharded (below)
     n = pr->num_params;
-    m = 2 * M;
+    m = 2 * M + nrows;
     rank = comm ? comm->rank : 0;
     nranks = comm ? comm->nranks : 1;
     require(F > 0 && M > 0 && n > 0, "empty problem");
@@ -103,9 +104,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     require(opt.scene_graph_mode == MMBA_SCENE_GRAPH_MAYA_DAG ||
                 opt.scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH,
             "scene_graph_mode");
-    if (opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER &&
-        opt.auto_diff_type == MMBA_AUTO_DIFF_CENTRAL)
-        throw Unsupported{"central differences (B15: reference zero-initialises errorListB)"};
+    const bool lmder_opt = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER;
+    // lmdif never reads autoDiffType (its fdjac2 is always forward)
+    central = lmder_opt && opt.auto_diff_type == MMBA_AUTO_DIFF_CENTRAL;
+    if (opt.robust_loss)
+        require(opt.robust_loss_type >= MMBA_ROBUST_LOSS_TRIVIAL &&
+                    opt.robust_loss_type <= MMBA_ROBUST_LOSS_CAUCHY && opt.robust_loss_scale != 0.,
+                "robust_loss_type / robust_loss_scale");
 
     // ---- validate indices ----
     for (int a = 0; a < nA; ++a) require(pr->attr_offset[a] >= 0, "attr_offset");
@@ -139,6 +144,39 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         require(pr->attr_animated[a] ? (pr->param_frame[p] >= 0 && pr->param_frame[p] < F)
                                      : pr->param_frame[p] < 0,
                 "param_frame must be -1 for static and a frame for animated attrs");
+    }
+    param_weight.assign(n, 1.0);
+    if (pr->param_weight)
+        for (int p = 0; p < n; ++p) param_weight[p] = pr->param_weight[p];
+    // stiffness / smoothness rows: the parameter setting each row's
+    // (attribute, frame), if any (a static attribute has one parameter)
+    std::vector<int> row_attr, row_frame, row_param;
+    std::vector<double> row_w, row_var, row_val;
+    {
+        std::map<std::pair<int, int>, int> attr_param;
+        for (int p = 0; p < n; ++p) attr_param[{pr->param_attr[p], pr->param_frame[p]}] = p;
+        auto add_rows = [&](int cnt, const int32_t *ra, const int32_t *rf, const double *w,
+                            const double *var, const double *val) {
+            for (int r = 0; r < cnt; ++r) {
+                const int a = ra[r];
+                require(a >= 0 && a < nA, "stiffness / smoothness attribute id");
+                const int f = pr->attr_animated[a] ? (rf ? rf[r] : 0) : 0;
+                require(f >= 0 && f < F, "stiffness / smoothness frame");
+                row_attr.push_back(a);
+                row_frame.push_back(f);
+                row_w.push_back(w[r]);
+                row_var.push_back(var[r]);
+                row_val.push_back(val[r]);
+                auto it = attr_param.find({a, pr->attr_animated[a] ? f : -1});
+                row_param.push_back(it == attr_param.end() ? -1 : it->second);
+            }
+        };
+        if (pr->num_stiff > 0)
+            add_rows(pr->num_stiff, pr->stiff_attr, pr->stiff_frame, pr->stiff_weight,
+                     pr->stiff_variance, pr->stiff_value);
+        if (pr->num_smooth > 0)
+            add_rows(pr->num_smooth, pr->smooth_attr, pr->smooth_frame, pr->smooth_weight,
+                     pr->smooth_variance, pr->smooth_value);
     }
     int lens_owner = -2;
     for (int c = 0; c < nC; ++c) {
@@ -421,6 +459,35 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                        (cam_lpar_off[d_cam[i] + 1] - cam_lpar_off[d_cam[i]]);
         if (nl > LMAX) throw Unsupported{"more than 20 parameters reach one observation"};
     }
+    // Central differences and the robust loss are only well defined where
+    // every lmder FD column re-measures every marker row: the reference
+    // zero-initialises errorListB (adjust_solveFunc.cpp:412) and re-applies
+    // the loss to the whole buffer (adjust_measureErrors.cpp:553-558), so a
+    // row a column skips (another frame than an animated parameter's, or an
+    // observation no parameter reaches) would get a dense garbage entry.
+    if (lmder_opt && (central || opt.robust_loss)) {
+        int fmin = F, fmax = -1;
+        for (int i = 0; i < Mg; ++i) {
+            fmin = std::min(fmin, (int)pr->obs_frame[i]);
+            fmax = std::max(fmax, (int)pr->obs_frame[i]);
+        }
+        bool masked = false;
+        for (int p = 0; p < n && !masked; ++p)
+            if (pr->param_frame[p] >= 0 && (fmin != pr->param_frame[p] || fmax != fmin))
+                masked = true;
+        for (int i = 0; i < M && !masked; ++i) {
+            const int cf = d_cf[i];
+            const int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
+                           (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) +
+                           (cam_lpar_off[d_cam[i] + 1] - cam_lpar_off[d_cam[i]]);
+            if (nl == 0) masked = true;
+        }
+        if (masked)
+            throw Unsupported{std::string(central ? "central differences" : "robust loss") +
+                              " with lmder where an FD column skips marker rows (animated "
+                              "parameters over several frames, or observations no parameter "
+                              "reaches): the reference's Jacobian is not defined there (B15)"};
+    }
     // observations grouped by bundle
     std::vector<int> bobs_off(nB + 1, 0), bobs(M);
     for (int i = 0; i < M; ++i) bobs_off[d_bnd[i] + 1]++;
@@ -443,6 +510,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 break;
             }
     }
+    stale_host = stale;
+    param_frame_host.assign(pr->param_frame, pr->param_frame + n);
 
     // ---- symbolic tile structure of the reduced system ----
     NT = (nR > 0 && !band) ? (nR + TILE - 1) / TILE : 0;
@@ -710,6 +779,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             if (cf_var_flags[t] != 0) fast = false;
         for (int cf = 0; cf < ncf && fast; ++cf)
             if (cf_var_off[cf + 1] - cf_var_off[cf] - 1 > pc_uniform) fast = false;
+        // central differences and the robust loss run on the generic kernel
+        if (central || opt.robust_loss) fast = false;
         jac_ncv = fast ? pc_uniform : 0;
         if (const char *e = std::getenv("MMBA_JAC_GENERIC"))
             if (std::atoi(e)) jac_ncv = 0;
@@ -750,6 +821,17 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.root = rank == 0 ? 1 : 0;
     D.Ra = Ra;
     D.Rb = Rb;
+    D.nrows = nrows;
+    D.rows_live = opt.scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH ? 0 : 1;
+    D.row_attr = upload(row_attr);
+    D.row_frame = upload(row_frame);
+    D.row_param = upload(row_param);
+    D.row_w = upload(row_w);
+    D.row_var = upload(row_var);
+    D.row_val = upload(row_val);
+    D.loss_on = opt.robust_loss ? 1 : 0;
+    D.loss_type = opt.robust_loss_type;
+    D.loss_scale = opt.robust_loss_scale;
     p_own.assign(n, 1);
     if (nranks > 1) {
         std::vector<int> bown(nB);
@@ -822,8 +904,17 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_ed = dalloc<double>(M);
     d_eu_s = dalloc<double>(m);
     d_ed_s = dalloc<double>(M);
+    for (double *b : {d_f, d_ftrial, d_eu, d_eu_s})
+        MMBA_HIP(hipMemsetAsync(b, 0, sizeof(double) * m, s));
+    d_Jrow = dalloc<double>(nrows);
     d_recs = dalloc<double>((size_t)nvar * CAMREC);
-    d_J = dalloc<double>((size_t)2 * LMAX * M);
+    if (central) {
+        d_ext_pertB = dalloc<double>(n);
+        d_stepB = dalloc<double>(n);
+        d_recsB = dalloc<double>((size_t)nvar * CAMREC);
+        d_brecB = dalloc<double>((size_t)nB * BREC);
+    }
+    d_J = dalloc<double>(std::max((size_t)2 * LMAX * M, (size_t)m + M));
     d_jcol = dalloc<int>((size_t)LMAX * M);
     d_nloc = dalloc<int>(M);
     d_Acc = dalloc<double>((size_t)ncf * PCMAX * PCMAX);

@@ -131,7 +131,16 @@ struct Plan {
     double *d_diag = nullptr, *d_acnorm = nullptr, *d_g = nullptr;
     double *d_wa1 = nullptr, *d_wa2 = nullptr, *d_wa3 = nullptr, *d_xs = nullptr,
            *d_v = nullptr;
+    // residual buffers: [2 M marker rows | nrows stiffness / smoothness rows]
     double *d_f = nullptr, *d_ftrial = nullptr, *d_eu = nullptr, *d_ed = nullptr;
+    int nrows = 0;                 // attribute rows (same on every shard)
+    double *d_Jrow = nullptr;      // their Jacobian entries (one column each)
+    // central differences (lmder, autoDiffType central): the deltaB pass
+    bool central = false;
+    double *d_ext_pertB = nullptr, *d_stepB = nullptr, *d_recsB = nullptr, *d_brecB = nullptr;
+    std::vector<double> param_weight;  // paramWeightList (diag in mode 2)
+    std::vector<int> stale_host;       // stale-column table (B13), host copy
+    std::vector<int> param_frame_host;
     double *d_recs = nullptr, *d_brec = nullptr;
     double *d_J = nullptr;
     int *d_jcol = nullptr, *d_nloc = nullptr;
@@ -221,7 +230,8 @@ struct Plan {
         SL_XN2 = 10,    // ||D x||^2 (first pass)
         SL_GNORM = 11,  // lmder gnorm (max)
         SL_RMS = 12,
-        SL_LAST = 12,
+        SL_NCENT = 13,  // central FD columns of the last Jacobian (second evaluations)
+        SL_LAST = 13,
         NSLOT = 16
     };
     void read_slots(int lo, int hi);
@@ -240,6 +250,15 @@ struct Plan {
         double fnorm;
     };
     void jac(const double *dx, const JacLM *lm = nullptr);
+    // interrupt polls of the reference (MComputation::isInterruptRequested):
+    // true once the caller's callback asks to stop
+    const mmba_callbacks *cbk = nullptr;
+    bool poll_interrupt() const {
+        return cbk && cbk->interrupt && cbk->interrupt(cbk->user) != 0;
+    }
+    // FD columns [0, k) only: errorList / errorDistanceList as an interrupted
+    // Jacobian leaves them (the stale-column table restricted to k columns)
+    void jac_partial_stale(const double *dx, int k);
     // trial point x - xs: setParameters, measureErrors into (d_ftrial, eu,
     // ed), ||J p||; scalars -> SL_PNORM, SL_XN2T, SL_FNORM, SL_JP
     void trial_enqueue(double *eu, double *ed);

@@ -78,6 +78,10 @@ _FIELDS_F64 = [
     "attr_values", "obs_xy", "obs_weight", "param_min", "param_max",
     "param_offset", "param_scale", "x0",
 ]
+# ABI 2 (optional: absent in fixtures written before it)
+_FIELDS_OPT_I32 = ["stiff_attr", "stiff_frame", "smooth_attr", "smooth_frame"]
+_FIELDS_OPT_F64 = ["stiff_weight", "stiff_variance", "stiff_value", "smooth_weight",
+                   "smooth_variance", "smooth_value"]
 
 
 @dataclass
@@ -113,6 +117,19 @@ class Problem:
     param_scale: np.ndarray
     x0: np.ndarray
     meta: Dict = field(default_factory=dict)
+    # ABI 2: paramWeightList (None = 1.0) and attribute stiffness / smoothness
+    # rows (adjust_measureErrors.cpp:311-387)
+    param_weight: Optional[np.ndarray] = None
+    stiff_attr: Optional[np.ndarray] = None
+    stiff_frame: Optional[np.ndarray] = None
+    stiff_weight: Optional[np.ndarray] = None
+    stiff_variance: Optional[np.ndarray] = None
+    stiff_value: Optional[np.ndarray] = None
+    smooth_attr: Optional[np.ndarray] = None
+    smooth_frame: Optional[np.ndarray] = None
+    smooth_weight: Optional[np.ndarray] = None
+    smooth_variance: Optional[np.ndarray] = None
+    smooth_value: Optional[np.ndarray] = None
 
     def __post_init__(self):
         for name in _FIELDS_I32:
@@ -121,6 +138,17 @@ class Problem:
             setattr(self, name, np.ascontiguousarray(getattr(self, name), dtype=np.int64).reshape(-1))
         for name in _FIELDS_F64:
             setattr(self, name, np.ascontiguousarray(getattr(self, name), dtype=np.float64).reshape(-1))
+        for name in _FIELDS_OPT_I32:
+            v = getattr(self, name)
+            setattr(self, name, np.zeros(0, np.int32) if v is None else
+                    np.ascontiguousarray(v, dtype=np.int32).reshape(-1))
+        for name in _FIELDS_OPT_F64:
+            v = getattr(self, name)
+            setattr(self, name, np.zeros(0, np.float64) if v is None else
+                    np.ascontiguousarray(v, dtype=np.float64).reshape(-1))
+        if self.param_weight is not None:
+            self.param_weight = np.ascontiguousarray(self.param_weight,
+                                                     dtype=np.float64).reshape(-1)
 
     # sizes -------------------------------------------------------------
     @property
@@ -132,8 +160,17 @@ class Problem:
         return int(self.param_attr.size)
 
     @property
+    def num_stiff(self):
+        return int(self.stiff_attr.size)
+
+    @property
+    def num_smooth(self):
+        return int(self.smooth_attr.size)
+
+    @property
     def num_residuals(self):
-        return 2 * self.num_obs
+        """2 per observation, then the stiffness and smoothness rows."""
+        return 2 * self.num_obs + self.num_stiff + self.num_smooth
 
     @property
     def num_cameras(self):
@@ -191,12 +228,31 @@ class Problem:
         p.param_max = ptr(self.param_max, C.c_double)
         p.param_offset = ptr(self.param_offset, C.c_double)
         p.param_scale = ptr(self.param_scale, C.c_double)
+        p.param_weight = (ptr(self.param_weight, C.c_double) if self.param_weight is not None
+                          else C.cast(None, C.POINTER(C.c_double)))
+        p.num_stiff = self.num_stiff
+        p.stiff_attr = ptr(self.stiff_attr, C.c_int32)
+        p.stiff_frame = ptr(self.stiff_frame, C.c_int32)
+        p.stiff_weight = ptr(self.stiff_weight, C.c_double)
+        p.stiff_variance = ptr(self.stiff_variance, C.c_double)
+        p.stiff_value = ptr(self.stiff_value, C.c_double)
+        p.num_smooth = self.num_smooth
+        p.smooth_attr = ptr(self.smooth_attr, C.c_int32)
+        p.smooth_frame = ptr(self.smooth_frame, C.c_int32)
+        p.smooth_weight = ptr(self.smooth_weight, C.c_double)
+        p.smooth_variance = ptr(self.smooth_variance, C.c_double)
+        p.smooth_value = ptr(self.smooth_value, C.c_double)
         return p, [self]
 
     # (de)serialisation ---------------------------------------------------
     def to_npz_dict(self):
         d = {name: getattr(self, name) for name in _FIELDS_I32 + _FIELDS_I64 + _FIELDS_F64}
         d["num_frames"] = np.array(self.num_frames, dtype=np.int64)
+        if self.num_stiff or self.num_smooth:
+            for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64:
+                d[name] = getattr(self, name)
+        if self.param_weight is not None:
+            d["param_weight"] = self.param_weight
         return d
 
     @classmethod
@@ -208,6 +264,9 @@ class Problem:
             la = np.concatenate([la.reshape(nl, 5), -np.ones((nl, abi.LENS_NUM_ATTRS - 5),
                                                              np.int32)], axis=1).reshape(-1)
             kw["lens_attrs"] = la
+        for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight"]:
+            if name in d:
+                kw[name] = np.asarray(d[name])
         return cls(num_frames=int(d["num_frames"]), **kw)
 
     def with_x0(self, x0):
@@ -267,6 +326,8 @@ class SceneBuilder:
         self._mkr_overscan: List[tuple] = []
         self._solve: List[tuple] = []
         self._bulk = None
+        self._stiff: List[tuple] = []
+        self._smooth: List[tuple] = []
 
     # attributes -----------------------------------------------------------
     def attr(self, value: Value) -> int:
@@ -414,6 +475,16 @@ class SceneBuilder:
                             0.0 if offset is None else float(offset),
                             1.0 if scale is None else float(scale)))
 
+    def stiffness(self, aid: int, weight: float, variance: float, value: float, frame: int = 0):
+        """Attribute stiffness row (StiffAttrs: weight / variance / value
+        attributes, adjust_measureErrors.cpp:318-348); rows with weight <= 0
+        are not counted (adjust_relationships.cpp:186-199)."""
+        self._stiff.append((int(aid), int(frame), float(weight), float(variance), float(value)))
+
+    def smoothness(self, aid: int, weight: float, variance: float, value: float, frame: int = 0):
+        """Attribute smoothness row (adjust_measureErrors.cpp:353-387)."""
+        self._smooth.append((int(aid), int(frame), float(weight), float(variance), float(value)))
+
     # assembly ---------------------------------------------------------------
     def build(self, meta=None) -> Problem:
         F = self.F
@@ -484,6 +555,16 @@ class SceneBuilder:
             param_scale=pscl,
             x0=x0,
         )
+        # countUpNumberOfErrors counts rows with weight > 0; measureErrors then
+        # reads the first `count` entries of the list (reference indexing)
+        for kind, rows in (("stiff", self._stiff), ("smooth", self._smooth)):
+            count = sum(1 for r in rows if r[2] > 0.0)
+            use = rows[:count]
+            setattr(prob, kind + "_attr", np.array([r[0] for r in use], np.int32))
+            setattr(prob, kind + "_frame", np.array([r[1] for r in use], np.int32))
+            setattr(prob, kind + "_weight", np.array([r[2] for r in use], np.float64))
+            setattr(prob, kind + "_variance", np.array([r[3] for r in use], np.float64))
+            setattr(prob, kind + "_value", np.array([r[4] for r in use], np.float64))
         prob.meta = dict(meta or {})
         return prob
 

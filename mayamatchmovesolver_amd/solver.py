@@ -40,6 +40,15 @@ class SolveResult:
     kernel_stats: Optional[Dict] = None
 
     problem: Optional[Problem] = None
+    x0: Optional[np.ndarray] = None
+
+    @property
+    def accepted_x(self):
+        """What solveFrames writes back: the solved x when the error got
+        better (adjust_base.cpp:1231-1244), else the starting x."""
+        if self.result.get("error_is_better", 1) or self.x0 is None:
+            return self.x
+        return self.x0
 
     @property
     def external(self):
@@ -191,6 +200,11 @@ class Solver:
         return fjac.reshape(n, m).T
 
     def solve(self, x0=None, trace_capacity=4096, interrupt=None) -> SolveResult:
+        """LM solve from x0 (internal parameters).  ``SolveResult.x`` is the
+        solved x as lmder leaves paramList; ``result["error_is_better"]`` says
+        whether solveFrames would write it back (``accepted_x``).
+        ``interrupt``: a callable polled where the reference polls
+        MComputation::isInterruptRequested (non-zero / True stops)."""
         p = self.problem
         m, M = p.num_residuals, p.num_obs
         x = np.array(p.x0 if x0 is None else x0, dtype=np.float64)
@@ -198,16 +212,14 @@ class Solver:
         res = abi.MmbaResult()
         tbuf = np.zeros(max(1, trace_capacity))
         tr = abi.MmbaTrace(_dp(tbuf), trace_capacity, 0)
-        cbs = None
-        if interrupt is not None:
-            cbs = abi.MmbaCallbacks(abi.INTERRUPT_FN(lambda _u: 1 if interrupt() else 0),
-                                    abi.PROGRESS_FN(lambda _u, _i: None), None)
+        cbs = _callbacks(interrupt)
         rc = lib().mmba_plan_solve(self._h, _dp(x), _dp(fvec), _dp(eu), _dp(ed), C.byref(res),
                                    C.byref(cbs) if cbs is not None else None, C.byref(tr))
         if rc not in (abi.MMBA_OK, abi.MMBA_ERR_INTERRUPTED):
             check(rc)
         return SolveResult(x=x, fvec=fvec, err_user=eu, err_dist=ed, result=res.as_dict(),
-                           fnorm_trace=tbuf[:min(tr.count, trace_capacity)].copy(), problem=p)
+                           fnorm_trace=tbuf[:min(tr.count, trace_capacity)].copy(), problem=p,
+                           x0=np.array(p.x0 if x0 is None else x0, dtype=np.float64))
 
 
 def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
@@ -219,20 +231,33 @@ def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
         s.close()
 
 
+def _callbacks(interrupt):
+    if interrupt is None:
+        return None
+    return abi.MmbaCallbacks(abi.INTERRUPT_FN(lambda _u: 1 if interrupt() else 0),
+                             abi.PROGRESS_FN(lambda _u, _i: None), None)
+
+
 def solve_per_frame(problem: Problem, options, x0=None, device: int = 0,
-                    max_concurrency: int = 1):
+                    max_concurrency: int = 0, interrupt=None, context=None):
     """Per-frame solve mode (``mmba_solve_per_frame``; FrameSolveMode::kPerFrame,
-    adjust_base.cpp:1430-1484).  Returns (x, [per-frame result dicts])."""
+    adjust_base.cpp:1430-1484).  Returns (x, [per-frame result dicts]); x holds
+    what each frame's solveFrames wrote back."""
     p, keep = problem.to_ctypes()
     x = np.array(problem.x0 if x0 is None else x0, dtype=np.float64)
     F = problem.num_frames
     res = (abi.MmbaResult * F)()
-    ctx = Context(device)
+    ctx = context or Context(device)
+    cbs = _callbacks(interrupt)
     try:
-        check(lib().mmba_solve_per_frame(ctx.handle, C.byref(p), C.byref(options), _dp(x),
-                                         res, int(max_concurrency)))
+        rc = lib().mmba_solve_per_frame(ctx.handle, C.byref(p), C.byref(options), _dp(x),
+                                        res, int(max_concurrency),
+                                        C.byref(cbs) if cbs is not None else None)
+        if rc not in (abi.MMBA_OK, abi.MMBA_ERR_INTERRUPTED):
+            check(rc)
     finally:
-        ctx.close()
+        if context is None:
+            ctx.close()
     return x, [r.as_dict() for r in res]
 
 

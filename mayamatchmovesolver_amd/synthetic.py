@@ -49,7 +49,44 @@ KNOWN_ANSWERS = {
     "weight_same": ([-1.00000134, 1.65000055], 1e-4),   # :276-336
     "weight_zero": ([-2.25, 1.65], 1e-3),               # :338-398
     "test12_single": ([-6.0, 3.6], 1e-4),               # test12.py (driven bundle)
+    # test_marker_enabled.py:43-111 (marker_02 disabled)
+    "enabled_single": ([-2.24999755, 1.65000644], 1e-4),
+    # test_marker_enabled.py:113-237, solved frame by frame (frames 1, 5, 10 of
+    # the keyed scene; marker_02 disabled on frames 5-9 by a stepped key)
+    "enabled_multi_f1": ([-0.51855463, 1.30993172], 1e-3),
+    "enabled_multi_f5": ([-2.266493967, 1.631927621], 1e-3),
+    "enabled_multi_f10": ([-1.48144697, 2.10503952], 1e-3),
+    # test_issue54.py:113-235: nodal camera, rotate x/y solved with a +360
+    # attribute offset, 10 iterations
+    "issue54_zero": ([-2.85, -2.86], 1e-1),
+    "issue54_twenty": ([0.0, 0.0], 1e-2),
+    "issue54_threesixty": ([360.0, 360.0], 1e-2),
 }
+
+
+def known_options(name, solver_type=abi.SOLVER_TYPE_CMINPACK_LMDER,
+                  scene_graph_mode=abi.SCENE_GRAPH_MODE_MAYA_DAG, **overrides):
+    """The mmSolver flags each known-answer test runs with (iterations 1000 for
+    test1, 10 for issue54, else the default 100; delta 1e-5 for test3)."""
+    from .options import make_options
+    iters = {"test1": 1000}.get(name, 10 if name.startswith("issue54_") else 100)
+    kw = dict(solver_type=solver_type, scene_graph_mode=scene_graph_mode, iterations=iters,
+              delta=1e-5 if name == "test3" else 1e-4)
+    kw.update(overrides)
+    return make_options(**kw)
+
+
+def known_answer_applies(name, solver_type):
+    """The per-frame marker-enabled test runs the default solver (lmder,
+    SOLVER_TYPE_DEFAULT_VALUE); its answers pin lmder only."""
+    return not (name.startswith("enabled_multi") and
+                solver_type != abi.SOLVER_TYPE_CMINPACK_LMDER)
+
+
+def _hermite_flat(a, b, s):
+    """A two-key Maya animation curve with flat (auto-clamped) end tangents
+    at parameter s in [0, 1]."""
+    return a + (b - a) * (3.0 * s * s - 2.0 * s * s * s)
 
 
 def _camera(b: SceneBuilder, t, r=(0.0, 0.0, 0.0)):
@@ -103,6 +140,50 @@ def known_scene(name: str) -> Problem:
         b.solve(gids[0])
         b.solve(gids[1])
         return b.build(meta={"name": name})
+    if name == "enabled_single":
+        cam, _, _ = _camera(b, (-1.0, 1.0, -5.0))
+        grp, gids = b.transform(t=(0.0, 0.0, -10.0))
+        b1t, _ = b.transform(parent=grp)
+        b2t, _ = b.transform(parent=grp)
+        bnd1, bnd2 = b.bundle(b1t), b.bundle(b2t)
+        b.marker(cam, bnd1, [[-0.243056042, 0.189583713]])
+        b.marker(cam, bnd2, [[0.243056042, 0.189583713]], enable=[False])
+        b.solve(gids[0])
+        b.solve(gids[1])
+        return b.build(meta={"name": name})
+    if name.startswith("enabled_multi_f"):
+        # keys at frames 1 and 10; frame f of the curve (flat tangents)
+        f = int(name[len("enabled_multi_f"):])
+        sfr = (f - 1) / 9.0
+        rx = _hermite_flat(-5.0, 5.0, sfr)
+        ry = _hermite_flat(-5.5, 5.5, sfr)
+        m1 = (_hermite_flat(-0.243056042, -0.29166725, sfr),
+              _hermite_flat(0.218750438, 0.189583713, sfr))
+        m2 = (_hermite_flat(0.243056042, 0.29166725, sfr),
+              _hermite_flat(0.218750438, 0.189583713, sfr))
+        en2 = not (5 <= f < 10)  # enable keys 1 / 0 / 1 at 1 / 5 / 10, stepped
+        cam, _, _ = _camera(b, (-1.0, 1.0, -5.0), r=(rx, ry, 0.0))
+        grp, gids = b.transform(t=(np.zeros(1), np.zeros(1), -10.0))
+        b1t, _ = b.transform(parent=grp)
+        b2t, _ = b.transform(parent=grp)
+        bnd1, bnd2 = b.bundle(b1t), b.bundle(b2t)
+        b.marker(cam, bnd1, [list(m1)])
+        b.marker(cam, bnd2, [list(m2)], enable=[en2])
+        b.solve(gids[0])
+        b.solve(gids[1])
+        return b.build(meta={"name": name})
+    if name.startswith("issue54_"):
+        kind = name[len("issue54_"):]
+        cam_t, cam_r = {"zero": ((-2.0, 2.0, -5.0), (0.0, 0.0, 0.0)),
+                        "twenty": ((-1.0, 1.0, -5.0), (20.0, 20.0, 20.0)),
+                        "threesixty": ((-1.0, 1.0, -5.0), (360.0, 360.0, 360.0))}[kind]
+        cam, ctids, _ = _camera(b, cam_t, r=cam_r)
+        btfm, _ = b.transform(t=(-1.0, 1.0, -25.0))
+        bnd = b.bundle(btfm)
+        b.marker(cam, bnd, [[0.0, 0.0]])
+        b.solve(ctids[3], offset=360.0)  # (attr, min, max, offset '360', scale)
+        b.solve(ctids[4], offset=360.0)
+        return b.build(meta={"name": name, "iterations": 10})
     raise KeyError(name)
 
 
@@ -394,6 +475,32 @@ def _obs_from_windows(rng, start, length, project_fn):
     return ks, fs, xy
 
 
+_ROO_FACTORS = {abi.ROO_XYZ: "zyx", abi.ROO_YZX: "xzy", abi.ROO_ZXY: "yxz",
+                abi.ROO_XZY: "yzx", abi.ROO_YXZ: "zxy", abi.ROO_ZYX: "xyz"}
+
+
+def _euler(rx, ry, rz, roo=abi.ROO_XYZ):
+    """Column-vector rotation of any rotate order (degrees): the product of the
+    three axis rotations in the order mmba_geom.h trs_matrix chains them."""
+    rx, ry, rz = (np.radians(np.asarray(v, dtype=np.float64)) for v in (rx, ry, rz))
+
+    def axis(a, ang):
+        c, s_ = np.cos(ang), np.sin(ang)
+        R = np.zeros(np.shape(ang) + (3, 3))
+        i, j = {"x": (1, 2), "y": (2, 0), "z": (0, 1)}[a]
+        k = "xyz".index(a)
+        R[..., k, k] = 1.0
+        R[..., i, i] = c
+        R[..., j, j] = c
+        R[..., i, j] = -s_
+        R[..., j, i] = s_
+        return R
+
+    ang = {"x": rx, "y": ry, "z": rz}
+    a, b_, c = _ROO_FACTORS[roo]
+    return axis(a, ang[a]) @ axis(b_, ang[b_]) @ axis(c, ang[c])
+
+
 def _pose_project(t, r, focal, pts, fs):
     R = _euler_xyz(r[fs, 0], r[fs, 1], r[fs, 2])
     pc = np.einsum("nij,ni->nj", R, pts - t[fs])
@@ -554,6 +661,147 @@ def _config_c5(rng, F, scale, lens_model="classic"):
                          lens_first=True,
                          meta={"name": CONFIG_NAMES[4] + ("" if lens_model == "classic"
                                                           else "_" + lens_model)})
+
+
+EDGE_RENDERS = {"wide": (2048, 858), "narrow": (2048, 1556)}  # aspect above / below 36x24 mm
+
+
+def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0.0, 0.0),
+               camera_scale=1.0, rotate_order=abi.ROO_XYZ, parented=False, frames=6,
+               bundles=24, seed=9, stiffness=False, static_focal=False,
+               offset_shifts=True, gauge=True) -> Problem:
+    """Small bundle-adjustment scene over the camera settings the synthetic
+    configs keep benign: any film fit, a render aspect above or
+    below the film aspect, film offsets (inches, Appendix B5/B6), a camera
+    scale, any rotate order (camera and its parent), and a parented camera
+    (camera transform under a static, rotated group).  One camera animated
+    over ``frames`` frames (pose solved, frame 0 locked), ``bundles`` bundles
+    seen on every frame (translate solved, bundle 0 locked).  Markers are a
+    plain pinhole projection of the truth plus noise: the reference geometry
+    (film fit, offsets, scale) then has something to fit, which is all a
+    parity scene needs.  ``stiffness``: stiffness rows on two bundle
+    translates and a smoothness row on one camera rotate
+    (adjust_measureErrors.cpp:311-387).  ``static_focal``: the camera focal
+    is solved too, as one static (global) parameter.  ``gauge=False``: nothing
+    locked (with one frame: a bundle-only solve against a fixed camera)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    F, B = frames, bundles
+    b = SceneBuilder(F)
+    f = np.arange(F, dtype=np.float64)
+    t_true = np.stack([0.4 * f, 1.5 + 0.1 * f, -0.2 * f], axis=1)
+    r_true = np.stack([2.0 + 0.5 * f, -8.0 + 0.7 * f, 1.0 + 0.3 * f], axis=1)
+    depth = rng.uniform(15.0, 40.0, size=B)
+    P = np.stack([rng.uniform(-0.3, 0.3, B) * depth, 1.5 + rng.uniform(-0.2, 0.2, B) * depth,
+                  -depth], axis=1)
+    t0 = t_true + rng.uniform(-0.05, 0.05, size=t_true.shape)
+    r0 = r_true + rng.uniform(-1.0, 1.0, size=r_true.shape)
+    t0[0], r0[0] = t_true[0], r_true[0]
+    parent = None
+    if parented:
+        parent, _ = b.transform(t=(0.3, -0.2, 0.5), r=(1.5, -2.0, 3.0), s=(1.0, 1.0, 1.0),
+                                rotate_order=rotate_order)
+    ctfm, tids = b.transform(t=[t0[:, 0], t0[:, 1], t0[:, 2]], r=[r0[:, 0], r0[:, 1], r0[:, 2]],
+                             parent=parent, rotate_order=rotate_order)
+    cam, cids = b.camera(ctfm, focal=FOCAL_MM * (1.03 if static_focal else 1.0),
+                         film_back=(FILM_W_IN, FILM_H_IN), film_offset=film_offset,
+                         film_fit=film_fit, render_size=EDGE_RENDERS[render],
+                         camera_scale=camera_scale)
+    P0 = P * (1.0 + rng.uniform(-0.03, 0.03, size=(B, 1)))
+    if gauge:
+        P0[0] = P[0]
+    bids = []
+    for j in range(B):
+        bt, ids = b.transform(t=tuple(P0[j]))
+        b.bundle(bt)
+        bids.append(ids)
+    # truth camera world pose (parent o local, any rotate order)
+    Rl = _euler(r_true[:, 0], r_true[:, 1], r_true[:, 2], rotate_order)
+    if parented:
+        Rp = _euler(1.5, -2.0, 3.0, rotate_order)
+        Rw = Rp[None] @ Rl
+        tw = t_true @ Rp.T + np.array([0.3, -0.2, 0.5])
+    else:
+        Rw, tw = Rl, t_true
+    fs = np.tile(np.arange(F), B)
+    pc = np.einsum("nji,nj->ni", Rw[fs], np.repeat(P, F, 0) - tw[fs])
+    mx = FOCAL_MM * pc[:, 0] / (FILM_W_MM * -pc[:, 2]) / camera_scale
+    my = FOCAL_MM * pc[:, 1] / (FILM_H_MM * -pc[:, 2]) / camera_scale
+    if offset_shifts:  # Maya DAG: the offset moves the image; MM Scene Graph: not (B6)
+        mx = mx - film_offset[0] / FILM_W_IN
+        my = my - film_offset[1] / FILM_H_IN
+    mx, my = _noisy(rng, mx).reshape(B, F), _noisy(rng, my).reshape(B, F)
+    for j in range(B):
+        b.marker(cam, j, np.stack([mx[j], my[j]], axis=1))
+    if static_focal:
+        b.solve(cids[abi.CAM_FOCAL_MM])
+    for a in tids[:6]:
+        b.solve(a)
+    for j in range(1 if gauge else 0, B):
+        for a in bids[j][:3]:
+            b.solve(a)
+    if stiffness:
+        b.stiffness(bids[1][0], weight=2.0, variance=0.5, value=float(P0[1][0]) + 0.1)
+        b.stiffness(bids[2][2], weight=1.0, variance=2.0, value=float(P0[2][2]) - 0.2)
+        b.smoothness(tids[4], weight=0.5, variance=1.5, value=float(r0[3][1]) + 0.3, frame=3)
+    prob = b.build(meta={"name": "edge"})
+    if gauge:  # camera pose at frame 0 locked (parameters of frame 0 dropped)
+        keep = ~(np.isin(prob.param_attr, tids[:6]) & (prob.param_frame == 0))
+        for name in ("param_attr", "param_frame", "param_min", "param_max", "param_offset",
+                     "param_scale", "x0"):
+            setattr(prob, name, np.ascontiguousarray(getattr(prob, name)[keep]))
+    return prob
+
+
+def rig_scene(n_cams=2, bundles=10, solve_cam1=True, stiffness=False, seed=11) -> Problem:
+    """Static rig: ``n_cams`` cameras with static (non-animated) poses 1.5
+    units apart on one frame, bundles in front solved (translate), camera 1's
+    rotation solved as three static (global) parameters (its translation
+    stays: it sets the scale).  Every parameter is static,
+    so every FD column re-measures every row: the scene on which the
+    reference's central differences and robust loss are well defined (see
+    Plan::build).  Markers camera-major (B4).  ``stiffness``: a stiffness row
+    on a bundle translate and a smoothness row on camera 1's rotate y."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    b = SceneBuilder(1)
+    B = bundles
+    depth = rng.uniform(12.0, 30.0, size=B)
+    P = np.stack([rng.uniform(-0.3, 0.3, B) * depth, rng.uniform(-0.2, 0.2, B) * depth,
+                  -depth], axis=1)
+    cams, cam_ids = [], []
+    for c in range(n_cams):
+        t = np.array([1.5 * c, 0.2 * c, 0.0])
+        r = np.array([0.5 * c, -2.0 * c, 0.3 * c])
+        t0 = t + (rng.uniform(-0.05, 0.05, 3) if c == 1 and solve_cam1 else 0.0)
+        r0 = r + (rng.uniform(-1.0, 1.0, 3) if c == 1 and solve_cam1 else 0.0)
+        tfm, tids = b.transform(t=tuple(t0), r=tuple(r0))
+        cam, _ = b.camera(tfm, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
+                          render_size=RENDER)
+        cams.append((cam, t, r))
+        cam_ids.append(tids)
+    P0 = P * (1.0 + rng.uniform(-0.04, 0.04, size=(B, 1)))
+    bids = []
+    for j in range(B):
+        bt, ids = b.transform(t=tuple(P0[j]))
+        b.bundle(bt)
+        bids.append(ids)
+    for cam, t, r in cams:
+        R = _euler_xyz(*r)
+        pc = (P - t) @ R
+        mx = FOCAL_MM * pc[:, 0] / (FILM_W_MM * -pc[:, 2])
+        my = FOCAL_MM * pc[:, 1] / (FILM_H_MM * -pc[:, 2])
+        for j in range(B):
+            b.marker(cam, j, [[_noisy(rng, mx[j]), _noisy(rng, my[j])]])
+    if solve_cam1 and n_cams > 1:  # rotate only: translating camera 1 is the free scale
+        for a in cam_ids[1][3:6]:
+            b.solve(a)
+    for j in range(B):
+        for a in bids[j][:3]:
+            b.solve(a)
+    if stiffness:
+        b.stiffness(bids[0][1], weight=1.5, variance=0.3, value=float(P0[0][1]) + 0.05)
+        if solve_cam1 and n_cams > 1:
+            b.smoothness(cam_ids[1][4], weight=0.7, variance=0.8, value=-1.5)
+    return b.build(meta={"name": "rig"})
 
 
 def config_options(prob: Problem, scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH,

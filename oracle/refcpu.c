@@ -19,6 +19,10 @@
 
 #define RMIN(a, b) ((a) < (b) ? (a) : (b))
 #define RMAX(a, b) ((a) > (b) ? (a) : (b))
+/* std::max<double>(v, lo) / std::min<double>(v, hi) as the reference clamps
+ * (adjust_base.cpp:202-203,217-218,232-233): a NaN value passes through. */
+#define CLAMP_LO(v, lo) (((v) < (lo)) ? (lo) : (v))
+#define CLAMP_HI(v, hi) (((hi) < (v)) ? (hi) : (v))
 
 /* lib/rust/mmscenegraph/src/constant.rs */
 static const double DEGREES_TO_RADIANS = 0.017453292519943295;
@@ -498,8 +502,8 @@ double ref_param_internal_to_external(double value, const double xmin,
     const double float_max = FLT_MAX;
     if ((xmin <= -float_max) && (xmax >= float_max)) {
         value = (value / scale) - offset;
-        value = RMAX(value, xmin);
-        value = RMIN(value, xmax);
+        value = CLAMP_LO(value, xmin);
+        value = CLAMP_HI(value, xmax);
         return value;
     } else if (xmax >= float_max) {
         value = xmin - (1.0 + sqrt(value * value + 1.0));
@@ -509,15 +513,15 @@ double ref_param_internal_to_external(double value, const double xmin,
         value = xmin + ((xmax - xmin) / 2.0) * (sin(value) + 1.0);
     }
     value = (value / scale) - offset;
-    value = RMAX(value, xmin);
-    value = RMIN(value, xmax);
+    value = CLAMP_LO(value, xmin);
+    value = CLAMP_HI(value, xmax);
     return value;
 }
 
 double ref_param_external_to_internal(double value, double xmin, double xmax,
                                       const double offset, const double scale) {
-    value = RMAX(value, xmin);
-    value = RMIN(value, xmax);
+    value = CLAMP_LO(value, xmin);
+    value = CLAMP_HI(value, xmax);
     value = (value * scale) + offset;
     xmin = (xmin * scale) + offset;
     xmax = (xmax * scale) + offset;
@@ -1033,7 +1037,62 @@ typedef struct {
     mmba_trace *trace;
     int interrupted;
     double *obs_pts, *obs_mkr; /* optional: reprojected point / corrected marker [2M] */
+    int m;                     /* residual rows: 2M + stiffness + smoothness */
 } ref_scene;
+
+/* Test hook standing in for MComputation::isInterruptRequested: the poll
+ * returns true from the `g_interrupt_after`-th poll on (sticky, like the Maya
+ * flag); < 0 never interrupts. */
+static int g_interrupt_after = -1;
+static int g_interrupt_polls = 0;
+void ref_set_interrupt_after(int k) {
+    g_interrupt_after = k;
+    g_interrupt_polls = 0;
+}
+static int interrupt_requested(ref_scene *s) {
+    const int k = g_interrupt_polls++;
+    if (g_interrupt_after >= 0 && k >= g_interrupt_after) {
+        s->interrupted = 1;
+        return 1;
+    }
+    return 0;
+}
+
+/* applyLossFunctionToErrors (adjust_base.cpp:132-187), over every row of the
+ * buffer measureErrors was handed (adjust_measureErrors.cpp:553-558). */
+static void apply_loss(int m, double *f, int type, double scale) {
+    for (int i = 0; i < m; ++i) {
+        double z = pow(f[i] / scale, 2);
+        double rho0 = z, rho1 = 1.0, rho2 = 0.0;
+        if (type == MMBA_ROBUST_LOSS_TRIVIAL) {
+            rho0 = z;
+            rho1 = 1.0;
+            rho2 = 0.0;
+        } else if (type == MMBA_ROBUST_LOSS_SOFT_L_ONE) {
+            double t = 1.0 + z;
+            rho0 = 2.0 * (pow(t, 0.5 - 1.0));
+            rho1 = pow(t, -0.5);
+            rho2 = -0.5 * pow(t, -1.5);
+        } else if (type == MMBA_ROBUST_LOSS_CAUCHY) {
+            rho0 = log1p(z);
+            double t = 1.0 + z;
+            rho1 = 1.0 / t;
+            rho2 = -1.0 / pow(t, 2.0);
+        }
+        rho0 *= pow(scale, 2.0);
+        rho2 /= pow(scale, 2.0);
+        double J_scale = rho1 + 2.0 * rho2 * pow(f[i], 2.0);
+        const double eps = DBL_EPSILON;
+        if (J_scale < eps) J_scale = eps;
+        J_scale = pow(J_scale, 0.5);
+        f[i] *= rho1 / J_scale;
+    }
+}
+
+/* gaussian() of adjust_measureErrors.cpp:106-109. */
+static double gaussian(double x, double mean, double sigma) {
+    return exp(-(pow((x - mean), 2.0) / (2.0 * (pow(sigma, 2.0)))));
+}
 
 static double attr_value(const ref_scene *s, int a, int f, double dflt) {
     if (a < 0) return dflt;
@@ -1249,6 +1308,30 @@ static void measure(ref_scene *s, const char *frame_mask, double *errors) {
         s->err_user[2 * i + 1] = dyp * factor;
         s->err_dist[i] = sqrt((dx * dx) + (dy * dy)) * image_width;
     }
+    /* Stiffness then smoothness rows (adjust_measureErrors.cpp:311-387), Maya
+     * DAG path only (the MM Scene Graph path leaves them untouched, :518);
+     * every call re-measures them, whatever the frame mask. */
+    if (s->o->scene_graph_mode != MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        const int base = 2 * p->num_obs;
+        for (int i = 0; i < p->num_stiff; ++i) {
+            const int a = p->stiff_attr[i];
+            const double v = attr_value(s, a, p->stiff_frame ? p->stiff_frame[i] : 0, 0.);
+            const double e = ((1.0 / gaussian(v, p->stiff_value[i], p->stiff_variance[i])) - 1.0);
+            s->err_user[base + i] = e * p->stiff_weight[i];
+            errors[base + i] = e * p->stiff_weight[i];
+        }
+        const int base2 = base + p->num_stiff;
+        for (int i = 0; i < p->num_smooth; ++i) {
+            const int a = p->smooth_attr[i];
+            const double v = attr_value(s, a, p->smooth_frame ? p->smooth_frame[i] : 0, 0.);
+            const double e =
+                ((1.0 / gaussian(v, p->smooth_value[i], p->smooth_variance[i])) - 1.0);
+            s->err_user[base2 + i] = e * p->smooth_weight[i];
+            errors[base2 + i] = e * p->smooth_weight[i];
+        }
+    }
+    if (s->o->robust_loss)
+        apply_loss(s->m, errors, s->o->robust_loss_type, s->o->robust_loss_scale);
 }
 
 /* setParameters (adjust_setParameters.cpp:174-276). */
@@ -1284,6 +1367,7 @@ static int scene_fun(void *c, int m, int n, const double *x, double *fvec) {
     ref_scene *s = (ref_scene *)c;
     (void)n;
     s->func_evals++;
+    if (interrupt_requested(s)) return -1; /* adjust_solveFunc.cpp:567-571 */
     set_parameters(s, x);
     measure(s, NULL, fvec);
     trace_push(s, m, fvec);
@@ -1298,7 +1382,15 @@ static int scene_jac_der(void *c, int m, int n, double *x, double *fvec,
     (void)nfev;
     const double delta = s->o->delta;
     const int F = p->num_frames;
+    if (interrupt_requested(s)) { /* solveFunc entry, adjust_solveFunc.cpp:567-571 */
+        ++(*njev);
+        return -1;
+    }
     for (int i = 0; i < n; ++i) {
+        if (interrupt_requested(s)) { /* per column, adjust_solveFunc.cpp:321-325 */
+            ++(*njev);
+            return -1;
+        }
         memcpy(s->xa, x, sizeof(double) * n);
         memcpy(s->ea, fvec, sizeof(double) * m);
         const double value = x[i];
@@ -1351,6 +1443,11 @@ static int scene_jac_dif(void *c, int m, int n, double *x, double *fvec,
         if (h == 0.) h = eps;
         x[j] = temp + h;
         s->jac_evals++;
+        if (interrupt_requested(s)) { /* every fdjac2 call is a solveFunc call */
+            x[j] = temp;
+            *nfev += n;
+            return -1;
+        }
         set_parameters(s, x);
         measure(s, NULL, s->ea);
         x[j] = temp;
@@ -1392,15 +1489,16 @@ static void scene_init(ref_scene *s, const mmba_problem *p,
     memcpy(s->attr, p->attr_values, sizeof(double) * nvals);
     s->tfm_world = (double *)malloc(sizeof(double) * 16 * (size_t)p->num_transforms * p->num_frames);
     s->pts = (double *)malloc(sizeof(double) * 2 * ((size_t)p->num_markers * p->num_frames + 1));
-    s->err_user = (double *)calloc(2 * (size_t)p->num_obs, sizeof(double));
+    s->m = 2 * p->num_obs + p->num_stiff + p->num_smooth;
+    s->err_user = (double *)calloc((size_t)s->m, sizeof(double));
     s->err_dist = (double *)calloc((size_t)p->num_obs, sizeof(double));
     s->frame_all = (char *)malloc(p->num_frames);
     memset(s->frame_all, 1, p->num_frames);
     s->frame_mask = (char *)malloc(p->num_frames);
     s->xa = (double *)malloc(sizeof(double) * p->num_params);
     s->xb = (double *)malloc(sizeof(double) * p->num_params);
-    s->ea = (double *)malloc(sizeof(double) * 2 * (size_t)p->num_obs);
-    s->eb = (double *)malloc(sizeof(double) * 2 * (size_t)p->num_obs);
+    s->ea = (double *)calloc((size_t)s->m, sizeof(double));
+    s->eb = (double *)calloc((size_t)s->m, sizeof(double));
 }
 
 static void scene_free(ref_scene *s) {
@@ -1441,8 +1539,8 @@ int ref_measure(const mmba_problem *prob, const mmba_options *opt,
     if (rc) return rc;
     ref_scene s;
     scene_init(&s, prob, opt);
-    const int m = 2 * prob->num_obs;
-    double *f = (double *)malloc(sizeof(double) * m);
+    const int m = s.m;
+    double *f = (double *)calloc((size_t)m, sizeof(double));
     if (x) set_parameters(&s, x);
     measure(&s, NULL, f);
     if (fvec) memcpy(fvec, f, sizeof(double) * m);
@@ -1464,8 +1562,8 @@ int ref_reproject_obs(const mmba_problem *prob, const mmba_options *opt, const d
     if (rc) return rc;
     ref_scene s;
     scene_init(&s, prob, opt);
-    const int m = 2 * prob->num_obs;
-    double *f = (double *)malloc(sizeof(double) * m);
+    const int m = s.m;
+    double *f = (double *)calloc((size_t)m, sizeof(double));
     s.obs_pts = point_xy;
     s.obs_mkr = marker_xy;
     if (x) set_parameters(&s, x);
@@ -1482,7 +1580,7 @@ int ref_jacobian(const mmba_problem *prob, const mmba_options *opt,
     if (rc) return rc;
     ref_scene s;
     scene_init(&s, prob, opt);
-    const int m = 2 * prob->num_obs, n = prob->num_params;
+    const int m = s.m, n = prob->num_params;
     double *xx = (double *)malloc(sizeof(double) * n);
     memcpy(xx, x, sizeof(double) * n);
     scene_fun(&s, m, n, xx, fvec);
@@ -1509,7 +1607,8 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
               double *err_dist_out, mmba_result *res, mmba_trace *trace) {
     int rc = validate(prob, opt);
     if (rc) return rc;
-    const int m = 2 * prob->num_obs, n = prob->num_params, M = prob->num_obs;
+    const int m = 2 * prob->num_obs + prob->num_stiff + prob->num_smooth;
+    const int n = prob->num_params, M = prob->num_obs;
     if (n > m) return MMBA_ERR_INVALID; /* adjust_base.cpp:864-881 */
     double t0 = now_s();
     ref_scene s;
@@ -1520,9 +1619,11 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
 
     double *fvec = (double *)calloc(m, sizeof(double));
     double init_avg = 0., init_min = 0., init_max = 0.;
-    if (opt->accept_only_better) {
+    if (opt->accept_only_better && !opt->initial_error_given) {
         measure(&s, NULL, fvec); /* scene values, before parameters are set */
         error_stats(s.err_dist, M, &init_avg, &init_min, &init_max);
+    } else if (opt->accept_only_better) {
+        init_avg = opt->initial_error_avg; /* measured by the caller */
     }
     r.error_initial_avg = init_avg;
     r.error_avg = init_avg;
@@ -1536,13 +1637,14 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
     const int ldfjac = m;
     double *fjac = (double *)calloc((size_t)m * n, sizeof(double));
     double *diag = (double *)malloc(sizeof(double) * n);
-    for (int j = 0; j < n; ++j) diag[j] = 1.0; /* paramWeightList */
+    for (int j = 0; j < n; ++j) /* paramWeightList */
+        diag[j] = prob->param_weight ? prob->param_weight[j] : 1.0;
     int *ipvt = (int *)malloc(sizeof(int) * n);
     double *qtf = (double *)malloc(sizeof(double) * n);
     double *wa1 = (double *)malloc(sizeof(double) * n);
     double *wa2 = (double *)malloc(sizeof(double) * n);
     double *wa3 = (double *)malloc(sizeof(double) * n);
-    double *wa4 = (double *)malloc(sizeof(double) * m);
+    double *wa4 = (double *)calloc((size_t)m, sizeof(double));
     s.trace = trace;
     const int mode = opt->auto_param_scale == 1 ? 1 : 2;
     const double factor = opt->tau * 100.0;
@@ -1559,6 +1661,7 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
     r.jacobian_evals = s.jac_evals;
     r.outer_iterations = njev;
     r.success = s.func_evals > 0;
+    r.user_interrupted = s.interrupted; /* out_cmdResult.solverResult.user_interrupted */
 
     /* Stats from the last measurement (B13), then accept-only-better. */
     double avg, mn, mx;
@@ -1572,7 +1675,10 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
     if (err_user_out) memcpy(err_user_out, s.err_user, sizeof(double) * m);
     if (err_dist_out) memcpy(err_dist_out, s.err_dist, sizeof(double) * M);
     if (fvec_out) memcpy(fvec_out, fvec, sizeof(double) * m);
-    memcpy(x_inout, better ? x : x0, sizeof(double) * n);
+    /* lmder leaves the solved x in paramList (adjust_cminpack_lmder.cpp:128);
+     * solveFrames writes it back only when error_is_better (:1231-1244) */
+    memcpy(x_inout, x, sizeof(double) * n);
+    (void)x0;
 
     /* RMS at the returned parameters (build's own metric). */
     {

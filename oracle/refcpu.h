@@ -96,6 +96,10 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
 int ref_jacobian(const mmba_problem *prob, const mmba_options *opt,
                  const double *x, double *fvec, double *fjac);
 
+/* Test hook for the interrupt path (MComputation::isInterruptRequested): the
+ * k-th poll (0-based) and every later one report an interrupt; k < 0 never. */
+void ref_set_interrupt_after(int k);
+
 double ref_param_external_to_internal(double value, double xmin, double xmax,
                                       double offset, double scale);
 double ref_param_internal_to_external(double value, double xmin, double xmax,

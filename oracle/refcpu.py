@@ -71,6 +71,8 @@ def lib():
         L.ref_jacobian.restype = C.c_int
         L.ref_jacobian.argtypes = [C.POINTER(abi.MmbaProblem), C.POINTER(abi.MmbaOptions), dp, dp,
                                    dp]
+        L.ref_set_interrupt_after.restype = None
+        L.ref_set_interrupt_after.argtypes = [C.c_int]
         for name in ("ref_param_external_to_internal", "ref_param_internal_to_external"):
             f = getattr(L, name)
             f.restype = C.c_double
@@ -260,8 +262,11 @@ def jacobian(problem, options, x):
     return fvec, fjac.reshape(n, m).T
 
 
-def solve(problem, options, x0=None, trace_capacity=4096):
-    """Reference CPU solve.  Returns (x, fvec, err_user, err_dist, result, fnorm_trace)."""
+def solve(problem, options, x0=None, trace_capacity=4096, interrupt_after=-1):
+    """Reference CPU solve.  Returns (x, fvec, err_user, err_dist, result, fnorm_trace).
+    ``interrupt_after`` = k >= 0: the k-th interrupt poll (0-based) and every
+    later one report an interrupt (the sticky MComputation flag)."""
+    lib().ref_set_interrupt_after(int(interrupt_after))
     p, keep = problem.to_ctypes()
     m, M = problem.num_residuals, problem.num_obs
     x = np.array(problem.x0 if x0 is None else x0, dtype=np.float64)
@@ -271,6 +276,7 @@ def solve(problem, options, x0=None, trace_capacity=4096):
     tr = abi.MmbaTrace(_dp(tbuf), trace_capacity, 0)
     rc = lib().ref_solve(C.byref(p), C.byref(options), _dp(x), _dp(fvec), _dp(eu), _dp(ed),
                          C.byref(res), C.byref(tr))
+    lib().ref_set_interrupt_after(-1)
     if rc != 0:
         raise RuntimeError("ref_solve failed rc=%d" % rc)
     return x, fvec, eu, ed, res, tbuf[:min(tr.count, trace_capacity)].copy()

@@ -69,7 +69,7 @@ def test_struct_layouts_match_header():
 
 
 def test_host_helpers(L, oracle):
-    assert L.mmba_abi_version() == 1
+    assert L.mmba_abi_version() == abi.ABI_VERSION == 2
     o = abi.MmbaOptions()
     L.mmba_options_default(C.byref(o), abi.SOLVER_TYPE_CMINPACK_LMDER)
     assert (o.iter_max, o.tau, o.eps1, o.delta, o.auto_param_scale, o.image_width) == \
@@ -91,3 +91,17 @@ def test_no_device_fails_loudly(L):
     rc = L.mmba_context_create(0, C.byref(h))
     assert rc == abi.MMBA_ERR_NO_DEVICE
     assert b"gfx950" in L.mmba_last_error()
+
+
+def test_bound_transforms_keep_nan(L, oracle):
+    """std::max<double>(v, xmin) / std::min<double>(v, xmax) (adjust_base.cpp:
+    202-203,217-218,232-233) return v when v is NaN: a NaN parameter stays NaN
+    instead of snapping to a bound, in the library and in the oracle alike."""
+    import math
+    from mayamatchmovesolver_amd.problem import FLOAT_MAX
+    nan = float("nan")
+    for lo, hi in ((-FLOAT_MAX, FLOAT_MAX), (-5.0, 5.0), (-FLOAT_MAX, 5.0), (-5.0, FLOAT_MAX)):
+        assert math.isnan(L.mmba_param_internal_to_external(nan, lo, hi, 0.0, 1.0))
+        assert math.isnan(oracle.param_internal_to_external(nan, lo, hi, 0.0, 1.0))
+        assert math.isnan(L.mmba_param_external_to_internal(nan, lo, hi, 0.0, 1.0))
+        assert math.isnan(oracle.param_external_to_internal(nan, lo, hi, 0.0, 1.0))

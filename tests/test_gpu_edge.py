@@ -1,0 +1,259 @@
+"""GPU parity on the reference edge cases the device accepts (VERDICT r1
+"what's weak" 1): every film fit with the render aspect on both sides of the
+film aspect, film offsets in both scene-graph modes (Appendix B5/B6), camera
+scale, all six rotate orders, a parented camera; the interrupt path (reason
+-1, adjust_solveFunc.cpp:321-325,567-571); lmdif stopped by maxfev (info 5,
+B9); central differences (adjust_solveFunc.cpp:405-475, B8); stiffness /
+smoothness rows (adjust_measureErrors.cpp:311-387); robust loss
+(adjust_base.cpp:132-187); paramWeightList in mode 2.  Each case: the
+library through the C ABI against the CPU oracle on the same inputs, 1e-6 on
+x and on every ||f|| of the trace, identical counts."""
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import abi, make_options, synthetic as S
+from mayamatchmovesolver_amd._lib import MmbaError
+from mayamatchmovesolver_amd.solver import Solver
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-6
+DAG, MMSG = abi.SCENE_GRAPH_MODE_MAYA_DAG, abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH
+LMDER, LMDIF = abi.SOLVER_TYPE_CMINPACK_LMDER, abi.SOLVER_TYPE_CMINPACK_LMDIF
+
+
+def check(prob, opt, oracle, ctx, interrupt_after=-1, x_tol=REL, trace_atol=1e-9):
+    xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt, interrupt_after=interrupt_after)
+    polls = [0]
+
+    def interrupt():
+        k = polls[0]
+        polls[0] += 1
+        return interrupt_after >= 0 and k >= interrupt_after
+
+    s = Solver(prob, opt, context=ctx)
+    try:
+        out = s.solve(interrupt=interrupt if interrupt_after >= 0 else None)
+    finally:
+        s.close()
+    g = out.result
+    for k in ("reason_number", "iterations", "function_evals", "jacobian_evals",
+              "user_interrupted", "error_is_better"):
+        assert g[k] == getattr(rr, k), (k, g, rr.as_dict())
+    if interrupt_after < 0:
+        assert g["outer_iterations"] == rr.outer_iterations
+    assert len(out.fnorm_trace) == len(trr)
+    if len(trr):
+        np.testing.assert_allclose(out.fnorm_trace, trr, rtol=REL, atol=trace_atol * trr[0])
+    xs = np.maximum(np.abs(xr), 1e-3)
+    assert np.max(np.abs(out.x - xr) / xs) <= x_tol, np.max(np.abs(out.x - xr) / xs)
+    scale = max(1.0, float(np.linalg.norm(fr)))
+    floor = trace_atol * trr[0] if len(trr) else 0.0
+    assert abs(g["error_final"] - rr.error_final) <= REL * scale + floor
+    assert np.linalg.norm(out.fvec - fr) <= REL * scale + floor
+    assert np.linalg.norm(out.err_user - eur) <= REL * max(1.0, float(np.linalg.norm(eur))) + floor
+    assert np.linalg.norm(out.err_dist - edr) <= REL * max(1.0, float(np.linalg.norm(edr))) + floor
+    return out, rr
+
+
+def check_measure_jacobian(prob, opt, oracle, ctx, dx=0.003):
+    s = Solver(prob, opt, context=ctx)
+    try:
+        for x in (None, prob.x0 + dx):
+            f, eu, ed, _ = s.measure(x)
+            f_ref, eu_ref, ed_ref, _ = oracle.measure(prob, opt, x)
+            np.testing.assert_allclose(f, f_ref, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(eu, eu_ref, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(ed, ed_ref, rtol=1e-12, atol=1e-12)
+        x1 = prob.x0 + dx
+        J = s.jacobian(x1)
+        _, J_ref = oracle.jacobian(prob, opt, x1)
+        scale = np.max(np.abs(J_ref))
+        assert np.max(np.abs(J - J_ref)) <= 1e-7 * scale
+    finally:
+        s.close()
+
+
+FITS = [abi.FILM_FIT_FILL, abi.FILM_FIT_HORIZONTAL, abi.FILM_FIT_VERTICAL,
+        abi.FILM_FIT_OVERSCAN]
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+@pytest.mark.parametrize("render", ["wide", "narrow"])
+@pytest.mark.parametrize("fit", FITS)
+def test_film_fit(fit, render, mode, oracle, gpu_ctx):
+    prob = S.edge_scene(film_fit=fit, render=render)
+    opt = make_options(scene_graph_mode=mode, iterations=100)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+@pytest.mark.parametrize("fit", [abi.FILM_FIT_HORIZONTAL, abi.FILM_FIT_FILL,
+                                 abi.FILM_FIT_OVERSCAN])
+def test_film_offsets(fit, mode, oracle, gpu_ctx):
+    """B5/B6: non-zero film offsets move the image in Maya DAG mode only."""
+    prob = S.edge_scene(film_fit=fit, film_offset=(0.05, -0.03), offset_shifts=(mode == DAG))
+    opt = make_options(scene_graph_mode=mode, iterations=100)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+def test_camera_scale(mode, oracle, gpu_ctx):
+    prob = S.edge_scene(camera_scale=1.7)
+    opt = make_options(scene_graph_mode=mode, iterations=100)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("parented", [False, True])
+@pytest.mark.parametrize("roo", range(6))
+def test_rotate_orders(roo, parented, oracle, gpu_ctx):
+    mode = DAG if roo % 2 else MMSG
+    prob = S.edge_scene(rotate_order=roo, parented=parented)
+    opt = make_options(scene_graph_mode=mode, iterations=100)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+def test_static_focal(mode, oracle, gpu_ctx):
+    """A static camera attribute solved beside the poses: one global parameter
+    coupling every camera-frame (arrow rows of the reduced system)."""
+    prob = S.edge_scene(static_focal=True, parented=True, rotate_order=abi.ROO_ZXY)
+    opt = make_options(scene_graph_mode=mode, iterations=100)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+# --- interrupt (reason -1) ----------------------------------------------------
+
+@pytest.mark.parametrize("solver_type", [LMDER, LMDIF])
+@pytest.mark.parametrize("k", [0, 1, 2, 7, 60, 95])
+def test_interrupt(k, solver_type, oracle, gpu_ctx):
+    """The k-th poll (0-based) of MComputation::isInterruptRequested returns
+    true: 0 = the first residual call, then the Jacobian entry and each FD
+    column (lmder) / each fdjac2 call (lmdif), trial points."""
+    prob = S.edge_scene(frames=3, bundles=12)
+    opt = make_options(solver_type=solver_type, scene_graph_mode=DAG, iterations=400)
+    out, rr = check(prob, opt, oracle, gpu_ctx, interrupt_after=k)
+    assert out.result["reason_number"] == -1 and out.result["user_interrupted"] == 1
+
+
+def test_interrupt_central(oracle, gpu_ctx):
+    prob = S.rig_scene(n_cams=3, bundles=6)
+    opt = make_options(auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL, scene_graph_mode=DAG)
+    for k in (3, 17, 40):
+        check(prob, opt, oracle, gpu_ctx, interrupt_after=k)
+
+
+# --- lmdif maxfev (B9) ----------------------------------------------------------
+
+@pytest.mark.parametrize("iterations", [10, 100, 150])
+def test_lmdif_maxfev(iterations, oracle, gpu_ctx):
+    """lmdif's maxfev counts the n FD evaluations: C1 (n = 90) at the
+    reference default iterMax 100 stops after one Jacobian (info 5)."""
+    prob = S.make_config(0)
+    opt = S.config_options(prob, iterations=iterations)
+    out, rr = check(prob, opt, oracle, gpu_ctx)
+    assert rr.reason_number == 5
+
+
+# --- central differences -----------------------------------------------------
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+@pytest.mark.parametrize("name", ["test1", "test3", "minmax_both", "weight_ratio",
+                                  "issue54_zero", "enabled_multi_f5"])
+def test_central_known_scenes(name, mode, oracle, gpu_ctx):
+    prob = S.known_scene(name)
+    opt = S.known_options(name, LMDER, mode, auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx, dx=0.01)
+    # exact-fit scenes: ||f|| runs down to roundoff, where 1e-8 of the
+    # initial ||f|| is the floor (the halved central slope, B8, converges slowly)
+    check(prob, opt, oracle, gpu_ctx, trace_atol=1e-8)
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+@pytest.mark.parametrize("kw", [dict(n_cams=3, bundles=6, seed=12), dict(solve_cam1=False)])
+def test_central_static_rig(kw, mode, oracle, gpu_ctx):
+    """Every parameter static (every FD column re-measures every row): a
+    camera rotation (global parameters) and bundles, central differences.
+    (Larger rigs with the halved central slope, B8, oscillate for 100
+    evaluations and a 1-ulp change of x0 moves their answer by 1e-3: no
+    parity bar is defined there, for the reference itself.)"""
+    prob = S.rig_scene(**kw)
+    opt = make_options(auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL, scene_graph_mode=mode)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+def test_central_refused_where_undefined(gpu_ctx):
+    """Animated parameters over several frames: the reference's central
+    Jacobian has dense garbage rows there (errorListB zero-initialised, B15),
+    so the library refuses instead of computing something else."""
+    prob = S.edge_scene()
+    opt = make_options(auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL)
+    with pytest.raises(MmbaError) as e:
+        Solver(prob, opt, context=gpu_ctx)
+    assert e.value.code == abi.MMBA_ERR_UNSUPPORTED
+
+
+# --- stiffness / smoothness rows, robust loss, paramWeightList ---------------
+
+@pytest.mark.parametrize("solver_type", [LMDER, LMDIF])
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+def test_stiffness_smoothness_rows(mode, solver_type, oracle, gpu_ctx):
+    prob = S.edge_scene(stiffness=True)
+    assert prob.num_stiff == 2 and prob.num_smooth == 1
+    opt = make_options(solver_type=solver_type, scene_graph_mode=mode, iterations=400)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    out, _ = check(prob, opt, oracle, gpu_ctx)
+    rows = out.err_user[2 * prob.num_obs:]
+    if mode == MMSG:
+        assert np.all(rows == 0.0)  # never measured on the MM Scene Graph path
+    else:
+        assert np.all(rows > 0.0)
+
+
+@pytest.mark.parametrize("solver_type", [LMDER, LMDIF])
+@pytest.mark.parametrize("loss", [abi.ROBUST_LOSS_TYPE_TRIVIAL, abi.ROBUST_LOSS_TYPE_SOFT_L_ONE,
+                                  abi.ROBUST_LOSS_TYPE_CAUCHY])
+def test_robust_loss(loss, solver_type, oracle, gpu_ctx):
+    prob = S.rig_scene(n_cams=3, bundles=6, stiffness=True)
+    opt = make_options(solver_type=solver_type, scene_graph_mode=DAG, robust_loss=1,
+                       robust_loss_type=loss, robust_loss_scale=100.0)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+def test_param_weight_mode2(oracle, gpu_ctx):
+    """auto_param_scale off: lmder's diag is paramWeightList."""
+    prob = S.edge_scene()
+    rng = np.random.Generator(np.random.PCG64(3))
+    prob.param_weight = rng.uniform(0.5, 2.0, prob.num_params)
+    opt = make_options(auto_param_scale=0, scene_graph_mode=DAG)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+def test_initial_error_given(oracle, gpu_ctx):
+    """initial_error_avg from the caller instead of the library's own
+    measurement: the same solve, accept-only-better against that value."""
+    prob = S.edge_scene()
+    opt = make_options(scene_graph_mode=DAG)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        base = s.solve()
+        _, _, ed, st = s.measure()
+        for given, better in ((st[0], True), (1e-9, False)):
+            opt2 = make_options(scene_graph_mode=DAG, initial_error_avg=given)
+            s2 = Solver(prob, opt2, context=gpu_ctx)
+            try:
+                out = s2.solve()
+            finally:
+                s2.close()
+            assert out.result["error_is_better"] == (1 if better else 0)
+            np.testing.assert_array_equal(out.x, base.x)
+            assert (out.accepted_x is out.x) == better
+    finally:
+        s.close()
