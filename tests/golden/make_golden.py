@@ -32,6 +32,8 @@ from mayamatchmovesolver_amd import abi, make_options, synthetic as S  # noqa: E
 OPT_FIELDS = ["solver_type", "iter_max", "tau", "eps1", "eps2", "eps3", "delta",
               "auto_diff_type", "auto_param_scale", "scene_graph_mode", "image_width",
               "accept_only_better"]
+# ABI-2 option fields: optional in the fixtures (0 = the reference behaviour)
+OPT_FIELDS_2 = ["robust_loss", "robust_loss_type", "robust_loss_scale"]
 RES_FIELDS = ["success", "reason_number", "iterations", "function_evals", "jacobian_evals",
               "outer_iterations", "error_final", "error_avg", "error_min", "error_max",
               "error_rms"]
@@ -58,14 +60,38 @@ def cases():
     for name, idx, kw in subsets:
         p = S.make_config(idx, **kw)
         out.append((name, p, S.config_options(p)))
+    # round 2: the edge cases and ABI-2 features (tests/test_gpu_edge.py)
+    DAG, MMSG = abi.SCENE_GRAPH_MODE_MAYA_DAG, abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH
+    edge = [
+        ("edge_fill_wide_dag", dict(film_fit=abi.FILM_FIT_FILL, render="wide"), DAG, {}),
+        ("edge_vertical_mmsg", dict(film_fit=abi.FILM_FIT_VERTICAL), MMSG, {}),
+        ("edge_overscan_narrow_dag", dict(film_fit=abi.FILM_FIT_OVERSCAN), DAG, {}),
+        ("edge_offsets_dag", dict(film_offset=(0.05, -0.03)), DAG, {}),
+        ("edge_offsets_mmsg", dict(film_offset=(0.05, -0.03), offset_shifts=False), MMSG, {}),
+        ("edge_scale_roo_zxy_parented_dag",
+         dict(camera_scale=1.7, rotate_order=abi.ROO_ZXY, parented=True), DAG, {}),
+        ("edge_stiffness_dag", dict(stiffness=True), DAG, {}),
+    ]
+    for name, kw, mode, okw in edge:
+        out.append((name, S.edge_scene(**kw), make_options(scene_graph_mode=mode, iterations=100,
+                                                           **okw)))
+    out.append(("rig_central_dag", S.rig_scene(n_cams=3, bundles=6, seed=12),
+                make_options(auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL, scene_graph_mode=DAG)))
+    out.append(("rig_softl1_stiffness_dag", S.rig_scene(n_cams=3, bundles=6, stiffness=True),
+                make_options(scene_graph_mode=DAG, robust_loss=1,
+                             robust_loss_type=abi.ROBUST_LOSS_TYPE_SOFT_L_ONE,
+                             robust_loss_scale=100.0)))
+    for name in ("enabled_single", "enabled_multi_f5", "issue54_zero", "issue54_threesixty"):
+        out.append(("known_%s_dag" % name, S.known_scene(name), S.known_options(name)))
     return out
 
 
 def options_from_npz(d):
     o = abi.MmbaOptions()
-    for f in OPT_FIELDS:
-        t = type(getattr(o, f))
-        setattr(o, f, t(d["opt_" + f]))
+    for f in OPT_FIELDS + OPT_FIELDS_2:
+        if "opt_" + f in d:
+            t = type(getattr(o, f))
+            setattr(o, f, t(d["opt_" + f]))
     return o
 
 
@@ -87,6 +113,9 @@ def main():
         d = prob.to_npz_dict()
         for f in OPT_FIELDS:
             d["opt_" + f] = np.array(getattr(opt, f))
+        if opt.robust_loss:
+            for f in OPT_FIELDS_2:
+                d["opt_" + f] = np.array(getattr(opt, f))
         rd = res.as_dict()
         for f in RES_FIELDS:
             d["res_" + f] = np.array(rd[f])
