@@ -20,9 +20,10 @@ broadcasts the RCCL id and brackets the timed region.
 
 The CPU baseline (rank 0, N = 1) is the oracle (oracle/refcpu.c, a
 cost-faithful restatement of the reference MM-Scene-Graph + cminpack path)
-timed single-threaded on bounded frame-window subsets of the same scene and
-extrapolated with t_iter = a*m*n^2 + b*n*(K*F + T*F); the full
-scene needs a 490 GB dense Jacobian and is infeasible on the CPU.
+timed single-threaded on full-density frame windows of the same scene (one LM
+iteration each), with the GPU timed on the same windows in the same run; the
+full scene needs a 490 GB dense Jacobian on the CPU, so its rate is only
+reported as a labelled extrapolation.
 """
 from __future__ import annotations
 
@@ -58,7 +59,8 @@ def parse():
                     help="per-frame solve mode (mmba_solve_per_frame) with CONC frames at "
                          "once; prints its own JSON line (not the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=60.0,
+                    help="skip the larger CPU window once this much CPU time is spent")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC passes that fill roofline.traffic")
     return ap.parse_args()
@@ -155,47 +157,86 @@ def pmc_traffic(args):
     return 2.0 * fetch + write, detail
 
 
-def cpu_baseline(cfg_index, budget_s):
-    """Time the oracle on bounded subsets and extrapolate per-iteration cost."""
+# Full-density frame windows of the workload timed on the CPU: the same
+# scene generator with the window's share of bundles (C4: 100 new bundles per
+# frame, each tracked over 4 frames), i.e. the full C4 density on F' frames.
+CPU_WINDOWS = {3: (4, 5), 2: (2, 3), 1: (2, 3), 4: (2, 3), 0: (10,)}
+
+
+def _window(cfg_index, frames):
     from mayamatchmovesolver_amd import synthetic as S
+    base = BASE_FRAMES.get(cfg_index, 10)
+    if cfg_index == 0:
+        return S.make_config(0)
+    return S.make_config(cfg_index, frames=frames, scale=frames / base)
+
+
+def cpu_baseline(cfg_index, budget_s, ctx):
+    """The oracle (oracle/refcpu.c: cost-faithful restatement of the reference
+    MM-Scene-Graph + cminpack lmder path, single thread) TIMED on full-density
+    frame windows of the benchmarked scene, one LM iteration each (lmder
+    iterMax 2: initial evaluation, one FD Jacobian + QR + lmpar, one trial
+    point); the GPU runs the identical call on the identical window in the
+    same process, so the ratio is measured, not modelled.  The full C4 scene
+    needs a 490 GB dense Jacobian on the CPU; its per-iteration time is only
+    given as a separately labelled extrapolation (t ~ m n^2, the QR term)."""
+    from mayamatchmovesolver_amd import synthetic as S
+    from mayamatchmovesolver_amd.solver import Solver
     from oracle import refcpu as R
 
     full = S.make_config(cfg_index)
-    F_full = full.num_frames
-    T_full = full.tfm_parent.size
-    K_full = full.num_markers
     n_full, m_full = full.num_params, full.num_residuals
     del full
     samples = []
     spent = 0.0
-    for frames, scale in [(8, 0.002), (12, 0.003), (16, 0.004), (20, 0.005)]:
-        if spent > budget_s:
+    for frames in CPU_WINDOWS.get(cfg_index, (2,)):
+        if samples and spent > budget_s:
             break
-        p = S.make_config(cfg_index, frames=frames, scale=scale)
-        o = S.config_options(p)
+        p = _window(cfg_index, frames)
+        o = S.config_options(p, iterations=2)
         t0 = time.perf_counter()
         _x, _f, _eu, _ed, res, _tr = R.solve(p, o)
         dt = time.perf_counter() - t0
         spent += dt
         it = max(1, res.outer_iterations)
-        feats = (p.num_residuals * p.num_params ** 2,
-                 p.num_params * (p.num_markers * p.num_frames + p.tfm_parent.size * p.num_frames))
-        samples.append((dt / it, feats, frames, scale, p.num_params, p.num_obs, it))
-    A = np.array([s[1] for s in samples], dtype=np.float64)
-    y = np.array([s[0] for s in samples])
-    coef, *_ = np.linalg.lstsq(A, y, rcond=None)
-    coef = np.maximum(coef, 0.0)
-    feats_full = np.array([m_full * n_full ** 2, n_full * (K_full * F_full + T_full * F_full)],
-                          dtype=np.float64)
-    t_iter_full = float(feats_full @ coef)
-    desc = ("oracle/refcpu.c single-thread, %d frame-window subsets of the same scene "
-            "(frames/scale/n/M/iters: %s), %.1f s of CPU; per-iteration time extrapolated "
-            "to the full scene with t = a*m*n^2 + b*n*(K*F+T*F)" % (
-                len(samples), "; ".join("%d/%.3f/%d/%d/%d" % (s[2], s[3], s[4], s[5], s[6])
-                                       for s in samples), spent))
-    return {"value": (1.0 / t_iter_full) if t_iter_full > 0 else None,
-            "unit": "LM iterations/s (extrapolated)", "cores": 1, "kind": "port",
-            "sample": desc, "t_iter_s_extrapolated": t_iter_full}
+        # the GPU on the same window and call (plan built outside the timing)
+        sv = Solver(p, o, context=ctx)
+        try:
+            sv.solve()
+            gts = []
+            for _ in range(5):
+                ctx.synchronize()
+                g0 = time.perf_counter()
+                gr = sv.solve().result
+                ctx.synchronize()
+                gts.append(time.perf_counter() - g0)
+            gt = float(np.median(gts))
+            git = max(1, gr["outer_iterations"])
+        finally:
+            sv.close()
+        samples.append({"frames": frames, "params": p.num_params, "residuals": p.num_residuals,
+                        "observations": p.num_obs, "cpu_s": dt, "cpu_lm_iterations": it,
+                        "cpu_lm_iterations_per_s": it / dt, "gpu_s": gt,
+                        "gpu_lm_iterations_per_s": git / gt,
+                        "speedup_measured": (git / gt) / (it / dt)})
+    big = samples[-1]
+    # separately labelled: the full scene's per-iteration time from the
+    # largest window by the dense-QR cost ratio m n^2 (not a measurement)
+    t_full = (big["cpu_s"] / big["cpu_lm_iterations"]) * (
+        (m_full * float(n_full) ** 2) / (big["residuals"] * float(big["params"]) ** 2))
+    desc = ("oracle/refcpu.c single thread, one LM iteration (lmder iterMax 2) on full-density "
+            "frame windows of the same scene: %s; the GPU timed on the same windows and calls "
+            "(median of 5) in this process" % "; ".join(
+                "F'=%d n=%d m=%d: CPU %.2f s, GPU %.2f ms" % (
+                    q["frames"], q["params"], q["residuals"], q["cpu_s"], 1e3 * q["gpu_s"])
+                for q in samples))
+    return {"value": big["cpu_lm_iterations_per_s"], "unit": "LM iterations/s", "cores": 1,
+            "kind": "port", "sample": desc, "windows": samples,
+            "speedup_measured_same_window": big["speedup_measured"],
+            "extrapolated_full_scene": {
+                "label": "EXTRAPOLATION, not a measurement: largest window's per-iteration time "
+                         "scaled by the dense-QR cost ratio m*n^2",
+                "t_iter_s": t_full, "lm_iterations_per_s": 1.0 / t_full}}
 
 
 def per_frame_line(args):
@@ -318,7 +359,7 @@ def main():
                             "k2_hbm": roofline}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.config, args.cpu_budget_s)
+            cpu = cpu_baseline(args.config, args.cpu_budget_s, ctx)
         r = last.result
         line = {
             "metric": "LM iterations/sec + residuals/sec (markers x frames) at 1/2/4/8 MI355X; "
@@ -355,7 +396,10 @@ def main():
                              "linear": r["time_linear_s"], "solve": r["time_solve_s"]},
         }
         if cpu and cpu.get("value"):
-            line["speedup_lm_rate_vs_cpu_port"] = lm_rate / cpu["value"]
+            # the measured ratio is on the same window (cpu_baseline.windows);
+            # this one divides the full-scene GPU rate by the CPU rate on the
+            # largest window it could run
+            line["speedup_lm_rate_vs_cpu_window"] = lm_rate / cpu["value"]
         print(json.dumps(line), flush=True)
     solver.close()
     if comm is not None:
