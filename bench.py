@@ -340,7 +340,8 @@ def main():
         chol = {"avg_ms": stats["chol_ms_avg"], "launches": stats["chol_launches"],
                 "reduced_dim": stats["reduced_dim"],
                 "solver": ["band (block cyclic reduction)", "tiled sparse Cholesky",
-                           "dense blocked Cholesky (MFMA GEMM trailing updates)"][kind],
+                           "dense blocked Cholesky (MFMA GEMM trailing updates)",
+                           "block diagonal + arrow (per camera-frame Cholesky)"][kind],
                 "note": "time per factorisation (+ fused forward solve), HIP events"}
         if kind == 2 and stats["chol_ms_avg"] > 0:
             tf = stats["chol_flops"] / (stats["chol_ms_avg"] * 1e-3) / 1e12

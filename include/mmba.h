@@ -430,7 +430,8 @@ typedef struct mmba_kernel_stats {
     int32_t reduced_dim;    /* n_r = camera-frame + global parameters     */
     int32_t reduced_kind;   /* 0 band (block cyclic reduction / partitioned),
                                1 tiled sparse Cholesky, 2 dense blocked
-                               Cholesky (chol_flops is exact only for 2) */
+                               Cholesky (chol_flops is exact only for 2),
+                               3 block diagonal + arrow (no solved bundle) */
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);

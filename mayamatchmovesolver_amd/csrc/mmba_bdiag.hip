@@ -1,0 +1,322 @@
+// mmba_bdiag.hip -- block-diagonal + arrow reduced system (no bundle is
+// solved: C2 pose + focal per frame, C5 poses + a shared lens, and every
+// per-frame solve).  Without a solved bundle no term couples two
+// camera-frames, so S is block diagonal in the camera-frame blocks (pc <= 10
+// rows each) plus nG dense arrow rows (global parameters).  The Cholesky of
+// such a matrix needs no cyclic reduction: each block is factored on its own
+// (one wave per block, all blocks at once), the arrow's Schur complement
+//   T = S_GG - sum_b Y_b^T Y_b,  Y_b = C_b^-1 S_bG
+// is one small dense factorisation, and the back substitution is again one
+// wave per block.  Without global parameters the whole damped solve
+// (A + lam D^2) x = g is ONE launch.  Same contract as the band solvers
+// (band_factor_forward / band_forward / band_backward): reduced-order
+// vectors, y = L^-1 r of the permuted factor, ||y|| as lmpar's Newton term.
+#include "mmba_kernels.h"
+#include "mmba_plan.h"
+
+namespace mmba {
+
+__device__ __forceinline__ double bd_rsq(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+__device__ __forceinline__ double bd_rdlane(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Lane roles of one block's wave: rows 0..PC-1 of the block, then one
+// right-hand-side lane per arrow row (Y_b columns), then the rhs lane.
+constexpr int BD_G0 = 16;  // first arrow lane
+constexpr int BD_R = 32;   // right-hand-side lane
+
+// Augmented Cholesky of one block by one wave (bcr_chol_aug_wave's scheme
+// with a register-only column broadcast: PC <= 10 is short enough for
+// v_readlane per entry): lane i < PC holds row i of [S_b], every
+// right-hand-side lane holds its column; afterwards rows hold C and the
+// right-hand-side lanes (C^-1 b)^T.  Rows >= pc are identity padding.
+template <int PC>
+__device__ __forceinline__ void bd_chol_aug(double (&a)[PC], double &rsl, bool &bad) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < PC; ++j) {
+        double d = bd_rdlane(a[j], j);
+        if (!(d > 0.) || !isfinite(d)) {
+            bad = true;
+            d = 1.;
+        }
+        const double rs = bd_rsq(d);
+        const double l = (lane > j) ? a[j] * rs : 0.;
+        a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+        if (lane == j) rsl = rs;
+#pragma unroll
+        for (int c = j + 1; c < PC; ++c) a[c] = fma(-l, bd_rdlane(l, c), a[c]);
+    }
+}
+
+// Block b (camera-frame cf = B.blk_cf[b]) of S from the band layout, its
+// arrow columns and rhs; factor; store C (diagonal = 1/C_jj), Y_b and y_b;
+// the arrow partials Y_b^T Y_b, Y_b^T y_b.  One wave per block, four blocks
+// per workgroup.
+template <int PC>
+__global__ void __launch_bounds__(256) k_bd_factor(BdDev B, const double *__restrict__ r,
+                                                   double *y, int *fail) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B.nblk) return;
+    const int r0 = B.roff[b], pc = B.pc[b], nG = B.nG, w = B.w, W1 = w + 1;
+    double a[PC];
+#pragma unroll
+    for (int c = 0; c < PC; ++c) {
+        double v = 0.;
+        if (lane < PC) {
+            if (lane < pc) {
+                if (c < pc && c <= lane) v = B.Bd[(size_t)(r0 + lane) * W1 + (c - lane + w)];
+            } else if (c == lane) {
+                v = 1.;  // identity padding
+            }
+        } else if (lane >= BD_G0 && lane < BD_G0 + nG) {
+            v = c < pc ? B.Ga[(size_t)(lane - BD_G0) * B.nb + r0 + c] : 0.;
+        } else if (lane == BD_R) {
+            v = c < pc ? r[r0 + c] : 0.;
+        }
+        a[c] = v;
+    }
+    double rsl = 0.;
+    bool bad = false;
+    bd_chol_aug<PC>(a, rsl, bad);
+    if (bad && lane == 0) atomicOr(fail, 1);
+    double *FC = B.FC + (size_t)b * PC * PC;
+    if (lane < PC) {
+#pragma unroll
+        for (int c = 0; c < PC; ++c) FC[lane * PC + c] = (c == lane) ? rsl : (c < lane ? a[c] : 0.);
+    } else if (lane >= BD_G0 && lane < BD_G0 + nG) {
+#pragma unroll
+        for (int c = 0; c < PC; ++c) B.FY[((size_t)b * NGMAX + (lane - BD_G0)) * PC + c] = a[c];
+    } else if (lane == BD_R) {
+#pragma unroll
+        for (int c = 0; c < PC; ++c)
+            if (c < pc) y[r0 + c] = a[c];
+    }
+    if (nG > 0) {
+        // arrow partials (Y^T Y)[q][q2] and (Y^T y)[q], one entry per lane,
+        // from the wave's Y / y staged in LDS (row NGMAX = y)
+        __shared__ double sy[4][(NGMAX + 1) * PC];
+        double *my = sy[threadIdx.x >> 6];
+        if (lane >= BD_G0 && lane < BD_G0 + nG) {
+#pragma unroll
+            for (int c = 0; c < PC; ++c) my[(lane - BD_G0) * PC + c] = a[c];
+        } else if (lane == BD_R) {
+#pragma unroll
+            for (int c = 0; c < PC; ++c) my[NGMAX * PC + c] = a[c];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int e = lane; e < nG * nG + nG; e += 64) {
+            double acc = 0.;
+            const int q = e < nG * nG ? e / nG : e - nG * nG;
+            const int q2 = e < nG * nG ? e % nG : NGMAX;
+            for (int c = 0; c < pc; ++c) acc = fma(my[q * PC + c], my[q2 * PC + c], acc);
+            if (q2 < NGMAX)
+                B.Zc[(size_t)b * NGMAX * NGMAX + q * NGMAX + q2] = acc;
+            else
+                B.gpart[(size_t)b * NGMAX + q] = acc;
+        }
+    }
+}
+
+// Back substitution x_b = C_b^-T (y_b - Y_b x_G) from the stored factor;
+// with xs the solution is also scattered to parameter order.  One wave per
+// block; lane i < pc owns row i.
+template <int PC>
+__global__ void __launch_bounds__(256) k_bd_back(BdDev B, const double *__restrict__ y, double *x,
+                                                 double *xs) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B.nblk) return;
+    const int r0 = B.roff[b], pc = B.pc[b], nG = B.nG, nb = B.nb;
+    const double *FC = B.FC + (size_t)b * PC * PC;
+    double cc[PC];  // column lane of C (diagonal 1/C_jj)
+    double v = 0.;
+    if (lane < PC) {
+#pragma unroll
+        for (int u = 0; u < PC; ++u) cc[u] = u >= lane ? FC[u * PC + lane] : 0.;
+        if (lane < pc) {
+            v = y[r0 + lane];
+            for (int q = 0; q < nG; ++q)
+                v = fma(-B.FY[((size_t)b * NGMAX + q) * PC + lane], x[nb + q], v);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < PC; ++u) cc[u] = 0.;
+    }
+#pragma unroll
+    for (int u = PC - 1; u >= 0; --u) {
+        if (lane == u) v *= cc[u];
+        const double xu = bd_rdlane(v, u);
+        if (lane < u) v = fma(-cc[u], xu, v);
+    }
+    if (lane < pc) {
+        const int R = r0 + lane;
+        x[R] = v;
+        if (xs) xs[B.row_param[R]] = v;
+    }
+}
+
+// Forward solve only (lmpar's Newton term): y_b = C_b^-1 w_b from the stored
+// factor, the arrow partials Y_b^T y_b.  One wave per block.
+template <int PC>
+__global__ void __launch_bounds__(256) k_bd_fwd(BdDev B, const double *__restrict__ wv,
+                                                double *y) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B.nblk) return;
+    const int r0 = B.roff[b], pc = B.pc[b], nG = B.nG;
+    const double *FC = B.FC + (size_t)b * PC * PC;
+    double cr[PC];  // row lane of C (diagonal 1/C_ii)
+    double v = 0.;
+    if (lane < PC) {
+#pragma unroll
+        for (int u = 0; u < PC; ++u) cr[u] = u <= lane ? FC[lane * PC + u] : 0.;
+        if (lane < pc) v = wv[r0 + lane];
+    } else {
+#pragma unroll
+        for (int u = 0; u < PC; ++u) cr[u] = 0.;
+    }
+#pragma unroll
+    for (int u = 0; u < PC; ++u) {
+        if (lane == u) v *= cr[u];
+        const double yu = bd_rdlane(v, u);
+        if (lane > u) v = fma(-cr[u], yu, v);
+    }
+    if (lane < pc) y[r0 + lane] = v;
+    if (nG > 0) {
+        double yv[PC];
+#pragma unroll
+        for (int c = 0; c < PC; ++c) yv[c] = bd_rdlane(v, c);
+        if (lane < nG) {
+            double acc = 0.;
+            const double *Yq = B.FY + ((size_t)b * NGMAX + lane) * PC;
+            for (int c = 0; c < pc; ++c) acc = fma(Yq[c], yv[c], acc);
+            B.gpart[(size_t)b * NGMAX + lane] = acc;
+        }
+    }
+}
+
+// Arrow corner: T = S_GG - sum_b Y_b^T Y_b = Ct Ct^T (dense, one wave, lane =
+// row), y_G = Ct^-1 (r_G - sum_b Y_b^T y_b); with back: x_G = Ct^-T y_G (the
+// back kernel then needs it).  factor = false: forward with the stored Ct.
+__global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restrict__ r, double *y,
+                                                double *x, double *xs, int factor, int *fail) {
+    __shared__ double zs[NGMAX * NGMAX], gs[NGMAX];
+    const int lane = threadIdx.x, nG = B.nG, nb = B.nb;
+    // sums over blocks: lanes stride, fixed xor tree
+    for (int e = 0; e < nG * NGMAX + NGMAX; ++e) {
+        const bool mat = e < nG * NGMAX;
+        if (mat && e % NGMAX >= nG) continue;
+        if (!mat && e - nG * NGMAX >= nG) continue;
+        if (mat && !factor) continue;
+        double v = 0.;
+        for (int b = lane; b < B.nblk; b += 64)
+            v += mat ? B.Zc[(size_t)b * NGMAX * NGMAX + e] : B.gpart[(size_t)b * NGMAX + (e - nG * NGMAX)];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) {
+            if (mat) zs[e] = v;
+            else gs[e - nG * NGMAX] = v;
+        }
+    }
+    __syncthreads();
+    double *Ct = B.FT;  // NGMAX x NGMAX lower, diagonal 1/C_jj
+    if (factor) {
+        // row `lane` of T
+        double a[NGMAX];
+#pragma unroll
+        for (int c = 0; c < NGMAX; ++c) {
+            double v = 0.;
+            if (lane < nG && c <= lane) v = B.Gd[lane * NGMAX + c] - zs[lane * NGMAX + c];
+            else if (lane < NGMAX && lane >= nG && c == lane) v = 1.;
+            a[c] = v;
+        }
+        double rsl = 0.;
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < NGMAX; ++j) {
+            double d = bd_rdlane(a[j], j);
+            if (!(d > 0.) || !isfinite(d)) {
+                bad = true;
+                d = 1.;
+            }
+            const double rs = bd_rsq(d);
+            const double l = (lane > j) ? a[j] * rs : 0.;
+            a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+            if (lane == j) rsl = rs;
+#pragma unroll
+            for (int c = j + 1; c < NGMAX; ++c) a[c] = fma(-l, bd_rdlane(l, c), a[c]);
+        }
+        if (bad && lane == 0) atomicOr(fail, 1);
+        if (lane < NGMAX)
+#pragma unroll
+            for (int c = 0; c < NGMAX; ++c) Ct[lane * NGMAX + c] = c == lane ? rsl : (c < lane ? a[c] : 0.);
+        __syncthreads();
+    }
+    // y_G = Ct^-1 (r_G - gs), x_G = Ct^-T y_G: serial in one lane (nG <= 16)
+    if (lane == 0) {
+        double v[NGMAX];
+        for (int q = 0; q < nG; ++q) {
+            double s = r[nb + q] - gs[q];
+            for (int c = 0; c < q; ++c) s = fma(-Ct[q * NGMAX + c], v[c], s);
+            v[q] = s * Ct[q * NGMAX + q];
+            y[nb + q] = v[q];
+        }
+        if (x) {
+            for (int q = nG - 1; q >= 0; --q) {
+                double s = v[q];
+                for (int c = q + 1; c < nG; ++c) s = fma(-Ct[c * NGMAX + q], v[c], s);
+                v[q] = s * Ct[q * NGMAX + q];
+                x[nb + q] = v[q];
+                if (xs) xs[B.row_param[nb + q]] = v[q];
+            }
+        }
+    }
+}
+
+template <int PC>
+static void bd_factor_k(hipStream_t s, const BdDev &D, int *fail, const double *r, double *y,
+                        double *x, double *xs) {
+    const int g = (D.nblk + 3) / 4;
+    if (D.nG == 0) {
+        // factor + forward + back in one launch
+        k_bd_factor<PC><<<g, 256, 0, s>>>(D, r, y, fail);
+        if (x) k_bd_back<PC><<<g, 256, 0, s>>>(D, y, x, xs);
+        return;
+    }
+    k_bd_factor<PC><<<g, 256, 0, s>>>(D, r, y, fail);
+    k_bd_root<<<1, 64, 0, s>>>(D, r, y, x, xs, 1, fail);
+    if (x) k_bd_back<PC><<<g, 256, 0, s>>>(D, y, x, xs);
+}
+
+void bd_factor_solve(hipStream_t s, const BdDev &D, int *fail, const double *r, double *y,
+                     double *x, double *xs) {
+    if (D.PC <= 8)
+        bd_factor_k<8>(s, D, fail, r, y, x, xs);
+    else
+        bd_factor_k<PCMAX>(s, D, fail, r, y, x, xs);
+}
+
+void bd_forward(hipStream_t s, const BdDev &D, const double *w, double *y) {
+    const int g = (D.nblk + 3) / 4;
+    if (D.PC <= 8)
+        k_bd_fwd<8><<<g, 256, 0, s>>>(D, w, y);
+    else
+        k_bd_fwd<PCMAX><<<g, 256, 0, s>>>(D, w, y);
+    if (D.nG > 0) k_bd_root<<<1, 64, 0, s>>>(D, w, y, nullptr, nullptr, 0, nullptr);
+}
+
+}  // namespace mmba

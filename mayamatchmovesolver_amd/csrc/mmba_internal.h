@@ -80,8 +80,21 @@ struct BcrDev {
     double *xs = nullptr;
 };
 
+// Block-diagonal + arrow reduced system (mmba_bdiag.hip): no solved bundle,
+// so the camera-frame blocks are uncoupled; block b = reduced rows
+// [roff[b], roff[b] + pc[b]), pc <= PC <= PCMAX.
+struct BdDev {
+    int nblk = 0, nb = 0, nG = 0, w = 0, PC = 0;
+    const int *roff = nullptr, *pc = nullptr;
+    const double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr;  // input (band layout)
+    double *FC = nullptr, *FY = nullptr, *Zc = nullptr, *gpart = nullptr, *FT = nullptr;
+    const int *row_param = nullptr;  // reduced row -> parameter (scatter of x)
+};
+
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
+    bool use_bd = false;                     // block diagonal + arrow (no solved bundle)
+    BdDev bd;
     bool use_bcr = false;                    // w <= 32: block cyclic reduction
     BcrDev bcr;
     // sharded BCR: Bd | Ga | Gd | rhs contiguous; every shard writes its own

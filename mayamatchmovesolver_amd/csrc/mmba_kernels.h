@@ -51,13 +51,17 @@ void launch_reproject(hipStream_t s, const DevProblem &P, const double *recs, do
                       double *mkr);
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out = nullptr,
-                     unsigned int *ticket = nullptr);
+                     unsigned int *ticket = nullptr, double *dist = nullptr);
+// errorDistanceList statistics (compute_error_stats) of ed: out[0] = sum of
+// the finite entries, out[1] = -min, out[2] = max (partial rows rstride apart)
+void launch_dist_stats(hipStream_t s, const DevProblem &P, const double *ed, double *partial,
+                       int nparts, int rstride, double *out);
 // launch_residual (partials only) plus ||J p||^2 partials of the same blocks
 // into partial_jp (k_jp_sumsq's sum, one launch)
 void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,
-                        double *partial_jp);
+                        double *partial_jp, double *dist = nullptr);
 // Second evaluation of central FD columns (lmder, autoDiffType central):
 // records / bundle records / perturbed values at x + deltaB and the column
 // factor 0.5 / (|dA| + |dB|) (0: forward column).  recs == nullptr: forward.
@@ -166,6 +170,12 @@ void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
                 const double *r = nullptr, double *y = nullptr);
 void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
 void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
+// Block-diagonal + arrow solver (mmba_bdiag.hip): factor S, y = L^-1 r and,
+// with x, the solution (scattered to parameter order into xs when non-null).
+void bd_factor_solve(hipStream_t s, const BdDev &D, int *fail, const double *r, double *y,
+                     double *x, double *xs);
+// y = L^-1 w with the stored factor (lmpar's Newton term)
+void bd_forward(hipStream_t s, const BdDev &D, const double *w, double *y);
 // mask (nullable): entries this shard owns
 void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double *partial,
                   int nparts, double *out, const int *mask = nullptr,

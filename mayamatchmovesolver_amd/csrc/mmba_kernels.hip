@@ -6,6 +6,7 @@
 //   k_chol_update                    fp64 MFMA (v_mfma_f64_16x16x4_f64),
 //                                    64x64 tiles staged in LDS.
 //   everything else                  small O(n) vector work.
+#include <cfloat>
 #include <cstdlib>
 
 #include "mmba_geom.h"
@@ -261,7 +262,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
                                                   const int *__restrict__ jcol,
                                                   const int *__restrict__ nloc,
                                                   const double *__restrict__ pstep,
-                                                  double *partial_jp) {
+                                                  double *partial_jp, double *dist) {
     __shared__ double red[256];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     double s = 0., sj = 0.;
@@ -294,6 +295,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
             eu[2 * i + 1] = r.uy;
             ed[i] = r.dist;
         }
+        if (dist) dist[i] = r.dist;  // errorDistanceList of this point (RMS at the accepted x)
         if (own_obs(P, i)) {
             s = r.ex * r.ex + r.ey * r.ey;
             if constexpr (JP) {
@@ -808,7 +810,8 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
         } else if (e < NE) {
             g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
         } else {
-            const int a = (e - NE) / NG, q = (e - NE) % NG;
+            constexpr int NGd = NG > 0 ? NG : 1;  // e < NE always when NG == 0
+            const int a = (e - NE) / NGd, q = (e - NE) % NGd;
             if (q < P.nG) Acg[((size_t)cf * PCMAX + a) * NGMAX + q] = v;
         }
     }
@@ -2160,13 +2163,15 @@ void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
 // for the attribute rows (k_rows_eval writes entry nblk(M, 256)).
 int residual_blocks(const DevProblem &P) { return nblk(P.M, 256) + (P.nrows > 0 ? 1 : 0); }
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
-                     double *ed, double *partial, double *out, unsigned int *ticket) {
+                     double *ed, double *partial, double *out, unsigned int *ticket, double *dist) {
     if (P.all_bnd_fast && P.no_lens)
         k_residual<false, true><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr);
+            P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
+            dist);
     else
         k_residual<false, false><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr);
+            P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
+            dist);
     if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, residual_blocks(P), out);
 }
 // Per-observation reprojection (FlatScene::evaluate's out_point_list /
@@ -2200,13 +2205,84 @@ void launch_reproject(hipStream_t s, const DevProblem &P, const double *recs, do
 void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,
-                        double *partial_jp) {
+                        double *partial_jp, double *dist) {
     if (P.all_bnd_fast && P.no_lens)
         k_residual<true, true><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp);
+            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
     else
         k_residual<true, false><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp);
+            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
+}
+
+// compute_error_stats (adjust_base.cpp:346-372) on the device: per block the
+// sum, minimum and maximum of the finite entries of errorDistanceList (own
+// observations) -> partial rows 0 / 1 / 2 (1 holds -min so every row folds
+// with max or sum); k_dist_stats_fin folds them into out[0..2] = sum, -min,
+// max.  The average is sum / M over every observation, as the reference
+// divides by the marker-error count.
+__global__ void __launch_bounds__(256) k_dist_stats(DevProblem P, const double *__restrict__ ed,
+                                                    double *partial, int rstride) {
+    __shared__ double red[3][256];
+    double sm = 0., nmn = -DBL_MAX, mx = -0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < P.M; i += gridDim.x * blockDim.x) {
+        if (!own_obs(P, i)) continue;
+        const double e = ed[i];
+        if (!isfinite(e)) continue;
+        sm += e;
+        nmn = fmax(nmn, -e);
+        mx = fmax(mx, e);
+    }
+    red[0][threadIdx.x] = sm;
+    red[1][threadIdx.x] = nmn;
+    red[2][threadIdx.x] = mx;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] = fmax(red[1][threadIdx.x], red[1][threadIdx.x + w]);
+            red[2][threadIdx.x] = fmax(red[2][threadIdx.x], red[2][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x] = red[0][0];
+        partial[rstride + blockIdx.x] = red[1][0];
+        partial[2 * rstride + blockIdx.x] = red[2][0];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dist_stats_fin(const double *__restrict__ partial,
+                                                        int n, int rstride, double *out) {
+    __shared__ double red[3][256];
+    double sm = 0., nmn = -DBL_MAX, mx = -0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        sm += partial[i];
+        nmn = fmax(nmn, partial[rstride + i]);
+        mx = fmax(mx, partial[2 * rstride + i]);
+    }
+    red[0][threadIdx.x] = sm;
+    red[1][threadIdx.x] = nmn;
+    red[2][threadIdx.x] = mx;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] = fmax(red[1][threadIdx.x], red[1][threadIdx.x + w]);
+            red[2][threadIdx.x] = fmax(red[2][threadIdx.x], red[2][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = red[0][0];
+        out[1] = red[1][0];
+        out[2] = red[2][0];
+    }
+}
+
+void launch_dist_stats(hipStream_t s, const DevProblem &P, const double *ed, double *partial,
+                       int nparts, int rstride, double *out) {
+    k_dist_stats<<<nparts, 256, 0, s>>>(P, ed, partial, rstride);
+    k_dist_stats_fin<<<1, 256, 0, s>>>(partial, nparts, rstride, out);
 }
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,

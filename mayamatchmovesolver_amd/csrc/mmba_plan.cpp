@@ -512,6 +512,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     stale_host = stale;
     param_frame_host.assign(pr->param_frame, pr->param_frame + n);
+    pmin_h.assign(pr->param_min, pr->param_min + n);
+    pmax_h.assign(pr->param_max, pr->param_max + n);
+    poff_h.assign(pr->param_offset, pr->param_offset + n);
+    pscale_h.assign(pr->param_scale, pr->param_scale + n);
+    param_vidx.resize(n);
+    for (int p = 0; p < n; ++p) {
+        const int a = pr->param_attr[p];
+        param_vidx[p] = pr->attr_offset[a] + (pr->attr_animated[a] ? pr->param_frame[p] : 0);
+    }
 
     // ---- symbolic tile structure of the reduced system ----
     NT = (nR > 0 && !band) ? (nR + TILE - 1) / TILE : 0;
@@ -880,6 +889,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_S = dalloc<double>((size_t)nslots * TILE * TILE);
         d_Linv = dalloc<double>((size_t)NT * TILE * TILE);
     }
+    cfblk_roff.clear();
+    cfblk_pc.clear();
+    for (int cf = 0; cf < ncf; ++cf)
+        if (cf_pc[cf] > 0) {
+            cfblk_roff.push_back(cf_roff[cf]);
+            cfblk_pc.push_back(cf_pc[cf]);
+        }
     if (band) setup_band();
     if (band && std::getenv("MMBA_PROBE")) {
         d_probe = dalloc<long long>(4);
@@ -907,6 +923,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     for (double *b : {d_f, d_ftrial, d_eu, d_eu_s})
         MMBA_HIP(hipMemsetAsync(b, 0, sizeof(double) * m, s));
     d_Jrow = dalloc<double>(nrows);
+    d_dist_x = dalloc<double>(M);
+    d_dist_t = dalloc<double>(M);
     d_recs = dalloc<double>((size_t)nvar * CAMREC);
     if (central) {
         d_ext_pertB = dalloc<double>(n);
@@ -935,9 +953,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_wR = dalloc<double>(nRpad);
     d_usq = dalloc<double>(nB);
     pw = std::max(std::max(nparts, residual_blocks(P)), ncf + (nB + 255) / 256);
-    d_partial = dalloc<double>((size_t)8 * pw);
+    d_partial = dalloc<double>((size_t)8 * pw);  // rows 0..7 (launch_dist_stats: 0..2)
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
+    if (bs.use_bd) {
+        std::vector<int> row_param(std::max(nR, 1), -1);
+        for (int p = 0; p < n; ++p)
+            if (p_class[p] != PC_B && p_pos[p] >= 0 && p_pos[p] < nR) row_param[p_pos[p]] = p;
+        bs.bd.row_param = upload(row_param);
+    }
     if (bs.use_bcr && bs.bcr.flags) {
         bs.bcr.fail = d_fail;
         if (nranks == 1) {
@@ -968,6 +992,46 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
 // mmba_band.hip) and the device buffers of the band factorisation.
 void Plan::setup_band(int Pforce) {
     const int nb = nR - nG, w = bw;
+    // No solved bundle (C2, C5, per-frame solves): the camera-frame blocks are
+    // uncoupled, so S is block diagonal + arrow (mmba_bdiag.hip);
+    // MMBA_BDIAG=0 keeps the band solvers (A/B)
+    {
+        const char *e = std::getenv("MMBA_BDIAG");
+        const bool off = e && std::atoi(e) == 0;
+        if (!off && nB_solved == 0 && nranks == 1 && !cfblk_pc.empty() && Pforce == 0) {
+            bs.use_bd = true;
+            bs.P = 1;
+            bs.w = w;
+            bs.nb = nb;
+            bs.nG = nG;
+            bs.Bd = dalloc<double>((size_t)nb * (w + 1));
+            bs.Ga = dalloc<double>(std::max<size_t>(1, (size_t)nG * nb));
+            bs.Gd = dalloc<double>(NGMAX * NGMAX);
+            MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (w + 1), s));
+            MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * std::max<size_t>(1, (size_t)nG * nb), s));
+            MMBA_HIP(hipMemsetAsync(bs.Gd, 0, sizeof(double) * NGMAX * NGMAX, s));
+            BdDev &D = bs.bd;
+            D.nblk = (int)cfblk_pc.size();
+            D.nb = nb;
+            D.nG = nG;
+            D.w = w;
+            int pmax = 1;
+            for (int v : cfblk_pc) pmax = std::max(pmax, v);
+            D.PC = pmax <= 8 ? 8 : PCMAX;
+            D.roff = upload(cfblk_roff);
+            D.pc = upload(cfblk_pc);
+            D.Bd = bs.Bd;
+            D.Ga = bs.Ga;
+            D.Gd = bs.Gd;
+            D.FC = dalloc<double>((size_t)D.nblk * PCMAX * PCMAX);
+            D.FY = dalloc<double>((size_t)D.nblk * NGMAX * PCMAX);
+            D.Zc = dalloc<double>((size_t)D.nblk * NGMAX * NGMAX);
+            D.gpart = dalloc<double>((size_t)D.nblk * NGMAX);
+            D.FT = dalloc<double>(NGMAX * NGMAX);
+            d_ymask = upload(std::vector<int>(std::max(nR, 1), 1));
+            return;
+        }
+    }
     // Unsharded and w <= 32: block cyclic reduction (mmba_bcr.hip).  Pforce < 0
     // forces it, Pforce > 0 forces the partitioned chain; MMBA_BAND_BCR=0
     // disables it (A/B measurements).

@@ -141,6 +141,9 @@ struct Plan {
     std::vector<double> param_weight;  // paramWeightList (diag in mode 2)
     std::vector<int> stale_host;       // stale-column table (B13), host copy
     std::vector<int> param_frame_host;
+    // solved camera-frame blocks (reduced rows [roff, roff + pc)), for the
+    // block-diagonal solver
+    std::vector<int> cfblk_roff, cfblk_pc;
     double *d_recs = nullptr, *d_brec = nullptr;
     double *d_J = nullptr;
     int *d_jcol = nullptr, *d_nloc = nullptr;
@@ -232,7 +235,11 @@ struct Plan {
         SL_RMS = 12,
         SL_NCENT = 13,  // central FD columns of the last Jacobian (second evaluations)
         SL_LAST = 13,
-        NSLOT = 16
+        // errorDistanceList statistics (launch_dist_stats): sum, -min, max
+        SL_ESUM = 16,
+        SL_ENMIN = 17,
+        SL_EMAX = 18,
+        NSLOT = 24
     };
     void read_slots(int lo, int hi);
     bool spin_wait = true;  // MMBA_SPIN_WAIT=0: blocking synchronisation
@@ -240,8 +247,17 @@ struct Plan {
     double read_scalar(int slot = 0);
     void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
     double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
-    void fun_enqueue(const double *dx, double *df, double *eu, double *ed);
-    double fun(const double *dx, double *df, double *eu, double *ed);
+    void fun_enqueue(const double *dx, double *df, double *eu, double *ed,
+                     double *dist = nullptr);
+    double fun(const double *dx, double *df, double *eu, double *ed, double *dist = nullptr);
+    // errorDistanceList of the accepted x and of the pending trial point
+    // (swapped on acceptance): the RMS at the returned x needs no extra
+    // evaluation
+    double *d_dist_x = nullptr, *d_dist_t = nullptr;
+    std::vector<long long> param_vidx;  // attribute-value index of each parameter
+    std::vector<double> pmin_h, pmax_h, poff_h, pscale_h;  // bound transform (host)
+    // compute_error_stats of ed on the device -> avg, min, max (host)
+    void error_stats_device(const double *ed, double *avg, double *mn, double *mx);
     // with lm: the lmder bookkeeping after the normal equations is fused
     // into the column-norm launch (k_jac_epilogue); scalars -> SL_ZERO,
     // SL_XN2 (first pass), SL_GNORM (fnorm != 0)
