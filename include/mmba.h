@@ -394,19 +394,34 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out,
  * parameters keyed at it plus every static parameter; results[num_frames]
  * gets each frame's SolverResult and x_inout the parameters each frame's
  * solveFrames writes back (the solved values when error_is_better, else the
- * frame's starting values).  Without static parameters the frames share
- * nothing and are solved together on the device by one batched LM (one
- * workgroup per frame, MINPACK control flow per frame on the device); with
- * one they are chained in order, as in the reference.  The first frame with
- * no parameters or fewer residuals than parameters stops the sequence (later
- * frames: success = 0).  cb->interrupt is polled before every frame batch;
- * frames that start after it returned non-zero report reason_number -1
- * without moving, as each solveFrames call of the reference does once the
- * interrupt flag is set.  max_concurrency: frames per batch (0 = all). */
+ * frame's starting values).  The first frame with no parameters or fewer
+ * residuals than parameters stops the sequence (later frames: success = 0).
+ *   - No static parameter, every parameter on one camera-frame, forward
+ *     differences, no robust loss / attribute rows, <= 8 cameras and <= 32
+ *     parameters per frame: every frame is solved in ONE launch (one
+ *     workgroup runs one frame's whole lmder / lmdif, mmba_batch.hip).
+ *     cb->interrupt is polled on the calling thread while the launch runs;
+ *     once it returns non-zero every frame stops at its next evaluation or
+ *     Jacobian poll (reason_number -1).  max_concurrency is not used.
+ *     MMBA_PERFRAME_BATCH=0 in the environment selects the path below.
+ *   - Otherwise one plan per frame: frames without a static parameter run
+ *     max_concurrency at a time (0 = all) on host worker threads, each with
+ *     its own stream; with a static parameter they are chained in order, as
+ *     in the reference, and cb->interrupt is polled at every reference poll
+ *     point. */
 int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
                          const mmba_options *opt, double *x_inout,
                          mmba_result *results /* [num_frames] */, int32_t max_concurrency,
                          const mmba_callbacks *cb);
+
+/* Per-frame solve mode on a plan of the whole problem (plan caching: the
+ * caller builds the plan once and solves every frame per call in one
+ * launch).  Same semantics as the batched path of mmba_solve_per_frame;
+ * results[num_frames].  MMBA_ERR_UNSUPPORTED (mmba_last_error says why)
+ * when the plan's parameters do not split into independent frames -- use
+ * mmba_solve_per_frame then. */
+int mmba_plan_solve_per_frame(mmba_plan *plan, double *x_inout, mmba_result *results,
+                              const mmba_callbacks *cb);
 
 /* One-shot convenience: plan_create + plan_solve + plan_destroy. */
 int mmba_solve(mmba_context *ctx, const mmba_problem *prob,

@@ -222,6 +222,7 @@ EXPORTED_SYMBOLS = [
     "mmba_plan_measure",
     "mmba_plan_reproject",
     "mmba_solve_per_frame",
+    "mmba_plan_solve_per_frame",
     "mmba_plan_jacobian",
     "mmba_plan_solve",
     "mmba_solve",

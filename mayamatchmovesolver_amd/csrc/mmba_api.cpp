@@ -203,6 +203,15 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *
     })
 }
 
+int mmba_plan_solve_per_frame(mmba_plan *plan, double *x_inout, mmba_result *results,
+                              const mmba_callbacks *cb) {
+    if (!plan || !x_inout || !results) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        return plan->impl.solve_frames(x_inout, results, cb);
+    })
+}
+
 int mmba_solve(mmba_context *ctx, const mmba_problem *prob, const mmba_options *opt,
                double *x_inout, double *fvec_out, double *err_user_out, double *err_dist_out,
                mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {

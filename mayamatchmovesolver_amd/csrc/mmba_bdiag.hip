@@ -11,25 +11,11 @@
 // (A + lam D^2) x = g is ONE launch.  Same contract as the band solvers
 // (band_factor_forward / band_forward / band_backward): reduced-order
 // vectors, y = L^-1 r of the permuted factor, ||y|| as lmpar's Newton term.
+#include "mmba_geom.h"
 #include "mmba_kernels.h"
 #include "mmba_plan.h"
 
 namespace mmba {
-
-__device__ __forceinline__ double bd_rsq(double d) {
-    double y = __builtin_amdgcn_rsq(d);
-    const double h = 0.5 * d;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
-}
-
-__device__ __forceinline__ double bd_rdlane(double v, int l) {
-    const long long x = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
-    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 
 // Lane roles of one block's wave: rows 0..PC-1 of the block, then one
 // right-hand-side lane per arrow row (Y_b columns), then the rhs lane.
@@ -46,17 +32,17 @@ __device__ __forceinline__ void bd_chol_aug(double (&a)[PC], double &rsl, bool &
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int j = 0; j < PC; ++j) {
-        double d = bd_rdlane(a[j], j);
+        double d = wave_rdlane(a[j], j);
         if (!(d > 0.) || !isfinite(d)) {
             bad = true;
             d = 1.;
         }
-        const double rs = bd_rsq(d);
+        const double rs = wave_rsq(d);
         const double l = (lane > j) ? a[j] * rs : 0.;
         a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
         if (lane == j) rsl = rs;
 #pragma unroll
-        for (int c = j + 1; c < PC; ++c) a[c] = fma(-l, bd_rdlane(l, c), a[c]);
+        for (int c = j + 1; c < PC; ++c) a[c] = fma(-l, wave_rdlane(l, c), a[c]);
     }
 }
 
@@ -159,7 +145,7 @@ __global__ void __launch_bounds__(256) k_bd_back(BdDev B, const double *__restri
 #pragma unroll
     for (int u = PC - 1; u >= 0; --u) {
         if (lane == u) v *= cc[u];
-        const double xu = bd_rdlane(v, u);
+        const double xu = wave_rdlane(v, u);
         if (lane < u) v = fma(-cc[u], xu, v);
     }
     if (lane < pc) {
@@ -192,14 +178,14 @@ __global__ void __launch_bounds__(256) k_bd_fwd(BdDev B, const double *__restric
 #pragma unroll
     for (int u = 0; u < PC; ++u) {
         if (lane == u) v *= cr[u];
-        const double yu = bd_rdlane(v, u);
+        const double yu = wave_rdlane(v, u);
         if (lane > u) v = fma(-cr[u], yu, v);
     }
     if (lane < pc) y[r0 + lane] = v;
     if (nG > 0) {
         double yv[PC];
 #pragma unroll
-        for (int c = 0; c < PC; ++c) yv[c] = bd_rdlane(v, c);
+        for (int c = 0; c < PC; ++c) yv[c] = wave_rdlane(v, c);
         if (lane < nG) {
             double acc = 0.;
             const double *Yq = B.FY + ((size_t)b * NGMAX + lane) * PC;
@@ -248,17 +234,17 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
         bool bad = false;
 #pragma unroll
         for (int j = 0; j < NGMAX; ++j) {
-            double d = bd_rdlane(a[j], j);
+            double d = wave_rdlane(a[j], j);
             if (!(d > 0.) || !isfinite(d)) {
                 bad = true;
                 d = 1.;
             }
-            const double rs = bd_rsq(d);
+            const double rs = wave_rsq(d);
             const double l = (lane > j) ? a[j] * rs : 0.;
             a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
             if (lane == j) rsl = rs;
 #pragma unroll
-            for (int c = j + 1; c < NGMAX; ++c) a[c] = fma(-l, bd_rdlane(l, c), a[c]);
+            for (int c = j + 1; c < NGMAX; ++c) a[c] = fma(-l, wave_rdlane(l, c), a[c]);
         }
         if (bad && lane == 0) atomicOr(fail, 1);
         if (lane < NGMAX)

@@ -654,4 +654,62 @@ __host__ __device__ inline double int_to_ext(double value, double xmin, double x
     return value;
 }
 
+// Forward-difference point of one FD column at internal value v: lmder
+// perturbs by +-delta and multiplies by inv_delta (adjust_solveFunc.cpp:
+// 148-180, 395-402); lmdif's fdjac2 uses h = eps_dif |v| (eps_dif when v is
+// 0) and divides.  Returns v + step, *step = inv_delta (lmder) or h (lmdif).
+MMBA_DEV double fd_point(double v, double xmin, double xmax, int solver_type, double delta,
+                         double eps_dif, double &step) {
+    if (solver_type == MMBA_SOLVER_CMINPACK_LMDER) {
+        double sign = 1.0;
+        if ((v + delta) > xmax) sign = -1;
+        if ((v - delta) < xmin) sign = 1;
+        const double d = delta * sign;
+        step = 1.0 / d;
+        return v + d;
+    }
+    double h = eps_dif * fabs(v);
+    if (h == 0.) h = eps_dif;
+    step = h;
+    return v + h;
+}
+
+// Lane-level helpers of the one-wave factorisations (mmba_bdiag.hip,
+// mmba_batch.hip): fp64 rsqrt refined twice, v_readlane of a double.
+MMBA_DEV double wave_rsq(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+MMBA_DEV double wave_rdlane(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Unperturbed bundle position of observation (b, frame f): the bundle record
+// of a fast bundle, else the transform chain.
+MMBA_DEV void base_bundle(const DevProblem &P, int b, int f, double *bp) {
+    if (P.bnd_p4[b].w >= 0) {
+        const double *br = &P.brec[(size_t)b * BREC];
+        bp[0] = br[0];
+        bp[1] = br[1];
+        bp[2] = br[2];
+    } else {
+        const Override none{-1, 0.};
+        bundle_position(P, b, f, none, bp);
+    }
+}
+
+// Lens model type of the camera's lens (MMBA_LENS_*), 0 without one.
+MMBA_DEV int obs_lens(const DevProblem &P, int cam, int &lens) {
+    if (!P.cam_lens) return MMBA_LENS_NONE;
+    lens = P.cam_lens[cam];
+    return lens >= 0 ? P.lens_type[lens] : MMBA_LENS_NONE;
+}
+
 }  // namespace mmba

@@ -91,6 +91,31 @@ struct BdDev {
     const int *row_param = nullptr;  // reduced row -> parameter (scatter of x)
 };
 
+// Batched per-frame LM (mmba_batch.hip): one workgroup runs the whole
+// lmder / lmdif solve of one frame's sub-problem (per-frame solve mode with
+// no static parameter: the frames share nothing).  Frame f owns camera-frames
+// [fr_cf_off[f], fr_cf_off[f + 1]) and local parameters k = reduced row -
+// cf_roff of its first camera-frame (fr_par[fr_par_off[f] + k] = parameter).
+constexpr int BATCH_CFMAX = 8;   // camera-frames per frame
+constexpr int BATCH_NFMAX = 32;  // parameters per frame
+struct BatchOut {
+    double fnorm, init_avg, avg, mn, mx, rms;
+    int info, nfev, njev, func_evals, jac_evals, interrupted, better, failed;
+    int measured, pad;
+};
+struct BatchArgs {
+    int nf;                      // frames solved: [0, nf)
+    const int *fr_cf_off, *fr_par_off, *fr_par, *fr_last, *fr_nobs;
+    const double *pweight;       // paramWeightList (mode 2)
+    double *J;                   // [M][2 PCMAX] Jacobian rows of the frame's last Jacobian
+    double *ed, *dist;           // errorDistanceList (last measured); distances [2][M]
+    double *x;                   // internal parameters, in / out (written when better)
+    BatchOut *out;
+    const int *interrupt;        // host-mapped stop flag (nullptr: none)
+    int solver_type, mode, maxfev, accept_only_better, initial_error_given;
+    double delta, factor, ftol, xtol, gtol, initial_error_avg;
+};
+
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
     bool use_bd = false;                     // block diagonal + arrow (no solved bundle)

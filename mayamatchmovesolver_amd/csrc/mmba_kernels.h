@@ -208,4 +208,7 @@ void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const int *ob
                       const double *eu2, const double *ed, double *f2o, double *eu2o,
                       double *edo);
 
+// Per-frame solve mode, one workgroup per frame (mmba_batch.hip).
+void launch_batch_lm(hipStream_t s, const DevProblem &P, const BatchArgs &B, int nf_max);
+
 }  // namespace mmba

@@ -68,20 +68,9 @@ __device__ __forceinline__ void param_prep_one(const DevProblem &P, int p, doubl
                                                double delta, double eps_dif) {
     const double xmin = P.p_min[p], xmax = P.p_max[p], off = P.p_off[p], sc = P.p_scale[p];
     ext[p] = int_to_ext(v, xmin, xmax, off, sc);
-    double xp;
-    if (solver_type == MMBA_SOLVER_CMINPACK_LMDER) {
-        double sign = 1.0;
-        if ((v + delta) > xmax) sign = -1;
-        if ((v - delta) < xmin) sign = 1;
-        double d = delta * sign;
-        xp = v + d;
-        step[p] = 1.0 / d;  // inv_delta, multiplied (adjust_solveFunc.cpp:395-402)
-    } else {
-        double h = eps_dif * fabs(v);
-        if (h == 0.) h = eps_dif;
-        xp = v + h;
-        step[p] = h;  // divided (fdjac2)
-    }
+    double st;
+    const double xp = fd_point(v, xmin, xmax, solver_type, delta, eps_dif, st);
+    step[p] = st;
     ext_pert[p] = int_to_ext(xp, xmin, xmax, off, sc);
 }
 
@@ -222,26 +211,6 @@ __global__ void __launch_bounds__(64) k_records(DevProblem P, const int *__restr
     else
         bnd_record_thread(P, (blockIdx.x - ncb) * 64 + threadIdx.x, ext_pert, step, brec,
                           base_only);
-}
-
-// Unperturbed bundle position of observation (b, frame f).
-__device__ __forceinline__ void base_bundle(const DevProblem &P, int b, int f, double *bp) {
-    if (P.bnd_p4[b].w >= 0) {
-        const double *br = &P.brec[(size_t)b * BREC];
-        bp[0] = br[0];
-        bp[1] = br[1];
-        bp[2] = br[2];
-    } else {
-        const Override none{-1, 0.};
-        bundle_position(P, b, f, none, bp);
-    }
-}
-
-// Lens model type of the camera's lens (MMBA_LENS_*), 0 without one.
-__device__ __forceinline__ int obs_lens(const DevProblem &P, int cam, int &lens) {
-    if (!P.cam_lens) return MMBA_LENS_NONE;
-    lens = P.cam_lens[cam];
-    return lens >= 0 ? P.lens_type[lens] : MMBA_LENS_NONE;
 }
 
 // -------------------------------------------------------------------------

@@ -17,12 +17,130 @@
 // untouched and report success = 0, reason_number = 0.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "mmba_kernels.h"
 #include "mmba_plan.h"
+
+namespace mmba {
+
+// Every frame's solve in one launch (mmba_batch.hip).  The interrupt
+// callback is polled on this (the calling) thread while the launch runs; a
+// request reaches the frames through a host-mapped flag they read at the
+// reference's poll points (each evaluation, each Jacobian).
+int Plan::solve_frames(double *x_inout, mmba_result *results, const mmba_callbacks *cb) {
+    if (!batch_ok) {
+        set_error("per-frame batch: " + batch_why);
+        return MMBA_ERR_UNSUPPORTED;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!d_bJ) {
+        d_bJ = dalloc<double>((size_t)M * 2 * PCMAX);
+        d_bdist = dalloc<double>((size_t)2 * M);
+        d_bx = dalloc<double>(n);
+        d_bpw = upload(param_weight);
+        d_bout = dalloc<BatchOut>(std::max(F, 1));
+        MMBA_HIP(hipHostMalloc(&h_bflag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        MMBA_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_bflag), h_bflag, 0));
+    }
+    const bool polls = cb && cb->interrupt;
+    // a request already pending stops every frame at its first poll
+    __atomic_store_n(h_bflag, polls && cb->interrupt(cb->user) ? 1 : 0, __ATOMIC_SEQ_CST);
+    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    // bundle records (no bundle is solved: computed once per call)
+    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+    MMBA_HIP(hipMemcpyAsync(d_bx, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    BatchArgs B{};
+    B.nf = batch_nf;
+    B.fr_cf_off = d_fr_cf_off;
+    B.fr_par_off = d_fr_par_off;
+    B.fr_par = d_fr_par;
+    B.fr_last = d_fr_last;
+    B.fr_nobs = d_fr_nobs;
+    B.pweight = d_bpw;
+    B.J = d_bJ;
+    B.ed = d_ed;
+    B.dist = d_bdist;
+    B.x = d_bx;
+    B.out = d_bout;
+    B.interrupt = polls ? d_bflag : nullptr;
+    B.solver_type = opt.solver_type;
+    B.mode = opt.auto_param_scale == 1 ? 1 : 2;
+    B.maxfev = opt.iter_max;
+    B.accept_only_better = opt.accept_only_better;
+    B.initial_error_given = opt.initial_error_given;
+    B.delta = opt.delta;
+    B.factor = opt.tau * 100.0;
+    B.ftol = opt.eps1;
+    B.xtol = opt.eps2;
+    B.gtol = opt.eps3;
+    B.initial_error_avg = opt.initial_error_avg;
+    launch_batch_lm(s, P, B, batch_nfmax);
+    MMBA_HIP(hipGetLastError());
+    if (polls) {
+        hipError_t q;
+        while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+            if (!__atomic_load_n(h_bflag, __ATOMIC_RELAXED) && cb->interrupt(cb->user))
+                __atomic_store_n(h_bflag, 1, __ATOMIC_SEQ_CST);
+            std::this_thread::yield();
+        }
+        if (q != hipSuccess) MMBA_HIP(q);
+    }
+    std::vector<double> xo(n);
+    std::vector<BatchOut> out(std::max(batch_nf, 1));
+    MMBA_HIP(hipMemcpyAsync(xo.data(), d_bx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    if (batch_nf > 0)
+        MMBA_HIP(hipMemcpyAsync(out.data(), d_bout, sizeof(BatchOut) * batch_nf,
+                                hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // the first frame whose damped factorisation broke down stops the loop
+    // like a failed frame of the reference (adjust_base.cpp:1471-1476)
+    int ef = batch_nf;
+    for (int f = 0; f < batch_nf; ++f)
+        if (out[f].failed) {
+            ef = f;
+            break;
+        }
+    for (int f = 0; f < F; ++f) {
+        mmba_result r;
+        std::memset(&r, 0, sizeof(r));
+        if (f < batch_nf && f <= ef) {
+            const BatchOut &o = out[f];
+            r.reason_number = o.info;
+            r.iterations = o.nfev;
+            r.function_evals = o.func_evals;
+            r.jacobian_evals = o.jac_evals;
+            r.outer_iterations = o.njev;
+            r.user_interrupted = o.interrupted;
+            r.success = o.func_evals > 0;
+            r.error_final = o.fnorm;
+            r.error_avg = o.avg;
+            r.error_min = o.mn;
+            r.error_max = o.mx;
+            r.error_rms = o.rms;
+            r.error_initial_avg = o.init_avg;
+            r.error_is_better = o.better;
+            r.time_solve_s = dt;
+        }
+        results[f] = r;
+    }
+    for (int p = 0; p < n; ++p)
+        if (param_frame_host[p] < ef) x_inout[p] = xo[p];
+    if (ef < batch_nf) {
+        set_error("damped normal-equation factorisation failed (frame " + std::to_string(ef) + ")");
+        return MMBA_ERR_DEVICE;
+    }
+    return MMBA_OK;
+}
+
+}  // namespace mmba
 
 namespace {
 
@@ -109,6 +227,20 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
             if (f < nf) {
                 fr[f].build(*prob, f);
                 if (!fr[f].solvable()) nf = f;
+            }
+        }
+        if (!chained) {
+            // one launch for every frame when the plan's structure allows it
+            // (MMBA_PERFRAME_BATCH=0: the per-frame plans below)
+            const char *e = std::getenv("MMBA_PERFRAME_BATCH");
+            if (!e || std::atoi(e) != 0) {
+                mmba_plan *plan = nullptr;
+                if (mmba_plan_create(ctx, prob, opt, &plan) == MMBA_OK) {
+                    int rc = MMBA_ERR_UNSUPPORTED;
+                    if (plan->impl.batch_ok) rc = mmba_plan_solve_per_frame(plan, x_inout, results, cb);
+                    mmba_plan_destroy(plan);
+                    if (rc != MMBA_ERR_UNSUPPORTED) return rc;
+                }
             }
         }
         if (max_concurrency <= 0) max_concurrency = nf;

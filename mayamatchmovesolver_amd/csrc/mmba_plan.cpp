@@ -45,6 +45,7 @@ Plan::~Plan() {
     for (void *p : allocs) (void)hipFree(p);
     if (h_scalar) (void)hipHostFree(h_scalar);
     if (h_fail) (void)hipHostFree(h_fail);
+    if (h_bflag) (void)hipHostFree(h_bflag);
 }
 
 static void require(bool c, const char *what) {
@@ -970,6 +971,65 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 if (p_class[p] != PC_B && p_pos[p] >= 0 && p_pos[p] < nR) row_param[p_pos[p]] = p;
             bs.bcr.row_param = upload(row_param);
             bs.bcr.xs = d_xs;
+        }
+    }
+    // ---- batched per-frame solve (mmba_batch.hip): frames share nothing
+    // when every parameter belongs to one camera-frame ----
+    batch_ok = false;
+    {
+        const char *why = nullptr;
+        for (int p = 0; p < n && !why; ++p)
+            if (p_class[p] != PC_CF) why = "a static or shared parameter chains the frames";
+        if (!why && nranks != 1) why = "sharded plan";
+        if (!why && nrows > 0) why = "attribute stiffness / smoothness rows";
+        if (!why && (central || opt.robust_loss)) why = "central differences / robust loss";
+        std::vector<int> fr_cf_off(F + 1, 0), fr_par_off(F + 1, 0), fr_par, fr_last, fr_nobs;
+        int nf = F, nfmax = 0;
+        if (!why) {
+            for (int cf = 0; cf < ncf; ++cf) fr_cf_off[cf_frame[cf] + 1]++;
+            for (int f = 0; f < F; ++f) fr_cf_off[f + 1] += fr_cf_off[f];
+            for (int f = 0; f < F && !why; ++f) {
+                const int c0 = fr_cf_off[f], c1 = fr_cf_off[f + 1];
+                int nl = 0, nobs = 0, last = -1;
+                for (int cf = c0; cf < c1; ++cf) {
+                    nl += cf_pc[cf];
+                    nobs += cf_obs_off[cf + 1] - cf_obs_off[cf];
+                }
+                if (f < nf && (nl == 0 || nl > 2 * nobs)) nf = f;  // the loop stops here
+                if (f >= nf) {
+                    fr_par_off[f + 1] = fr_par_off[f];
+                    fr_last.push_back(-1);
+                    fr_nobs.push_back(nobs);
+                    continue;
+                }
+                if (c1 - c0 > BATCH_CFMAX) why = "more than 8 cameras in one frame";
+                if (nl > BATCH_NFMAX) why = "more than 32 parameters in one frame";
+                const int r0 = cf_roff[c0];
+                for (int k = 0; k < nl; ++k) {
+                    int pk = -1;
+                    for (int cf = c0; cf < c1 && pk < 0; ++cf)
+                        if (r0 + k >= cf_roff[cf] && r0 + k < cf_roff[cf] + cf_pc[cf])
+                            pk = cf_params[cf][r0 + k - cf_roff[cf]];
+                    fr_par.push_back(pk);
+                    last = std::max(last, pk);
+                }
+                fr_par_off[f + 1] = fr_par_off[f] + nl;
+                fr_last.push_back(last);
+                fr_nobs.push_back(nobs);
+                nfmax = std::max(nfmax, nl);
+            }
+        }
+        if (why) {
+            batch_why = why;
+        } else {
+            batch_ok = true;
+            batch_nf = nf;
+            batch_nfmax = nfmax;
+            d_fr_cf_off = upload(fr_cf_off);
+            d_fr_par_off = upload(fr_par_off);
+            d_fr_par = upload(fr_par);
+            d_fr_last = upload(fr_last);
+            d_fr_nobs = upload(fr_nobs);
         }
     }
     MMBA_HIP(hipMemsetAsync(d_fail, 0, sizeof(int), s));

@@ -293,6 +293,19 @@ struct Plan {
     double dnorm(const double *dv);
     int solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
               mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace);
+    // Per-frame solve mode in one launch (mmba_batch.hip), valid when every
+    // parameter is a camera-frame parameter (no static parameter chains the
+    // frames); frames [0, batch_nf) are solvable, batch_nfmax = most
+    // parameters of one frame
+    bool batch_ok = false;
+    std::string batch_why;
+    int batch_nf = 0, batch_nfmax = 0;
+    int *d_fr_cf_off = nullptr, *d_fr_par_off = nullptr, *d_fr_par = nullptr,
+        *d_fr_last = nullptr, *d_fr_nobs = nullptr;
+    double *d_bJ = nullptr, *d_bdist = nullptr, *d_bx = nullptr, *d_bpw = nullptr;
+    BatchOut *d_bout = nullptr;
+    int *h_bflag = nullptr, *d_bflag = nullptr;  // host-mapped interrupt flag
+    int solve_frames(double *x_inout, mmba_result *results, const mmba_callbacks *cb);
     int dense_jacobian(const double *x, double *fjac);
     int reproject(const double *x, double *point_out, double *marker_out);
     int measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,

@@ -222,6 +222,20 @@ class Solver:
                            x0=np.array(p.x0 if x0 is None else x0, dtype=np.float64))
 
 
+    def solve_per_frame(self, x0=None, interrupt=None):
+        """Per-frame solve mode on this plan (``mmba_plan_solve_per_frame``):
+        every frame in one launch.  Returns (x, [per-frame result dicts]);
+        raises MmbaError (MMBA_ERR_UNSUPPORTED) when the parameters do not
+        split into independent frames."""
+        p = self.problem
+        x = np.array(p.x0 if x0 is None else x0, dtype=np.float64)
+        res = (abi.MmbaResult * p.num_frames)()
+        cbs = _callbacks(interrupt)
+        check(lib().mmba_plan_solve_per_frame(self._h, _dp(x), res,
+                                              C.byref(cbs) if cbs is not None else None))
+        return x, [r.as_dict() for r in res]
+
+
 def solve(problem: Problem, options, x0=None, device: int = 0) -> SolveResult:
     """One-shot solve (``mmba_solve``)."""
     s = Solver(problem, options, device=device)
