@@ -103,7 +103,7 @@ def broadcast_bytes(dist, data: bytes | None, n: int) -> bytes:
 
 # Kernels inside the K2 span (Plan::jac: span_begin .. span_end), i.e. the
 # launches whose HIP-event time is roofline.avg_ms.
-K2_REGEX = "k_jacobian|k_ne_|k_colnorms|k_jac_epilogue"
+K2_REGEX = "k_jacobian|k_jac_ne|k_ne_|k_colnorms|k_jac_epilogue"
 
 
 def pmc_traffic(args):
@@ -323,9 +323,11 @@ def main():
     solver = Solver(prob, opt, context=ctx, comm=comm)
     upload_s = time.perf_counter() - t0
 
+    # the caller's output buffers (errorList, ud->errorList,
+    # errorDistanceList) are allocated once and refilled by every solve
+    outs = (np.zeros(prob.num_residuals), np.zeros(prob.num_residuals), np.zeros(prob.num_obs))
     for _ in range(args.warmup):
-        solver.solve()
-    solver.set_timing(True)
+        solver.solve(out=outs)
 
     barrier(dist)
     ctx.synchronize()
@@ -333,15 +335,21 @@ def main():
     iters = nfev = njev = 0
     last = None
     for _ in range(args.steps):
-        last = solver.solve()
+        last = solver.solve(out=outs)
         iters += last.result["outer_iterations"]
         nfev += last.result["function_evals"]
         njev += last.result["outer_iterations"]
     ctx.synchronize()
     barrier(dist)
     dt = time.perf_counter() - t0
-    stats = solver.kernel_stats()
     dt_max = allreduce(dist, dt, "max")
+    # kernel timing (HIP events around the spans) on separate, untimed
+    # solves, so the events do not weigh on the timed steps
+    solver.set_timing(True)
+    for _ in range(max(1, min(args.steps, 5))):
+        solver.solve(out=outs)
+    stats = solver.kernel_stats()
+    solver.set_timing(False)
 
     if rank == 0:
         # one solve of the whole scene per step: count observations once

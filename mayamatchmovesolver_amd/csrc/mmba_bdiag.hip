@@ -273,12 +273,136 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
     }
 }
 
+// Damped solve straight from the normal equations when there is no arrow
+// (nG == 0): S_b = Acc_b + lam D_b^2 with k_schur_init's rules (an exactly
+// zero diagonal at lam == 0 becomes 1 with a zero right-hand side: the
+// component solves to 0), augmented Cholesky, back substitution from the
+// register rows, scatter to parameter order, and ||D xs||^2 plus the fail
+// flag reduced by the last block into scalar[dn_slot] / scalar[fail_slot]
+// (the flag is cleared).  One launch replaces k_schur_init, k_bd_factor,
+// k_bd_back, k_sumsq and k_reduce_multi.
+template <int PC>
+__global__ void __launch_bounds__(256) k_bd_direct(DevProblem P, BdDev B,
+                                                   const double *__restrict__ Acc,
+                                                   const double *__restrict__ g,
+                                                   const double *__restrict__ diag, double lam,
+                                                   double *xR, double *xs, int *fail,
+                                                   double *scalar, int dn_slot, int fail_slot) {
+    __shared__ double wpart[4];
+    __shared__ double red[256];
+    __shared__ int last;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x * 4 + wv;
+    double dn = 0.;
+    if (b < B.nblk) {
+        const int cf = B.cf[b], r0 = B.roff[b], pc = B.pc[b];
+        const int v0 = P.cf_var_off[cf] + 1;
+        const double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
+        int pk = -1;
+        double dk = 0.;
+        if (lane < pc) {
+            pk = P.cf_var_param[v0 + lane];
+            dk = diag[pk];
+        }
+        double a[PC];
+#pragma unroll
+        for (int c = 0; c < PC; ++c) {
+            double v = 0.;
+            if (lane < pc) {
+                if (c <= lane) {
+                    v = A[lane * PCMAX + c];
+                    if (c == lane) {
+                        v += lam * (dk * dk);
+                        if (v == 0.) v = 1.;
+                    }
+                }
+            } else if (lane < PC) {
+                v = c == lane ? 1. : 0.;
+            } else if (lane == BD_R && c < pc) {
+                v = (A[c * PCMAX + c] == 0. && lam == 0.) ? 0. : g[P.cf_var_param[v0 + c]];
+            }
+            a[c] = v;
+        }
+        double rsl = 0.;
+        bool bad = false;
+        bd_chol_aug<PC>(a, rsl, bad);
+        if (bad && lane == 0) atomicOr(fail, 1);
+        double *FC = B.FC + (size_t)b * PC * PC;  // rows for the Newton forward solve
+        if (lane < PC) {
+#pragma unroll
+            for (int c = 0; c < PC; ++c) FC[lane * PC + c] = (c == lane) ? rsl : (c < lane ? a[c] : 0.);
+        }
+        double acc = 0.;
+#pragma unroll
+        for (int j = 0; j < PC; ++j) {
+            const double y = wave_rdlane(a[j], BD_R);
+            if (lane == j) acc = y;
+        }
+#pragma unroll
+        for (int i = PC - 1; i >= 0; --i) {
+            const double xi = wave_rdlane(acc, i) * wave_rdlane(rsl, i);
+            if (lane == i) acc = xi;
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                const double cij = wave_rdlane(a[j], i);
+                if (lane == j) acc = fma(-cij, xi, acc);
+            }
+        }
+        if (lane < pc) {
+            xR[r0 + lane] = acc;
+            xs[pk] = acc;
+            const double t = dk * acc;
+            dn = t * t;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) dn += __shfl_xor(dn, off);
+    }
+    if (lane == 0) wpart[wv] = dn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double v = (wpart[0] + wpart[1]) + (wpart[2] + wpart[3]);
+        __hip_atomic_store(&B.part[blockIdx.x], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        last = atomicAdd(B.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    double s = 0.;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+        s += __hip_atomic_load(&B.part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        scalar[dn_slot] = red[0];
+        scalar[fail_slot] = (double)__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(B.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+void bd_direct(hipStream_t s, const DevProblem &P, const BdDev &D, const double *Acc,
+               const double *g, const double *diag, double lam, double *xR, double *xs,
+               int *fail, double *scalar, int dn_slot, int fail_slot) {
+    const int grid = (D.nblk + 3) / 4;
+    if (D.PC <= 8)
+        k_bd_direct<8><<<grid, 256, 0, s>>>(P, D, Acc, g, diag, lam, xR, xs, fail, scalar,
+                                            dn_slot, fail_slot);
+    else
+        k_bd_direct<PCMAX><<<grid, 256, 0, s>>>(P, D, Acc, g, diag, lam, xR, xs, fail, scalar,
+                                                dn_slot, fail_slot);
+}
+
 template <int PC>
 static void bd_factor_k(hipStream_t s, const BdDev &D, int *fail, const double *r, double *y,
                         double *x, double *xs) {
     const int g = (D.nblk + 3) / 4;
     if (D.nG == 0) {
-        // factor + forward + back in one launch
+        // factor + forward, then back
         k_bd_factor<PC><<<g, 256, 0, s>>>(D, r, y, fail);
         if (x) k_bd_back<PC><<<g, 256, 0, s>>>(D, y, x, xs);
         return;

@@ -579,6 +579,27 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
     return r;
 }
 
+// The weighted errors of residual() only (same operations): the FD
+// columns that do not leave errorList / errorDistanceList behind need no
+// distance (one square root fewer per perturbed evaluation).
+MMBA_DEV double2 residual_e(const double *rec, const double *bp, double mkr_x, double mkr_y,
+                            double sqrtw, int mode, double image_width) {
+    double point_x, point_y;
+    project_point(rec, bp, point_x, point_y);
+    mkr_x *= rec[18];
+    mkr_y *= rec[19];
+    double factor = 1.0;
+    if (mode != MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        double bd0 = bp[0] - rec[12], bd1 = bp[1] - rec[13], bd2 = bp[2] - rec[14];
+        double bl = sqrt(bd0 * bd0 + bd1 * bd1 + bd2 * bd2);
+        double dot = rec[15] * (bd0 / bl) + rec[16] * (bd1 / bl) + rec[17] * (bd2 / bl);
+        if (dot < 0.0) factor = 1e+6;
+    }
+    double dx = fabs(mkr_x - point_x), dy = fabs(mkr_y - point_y);
+    double dxp = dx * image_width, dyp = dy * image_width;
+    return make_double2(dxp * sqrtw * factor, dyp * sqrtw * factor);
+}
+
 // applyLossFunctionToErrors for one row (adjust_base.cpp:158-187), same
 // operation order as the reference (pow, log1p).
 MMBA_DEV double robust_loss(double f, int type, double scale) {

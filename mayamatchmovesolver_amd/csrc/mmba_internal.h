@@ -89,6 +89,10 @@ struct BdDev {
     const double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr;  // input (band layout)
     double *FC = nullptr, *FY = nullptr, *Zc = nullptr, *gpart = nullptr, *FT = nullptr;
     const int *row_param = nullptr;  // reduced row -> parameter (scatter of x)
+    // direct path (nG == 0): block -> camera-frame, single-launch reduction
+    const int *cf = nullptr;
+    unsigned int *ticket = nullptr;
+    double *part = nullptr;
 };
 
 // Batched per-frame LM (mmba_batch.hip): one workgroup runs the whole
@@ -164,6 +168,7 @@ enum VarFlags : int { VF_BUNDLE_SIDE = 1 };
 // Device view of the problem + derived structure (all device pointers).
 struct DevProblem {
     int F, nA, nT, nC, nL, nB, nK, M, n, ncf, nR, nG, mode;
+    int nbs;  // bundles with solved parameters (a B block)
     double image_width;
     const int64_t *attr_off;
     const int *attr_anim;

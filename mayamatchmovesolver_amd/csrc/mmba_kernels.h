@@ -104,11 +104,17 @@ struct NeEpi {
 };
 // Whether launch_ne can fuse the bookkeeping (uniform camera blocks, fast
 // bundles, no global parameters).
+// Fused K2 (k_jac_ne_u): FD Jacobian + camera-frame normal equations in one
+// pass for uniform fast plans without global parameters (ncv = jac_ncv).
+bool jac_ne_fusable(const DevProblem &P, int ncv);
+void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const double *step,
+                   int solver_type, double *J, int *jcol, int *nloc, const int *stale_param,
+                   double *eu, double *ed, double *Acc, double *g, const NeEpi &E);
 bool ne_epilogue_fusable(const DevProblem &P);
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
                double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk,
-               const NeEpi &epi = NeEpi());
+               const NeEpi &epi = NeEpi(), bool cf_done = false);
 void launch_colnorms(hipStream_t s, const DevProblem &P, const double *Acc, const double *Abb,
                      const double *aggbuf, double *acnorm, double *g);
 void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
@@ -172,6 +178,9 @@ void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y)
 void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
 // Block-diagonal + arrow solver (mmba_bdiag.hip): factor S, y = L^-1 r and,
 // with x, the solution (scattered to parameter order into xs when non-null).
+void bd_direct(hipStream_t s, const DevProblem &P, const BdDev &D, const double *Acc,
+               const double *g, const double *diag, double lam, double *xR, double *xs,
+               int *fail, double *scalar, int dn_slot, int fail_slot);
 void bd_factor_solve(hipStream_t s, const BdDev &D, int *fail, const double *r, double *y,
                      double *x, double *xs);
 // y = L^-1 w with the stored factor (lmpar's Newton term)

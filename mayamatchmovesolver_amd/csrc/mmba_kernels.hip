@@ -457,20 +457,19 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     }
 }
 
-// Uniform fast case of k_jacobian (every camera-frame has at most NCV
-// camera-side variants, no bundle-side variants, every solved bundle is a
-// fast bundle, no lens): the same residuals and differences, but every
-// index and record load is issued up front and the NCV + 3 perturbed
-// residuals are independent straight-line code, so their fp64 latency
-// chains overlap (the generic loop serialises them behind its dependent
-// variant-table loads).  Emits columns in the generic kernel's order.
+// One observation of the uniform fast Jacobian: writes its J columns (and
+// jcol / the bundle block record / the stale errorList) and returns the
+// camera columns and f at x for a fused normal-equation accumulation.
 template <int NCV, bool GEN>  // GEN: some bundle needs the transform-chain path
-__global__ void __launch_bounds__(128) k_jacobian_u(
-    DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
-    int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
-    const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.M) return;
+__device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i,
+                                          const double *__restrict__ recs,
+                                          const double *__restrict__ step, bool lmder,
+                                          double *__restrict__ J, int *__restrict__ jcol,
+                                          int *__restrict__ nloc,
+                                          const int *__restrict__ stale_param,
+                                          double *__restrict__ eu, double *__restrict__ ed,
+                                          double (&cx)[NCV], double (&cy)[NCV], double &fx,
+                                          double &fy) {
     const int M = P.M;
     const int cf = P.obs_cf[i];
     const int b = P.obs_bnd[i];
@@ -480,7 +479,6 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     const int voff = P.cf_var_off[cf];
     const int nv = min(P.cf_var_off[cf + 1] - voff - 1, NCV);
     const int pstale = stale_param[fr];
-    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     int pv[NCV];
     double st[NCV];
 #pragma unroll
@@ -500,38 +498,40 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     const double *__restrict__ br = &P.brec[(size_t)b * BREC];
     const double *__restrict__ rec0 = &recs[(size_t)voff * CAMREC];
     const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr);
+    fx = r0.ex;
+    fy = r0.ey;
     int l = 0;
-    double rsx = r0.ux, rsy = r0.uy, rsd = r0.dist;  // errorList of the stale column
-    bool hit = false;
+    // the stale column (B13): re-evaluated in full below when it moves this
+    // observation; the other columns need only the weighted errors
+    int hit = -1;
     const bool wcol = !P.jcol_implicit;
     double jb[8] = {0., 0., 0., 0., 0., 0., r0.ex, r0.ey};
-    auto emit = [&](int p, const Resid &r, double s) {
+    auto emit = [&](int p, const double2 &r, double s, int tag) {
         double jx, jy;
         if (lmder) {  // s = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
-            jx = (r.ex - r0.ex) * s;
-            jy = (r.ey - r0.ey) * s;
+            jx = (r.x - r0.ex) * s;
+            jy = (r.y - r0.ey) * s;
         } else {      // s = h, divided (fdjac2)
-            jx = (r.ex - r0.ex) / s;
-            jy = (r.ey - r0.ey) / s;
+            jx = (r.x - r0.ex) / s;
+            jy = (r.y - r0.ey) / s;
         }
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
         if (wcol) jcol[(size_t)l * M + i] = p;
-        if (p == pstale) {
-            rsx = r.ux;
-            rsy = r.uy;
-            rsd = r.dist;
-            hit = true;
-        }
+        if (p == pstale) hit = tag;
         ++l;
         return make_double2(jx, jy);
     };
 #pragma unroll
     for (int v = 0; v < NCV; ++v) {
+        cx[v] = 0.;
+        cy[v] = 0.;
         if (v < nv) {
             const double *__restrict__ rec = &recs[(size_t)(voff + 1 + v) * CAMREC];
-            emit(pv[v], residual(rec, bp0, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr),
-                 st[v]);
+            const double2 j =
+                emit(pv[v], residual_e(rec, bp0, mx, my, sw, P.mode, P.image_width), st[v], v);
+            cx[v] = j.x;
+            cy[v] = j.y;
         }
     }
 #pragma unroll
@@ -539,12 +539,26 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
         if (a < nb) {
             const double bq[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
             const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
-            const double2 j = emit(
-                p, residual(rec0, bq, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr),
-                br[12 + a]);
+            const double2 j = emit(p, residual_e(rec0, bq, mx, my, sw, P.mode, P.image_width),
+                                   br[12 + a], NCV + a);
             jb[2 * a] = j.x;
             jb[2 * a + 1] = j.y;
         }
+    }
+    double rsx = r0.ux, rsy = r0.uy, rsd = r0.dist;  // errorList of the stale column
+    if (hit >= 0) {
+        const double *rec = hit < NCV ? &recs[(size_t)(voff + 1 + hit) * CAMREC] : rec0;
+        double bq[3] = {bp0[0], bp0[1], bp0[2]};
+        if (hit >= NCV) {
+            const int a = hit - NCV;
+            bq[0] = br[3 + 3 * a];
+            bq[1] = br[4 + 3 * a];
+            bq[2] = br[5 + 3 * a];
+        }
+        const Resid r = residual(rec, bq, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr);
+        rsx = r.ux;
+        rsy = r.uy;
+        rsd = r.dist;
     }
     if (p4.w >= 0 && P.JB) {
         double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)i * 8]);
@@ -555,11 +569,30 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     // errorList / errorDistanceList as left by the last FD column: only the
     // observations that column moves change; the others keep their values at
     // x (what d_eu / d_ed already hold from the evaluation that accepted x)
-    if (eu && (hit || !P.jcol_implicit)) {
+    if (eu && (hit >= 0 || !P.jcol_implicit)) {
         eu[2 * i] = rsx;
         eu[2 * i + 1] = rsy;
         ed[i] = rsd;
     }
+}
+
+// Uniform fast case of k_jacobian (every camera-frame has at most NCV
+// camera-side variants, no bundle-side variants, every solved bundle is a
+// fast bundle, no lens): the same residuals and differences, but every
+// index and record load is issued up front and the NCV + 3 perturbed
+// residuals are independent straight-line code, so their fp64 latency
+// chains overlap (the generic loop serialises them behind its dependent
+// variant-table loads).  Emits columns in the generic kernel's order.
+template <int NCV, bool GEN>
+__global__ void __launch_bounds__(128) k_jacobian_u(
+    DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
+    int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
+    const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    double cx[NCV], cy[NCV], fx, fy;
+    jac_obs_u<NCV, GEN>(P, i, recs, step, solver_type == MMBA_SOLVER_CMINPACK_LMDER, J, jcol,
+                        nloc, stale_param, eu, ed, cx, cy, fx, fy);
 }
 
 // -------------------------------------------------------------------------
@@ -794,6 +827,97 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
 #pragma unroll
             for (int w = 1; w < NW; ++w) {
                 d += wsum[w][ed];
+                gp += wsum[w][NCC + a];
+            }
+            epi_param(E, P.cf_var_param[v0 + a], d, gp, zf, xn, gm);
+        }
+        epi_store(E, E.cf_base + cf, zf, xn, gm);
+    }
+}
+
+// Camera-frame -> XCD-contiguous order: workgroups are dispatched to the 8
+// XCDs round-robin, so workgroup b runs on XCD b % 8; giving each XCD a
+// contiguous range of camera-frames keeps consecutive frames (which share
+// bundles) on one L2 and the bundle records they gather are fetched once.
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+    const int x = b & 7, idx = b >> 3, q = G >> 3, r = G & 7;
+    return x * q + min(x, r) + idx;
+}
+
+// Fused K2 for uniform fast plans without global parameters: one workgroup
+// per camera-frame segment computes the FD Jacobian of its observations
+// (jac_obs_u, the k_jacobian_u arithmetic), keeps the camera columns in
+// registers and reduces Acc / gC (+ the lmder epilogue of the block's
+// parameters) in the same pass -- the J blocks are written once for the
+// Schur / ||J p|| passes and never re-read here (k_ne_cf_u's 19 MB on C4).
+// Same per-lane summation order as k_ne_cf_u with its NW.
+template <int PC, int NW, bool GEN>
+__global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
+    DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
+    int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
+    const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed,
+    double *Acc, double *g, NeEpi E) {
+    constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC;
+    __shared__ double wsum[NW][NE];
+    const int cf = xcd_remap(blockIdx.x, gridDim.x);
+    const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
+    const bool solved = P.cf_pc[cf] == PC;
+    double acc[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[e] = 0.;
+    for (int i = o0 + tid; i < o1; i += 64 * NW) {
+        double jx[PC], jy[PC], fx, fy;
+        jac_obs_u<PC, GEN>(P, i, recs, step, lmder, J, jcol, nloc, stale_param, eu, ed, jx, jy,
+                           fx, fy);
+        int e = 0;
+#pragma unroll
+        for (int a = 0; a < PC; ++a)
+#pragma unroll
+            for (int c = a; c < PC; ++c) acc[e++] += jx[a] * jx[c] + jy[a] * jy[c];
+#pragma unroll
+        for (int a = 0; a < PC; ++a) acc[NCC + a] += jx[a] * fx + jy[a] * fy;
+    }
+    if (!solved) {  // no camera parameter on this camera-frame: J only
+        if (E.on && tid == 0) epi_store(E, E.cf_base + cf, 0., 0., 0.);
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        double v = acc[e];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) wsum[wv][e] = v;
+    }
+    __syncthreads();
+    double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
+    for (int e = tid; e < NE; e += 64 * NW) {
+        double v = wsum[0][e];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v += wsum[w][e];
+        if (e < NCC) {
+            int a = 0, rem = e;
+            while (rem >= PC - a) {
+                rem -= PC - a;
+                ++a;
+            }
+            const int c = a + rem;
+            A[a * PCMAX + c] = v;
+            A[c * PCMAX + a] = v;
+        } else {
+            g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
+        }
+    }
+    if (E.on && tid == 0) {
+        double zf = 0., xn = 0., gm = 0.;
+        const int v0 = P.cf_var_off[cf] + 1;
+        for (int a = 0; a < PC; ++a) {
+            const int ed2 = a * PC - a * (a - 1) / 2;
+            double d = wsum[0][ed2], gp = wsum[0][NCC + a];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) {
+                d += wsum[w][ed2];
                 gp += wsum[w][NCC + a];
             }
             epi_param(E, P.cf_var_param[v0 + a], d, gp, zf, xn, gm);
@@ -2273,21 +2397,61 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
     k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
                                                 nloc, stale_param, eu, ed, CB);
 }
+// One workgroup per camera-frame only fills the chip with enough
+// camera-frames (C4: 500 x 400 observations); a few long segments (C2: 120 x
+// 1,650) keep the split passes, whose Jacobian kernel spreads every
+// observation over the whole GPU.
+bool jac_ne_fusable(const DevProblem &P, int ncv) {
+    return P.nG == 0 && !P.obs_own && P.pc_uniform == ncv && (ncv == 6 || ncv == 7) &&
+           P.nrows == 0 && !P.loss_on && P.ncf >= 256;
+}
+void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const double *step,
+                   int solver_type, double *J, int *jcol, int *nloc, const int *stale_param,
+                   double *eu, double *ed, double *Acc, double *g, const NeEpi &E) {
+    if (P.ncf == 0) return;
+    // 2 waves per camera-frame measured fastest on C4 (400 observations per
+    // segment: 42 us; 8 waves 46 us -- the 230-VGPR kernel runs 2 waves per
+    // SIMD either way)
+    const long long per = (P.M + P.ncf - 1) / P.ncf;
+    const int nw = per > 1024 ? 8 : (per > 512 ? 4 : 2);
+#define MMBA_JN(PC, NW, GEN)                                                                  \
+    k_jac_ne_u<PC, NW, GEN><<<P.ncf, 64 * NW, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc, \
+                                                        stale_param, eu, ed, Acc, g, E)
+#define MMBA_JN_NW(PC, GEN)                                         \
+    do {                                                            \
+        if (nw == 8) MMBA_JN(PC, 8, GEN);                           \
+        else if (nw == 4) MMBA_JN(PC, 4, GEN);                      \
+        else MMBA_JN(PC, 2, GEN);                                   \
+    } while (0)
+#define MMBA_JN_PC(PC)                                              \
+    do {                                                            \
+        if (P.all_bnd_fast) MMBA_JN_NW(PC, false);                  \
+        else MMBA_JN_NW(PC, true);                                  \
+    } while (0)
+    if (P.pc_uniform == 6)
+        MMBA_JN_PC(6);
+    else
+        MMBA_JN_PC(7);
+#undef MMBA_JN_PC
+#undef MMBA_JN_NW
+#undef MMBA_JN
+}
 void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
                           double *stepB, double delta, double *count) {
     if (P.n > 0)
         k_param_central<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext_pertB, stepB, delta, count);
 }
 bool ne_epilogue_fusable(const DevProblem &P) {
-    return P.nG == 0 && P.JB && (P.pc_uniform == 6 || P.pc_uniform == 7) && !P.obs_own;
+    return P.nG == 0 && (P.JB || P.nbs == 0) && (P.pc_uniform == 6 || P.pc_uniform == 7) &&
+           !P.obs_own;
 }
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
                double *Abg, double *aggbuf, double *g, double *glob_partial, int glob_chunk,
-               const NeEpi &epi) {
+               const NeEpi &epi, bool cf_done) {
     const NeEpi E = ne_epilogue_fusable(P) ? epi : NeEpi();
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
-    if (P.ncf > 0) {
+    if (P.ncf > 0 && !cf_done) {
         const bool wide = P.M > 1024 * P.ncf;  // long camera-frame segments (C2): 4 waves
 #define MMBA_NE_U(PC, NW, NG)                                                              \
     k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E)
@@ -2311,7 +2475,7 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
         }
 #undef MMBA_NE_U
     }
-    if (P.nB > 0) {
+    if (P.nbs > 0) {
         if (P.JB)  // every solved bundle fast and no global parameters
             k_ne_bnd_jb<<<nblk(P.nB, 256), 256, 0, s>>>(P, Abb, g, E);
         else

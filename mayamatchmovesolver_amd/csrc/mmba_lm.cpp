@@ -165,14 +165,10 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         CB.step = d_stepB;
     }
     span_begin(SPAN_JAC);
-    launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
-                    d_stale, d_eu, d_ed, jac_ncv, d_f, CB);
-    launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
-                    central ? d_stepB : nullptr, lmder ? 1 : 0, d_Jrow, d_eu + 2 * (size_t)M,
-                    n - 1);
-    if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     // uniform unsharded plans: the lmder bookkeeping rides in the
-    // normal-equation kernels (no k_jac_epilogue launch)
+    // normal-equation kernels (no k_jac_epilogue launch), and with one
+    // block size the camera-frame normal equations ride in the Jacobian
+    // pass itself (k_jac_ne_u: J is written once and not re-read)
     const bool fuse = lm && ne_epilogue_fusable(P) && nrows == 0;
     NeEpi epi;
     if (fuse) {
@@ -190,13 +186,24 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.cf_base = 0;
         epi.bnd_base = ncf;
     }
+    const bool k2_fused = !central && jac_ne_fusable(P, jac_ncv) && !k2_split;
+    if (k2_fused)
+        launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, d_nloc, d_stale, d_eu,
+                      d_ed, d_Acc, d_g, epi);
+    else
+        launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
+                        d_stale, d_eu, d_ed, jac_ncv, d_f, CB);
+    launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
+                    central ? d_stepB : nullptr, lmder ? 1 : 0, d_Jrow, d_eu + 2 * (size_t)M,
+                    n - 1);
+    if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
-              d_glob_partial, glob_chunk, epi);
+              d_glob_partial, glob_chunk, epi, k2_fused);
     launch_rows_ne(s, P, d_Jrow, d_f + 2 * (size_t)M, d_p_own, d_Acc, d_Abb, d_Agg, d_g);
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
     if (fuse) {
         span_end(SPAN_JAC);
-        const int ncol = ncf + (nB + 255) / 256;
+        const int ncol = ncf + (nB_solved > 0 ? (nB + 255) / 256 : 0);
         RedSpec rs{};
         rs.flag_slot = -1;
         rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
@@ -252,6 +259,15 @@ void Plan::trial_enqueue(double *eu, double *ed) {
 void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
     const double t0 = wall_now();
     // d_fail is zero here: launch_flag_to_scalar clears it after every use
+    if (band && bs.use_bd && nG == 0 && nranks == 1 && dnorm_slot >= 0) {
+        // the whole damped solve, ||D xs||^2 and the flag in one launch
+        span_begin(SPAN_CHOL);
+        bd_direct(s, P, bs.bd, d_Acc, d_g, d_diag, lam, d_xR, d_xs, d_fail, d_scalar, dnorm_slot,
+                  SL_FAIL);
+        span_end(SPAN_CHOL);
+        t_linear += wall_now() - t0;
+        return;
+    }
     if (nB_solved > 0) {
         launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
         launch_schur_obs(s, P, d_J, d_Lb, d_W);
@@ -514,10 +530,14 @@ void Plan::download_params(const double *dx, double *x_out) {
     MMBA_HIP(hipStreamSynchronize(s));
 }
 
-void Plan::error_stats_device(const double *ed, double *avg, double *mn, double *mx) {
+void Plan::error_stats_enqueue(const double *ed) {
     launch_dist_stats(s, P, ed, d_partial, nparts, pw, d_scalar + SL_ESUM);
     allreduce(d_scalar + SL_ESUM, 1);
     allreduce(d_scalar + SL_ENMIN, 2, ReduceOp::Max);
+}
+
+void Plan::error_stats_device(const double *ed, double *avg, double *mn, double *mx) {
+    error_stats_enqueue(ed);
     read_slots(SL_ESUM, SL_EMAX);
     *avg = h_scalar[SL_ESUM] / Mg;
     *mn = -h_scalar[SL_ENMIN];
@@ -681,15 +701,22 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FNORM, nullptr,
                         d_dist_x);
         allreduce(d_scalar + SL_FNORM, 1);
-        error_stats_device(d_ed, &init_avg, &init_min, &init_max);  // also reads SL_FNORM's stream
-        init_fnorm = std::sqrt(read_scalar(SL_FNORM));
+        error_stats_enqueue(d_ed);
+        read_slots(SL_FNORM, SL_EMAX);  // one synchronisation for both
+        init_avg = h_scalar[SL_ESUM] / Mg;
+        init_min = -h_scalar[SL_ENMIN];
+        init_max = h_scalar[SL_EMAX];
+        init_fnorm = std::sqrt(h_scalar[SL_FNORM]);
         measured = true;
     } else if (opt.accept_only_better) {
         init_avg = opt.initial_error_avg;  // the caller measured it
     }
     r.error_initial_avg = init_avg;
 
-    MMBA_HIP(hipMemcpyAsync(d_x, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    // x0 through the pinned stage: no blocking pageable copy (the previous
+    // solve's last synchronisation released the stage)
+    if (n > 0) std::memcpy(h_xstage, x_inout, sizeof(double) * n);
+    MMBA_HIP(hipMemcpyAsync(d_x, h_xstage, sizeof(double) * n, hipMemcpyHostToDevice, s));
     MMBA_HIP(hipMemsetAsync(d_diag, 0, sizeof(double) * n, s));
 
     const double p1 = .1, p5 = .5, p25 = .25, p75 = .75, p0001 = 1e-4;
@@ -908,19 +935,30 @@ TERMINATE:
         // lmder leaves the solved x in paramList (adjust_cminpack_lmder.cpp:128);
         // solveFrames writes it back only when the error got better
         // (:1227-1244), which error_is_better reports
-        double avg, mn, mx;
-        error_stats_device(d_ed, &avg, &mn, &mx);  // compute_error_stats (B13: last measured)
-        r.error_avg = avg;
-        r.error_min = mn;
-        r.error_max = mx;
-        r.error_is_better = opt.accept_only_better ? (avg <= init_avg) : 1;
         // RMS at the returned parameters: the accepted point's distances
         if (!dist_ok) {  // stopped before the first evaluation
             fun(d_x, d_ftrial, d_J, d_J + m, d_dist_x);  // scratch user buffers
         }
-        launch_sumsq(s, d_dist_x, nullptr, M, d_partial, nparts, d_scalar + SL_RMS, P.obs_own);
-        r.error_rms = std::sqrt(reduce_read(SL_RMS) / Mg);
-        download_params(d_x, x_inout);
+        // compute_error_stats (B13: the last measured distances), the RMS
+        // and x: one synchronisation
+        error_stats_enqueue(d_ed);
+        launch_sumsq(s, d_dist_x, nullptr, M, d_partial + 3 * (size_t)pw, nparts,
+                     d_scalar + SL_RMS, P.obs_own);
+        allreduce(d_scalar + SL_RMS, 1);
+        const bool staged = nranks == 1 && n > 0;
+        if (staged)
+            MMBA_HIP(hipMemcpyAsync(h_xstage, d_x, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+        read_slots(SL_RMS, SL_EMAX);
+        const double avg = h_scalar[SL_ESUM] / Mg;
+        r.error_avg = avg;
+        r.error_min = -h_scalar[SL_ENMIN];
+        r.error_max = h_scalar[SL_EMAX];
+        r.error_is_better = opt.accept_only_better ? (avg <= init_avg) : 1;
+        r.error_rms = std::sqrt(h_scalar[SL_RMS] / Mg);
+        if (staged)
+            std::memcpy(x_inout, h_xstage, sizeof(double) * n);
+        else
+            download_params(d_x, x_inout);
         if (fvec_out || eu_out || ed_out)
             download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out);
     }

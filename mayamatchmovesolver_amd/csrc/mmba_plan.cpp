@@ -46,6 +46,7 @@ Plan::~Plan() {
     if (h_scalar) (void)hipHostFree(h_scalar);
     if (h_fail) (void)hipHostFree(h_fail);
     if (h_bflag) (void)hipHostFree(h_bflag);
+    if (h_xstage) (void)hipHostFree(h_xstage);
 }
 
 static void require(bool c, const char *what) {
@@ -764,6 +765,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             D.cf_aidx = upload(tab);
         }
     }
+    D.nbs = nB_solved;
     D.all_bnd_fast = 1;
     for (int b = 0; b < nB; ++b)
         if (bnd_p4[b].w < 0) D.all_bnd_fast = 0;
@@ -892,10 +894,12 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     cfblk_roff.clear();
     cfblk_pc.clear();
+    cfblk_cf.clear();
     for (int cf = 0; cf < ncf; ++cf)
         if (cf_pc[cf] > 0) {
             cfblk_roff.push_back(cf_roff[cf]);
             cfblk_pc.push_back(cf_pc[cf]);
+            cfblk_cf.push_back(cf);
         }
     if (band) setup_band();
     if (band && std::getenv("MMBA_PROBE")) {
@@ -1044,7 +1048,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
     MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
     if (const char *e = std::getenv("MMBA_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
+    if (const char *e = std::getenv("MMBA_K2_FUSED")) k2_split = std::atoi(e) == 0;
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
+    MMBA_HIP(hipHostMalloc(&h_xstage, sizeof(double) * std::max(n, 1)));
     MMBA_HIP(hipStreamSynchronize(s));
 }
 
@@ -1080,6 +1086,10 @@ void Plan::setup_band(int Pforce) {
             D.PC = pmax <= 8 ? 8 : PCMAX;
             D.roff = upload(cfblk_roff);
             D.pc = upload(cfblk_pc);
+            D.cf = upload(cfblk_cf);
+            D.ticket = dalloc<unsigned int>(1);
+            D.part = dalloc<double>((D.nblk + 3) / 4);
+            MMBA_HIP(hipMemsetAsync(D.ticket, 0, sizeof(unsigned int), s));
             D.Bd = bs.Bd;
             D.Ga = bs.Ga;
             D.Gd = bs.Gd;

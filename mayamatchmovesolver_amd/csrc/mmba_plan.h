@@ -92,6 +92,7 @@ struct Plan {
     bool use_dest = false;
     int ndest = 0;
     int jac_ncv = 0;     // uniform fast Jacobian kernel (k_jacobian_u<jac_ncv>), 0: generic
+    bool k2_split = false;  // MMBA_K2_FUSED=0: separate Jacobian and normal-equation passes
     int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
@@ -143,7 +144,7 @@ struct Plan {
     std::vector<int> param_frame_host;
     // solved camera-frame blocks (reduced rows [roff, roff + pc)), for the
     // block-diagonal solver
-    std::vector<int> cfblk_roff, cfblk_pc;
+    std::vector<int> cfblk_roff, cfblk_pc, cfblk_cf;
     double *d_recs = nullptr, *d_brec = nullptr;
     double *d_J = nullptr;
     int *d_jcol = nullptr, *d_nloc = nullptr;
@@ -157,6 +158,7 @@ struct Plan {
     int *d_fail = nullptr;
     unsigned int *d_ticket = nullptr;  // single-launch reduction ticket (zero between uses)
     double *h_scalar = nullptr;  // pinned
+    double *h_xstage = nullptr;  // pinned [n]: x in / out without a blocking pageable copy
     int *h_fail = nullptr;       // pinned
 
     // timing (HIP events on the plan stream, read back only at the end of a
@@ -258,6 +260,7 @@ struct Plan {
     std::vector<double> pmin_h, pmax_h, poff_h, pscale_h;  // bound transform (host)
     // compute_error_stats of ed on the device -> avg, min, max (host)
     void error_stats_device(const double *ed, double *avg, double *mn, double *mx);
+    void error_stats_enqueue(const double *ed);  // -> SL_ESUM, SL_ENMIN, SL_EMAX
     // with lm: the lmder bookkeeping after the normal equations is fused
     // into the column-norm launch (k_jac_epilogue); scalars -> SL_ZERO,
     // SL_XN2 (first pass), SL_GNORM (fnorm != 0)

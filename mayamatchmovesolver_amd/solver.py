@@ -199,16 +199,24 @@ class Solver:
         check(lib().mmba_plan_jacobian(self._h, _dp(xx), _dp(fjac)))
         return fjac.reshape(n, m).T
 
-    def solve(self, x0=None, trace_capacity=4096, interrupt=None) -> SolveResult:
+    def solve(self, x0=None, trace_capacity=4096, interrupt=None, out=None) -> SolveResult:
         """LM solve from x0 (internal parameters).  ``SolveResult.x`` is the
         solved x as lmder leaves paramList; ``result["error_is_better"]`` says
         whether solveFrames would write it back (``accepted_x``).
         ``interrupt``: a callable polled where the reference polls
-        MComputation::isInterruptRequested (non-zero / True stops)."""
+        MComputation::isInterruptRequested (non-zero / True stops).
+        ``out``: (fvec, err_user, err_dist) float64 arrays to fill instead of
+        fresh ones (a caller solving repeatedly keeps its buffers)."""
         p = self.problem
         m, M = p.num_residuals, p.num_obs
         x = np.array(p.x0 if x0 is None else x0, dtype=np.float64)
-        fvec, eu, ed = np.zeros(m), np.zeros(m), np.zeros(M)
+        if out is None:
+            fvec, eu, ed = np.zeros(m), np.zeros(m), np.zeros(M)
+        else:
+            fvec, eu, ed = out
+            assert fvec.dtype == eu.dtype == ed.dtype == np.float64
+            assert fvec.size >= m and eu.size >= m and ed.size >= M
+            assert fvec.flags.c_contiguous and eu.flags.c_contiguous and ed.flags.c_contiguous
         res = abi.MmbaResult()
         tbuf = np.zeros(max(1, trace_capacity))
         tr = abi.MmbaTrace(_dp(tbuf), trace_capacity, 0)
