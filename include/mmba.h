@@ -349,6 +349,13 @@ int mmba_shard_layout(int32_t num_frames, int32_t num_obs, const int32_t *obs_fr
                       const int32_t *obs_bundle, int32_t num_bundles, int32_t nranks,
                       int32_t *bounds_out /* nranks + 1 */, int32_t *bundle_owner_out);
 
+/* Plan caching (the Maya-side shim keeps one plan per problem shape):
+ * replace the scene's attribute values (the problem's attr_values, same
+ * attr_offset layout) of an existing plan, e.g. after a previous solve's
+ * results were written back.  Structure, observations, parameters and
+ * options are kept; the next solve / measure starts from these values. */
+int mmba_plan_set_attr_values(mmba_plan *plan, const double *attr_values);
+
 /* One residual evaluation (measureErrors, adjust_measureErrors.cpp:523) at
  * internal parameters x.  Any output pointer may be NULL. */
 int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out,

@@ -69,6 +69,8 @@ def lib():
         L.mmba_solve_per_frame.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, dp, C.c_void_p,
                                            C.c_int32, C.POINTER(abi.MmbaCallbacks)]
         L.mmba_plan_reproject.argtypes = [C.c_void_p, dp, dp, dp]
+        L.mmba_plan_set_attr_values.restype = C.c_int
+        L.mmba_plan_set_attr_values.argtypes = [C.c_void_p, dp]
         L.mmba_plan_solve_per_frame.restype = C.c_int
         L.mmba_plan_solve_per_frame.argtypes = [C.c_void_p, dp, C.c_void_p,
                                                 C.POINTER(abi.MmbaCallbacks)]

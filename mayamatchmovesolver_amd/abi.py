@@ -223,6 +223,7 @@ EXPORTED_SYMBOLS = [
     "mmba_plan_reproject",
     "mmba_solve_per_frame",
     "mmba_plan_solve_per_frame",
+    "mmba_plan_set_attr_values",
     "mmba_plan_jacobian",
     "mmba_plan_solve",
     "mmba_solve",

@@ -203,6 +203,19 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *
     })
 }
 
+int mmba_plan_set_attr_values(mmba_plan *plan, const double *attr_values) {
+    if (!plan || !attr_values) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        Plan &p = plan->impl;
+        MMBA_HIP(hipSetDevice(p.ctx->device));
+        std::memcpy(p.host_attr0.data(), attr_values, p.attr_bytes);
+        MMBA_HIP(hipMemcpyAsync(p.d_attr0, p.host_attr0.data(), p.attr_bytes,
+                                hipMemcpyHostToDevice, p.s));
+        MMBA_HIP(hipStreamSynchronize(p.s));
+        return MMBA_OK;
+    })
+}
+
 int mmba_plan_solve_per_frame(mmba_plan *plan, double *x_inout, mmba_result *results,
                               const mmba_callbacks *cb) {
     if (!plan || !x_inout || !results) return MMBA_ERR_INVALID;

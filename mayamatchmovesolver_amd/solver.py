@@ -230,6 +230,13 @@ class Solver:
                            x0=np.array(p.x0 if x0 is None else x0, dtype=np.float64))
 
 
+    def set_attr_values(self, attr_values):
+        """Replace the scene's attribute values of this plan
+        (``mmba_plan_set_attr_values``; plan caching across solves)."""
+        v = np.ascontiguousarray(attr_values, dtype=np.float64)
+        assert v.size >= np.asarray(self.problem.attr_values).size
+        check(lib().mmba_plan_set_attr_values(self._h, _dp(v)))
+
     def solve_per_frame(self, x0=None, interrupt=None):
         """Per-frame solve mode on this plan (``mmba_plan_solve_per_frame``):
         every frame in one launch.  Returns (x, [per-frame result dicts]);
