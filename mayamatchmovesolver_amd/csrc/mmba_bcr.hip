@@ -258,6 +258,42 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
     if (rs_out && lane < K) rs_out[lane] = rsl;
 }
 
+// bcr_chol_aug_wave with the column broadcast in registers: l_c is read
+// from lane c by v_readlane (SGPR operand of the update fma), so a pivot
+// step has no LDS round trip and no wave barrier; the next pivot's chain
+// (its column update, v_readlane, v_rsq + two Newton steps) is issued
+// first and the bulk update's independent readlane / fma pairs fill its
+// latency.  Same operations and operands as the LDS version.
+template <int K>
+__device__ __forceinline__ void bcr_chol_aug_reg(double (&a)[K], double *rs_out, int &bad) {
+    const int lane = threadIdx.x & 63;
+    double rsl = 0.;
+    bool anybad = false;
+    double d = bcr_rdlane(a[0], 0);
+    bool dbad = !(d > 0.) || !isfinite(d);
+    if (dbad) d = 1.;
+    double rs = bcr_rsq(d);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        anybad |= dbad;
+        const double l = (lane > j) ? a[j] * rs : 0.;
+        a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+        if (lane == j) rsl = rs;
+        if (j + 1 < K) {
+            const double lj1 = bcr_rdlane(l, j + 1);
+            a[j + 1] = fma(-l, lj1, a[j + 1]);
+            d = bcr_rdlane(a[j + 1], j + 1);
+            dbad = !(d > 0.) || !isfinite(d);
+            if (dbad) d = 1.;
+            rs = bcr_rsq(d);
+        }
+#pragma unroll
+        for (int c = j + 2; c < K; ++c) a[c] = fma(-l, bcr_rdlane(l, c), a[c]);
+    }
+    if (anybad) bad = 1;
+    if (rs_out && lane < K) rs_out[lane] = rsl;
+}
+
 // In-place forward substitution X <- C^-1 X for the column this lane owns
 // (x points at its first entry, stride xs between rows); column-oriented
 // (axpy) steps so the K dependent steps are short.
@@ -384,7 +420,12 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         for (int c = 0; c < K; ++c)
             a[c] = lane < K ? (c <= lane ? sD[w][lane * KS + c] : 0.) : (xp ? xp[c * xs] : 0.);
         __syncthreads();  // every wave holds its operands: stores below may overwrite them
-        if (act) bcr_chol_aug_wave<K>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
+        if (act) {
+            if (B.regchol)
+                bcr_chol_aug_reg<K>(a, half == 0 ? sRs[w] : nullptr, bad);
+            else
+                bcr_chol_aug_wave<K>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
+        }
         if (act) {
             if (lane < K) {
                 if (half == 0)

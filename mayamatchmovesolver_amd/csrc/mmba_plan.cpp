@@ -1145,6 +1145,7 @@ void Plan::setup_band(int Pforce) {
             B.w = w;
             B.nblk = std::max(1, (nb + B.K - 1) / B.K);
             B.NR = B.K + (nG + 7) / 8 * 8;
+            if (const char *e3 = std::getenv("MMBA_BCR_REGCHOL")) B.regchol = std::atoi(e3) != 0;
             B.Bd = bs.Bd;
             B.Ga = bs.Ga;
             B.Gd = bs.Gd;
