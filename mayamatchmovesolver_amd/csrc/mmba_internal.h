@@ -65,7 +65,7 @@ struct BandPart {
 struct BcrDev {
     int K = 0, nb = 0, nG = 0, nblk = 0, w = 0;
     int NR = 0;  // root system size: K + nG rounded up to 8
-    int regchol = 1;  // pivot-chain broadcast in registers (MMBA_BCR_REGCHOL=0: through LDS)
+    int regchol = 0;  // pivot-chain broadcast in registers (MMBA_BCR_REGCHOL=1; default LDS: faster)
     const double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr;  // input (band layout)
     double *Dk = nullptr, *Lk0 = nullptr, *Lk1 = nullptr, *Gk = nullptr;
     double *FC = nullptr, *FU = nullptr, *FV = nullptr, *FY = nullptr, *Zc = nullptr;
