@@ -258,37 +258,53 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
     if (rs_out && lane < K) rs_out[lane] = rsl;
 }
 
-// bcr_chol_aug_wave with the column broadcast in registers: l_c is read
-// from lane c by v_readlane (SGPR operand of the update fma), so a pivot
-// step has no LDS round trip and no wave barrier; the next pivot's chain
-// (its column update, v_readlane, v_rsq + two Newton steps) is issued
-// first and the bulk update's independent readlane / fma pairs fill its
-// latency.  Same operations and operands as the LDS version.
-template <int K>
-__device__ __forceinline__ void bcr_chol_aug_reg(double (&a)[K], double *rs_out, int &bad) {
+// Blocked augmented Cholesky by ONE wave (same rows / right-hand-side lanes
+// as bcr_chol_aug_wave): the pivot chain runs over panels of PW columns and
+// only updates the columns of its own panel (v_readlane broadcasts, at most
+// PW - 1 per step, no LDS); after each panel the trailing columns take the
+// panel's PW updates at once from an LDS image of the panel (a broadcast
+// read per entry, no synchronisation inside the loop).  Every entry still
+// receives its updates in column order as fma(-l_k, L_ck, a), so the result
+// is bit-identical to the unblocked chain.  pl: PW * 64 doubles of this
+// wave's LDS.
+template <int K, int PW>
+__device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out, double *pl,
+                                                 int &bad) {
     const int lane = threadIdx.x & 63;
     double rsl = 0.;
     bool anybad = false;
-    double d = bcr_rdlane(a[0], 0);
-    bool dbad = !(d > 0.) || !isfinite(d);
-    if (dbad) d = 1.;
-    double rs = bcr_rsq(d);
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        anybad |= dbad;
-        const double l = (lane > j) ? a[j] * rs : 0.;
-        a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
-        if (lane == j) rsl = rs;
-        if (j + 1 < K) {
-            const double lj1 = bcr_rdlane(l, j + 1);
-            a[j + 1] = fma(-l, lj1, a[j + 1]);
-            d = bcr_rdlane(a[j + 1], j + 1);
-            dbad = !(d > 0.) || !isfinite(d);
-            if (dbad) d = 1.;
-            rs = bcr_rsq(d);
+    for (int j0 = 0; j0 < K; j0 += PW) {
+#pragma unroll
+        for (int j = j0; j < j0 + PW && j < K; ++j) {
+            double d = bcr_rdlane(a[j], j);
+            if (!(d > 0.) || !isfinite(d)) {
+                anybad = true;
+                d = 1.;
+            }
+            const double rs = bcr_rsq(d);
+            const double l = (lane > j) ? a[j] * rs : 0.;
+            a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+            if (lane == j) rsl = rs;
+#pragma unroll
+            for (int c = j + 1; c < j0 + PW && c < K; ++c) a[c] = fma(-l, bcr_rdlane(l, c), a[c]);
         }
+        if (j0 + PW < K) {
+            // panel image: p_k(lane) = L[lane][k] below the diagonal, x_k in
+            // the right-hand-side lanes, 0 on and above the diagonal
 #pragma unroll
-        for (int c = j + 2; c < K; ++c) a[c] = fma(-l, bcr_rdlane(l, c), a[c]);
+            for (int k = 0; k < PW; ++k) pl[lane * PW + k] = lane > j0 + k ? a[j0 + k] : 0.;
+            wave_lds_sync();
+#pragma unroll
+            for (int c = j0 + PW; c < K; ++c) {
+#pragma unroll
+                for (int k = 0; k < PW; ++k) {
+                    const double pk = lane > j0 + k ? a[j0 + k] : 0.;
+                    a[c] = fma(-pk, pl[c * PW + k], a[c]);
+                }
+            }
+            wave_lds_sync();
+        }
     }
     if (anybad) bad = 1;
     if (rs_out && lane < K) rs_out[lane] = rsl;
@@ -314,10 +330,53 @@ __device__ __forceinline__ void bcr_trsv_col(const double *C, const double *rs, 
     for (int i = 0; i < K; ++i) x0[i * xs] = x[i];
 }
 
+typedef double bcr_d4 __attribute__((ext_vector_type(4)));
+
+// Updates of the even block with fp64 MFMA (v_mfma_f64_16x16x4_f64): wave w
+// owns the 16 x 16 output tile (w >> 1, w & 1) of the (padded 32 x 32)
+// K x K results
+//   D_e -= V1^T V1 + U2^T U2   (lower tiles),   L'_e = -V1^T U1,
+// summing u in K / 4 steps of 4.  A operand lane l: A[l & 15][l >> 4] =
+// X[u0 + (l >> 4)][row], B operand B[l >> 4][l & 15] = Y[u0 + (l >> 4)][col];
+// result lane l, register r: row (l >> 4) + 4 r, column l & 15.
+template <int K, int KS>
+__device__ __forceinline__ void bcr_updates_mfma(const double *U1, const double *V1,
+                                                 const double *U2, const double *sDe, double *De,
+                                                 double *Lo, bool h1, int wv, int lane) {
+    const int ti = wv >> 1, tc = wv & 1;
+    const int i = ti * 16 + (lane & 15), c = tc * 16 + (lane & 15), k4 = lane >> 4;
+    const bool dtile = tc <= ti;
+    bcr_d4 dacc = {0., 0., 0., 0.}, lacc = {0., 0., 0., 0.};
+#pragma unroll
+    for (int u0 = 0; u0 < K; u0 += 4) {
+        const int u = u0 + k4;
+        const double v1i = i < K ? V1[u * KS + i] : 0.;
+        if (dtile) {
+            const double v1c = c < K ? V1[u * KS + c] : 0.;
+            const double u2i = i < K ? U2[u * KS + i] : 0.;
+            const double u2c = c < K ? U2[u * KS + c] : 0.;
+            dacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v1i, v1c, dacc, 0, 0, 0);
+            dacc = __builtin_amdgcn_mfma_f64_16x16x4f64(u2i, u2c, dacc, 0, 0, 0);
+        }
+        if (h1) {
+            const double u1c = c < K ? U1[u * KS + c] : 0.;
+            lacc = __builtin_amdgcn_mfma_f64_16x16x4f64(v1i, u1c, lacc, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = ti * 16 + k4 + 4 * r, col = tc * 16 + (lane & 15);
+        if (row < K && col < K) {
+            if (dtile && col <= row) De[row * K + col] = sDe[row * KS + col] - dacc[r];
+            if (h1) Lo[row * K + col] = -lacc[r];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // One elimination level.  blockIdx.x = even index / 2 (t = 2 blockIdx.x).
 // ---------------------------------------------------------------------------
-template <int K>
+template <int K, int CH, bool MF>  // CH: pivot chain variant (BcrDev::regchol); MF: MFMA updates
 __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
                                                    int *fail, long long *probe, double *y) {
     constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
@@ -329,7 +388,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     __shared__ double sGT[2][K * GS];  // G_o^T -> Y_o
     __shared__ double sR[3][K];        // r_o1 -> y1, r_o2 -> y2, r_e (fused forward solve)
     __shared__ double sRs[2][K];       // 1 / C_jj
-    __shared__ double col[4][64];
+    __shared__ double col[4][64 * 8];  // pivot column (LDS chain) / panel image (blocked chain)
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
     __shared__ int bad_s;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -421,8 +480,8 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             a[c] = lane < K ? (c <= lane ? sD[w][lane * KS + c] : 0.) : (xp ? xp[c * xs] : 0.);
         __syncthreads();  // every wave holds its operands: stores below may overwrite them
         if (act) {
-            if (B.regchol)
-                bcr_chol_aug_reg<K>(a, half == 0 ? sRs[w] : nullptr, bad);
+            if constexpr (CH == 2)
+                bcr_chol_aug_blk<K, 8>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
             else
                 bcr_chol_aug_wave<K>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
         }
@@ -472,6 +531,9 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     const double *U1 = sB[0], *V1 = sB[1], *U2 = sB[2], *V2 = sB[3];
     const double *Y1 = sGT[0], *Y2 = sGT[1];
     double *De = bcr_blk(B.Dk, e, K);
+    if constexpr (MF && K <= 32) {
+        bcr_updates_mfma<K, KS>(U1, V1, U2, sDe, De, bcr_blk(Lout, e, K), h1, wv, lane);
+    } else
     for (int q = tid; q < 2 * 4 * K; q += blockDim.x) {
         const int m = q / (4 * K), r = q % (4 * K), i = r / 4, c0 = (r % 4) * CG;
         if (m == 0) {
@@ -947,7 +1009,18 @@ static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long lon
     double *yy = r ? y : nullptr;
     int ping = 0;
     for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) {
-        k_bcr_level<K><<<(nact + 1) / 2, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
+        const int g = (nact + 1) / 2;
+        if (D.regchol == 2) {
+            if (D.mfma_upd)
+                k_bcr_level<K, 2, true><<<g, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
+            else
+                k_bcr_level<K, 2, false><<<g, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
+        } else {
+            if (D.mfma_upd)
+                k_bcr_level<K, 0, true><<<g, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
+            else
+                k_bcr_level<K, 0, false><<<g, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
+        }
         ping ^= 1;
     }
     switch (D.NR) {

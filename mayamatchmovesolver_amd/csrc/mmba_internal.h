@@ -65,7 +65,11 @@ struct BandPart {
 struct BcrDev {
     int K = 0, nb = 0, nG = 0, nblk = 0, w = 0;
     int NR = 0;  // root system size: K + nG rounded up to 8
-    int regchol = 0;  // pivot-chain broadcast in registers (MMBA_BCR_REGCHOL=1; default LDS: faster)
+    // level pivot chain (MMBA_BCR_CHOL): 0 column broadcast through LDS per
+    // step, 2 blocked (8-column panels); a v_readlane-per-entry chain measured
+    // 13 % slower than 0 and was dropped
+    int regchol = 2;
+    int mfma_upd = 1;  // even-block updates as fp64 MFMA (MMBA_BCR_MFMA=0: VALU)
     const double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr;  // input (band layout)
     double *Dk = nullptr, *Lk0 = nullptr, *Lk1 = nullptr, *Gk = nullptr;
     double *FC = nullptr, *FU = nullptr, *FV = nullptr, *FY = nullptr, *Zc = nullptr;

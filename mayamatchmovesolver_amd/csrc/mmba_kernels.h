@@ -217,6 +217,10 @@ void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const int *ob
                       const double *eu2, const double *ed, double *f2o, double *eu2o,
                       double *edo);
 
+// Sharded Jacobian scalars: [ZERO, XN2, gnorm per rank] -> SL_ZERO.. (max fold).
+void launch_fold_ranks(hipStream_t s, const double *t, int nranks, double *out, int do_xn,
+                       int do_gn);
+
 // Per-frame solve mode, one workgroup per frame (mmba_batch.hip).
 void launch_batch_lm(hipStream_t s, const DevProblem &P, const BatchArgs &B, int nf_max);
 

@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
-    const bool solved = P.cf_pc[cf] == PC;
+    const bool solved = P.cf_pc[cf] == PC && own_cf(P, cf);  // sharded: owner's blocks only
     double acc[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) acc[e] = 0.;
@@ -959,9 +959,17 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
         if (pb > 1) g[p4.y] = gb[1];
         if (pb > 2) g[p4.z] = gb[2];
         if (E.on) {
-            epi_param(E, p4.x, A[0][0], gb[0], zf, xn, gm);
-            if (pb > 1) epi_param(E, p4.y, A[1][1], gb[1], zf, xn, gm);
-            if (pb > 2) epi_param(E, p4.z, A[2][2], gb[2], zf, xn, gm);
+            // sharded: every bundle of the shard gets acnorm / diag, only the
+            // owned ones enter the rank-summed scalars
+            double zo = 0., xo = 0., go = 0.;
+            epi_param(E, p4.x, A[0][0], gb[0], zo, xo, go);
+            if (pb > 1) epi_param(E, p4.y, A[1][1], gb[1], zo, xo, go);
+            if (pb > 2) epi_param(E, p4.z, A[2][2], gb[2], zo, xo, go);
+            if (own_bnd(P, b)) {
+                zf = zo;
+                xn = xo;
+                gm = go;
+            }
         }
     }
     if (!E.on) return;
@@ -2402,7 +2410,7 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
 // 1,650) keep the split passes, whose Jacobian kernel spreads every
 // observation over the whole GPU.
 bool jac_ne_fusable(const DevProblem &P, int ncv) {
-    return P.nG == 0 && !P.obs_own && P.pc_uniform == ncv && (ncv == 6 || ncv == 7) &&
+    return P.nG == 0 && P.pc_uniform == ncv && (ncv == 6 || ncv == 7) &&
            P.nrows == 0 && !P.loss_on && P.ncf >= 256;
 }
 void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const double *step,
@@ -2436,14 +2444,30 @@ void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const
 #undef MMBA_JN_NW
 #undef MMBA_JN
 }
+// [ZERO, XN2, gnorm_0 .. gnorm_{n-1}] after the sum all-reduce -> the
+// ZERO / XN2 / GNORM slots (gnorm = max over ranks)
+__global__ void k_fold_ranks(const double *__restrict__ t, int nranks, double *out, int do_xn,
+                             int do_gn) {
+    if (threadIdx.x != 0) return;
+    out[0] = t[0];
+    if (do_xn) out[1] = t[1];
+    if (do_gn) {
+        double g = 0.;
+        for (int r = 0; r < nranks; ++r) g = fmax(g, t[2 + r]);
+        out[2] = g;
+    }
+}
+void launch_fold_ranks(hipStream_t s, const double *t, int nranks, double *out, int do_xn,
+                       int do_gn) {
+    k_fold_ranks<<<1, 64, 0, s>>>(t, nranks, out, do_xn, do_gn);
+}
 void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
                           double *stepB, double delta, double *count) {
     if (P.n > 0)
         k_param_central<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext_pertB, stepB, delta, count);
 }
 bool ne_epilogue_fusable(const DevProblem &P) {
-    return P.nG == 0 && (P.JB || P.nbs == 0) && (P.pc_uniform == 6 || P.pc_uniform == 7) &&
-           !P.obs_own;
+    return P.nG == 0 && (P.JB || P.nbs == 0) && (P.pc_uniform == 6 || P.pc_uniform == 7);
 }
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,

@@ -206,10 +206,21 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         const int ncol = ncf + (nB_solved > 0 ? (nB + 255) / 256 : 0);
         RedSpec rs{};
         rs.flag_slot = -1;
-        rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
-        if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, SL_XN2};
-        if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
-        launch_reduce_multi(s, d_partial, rs, d_scalar);
+        if (nranks > 1) {  // [ZERO, XN2, gnorm per rank]: one collective (see below)
+            double *tail = d_Agg + NGMAX * NGMAX + NGMAX;
+            MMBA_HIP(hipMemsetAsync(tail, 0, sizeof(double) * (2 + nranks), s));
+            rs.row[rs.nrows++] = {0, ncol, 1, 0};
+            if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, 1};
+            if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, 2 + rank};
+            launch_reduce_multi(s, d_partial, rs, tail);
+            allreduce(tail, 2 + nranks);
+            launch_fold_ranks(s, tail, nranks, d_scalar + SL_ZERO, epi.do_xn, epi.do_gn);
+        } else {
+            rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
+            if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, SL_XN2};
+            if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
+            launch_reduce_multi(s, d_partial, rs, d_scalar);
+        }
     } else if (!lm) {
         launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
         span_end(SPAN_JAC);
@@ -223,16 +234,29 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         rs.row[rs.nrows++] = {0, nparts, 1, SL_ZERO};
         if (do_xn) rs.row[rs.nrows++] = {pw, nparts, 0, SL_XN2};
         if (do_gn) rs.row[rs.nrows++] = {2 * pw, nparts, 1, SL_GNORM};
-        launch_reduce_multi(s, d_partial, rs, d_scalar);
-        allreduce(d_scalar + SL_ZERO, do_xn ? 2 : 1);  // [ZERO, XN2]
-        if (do_gn) allreduce(d_scalar + SL_GNORM, 1, ReduceOp::Max);
+        if (nranks > 1) {
+            // one collective for the three scalars: the gnorm max travels as
+            // one slot per rank of a sum all-reduce and is folded after it
+            double *tail = d_Agg + NGMAX * NGMAX + NGMAX;
+            MMBA_HIP(hipMemsetAsync(tail, 0, sizeof(double) * (2 + nranks), s));
+            RedSpec rj{};
+            rj.flag_slot = -1;
+            rj.row[rj.nrows++] = {0, nparts, 1, 0};
+            if (do_xn) rj.row[rj.nrows++] = {pw, nparts, 0, 1};
+            if (do_gn) rj.row[rj.nrows++] = {2 * pw, nparts, 1, 2 + rank};
+            launch_reduce_multi(s, d_partial, rj, tail);
+            allreduce(tail, 2 + nranks);
+            launch_fold_ranks(s, tail, nranks, d_scalar + SL_ZERO, do_xn, do_gn);
+        } else {
+            launch_reduce_multi(s, d_partial, rs, d_scalar);
+        }
     }
     t_jac += wall_now() - t0;
 }
 
 // Trial point x + p, p = -xs (lmder): one parameter pass (step, norms,
 // setParameters), measureErrors, ||J p||, one reduction launch.
-void Plan::trial_enqueue(double *eu, double *ed) {
+void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm) {
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
@@ -251,12 +275,13 @@ void Plan::trial_enqueue(double *eu, double *ed) {
     rs.row[rs.nrows++] = {5 * pw, residual_blocks(P), 0, SL_FNORM};
     rs.row[rs.nrows++] = {6 * pw, residual_blocks(P), 0, SL_JP};
     launch_reduce_multi(s, d_partial, rs, d_scalar);
-    allreduce(d_scalar + SL_PNORM, 4);  // [PNORM, XN2T, FNORM, JP]
+    // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
+    allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
     t_func += wall_now() - t0;
 }
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
-void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
+void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer) {
     const double t0 = wall_now();
     // d_fail is zero here: launch_flag_to_scalar clears it after every use
     if (band && bs.use_bd && nG == 0 && nranks == 1 && dnorm_slot >= 0) {
@@ -363,7 +388,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot) {
         launch_reduce_multi(s, d_partial, rs, d_scalar, d_fail);
     }
     if (dnorm_slot == SL_DNORM) {
-        allreduce(d_scalar + SL_DNORM, 2);  // [DNORM, FAIL]
+        if (!defer) allreduce(d_scalar + SL_DNORM, 2);  // [DNORM, FAIL]
     } else {
         if (dnorm_slot >= 0) allreduce(d_scalar + dnorm_slot, 1);
         allreduce(d_scalar + SL_FAIL, 1);
@@ -414,8 +439,8 @@ void Plan::newton_enqueue(double dxnorm) {
 // decision point reads its scalars with one synchronisation.
 // pre: the undamped solve and its ||D x|| were enqueued and read already
 // (lmpar_first_enqueue); *undamped is set when lmpar returns that step.
-static void lmpar_first_enqueue(Plan &pl) {
-    pl.solve_damped_enqueue(0.0, Plan::SL_DNORM);
+static void lmpar_first_enqueue(Plan &pl, bool defer = false) {
+    pl.solve_damped_enqueue(0.0, Plan::SL_DNORM, defer);
 }
 
 static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *undamped) {
@@ -821,9 +846,12 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             // outer iteration needs one synchronisation; a speculative
             // trial that lmpar does not take is discarded (its errorList /
             // errorDistanceList went to d_eu_s / d_ed_s).
-            lmpar_first_enqueue(*this);
+            // sharded: the speculative trial's all-reduce also carries the
+            // undamped solve's [DNORM, FAIL] -- two scalar collectives per
+            // outer iteration (Jacobian scalars, trial + step norm)
             const bool spec = spec_ok;
-            if (spec) trial_enqueue(d_eu_s, d_ed_s);
+            lmpar_first_enqueue(*this, spec && nranks > 1);
+            if (spec) trial_enqueue(d_eu_s, d_ed_s, nranks > 1);
             {
                 const double t0 = wall_now();
                 read_slots(0, SL_LAST);

@@ -944,7 +944,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_Acg = dalloc<double>((size_t)ncf * PCMAX * NGMAX);
     d_Abb = dalloc<double>((size_t)nB * 9);
     d_Abg = dalloc<double>((size_t)nB * PBMAX * NGMAX);
-    d_Agg = dalloc<double>(NGMAX * NGMAX + NGMAX);  // [Agg | g_G], see launch_ne
+    // [Agg | g_G] (launch_ne), then the sharded Jacobian scalars [ZERO, XN2,
+    // gnorm of rank 0 .. nranks-1] all-reduced together (Plan::jac)
+    d_Agg = dalloc<double>(NGMAX * NGMAX + NGMAX + 2 + std::max(nranks, 1));
     d_gather = dalloc<double>((size_t)2 * mg + Mg + n);
     d_glob_partial = dalloc<double>((size_t)((M + glob_chunk - 1) / glob_chunk) * (NGMAX * NGMAX + NGMAX));
     d_Lb = dalloc<double>((size_t)nB * 9);
@@ -1145,7 +1147,8 @@ void Plan::setup_band(int Pforce) {
             B.w = w;
             B.nblk = std::max(1, (nb + B.K - 1) / B.K);
             B.NR = B.K + (nG + 7) / 8 * 8;
-            if (const char *e3 = std::getenv("MMBA_BCR_REGCHOL")) B.regchol = std::atoi(e3) != 0;
+            if (const char *e3 = std::getenv("MMBA_BCR_CHOL")) B.regchol = std::atoi(e3) == 0 ? 0 : 2;
+            if (const char *e4 = std::getenv("MMBA_BCR_MFMA")) B.mfma_upd = std::atoi(e4) != 0;
             B.Bd = bs.Bd;
             B.Ga = bs.Ga;
             B.Gd = bs.Gd;

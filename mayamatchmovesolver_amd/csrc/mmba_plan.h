@@ -280,7 +280,9 @@ struct Plan {
     void jac_partial_stale(const double *dx, int k);
     // trial point x - xs: setParameters, measureErrors into (d_ftrial, eu,
     // ed), ||J p||; scalars -> SL_PNORM, SL_XN2T, SL_FNORM, SL_JP
-    void trial_enqueue(double *eu, double *ed);
+    // with_dnorm (sharded speculative trial): the undamped solve's [DNORM,
+    // FAIL] ride in the trial's all-reduce (slots 0..5, one collective)
+    void trial_enqueue(double *eu, double *ed, bool with_dnorm = false);
     // speculative trial (lmpar's first, undamped, step taken before the
     // host has read it): its errorList / errorDistanceList land here and are
     // swapped in when lmpar accepts that step
@@ -289,7 +291,9 @@ struct Plan {
     int pw = 0;           // partial-row stride of d_partial (8 rows)
     // dnorm_slot >= 0: also ||D xs||^2 -> that slot (one reduction launch
     // with the fail flag)
-    void solve_damped_enqueue(double lam, int dnorm_slot = -1);
+    // defer: leave [DNORM, FAIL] un-reduced (the caller's next all-reduce
+    // carries them)
+    void solve_damped_enqueue(double lam, int dnorm_slot = -1, bool defer = false);
     bool solve_damped(double lam);
     void newton_enqueue(double dxnorm);
     void dnorm_enqueue(const double *dv, int slot);
