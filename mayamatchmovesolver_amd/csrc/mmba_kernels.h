@@ -102,14 +102,14 @@ struct NeEpi {
     double *diag = nullptr, *acnorm = nullptr, *partial = nullptr;
     int rstride = 0, cf_base = 0, bnd_base = 0;
 };
-// Whether launch_ne can fuse the bookkeeping (uniform camera blocks, fast
-// bundles, no global parameters).
 // Fused K2 (k_jac_ne_u): FD Jacobian + camera-frame normal equations in one
 // pass for uniform fast plans without global parameters (ncv = jac_ncv).
 bool jac_ne_fusable(const DevProblem &P, int ncv);
 void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const double *step,
                    int solver_type, double *J, int *jcol, int *nloc, const int *stale_param,
                    double *eu, double *ed, double *Acc, double *g, const NeEpi &E);
+// Whether launch_ne can fuse the bookkeeping (uniform camera blocks, fast
+// bundles, no global parameters).
 bool ne_epilogue_fusable(const DevProblem &P);
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,

@@ -256,7 +256,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
 
 // Trial point x + p, p = -xs (lmder): one parameter pass (step, norms,
 // setParameters), measureErrors, ||J p||, one reduction launch.
-void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm) {
+void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnorm) {
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
@@ -274,14 +274,18 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm) {
     rs.row[rs.nrows++] = {4 * pw, nparts, 0, SL_XN2T};
     rs.row[rs.nrows++] = {5 * pw, residual_blocks(P), 0, SL_FNORM};
     rs.row[rs.nrows++] = {6 * pw, residual_blocks(P), 0, SL_JP};
-    launch_reduce_multi(s, d_partial, rs, d_scalar);
+    if (fill_dnorm) {  // the undamped solve's ||D xs||^2 and fail flag (solve_damped_enqueue)
+        rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_DNORM};
+        rs.flag_slot = SL_FAIL;
+    }
+    launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr);
     // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
     allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
     t_func += wall_now() - t0;
 }
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
-void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer) {
+void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dnorm_by_trial) {
     const double t0 = wall_now();
     // d_fail is zero here: launch_flag_to_scalar clears it after every use
     if (band && bs.use_bd && nG == 0 && nranks == 1 && dnorm_slot >= 0) {
@@ -294,6 +298,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer) {
         return;
     }
     if (nB_solved > 0) {
+        // (folding the 3 x 3 factor into k_schur_obs, one factor per
+        // observation, measured 34 us against 16 + 6 us: the per-observation
+        // square roots and divisions lengthen the latency-bound pass)
         launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
         launch_schur_obs(s, P, d_J, d_Lb, d_W);
     }
@@ -377,6 +384,13 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer) {
             launch_scatter_xR(s, P, d_xR, d_xs);
     }
     if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
+    if (dnorm_by_trial) {
+        // the speculative trial's ||D p||^2 (p = -xs, same partial blocks and
+        // order as k_sumsq: bit-identical) becomes ||D xs||^2, and its
+        // reduction also converts the fail flag (trial_enqueue)
+        t_linear += wall_now() - t0;
+        return;
+    }
     if (dnorm_slot < 0) {
         launch_flag_to_scalar(s, d_fail, d_scalar + SL_FAIL);
     } else {  // ||D xs||^2 and the fail flag in one reduction launch
@@ -439,8 +453,8 @@ void Plan::newton_enqueue(double dxnorm) {
 // decision point reads its scalars with one synchronisation.
 // pre: the undamped solve and its ||D x|| were enqueued and read already
 // (lmpar_first_enqueue); *undamped is set when lmpar returns that step.
-static void lmpar_first_enqueue(Plan &pl, bool defer = false) {
-    pl.solve_damped_enqueue(0.0, Plan::SL_DNORM, defer);
+static void lmpar_first_enqueue(Plan &pl, bool defer = false, bool by_trial = false) {
+    pl.solve_damped_enqueue(0.0, Plan::SL_DNORM, defer, by_trial);
 }
 
 static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *undamped) {
@@ -850,8 +864,13 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             // undamped solve's [DNORM, FAIL] -- two scalar collectives per
             // outer iteration (Jacobian scalars, trial + step norm)
             const bool spec = spec_ok;
-            lmpar_first_enqueue(*this, spec && nranks > 1);
-            if (spec) trial_enqueue(d_eu_s, d_ed_s, nranks > 1);
+            // with the speculative trial behind it, the undamped solve's
+            // ||D xs|| comes from the trial's ||D p|| reduction (no separate
+            // norm launches), and sharded plans fold [DNORM, FAIL] into the
+            // trial's all-reduce
+            const bool by_trial = spec && !(band && bs.use_bd && nG == 0 && nranks == 1);
+            lmpar_first_enqueue(*this, spec && nranks > 1, by_trial);
+            if (spec) trial_enqueue(d_eu_s, d_ed_s, nranks > 1, by_trial);
             {
                 const double t0 = wall_now();
                 read_slots(0, SL_LAST);

@@ -282,7 +282,9 @@ struct Plan {
     // ed), ||J p||; scalars -> SL_PNORM, SL_XN2T, SL_FNORM, SL_JP
     // with_dnorm (sharded speculative trial): the undamped solve's [DNORM,
     // FAIL] ride in the trial's all-reduce (slots 0..5, one collective)
-    void trial_enqueue(double *eu, double *ed, bool with_dnorm = false);
+    // fill_dnorm: this trial's ||D p||^2 also fills SL_DNORM and the fail
+    // flag SL_FAIL of the undamped solve enqueued with dnorm_by_trial
+    void trial_enqueue(double *eu, double *ed, bool with_dnorm = false, bool fill_dnorm = false);
     // speculative trial (lmpar's first, undamped, step taken before the
     // host has read it): its errorList / errorDistanceList land here and are
     // swapped in when lmpar accepts that step
@@ -293,7 +295,8 @@ struct Plan {
     // with the fail flag)
     // defer: leave [DNORM, FAIL] un-reduced (the caller's next all-reduce
     // carries them)
-    void solve_damped_enqueue(double lam, int dnorm_slot = -1, bool defer = false);
+    void solve_damped_enqueue(double lam, int dnorm_slot = -1, bool defer = false,
+                              bool dnorm_by_trial = false);
     bool solve_damped(double lam);
     void newton_enqueue(double dxnorm);
     void dnorm_enqueue(const double *dv, int slot);
