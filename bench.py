@@ -314,7 +314,9 @@ def main():
     prob = S.make_config(args.config, frames=frames, scale=scale, **kw)
     opt = S.config_options(prob)
     gen_s = time.perf_counter() - t0
-    ctx = Context(local)
+    # MMBA_BENCH_DEVICE: every rank on one device (RCCL path rehearsal on a
+    # one-GPU box; the driver's multi-GPU runs leave it unset)
+    ctx = Context(int(os.environ.get("MMBA_BENCH_DEVICE", local)))
     comm = None
     if world > 1:
         uid = broadcast_bytes(dist, comm_unique_id() if rank == 0 else None, 128)

@@ -2421,7 +2421,8 @@ void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const
     // segment: 42 us; 8 waves 46 us -- the 230-VGPR kernel runs 2 waves per
     // SIMD either way)
     const long long per = (P.M + P.ncf - 1) / P.ncf;
-    const int nw = per > 1024 ? 8 : (per > 512 ? 4 : 2);
+    int nw = per > 1024 ? 8 : (per > 512 ? 4 : 2);
+    if (const char *e = std::getenv("MMBA_K2_WAVES")) nw = std::atoi(e);
 #define MMBA_JN(PC, NW, GEN)                                                                  \
     k_jac_ne_u<PC, NW, GEN><<<P.ncf, 64 * NW, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc, \
                                                         stale_param, eu, ed, Acc, g, E)
