@@ -2417,11 +2417,11 @@ void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const
                    int solver_type, double *J, int *jcol, int *nloc, const int *stale_param,
                    double *eu, double *ed, double *Acc, double *g, const NeEpi &E) {
     if (P.ncf == 0) return;
-    // 2 waves per camera-frame measured fastest on C4 (400 observations per
-    // segment: 42 us; 8 waves 46 us -- the 230-VGPR kernel runs 2 waves per
-    // SIMD either way)
+    // the 232-VGPR kernel runs 2 waves per SIMD, so 4-wave workgroups fill
+    // the chip with C4's 500 segments in one round (400 observations per
+    // segment: 2 waves 41.7 us, 4 waves 34.6 us, 8 waves 45.7 us)
     const long long per = (P.M + P.ncf - 1) / P.ncf;
-    int nw = per > 1024 ? 8 : (per > 512 ? 4 : 2);
+    int nw = per > 1024 ? 8 : (per > 256 ? 4 : 2);
     if (const char *e = std::getenv("MMBA_K2_WAVES")) nw = std::atoi(e);
 #define MMBA_JN(PC, NW, GEN)                                                                  \
     k_jac_ne_u<PC, NW, GEN><<<P.ncf, 64 * NW, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc, \
