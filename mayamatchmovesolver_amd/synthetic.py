@@ -318,7 +318,8 @@ CONFIG_NAMES = {
 
 def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                 scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH, window: int = 4,
-                depth=(20.0, 200.0), lens_model: str = "classic") -> Problem:
+                depth=(20.0, 200.0), lens_model: str = "classic",
+                init_noise: float = 1.0, obs_noise: float = 1.0) -> Problem:
     """Concrete synthetic input for BASELINE.json ``configs[index]``.
 
     ``frames`` / ``scale`` shrink a configuration (frame-window subsets and
@@ -327,6 +328,13 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
     frames) and ``depth`` (bundle depth range) apply to configs[3] only: the
     defaults are the C4 spec; longer tracks / nearer bundles give the
     well-conditioned variants the sharded-solve tests compare x on.
+    ``init_noise`` (configs[2] / configs[3]) scales the initial-guess
+    perturbation of poses and bundles (1.0 = the spec).  ``obs_noise`` (configs[2] / configs[3]) scales
+    the 0.5 px marker noise: 0 gives a zero-residual minimum, where x is
+    determined to roundoff; with the spec noise the minimum of the C4
+    structure lies in a flat valley (far bundles on a 1.5-unit baseline) and
+    the lmder stopping point moves along it by ~1e-3 under a 1-ulp change of
+    x0 -- in the reference as in any fp64 implementation.
     ``lens_model`` (configs[4] only): "classic" (the C5 spec), "radial" (the
     same scene through a 3DE radial decentered deg 4 cylindric lens, degree-2
     and degree-4 distortion solved), "anamorphic" / "anamorphic_rescaled"
@@ -342,11 +350,12 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
         return _config_c2(rng, frames or 120, scale)
     if index == 2:
         return _config_ba(rng, index, n_cams=10, F=frames or 500, B=int(10000 * scale),
-                          K=int(50000 * scale), window=20, per_cam_markers=True)
+                          K=int(50000 * scale), window=20, per_cam_markers=True,
+                          init_noise=init_noise, obs_noise=obs_noise)
     if index == 3:
         return _config_ba(rng, index, n_cams=1, F=frames or 500, B=int(50000 * scale),
                           K=int(50000 * scale), window=window, per_cam_markers=False,
-                          depth=depth)
+                          depth=depth, init_noise=init_noise, obs_noise=obs_noise)
     if index == 4:
         return _config_c5(rng, frames or 240, scale, lens_model)
     raise KeyError(index)
@@ -371,8 +380,8 @@ def _bundles_in_front(rng, B, depth_lo=20.0, depth_hi=200.0):
     return np.stack([x, y + 1.5, -depth], axis=1)
 
 
-def _noisy(rng, v):
-    return v + rng.normal(0.0, 0.5, size=v.shape) / IMAGE_WIDTH
+def _noisy(rng, v, a=1.0):
+    return v + a * rng.normal(0.0, 0.5, size=v.shape) / IMAGE_WIDTH
 
 
 def _config_c1(rng, F):
@@ -466,12 +475,12 @@ def _windows(rng, K, F, mean_len, lo=None, hi=None):
     return start, length
 
 
-def _obs_from_windows(rng, start, length, project_fn):
+def _obs_from_windows(rng, start, length, project_fn, noise=1.0):
     ks = np.repeat(np.arange(start.size), length)
     offs = np.arange(length.sum()) - np.repeat(np.cumsum(length) - length, length)
     fs = np.repeat(start, length) + offs
     mx, my = project_fn(ks, fs)
-    xy = np.stack([_noisy(rng, mx), _noisy(rng, my)], axis=1)
+    xy = np.stack([_noisy(rng, mx, noise), _noisy(rng, my, noise)], axis=1)
     return ks, fs, xy
 
 
@@ -529,7 +538,8 @@ def _config_c2(rng, F, scale):
                          meta={"name": CONFIG_NAMES[1]})
 
 
-def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0, 200.0)):
+def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0, 200.0),
+               init_noise=1.0, obs_noise=1.0):
     """Full BA: animated cameras (t, r per frame) + static bundles, gauge-locked.
 
     C3 (``per_cam_markers``): a 10-camera rig (2 units apart) moving slowly,
@@ -583,9 +593,10 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0
             mx[sel], my[sel] = _pose_project(ts[c], rs[c], FOCAL_MM, P[mkr_bnd[ks[sel]]], fs[sel])
         return mx, my
 
-    ks, fs, xy = _obs_from_windows(rng, start, length, proj)
-    t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
-    r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
+    ks, fs, xy = _obs_from_windows(rng, start, length, proj, obs_noise)
+    a = init_noise
+    t0 = [tc + a * rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
+    r0 = [rc + a * rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
     for c in (0,):  # gauge: camera-0 pose at frame 0 exact
         t0[c][0] = ts[c][0]
         r0[c][0] = rs[c][0]
@@ -600,7 +611,7 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0
             first_f[j] = fs[q]
             first_c[j] = mkr_cam[ks[q]]
     origin = np.stack([ts[first_c[j]][first_f[j]] for j in range(B)]) if B else np.zeros((0, 3))
-    P0 = origin + (P - origin) * (1.0 + rng.uniform(-0.05, 0.05, size=(B, 1)))
+    P0 = origin + (P - origin) * (1.0 + a * rng.uniform(-0.05, 0.05, size=(B, 1)))
     P0[0] = P[0]  # gauge: bundle 0 locked at truth
     solved = np.ones(B, bool)
     solved[0] = False

@@ -13,7 +13,7 @@ REL = 1e-6
 
 
 @pytest.mark.parametrize("name", G.fixture_names())
-def test_gpu_matches_fixture(name, gpu_ctx):
+def test_gpu_matches_fixture(name, gpu_ctx, oracle):
     prob, opt, d = G.load(name)
     s = Solver(prob, opt, context=gpu_ctx)
     try:
@@ -36,3 +36,37 @@ def test_gpu_matches_fixture(name, gpu_ctx):
     assert np.max(np.abs(out.x - xr) / np.maximum(np.abs(xr), 1e-3)) <= tol
     # final residual vector: norm of the difference against the initial ||f||
     assert np.linalg.norm(out.fvec - d["exp_fvec"]) <= REL * float(tr[0])
+    # the oracle's residual function evaluated at the GPU's x: the GPU's fvec
+    # is that vector (to roundoff), and where x is only pinned at the
+    # envelope, the GPU's x is as good a stopping point as the reference's
+    # (its cost within 1e-6 of the fixture's final ||f||: the x difference
+    # lies along the flat valley, not across it)
+    fo = oracle.measure(prob, opt, out.x)[0]
+    assert np.linalg.norm(out.fvec - fo) <= 1e-9 * float(tr[0])
+    fn, fr = float(np.linalg.norm(fo)), float(np.linalg.norm(d["exp_fvec"]))
+    assert abs(fn - fr) <= REL * fr + 1e-12 * float(tr[0]), (fn, fr)
+
+
+def test_c4_structure_first_step_x(gpu_ctx, oracle):
+    """c4_f16's scene with the evaluation budget capped at 2 (x0 and one
+    full LM step through the Schur / reduced solve): x against the oracle at
+    1e-6 relative on every component.  Past this point the reference itself
+    does not determine x to 1e-6 on this structure (the oracle's own x moves
+    by 2.5e-6 after 3 evaluations and 8.1e-3 at the full-run stop under a
+    1-ulp change of x0; profiles/r2_parity/c4_envelope.txt),
+    so the full run is pinned by the trace, fvec and the cost at the GPU's x
+    (test_gpu_matches_fixture)."""
+    from mayamatchmovesolver_amd import synthetic as S
+    prob = S.make_config(3, frames=16, scale=0.002)
+    opt = S.config_options(prob, iterations=2)
+    xr, fr, _eu, _ed, rr, trr = oracle.solve(prob, opt)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        out = s.solve()
+    finally:
+        s.close()
+    assert out.result["reason_number"] == rr.reason_number
+    assert out.result["function_evals"] == rr.function_evals
+    np.testing.assert_allclose(out.fnorm_trace, trr, rtol=REL)
+    dx = np.max(np.abs(out.x - xr) / np.maximum(np.abs(xr), 1e-3))
+    assert dx <= REL, dx

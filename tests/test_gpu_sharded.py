@@ -141,3 +141,33 @@ def test_sharded_ba_many_shards(nshards, gpu_ctx):
     np.testing.assert_allclose(g.fnorm_trace[:5], ref.fnorm_trace[:5], rtol=1e-6)
     assert abs(g.result["error_final"] - ref.result["error_final"]) <= \
         1e-3 * ref.result["error_final"]
+
+
+@pytest.mark.parametrize("nshards", [2, 4, 8])
+@pytest.mark.parametrize("scene", ["c4", "wc"])
+def test_sharded_ba_x_before_the_valley(scene, nshards, gpu_ctx):
+    """x itself, on the headline C4 structure (4-frame tracks at depth
+    20-200) and on the 6-frame variant, sharded against unsharded, with the
+    evaluation budget capped at 2 (x0 and one full LM step): past that the
+    reference itself does not determine x to 1e-6 on this structure
+    (profiles/r2_parity/c4_envelope.txt).  The step is a full
+    Schur / reduced solve across every shard boundary, so a wrong block, a
+    missing halo term or a wrong separator shows up in x at 1e-3..1e-2; the
+    bar here is 1e-6 relative on every component."""
+    kw = WC if scene == "wc" else {}
+    prob = S.make_config(3, frames=20 * nshards, scale=0.002 * nshards, **kw)
+    opt = S.config_options(prob, iterations=2)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        ref = s.solve()
+    finally:
+        s.close()
+    outs = run_sharded(prob, opt, nshards)
+    check_shards_agree(outs)
+    g = outs[0]
+    for k in ("reason_number", "iterations", "function_evals"):
+        assert g.result[k] == ref.result[k], k
+    assert ref.fnorm_trace[-1] < 0.5 * ref.fnorm_trace[0]  # the step was taken
+    np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-9)
+    dx = np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3))
+    assert dx <= 1e-6, dx
