@@ -51,6 +51,18 @@ __device__ __forceinline__ double bcr_rsq(double d) {
     return y;
 }
 
+typedef __attribute__((address_space(1))) unsigned int bcr_gu32;
+typedef __attribute__((address_space(1))) unsigned long long bcr_gu64;
+
+// Store of a value another workgroup of the SAME launch reads (dataflow
+// factor, k_bcr_factor_df): write-through (agent-scope relaxed atomic store,
+// global_store ... sc1), MI355X guide G16 R1.  Per-level launches take the
+// same stores (the kernel boundary would order plain ones too).
+__device__ __forceinline__ void bcr_st(double *p, double v) {
+    __hip_atomic_store((bcr_gu64 *)p, (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ double *bcr_blk(double *base, int b, int K) {
     return base + (size_t)b * K * K;
 }
@@ -367,18 +379,39 @@ __device__ __forceinline__ void bcr_updates_mfma(const double *U1, const double 
     for (int r = 0; r < 4; ++r) {
         const int row = ti * 16 + k4 + 4 * r, col = tc * 16 + (lane & 15);
         if (row < K && col < K) {
-            if (dtile && col <= row) De[row * K + col] = sDe[row * KS + col] - dacc[r];
-            if (h1) Lo[row * K + col] = -lacc[r];
+            if (dtile && col <= row) bcr_st(&De[row * K + col], sDe[row * KS + col] - dacc[r]);
+            if (h1) bcr_st(&Lo[row * K + col], -lacc[r]);
         }
     }
 }
 
+// Entry (i, c) of block b of D and of the coupling L = S[b, b-1], read from
+// the band layout (k_bcr_load's job; padding rows: identity, uncoupled).
+template <int K>
+__device__ __forceinline__ void bcr_band_dl(const BcrDev &B, int b, int q, double &dv,
+                                            double &lv) {
+    const int i = q / K, c = q % K, R = b * K + i, W1 = B.w + 1;
+    dv = 0.;
+    lv = 0.;
+    if (R < B.nb) {
+        const int C = b * K + c;
+        if (c <= i && R - C <= B.w) dv = B.Bd[(size_t)R * W1 + (C - R + B.w)];
+        const int Cp = (b - 1) * K + c;
+        if (b > 0 && R - Cp <= B.w) lv = B.Bd[(size_t)R * W1 + (Cp - R + B.w)];
+    } else if (i == c) {
+        dv = 1.;
+    }
+}
+
 // ---------------------------------------------------------------------------
-// One elimination level.  blockIdx.x = even index / 2 (t = 2 blockIdx.x).
+// One elimination level, one item: the even block e = t s (t even) and its
+// odd neighbours.  band: level 0 of the dataflow factor, operands staged
+// straight from the band layout and the right-hand side rsrc (no load pass).
 // ---------------------------------------------------------------------------
 template <int K, int CH, bool MF>  // CH: pivot chain variant (BcrDev::regchol); MF: MFMA updates
-__global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
-                                                   int *fail, long long *probe, double *y) {
+__device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact, int ping,
+                                               const int t, int *fail, long long *probe,
+                                               double *y, bool band, const double *rsrc) {
     constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
     constexpr int CG = K / 4;     // columns per update task
     constexpr int GS = NGMAX;     // row stride of the K x nG arrays
@@ -392,7 +425,6 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
     __shared__ int bad_s;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int t = 2 * blockIdx.x;
     const int e = t * s;
     const bool h1 = t >= 2;                 // o1 = e - s exists (and so does its prev e - 2s)
     const bool h2 = t + 1 < nact;           // o2 = e + s
@@ -421,13 +453,22 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         const int q = q0 + tid;
         if (q >= K * K) break;
         const int i = q / K, c = q % K, x = i * KS + c, xt = c * KS + i;
-        const double d0 = h1 ? bcr_blk(B.Dk, o1, K)[q] : 0.;
-        const double d1 = h2 ? bcr_blk(B.Dk, o2, K)[q] : 0.;
-        const double b0 = h1 ? bcr_blk((double *)Lin, o1, K)[q] : 0.;
-        const double b1 = h1 ? bcr_blk((double *)Lin, e, K)[q] : 0.;
-        const double b2 = h2 ? bcr_blk((double *)Lin, o2, K)[q] : 0.;
-        const double b3 = hn ? bcr_blk((double *)Lin, en, K)[q] : 0.;
-        const double de = bcr_blk(B.Dk, e, K)[q];
+        double d0 = 0., d1 = 0., b0 = 0., b1 = 0., b2 = 0., b3 = 0., de, dz;
+        if (band) {
+            if (h1) bcr_band_dl<K>(B, o1, q, d0, b0);
+            bcr_band_dl<K>(B, e, q, de, b1);
+            if (!h1) b1 = 0.;
+            if (h2) bcr_band_dl<K>(B, o2, q, d1, b2);
+            if (hn) bcr_band_dl<K>(B, en, q, dz, b3);
+        } else {
+            if (h1) d0 = bcr_blk(B.Dk, o1, K)[q];
+            if (h2) d1 = bcr_blk(B.Dk, o2, K)[q];
+            if (h1) b0 = bcr_blk((double *)Lin, o1, K)[q];
+            if (h1) b1 = bcr_blk((double *)Lin, e, K)[q];
+            if (h2) b2 = bcr_blk((double *)Lin, o2, K)[q];
+            if (hn) b3 = bcr_blk((double *)Lin, en, K)[q];
+            de = bcr_blk(B.Dk, e, K)[q];
+        }
         sD[0][x] = d0;
         sD[1][x] = d1;
         sB[0][x] = b0;
@@ -440,14 +481,24 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         const int which = q / (K * GS), r = q % (K * GS), u = r / GS, qq = r % GS;
         const int o = which ? o2 : o1;
         const bool h = which ? h2 : h1;
-        sGT[which][r] = (h && qq < nG) ? B.Gk[((size_t)o * nG + qq) * K + u] : 0.;
+        double g = 0.;
+        if (h && qq < nG) {
+            const int C = o * K + u;
+            g = band ? (C < B.nb ? B.Ga[(size_t)qq * B.nb + C] : 0.)
+                     : B.Gk[((size_t)o * nG + qq) * K + u];
+        }
+        sGT[which][r] = g;
     }
-    for (int q = tid; q < nG * K; q += blockDim.x) sGe[q] = B.Gk[(size_t)e * nG * K + q];
+    for (int q = tid; q < nG * K; q += blockDim.x) {
+        const int C = e * K + q % K;
+        sGe[q] = band ? (C < B.nb ? B.Ga[(size_t)(q / K) * B.nb + C] : 0.)
+                      : B.Gk[(size_t)e * nG * K + q];
+    }
     if (tid < 3 * K) {
         const int w = tid / K, i = tid % K;
         const int blk = w == 0 ? o1 : (w == 1 ? o2 : e);
         const bool hv = fwd && (w == 0 ? h1 : (w == 1 ? h2 : true));
-        sR[w][i] = hv ? bcr_get(B.rw, blk * K + i, B.nb) : 0.;
+        sR[w][i] = hv ? bcr_get(band ? rsrc : B.rw, blk * K + i, B.nb) : 0.;
     }
     __syncthreads();
     stamp(0);
@@ -550,7 +601,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             }
 #pragma unroll
             for (int c = 0; c < CG; ++c)
-                if (c0 + c <= i) De[i * K + c0 + c] = sDe[i * KS + c0 + c] - acc[c];
+                if (c0 + c <= i) bcr_st(&De[i * K + c0 + c], sDe[i * KS + c0 + c] - acc[c]);
         } else if (h1) {
             double acc[CG];
 #pragma unroll
@@ -562,7 +613,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
                 for (int c = 0; c < CG; ++c) acc[c] = fma(v, U1[u * KS + c0 + c], acc[c]);
             }
 #pragma unroll
-            for (int c = 0; c < CG; ++c) bcr_blk(Lout, e, K)[i * K + c0 + c] = -acc[c];
+            for (int c = 0; c < CG; ++c) bcr_st(&bcr_blk(Lout, e, K)[i * K + c0 + c], -acc[c]);
         }
     }
     if (fwd) {  // r_e -= V1^T y1 + U2^T y2; the owner of o2 stores y2 and Y2^T y2
@@ -575,7 +626,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
                 acc1 = fma(U2[u * KS + ft], sR[1][u], acc1);
             }
             const int R = e * K + ft;
-            if (R < B.nb) B.rw[R] = sR[2][ft] - (acc0 + acc1);
+            if (R < B.nb) bcr_st(&B.rw[R], sR[2][ft] - (acc0 + acc1));
         } else if (h2 && ft >= 32 && ft < 32 + K) {
             const int i = ft - 32, R = o2 * K + i;
             if (R < B.nb) y[R] = sR[1][i];
@@ -583,7 +634,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             const int q = ft - 64;
             double acc = 0.;
             for (int u = 0; u < K; ++u) acc = fma(Y2[u * GS + q], sR[1][u], acc);
-            B.gpart[(size_t)o2 * nG + q] = acc;
+            bcr_st(&B.gpart[(size_t)o2 * nG + q], acc);
         }
     }
     for (int q = tid; q < nG * 4; q += blockDim.x) {
@@ -600,7 +651,7 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
         }
 #pragma unroll
         for (int c = 0; c < CG; ++c)
-            B.Gk[((size_t)e * nG + qq) * K + c0 + c] = sGe[qq * K + c0 + c] - acc[c];
+            bcr_st(&B.Gk[((size_t)e * nG + qq) * K + c0 + c], sGe[qq * K + c0 + c] - acc[c]);
     }
     if (h2) {
         // factor column of o2 for the solves: C with its diagonal replaced by
@@ -619,11 +670,18 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
             const int a = q / nG, c = q % nG;
             double acc = 0.;
             for (int u = 0; u < K; ++u) acc = fma(Y2[u * GS + a], Y2[u * GS + c], acc);
-            B.Zc[(size_t)o2 * nG * nG + q] = acc;
+            bcr_st(&B.Zc[(size_t)o2 * nG * nG + q], acc);
         }
     }
     stamp(3);
     if (tid == 0 && bad_s) atomicOr(fail, 1);  // bad_s settled at the solve barrier
+}
+
+// One elimination level.  blockIdx.x = even index / 2 (t = 2 blockIdx.x).
+template <int K, int CH, bool MF>
+__global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
+                                                   int *fail, long long *probe, double *y) {
+    bcr_level_item<K, CH, MF>(B, s, nact, ping, 2 * blockIdx.x, fail, probe, y, false, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -631,12 +689,15 @@ __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, in
 // to 8 (identity padding).  T = [D_0, G_0^T; G_0, Gd - sum_o Y_o^T Y_o] =
 // Ct Ct^T, FT = Ct^-1 (lower, N x N).
 // ---------------------------------------------------------------------------
+// ONE wave (lanes 0..63 of the workgroup; no workgroup barrier inside).
+// rg: the arrow rows of the right-hand side (nG entries).
 template <int N>
-__global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y) {
+__device__ __forceinline__ void bcr_root_wave(const BcrDev &B, int *fail, double *y,
+                                              const double *rg) {
     constexpr int NS = N + 2;
     __shared__ double T[N * NS], Ti[N * NS], col[64];
     __shared__ double zsum[NGMAX * NGMAX], gsum[NGMAX];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int K = B.K, nG = B.nG, n0 = K + nG;
     const double *D0 = B.Dk;
     // sum_o Y_o^T Y_o and sum_o gpart_o over the eliminated blocks: lanes
@@ -659,7 +720,7 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
                 gsum[e - nG * nG] = v;
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int q = lane; q < N * N; q += 64) {
         const int i = q / N, c = q % N;
         double v = 0.;
@@ -675,7 +736,7 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
         }
         T[i * NS + c] = v;
     }
-    __syncthreads();
+    wave_lds_sync();
     int bad = 0;
     bcr_chol_inv_wave<N, NS>(T, Ti, col, bad);
     wave_lds_sync();
@@ -686,7 +747,7 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
         if (lane < K) col[lane] = bcr_get(B.rw, lane, nb);
         if (lane >= K && lane < n0) {
             const int q = lane - K;
-            col[lane] = B.rw[nb + q] - gsum[q];
+            col[lane] = rg[q] - gsum[q];
         }
         wave_lds_sync();
         if (lane < n0) {
@@ -699,6 +760,11 @@ __global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y)
             }
         }
     }
+}
+
+template <int N>
+__global__ void __launch_bounds__(64) k_bcr_root(BcrDev B, int *fail, double *y) {
+    bcr_root_wave<N>(B, fail, y, B.rw + B.nb);
 }
 
 // ---------------------------------------------------------------------------
@@ -879,9 +945,6 @@ __global__ void __launch_bounds__(64) k_bcr_bwd(BcrDev B, int s, int nact, const
 // launches) are loaded before the wait.  Every spin is bounded: a timeout
 // sets bit 1 of *fail (the solve then counts as failed) instead of hanging.
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) unsigned int bcr_gu32;
-typedef __attribute__((address_space(1))) unsigned long long bcr_gu64;
-
 __device__ __forceinline__ void bcr_put(double *x, int R, double v) {
     __hip_atomic_store((bcr_gu64 *)(x + R), (unsigned long long)__double_as_longlong(v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -997,6 +1060,113 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
 }
 
 // ---------------------------------------------------------------------------
+// Factorisation in ONE launch (dataflow, MMBA_BCR_DF=0: per-level launches).
+// Items: the levels' even blocks in level order (level l has g_l = ceil(nact_l
+// / 2) items), then the root; dealt round robin to G = min(g_0, 256)
+// workgroups, all resident (one 256-thread workgroup per CU fits), each
+// taking its items in increasing order, so every wait ends.  Item k of level
+// l (e = 2k s) reads blocks e - s, e, e + s, e + 2s, which are the even blocks
+// of items 2k-1 .. 2k+2 of level l-1; it waits for exactly those (the same
+// items are the only earlier readers of the coupling buffer it overwrites,
+// Lin of level l-1).  Level 0 stages its operands from the band layout (no
+// k_bcr_load pass); the root waits for every item (the arrow sums).
+// Hand-off per MI355X guide G16 R1: every value read by another item is
+// stored write-through (bcr_st), each storing wave drains (vmcnt 0), the
+// workgroup barrier, one lane stores the item's flag = epoch; the consumer's
+// wave 0 polls its producers' flags relaxed, takes one agent-scope acquire,
+// drains, and the barrier releases the other waves to load.  Every spin is
+// bounded (timeout: bit 1 of *fail, the solve counts as failed).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool bcr_wait_items(const int *flags, int lo, int hi,
+                                               unsigned epoch) {
+    // flags[lo .. hi) == epoch (hi - lo <= 64 per pass; wave-uniform result)
+    const int lane = threadIdx.x & 63;
+    for (int b = lo; b < hi; b += 64) {
+        const int i = b + lane;
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+            if (i < hi)
+                ok = __hip_atomic_load((bcr_gu32 *)(flags + i), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+            if (spins > (1u << 22)) return false;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return true;
+}
+
+template <int K, int N>
+__global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, const double *r,
+                                                       double *y, unsigned epoch,
+                                                       long long *trace) {
+    // trace (diagnostic, MMBA_PROBE=1): per item the 100 MHz wall clock at
+    // entry, after the wait, after the item, after the flag store
+    __shared__ int ok_s;
+    const int tid = threadIdx.x;
+    int base = 0, pbase = 0, pg = 0, s = 1, nact = B.nblk, lvl = 0;
+    for (int it = blockIdx.x;; it += gridDim.x) {
+        while (nact > 1 && it >= base + (nact + 1) / 2) {
+            pbase = base;
+            pg = (nact + 1) / 2;
+            base += pg;
+            s *= 2;
+            nact = pg;
+            ++lvl;
+        }
+        if (nact <= 1) {  // the root: item index base, after every level item
+            if (it == base && tid < 64) {
+                if (trace && tid == 0) trace[4 * it] = (long long)wall_clock64();
+                if (bcr_wait_items(B.fflags, 0, base, epoch)) {
+                    if (trace && tid == 0) trace[4 * it + 1] = (long long)wall_clock64();
+                    bcr_root_wave<N>(B, fail, y, y ? r + B.nb : nullptr);
+                    if (trace && tid == 0) trace[4 * it + 2] = trace[4 * it + 3] =
+                        (long long)wall_clock64();
+                } else if (tid == 0) {
+                    atomicOr(fail, 2);
+                }
+            }
+            return;
+        }
+        const int k = it - base;
+        if (trace && tid == 0) trace[4 * it] = (long long)wall_clock64();
+        __syncthreads();  // the previous item's LDS reads are done
+        if (lvl > 0) {
+            if (tid < 64) {
+                const int lo = max(2 * k - 1, 0), hi = min(2 * k + 3, pg);
+                const bool ok = bcr_wait_items(B.fflags, pbase + lo, pbase + hi, epoch);
+                if (tid == 0) ok_s = ok;
+            }
+            __syncthreads();
+            if (!ok_s) {
+                if (tid == 0) atomicOr(fail, 2);
+                continue;  // no flag: the items that need this one time out too
+            }
+        }
+        if (trace && tid == 0) trace[4 * it + 1] = (long long)wall_clock64();
+        bcr_level_item<K, 2, true>(B, s, nact, lvl & 1, 2 * k, fail, nullptr, y, lvl == 0, r);
+        if (trace && tid == 0) trace[4 * it + 2] = (long long)wall_clock64();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_store((bcr_gu32 *)(B.fflags + it), epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            if (trace) trace[4 * it + 3] = (long long)wall_clock64();
+        }
+    }
+}
+
+static std::atomic<unsigned> g_bcr_epoch{0};
+
+static unsigned bcr_next_epoch() {
+    unsigned ep = ++g_bcr_epoch;
+    if (ep == 0) ep = ++g_bcr_epoch;  // flags start at 0: never use epoch 0
+    return ep;
+}
+
+// ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
 // Factorisation; with r != nullptr the forward solve y = L^-1 r runs inside
@@ -1005,8 +1175,19 @@ template <int K>
 static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
                          const double *r, double *y) {
     const BcrDev &D = B.bcr;
-    k_bcr_load<K><<<D.nblk, 256, 0, s>>>(D, r);
     double *yy = r ? y : nullptr;
+    if (D.fflags && D.nblk >= 2 && D.regchol == 2 && D.mfma_upd) {
+        const unsigned ep = bcr_next_epoch();
+        const int G = std::min((D.nblk + 1) / 2, 256);
+        long long *tr = probe ? probe + 4 : nullptr;
+        switch (D.NR - K) {
+            case 0: k_bcr_factor_df<K, K><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
+            case 8: k_bcr_factor_df<K, K + 8><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
+            default: k_bcr_factor_df<K, K + 16><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
+        }
+        return;
+    }
+    k_bcr_load<K><<<D.nblk, 256, 0, s>>>(D, r);
     int ping = 0;
     for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) {
         const int g = (nact + 1) / 2;
@@ -1043,14 +1224,11 @@ static void bcr_forward_k(hipStream_t s, const BandSolver &B, const double *r, d
     k_bcr_fwd_root<K><<<1, 64, 0, s>>>(D, D.rw, y);
 }
 
-static std::atomic<unsigned> g_bcr_epoch{0};
-
 template <int K>
 static void bcr_backward_k(hipStream_t s, const BandSolver &B, const double *y, double *x) {
     const BcrDev &D = B.bcr;
     if (D.flags && D.fail) {  // one dataflow launch
-        unsigned ep = ++g_bcr_epoch;
-        if (ep == 0) ep = ++g_bcr_epoch;  // flags start at 0: never use epoch 0
+        const unsigned ep = bcr_next_epoch();
         k_bcr_bwd_all<K><<<std::min(D.nblk, 256), 64, 0, s>>>(D, y, x, ep, D.fail);
         return;
     }

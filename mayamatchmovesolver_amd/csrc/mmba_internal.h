@@ -78,6 +78,9 @@ struct BcrDev {
     // blocks in dependency order, the plan's fail flag (nullptr: per-level launches)
     int *flags = nullptr;
     const int *ord = nullptr;
+    // dataflow factorisation (k_bcr_factor_df): one flag per level item and
+    // the root (nullptr: per-level launches, MMBA_BCR_DF=0)
+    int *fflags = nullptr;
     int *fail = nullptr;
     // with xs: the backward solve also scatters x_R to parameter order
     // (xs[row_param[R]] = x_R, k_scatter_xR's job)

@@ -156,7 +156,8 @@ void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, 
                            double *x);
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                          const double *Lb, const double *v, double *wR, double *usq);
+                          const double *Lb, const double *v, double *wR, double *usq,
+                          double *un, double *gp);
 void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double *vR, int nRpad);
 // Band + arrow reduced system (mmba_band.hip): factorisation in place, then
 // L y = r (band_forward; keeps the separator part of y for band_backward) and

@@ -1925,50 +1925,54 @@ __global__ void k_scatter_xR(DevProblem P, const double *__restrict__ xR, double
     if (P.p_class[p] != PC_B) x[p] = xR[P.p_pos[p]];
 }
 
-// Newton-correction helpers: u_b = Lb^-1 v_b (sum |u_b|^2 per bundle into
-// usq[b]) and w_R = v_R - sum_b W_b u_b.
-__global__ void k_newton_bundle(DevProblem P, const double *__restrict__ W,
-                                const double *__restrict__ Wg, const double *__restrict__ Lb,
-                                const double *__restrict__ v, double *wR, double *usq) {
+// Newton-correction helpers: u_b = Lb^-1 v_b per bundle (|u_b|^2 into
+// usq[b], u_b into un[3 b], and the bundle's global-row terms Wg_b u_b into
+// gp[q nB + b]); the camera-frame rows w_R -= sum_b W_b u_b are then the
+// fixed-order per-camera-frame gather of k_schur_rhs and the global rows a
+// fixed-order reduction (k_newton_glob): no floating-point atomics, so the
+// solve is bit-for-bit repeatable.
+__global__ void k_newton_bundle(DevProblem P, const double *__restrict__ Wg,
+                                const double *__restrict__ Lb, const double *__restrict__ v,
+                                double *un, double *gp, double *usq) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
-    if (pb == 0) {
-        usq[b] = 0.;
-        return;
-    }
     const int nG = P.nG;
-    const int nCF = P.nR - nG;
-    const int po = P.bnd_par_off[b];
-    const bool ownb = own_bnd(P, b);
-    double L[3][3];
-    for (int a = 0; a < 3; ++a)
-        for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
     double u[3] = {0., 0., 0.};
-    for (int a = 0; a < pb; ++a) {
-        double t = v[P.bnd_par[po + a]];
-        for (int k = 0; k < a; ++k) t -= L[a][k] * u[k];
-        u[a] = t / L[a][a];
-    }
-    usq[b] = ownb ? u[0] * u[0] + u[1] * u[1] + u[2] * u[2] : 0.;
-    for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-        const int i = P.bobs[q];
-        const int cf = P.obs_cf[i];
-        if (!own_cf(P, cf)) continue;
-        const int pc = P.cf_pc[cf];
-        const int r0 = P.cf_roff[cf];
-        for (int a = 0; a < pc; ++a) {
-            double s = 0.;
-            for (int c = 0; c < 3; ++c) s += W[widx(P, a * 3 + c, i)] * u[c];
-            atomicAdd(&wR[r0 + a], -s);
+    if (pb > 0) {
+        const int po = P.bnd_par_off[b];
+        double L[3][3];
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+        for (int a = 0; a < pb; ++a) {
+            double t = v[P.bnd_par[po + a]];
+            for (int k = 0; k < a; ++k) t -= L[a][k] * u[k];
+            u[a] = t / L[a][a];
         }
     }
-    if (!ownb) return;
+    const bool ownb = pb > 0 && own_bnd(P, b);
+    usq[b] = ownb ? u[0] * u[0] + u[1] * u[1] + u[2] * u[2] : 0.;
+    for (int c = 0; c < 3; ++c) un[(size_t)b * 3 + c] = u[c];
     for (int q = 0; q < nG; ++q) {
-        double s = 0.;
-        for (int c = 0; c < 3; ++c) s += Wg[((size_t)b * NGMAX + q) * 3 + c] * u[c];
-        atomicAdd(&wR[nCF + q], -s);
+        double g = 0.;
+        if (ownb)
+            for (int c = 0; c < 3; ++c) g += Wg[((size_t)b * NGMAX + q) * 3 + c] * u[c];
+        gp[(size_t)q * P.nB + b] = g;
     }
+}
+
+// w_R[nCF + q] -= sum_b gp[q nB + b], one workgroup per global row, fixed order.
+__global__ void __launch_bounds__(256) k_newton_glob(DevProblem P, const double *__restrict__ gp,
+                                                     double *wR) {
+    const int q = blockIdx.x;
+    __shared__ double red[4];
+    double acc = 0.;
+    for (int b = threadIdx.x; b < P.nB; b += 256) acc += gp[(size_t)q * P.nB + b];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) wR[P.nR - P.nG + q] -= (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // v (parameter order) -> R order (non-bundle parameters); padded tail zero.
@@ -2594,9 +2598,12 @@ void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, dou
     k_scatter_xR<<<nblk(P.n, 256), 256, 0, s>>>(P, xR, x);
 }
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
-                          const double *Lb, const double *v, double *wR, double *usq) {
-    if (P.nB > 0)
-        k_newton_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, W, Wg, Lb, v, wR, usq);
+                          const double *Lb, const double *v, double *wR, double *usq,
+                          double *un, double *gp) {
+    if (P.nB == 0) return;
+    k_newton_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, Wg, Lb, v, un, gp, usq);
+    if (P.ncf > 0) k_schur_rhs<<<P.ncf, 64, 0, s>>>(P, W, un, wR);
+    if (P.nG > 0) k_newton_glob<<<P.nG, 256, 0, s>>>(P, gp, wR);
 }
 void launch_gather_R(hipStream_t s, const DevProblem &P, const double *v, double *vR, int nRpad) {
     const int n = P.n > nRpad ? P.n : nRpad;

@@ -424,7 +424,7 @@ void Plan::newton_enqueue(double dxnorm) {
     MMBA_HIP(hipMemsetAsync(d_scalar + SL_NEWT_B, 0, 2 * sizeof(double), s));
     if (nR > 0) launch_gather_R(s, P, d_v, d_wR, nRpad);
     if (nB_solved > 0) {
-        launch_newton_bundle(s, P, d_W, d_Wg, d_Lb, d_v, d_wR, d_usq);
+        launch_newton_bundle(s, P, d_W, d_Wg, d_Lb, d_v, d_wR, d_usq, d_nu, d_ngp);
         launch_reduce_sum(s, d_usq, nB, d_scalar + SL_NEWT_B);
     }
     if (nR > 0) {

@@ -25,7 +25,38 @@
 namespace mmba {
 
 Plan::~Plan() {
-    if (d_probe && bs.use_bcr) {
+    if (d_probe && bs.use_bcr && bs.bcr.fflags && bs.bcr.nblk >= 2) {
+        // dataflow factor trace of the last factorisation: per level, the
+        // mean wait, item and publish times and the level's span (us)
+        const int nit = bs.bcr.nblk + 64;
+        std::vector<long long> t((size_t)4 + 4 * nit, 0);
+        if (hipMemcpy(t.data(), d_probe, sizeof(long long) * t.size(), hipMemcpyDeviceToHost) ==
+            hipSuccess) {
+            const long long *tr = t.data() + 4;
+            long long t0 = tr[0];
+            for (int i = 0; i < nit && (tr[4 * i] || tr[4 * i + 3]); ++i) t0 = std::min(t0, tr[4 * i]);
+            int base = 0, lvl = 0;
+            for (int nact = bs.bcr.nblk;; nact = (nact + 1) / 2, ++lvl) {
+                const int g = nact > 1 ? (nact + 1) / 2 : 1;
+                double w = 0, c = 0, p = 0, lo = 1e30, hi = 0;
+                for (int i = base; i < base + g; ++i) {
+                    const long long *q = tr + 4 * i;
+                    w += q[1] - q[0];
+                    c += q[2] - q[1];
+                    p += q[3] - q[2];
+                    lo = std::min(lo, (double)(q[1] - t0));
+                    hi = std::max(hi, (double)(q[3] - t0));
+                }
+                std::fprintf(stderr,
+                             "[mmba probe] bcr df level %d items %d: wait %.2f item %.2f publish "
+                             "%.2f us (means); work from %.2f to %.2f us\n",
+                             lvl, g, w / g / 100., c / g / 100., p / g / 100., lo / 100.,
+                             hi / 100.);
+                base += g;
+                if (nact <= 1) break;
+            }
+        }
+    } else if (d_probe && bs.use_bcr) {
         long long h[4] = {0, 0, 0, 0};
         if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
             std::fprintf(stderr,
@@ -903,8 +934,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         }
     if (band) setup_band();
     if (band && std::getenv("MMBA_PROBE")) {
-        d_probe = dalloc<long long>(4);
-        MMBA_HIP(hipMemsetAsync(d_probe, 0, 4 * sizeof(long long), s));
+        const size_t np = 4 + 4 * ((size_t)std::max(nR, 1) + 64);  // + the dataflow trace
+        d_probe = dalloc<long long>(np);
+        MMBA_HIP(hipMemsetAsync(d_probe, 0, np * sizeof(long long), s));
     }
 
     d_x = dalloc<double>(n);
@@ -959,6 +991,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_xR = dalloc<double>(nRpad);
     d_wR = dalloc<double>(nRpad);
     d_usq = dalloc<double>(nB);
+    d_nu = dalloc<double>((size_t)3 * std::max(nB, 1));
+    d_ngp = dalloc<double>((size_t)std::max(nG, 1) * std::max(nB, 1));
     pw = std::max(std::max(nparts, residual_blocks(P)), ncf + (nB + 255) / 256);
     d_partial = dalloc<double>((size_t)8 * pw);  // rows 0..7 (launch_dist_stats: 0..2)
     d_scalar = dalloc<double>(NSLOT);
@@ -1165,6 +1199,13 @@ void Plan::setup_band(int Pforce) {
             B.FT = dalloc<double>((size_t)B.NR * B.NR);
             B.gpart = dalloc<double>((size_t)B.nblk * nG);
             B.rw = dalloc<double>((size_t)nb + nG);
+            {
+                const char *e5 = std::getenv("MMBA_BCR_DF");
+                if (!(e5 && std::atoi(e5) == 0)) {
+                    B.fflags = dalloc<int>((size_t)B.nblk + 64);  // items < nblk + levels
+                    MMBA_HIP(hipMemsetAsync(B.fflags, 0, sizeof(int) * ((size_t)B.nblk + 64), s));
+                }
+            }
             {
                 // dataflow backward solve: blocks in dependency order (root,
                 // then levels coarse to fine); MMBA_BCR_BWD_LEVELS=1 keeps the

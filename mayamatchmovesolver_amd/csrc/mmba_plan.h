@@ -152,7 +152,7 @@ struct Plan {
            *d_Agg = nullptr, *d_glob_partial = nullptr;
     double *d_Lb = nullptr, *d_tb = nullptr, *d_Wg = nullptr, *d_W = nullptr, *d_U = nullptr;
     double *d_rhs = nullptr, *d_yR = nullptr, *d_xR = nullptr, *d_wR = nullptr,
-           *d_usq = nullptr;
+           *d_usq = nullptr, *d_nu = nullptr, *d_ngp = nullptr;  // Newton-term scratch
     double *d_partial = nullptr, *d_scalar = nullptr;
     double *d_gather = nullptr;  // outputs in reference order: f | eu | ed | x
     int *d_fail = nullptr;
