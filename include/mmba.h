@@ -447,12 +447,15 @@ typedef struct mmba_kernel_stats {
     double resid_bytes;
     int32_t resid_launches;
     double chol_ms_avg;     /* reduced camera system Cholesky             */
-    double chol_flops;      /* n_r^3/3 per factorisation                  */
+    double chol_flops;      /* flops per factorisation as performed: n_r^3/3
+                               (dense / tiled), block cyclic reduction's
+                               per-block count, band or block-diagonal
+                               Cholesky counts                             */
     int32_t chol_launches;
     int32_t reduced_dim;    /* n_r = camera-frame + global parameters     */
     int32_t reduced_kind;   /* 0 band (block cyclic reduction / partitioned),
                                1 tiled sparse Cholesky, 2 dense blocked
-                               Cholesky (chol_flops is exact only for 2),
+                               Cholesky,
                                3 block diagonal + arrow (no solved bundle) */
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,

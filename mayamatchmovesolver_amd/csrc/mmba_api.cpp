@@ -261,7 +261,24 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         }
         out->jac_bytes = bj * p.M;
         out->resid_bytes = 48.0 * p.M;
-        out->chol_flops = (double)p.nRpad * p.nRpad * p.nRpad / 3.0;
+        // reduced-system flops per factorisation as each solver performs them
+        if (p.band && p.bs.use_bcr) {
+            // block cyclic reduction: per eliminated K x K block its Cholesky
+            // (K^3/3), U / V / Y / y solves (2K^3 + nG K^2 + K^2), the two
+            // symmetric Schur updates (2 x K^3), the coupling (2K^3), the arrow
+            // terms (4 nG K^2 + nG^2 K); the root: Cholesky + inverse (2 N^3/3)
+            const double K = p.bs.bcr.K, G = p.bs.bcr.nG, N = p.bs.bcr.NR;
+            out->chol_flops = (p.bs.bcr.nblk - 1) * (19.0 / 3.0 * K * K * K + 5.0 * G * K * K +
+                                                     G * G * K + K * K) +
+                              2.0 * N * N * N / 3.0;
+        } else if (p.band && p.bs.use_bd) {
+            const double pc = p.ncf ? (double)p.nCF / p.ncf : 0.;  // per camera-frame block
+            out->chol_flops = (double)p.nCF * pc * pc / 3.0;
+        } else if (p.band) {
+            out->chol_flops = (double)(p.nR - p.nG) * p.bw * p.bw;  // band Cholesky
+        } else {
+            out->chol_flops = (double)p.nRpad * p.nRpad * p.nRpad / 3.0;
+        }
     }
     p.timing = enable_timing != 0;
     if (enable_timing) {

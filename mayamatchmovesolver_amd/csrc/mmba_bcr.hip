@@ -282,13 +282,18 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
 template <int K, int PW>
 __device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out, double *pl,
                                                  int &bad) {
-    const int lane = threadIdx.x & 63;
+    const int lane0 = threadIdx.x & 63;
     double rsl = 0.;
     bool anybad = false;
 #pragma unroll
     for (int j0 = 0; j0 < K; j0 += PW) {
 #pragma unroll
         for (int j = j0; j < j0 + PW && j < K; ++j) {
+            // the lane id laundered per step: the lane masks of this step are
+            // formed here (one v_cmp each) instead of 2K masks live across the
+            // whole chain (SGPR spills to VGPR lanes)
+            int lane = lane0;
+            asm volatile("" : "+v"(lane));
             double d = bcr_rdlane(a[j], j);
             if (!(d > 0.) || !isfinite(d)) {
                 anybad = true;
@@ -302,6 +307,8 @@ __device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out,
             for (int c = j + 1; c < j0 + PW && c < K; ++c) a[c] = fma(-l, bcr_rdlane(l, c), a[c]);
         }
         if (j0 + PW < K) {
+            int lane = lane0;
+            asm volatile("" : "+v"(lane));
             // panel image: p_k(lane) = L[lane][k] below the diagonal, x_k in
             // the right-hand-side lanes, 0 on and above the diagonal
 #pragma unroll
@@ -319,7 +326,7 @@ __device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out,
         }
     }
     if (anybad) bad = 1;
-    if (rs_out && lane < K) rs_out[lane] = rsl;
+    if (rs_out && lane0 < K) rs_out[lane0] = rsl;
 }
 
 // In-place forward substitution X <- C^-1 X for the column this lane owns
@@ -423,6 +430,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     __shared__ double sRs[2][K];       // 1 / C_jj
     __shared__ double col[4][64 * 8];  // pivot column (LDS chain) / panel image (blocked chain)
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
+    __shared__ double sZero[2];
     __shared__ int bad_s;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int e = t * s;
@@ -435,13 +443,14 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     const double *Lin = ping ? B.Lk1 : B.Lk0;
     double *Lout = ping ? B.Lk0 : B.Lk1;
     if (tid == 0) bad_s = 0;
+    if (tid == 1) sZero[0] = 0.;
     // probe (diagnostic, MMBA_PROBE=1): thread 0 of workgroup 0 accumulates
-    // clock64 cycles per phase; never read by the solver.
+    // wall-clock ticks (100 MHz) per phase; never read by the solver.
     const bool prb = probe && blockIdx.x == 0 && tid == 0;
-    long long tprev = prb ? (long long)clock64() : 0;
+    long long tprev = prb ? (long long)wall_clock64() : 0;
     auto stamp = [&](int ph) {
         if (prb) {
-            const long long tn = (long long)clock64();
+            const long long tn = (long long)wall_clock64();
             atomicAdd((unsigned long long *)&probe[ph], (unsigned long long)(tn - tprev));
             tprev = tn;
         }
@@ -461,8 +470,9 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
             if (h2) bcr_band_dl<K>(B, o2, q, d1, b2);
             if (hn) bcr_band_dl<K>(B, en, q, dz, b3);
         } else {
-            if (h1) d0 = bcr_blk(B.Dk, o1, K)[q];
-            if (h2) d1 = bcr_blk(B.Dk, o2, K)[q];
+            // lower part only (the upper part of a stored block is never written)
+            if (h1 && c <= i) d0 = bcr_blk(B.Dk, o1, K)[q];
+            if (h2 && c <= i) d1 = bcr_blk(B.Dk, o2, K)[q];
             if (h1) b0 = bcr_blk((double *)Lin, o1, K)[q];
             if (h1) b1 = bcr_blk((double *)Lin, e, K)[q];
             if (h2) b2 = bcr_blk((double *)Lin, o2, K)[q];
@@ -525,31 +535,51 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
                 xs = GS;
             }
         }
+        // one LDS source per lane (rows: D_o with its upper part zeroed by
+        // the stage; lanes without an operand read a zero), no per-entry masks
+        const double *src = sZero;
+        int st = 0;
+        if (lane < K) {
+            src = &sD[w][lane * KS];
+            st = 1;
+        } else if (xp) {
+            src = xp;
+            st = xs;
+        }
         double a[K];
 #pragma unroll
-        for (int c = 0; c < K; ++c)
-            a[c] = lane < K ? (c <= lane ? sD[w][lane * KS + c] : 0.) : (xp ? xp[c * xs] : 0.);
+        for (int c = 0; c < K; ++c) a[c] = src[c * st];
         __syncthreads();  // every wave holds its operands: stores below may overwrite them
+        stamp(1);
         if (act) {
             if constexpr (CH == 2)
                 bcr_chol_aug_blk<K, 8>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
             else
                 bcr_chol_aug_wave<K>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
         }
+        stamp(2);
         if (act) {
+            // one LDS destination per lane: C (rows of the half-0 wave; its
+            // dead upper entries are stored too, every reader of FC masks
+            // them), the solved right-hand sides; other lanes write their own
+            // slot of the chain scratch
+            double *dst = &col[wv][lane * 8];
+            int dt = 0;
             if (lane < K) {
-                if (half == 0)
-#pragma unroll
-                    for (int c = 0; c < K; ++c) sD[w][lane * KS + c] = (c <= lane) ? a[c] : 0.;
+                if (half == 0) {
+                    dst = &sD[w][lane * KS];
+                    dt = 1;
+                }
             } else if (xp) {
-#pragma unroll
-                for (int c = 0; c < K; ++c) xp[c * xs] = a[c];
+                dst = xp;
+                dt = xs;
             }
+#pragma unroll
+            for (int c = 0; c < K; ++c) dst[c * dt] = a[c];
         }
         if (bad) atomicOr(&bad_s, 1);
         __syncthreads();
-        stamp(1);
-        stamp(2);
+        stamp(3);
     } else {
     // A. Cholesky of the two odd neighbours, one wave each
     if (wv == 0 && h1) bcr_chol_wave<K, KS>(sD[0], sRs[0], col[0], bad);
@@ -576,6 +606,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     }
     __syncthreads();
     stamp(2);
+    stamp(3);
     }
     // C. updates of the even block: D_e -= V1^T V1 + U2^T U2 (lower), new
     // coupling -V1^T U1, G_e -= Y1^T V1 + Y2^T U2; stored factor columns of o2
@@ -584,6 +615,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     double *De = bcr_blk(B.Dk, e, K);
     if constexpr (MF && K <= 32) {
         bcr_updates_mfma<K, KS>(U1, V1, U2, sDe, De, bcr_blk(Lout, e, K), h1, wv, lane);
+        stamp(4);
     } else
     for (int q = tid; q < 2 * 4 * K; q += blockDim.x) {
         const int m = q / (4 * K), r = q % (4 * K), i = r / 4, c0 = (r % 4) * CG;
@@ -673,7 +705,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
             bcr_st(&B.Zc[(size_t)o2 * nG * nG + q], acc);
         }
     }
-    stamp(3);
+    stamp(5);
     if (tid == 0 && bad_s) atomicOr(fail, 1);  // bad_s settled at the solve barrier
 }
 
@@ -738,7 +770,22 @@ __device__ __forceinline__ void bcr_root_wave(const BcrDev &B, int *fail, double
     }
     wave_lds_sync();
     int bad = 0;
-    bcr_chol_inv_wave<N, NS>(T, Ti, col, bad);
+    if constexpr (2 * N <= 64) {
+        // augmented chain: identity columns in lanes N..2N-1 come out as the
+        // columns of Ct^-1 (the same operations as the column-oriented
+        // inverse of bcr_chol_inv_wave, riding on the one pivot chain)
+        double a[N];
+        const int cc = lane - N;
+#pragma unroll
+        for (int c = 0; c < N; ++c)
+            a[c] = lane < N ? (c <= lane ? T[lane * NS + c] : 0.) : (c == cc ? 1. : 0.);
+        bcr_chol_aug_wave<N>(a, nullptr, col, bad);
+        if (lane >= N && lane < 2 * N)
+#pragma unroll
+            for (int i = 0; i < N; ++i) Ti[i * NS + cc] = a[i];
+    } else {
+        bcr_chol_inv_wave<N, NS>(T, Ti, col, bad);
+    }
     wave_lds_sync();
     for (int q = lane; q < N * N; q += 64) B.FT[q] = Ti[(q / N) * NS + q % N];
     if (bad && lane == 0) atomicOr(fail, 1);
@@ -1146,7 +1193,8 @@ __global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, cons
             }
         }
         if (trace && tid == 0) trace[4 * it + 1] = (long long)wall_clock64();
-        bcr_level_item<K, 2, true>(B, s, nact, lvl & 1, 2 * k, fail, nullptr, y, lvl == 0, r);
+        bcr_level_item<K, 2, true>(B, s, nact, lvl & 1, 2 * k, fail, trace ? trace - 8 : nullptr, y,
+                                   lvl == 0, r);
         if (trace && tid == 0) trace[4 * it + 2] = (long long)wall_clock64();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1179,7 +1227,7 @@ static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long lon
     if (D.fflags && D.nblk >= 2 && D.regchol == 2 && D.mfma_upd) {
         const unsigned ep = bcr_next_epoch();
         const int G = std::min((D.nblk + 1) / 2, 256);
-        long long *tr = probe ? probe + 4 : nullptr;
+        long long *tr = probe ? probe + 8 : nullptr;
         switch (D.NR - K) {
             case 0: k_bcr_factor_df<K, K><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
             case 8: k_bcr_factor_df<K, K + 8><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;

@@ -29,10 +29,14 @@ Plan::~Plan() {
         // dataflow factor trace of the last factorisation: per level, the
         // mean wait, item and publish times and the level's span (us)
         const int nit = bs.bcr.nblk + 64;
-        std::vector<long long> t((size_t)4 + 4 * nit, 0);
+        std::vector<long long> t((size_t)8 + 4 * nit, 0);
         if (hipMemcpy(t.data(), d_probe, sizeof(long long) * t.size(), hipMemcpyDeviceToHost) ==
             hipSuccess) {
-            const long long *tr = t.data() + 4;
+            std::fprintf(stderr,
+                         "[mmba probe] bcr df phase 10-ns ticks (workgroup 0, all items, all solves): "
+                         "stage %lld a-load %lld chain %lld store %lld mfma-upd %lld tail %lld\n",
+                         t[0], t[1], t[2], t[3], t[4], t[5]);
+            const long long *tr = t.data() + 8;
             long long t0 = tr[0];
             for (int i = 0; i < nit && (tr[4 * i] || tr[4 * i + 3]); ++i) t0 = std::min(t0, tr[4 * i]);
             int base = 0, lvl = 0;
@@ -57,12 +61,12 @@ Plan::~Plan() {
             }
         }
     } else if (d_probe && bs.use_bcr) {
-        long long h[4] = {0, 0, 0, 0};
+        long long h[6] = {0, 0, 0, 0, 0, 0};
         if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
             std::fprintf(stderr,
-                         "[mmba probe] bcr level cycles (workgroup 0, all levels): stage %lld "
-                         "chol+inv %lld products %lld updates %lld (K=%d nblk=%d)\n",
-                         h[0], h[1], h[2], h[3], bs.bcr.K, bs.bcr.nblk);
+                         "[mmba probe] bcr level 10-ns ticks (workgroup 0, all levels): stage %lld "
+                         "a-load %lld chain %lld store %lld mfma-upd %lld tail %lld (K=%d nblk=%d)\n",
+                         h[0], h[1], h[2], h[3], h[4], h[5], bs.bcr.K, bs.bcr.nblk);
     } else if (d_probe) {
         long long h[4] = {0, 0, 0, 0};
         if (hipMemcpy(h, d_probe, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
@@ -934,7 +938,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         }
     if (band) setup_band();
     if (band && std::getenv("MMBA_PROBE")) {
-        const size_t np = 4 + 4 * ((size_t)std::max(nR, 1) + 64);  // + the dataflow trace
+        const size_t np = 8 + 4 * ((size_t)std::max(nR, 1) + 64);  // + the dataflow trace
         d_probe = dalloc<long long>(np);
         MMBA_HIP(hipMemsetAsync(d_probe, 0, np * sizeof(long long), s));
     }

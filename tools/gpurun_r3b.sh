@@ -1,0 +1,7 @@
+set -o pipefail
+OUT=gpurun_out/r3b
+mkdir -p $OUT
+timeout -k 10 60 ./tools/ubench/bcr_chain > $OUT/chain.txt 2>&1 || exit 1
+cat $OUT/chain.txt
+timeout -k 10 60 ./tools/ubench/bcr_item > $OUT/item.txt 2>&1 || exit 1
+cat $OUT/item.txt
