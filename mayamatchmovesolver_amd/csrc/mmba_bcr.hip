@@ -418,7 +418,8 @@ __device__ __forceinline__ void bcr_band_dl(const BcrDev &B, int b, int q, doubl
 template <int K, int CH, bool MF>  // CH: pivot chain variant (BcrDev::regchol); MF: MFMA updates
 __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact, int ping,
                                                const int t, int *fail, long long *probe,
-                                               double *y, bool band, const double *rsrc) {
+                                               double *y, bool band, const double *rsrc,
+                                               int *pub = nullptr, unsigned pub_epoch = 0) {
     constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
     constexpr int CG = K / 4;     // columns per update task
     constexpr int GS = NGMAX;     // row stride of the K x nG arrays
@@ -455,6 +456,15 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
             tprev = tn;
         }
     };
+    // the right-hand-side rows first: their loads join the operand loads
+    // below (one memory round trip for the whole stage)
+    double rv = 0.;
+    if (tid < 3 * K) {
+        const int w = tid / K, i = tid % K;
+        const int blk = w == 0 ? o1 : (w == 1 ? o2 : e);
+        const bool hv = fwd && (w == 0 ? h1 : (w == 1 ? h2 : true));
+        rv = hv ? bcr_get(band ? rsrc : B.rw, blk * K + i, B.nb) : 0.;
+    }
     // stage every operand (zeros where a neighbour does not exist); fixed
     // trip count so every round's loads are issued before the first store
 #pragma unroll
@@ -504,12 +514,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
         sGe[q] = band ? (C < B.nb ? B.Ga[(size_t)(q / K) * B.nb + C] : 0.)
                       : B.Gk[(size_t)e * nG * K + q];
     }
-    if (tid < 3 * K) {
-        const int w = tid / K, i = tid % K;
-        const int blk = w == 0 ? o1 : (w == 1 ? o2 : e);
-        const bool hv = fwd && (w == 0 ? h1 : (w == 1 ? h2 : true));
-        sR[w][i] = hv ? bcr_get(band ? rsrc : B.rw, blk * K + i, B.nb) : 0.;
-    }
+    if (tid < 3 * K) sR[tid / K][tid % K] = rv;
     __syncthreads();
     stamp(0);
     int bad = 0;
@@ -668,6 +673,16 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
             for (int u = 0; u < K; ++u) acc = fma(Y2[u * GS + q], sR[1][u], acc);
             bcr_st(&B.gpart[(size_t)o2 * nG + q], acc);
         }
+    }
+    if (pub && nG == 0) {
+        // dataflow factor without an arrow: the next level reads only D_e,
+        // the new coupling and r_e, all stored above -- release them now;
+        // the factor columns of o2 below are read by later launches only
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store((bcr_gu32 *)pub, pub_epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     for (int q = tid; q < nG * 4; q += blockDim.x) {
         const int qq = q / 4, c0 = (q % 4) * CG;
@@ -1122,7 +1137,9 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
 // workgroup barrier, one lane stores the item's flag = epoch; the consumer's
 // wave 0 polls its producers' flags relaxed, takes one agent-scope acquire,
 // drains, and the barrier releases the other waves to load.  Every spin is
-// bounded (timeout: bit 1 of *fail, the solve counts as failed).
+// bounded (timeout: bit 1 of *fail, the solve counts as failed).  Without
+// an arrow (nG = 0) the item publishes as soon as D_e, the new coupling and
+// r_e are stored, before its factor-column stores (read by later launches).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool bcr_wait_items(const int *flags, int lo, int hi,
                                                unsigned epoch) {
@@ -1194,7 +1211,7 @@ __global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, cons
         }
         if (trace && tid == 0) trace[4 * it + 1] = (long long)wall_clock64();
         bcr_level_item<K, 2, true>(B, s, nact, lvl & 1, 2 * k, fail, trace ? trace - 8 : nullptr, y,
-                                   lvl == 0, r);
+                                   lvl == 0, r, B.fflags + it, epoch);
         if (trace && tid == 0) trace[4 * it + 2] = (long long)wall_clock64();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();

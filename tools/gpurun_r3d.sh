@@ -1,8 +1,8 @@
 # BCR laundered chain + uniform LDS operand addressing: parity subset, probe, C4 kernel stats
 set -o pipefail
-OUT=gpurun_out/r3d
+OUT=gpurun_out/r3e
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_bcr_variants.py tests/test_gpu_band.py tests/test_gpu_golden.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
+timeout -k 10 60 ./tools/ubench/bcr_item > $OUT/item.txt 2>&1 && tail -2 $OUT/item.txt && timeout -k 10 400 python -u -m pytest tests/test_gpu_bcr_variants.py tests/test_gpu_band.py tests/test_gpu_golden.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit 1
 MMBA_PROBE=1 timeout -k 10 120 python -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > $OUT/probe.json 2> $OUT/probe.err || exit 1
 grep "mmba probe" $OUT/probe.err

@@ -10,11 +10,12 @@
 using namespace mmba;
 constexpr int K = 24, NBLK = 8, REPS = 16;
 
+template <int CH>
 __global__ void __launch_bounds__(256) kitem(BcrDev B, int *fail, long long *t) {
     for (int r = 0; r < REPS; ++r) {
         __syncthreads();
         const long long t0 = wall_clock64();
-        bcr_level_item<K, 2, true>(B, 2, NBLK, 0, 2, fail, r > 0 ? t + 64 : nullptr, B.rw + 4096,
+        bcr_level_item<K, CH, true>(B, 2, NBLK, 0, 2, fail, r > 0 ? t + 64 : nullptr, B.rw + 4096,
                                    false, nullptr);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -69,15 +70,18 @@ int main() {
     double *x;
     hipMalloc(&x, 256 * sizeof(double));
     hipMemset(x, 0, 256 * sizeof(double));
-    for (int run = 0; run < 3; ++run) {
+    for (int run = 0; run < 4; ++run) {
         hipMemcpy(B.Dk, hD.data(), kk * sizeof(double), hipMemcpyHostToDevice);
         hipMemcpy(B.Lk0, hL.data(), kk * sizeof(double), hipMemcpyHostToDevice);
         hipMemset(t, 0, 128 * sizeof(long long));
         kother<<<1024, 256>>>(x);
-        kitem<<<1, 256>>>(B, fail, t);
+        if (run & 1)
+            kitem<0><<<1, 256>>>(B, fail, t);
+        else
+            kitem<2><<<1, 256>>>(B, fail, t);
         hipDeviceSynchronize();
         hipMemcpy(h, t, sizeof(h), hipMemcpyDeviceToHost);
-        std::printf("run %d: item us per rep:", run);
+        std::printf("run %d (%s chain): item us per rep:", run, (run & 1) ? "LDS" : "blocked");
         for (int r = 0; r < REPS; ++r) std::printf(" %.2f", h[r] / 100.);
         std::printf("\n");
         hipMemcpy(ph, t + 64, sizeof(ph), hipMemcpyDeviceToHost);
