@@ -5,12 +5,15 @@
 // reduced system S has almost no zero tiles and its Cholesky factor is
 // dense.  S is then held as one column-major lower triangle A (n = nRpad
 // columns, ld = n + 64 rows) and factored right-looking in 64-column panels
-// grouped into 256-column blocks:
+// grouped into 512-column blocks:
 //
 //   panel k:  L_kk = chol(A_kk), Linv_kk = L_kk^-1     k_dense_potf64 (one wave)
-//             L_ik = A_ik Linv_kk^T                    rocblas_dgemm (MFMA fp64)
-//             in-block trailing columns                 rocblas_dsyrk / dgemm
-//   block:    A_22 -= L_21 L_21^T (rank 256)            rocblas_dsyrk (MFMA fp64)
+//             L_ik = A_ik Linv_kk^T                    k_dgemm_nt (fp64 MFMA)
+//             in-block trailing columns                 k_dgemm_nt<TRI> / k_dgemm_nt
+//   block:    A_22 -= L_21 L_21^T (rank 512)            k_dgemm_nt<TRI> (fp64 MFMA)
+//
+// k_dgemm_nt is the hand-written fp64 MFMA GEMM/SYRK of mmba_gemm.hip;
+// MMBA_DENSE_HAND=0 runs the same steps through rocBLAS (A/B).
 //
 // The right-hand side rides along as row n of A (A[n, j] = r_j): the panel
 // GEMMs and trailing updates that produce L also produce row n of the
@@ -19,9 +22,11 @@
 // solve for lmpar's Newton term) walk the 64-row blocks with two GEMVs per
 // block (the diagonal block through the stored Linv_kk, then the update of
 // the rest), rocblas_dgemv.  The flops are those of a dense Cholesky, n^3/3,
-// in MFMA library GEMMs; the panel factorisation is the hand-written,
-// latency-bound part.
+// in fp64 MFMA GEMMs; the panel factorisation is the latency-bound part.
 #include <rocblas/rocblas.h>
+
+#include <algorithm>
+#include <cstdlib>
 
 #include "mmba_kernels.h"
 #include "mmba_plan.h"
@@ -49,61 +54,64 @@ __device__ __forceinline__ void dn_wave_sync() {
 }
 
 // In-place Cholesky of the 64 x 64 diagonal block at A (column-major, ld)
-// and its inverse Linv (column-major 64 x 64, lower, ld 64): lane r holds row
-// r in registers, the pivot is broadcast with v_readlane and column j
-// through LDS; the inverse is formed column-oriented (lane = column of the
-// identity).  A non-positive or non-finite pivot sets *fail and is replaced
-// by 1 (the factorisation continues; the LM treats the solve as failed).
-__global__ void __launch_bounds__(64) k_dense_potf64(double *A, int ld, double *Linv,
-                                                     int *fail) {
-    __shared__ double col[64];
-    __shared__ double Ls[64][65];
+// and its inverse Linv (column-major 64 x 64, lower, ld 64), two waves in
+// lockstep: wave 0 holds row r in lane r and runs the pivot chain (pivot by
+// v_readlane, column j published through LDS), wave 1 holds column cc of the
+// identity in lane cc and forms L^-1 e_cc with the same column as it is
+// published (x_j *= 1 / L_jj, x_i -= L_ij x_j) -- one barrier per step
+// instead of a second 64-step pass over the stored factor.  Double-buffered
+// column: step j + 2 overwrites the buffer of step j only after both waves
+// passed the barrier of step j + 1.  A non-positive or non-finite pivot sets
+// *fail and is replaced by 1 (the factorisation continues; the LM treats the
+// solve as failed).
+__global__ void __launch_bounds__(128) k_dense_potf64(double *A, int ld, double *Linv,
+                                                      int *fail) {
+    __shared__ double col[2][64];
     __shared__ double rsv[64];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double a[64];
+    if (wv == 0) {
 #pragma unroll
-    for (int c = 0; c < 64; ++c) a[c] = c <= lane ? A[(size_t)c * ld + lane] : 0.;
+        for (int c = 0; c < 64; ++c) a[c] = c <= lane ? A[(size_t)c * ld + lane] : 0.;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) a[i] = (i == lane) ? 1. : 0.;
+    }
     int bad = 0;
 #pragma unroll
     for (int j = 0; j < 64; ++j) {
-        double d = dn_rdlane(a[j], j);
-        if (!(d > 0.) || !isfinite(d)) {
-            bad = 1;
-            d = 1.;
+        double l = 0.;
+        if (wv == 0) {
+            double d = dn_rdlane(a[j], j);
+            if (!(d > 0.) || !isfinite(d)) {
+                bad = 1;
+                d = 1.;
+            }
+            const double rs = dn_rsq(d);
+            l = lane > j ? a[j] * rs : 0.;
+            a[j] = lane == j ? d * rs : (lane > j ? l : a[j]);
+            col[j & 1][lane] = l;
+            if (lane == 0) rsv[j] = rs;
         }
-        const double rs = dn_rsq(d);
-        const double l = lane > j ? a[j] * rs : 0.;
-        a[j] = lane == j ? d * rs : (lane > j ? l : a[j]);
-        col[lane] = l;
-        if (lane == 0) rsv[j] = rs;
-        dn_wave_sync();
+        __syncthreads();
+        if (wv == 0) {
 #pragma unroll
-        for (int c = j + 1; c < 64; ++c) a[c] = fma(-l, col[c], a[c]);
-        dn_wave_sync();
-    }
+            for (int c = j + 1; c < 64; ++c) a[c] = fma(-l, col[j & 1][c], a[c]);
+        } else {
+            a[j] *= rsv[j];  // zero above the diagonal stays zero
 #pragma unroll
-    for (int c = 0; c < 64; ++c) {
-        const double v = c <= lane ? a[c] : 0.;
-        Ls[lane][c] = v;
-        if (c <= lane) A[(size_t)c * ld + lane] = v;
-    }
-    dn_wave_sync();
-    // inverse, column cc = lane of the identity: x <- L^-1 e_cc
-    {
-        const int cc = lane;
-        double x[64];
-#pragma unroll
-        for (int i = 0; i < 64; ++i) x[i] = (i == cc) ? 1. : 0.;
-#pragma unroll
-        for (int t = 0; t < 64; ++t) {
-            x[t] *= rsv[t];
-#pragma unroll
-            for (int i = t + 1; i < 64; ++i) x[i] = fma(-Ls[i][t], x[t], x[i]);
+            for (int i = j + 1; i < 64; ++i) a[i] = fma(-col[j & 1][i], a[j], a[i]);
         }
-#pragma unroll
-        for (int i = 0; i < 64; ++i) Linv[(size_t)cc * 64 + i] = x[i];  // column cc
     }
-    if (bad && lane == 0) atomicOr(fail, 1);
+    if (wv == 0) {
+#pragma unroll
+        for (int c = 0; c < 64; ++c)
+            if (c <= lane) A[(size_t)c * ld + lane] = a[c];
+        if (bad && lane == 0) atomicOr(fail, 1);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) Linv[(size_t)lane * 64 + i] = a[i];  // column lane
+    }
 }
 
 // A[n, j] = r[j] (the right-hand side as row n of the factored matrix) and
@@ -138,6 +146,8 @@ void DenseSolver::init(hipStream_t s) {
     }
     MMBA_RB(rocblas_set_stream((rocblas_handle)handle, s));
     MMBA_RB(rocblas_set_pointer_mode((rocblas_handle)handle, rocblas_pointer_mode_host));
+    const char *e = std::getenv("MMBA_DENSE_HAND");
+    hand = !(e && std::atoi(e) == 0);
 }
 
 // Panels of the block of columns [k0, k0 + nb); rows below the diagonal run
@@ -148,26 +158,37 @@ void DenseSolver::block(hipStream_t s, double *A, int ld, int k0, int nb, int en
     for (int p = k0; p < k0 + nb; p += 64) {
         double *App = A + (size_t)p * ld + p;
         double *Li = Linv + (size_t)(p / 64) * 64 * 64;
-        k_dense_potf64<<<1, 64, 0, s>>>(App, ld, Li, fail);
+        k_dense_potf64<<<1, 128, 0, s>>>(App, ld, Li, fail);
         const int m = end - (p + 64);
         if (m <= 0) continue;
         double *Aip = App + 64;
-        // L_ip = A_ip Linv^T, out of place, then back into A
-        MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, 64, 64,
-                              &one, Aip, ld, Li, 64, &zero, ws, m));
-        MMBA_HIP(hipMemcpy2DAsync(Aip, sizeof(double) * ld, ws, sizeof(double) * m,
-                                  sizeof(double) * m, 64, hipMemcpyDeviceToDevice, s));
+        // L_ip = A_ip Linv^T.  k_dgemm_nt works in place (each workgroup
+        // reads its own 128 rows of A_ip in full before it writes them, and
+        // no other workgroup reads them); rocBLAS goes out of place
+        if (hand) {
+            launch_dgemm_nt(s, false, m, 64, 64, Aip, ld, Li, 64, Aip, ld, 1., 0.);
+        } else {
+            MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, 64,
+                                  64, &one, Aip, ld, Li, 64, &zero, ws, m));
+            MMBA_HIP(hipMemcpy2DAsync(Aip, sizeof(double) * ld, ws, sizeof(double) * m,
+                                      sizeof(double) * m, 64, hipMemcpyDeviceToDevice, s));
+        }
         // the rest of this block's columns [p + 64, k0 + nb)
         const int mb = k0 + nb - (p + 64);
         if (mb > 0) {
             double *Aqq = A + (size_t)(p + 64) * ld + (p + 64);
-            MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mb, 64, &mone,
-                                  Aip, ld, &one, Aqq, ld));
             const int mr = end - (k0 + nb);
-            if (mr > 0)
-                MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, mr,
-                                      mb, 64, &mone, Aip + mb, ld, Aip, ld, &one, Aqq + mb,
-                                      ld));
+            if (hand) {
+                launch_dgemm_nt(s, true, mb, mb, 64, Aip, ld, Aip, ld, Aqq, ld, -1., 1.);
+                launch_dgemm_nt(s, false, mr, mb, 64, Aip + mb, ld, Aip, ld, Aqq + mb, ld, -1., 1.);
+            } else {
+                MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mb, 64,
+                                      &mone, Aip, ld, &one, Aqq, ld));
+                if (mr > 0)
+                    MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose,
+                                          mr, mb, 64, &mone, Aip + mb, ld, Aip, ld, &one,
+                                          Aqq + mb, ld));
+            }
         }
     }
 }
@@ -186,7 +207,12 @@ void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int 
     const double one = 1.0, mone = -1.0;
     k_dense_row_put<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, r);
     const int end = n + 1;  // rows 0..n-1 and the right-hand-side row n
-    constexpr int NB = 256;
+    // block width of the trailing updates (MMBA_DENSE_NB, a multiple of 64):
+    // 512 measured 229.6 ms per C3 factorisation with k_dgemm_nt (39.3 TF/s,
+    // 50 % of the fp64 MFMA peak) against 251.6 ms at 256 -- half as many
+    // read-modify-write passes over the trailing matrix
+    int NB = 512;
+    if (const char *e = std::getenv("MMBA_DENSE_NB")) NB = std::max(64, std::atoi(e) / 64 * 64);
     for (int k0 = 0; k0 < n; k0 += NB) {
         const int nb = std::min(NB, n - k0);
         block(s, A, ld, k0, nb, end, fail);
@@ -196,8 +222,11 @@ void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int 
         // updates the unused A[n][n])
         double *L21 = A + (size_t)k0 * ld + k0 + nb;
         double *S22 = A + (size_t)(k0 + nb) * ld + (k0 + nb);
-        MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, nb, &mone, L21,
-                              ld, &one, S22, ld));
+        if (hand)
+            launch_dgemm_nt(s, true, m, m, nb, L21, ld, L21, ld, S22, ld, -1., 1.);
+        else
+            MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, nb, &mone,
+                                  L21, ld, &one, S22, ld));
     }
     k_dense_row_get<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, y);
 }

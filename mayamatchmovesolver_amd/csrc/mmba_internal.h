@@ -218,8 +218,10 @@ struct DevProblem {
     const int *cf_aidx;
     int no_lens;       // no camera has a (3DE classic) lens
     // position of each observation in bundle order (bobs) and the bundle
-    // block records JB[8 * i] = [jx_a, jy_a] (a < 3), f_x, f_y written by
-    // k_jacobian (nullptr unless every solved bundle is fast and nG == 0)
+    // block records JB[8 * obs_bpos[i]] = [jx_a, jy_a] (a < 3), f_x, f_y
+    // written by the Jacobian kernels in bundle order, so k_ne_bnd_jb reads
+    // each bundle's records contiguously (nullptr unless every solved bundle
+    // is fast and nG == 0)
     const int *obs_bpos;
     double *JB;
     // per camera lens parameter lists

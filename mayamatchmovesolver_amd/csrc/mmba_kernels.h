@@ -225,4 +225,9 @@ void launch_fold_ranks(hipStream_t s, const double *t, int nranks, double *out, 
 // Per-frame solve mode, one workgroup per frame (mmba_batch.hip).
 void launch_batch_lm(hipStream_t s, const DevProblem &P, const BatchArgs &B, int nf_max);
 
+// mmba_gemm.hip: C = beta C + alpha A B^T (fp64 MFMA; tri: lower triangle,
+// A == B, M == N); column-major, K a multiple of 16.
+void launch_dgemm_nt(hipStream_t s, bool tri, int M, int N, int Kd, const double *A, int lda,
+                     const double *B, int ldb, double *C, int ldc, double alpha, double beta);
+
 }  // namespace mmba

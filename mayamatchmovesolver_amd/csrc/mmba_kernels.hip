@@ -412,7 +412,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
         // store; k_ne_bnd_jb gathers one record per observation of a bundle
         // instead of 8 SoA rows): [jx_a, jy_a]_a, f_x, f_y
         if (P.JB) {
-            double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)i * 8]);
+            double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)P.obs_bpos[i] * 8]);
             dst[0] = make_double4(jb[0], jb[1], jb[2], jb[3]);
             dst[1] = make_double4(jb[4], jb[5], jb[6], jb[7]);
         }
@@ -561,11 +561,11 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i,
         rsd = r.dist;
     }
     if (p4.w >= 0 && P.JB) {
-        double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)i * 8]);
+        double4 *dst = reinterpret_cast<double4 *>(&P.JB[(size_t)P.obs_bpos[i] * 8]);
         dst[0] = make_double4(jb[0], jb[1], jb[2], jb[3]);
         dst[1] = make_double4(jb[4], jb[5], jb[6], jb[7]);
     }
-    nloc[i] = l;
+    if (nloc) nloc[i] = l;  // constant per plan: stored by the first pass only
     // errorList / errorDistanceList as left by the last FD column: only the
     // observations that column moves change; the others keep their values at
     // x (what d_eu / d_ed already hold from the evaluation that accepted x)
@@ -939,7 +939,7 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
         double A[PBMAX][PBMAX] = {};
         double gb[PBMAX] = {};
         for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-            const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)P.bobs[q] * 8]);
+            const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)q * 8]);
             const double4 u = src[0], v = src[1];
             const double jx[3] = {u.x, u.z, v.x}, jy[3] = {u.y, u.w, v.y};
             const double fx = v.z, fy = v.w;

@@ -187,9 +187,12 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.bnd_base = ncf;
     }
     const bool k2_fused = !central && jac_ne_fusable(P, jac_ncv) && !k2_split;
-    if (k2_fused)
-        launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, d_nloc, d_stale, d_eu,
-                      d_ed, d_Acc, d_g, epi);
+    if (k2_fused) {
+        // the local column counts are a property of the plan: stored once
+        launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, nloc_set ? nullptr : d_nloc,
+                      d_stale, d_eu, d_ed, d_Acc, d_g, epi);
+        nloc_set = true;
+    }
     else
         launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
                         d_stale, d_eu, d_ed, jac_ncv, d_f, CB);

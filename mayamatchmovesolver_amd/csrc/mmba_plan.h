@@ -44,6 +44,7 @@ struct Plan;
 struct DenseSolver {
     void *handle = nullptr;  // rocblas_handle
     int n = 0, ld = 0;       // columns (nRpad), leading dimension (n + 64)
+    bool hand = true;        // k_dgemm_nt (MMBA_DENSE_HAND=0: rocBLAS)
     double *A = nullptr, *Linv = nullptr, *ws = nullptr;
     ~DenseSolver();
     void setup(Plan &pl, int n);
@@ -121,6 +122,7 @@ struct Plan {
     int dld = 0;
     DenseSolver ds;
     long long *d_probe = nullptr;  // MMBA_PROBE=1: band-kernel phase cycles
+    bool nloc_set = false;         // d_nloc stored by a fused Jacobian pass
     // single-workgroup triangular solves for narrow (banded) structures
     bool narrow = false;
     int *d_rows_off = nullptr, *d_cols_off = nullptr;
