@@ -7,7 +7,7 @@
 // columns, ld = n + 64 rows) and factored right-looking in 64-column panels
 // grouped into 512-column blocks:
 //
-//   panel k:  L_kk = chol(A_kk), Linv_kk = L_kk^-1     k_dense_potf64 (one wave)
+//   panel k:  L_kk = chol(A_kk), Linv_kk = L_kk^-1     k_dense_potf64 (two waves)
 //             L_ik = A_ik Linv_kk^T                    k_dgemm_nt (fp64 MFMA)
 //             in-block trailing columns                 k_dgemm_nt<TRI> / k_dgemm_nt
 //   block:    A_22 -= L_21 L_21^T (rank 512)            k_dgemm_nt<TRI> (fp64 MFMA)
