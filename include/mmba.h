@@ -470,6 +470,21 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
  * quantity lmpar's Newton correction uses); parts_used = partitions run. */
 int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const double *S,
                           const double *r, double *x, double *ynorm2, int *parts_used);
+/* Test hook (not part of the solver seam): the in-place all-reduce a sharded
+ * plan issues, on a host buffer (copied to ctx's device, reduced on ctx's
+ * stream through comm, copied back); op 0 = sum, 1 = max.  Collective: every
+ * rank of comm calls it with the same count. */
+int mmba_debug_comm_allreduce(mmba_context *ctx, mmba_comm *comm, double *buf, int count,
+                              int op);
+/* Test hook (not part of the solver seam): the dense reduced solve's fp64
+ * MFMA GEMM / SYRK on host buffers, C = beta C + alpha A B^T (column-major;
+ * A: M x K, lda; B: N x K, ldb; C: M x N, ldc; K a multiple of 16).  tri != 0:
+ * lower triangle only (M == N, B is ignored and A is used for both).
+ * in_place != 0: C = alpha A B^T computed in the array holding A (the
+ * dense solver's panel solve: N == K <= 64, lda == ldc, beta 0). */
+int mmba_debug_dgemm(mmba_context *ctx, int tri, int in_place, int M, int N, int K,
+                     const double *A, int lda, const double *B, int ldb, double *C, int ldc,
+                     double alpha, double beta);
 
 #ifdef __cplusplus
 }

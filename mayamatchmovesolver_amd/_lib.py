@@ -98,6 +98,12 @@ def lib():
         L.mmba_comm_create_local.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.mmba_comm_destroy.restype = None
         L.mmba_comm_destroy.argtypes = [C.c_void_p]
+        L.mmba_debug_dgemm.restype = C.c_int
+        L.mmba_debug_dgemm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       dp, C.c_int, C.c_void_p, C.c_int, dp, C.c_int,
+                                       C.c_double, C.c_double]
+        L.mmba_debug_comm_allreduce.restype = C.c_int
+        L.mmba_debug_comm_allreduce.argtypes = [C.c_void_p, C.c_void_p, dp, C.c_int, C.c_int]
         L.mmba_plan_create_sharded.restype = C.c_int
         L.mmba_plan_create_sharded.argtypes = [C.c_void_p, C.POINTER(abi.MmbaProblem),
                                                C.POINTER(abi.MmbaOptions), C.c_void_p,

@@ -229,4 +229,6 @@ EXPORTED_SYMBOLS = [
     "mmba_solve",
     "mmba_plan_kernel_stats",
     "mmba_debug_band_solve",
+    "mmba_debug_comm_allreduce",
+    "mmba_debug_dgemm",
 ]

@@ -289,6 +289,41 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
     return MMBA_OK;
 }
 
+int mmba_debug_dgemm(mmba_context *ctx, int tri, int in_place, int M, int N, int K,
+                     const double *A, int lda, const double *B, int ldb, double *C, int ldc,
+                     double alpha, double beta) {
+    if (!ctx || !A || !C || M < 0 || N < 0 || K < 0 || lda < M || ldc < M) return MMBA_ERR_INVALID;
+    if (tri && (M != N || in_place)) return MMBA_ERR_INVALID;
+    if (!tri && (!B || ldb < N)) return MMBA_ERR_INVALID;
+    if (in_place && (N != K || N > 64 || lda != ldc || beta != 0.)) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;
+        hipStream_t s = ctx->stream;
+        const size_t na = (size_t)lda * K, nc = (size_t)ldc * N;
+        const size_t nbb = tri ? 0 : (size_t)ldb * K;
+        double *dA = nullptr, *dB = nullptr, *dC = nullptr;
+        MMBA_HIP(hipMalloc(&dA, sizeof(double) * std::max<size_t>(na, 1)));
+        MMBA_HIP(hipMalloc(&dC, sizeof(double) * std::max<size_t>(nc, 1)));
+        if (nbb) MMBA_HIP(hipMalloc(&dB, sizeof(double) * nbb));
+        if (nbb) MMBA_HIP(hipMemcpyAsync(dB, B, sizeof(double) * nbb, hipMemcpyHostToDevice, s));
+        if (in_place) {  // C = alpha A B^T with C and A one device array
+            MMBA_HIP(hipMemcpyAsync(dC, A, sizeof(double) * na, hipMemcpyHostToDevice, s));
+            launch_dgemm_nt(s, false, M, N, K, dC, ldc, dB, ldb, dC, ldc, alpha, 0.);
+        } else {
+            MMBA_HIP(hipMemcpyAsync(dA, A, sizeof(double) * na, hipMemcpyHostToDevice, s));
+            MMBA_HIP(hipMemcpyAsync(dC, C, sizeof(double) * nc, hipMemcpyHostToDevice, s));
+            launch_dgemm_nt(s, tri != 0, M, N, K, dA, lda, tri ? dA : dB, tri ? lda : ldb, dC, ldc,
+                            alpha, beta);
+        }
+        MMBA_HIP(hipMemcpyAsync(C, dC, sizeof(double) * nc, hipMemcpyDeviceToHost, s));
+        MMBA_HIP(hipStreamSynchronize(s));
+        (void)hipFree(dA);
+        (void)hipFree(dC);
+        if (dB) (void)hipFree(dB);
+        return MMBA_OK;
+    });
+}
+
 int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const double *S,
                           const double *r, double *x, double *ynorm2, int *parts_used) {
     if (!ctx || nb < 0 || w < 0 || w > WBAND_MAX || nG < 0 || nG > NGMAX || !S || !r || !x)

@@ -8,6 +8,7 @@
 //              all shards get bitwise identical results.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstring>
 #include <memory>
@@ -154,6 +155,30 @@ int mmba_comm_create_local(int nranks, mmba_comm **out) {
 
 void mmba_comm_destroy(mmba_comm *comm) {
     delete reinterpret_cast<Comm *>(comm);
+}
+
+int mmba_debug_comm_allreduce(mmba_context *ctx, mmba_comm *comm, double *buf, int count,
+                              int op) {
+    if (!ctx || !comm || !buf || count < 0 || op < 0 || op > 1) return MMBA_ERR_INVALID;
+    if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;
+    double *d = nullptr;
+    int rc = MMBA_OK;
+    try {
+        MMBA_HIP(hipMalloc(&d, sizeof(double) * (size_t)std::max(count, 1)));
+        MMBA_HIP(hipMemcpyAsync(d, buf, sizeof(double) * (size_t)count, hipMemcpyHostToDevice,
+                                ctx->stream));
+        reinterpret_cast<Comm *>(comm)->allreduce(d, (size_t)count,
+                                                  op ? ReduceOp::Max : ReduceOp::Sum, ctx->stream);
+        MMBA_HIP(hipMemcpyAsync(buf, d, sizeof(double) * (size_t)count, hipMemcpyDeviceToHost,
+                                ctx->stream));
+        MMBA_HIP(hipStreamSynchronize(ctx->stream));
+    } catch (const CommError &) {
+        rc = MMBA_ERR_COMM;
+    } catch (const DeviceError &) {
+        rc = MMBA_ERR_DEVICE;
+    }
+    if (d) (void)hipFree(d);
+    return rc;
 }
 
 }  // extern "C"

@@ -123,10 +123,39 @@ class Comm:
     def handle(self):
         return self._h
 
+    def debug_allreduce(self, ctx: "Context", values, op: str = "sum") -> np.ndarray:
+        """The plan's in-place all-reduce on a copy of ``values`` (test hook,
+        ``mmba_debug_comm_allreduce``); collective over the communicator."""
+        buf = np.ascontiguousarray(values, dtype=np.float64).copy()
+        check(lib().mmba_debug_comm_allreduce(ctx.handle, self._h, _dp(buf), int(buf.size),
+                                              1 if op == "max" else 0))
+        return buf
+
     def close(self):
         if self._h:
             lib().mmba_comm_destroy(self._h)
             self._h = C.c_void_p()
+
+
+def debug_dgemm(ctx: "Context", A, B, Cm, alpha=1.0, beta=0.0, tri=False, in_place=False):
+    """The dense solver's fp64 MFMA GEMM / SYRK (test hook, ``mmba_debug_dgemm``):
+    returns beta Cm + alpha A B^T (``tri``: lower triangle of a SYRK with B = A,
+    entries above the diagonal keep Cm's; ``in_place``: the panel-solve form,
+    computed in A's array, beta 0)."""
+    A = np.asfortranarray(A, dtype=np.float64)
+    out = np.array(Cm, dtype=np.float64, order="F", copy=True)
+    M, K = A.shape
+    N = out.shape[1]
+    bp, ldb = None, 0
+    if B is not None:
+        B = np.asfortranarray(B, dtype=np.float64)
+        bp, ldb = B.ctypes.data_as(C.c_void_p), B.shape[0]
+    flat = out.ravel(order="K")  # a view: the hook writes the result into `out`
+    af = A.ravel(order="F")
+    check(lib().mmba_debug_dgemm(ctx.handle, int(bool(tri)), int(bool(in_place)), M, N, K,
+                                 _dp(af), M, bp, ldb, _dp(flat), M, float(alpha),
+                                 float(beta)))
+    return out
 
 
 def comm_unique_id() -> bytes:

@@ -58,3 +58,44 @@ def test_band_solve_matches_numpy(nb, w, nG, P, gpu_ctx):
     assert abs(yn - ynr) <= 1e-10 * abs(ynr)
     if P > 1:
         assert used > 1
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 300, 64), (129, 129, 512), (1000, 1000, 256),
+                                   (257, 130, 64), (1, 1, 16)])
+def test_dgemm_nt_tri_and_general(M, N, K, gpu_ctx):
+    """The dense solver's hand-written fp64 MFMA GEMM / SYRK (k_dgemm_nt) on
+    ragged shapes against numpy: C - A B^T (general) and the lower triangle of
+    C - A A^T (SYRK, upper triangle untouched).  The MFMA sums 4 products per
+    step in fp64: agreement to 1e-13 of sum |a b|."""
+    from mayamatchmovesolver_amd.solver import debug_dgemm
+
+    rng = np.random.default_rng(M * 7 + N + K)
+    A = rng.standard_normal((M, K))
+    B = rng.standard_normal((N, K))
+    C0 = rng.standard_normal((M, N))
+    scale = np.abs(A) @ np.abs(B).T + 1.0
+    got = debug_dgemm(gpu_ctx, A, B, C0, alpha=-1.0, beta=1.0)
+    assert np.all(np.abs(got - (C0 - A @ B.T)) <= 1e-13 * scale)
+    if M == N:
+        S0 = rng.standard_normal((M, M))
+        got = debug_dgemm(gpu_ctx, A, None, S0, alpha=-1.0, beta=1.0, tri=True)
+        ref = S0 - A @ A.T
+        low = np.tril(np.ones((M, M), dtype=bool))
+        sc = np.abs(A) @ np.abs(A).T + 1.0
+        assert np.all(np.abs(got - ref)[low] <= 1e-13 * sc[low])
+        np.testing.assert_array_equal(got[~low], S0[~low])
+
+
+@pytest.mark.parametrize("M", [64, 200, 3001])
+def test_dgemm_nt_in_place_panel(M, gpu_ctx):
+    """The panel solve L_ip = A_ip Linv^T computed in A_ip's own array (the
+    128 x 64 two-wave variant): every workgroup reads its rows in full before
+    it overwrites them."""
+    from mayamatchmovesolver_amd.solver import debug_dgemm
+
+    rng = np.random.default_rng(M)
+    A = rng.standard_normal((M, 64))
+    Li = np.tril(rng.standard_normal((64, 64)))
+    got = debug_dgemm(gpu_ctx, A, Li, np.zeros((M, 64)), alpha=1.0, beta=0.0, in_place=True)
+    scale = np.abs(A) @ np.abs(Li).T + 1.0
+    assert np.all(np.abs(got - A @ Li.T) <= 1e-13 * scale)

@@ -173,3 +173,57 @@ def test_sharded_ba_x_before_the_valley(scene, nshards, gpu_ctx):
     np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-7)
     dx = np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3))
     assert dx <= 1e-6, dx
+
+
+def test_rccl_communicator_one_rank(gpu_ctx):
+    """A real RCCL communicator on the box's GPU (ncclGetUniqueId,
+    ncclCommInitRank, ncclAllReduce in place on the plan's stream -- the calls
+    the multi-GPU bench makes).  RCCL refuses two ranks on one device, so on a
+    one-GPU box the communicator has one rank and the all-reduce is the
+    identity, bit for bit, for both operations."""
+    from mayamatchmovesolver_amd.solver import comm_unique_id
+
+    c = Comm.rccl(gpu_ctx, 0, 1, comm_unique_id())
+    try:
+        v = np.linspace(-3.0, 7.0, 1001) ** 3
+        np.testing.assert_array_equal(c.debug_allreduce(gpu_ctx, v), v)
+        np.testing.assert_array_equal(c.debug_allreduce(gpu_ctx, v, "max"), v)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_local_group_allreduce(n):
+    """The in-process group's all-reduce (sum in rank order, max) on n host
+    threads, each with its own stream: every rank gets the same bits, equal to
+    the rank-ordered numpy sum."""
+    comms = Comm.local_group(n)
+    ctxs = [Context(0) for _ in range(n)]
+    rng = np.random.default_rng(7)
+    vals = [rng.standard_normal(777) for _ in range(n)]
+    outs, errs = [None] * n, [None] * n
+
+    def work(r):
+        try:
+            outs[r] = (comms[r].debug_allreduce(ctxs[r], vals[r]),
+                       comms[r].debug_allreduce(ctxs[r], vals[r], "max"))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs[r] = e
+
+    ths = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(n)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in ths), "group all-reduce hung"
+    for c in comms:
+        c.close()
+    for c in ctxs:
+        c.close()
+    assert errs == [None] * n, errs
+    ref = vals[0].copy()
+    for v in vals[1:]:
+        ref = ref + v
+    for s, m in outs:
+        np.testing.assert_array_equal(s, ref)
+        np.testing.assert_array_equal(m, np.max(np.stack(vals), axis=0))
