@@ -236,14 +236,10 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
     // per-step bookkeeping stays in one register each: lane j keeps 1 / C_jj
     // (stored once after the chain), the pivot checks fold into one flag
     double rsl = 0.;
-    bool anybad = false;
     double d = bcr_rdlane(a[0], 0);
-    bool dbad = !(d > 0.) || !isfinite(d);
-    if (dbad) d = 1.;
-    double rs = bcr_rsq(d);
+    double rs = bcr_rsq(d);  // bad pivots: checked once after the chain (bcr_chol_aug_blk)
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        anybad |= dbad;
         const double l = (lane > j) ? a[j] * rs : 0.;
         a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
         if (lane == j) rsl = rs;
@@ -258,15 +254,14 @@ __device__ __forceinline__ void bcr_chol_aug_wave(double (&a)[K], double *rs_out
             const double lj1 = bcr_rdlane(l, j + 1);
             a[j + 1] = fma(-l, lj1, a[j + 1]);
             d = bcr_rdlane(a[j + 1], j + 1);
-            dbad = !(d > 0.) || !isfinite(d);
-            if (dbad) d = 1.;
             rs = bcr_rsq(d);
         }
 #pragma unroll
         for (int c = j + 2; c < K; ++c) a[c] = fma(-l, cv[c], a[c]);
         wave_lds_sync();
     }
-    if (anybad) bad = 1;
+    const bool anybad = lane < K && !(rsl > 0. && rsl < __builtin_inf());
+    if (__builtin_amdgcn_ballot_w64(anybad) != 0) bad = 1;
     if (rs_out && lane < K) rs_out[lane] = rsl;
 }
 
@@ -294,11 +289,10 @@ __device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out,
             // whole chain (SGPR spills to VGPR lanes)
             int lane = lane0;
             asm volatile("" : "+v"(lane));
-            double d = bcr_rdlane(a[j], j);
-            if (!(d > 0.) || !isfinite(d)) {
-                anybad = true;
-                d = 1.;
-            }
+            // no per-step pivot test: a non-positive or non-finite pivot makes
+            // rs NaN / inf / 0, which the check after the chain catches (the
+            // solve is then flagged failed; a valid pivot takes the same ops)
+            const double d = bcr_rdlane(a[j], j);
             const double rs = bcr_rsq(d);
             const double l = (lane > j) ? a[j] * rs : 0.;
             a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
@@ -325,7 +319,9 @@ __device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out,
             wave_lds_sync();
         }
     }
-    if (anybad) bad = 1;
+    // lane j < K holds 1 / C_jj: every bad pivot leaves it NaN, inf or 0
+    anybad = lane0 < K && !(rsl > 0. && rsl < __builtin_inf());
+    if (__builtin_amdgcn_ballot_w64(anybad) != 0) bad = 1;
     if (rs_out && lane0 < K) rs_out[lane0] = rsl;
 }
 
