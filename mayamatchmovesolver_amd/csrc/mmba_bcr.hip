@@ -51,6 +51,13 @@ __device__ __forceinline__ double bcr_rsq(double d) {
     return y;
 }
 
+// panel width of the blocked pivot chain (compile-time; the item
+// microbenchmark tools/ubench/bcr_item.hip rebuilds with other widths: warm
+// K = 24 item 8.58 us at 6 and at 12, 8.92 us at 8)
+#ifndef MMBA_BCR_PW
+#define MMBA_BCR_PW 6
+#endif
+
 typedef __attribute__((address_space(1))) unsigned int bcr_gu32;
 typedef __attribute__((address_space(1))) unsigned long long bcr_gu64;
 
@@ -425,7 +432,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     __shared__ double sGT[2][K * GS];  // G_o^T -> Y_o
     __shared__ double sR[3][K];        // r_o1 -> y1, r_o2 -> y2, r_e (fused forward solve)
     __shared__ double sRs[2][K];       // 1 / C_jj
-    __shared__ double col[4][64 * 8];  // pivot column (LDS chain) / panel image (blocked chain)
+    __shared__ double col[4][64 * (MMBA_BCR_PW > 8 ? MMBA_BCR_PW : 8)];  // pivot column (LDS chain) / panel image (blocked chain)
     __shared__ double sDe[K * KS], sGe[NGMAX * K];
     __shared__ double sZero[2];
     __shared__ int bad_s;
@@ -554,7 +561,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
         stamp(1);
         if (act) {
             if constexpr (CH == 2)
-                bcr_chol_aug_blk<K, 8>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
+                bcr_chol_aug_blk<K, MMBA_BCR_PW>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
             else
                 bcr_chol_aug_wave<K>(a, half == 0 ? sRs[w] : nullptr, col[wv], bad);
         }
