@@ -771,10 +771,17 @@ __device__ __forceinline__ void bcr_root_wave(const BcrDev &B, int *fail, double
         }
     }
     wave_lds_sync();
-    for (int q = lane; q < N * N; q += 64) {
+    // every load of the fill is issued before the first LDS store (a loop of
+    // load -> store rounds cost one memory round trip per round)
+    constexpr int TR = (N * N + 63) / 64;
+    double tv[TR];
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+        const int q = lane + 64 * t;
         const int i = q / N, c = q % N;
         double v = 0.;
-        if (i < K && c < K) {
+        if (q >= N * N) {
+        } else if (i < K && c < K) {
             v = c <= i ? D0[i * K + c] : 0.;
         } else if (i >= K && i < n0 && c < K) {
             v = B.Gk[(i - K) * K + c];  // block 0 arrow
@@ -784,7 +791,12 @@ __device__ __forceinline__ void bcr_root_wave(const BcrDev &B, int *fail, double
         } else if (i == c) {
             v = 1.;  // padding beyond n0
         }
-        T[i * NS + c] = v;
+        tv[t] = v;
+    }
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+        const int q = lane + 64 * t;
+        if (q < N * N) T[(q / N) * NS + q % N] = tv[t];
     }
     wave_lds_sync();
     int bad = 0;
@@ -1054,8 +1066,15 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
             if (lane < NGMAX) v0[K + lane] = lane < nG ? y[nb + lane] : 0.;
             __syncthreads();
             if (lane < K + nG) {
+                // FT column loads issued together, then the same ascending sum
+                double ft[K + NGMAX];
+#pragma unroll
+                for (int u = 0; u < K + NGMAX; ++u)
+                    ft[u] = (u >= lane && u < K + nG) ? B.FT[u * N + lane] : 0.;
                 double acc = 0.;
-                for (int u = lane; u < K + nG; ++u) acc = fma(B.FT[u * N + lane], v0[u], acc);
+#pragma unroll
+                for (int u = 0; u < K + NGMAX; ++u)
+                    if (u >= lane && u < K + nG) acc = fma(ft[u], v0[u], acc);
                 const int R = lane < K ? lane : nb + lane - K;
                 if (lane >= K || lane < nb) {
                     bcr_put(x, R, acc);
