@@ -1,5 +1,5 @@
 set -o pipefail
-OUT=gpurun_out/r3r
+OUT=gpurun_out/r3s
 mkdir -p $OUT
 timeout -k 10 500 python -u -m pytest tests/test_gpu_bcr_variants.py tests/test_gpu_band.py tests/test_gpu_golden.py tests/test_gpu_sharded.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit 1
