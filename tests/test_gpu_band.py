@@ -99,3 +99,26 @@ def test_dgemm_nt_in_place_panel(M, gpu_ctx):
     got = debug_dgemm(gpu_ctx, A, Li, np.zeros((M, 64)), alpha=1.0, beta=0.0, in_place=True)
     scale = np.abs(A) @ np.abs(Li).T + 1.0
     assert np.all(np.abs(got - A @ Li.T) <= 1e-13 * scale)
+
+
+@pytest.mark.parametrize("nb,w,nG", [(2994, 23, 0), (500, 23, 3), (1000, 15, 0)])
+@pytest.mark.parametrize("where", ["odd_block", "even_block", "root", "arrow", "nan"])
+def test_bcr_indefinite_is_reported(nb, w, nG, where, gpu_ctx):
+    """A non-positive (or NaN) pivot anywhere in the block cyclic reduction --
+    a block eliminated at level 0, a block eliminated at a later level, the
+    root block, the arrow corner -- is reported as a failed factorisation (the
+    LM then raises its damping), never returned as a solution.  The pivot
+    chains test the pivots once after the chain (a bad pivot leaves 1/C_jj
+    NaN, inf or 0)."""
+    from mayamatchmovesolver_amd._lib import MmbaError
+
+    if where == "arrow" and nG == 0:
+        pytest.skip("no arrow rows")
+    S = band_arrow_spd(nb, w, nG, seed=nb + w + nG)
+    K = max(8, (w + 7) // 8 * 8)
+    row = {"odd_block": K + 3, "even_block": 2 * K + 5, "root": 2, "arrow": nb + nG - 1,
+           "nan": 4 * K + 1}[where]
+    S[row, row] = np.nan if where == "nan" else -10.0 * abs(S[row, row])
+    solve = debug_band_solve(gpu_ctx, S, nb, w, nG, parts=-1)
+    with pytest.raises(MmbaError, match="non-positive pivot"):
+        solve(np.ones(nb + nG))
