@@ -326,8 +326,11 @@ def main():
     upload_s = time.perf_counter() - t0
 
     # the caller's output buffers (errorList, ud->errorList,
-    # errorDistanceList) are allocated once and refilled by every solve
-    outs = (np.zeros(prob.num_residuals), np.zeros(prob.num_residuals), np.zeros(prob.num_obs))
+    # errorDistanceList) are allocated once, in page-locked host memory
+    # (mmba_host_alloc), and refilled by every solve
+    from mayamatchmovesolver_amd.solver import host_array
+    outs = (host_array(prob.num_residuals), host_array(prob.num_residuals),
+            host_array(prob.num_obs))
     for _ in range(args.warmup):
         solver.solve(out=outs)
 

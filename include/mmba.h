@@ -307,6 +307,13 @@ int mmba_context_create(int device, mmba_context **out);
 void mmba_context_destroy(mmba_context *ctx);
 /* Wait for all work on the context's device (bench timing brackets). */
 int mmba_context_synchronize(mmba_context *ctx);
+/* Page-locked host memory (hipHostMalloc) for buffers a caller keeps across
+ * solves -- x, fvec, errorList, errorDistanceList: the end-of-solve
+ * device-to-host copies then run at full link rate instead of through the
+ * driver's staging copies of pageable memory.  Optional; any host pointer
+ * works. */
+int mmba_host_alloc(size_t bytes, void **out);
+void mmba_host_free(void *p);
 
 /* Upload a problem into HBM once; the plan can then be solved many times
  * (cached device context for the many small calls the Python standard solver

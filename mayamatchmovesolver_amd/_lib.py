@@ -55,6 +55,10 @@ def lib():
         L.mmba_context_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.mmba_context_synchronize.restype = C.c_int
         L.mmba_context_synchronize.argtypes = [C.c_void_p]
+        L.mmba_host_alloc.restype = C.c_int
+        L.mmba_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+        L.mmba_host_free.restype = None
+        L.mmba_host_free.argtypes = [C.c_void_p]
         L.mmba_context_destroy.restype = None
         L.mmba_context_destroy.argtypes = [C.c_void_p]
         L.mmba_plan_create.restype = C.c_int

@@ -211,6 +211,8 @@ EXPORTED_SYMBOLS = [
     "mmba_context_create",
     "mmba_context_destroy",
     "mmba_context_synchronize",
+    "mmba_host_alloc",
+    "mmba_host_free",
     "mmba_plan_create",
     "mmba_plan_destroy",
     "mmba_comm_unique_id",

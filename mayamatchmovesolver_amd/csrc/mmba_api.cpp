@@ -126,6 +126,22 @@ int mmba_context_create(int device, mmba_context **out) {
     })
 }
 
+int mmba_host_alloc(size_t bytes, void **out) {
+    if (!out) return MMBA_ERR_INVALID;
+    *out = nullptr;
+    if (bytes == 0) return MMBA_OK;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        set_error("hipHostMalloc failed");
+        return MMBA_ERR_DEVICE;
+    }
+    return MMBA_OK;
+}
+
+void mmba_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int mmba_context_synchronize(mmba_context *ctx) {
     if (!ctx) return MMBA_ERR_INVALID;
     if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;

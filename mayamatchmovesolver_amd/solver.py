@@ -158,6 +158,36 @@ def debug_dgemm(ctx: "Context", A, B, Cm, alpha=1.0, beta=0.0, tri=False, in_pla
     return out
 
 
+class _HostBlock:
+    """Owner of one mmba_host_alloc block (freed with the last array view)."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = C.c_void_p()
+        check(lib().mmba_host_alloc(int(nbytes), C.byref(self.ptr)))
+
+    def __del__(self):
+        if self.ptr:
+            lib().mmba_host_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+
+class _Pinned(np.ndarray):
+    """ndarray over page-locked host memory; holds the block (views keep it
+    alive through their base)."""
+
+
+def host_array(n: int) -> np.ndarray:
+    """A float64 array of n entries in page-locked host memory
+    (``mmba_host_alloc``) for buffers kept across solves (``Solver.solve(out=...)``):
+    the end-of-solve device-to-host copies run at full link rate."""
+    n = max(int(n), 1)
+    blk = _HostBlock(8 * n)
+    arr = np.ctypeslib.as_array((C.c_double * n).from_address(blk.ptr.value)).view(_Pinned)
+    arr._blk = blk
+    arr[:] = 0.0
+    return arr
+
+
 def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     check(lib().mmba_comm_unique_id(buf))
