@@ -47,3 +47,27 @@ def test_set_attr_values_equals_fresh_plan(cfg, kw):
     np.testing.assert_array_equal(cached.fnorm_trace, fresh.fnorm_trace)
     np.testing.assert_array_equal(cached.err_dist, fresh.err_dist)
     assert cached.result["error_initial_avg"] == fresh.result["error_initial_avg"]
+
+
+def test_solve_into_page_locked_buffers(gpu_ctx):
+    """Output buffers in page-locked host memory (mmba_host_alloc, as bench.py
+    and a caching caller keep them) receive the same bits as ordinary numpy
+    arrays, solve after solve."""
+    from mayamatchmovesolver_amd import synthetic as S
+    from mayamatchmovesolver_amd.solver import Solver, host_array
+
+    prob = S.make_config(3, frames=12, scale=0.002)
+    opt = S.config_options(prob)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        m, M = prob.num_residuals, prob.num_obs
+        ref = s.solve(out=(np.zeros(m), np.zeros(m), np.zeros(M)))
+        pin = (host_array(m), host_array(m), host_array(M))
+        for _ in range(2):
+            got = s.solve(out=pin)
+            np.testing.assert_array_equal(got.x, ref.x)
+            np.testing.assert_array_equal(pin[0], ref.fvec)
+            np.testing.assert_array_equal(pin[1], ref.err_user)
+            np.testing.assert_array_equal(pin[2], ref.err_dist)
+    finally:
+        s.close()
