@@ -20,17 +20,29 @@ MMBA_DEV bool own_cf(const DevProblem &P, int cf) { return !P.cf_own || P.cf_own
 MMBA_DEV bool own_bnd(const DevProblem &P, int b) { return !P.bnd_own || P.bnd_own[b]; }
 MMBA_DEV bool own_mask(const int *m, int i) { return !m || m[i]; }
 
+// Workgroup b of a G-workgroup grid runs on XCD b mod 8; xcd_remap(b, G) is
+// the logical block it takes so that each XCD sweeps one contiguous range of
+// logical blocks (a bijection of [0, G)).  Kernels that walk the
+// camera-frame-sorted observations, the records they read and the Jacobian
+// they write use it alike, so a producer's lines sit in the L2 of the XCD
+// that reads them next.
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+    const int x = b & 7, idx = b >> 3, q = G >> 3, r = G & 7;
+    return x * q + min(x, r) + idx;
+}
+
 // Deterministic single-launch reduction epilogue (see the reductions section).
 template <bool MAX>
 __device__ __forceinline__ void finish_blocks(double v, double *partial, double *out,
-                                              unsigned int *ticket) {
+                                              unsigned int *ticket, int blk = -1) {
+    if (blk < 0) blk = blockIdx.x;
     __shared__ int last;
     __shared__ double red[256];
     if (threadIdx.x == 0) {
         if (!ticket) {
-            partial[blockIdx.x] = v;
+            partial[blk] = v;
         } else {
-            __hip_atomic_store(&partial[blockIdx.x], v, __ATOMIC_RELAXED,
+            __hip_atomic_store(&partial[blk], v, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             __threadfence();  // release the partial before the ticket
             last = atomicAdd(ticket, 1u) == gridDim.x - 1;
@@ -205,12 +217,15 @@ __global__ void __launch_bounds__(64) k_records(DevProblem P, const int *__restr
                                                 const double *__restrict__ ext_pert,
                                                 const double *__restrict__ step, double *recs,
                                                 int nvar, double *brec, int base_only, int ncb) {
+    // ncb is a multiple of 8 (launch_records), so both ranges start on XCD 0
+    // and each maps XCD-contiguously (the K2 and residual passes read these
+    // records on the XCD that owns the same camera-frames / bundles)
     if ((int)blockIdx.x < ncb)
-        cam_record_thread(P, blockIdx.x * 64 + threadIdx.x, var_cf, ext_pert, recs, nvar,
-                          base_only);
+        cam_record_thread(P, xcd_remap(blockIdx.x, ncb) * 64 + threadIdx.x, var_cf, ext_pert,
+                          recs, nvar, base_only);
     else
-        bnd_record_thread(P, (blockIdx.x - ncb) * 64 + threadIdx.x, ext_pert, step, brec,
-                          base_only);
+        bnd_record_thread(P, xcd_remap(blockIdx.x - ncb, gridDim.x - ncb) * 64 + threadIdx.x,
+                          ext_pert, step, brec, base_only);
 }
 
 // -------------------------------------------------------------------------
@@ -233,7 +248,8 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
                                                   const double *__restrict__ pstep,
                                                   double *partial_jp, double *dist) {
     __shared__ double red[256];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);  // logical block (XCD-contiguous)
+    const int i = lb * blockDim.x + threadIdx.x;
     double s = 0., sj = 0.;
     if (i < P.M) {
         const int cf = P.obs_cf[i];
@@ -303,7 +319,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
             if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
             __syncthreads();
         }
-        if (threadIdx.x == 0) partial_jp[blockIdx.x] = red[0];
+        if (threadIdx.x == 0) partial_jp[lb] = red[0];
         __syncthreads();
     }
     red[threadIdx.x] = s;
@@ -312,7 +328,7 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    finish_blocks<false>(red[0], partial, out, ticket);
+    finish_blocks<false>(red[0], partial, out, ticket, lb);
 }
 
 // -------------------------------------------------------------------------
@@ -839,10 +855,6 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
 // XCDs round-robin, so workgroup b runs on XCD b % 8; giving each XCD a
 // contiguous range of camera-frames keeps consecutive frames (which share
 // bundles) on one L2 and the bundle records they gather are fetched once.
-__device__ __forceinline__ int xcd_remap(int b, int G) {
-    const int x = b & 7, idx = b >> 3, q = G >> 3, r = G & 7;
-    return x * q + min(x, r) + idx;
-}
 
 // Fused K2 for uniform fast plans without global parameters: one workgroup
 // per camera-frame segment computes the FD Jacobian of its observations
@@ -931,7 +943,7 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
 __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, double *g,
                                                    NeEpi E) {
     __shared__ double red[3][256];
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     const int4 p4 = b < P.nB ? P.bnd_p4[b] : make_int4(-1, -1, -1, 0);
     const int pb = p4.w;
     double zf = 0., xn = 0., gm = 0.;
@@ -985,7 +997,9 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) epi_store(E, E.bnd_base + blockIdx.x, red[0][0], red[1][0], red[2][0]);
+    if (threadIdx.x == 0)
+        epi_store(E, E.bnd_base + xcd_remap(blockIdx.x, gridDim.x), red[0][0], red[1][0],
+                  red[2][0]);
 }
 
 // Per bundle: Abb (pb x pb), gB, Abg (pb x nG).  One thread per bundle.
@@ -1304,7 +1318,7 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
                                 const double *__restrict__ Abg, const double *__restrict__ g,
                                 const double *__restrict__ diag, double lam, double *Lb,
                                 double *tb, double *Wg, int *fail) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
     if (pb == 0) return;
@@ -1385,7 +1399,7 @@ __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__
                                                   const double *__restrict__ Lb, double *W) {
     extern __shared__ double sw[];  // 64 x wst doubles (9 KB for pose-only BA)
     const int lane = threadIdx.x;
-    const int i0 = blockIdx.x * 64;
+    const int i0 = xcd_remap(blockIdx.x, gridDim.x) * 64;  // J rows from this XCD's L2
     const int i = i0 + lane;
     const int M = P.M, wst = P.wst;
     double *row = &sw[lane * wst];
@@ -1829,7 +1843,7 @@ __global__ void __launch_bounds__(64) k_obs_wtx(DevProblem P, const double *__re
                                                 const double *__restrict__ xR, double *U) {
     extern __shared__ double sw[];  // 64 x wst doubles
     const int lane = threadIdx.x;
-    const int i0 = blockIdx.x * 64;
+    const int i0 = xcd_remap(blockIdx.x, gridDim.x) * 64;  // W rows from this XCD's L2
     const int i = i0 + lane;
     const int M = P.M, wst = P.wst;
     const int nrow = min(64, M - i0);
@@ -1863,7 +1877,7 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
                                  const double *__restrict__ Wg, const double *__restrict__ tb,
                                  const double *__restrict__ Lb, const double *__restrict__ xR,
                                  double *x) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     if (b >= P.nB) return;
     const int pb = P.bnd_pb[b];
     if (pb == 0) return;
@@ -2214,7 +2228,7 @@ void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, doub
 void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
                     const double *ext_pert, const double *step, double *recs, int nvar,
                     double *brec, int base_only) {
-    const int ncb = nblk(base_only ? P.ncf : nvar, 64);
+    const int ncb = (nblk(base_only ? P.ncf : nvar, 64) + 7) / 8 * 8;  // see k_records
     const int nbb = nblk(P.nB, 64);
     static const bool split = [] {
         const char *e = std::getenv("MMBA_REC_SPLIT");
