@@ -604,7 +604,7 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
     int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
     const int *__restrict__ stale_param, double *__restrict__ eu, double *__restrict__ ed) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     if (i >= P.M) return;
     double cx[NCV], cy[NCV], fx, fy;
     jac_obs_u<NCV, GEN>(P, i, recs, step, solver_type == MMBA_SOLVER_CMINPACK_LMDER, J, jcol,
@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
     // follow the camera block in each observation (found through jcol).
     constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC, NT = NE + PC * NG;
     __shared__ double wsum[NW][NT];
-    const int cf = blockIdx.x;
+    const int cf = xcd_remap(blockIdx.x, gridDim.x);  // the XCD that wrote its J rows
     if (!own_cf(P, cf) || P.cf_pc[cf] != PC) {
         if (E.on && threadIdx.x == 0) epi_store(E, E.cf_base + cf, 0., 0., 0.);
         return;
