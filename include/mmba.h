@@ -27,6 +27,7 @@
 #ifndef MMBA_H
 #define MMBA_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
