@@ -59,7 +59,7 @@ def parse():
                     help="per-frame solve mode (mmba_solve_per_frame) with CONC frames at "
                          "once; prints its own JSON line (not the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=60.0,
+    ap.add_argument("--cpu-budget-s", type=float, default=30.0,
                     help="skip the larger CPU window once this much CPU time is spent")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC passes that fill roofline.traffic")
@@ -160,7 +160,16 @@ def pmc_traffic(args):
 # Full-density frame windows of the workload timed on the CPU: the same
 # scene generator with the window's share of bundles (C4: 100 new bundles per
 # frame, each tracked over 4 frames), i.e. the full C4 density on F' frames.
-CPU_WINDOWS = {3: (4, 5), 2: (2, 3), 1: (2, 3), 4: (2, 3), 0: (10,)}
+CPU_WINDOWS = {3: (5, 10), 2: (2, 3), 1: (2, 3), 4: (2, 3), 0: (10,)}
+
+
+def _pinned_core():
+    """One core of this process's CPU set (the reference solve is single
+    threaded: `taskset -c <core>` for the oracle's timed calls)."""
+    try:
+        return min(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
 
 
 def _window(cfg_index, frames):
@@ -189,14 +198,25 @@ def cpu_baseline(cfg_index, budget_s, ctx):
     del full
     samples = []
     spent = 0.0
+    core = _pinned_core()
     for frames in CPU_WINDOWS.get(cfg_index, (2,)):
         if samples and spent > budget_s:
             break
         p = _window(cfg_index, frames)
         o = S.config_options(p, iterations=2)
-        t0 = time.perf_counter()
-        _x, _f, _eu, _ed, res, _tr = R.solve(p, o)
-        dt = time.perf_counter() - t0
+        R.lib()  # loaded outside the timing
+        # the oracle call runs pinned to one core (taskset -c <core>): the
+        # reference solve is single threaded on Maya's main thread
+        prev = os.sched_getaffinity(0) if core is not None else None
+        if core is not None:
+            os.sched_setaffinity(0, {core})
+        try:
+            t0 = time.perf_counter()
+            _x, _f, _eu, _ed, res, _tr = R.solve(p, o)
+            dt = time.perf_counter() - t0
+        finally:
+            if prev is not None:
+                os.sched_setaffinity(0, prev)
         spent += dt
         it = max(1, res.outer_iterations)
         # the GPU on the same window and call (plan built outside the timing)
@@ -224,12 +244,13 @@ def cpu_baseline(cfg_index, budget_s, ctx):
     # largest window by the dense-QR cost ratio m n^2 (not a measurement)
     t_full = (big["cpu_s"] / big["cpu_lm_iterations"]) * (
         (m_full * float(n_full) ** 2) / (big["residuals"] * float(big["params"]) ** 2))
-    desc = ("oracle/refcpu.c single thread, one LM iteration (lmder iterMax 2) on full-density "
+    desc = ("oracle/refcpu.c single thread pinned to core %s (taskset), one LM iteration "
+            "(lmder iterMax 2) on full-density "
             "frame windows of the same scene: %s; the GPU timed on the same windows and calls "
-            "(median of 5) in this process" % "; ".join(
+            "(median of 5) in this process" % (core, "; ".join(
                 "F'=%d n=%d m=%d: CPU %.2f s, GPU %.2f ms" % (
                     q["frames"], q["params"], q["residuals"], q["cpu_s"], 1e3 * q["gpu_s"])
-                for q in samples))
+                for q in samples)))
     return {"value": big["cpu_lm_iterations_per_s"], "unit": "LM iterations/s", "cores": 1,
             "kind": "port", "sample": desc, "windows": samples,
             "speedup_measured_same_window": big["speedup_measured"],
@@ -439,11 +460,6 @@ def main():
             "time_split_s": {"func": r["time_func_s"], "jac": r["time_jac_s"],
                              "linear": r["time_linear_s"], "solve": r["time_solve_s"]},
         }
-        if cpu and cpu.get("value"):
-            # the measured ratio is on the same window (cpu_baseline.windows);
-            # this one divides the full-scene GPU rate by the CPU rate on the
-            # largest window it could run
-            line["speedup_lm_rate_vs_cpu_window"] = lm_rate / cpu["value"]
         print(json.dumps(line), flush=True)
     solver.close()
     if comm is not None:

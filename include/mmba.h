@@ -388,8 +388,9 @@ int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac);
 
 /* Run the LM solve from internal parameters x_inout: the
  * solve_3d_cminpack_lmder / _lmdif call inside solveFrames, bracketed by the
- * initial error measurement (adjust_base.cpp:1080-1103, unless
- * opt->initial_measure == 0) and the accept-only-better test (:1208-1229).
+ * initial error measurement (adjust_base.cpp:1080-1103; it runs unless
+ * opt->initial_error_given != 0 or opt->accept_only_better == 0) and the
+ * accept-only-better test (:1208-1229).
  *   x_inout      [num_params]      in: x0; out: the solved x, as lmder leaves
  *                                  paramList.  res->error_is_better says
  *                                  whether the caller should write it back
@@ -465,6 +466,9 @@ typedef struct mmba_kernel_stats {
                                1 tiled sparse Cholesky, 2 dense blocked
                                Cholesky,
                                3 block diagonal + arrow (no solved bundle) */
+    int32_t dataflow_fallback; /* 1 once a timed-out dataflow wait in the block
+                               cyclic reduction switched this plan to the
+                               per-level launches (ABI 3)                  */
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);

@@ -193,6 +193,7 @@ class MmbaKernelStats(C.Structure):
         ("chol_launches", C.c_int32),
         ("reduced_dim", C.c_int32),
         ("reduced_kind", C.c_int32),
+        ("dataflow_fallback", C.c_int32),
     ]
 
     def as_dict(self):

@@ -265,6 +265,7 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         out->chol_ms_avg = p.chol_n ? p.chol_ms / p.chol_n : 0.;
         out->reduced_dim = p.nR;
         out->reduced_kind = p.band ? (p.bs.use_bd ? 3 : 0) : (p.dense ? 2 : 1);
+        out->dataflow_fallback = p.bs.df_off ? 1 : 0;
         // Algorithmic bytes: B_J = 48 + 8 p_c p_b per observation
         // for the Jacobian + normal-equation pass, B_f = 48 per observation for
         // the residual pass.
@@ -318,6 +319,13 @@ int mmba_debug_dgemm(mmba_context *ctx, int tri, int in_place, int M, int N, int
         const size_t na = (size_t)lda * K, nc = (size_t)ldc * N;
         const size_t nbb = tri ? 0 : (size_t)ldb * K;
         double *dA = nullptr, *dB = nullptr, *dC = nullptr;
+        struct Free {  // every exit (an MMBA_HIP early return included) frees
+            double **p[3];
+            ~Free() {
+                for (double **q : p)
+                    if (*q) (void)hipFree(*q);
+            }
+        } guard{{&dA, &dB, &dC}};
         MMBA_HIP(hipMalloc(&dA, sizeof(double) * std::max<size_t>(na, 1)));
         MMBA_HIP(hipMalloc(&dC, sizeof(double) * std::max<size_t>(nc, 1)));
         if (nbb) MMBA_HIP(hipMalloc(&dB, sizeof(double) * nbb));
@@ -333,9 +341,6 @@ int mmba_debug_dgemm(mmba_context *ctx, int tri, int in_place, int M, int N, int
         }
         MMBA_HIP(hipMemcpyAsync(C, dC, sizeof(double) * nc, hipMemcpyDeviceToHost, s));
         MMBA_HIP(hipStreamSynchronize(s));
-        (void)hipFree(dA);
-        (void)hipFree(dC);
-        if (dB) (void)hipFree(dB);
         return MMBA_OK;
     });
 }

@@ -1052,14 +1052,29 @@ __device__ __forceinline__ bool bcr_wait(const int *flags, int a, int b, unsigne
     return true;
 }
 
+// Item tickets (both dataflow launches): every workgroup draws its first item
+// from the launch's counter, and the next one as it starts an item, so
+// tickets are handed out in dependency order and every item waited on has
+// been drawn by a running workgroup -- forward progress holds with any number
+// of resident workgroups (other streams on the device, fewer CUs).  A
+// workgroup draws 1 + (items it runs) tickets, so one launch draws exactly
+// G + items: the host advances tbase by that (counters wrap modulo 2^32).
+__device__ __forceinline__ unsigned bcr_ticket(unsigned *ctr) {
+    return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int K>
 __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, double *x,
-                                                    unsigned epoch, int *fail) {
+                                                    unsigned epoch, int *fail, unsigned tbase) {
     __shared__ double xg[NGMAX], xp[K], xn[K], v0[K + NGMAX];
     const int lane = threadIdx.x;
     const int nb = B.nb, nG = B.nG, nblk = B.nblk;
-    for (int k = blockIdx.x; k < nblk; k += gridDim.x) {
+    int k = (int)(__builtin_amdgcn_readfirstlane(lane == 0 ? bcr_ticket(B.tick + 1) : 0u) - tbase);
+    for (; k < nblk;) {
         const int o = B.ord[k];
+        // the next item's ticket, drawn as this one starts (one lane; the
+        // value is wave-uniform after readfirstlane)
+        unsigned nxt = lane == 0 ? bcr_ticket(B.tick + 1) : 0u;
         if (o == 0) {  // root: x_T = FT^T y_T (k_bcr_bwd_root)
             const int N = B.NR;
             if (lane < K) v0[lane] = bcr_get(y, lane, nb);
@@ -1083,6 +1098,7 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
             }
             bcr_publish(B.flags, 0, epoch, lane);
             __syncthreads();
+            k = (int)(__builtin_amdgcn_readfirstlane(nxt) - tbase);
             continue;
         }
         const int s = 1 << __builtin_ctz(o);
@@ -1109,6 +1125,7 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
         if (ok && nG > 0 && o - s != 0) ok = bcr_wait(B.flags, 0, -1, epoch);
         if (!ok) {
             if (lane == 0) atomicOr(fail, 2);
+            k = (int)(__builtin_amdgcn_readfirstlane(nxt) - tbase);
             continue;
         }
         if (lane < K) {
@@ -1140,6 +1157,7 @@ __global__ void __launch_bounds__(64) k_bcr_bwd_all(BcrDev B, const double *y, d
         }
         bcr_publish(B.flags, o, epoch, lane);
         __syncthreads();
+        k = (int)(__builtin_amdgcn_readfirstlane(nxt) - tbase);
     }
 }
 
@@ -1187,13 +1205,15 @@ __device__ __forceinline__ bool bcr_wait_items(const int *flags, int lo, int hi,
 template <int K, int N>
 __global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, const double *r,
                                                        double *y, unsigned epoch,
-                                                       long long *trace) {
+                                                       long long *trace, unsigned tbase) {
     // trace (diagnostic, MMBA_PROBE=1): per item the 100 MHz wall clock at
     // entry, after the wait, after the item, after the flag store
-    __shared__ int ok_s;
+    __shared__ int ok_s, it_s;
     const int tid = threadIdx.x;
     int base = 0, pbase = 0, pg = 0, s = 1, nact = B.nblk, lvl = 0;
-    for (int it = blockIdx.x;; it += gridDim.x) {
+    if (tid == 0) it_s = (int)(bcr_ticket(B.tick) - tbase);  // items in ticket order
+    __syncthreads();
+    for (int it = it_s;;) {
         while (nact > 1 && it >= base + (nact + 1) / 2) {
             pbase = base;
             pg = (nact + 1) / 2;
@@ -1217,6 +1237,8 @@ __global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, cons
             return;
         }
         const int k = it - base;
+        unsigned nxt = 0;  // the next item's ticket, drawn as this one starts
+        if (tid == 0) nxt = bcr_ticket(B.tick);
         if (trace && tid == 0) trace[4 * it] = (long long)wall_clock64();
         __syncthreads();  // the previous item's LDS reads are done
         if (lvl > 0) {
@@ -1227,7 +1249,12 @@ __global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, cons
             }
             __syncthreads();
             if (!ok_s) {
-                if (tid == 0) atomicOr(fail, 2);
+                if (tid == 0) {
+                    atomicOr(fail, 2);
+                    it_s = (int)(nxt - tbase);
+                }
+                __syncthreads();
+                it = it_s;
                 continue;  // no flag: the items that need this one time out too
             }
         }
@@ -1241,11 +1268,15 @@ __global__ void __launch_bounds__(256) k_bcr_factor_df(BcrDev B, int *fail, cons
             __hip_atomic_store((bcr_gu32 *)(B.fflags + it), epoch, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             if (trace) trace[4 * it + 3] = (long long)wall_clock64();
+            it_s = (int)(nxt - tbase);
         }
+        __syncthreads();
+        it = it_s;
     }
 }
 
 static std::atomic<unsigned> g_bcr_epoch{0};
+
 
 static unsigned bcr_next_epoch() {
     unsigned ep = ++g_bcr_epoch;
@@ -1263,14 +1294,22 @@ static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long lon
                          const double *r, double *y) {
     const BcrDev &D = B.bcr;
     double *yy = r ? y : nullptr;
-    if (D.fflags && D.nblk >= 2 && D.regchol == 2 && D.mfma_upd) {
+    if (D.fflags && D.tick && !B.df_off && D.nblk >= 2 && D.regchol == 2 && D.mfma_upd) {
         const unsigned ep = bcr_next_epoch();
-        const int G = std::min((D.nblk + 1) / 2, 256);
+        // level items (the root is item `items`); G workgroups need not all
+        // be resident (tickets), so the grid is the level-0 width (<= 256)
+        int items = 0;
+        for (int nact = D.nblk; nact > 1; nact = (nact + 1) / 2) items += (nact + 1) / 2;
+        const int G = std::min((D.nblk + 1) / 2, B.df_grid);
+        const unsigned tb = B.tick_f;
+        B.tick_f += (unsigned)(G + items);
         long long *tr = probe ? probe + 8 : nullptr;
         switch (D.NR - K) {
-            case 0: k_bcr_factor_df<K, K><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
-            case 8: k_bcr_factor_df<K, K + 8><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
-            default: k_bcr_factor_df<K, K + 16><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr); break;
+            case 0: k_bcr_factor_df<K, K><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr, tb); break;
+            case 8: k_bcr_factor_df<K, K + 8><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr, tb); break;
+            default:
+                k_bcr_factor_df<K, K + 16><<<G, 256, 0, s>>>(D, fail, r, yy, ep, tr, tb);
+                break;
         }
         return;
     }
@@ -1314,9 +1353,12 @@ static void bcr_forward_k(hipStream_t s, const BandSolver &B, const double *r, d
 template <int K>
 static void bcr_backward_k(hipStream_t s, const BandSolver &B, const double *y, double *x) {
     const BcrDev &D = B.bcr;
-    if (D.flags && D.fail) {  // one dataflow launch
+    if (D.flags && D.fail && D.tick && !B.df_off) {  // one dataflow launch
         const unsigned ep = bcr_next_epoch();
-        k_bcr_bwd_all<K><<<std::min(D.nblk, 256), 64, 0, s>>>(D, y, x, ep, D.fail);
+        const int G = std::min(D.nblk, B.df_grid);
+        const unsigned tb = B.tick_b;
+        B.tick_b += (unsigned)(G + D.nblk);
+        k_bcr_bwd_all<K><<<G, 64, 0, s>>>(D, y, x, ep, D.fail, tb);
         return;
     }
     k_bcr_bwd_root<K><<<1, 64, 0, s>>>(D, y, x);

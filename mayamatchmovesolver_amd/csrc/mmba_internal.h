@@ -82,6 +82,11 @@ struct BcrDev {
     // the root (nullptr: per-level launches, MMBA_BCR_DF=0)
     int *fflags = nullptr;
     int *fail = nullptr;
+    // item tickets of the two dataflow launches ([0] factorisation, [1]
+    // backward solve): a workgroup takes its next item from the counter, so
+    // items are started in dependency order whatever the residency (forward
+    // progress does not assume every workgroup is resident)
+    unsigned *tick = nullptr;
     // with xs: the backward solve also scatters x_R to parameter order
     // (xs[row_param[R]] = x_R, k_scatter_xR's job)
     const int *row_param = nullptr;
@@ -134,6 +139,14 @@ struct BandSolver {
     BdDev bd;
     bool use_bcr = false;                    // w <= 32: block cyclic reduction
     BcrDev bcr;
+    // host copies of the ticket counters (every launch draws a known count)
+    // and the switch to the per-level launches after a timed-out dataflow wait
+    mutable unsigned tick_f = 0, tick_b = 0;
+    mutable bool df_off = false;
+    // dataflow grid cap (MMBA_BCR_DF_GRID at plan build: a small grid makes
+    // most items run on workgroups that already ran others -- the
+    // forward-progress test)
+    int df_grid = 256;
     // sharded BCR: Bd | Ga | Gd | rhs contiguous; every shard writes its own
     // Schur terms, one all-reduce (sum) assembles S, every shard factors it
     double *red = nullptr, *red_rhs = nullptr;

@@ -2283,6 +2283,10 @@ void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
 int residual_blocks(const DevProblem &P) { return nblk(P.M, 256) + (P.nrows > 0 ? 1 : 0); }
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out, unsigned int *ticket, double *dist) {
+    // the ticket epilogue sums the residual kernel's own nblk(M) partials
+    // only: with stiffness / smoothness rows (one more partial, k_rows_eval)
+    // the two-launch reduction runs
+    if (ticket && residual_blocks(P) != nblk(P.M, 256)) ticket = nullptr;
     if (P.all_bnd_fast && P.no_lens)
         k_residual<false, true><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,

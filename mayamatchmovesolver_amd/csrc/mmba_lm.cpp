@@ -460,13 +460,22 @@ static void lmpar_first_enqueue(Plan &pl, bool defer = false, bool by_trial = fa
     pl.solve_damped_enqueue(0.0, Plan::SL_DNORM, defer, by_trial);
 }
 
-static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *undamped) {
+// A timed-out dataflow wait in the undamped solve (flag bit 2) switches the
+// plan to the per-level launches and solves again; `pre` is cleared then, so
+// the caller does not take the speculative trial built on the failed solve.
+static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *undamped) {
     const double p1 = .1, p001 = .001;
     const double dwarf = DBL_MIN;
     double *h = pl.h_scalar;
     int iter = 0;
     *undamped = false;
     if (!pre) {
+        lmpar_first_enqueue(pl);
+        pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+    }
+    if (h[Plan::SL_FAIL] >= 2. && !pl.bs.df_off) {
+        pl.bs.df_off = true;
+        pre = false;
         lmpar_first_enqueue(pl);
         pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
     }
@@ -506,6 +515,14 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool pre, bool *unda
         // step.  Raise par (a larger damping is better conditioned) a few
         // times, then give up with an error.
         for (int retry = 0; h[Plan::SL_FAIL] != 0.; ++retry) {
+            if (h[Plan::SL_FAIL] >= 2. && !pl.bs.df_off) {
+                // a timed-out dataflow wait (bit 2): the plan switches to the
+                // per-level launches for good and this damped solve runs again
+                pl.bs.df_off = true;
+                pl.solve_damped_enqueue(*par, Plan::SL_DNORM);
+                pl.read_slots(Plan::SL_DNORM, Plan::SL_FAIL);
+                continue;
+            }
             if (h[Plan::SL_FAIL] >= 2. || retry == 8) {
                 set_error("damped normal-equation factorisation failed (par " +
                           std::to_string(*par) + ", flag " + std::to_string(h[Plan::SL_FAIL]) +

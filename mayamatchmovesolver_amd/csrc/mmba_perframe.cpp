@@ -261,7 +261,7 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
         // Maya main-thread contract): it is polled here before each frame is
         // handed out, and a set interrupt reaches the frames' own solves
         // through a flag.
-        std::atomic<int> next{0}, first_err{MMBA_OK}, err_frame{F};
+        std::atomic<int> next{0}, first_err{MMBA_OK}, err_frame{F}, active{workers};
         std::atomic<bool> stop_flag{false};
         std::mutex mu;
         std::string err_msg;
@@ -276,6 +276,10 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
         };
         wcb.user = &sticky;
         auto work = [&]() {
+            struct Done {  // every exit of the worker counts it out
+                std::atomic<int> *a;
+                ~Done() { a->fetch_sub(1); }
+            } done_{&active};
             mmba_context *c = nullptr;
             int rc = mmba_context_create(ctx->device, &c);
             if (rc != MMBA_OK) {
@@ -314,8 +318,10 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
         std::vector<std::thread> pool;
         for (int w = 0; w < workers; ++w) pool.emplace_back(work);
         if (cb && cb->interrupt) {
-            // poll from the calling thread while the workers run
-            while (next.load() < nf && first_err.load() == MMBA_OK && !stop_flag.load()) {
+            // poll from the calling thread until every worker has finished
+            // (frames still running see an interrupt requested after the last
+            // frame was handed out)
+            while (active.load() > 0 && first_err.load() == MMBA_OK && !stop_flag.load()) {
                 if (cb->interrupt(cb->user)) stop_flag = true;
                 std::this_thread::yield();
             }

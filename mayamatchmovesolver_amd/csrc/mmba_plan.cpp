@@ -1209,6 +1209,10 @@ void Plan::setup_band(int Pforce) {
                     B.fflags = dalloc<int>((size_t)B.nblk + 64);  // items < nblk + levels
                     MMBA_HIP(hipMemsetAsync(B.fflags, 0, sizeof(int) * ((size_t)B.nblk + 64), s));
                 }
+                B.tick = dalloc<unsigned>(2);
+                MMBA_HIP(hipMemsetAsync(B.tick, 0, sizeof(unsigned) * 2, s));
+                if (const char *e6 = std::getenv("MMBA_BCR_DF_GRID"))
+                    bs.df_grid = std::max(1, std::min(256, std::atoi(e6)));
             }
             {
                 // dataflow backward solve: blocks in dependency order (root,

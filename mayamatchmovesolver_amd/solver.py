@@ -224,12 +224,20 @@ class Solver:
 
     def set_timing(self, enable=True):
         st = abi.MmbaKernelStats()
+        self._timing = bool(enable)
         check(lib().mmba_plan_kernel_stats(self._h, 1 if enable else 0, C.byref(st)))
 
     def kernel_stats(self):
+        """The plan's kernel statistics (the timing switch is left as set)."""
         st = abi.MmbaKernelStats()
-        check(lib().mmba_plan_kernel_stats(self._h, 1, C.byref(st)))
+        check(lib().mmba_plan_kernel_stats(self._h, 1 if getattr(self, "_timing", False) else 0,
+                                           C.byref(st)))
         return st.as_dict()
+
+    def dataflow_fallback(self) -> bool:
+        """True once a timed-out dataflow wait switched this plan's block
+        cyclic reduction to the per-level launches."""
+        return bool(self.kernel_stats()["dataflow_fallback"])
 
     def measure(self, x=None):
         p = self.problem

@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Full-size golden fixtures (tests/golden/full/*.npz): the CPU oracle
+(oracle/refcpu.c, the restatement of solveFrames -> cminpack lmder ->
+solveFunc / measureErrors) run on the BASELINE.json
+configurations at their full size, or on full-density C4 frame windows.
+
+The scenes are far too large to store (C2: 200k observations), so a fixture
+holds the generator call (config index, frames, scale, iteration cap) and a
+SHA-256 digest of the generated problem arrays; the GPU test regenerates the
+scene from the seed, checks the digest, and compares the oracle's outputs:
+
+- the solved internal x after the capped run (``iterations=2``: the initial
+  evaluation, one FD Jacobian + damped solve, one trial point = one LM step,
+  the call count the reference passes as maxfev; adjust_cminpack_lmder.cpp:
+  114-185),
+- fvec at that x, the per-evaluation ||f|| trace, the SolverResult counters,
+- ``exp_x_envelope``: how far the oracle's own x moves when x0 is perturbed by
+  ~1 ulp (relative 1e-15; one run per seed), i.e. how closely any fp64
+  implementation of the reference determines x at this point.
+
+Each oracle run is one process (the full configs take 10-60 min single
+threaded), so the runs go in parallel and a final ``--combine`` writes the
+fixture:
+
+    python tests/golden/make_full_golden.py --case c2_full_it1 --seed -1   # main run
+    python tests/golden/make_full_golden.py --case c2_full_it1 --seed 0    # envelope seeds
+    python tests/golden/make_full_golden.py --case c2_full_it1 --combine
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FULL = os.path.join(HERE, "full")
+PARTS = os.path.join(FULL, "_parts")
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from mayamatchmovesolver_amd import synthetic as S  # noqa: E402
+
+RES_FIELDS = ["success", "reason_number", "iterations", "function_evals", "jacobian_evals",
+              "outer_iterations", "error_final", "error_avg", "error_min", "error_max",
+              "error_rms"]
+
+# name: (config index, frames, scale, iterations cap, store fvec)
+#   C2 / C5: the full configurations, one LM step (profiles/r2_cpu: 509 s / 3,468 s)
+#   C4 windows: full C4 density (100 new bundles per frame, 4-frame tracks) on F'
+#   frames; w24 one step (the largest window one step of which finishes in
+#   about half an hour), w10 the full run (the trace; x is pinned by the envelope)
+CASES = {
+    "c2_full_it1": (1, None, 1.0, 2, True),
+    "c5_full_it1": (4, None, 1.0, 2, True),
+    "c4_w24_it1": (3, 24, 24 / 500.0, 2, True),
+    "c4_w10_full": (3, 10, 10 / 500.0, 1000, True),
+}
+
+
+def make_problem(name):
+    idx, frames, scale, _it, _f = CASES[name]
+    return S.make_config(idx, frames=frames, scale=scale)
+
+
+def make_options(name, prob):
+    return S.config_options(prob, iterations=CASES[name][3])
+
+
+def problem_digest(prob) -> str:
+    """SHA-256 over every array of the flat problem (field order fixed)."""
+    h = hashlib.sha256()
+    d = prob.to_npz_dict()
+    for k in sorted(d):
+        a = np.ascontiguousarray(d[k])
+        h.update(k.encode())
+        h.update(str(a.dtype).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def run(name, seed):
+    from oracle import refcpu as R
+    os.makedirs(PARTS, exist_ok=True)
+    prob = make_problem(name)
+    opt = make_options(name, prob)
+    x0 = prob.x0
+    if seed >= 0:
+        rng = np.random.default_rng(seed)
+        x0 = prob.x0 * (1.0 + 1e-15 * rng.standard_normal(prob.x0.size))
+    t = time.perf_counter()
+    x, fvec, eu, ed, res, tr = R.solve(prob, opt, x0=x0)
+    dt = time.perf_counter() - t
+    out = {"x": x, "seconds": np.array(dt)}
+    if seed < 0:
+        rd = res.as_dict()
+        out.update(fvec=fvec, trace=tr, digest=np.array(problem_digest(prob)))
+        for f in RES_FIELDS:
+            out["res_" + f] = np.array(rd[f])
+    np.savez(os.path.join(PARTS, "%s_s%d.npz" % (name, seed)), **out)
+    print(json.dumps({"case": name, "seed": seed, "seconds": dt, "n": prob.num_params,
+                      "m": prob.num_residuals, "outer": res.outer_iterations,
+                      "reason": res.reason_number}), flush=True)
+
+
+def combine(name):
+    idx, frames, scale, iters, keep_f = CASES[name]
+    main = dict(np.load(os.path.join(PARTS, "%s_s-1.npz" % name), allow_pickle=False))
+    x = main["x"]
+    env, seeds = 0.0, []
+    for f in sorted(os.listdir(PARTS)):
+        if f.startswith(name + "_s") and not f.endswith("_s-1.npz"):
+            xp = np.load(os.path.join(PARTS, f), allow_pickle=False)["x"]
+            env = max(env, float(np.max(np.abs(xp - x) / np.maximum(np.abs(x), 1e-3))))
+            seeds.append(f)
+    d = {"gen_config": np.array(idx), "gen_frames": np.array(-1 if frames is None else frames),
+         "gen_scale": np.array(scale), "gen_iterations": np.array(iters),
+         "digest": main["digest"], "exp_x": x, "exp_trace": main["trace"],
+         "exp_x_envelope": np.array(env), "envelope_runs": np.array(len(seeds)),
+         "oracle_seconds": main["seconds"]}
+    if keep_f:
+        d["exp_fvec"] = main["fvec"]
+    for k, v in main.items():
+        if k.startswith("res_"):
+            d[k] = v
+    os.makedirs(FULL, exist_ok=True)
+    path = os.path.join(FULL, name + ".npz")
+    np.savez_compressed(path, **d)
+    print("%-14s n=%d reason=%d trace=%d x-envelope=%.2e (%d runs) oracle %.0f s  %.0f KB" % (
+        name, x.size, int(d["res_reason_number"]), d["exp_trace"].size, env, len(seeds),
+        float(main["seconds"]), os.path.getsize(path) / 1024))
+
+
+def load(name):
+    """(problem, options, fixture dict); raises if the regenerated scene's
+    digest differs from the one the oracle ran on."""
+    d = dict(np.load(os.path.join(FULL, name + ".npz"), allow_pickle=False))
+    frames = int(d["gen_frames"])
+    prob = S.make_config(int(d["gen_config"]), frames=None if frames < 0 else frames,
+                         scale=float(d["gen_scale"]))
+    dg = problem_digest(prob)
+    if dg != str(d["digest"]):
+        raise RuntimeError("%s: regenerated scene differs from the fixture's (%s != %s)" % (
+            name, dg[:12], str(d["digest"])[:12]))
+    opt = S.config_options(prob, iterations=int(d["gen_iterations"]))
+    return prob, opt, d
+
+
+def fixture_names():
+    if not os.path.isdir(FULL):
+        return []
+    return sorted(f[:-4] for f in os.listdir(FULL) if f.endswith(".npz"))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", required=True, choices=sorted(CASES))
+    ap.add_argument("--seed", type=int, default=-1)
+    ap.add_argument("--combine", action="store_true")
+    a = ap.parse_args()
+    if a.combine:
+        combine(a.case)
+    else:
+        run(a.case, a.seed)

@@ -46,3 +46,24 @@ def test_fixture_consistency(name):
     assert d["exp_trace"].size == int(d["res_function_evals"])
     assert abs(np.linalg.norm(d["exp_fvec"]) - float(d["res_error_final"])) <= \
         1e-12 * max(1.0, float(d["res_error_final"]))
+
+
+# ---- full-size fixtures (tests/golden/make_full_golden.py): the oracle's
+# outputs on the full BASELINE configurations / full-density C4 windows; the
+# scenes are regenerated from their seed, so the generator must reproduce the
+# exact problem the oracle ran on (SHA-256 digest).
+from tests.golden import make_full_golden as FG  # noqa: E402
+
+FULL = FG.fixture_names()
+
+
+@pytest.mark.parametrize("name", FULL)
+def test_full_fixture_scene_digest(name):
+    prob, opt, d = FG.load(name)  # raises on a digest mismatch
+    assert d["exp_x"].size == prob.num_params
+    if "exp_fvec" in d:
+        assert d["exp_fvec"].size == prob.num_residuals
+        assert abs(np.linalg.norm(d["exp_fvec"]) - float(d["res_error_final"])) <= \
+            1e-12 * float(d["res_error_final"])
+    assert d["exp_trace"].size == int(d["res_function_evals"])
+    assert int(d["envelope_runs"]) >= 1

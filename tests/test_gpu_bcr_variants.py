@@ -23,11 +23,17 @@ SCENES = {
 VARIANTS = {
     "levels": {"MMBA_BCR_DF": "0"},
     "chain": {"MMBA_BCR_CHOL": "0"},
+    # dataflow launches on 1 / 3 workgroups: most items are drawn (item
+    # tickets) by workgroups that already ran others -- the forward-progress
+    # path when few workgroups are resident
+    "grid1": {"MMBA_BCR_DF_GRID": "1"},
+    "grid3": {"MMBA_BCR_DF_GRID": "3"},
 }
+ENV_KEYS = ("MMBA_BCR_DF", "MMBA_BCR_MFMA", "MMBA_BCR_CHOL", "MMBA_BCR_DF_GRID")
 
 
 def run(prob, opt, ctx, monkeypatch, env):
-    for k in ("MMBA_BCR_DF", "MMBA_BCR_MFMA", "MMBA_BCR_CHOL"):
+    for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -58,7 +64,7 @@ def test_bcr_dataflow_repeatable(gpu_ctx, monkeypatch):
     idx, kw = SCENES["c4"]
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
-    for k in ("MMBA_BCR_DF", "MMBA_BCR_MFMA", "MMBA_BCR_CHOL"):
+    for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     s = Solver(prob, opt, context=gpu_ctx)
     try:
@@ -85,3 +91,60 @@ def test_bcr_band_arrow_dataflow_bitwise(nb, w, nG, gpu_ctx, monkeypatch):
         outs.append((x, yn))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
+
+
+def _threads(n, fn):
+    import threading
+    outs, errs = [None] * n, [None] * n
+
+    def work(r):
+        try:
+            outs[r] = fn(r)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs[r] = e
+
+    ths = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(n)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ths), "concurrent solves hung"
+    assert errs == [None] * n, errs
+    return outs
+
+
+def test_bcr_dataflow_concurrent_full_c4(gpu_ctx, monkeypatch):
+    """Eight full-size C4 solves (125 band blocks: 63 workgroups of 256
+    threads per dataflow factorisation, 125 per backward solve) at once, one
+    host thread and one stream each: about 500 workgroups that each fill a CU
+    compete for 256 CUs, so the dataflow launches cannot all be resident.
+    With item tickets every wait still ends: each solve must equal the solo
+    solve bit for bit (a timed-out wait would fail the solve or switch the
+    plan to the per-level launches, whose bits are the same -- so the flag is
+    checked too)."""
+    from mayamatchmovesolver_amd.solver import Context
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    prob = S.make_config(3)
+    opt = S.config_options(prob)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        ref = s.solve()
+    finally:
+        s.close()
+    assert ref.result["success"]
+    n = 8
+    ctxs = [Context(0) for _ in range(n)]
+    solvers = [Solver(prob, opt, context=ctxs[r]) for r in range(n)]
+    try:
+        for _ in range(2):
+            outs = _threads(n, lambda r: solvers[r].solve())
+            for o in outs:
+                np.testing.assert_array_equal(o.fnorm_trace, ref.fnorm_trace)
+                np.testing.assert_array_equal(o.x, ref.x)
+        assert all(not sv.dataflow_fallback() for sv in solvers)
+    finally:
+        for sv in solvers:
+            sv.close()
+        for c in ctxs:
+            c.close()

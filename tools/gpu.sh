@@ -1,0 +1,46 @@
+# GPU-box steps, run through gpurun from the repo root:
+#   gpurun --timeout 1200 -- 'bash tools/gpu.sh OUT STEP [STEP ...]'
+# Steps (each under its own time limit; the first failure ends the call):
+#   tests[:PYTEST_K]  the -m gpu suite (optionally only tests matching -k)
+#   smoke             __graft_entry__.smoke()
+#   bench             the default bench line (C4, CPU baseline, PMC traffic)
+#   benchcfg:I        bench line of configs[I] (no CPU baseline)
+#   prof              rocprofv3 --kernel-trace --stats of the default bench
+#   pmc               FETCH_SIZE / WRITE_SIZE passes of the default bench
+set -o pipefail
+OUT=${1:?out dir}
+shift
+mkdir -p "$OUT"
+ROOT=$(pwd)
+export TMPDIR=/tmp
+for step in "$@"; do
+  case "$step" in
+    tests*)
+      K=${step#tests}; K=${K#:}
+      if [ -n "$K" ]; then
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "$K" > "$OUT/tests.log" 2>&1
+      else
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/tests.log" 2>&1
+      fi
+      rc=$?; tail -25 "$OUT/tests.log"; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; } ;;
+    bench)
+      timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail "$OUT/bench.err"; exit 1; }
+      cat "$OUT/bench.json" ;;
+    benchcfg:*)
+      c=${step#benchcfg:}
+      timeout -k 10 400 python -u bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
+      cat "$OUT/bench_$c.json" ;;
+    prof)
+      cd /tmp && cd "$ROOT"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c4 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" || { tail "$OUT/prof_bench.err"; exit 1; }
+      python3 tools/iter_trace.py "$OUT/prof/c4_kernel_trace.csv" > "$OUT/c4_iteration_trace.txt" && rm -f "$OUT/prof/c4_kernel_trace.csv" ;;
+    pmc)
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$OUT/pmc_$ctr" -o c4 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/pmc_$ctr.json" 2> "$OUT/pmc_$ctr.err" || exit 1
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps done"
