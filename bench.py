@@ -55,6 +55,9 @@ def parse():
                     choices=["classic", "classic_animated", "radial", "anamorphic",
                              "anamorphic_rescaled"],
                     help="configs[4] lens model (classic = the C5 spec)")
+    ap.add_argument("--rolling-shutter", type=float, default=0.0, metavar="RS",
+                    help="configs[4]: rolling-shutter value in frames (time shift x fps; "
+                         "the configs[4] per-scanline pose, mmba.h ABI 3)")
     ap.add_argument("--per-frame", type=int, default=0, metavar="CONC",
                     help="per-frame solve mode (mmba_solve_per_frame) with CONC frames at "
                          "once; prints its own JSON line (not the headline metric)")
@@ -125,6 +128,8 @@ def pmc_traffic(args):
             "--scale", str(args.scale)]
     if args.frames:
         base += ["--frames", str(args.frames)]
+    if args.config == 4:
+        base += ["--lens-model", args.lens_model, "--rolling-shutter", str(args.rolling_shutter)]
     env = dict(os.environ, TMPDIR="/tmp")
     per = {}
     tmp = tempfile.mkdtemp(prefix="mmba_pmc_", dir="/tmp")
@@ -269,7 +274,8 @@ def per_frame_line(args):
     from mayamatchmovesolver_amd import synthetic as S
     from mayamatchmovesolver_amd._lib import MmbaError
     from mayamatchmovesolver_amd.solver import Solver, solve_per_frame
-    kw = {"lens_model": args.lens_model} if args.config == 4 else {}
+    kw = ({"lens_model": args.lens_model, "rolling_shutter": args.rolling_shutter}
+          if args.config == 4 else {})
     prob = S.make_config(args.config, frames=args.frames, scale=args.scale, **kw)
     opt = S.config_options(prob)
     obs_per_frame = np.bincount(np.asarray(prob.obs_frame), minlength=prob.num_frames)
@@ -331,7 +337,8 @@ def main():
         frames = (frames or BASE_FRAMES.get(args.config, 500)) * world
         scale = scale * world
     t0 = time.perf_counter()
-    kw = {"lens_model": args.lens_model} if args.config == 4 else {}
+    kw = ({"lens_model": args.lens_model, "rolling_shutter": args.rolling_shutter}
+          if args.config == 4 else {})
     prob = S.make_config(args.config, frames=frames, scale=scale, **kw)
     opt = S.config_options(prob)
     gen_s = time.perf_counter() - t0

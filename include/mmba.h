@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 2
+#define MMBA_ABI_VERSION 3
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -199,6 +199,27 @@ typedef struct mmba_problem {
     const double *smooth_weight;
     const double *smooth_variance;
     const double *smooth_value;
+
+    /* ---- ABI 3 ---- */
+    /* Rolling shutter (BASELINE configs[4]; an extension: the reference
+     * solver has no rolling-shutter model, its only rolling-shutter
+     * arithmetic is the 3DE exporter's 2D correction,
+     * share/3dequalizer/python/uvtrack_format.py:243-330).  Per camera the
+     * rolling-shutter value in frames, rs = time shift x fps (:269-270);
+     * 0 = a global shutter.  NULL = off for every camera (the reference
+     * behaviour).  With rs != 0 and num_frames > 1, the camera transform's
+     * translate / rotate attributes seen by observation (marker, frame f) are
+     * the exporter's three-frame blend (_apply_rs_correction, :186-203) at the
+     * scanline time tau = rs * (0.5 - y) (y = obs_xy's y, film-height units,
+     * +y up: the top scanline is read first, :318):
+     *   b = (v(f+1) - v(f-1)) / 2,  c = -v(f) + (v(f+1) + v(f-1)) / 2,
+     *   v(f + tau) = v(f) + tau b + tau^2 c,
+     * with the exporter's end extrapolation v(-1) = v(0) + (v(0) - v(1)),
+     * v(F) = v(F-1) + (v(F-1) - v(F-2)) (:311-314).  The FD column of an
+     * animated parameter then re-measures frames f-1..f+1.  Supported on
+     * camera transforms without a parent, without solved bundles, unsharded
+     * (MMBA_ERR_UNSUPPORTED otherwise). */
+    const double *cam_rs_value;   /* [num_cameras] */
 } mmba_problem;
 
 /* SolverOptions subset that the LM path reads (adjust_data.h:133-185). */

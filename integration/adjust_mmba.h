@@ -3,9 +3,12 @@
 // solveFrames (src/mmSolver/adjust/adjust_base.cpp:1175-1184); see
 // INTEGRATION.md for the three lines that dispatch to it.
 //
-// This file and adjust_mmba.cpp belong in src/mmSolver/adjust/ of the
-// mmSolver tree and build with the plug-in (Maya SDK, mmscenegraph, mmlens);
-// they are not compiled in this repository, which has no Maya SDK.
+// This file and adjust_mmba.cpp (the Maya layer: scene reads through the
+// reference's Maya helpers) belong in src/mmSolver/adjust/ of the mmSolver
+// tree and build with the plug-in (Maya SDK).  Everything below the reads --
+// SolverData -> mmba_problem, the plan cache, the solve, the result mapping --
+// is adjust_mmba_core.{h,cpp}, which has no Maya dependency and is built and
+// tested in this repository (tests/shim, tests/test_shim_core.py).
 #ifndef MM_SOLVER_CORE_BUNDLE_ADJUST_MMBA_H
 #define MM_SOLVER_CORE_BUNDLE_ADJUST_MMBA_H
 

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -104,6 +104,8 @@ class MmbaProblem(C.Structure):
         ("smooth_weight", _f64p),
         ("smooth_variance", _f64p),
         ("smooth_value", _f64p),
+        # ---- ABI 3 ----
+        ("cam_rs_value", _f64p),
     ]
 
 

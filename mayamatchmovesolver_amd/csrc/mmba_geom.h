@@ -389,6 +389,47 @@ MMBA_DEV void camera_record_fast(const DevProblem &P, int cf, long long ov_idx, 
     camera_record_tail(P, c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], W, rec);
 }
 
+// Rolling shutter (mmba.h ABI 3): the camera-frame record as an observation
+// at scanline time tau sees it -- camera_record_fast with the transform's
+// translate / rotate values replaced by the 3DE exporter's three-frame blend
+// (uvtrack_format.py:186-203, end frames extrapolated as at :311-314); the
+// same operations as oracle/refcpu.c rs_blend.  The override (ov_idx,
+// ov_val) applies to every value read, the neighbouring frames' included.
+MMBA_DEV double rs_val(const DevProblem &P, int ix, long long ov_idx, double ov_val) {
+    return ix == ov_idx ? ov_val : P.attr_val[ix];
+}
+
+MMBA_DEV void camera_record_rs(const DevProblem &P, int cf, double tau, long long ov_idx,
+                               double ov_val, double *rec) {
+    const int *ix = &P.cf_aidx[(size_t)CF_AIDX * cf];
+    const int *nx = &P.cf_rs_vidx[(size_t)12 * cf];
+    const double dflt[CF_AIDX] = {36.0 / 25.4, 24.0 / 25.4, 0., 0., 35.0, 10000.0, 1.0,
+                                  0., 0., 0., 0., 0., 0., 1., 1., 1.};
+    double v[CF_AIDX];
+#pragma unroll
+    for (int k = 0; k < CF_AIDX; ++k) {
+        const int a = ix[k];
+        v[k] = a < 0 ? dflt[k] : (a == ov_idx ? ov_val : P.attr_val[a]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const double cv = v[7 + k];
+        const int ip = nx[k], in = nx[6 + k];
+        double pv = ip >= 0 ? rs_val(P, ip, ov_idx, ov_val) : 0.;
+        double nv = in >= 0 ? rs_val(P, in, ov_idx, ov_val) : 0.;
+        if (ip == -2) pv = cv + (cv - nv);
+        if (in == -2) nv = cv + (cv - pv);
+        const double b = (nv - pv) / 2.0;
+        const double c = -cv + ((nv + pv) / 2.0);
+        v[7 + k] = (cv + tau * b) + (tau * tau) * c;
+    }
+    const int c = P.cf_cam[cf];
+    double W[16];
+    trs_matrix(v[7], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15],
+               P.tfm_roo[P.cam_tfm[c]], W);
+    camera_record_tail(P, c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], W, rec);
+}
+
 // ---- LDPK classic 3DE model (undistort polynomial + fixed-point inverse) ----
 MMBA_DEV void lens_eval(const double *c, double px, double py, double &qx, double &qy) {
     const double ld = c[0], sq = c[1], cx = c[2], cy = c[3], qu = c[4];

@@ -258,6 +258,21 @@ struct DevProblem {
     // robust loss on every residual row (applyLossFunctionToErrors), when on
     int loss_on, loss_type;
     double loss_scale;
+    // rolling shutter (mmba.h ABI 3, mmba_rs.hip): every observation sees its
+    // camera's translate / rotate values blended over frames f-1, f, f+1 at
+    // its scanline time obs_tau[i] (device order; 0 for a global shutter).
+    // cf_rs_nb[2 cf + 0/1] = camera-frame of the same camera at f-1 / f+1
+    // (-1: none); cf_rs_vidx[12 cf + k / 6 + k] = attribute-value index of
+    // transform attribute k (tx ty tz rx ry rz) at f-1 / f+1 (-1: absent,
+    // value 0; -2: outside the frame range, the exporter's extrapolation).
+    // Jacobian columns of an observation: its camera-frame's variants, then
+    // the CF parameters of cf_rs_nb[0], then those of cf_rs_nb[1], then the
+    // lens parameters.  rs_Aoff[(2 cf + d - 1) PCMAX^2]: the camera-frame
+    // coupling blocks A(cf, next^d(cf)), d = 1, 2.
+    int rs;
+    const double *obs_tau;
+    const int *cf_rs_nb, *cf_rs_vidx;
+    double *rs_Aoff;
 };
 
 __device__ __forceinline__ size_t widx(const DevProblem &P, int k, int i) {

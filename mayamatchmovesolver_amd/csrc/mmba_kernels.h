@@ -230,4 +230,12 @@ void launch_batch_lm(hipStream_t s, const DevProblem &P, const BatchArgs &B, int
 void launch_dgemm_nt(hipStream_t s, bool tri, int M, int N, int Kd, const double *A, int lda,
                      const double *B, int ldb, double *C, int ldc, double alpha, double beta);
 
+// rolling shutter (mmba_rs.hip)
+void launch_jacobian_rs(hipStream_t s, const DevProblem &P, const double *ext_pert,
+                        const double *step, int solver_type, double *J, int *jcol, int *nloc,
+                        const int *stale_param, double *eu, double *ed);
+void launch_ne_rs(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
+                  const int *nloc, const double *f, double *Acc, double *Acg, double *g);
+void launch_rs_offdiag(hipStream_t s, const DevProblem &P, const SView &V);
+
 }  // namespace mmba

@@ -237,7 +237,9 @@ __global__ void __launch_bounds__(64) k_records(DevProblem P, const int *__restr
 // k_jp_sumsq) into a second partial row.
 // FAST: every bundle is fast and no camera has a lens (the transform-chain
 // and lens code, and their registers, are compiled out).
-template <bool JP, bool FAST>
+// RS: rolling shutter (mmba_rs.hip): each observation's camera record is
+// its own scanline pose (camera_record_rs), not the camera-frame's.
+template <bool JP, bool FAST, bool RS = false>
 __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__restrict__ recs,
                                                   double *f, double *eu, double *ed,
                                                   double *partial, double *out,
@@ -271,6 +273,11 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         const int hl = FAST ? MMBA_LENS_NONE : obs_lens(P, cam, lens);
         if (hl) lens_coeffs(P, lens, fr, none, lc);
         const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
+        double rloc[RS ? CAMREC : 1];
+        if constexpr (RS) {
+            camera_record_rs(P, cf, P.obs_tau[i], -1, 0., rloc);
+            rec = rloc;
+        }
         Resid r = residual_l(P, rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i],
                              hl, lc);
         f[2 * i] = r.ex;
@@ -2287,7 +2294,11 @@ void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, dou
     // only: with stiffness / smoothness rows (one more partial, k_rows_eval)
     // the two-launch reduction runs
     if (ticket && residual_blocks(P) != nblk(P.M, 256)) ticket = nullptr;
-    if (P.all_bnd_fast && P.no_lens)
+    if (P.rs)
+        k_residual<false, false, true><<<nblk(P.M, 256), 256, 0, s>>>(
+            P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
+            dist);
+    else if (P.all_bnd_fast && P.no_lens)
         k_residual<false, true><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
             dist);
@@ -2313,6 +2324,11 @@ __global__ void __launch_bounds__(256) k_reproject(DevProblem P, const double *_
     const int hl = obs_lens(P, cam, lens);
     if (hl) lens_coeffs(P, lens, fr, none, lc);
     const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
+    double rloc[CAMREC];
+    if (P.rs) {  // this observation's scanline pose
+        camera_record_rs(P, cf, P.obs_tau[i], -1, 0., rloc);
+        rec = rloc;
+    }
     double px, py;
     project_point(rec, bp, px, py);
     distort_point(hl, lc, px, py);
@@ -2329,7 +2345,10 @@ void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, 
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,
                         double *partial_jp, double *dist) {
-    if (P.all_bnd_fast && P.no_lens)
+    if (P.rs)
+        k_residual<true, false, true><<<nblk(P.M, 256), 256, 0, s>>>(
+            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
+    else if (P.all_bnd_fast && P.no_lens)
         k_residual<true, true><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
     else
@@ -2412,6 +2431,10 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
                      int ncv, const double *f, const CentralB &CB) {
     (void)f;
+    if (P.rs) {  // rolling shutter: three camera-frame blocks per row (mmba_rs.hip)
+        launch_jacobian_rs(s, P, ext_pert, step, solver_type, J, jcol, nloc, stale_param, eu, ed);
+        return;
+    }
 #define MMBA_JAC_U(NCV, GEN)                                                                \
     k_jacobian_u<NCV, GEN><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, \
                                                            nloc, stale_param, eu, ed)
@@ -2433,7 +2456,7 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
 // observation over the whole GPU.
 bool jac_ne_fusable(const DevProblem &P, int ncv) {
     return P.nG == 0 && P.pc_uniform == ncv && (ncv == 6 || ncv == 7) &&
-           P.nrows == 0 && !P.loss_on && P.ncf >= 256;
+           P.nrows == 0 && !P.loss_on && P.ncf >= 256 && !P.rs;
 }
 void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const double *step,
                    int solver_type, double *J, int *jcol, int *nloc, const int *stale_param,
@@ -2490,7 +2513,8 @@ void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, d
         k_param_central<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext_pertB, stepB, delta, count);
 }
 bool ne_epilogue_fusable(const DevProblem &P) {
-    return P.nG == 0 && (P.JB || P.nbs == 0) && (P.pc_uniform == 6 || P.pc_uniform == 7);
+    return P.nG == 0 && (P.JB || P.nbs == 0) && (P.pc_uniform == 6 || P.pc_uniform == 7) &&
+           !P.rs;
 }
 void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                const int *nloc, const double *f, double *Acc, double *Acg, double *Abb,
@@ -2498,7 +2522,9 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
                const NeEpi &epi, bool cf_done) {
     const NeEpi E = ne_epilogue_fusable(P) ? epi : NeEpi();
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
-    if (P.ncf > 0 && !cf_done) {
+    if (P.rs) {  // coupled camera-frame blocks (mmba_rs.hip)
+        launch_ne_rs(s, P, J, jcol, nloc, f, Acc, Acg, g);
+    } else if (P.ncf > 0 && !cf_done) {
         const bool wide = P.M > 1024 * P.ncf;  // long camera-frame segments (C2): 4 waves
 #define MMBA_NE_U(PC, NW, NG)                                                              \
     k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E)
@@ -2561,6 +2587,7 @@ void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, co
                        const SView &V, int npad, double *rhs) {
     const int n = P.ncf * PCMAX + P.nG + npad;
     k_schur_init<<<nblk(n, 256), 256, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs);
+    if (P.rs) launch_rs_offdiag(s, P, V);  // camera-frame coupling blocks
 }
 void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                         const double *tb, const SView &V, double *rhs) {

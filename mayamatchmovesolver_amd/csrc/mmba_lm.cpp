@@ -703,7 +703,8 @@ void Plan::jac_partial_stale(const double *dx, int k) {
             continue;
         }
         for (int p = k - 1; p >= 0; --p)
-            if (param_frame_host[p] < 0 || param_frame_host[p] == f) {
+            if (param_frame_host[p] < 0 || param_frame_host[p] == f ||
+                (rs_on && std::abs(param_frame_host[p] - f) <= 1)) {
                 st[f] = p;
                 break;
             }

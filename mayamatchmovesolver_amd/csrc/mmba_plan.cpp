@@ -149,6 +149,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                     opt.robust_loss_type <= MMBA_ROBUST_LOSS_CAUCHY && opt.robust_loss_scale != 0.,
                 "robust_loss_type / robust_loss_scale");
 
+    // rolling shutter (mmba.h ABI 3, mmba_rs.hip): on when some camera has
+    // rs != 0 and there is more than one frame (oracle/refcpu.c rs_on)
+    rs_on = false;
+    if (pr->cam_rs_value && F > 1)
+        for (int c = 0; c < pr->num_cameras; ++c)
+            if (pr->cam_rs_value[c] != 0.) rs_on = true;
+
     // ---- validate indices ----
     for (int a = 0; a < nA; ++a) require(pr->attr_offset[a] >= 0, "attr_offset");
     for (int t = 0; t < nT; ++t) {
@@ -403,9 +410,41 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     for (int i = 0; i < Mg; ++i) obs_cf[i] = cf_id[{pr->obs_frame[i], obs_cam[i]}];
     std::vector<int> obs_bnd_g(Mg);
     for (int i = 0; i < Mg; ++i) obs_bnd_g[i] = pr->mkr_bnd[pr->obs_marker[i]];
+    // rolling shutter: the camera-frames of the same camera at f - 1 / f + 1
+    // (cameras with rs != 0), whose translate / rotate values the blend reads
+    std::vector<int> cf_nb(2 * (size_t)std::max(ncf, 1), -1);
+    if (rs_on) {
+        if (nranks > 1) throw Unsupported{"rolling shutter: sharded solve"};
+        if (central) throw Unsupported{"rolling shutter with central differences"};
+        if (nB_solved > 0) throw Unsupported{"rolling shutter with solved bundles"};
+        if (!bnd_par.empty()) throw Unsupported{"rolling shutter with bundle-side parameters"};
+        for (int c = 0; c < nC; ++c)
+            if (pr->tfm_parent[pr->cam_tfm[c]] >= 0)
+                throw Unsupported{"rolling shutter on a camera transform with a parent"};
+        for (int v : cf_var_flags)
+            if (v != 0) throw Unsupported{"rolling shutter with a camera / bundle shared attribute"};
+        for (int cf = 0; cf < ncf; ++cf) {
+            const int c = cf_cam[cf], f = cf_frame[cf];
+            if (pr->cam_rs_value[c] == 0.) continue;
+            auto a = cf_id.find({f - 1, c}), b = cf_id.find({f + 1, c});
+            if (a != cf_id.end()) cf_nb[2 * cf] = a->second;
+            if (b != cf_id.end()) cf_nb[2 * cf + 1] = b->second;
+        }
+    }
     bw = 0;
     for (int cf = 0; cf < ncf; ++cf)
         if (cf_pc[cf] > 0) bw = std::max(bw, cf_pc[cf] - 1);
+    if (rs_on)  // an observation couples its camera-frame with both neighbours
+        for (int cf = 0; cf < ncf; ++cf) {
+            int lo = cf_pc[cf] > 0 ? cf_roff[cf] : nCF, hi = cf_pc[cf] > 0 ? cf_roff[cf] + cf_pc[cf] - 1 : -1;
+            for (int side = 0; side < 2; ++side) {
+                const int cn = cf_nb[2 * cf + side];
+                if (cn < 0 || cf_pc[cn] == 0) continue;
+                lo = std::min(lo, cf_roff[cn]);
+                hi = std::max(hi, cf_roff[cn] + cf_pc[cn] - 1);
+            }
+            if (hi >= lo) bw = std::max(bw, hi - lo);
+        }
     {
         std::vector<int> blo(nB, nCF), bhi(nB, -1);
         for (int i = 0; i < Mg; ++i) {
@@ -418,6 +457,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             if (bhi[b] >= 0) bw = std::max(bw, bhi[b] - blo[b]);
     }
     band = nR > 0 && bw <= WBAND_MAX;
+    if (rs_on && !band) throw Unsupported{"rolling shutter: camera-frame band wider than WBAND_MAX (80)"};
 
     // ---- frame sharding: this shard's frames, camera-frame rows, observations
     // (own = in its frames; halo = other observations of solved bundles seen in
@@ -488,14 +528,32 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         cf_obs_off[d_cf[i] + 1]++;
     }
     for (int cf = 0; cf < ncf; ++cf) cf_obs_off[cf + 1] += cf_obs_off[cf];
-    // local column bound
-    for (int i = 0; i < M; ++i) {
+    // local column bound (rolling shutter: + the neighbouring frames' CF blocks)
+    // lens parameters that reach an observation: static ones and those keyed
+    // at its frame (an animated coefficient has one parameter per frame)
+    std::vector<int> cam_lpar_static(nC, 0);
+    std::vector<std::map<int, int>> cam_lpar_frame(nC);
+    for (int c = 0; c < nC; ++c)
+        for (int q = cam_lpar_off[c]; q < cam_lpar_off[c + 1]; ++q) {
+            const int fp = pr->param_frame[cam_lpar[q]];
+            if (fp < 0) ++cam_lpar_static[c];
+            else ++cam_lpar_frame[c][fp];
+        }
+    auto lens_cols = [&](int c, int f) {
+        auto it = cam_lpar_frame[c].find(f);
+        return cam_lpar_static[c] + (it == cam_lpar_frame[c].end() ? 0 : it->second);
+    };
+    auto obs_cols = [&](int i) {
         const int cf = d_cf[i];
-        const int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
-                       (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) +
-                       (cam_lpar_off[d_cam[i] + 1] - cam_lpar_off[d_cam[i]]);
-        if (nl > LMAX) throw Unsupported{"more than 20 parameters reach one observation"};
-    }
+        int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
+                 (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) +
+                 lens_cols(d_cam[i], d_frame[i]);
+        for (int side = 0; side < 2; ++side)
+            if (cf_nb[2 * cf + side] >= 0) nl += cf_pc[cf_nb[2 * cf + side]];
+        return nl;
+    };
+    for (int i = 0; i < M; ++i)
+        if (obs_cols(i) > LMAX) throw Unsupported{"more than 20 parameters reach one observation"};
     // Central differences and the robust loss are only well defined where
     // every lmder FD column re-measures every marker row: the reference
     // zero-initialises errorListB (adjust_solveFunc.cpp:412) and re-applies
@@ -542,7 +600,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             continue;
         }
         for (int p = n - 1; p >= 0; --p)
-            if (pr->param_frame[p] < 0 || pr->param_frame[p] == f) {
+            if (pr->param_frame[p] < 0 || pr->param_frame[p] == f ||
+                (rs_on && std::abs(pr->param_frame[p] - f) <= 1)) {
                 stale[f] = p;
                 break;
             }
@@ -775,7 +834,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int c = 0; c < nC && ok; ++c)
             if (pr->tfm_parent[pr->cam_tfm[c]] >= 0) ok = false;
         if (const char *e = std::getenv("MMBA_CAM_TABLE"))
-            if (std::atoi(e) == 0) ok = false;
+            if (std::atoi(e) == 0 && !rs_on) ok = false;
         D.cf_aidx = nullptr;
         if (ok && ncf > 0) {
             static const int cam_k[7] = {MMBA_CAM_FILM_BACK_W_INCH, MMBA_CAM_FILM_BACK_H_INCH,
@@ -826,8 +885,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             if (cf_var_flags[t] != 0) fast = false;
         for (int cf = 0; cf < ncf && fast; ++cf)
             if (cf_var_off[cf + 1] - cf_var_off[cf] - 1 > pc_uniform) fast = false;
-        // central differences and the robust loss run on the generic kernel
-        if (central || opt.robust_loss) fast = false;
+        // central differences, the robust loss and the rolling shutter run on
+        // the generic kernels
+        if (central || opt.robust_loss || rs_on) fast = false;
         jac_ncv = fast ? pc_uniform : 0;
         if (const char *e = std::getenv("MMBA_JAC_GENERIC"))
             if (std::atoi(e)) jac_ncv = 0;
@@ -845,13 +905,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         // widest observation (local Jacobian columns): camera variants +
         // bundle-side parameters + the camera's lens parameters
         int lm = 1;
-        for (int i = 0; i < M; ++i) {
-            const int cf = d_cf[i], b = d_bnd[i], cam = d_cam[i];
-            const int w = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
-                          (bnd_par_off[b + 1] - bnd_par_off[b]) +
-                          (cam_lpar_off[cam + 1] - cam_lpar_off[cam]);
-            lm = std::max(lm, w);
-        }
+        for (int i = 0; i < M; ++i) lm = std::max(lm, obs_cols(i));
         D.lmax = std::min(lm, LMAX);
     }
     D.p_attr = upload(pr->param_attr, n);
@@ -876,6 +930,38 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.row_w = upload(row_w);
     D.row_var = upload(row_var);
     D.row_val = upload(row_val);
+    D.rs = rs_on ? 1 : 0;
+    D.obs_tau = nullptr;
+    D.cf_rs_nb = nullptr;
+    D.cf_rs_vidx = nullptr;
+    D.rs_Aoff = nullptr;
+    if (rs_on) {
+        if (!D.cf_aidx) throw Unsupported{"rolling shutter needs the camera-frame table"};
+        std::vector<double> tau(M);
+        for (int i = 0; i < M; ++i) {
+            const int r = ref_of_dev[i];
+            tau[i] = pr->cam_rs_value[d_cam[i]] * (0.5 - pr->obs_xy[2 * r + 1]);
+        }
+        D.obs_tau = upload(tau);
+        D.cf_rs_nb = upload(cf_nb);
+        std::vector<int> vx((size_t)12 * ncf, -1);
+        for (int cf = 0; cf < ncf; ++cf) {
+            const int c = cf_cam[cf], f = cf_frame[cf], t = pr->cam_tfm[c];
+            for (int k = 0; k < 6; ++k) {
+                const int a = pr->tfm_attrs[9 * t + k];
+                auto vi = [&](int fr) -> int {
+                    if (fr < 0 || fr >= F) return -2;  // the exporter's extrapolation
+                    if (a < 0) return -1;
+                    return (int)(pr->attr_offset[a] + (pr->attr_animated[a] ? fr : 0));
+                };
+                vx[(size_t)12 * cf + k] = vi(f - 1);
+                vx[(size_t)12 * cf + 6 + k] = vi(f + 1);
+            }
+        }
+        D.cf_rs_vidx = upload(vx);
+        D.rs_Aoff = dalloc<double>((size_t)2 * ncf * PCMAX * PCMAX);
+        MMBA_HIP(hipMemsetAsync(D.rs_Aoff, 0, sizeof(double) * 2 * ncf * PCMAX * PCMAX, s));
+    }
     D.loss_on = opt.robust_loss ? 1 : 0;
     D.loss_type = opt.robust_loss_type;
     D.loss_scale = opt.robust_loss_scale;
@@ -1026,6 +1112,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             if (p_class[p] != PC_CF) why = "a static or shared parameter chains the frames";
         if (!why && nranks != 1) why = "sharded plan";
         if (!why && nrows > 0) why = "attribute stiffness / smoothness rows";
+        if (!why && rs_on) why = "rolling shutter";
         if (!why && (central || opt.robust_loss)) why = "central differences / robust loss";
         std::vector<int> fr_cf_off(F + 1, 0), fr_par_off(F + 1, 0), fr_par, fr_last, fr_nobs;
         int nf = F, nfmax = 0;
@@ -1104,7 +1191,7 @@ void Plan::setup_band(int Pforce) {
     {
         const char *e = std::getenv("MMBA_BDIAG");
         const bool off = e && std::atoi(e) == 0;
-        if (!off && nB_solved == 0 && nranks == 1 && !cfblk_pc.empty() && Pforce == 0) {
+        if (!off && nB_solved == 0 && nranks == 1 && !cfblk_pc.empty() && Pforce == 0 && !rs_on) {
             bs.use_bd = true;
             bs.P = 1;
             bs.w = w;

@@ -140,6 +140,8 @@ struct Plan {
     double *d_Jrow = nullptr;      // their Jacobian entries (one column each)
     // central differences (lmder, autoDiffType central): the deltaB pass
     bool central = false;
+    // rolling shutter (mmba.h ABI 3, mmba_rs.hip)
+    bool rs_on = false;
     double *d_ext_pertB = nullptr, *d_stepB = nullptr, *d_recsB = nullptr, *d_brecB = nullptr;
     std::vector<double> param_weight;  // paramWeightList (diag in mode 2)
     std::vector<int> stale_host;       // stale-column table (B13), host copy

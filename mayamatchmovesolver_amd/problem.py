@@ -130,6 +130,9 @@ class Problem:
     smooth_weight: Optional[np.ndarray] = None
     smooth_variance: Optional[np.ndarray] = None
     smooth_value: Optional[np.ndarray] = None
+    # ABI 3: per-camera rolling-shutter value in frames (time shift x fps;
+    # None = every camera a global shutter, the reference behaviour)
+    cam_rs_value: Optional[np.ndarray] = None
 
     def __post_init__(self):
         for name in _FIELDS_I32:
@@ -148,6 +151,9 @@ class Problem:
                     np.ascontiguousarray(v, dtype=np.float64).reshape(-1))
         if self.param_weight is not None:
             self.param_weight = np.ascontiguousarray(self.param_weight,
+                                                     dtype=np.float64).reshape(-1)
+        if self.cam_rs_value is not None:
+            self.cam_rs_value = np.ascontiguousarray(self.cam_rs_value,
                                                      dtype=np.float64).reshape(-1)
 
     # sizes -------------------------------------------------------------
@@ -242,6 +248,8 @@ class Problem:
         p.smooth_weight = ptr(self.smooth_weight, C.c_double)
         p.smooth_variance = ptr(self.smooth_variance, C.c_double)
         p.smooth_value = ptr(self.smooth_value, C.c_double)
+        p.cam_rs_value = (ptr(self.cam_rs_value, C.c_double) if self.cam_rs_value is not None
+                          else C.cast(None, C.POINTER(C.c_double)))
         return p, [self]
 
     # (de)serialisation ---------------------------------------------------
@@ -253,6 +261,8 @@ class Problem:
                 d[name] = getattr(self, name)
         if self.param_weight is not None:
             d["param_weight"] = self.param_weight
+        if self.cam_rs_value is not None:
+            d["cam_rs_value"] = self.cam_rs_value
         return d
 
     @classmethod
@@ -264,7 +274,7 @@ class Problem:
             la = np.concatenate([la.reshape(nl, 5), -np.ones((nl, abi.LENS_NUM_ATTRS - 5),
                                                              np.int32)], axis=1).reshape(-1)
             kw["lens_attrs"] = la
-        for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight"]:
+        for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight", "cam_rs_value"]:
             if name in d:
                 kw[name] = np.asarray(d[name])
         return cls(num_frames=int(d["num_frames"]), **kw)

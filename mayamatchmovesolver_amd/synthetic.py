@@ -319,7 +319,8 @@ CONFIG_NAMES = {
 def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                 scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH, window: int = 4,
                 depth=(20.0, 200.0), lens_model: str = "classic",
-                init_noise: float = 1.0, obs_noise: float = 1.0) -> Problem:
+                init_noise: float = 1.0, obs_noise: float = 1.0,
+                rolling_shutter: float = 0.0) -> Problem:
     """Concrete synthetic input for BASELINE.json ``configs[index]``.
 
     ``frames`` / ``scale`` shrink a configuration (frame-window subsets and
@@ -342,6 +343,8 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
     "classic_animated" (the classic lens with its distortion animated, one
     parameter per frame):
     SURVEY 8(f) row 2.
+    ``rolling_shutter`` (configs[4] only): rs in frames (time shift x fps),
+    the configs[4] "rolling-shutter per-scanline pose" (mmba.h ABI 3; 0 = off).
     """
     rng = np.random.Generator(np.random.PCG64(20241008 + index))
     if index == 0:
@@ -357,7 +360,7 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                           K=int(50000 * scale), window=window, per_cam_markers=False,
                           depth=depth, init_noise=init_noise, obs_noise=obs_noise)
     if index == 4:
-        return _config_c5(rng, frames or 240, scale, lens_model)
+        return _config_c5(rng, frames or 240, scale, lens_model, rolling_shutter)
     raise KeyError(index)
 
 
@@ -518,6 +521,55 @@ def _pose_project(t, r, focal, pts, fs):
     return fcl * pc[:, 0] / (FILM_W_MM * depth), fcl * pc[:, 1] / (FILM_H_MM * depth)
 
 
+def rs_blend(v, tau):
+    """Rolling-shutter pose blend (mmba.h ABI 3; the 3DE exporter's
+    _apply_rs_correction, uvtrack_format.py:186-203, with its end-frame
+    extrapolation :311-314): per-frame values v[F, ...] at time f + tau[f].
+    Used here only to synthesise markers through the same model."""
+    v = np.asarray(v, dtype=np.float64)
+    pv = np.concatenate([v[:1] + (v[:1] - v[1:2]), v[:-1]])
+    nv = np.concatenate([v[1:], v[-1:] + (v[-1:] - v[-2:-1])])
+    b = (nv - pv) / 2.0
+    c = -v + ((nv + pv) / 2.0)
+    tau = np.asarray(tau, dtype=np.float64).reshape((-1,) + (1,) * (v.ndim - 1))
+    return (v + tau * b) + (tau * tau) * c
+
+
+def _pose_project_rs(t, r, focal, pts, fs, rs, y_guess, iters=4):
+    """_pose_project with the camera pose of each observation taken at its
+    scanline time tau = rs * (0.5 - y) (a fixed point in the marker's own y)."""
+    y = np.asarray(y_guess, dtype=np.float64)
+    mx = my = None
+    for _ in range(iters):
+        tau = rs * (0.5 - y)
+        tb = np.empty((fs.size, 3))
+        rb = np.empty((fs.size, 3))
+        for k in range(3):
+            tb[:, k] = _blend_at(t[:, k], fs, tau)
+            rb[:, k] = _blend_at(r[:, k], fs, tau)
+        R = _euler_xyz(rb[:, 0], rb[:, 1], rb[:, 2])
+        pc = np.einsum("nij,ni->nj", R, pts - tb)
+        depth = -pc[:, 2]
+        fcl = focal[fs] if np.ndim(focal) else focal
+        mx, my = fcl * pc[:, 0] / (FILM_W_MM * depth), fcl * pc[:, 1] / (FILM_H_MM * depth)
+        y = my
+    return mx, my
+
+
+def _blend_at(v, fs, tau):
+    """rs_blend of the per-frame series v evaluated per observation (frame fs,
+    time offset tau)."""
+    F = v.size
+    cv = v[fs]
+    pv = np.where(fs > 0, v[np.maximum(fs - 1, 0)], 0.0)
+    nv = np.where(fs < F - 1, v[np.minimum(fs + 1, F - 1)], 0.0)
+    pv = np.where(fs == 0, cv + (cv - nv), pv)
+    nv = np.where(fs == F - 1, cv + (cv - pv), nv)
+    b = (nv - pv) / 2.0
+    c = -cv + ((nv + pv) / 2.0)
+    return (cv + tau * b) + (tau * tau) * c
+
+
 def _config_c2(rng, F, scale):
     """1 camera, 1k locked bundles, 5k markers (k -> k mod 1000), windows U[20,60];
     solve camera translate/rotate + focal per frame."""
@@ -620,9 +672,12 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0
                          meta={"name": CONFIG_NAMES[index]})
 
 
-def _config_c5(rng, F, scale, lens_model="classic"):
+def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0):
     """2 cams, 1k locked bundles, 2k markers (1k per cam), windows mean 60,
-    one shared 3DE-classic lens with distortion + quartic solved (lens attrs first)."""
+    one shared 3DE-classic lens with distortion + quartic solved (lens attrs first).
+    ``rolling_shutter`` = rs (frames, time shift x fps) != 0: both cameras
+    have that rolling shutter (mmba.h ABI 3) and the markers are synthesised
+    through the same per-scanline pose blend."""
     B, K = max(1, int(1000 * scale)), max(2, int(2000 * scale))
     ts, rs = zip(*[_camera_path(rng, F, c) for c in range(2)])
     P = _bundles_in_front(rng, B)
@@ -656,8 +711,18 @@ def _config_c5(rng, F, scale, lens_model="classic"):
         for c in range(2):
             sel = mkr_cam[ks] == c
             mx[sel], my[sel] = _pose_project(ts[c], rs[c], FOCAL_MM, P[mkr_bnd[ks[sel]]], fs[sel])
+            if rolling_shutter:
+                # the scanline pose: a fixed point in the distorted marker y
+                for _ in range(4):
+                    _dx, _dy = _c5_lens(mx[sel], my[sel])
+                    mx[sel], my[sel] = _pose_project_rs(
+                        ts[c], rs[c], FOCAL_MM, P[mkr_bnd[ks[sel]]], fs[sel], rolling_shutter,
+                        _dy, iters=1)
         # Horizontal fit marker y is in film-height units; the lens works on the
         # projected (film-fit scaled) point, see adjust_measureErrors.cpp:458-472.
+        return _c5_lens(mx, my)
+
+    def _c5_lens(mx, my):
         ra = RENDER[0] / RENDER[1]
         fa = FILM_W_MM / FILM_H_MM
         py = my * (ra / fa)
@@ -667,11 +732,15 @@ def _config_c5(rng, F, scale, lens_model="classic"):
     ks, fs, xy = _obs_from_windows(rng, start, length, proj)
     t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
     r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
-    return _bulk_problem(F, t0, r0, [FOCAL_MM, FOCAL_MM], lambda tids, cids: list(tids[:6]),
+    prob = _bulk_problem(F, t0, r0, [FOCAL_MM, FOCAL_MM], lambda tids, cids: list(tids[:6]),
                          P, np.zeros(B, bool), mkr_cam, mkr_bnd, ks, fs, xy, lens=lens,
                          lens_first=True,
                          meta={"name": CONFIG_NAMES[4] + ("" if lens_model == "classic"
-                                                          else "_" + lens_model)})
+                                                          else "_" + lens_model) +
+                               ("_rs" if rolling_shutter else "")})
+    if rolling_shutter:
+        prob.cam_rs_value = np.full(prob.num_cameras, float(rolling_shutter))
+    return prob
 
 
 EDGE_RENDERS = {"wide": (2048, 858), "narrow": (2048, 1556)}  # aspect above / below 36x24 mm

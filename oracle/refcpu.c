@@ -1038,6 +1038,7 @@ typedef struct {
     int interrupted;
     double *obs_pts, *obs_mkr; /* optional: reprojected point / corrected marker [2M] */
     int m;                     /* residual rows: 2M + stiffness + smoothness */
+    int rs_any;                /* some camera has a rolling shutter (mmba.h ABI 3) */
 } ref_scene;
 
 /* Test hook standing in for MComputation::isInterruptRequested: the poll
@@ -1231,6 +1232,49 @@ static void apply_lens(const ref_scene *s, int cam, int f, double *px,
     if (isfinite(oy)) *py = oy;
 }
 
+/* Rolling shutter (mmba.h ABI 3; an extension with no solver counterpart in
+ * the reference -- "parity unpinned against the reference").  The arithmetic
+ * is the 3DE exporter's (share/3dequalizer/python/uvtrack_format.py):
+ * rs = time shift x fps (:269-270), scanline time from the point's vertical
+ * position (:318, 3DE y in [0, 1] bottom-up = 0.5 + y here), the end-frame
+ * extrapolation (:311-314) and the three-frame quadratic blend
+ * _apply_rs_correction (:186-203), applied to the camera transform's
+ * translate / rotate attribute values at the observation's time f + tau. */
+static int rs_on(const ref_scene *s, int c) {
+    return s->p->cam_rs_value && s->p->cam_rs_value[c] != 0.0 && s->p->num_frames > 1;
+}
+
+static double rs_blend(const ref_scene *s, int a, int f, double tau) {
+    const int F = s->p->num_frames;
+    const double cv = attr_value(s, a, f, 0.);
+    double pv = f > 0 ? attr_value(s, a, f - 1, 0.) : 0.;
+    double nv = f < F - 1 ? attr_value(s, a, f + 1, 0.) : 0.;
+    if (f == 0) pv = cv + (cv - nv);
+    if (f == F - 1) nv = cv + (cv - pv);
+    const double b = (nv - pv) / 2.0;
+    const double c = -cv + ((nv + pv) / 2.0);
+    return (cv + tau * b) + (tau * tau) * c;
+}
+
+/* World matrix of camera c's transform as observation (f, y) sees it. */
+static void rs_camera_world(const ref_scene *s, int c, int f, double y, double W[16]) {
+    const mmba_problem *p = s->p;
+    const int t = p->cam_tfm[c];
+    const int *ta = &p->tfm_attrs[9 * t];
+    const double tau = p->cam_rs_value[c] * (0.5 - y);
+    double local[16];
+    ref_trs_matrix(rs_blend(s, ta[0], f, tau), rs_blend(s, ta[1], f, tau),
+                   rs_blend(s, ta[2], f, tau), rs_blend(s, ta[3], f, tau),
+                   rs_blend(s, ta[4], f, tau), rs_blend(s, ta[5], f, tau),
+                   attr_value(s, ta[6], f, 1.), attr_value(s, ta[7], f, 1.),
+                   attr_value(s, ta[8], f, 1.), p->tfm_rotate_order[t], local);
+    const int parent = p->tfm_parent[t];
+    if (parent >= 0)
+        mat4_mul(&s->tfm_world[((size_t)parent * p->num_frames + f) * 16], local, W);
+    else
+        memcpy(W, local, sizeof(local));
+}
+
 /* Writes errors for observations whose frame is enabled (mask). */
 static void measure(ref_scene *s, const char *frame_mask, double *errors) {
     const mmba_problem *p = s->p;
@@ -1273,7 +1317,18 @@ static void measure(ref_scene *s, const char *frame_mask, double *errors) {
         const double *cw = &s->tfm_world[((size_t)ct * F + f) * 16];
         const double *bw = &s->tfm_world[((size_t)bt * F + f) * 16];
         double bp[3] = {bw[3], bw[7], bw[11]};
-        if (s->o->scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        double cw_rs[16];
+        const int rs = rs_on(s, c);
+        if (rs) { /* this observation's scanline pose (both modes) */
+            rs_camera_world(s, c, f, p->obs_xy[2 * i + 1], cw_rs);
+            cw = cw_rs;
+        }
+        if (rs && s->o->scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+            double xy[2];
+            ref_reproject(cw, P, bp, xy);
+            point_x = xy[0];
+            point_y = xy[1];
+        } else if (s->o->scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
             const double *pt = &s->pts[((size_t)k * F + f) * 2];
             point_x = pt[0];
             point_y = pt[1];
@@ -1400,6 +1455,10 @@ static int scene_jac_der(void *c, int m, int n, double *x, double *fvec,
         if (p->param_frame[i] >= 0) {
             memset(s->frame_mask, 0, F);
             s->frame_mask[p->param_frame[i]] = 1;
+            if (s->rs_any) { /* the blend reaches the neighbouring frames */
+                if (p->param_frame[i] > 0) s->frame_mask[p->param_frame[i] - 1] = 1;
+                if (p->param_frame[i] < F - 1) s->frame_mask[p->param_frame[i] + 1] = 1;
+            }
             mask = s->frame_mask;
         }
         s->jac_evals++;
@@ -1499,6 +1558,7 @@ static void scene_init(ref_scene *s, const mmba_problem *p,
     s->xb = (double *)malloc(sizeof(double) * p->num_params);
     s->ea = (double *)calloc((size_t)s->m, sizeof(double));
     s->eb = (double *)calloc((size_t)s->m, sizeof(double));
+    for (int c = 0; c < p->num_cameras; ++c) s->rs_any |= rs_on(s, c);
 }
 
 static void scene_free(ref_scene *s) {

@@ -59,6 +59,10 @@ def cases():
         # stopping point is not determined that closely)
         ("c4_f8_dense", 3, dict(frames=8, scale=0.002)),
         ("c5_f8_lens", 4, dict(frames=8, scale=0.05)),
+        # configs[4]'s rolling shutter (mmba.h ABI 3; an extension, parity
+        # against the reference unpinned: the oracle's blend follows the 3DE
+        # exporter, share/3dequalizer/python/uvtrack_format.py:186-203)
+        ("c5_f8_lens_rs", 4, dict(frames=8, scale=0.05, rolling_shutter=0.5)),
     ]
     for name, idx, kw in subsets:
         p = S.make_config(idx, **kw)

@@ -1,0 +1,112 @@
+"""Rolling shutter on the GPU (BASELINE configs[4] "rolling-shutter
+per-scanline pose"; mmba.h ABI 3, csrc/mmba_rs.hip) against the CPU oracle
+(oracle/refcpu.c rs_blend, pinned in tests/test_oracle_rs.py).
+
+The reference solver has no rolling-shutter model -- its only rolling-shutter
+arithmetic is the 3DE exporter's 2D correction
+(share/3dequalizer/python/uvtrack_format.py:186-203, 243-330), whose blend
+both sides apply to the camera pose -- so parity against the reference itself
+is unpinned; these tests hold the HIP path to the oracle at the north star's
+bar (reason, counts, every ||f|| and x at 1e-6; residuals 1e-12; the FD
+Jacobian 1e-7 of its max entry)."""
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import abi, synthetic as S
+from mayamatchmovesolver_amd._lib import MmbaError
+from mayamatchmovesolver_amd.solver import Solver
+from tests.test_gpu_parity import check_solve
+
+pytestmark = pytest.mark.gpu
+
+MODES = [abi.SCENE_GRAPH_MODE_MAYA_DAG, abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH]
+
+
+def rs_scene(frames=8, scale=0.05, rs=0.5, **kw):
+    return S.make_config(4, frames=frames, scale=scale, rolling_shutter=rs, **kw)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_rs_measure_jacobian_reproject(mode, oracle, gpu_ctx):
+    prob = rs_scene()
+    opt = S.config_options(prob, scene_graph_mode=mode)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        for x in (None, prob.x0 + 0.01):
+            f, eu, ed, _ = s.measure(x)
+            fr, eur, edr, _ = oracle.measure(prob, opt, x)
+            np.testing.assert_allclose(f, fr, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(eu, eur, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(ed, edr, rtol=1e-12, atol=1e-12)
+            pts, mkr = s.reproject(x)
+            pr, mr = oracle.reproject_obs(prob, opt, x)
+            np.testing.assert_allclose(pts, pr, rtol=1e-12, atol=1e-14)
+            np.testing.assert_allclose(mkr, mr, rtol=1e-15, atol=0)
+        x1 = prob.x0 + 0.01
+        J = s.jacobian(x1)
+        _, Jr = oracle.jacobian(prob, opt, x1)
+        scale = np.max(np.abs(Jr))
+        assert np.max(np.abs(J - Jr)) <= 1e-7 * scale
+        # the structure: neighbouring-frame columns are non-zero where the
+        # oracle's are (the blend reaches frames f - 1 .. f + 1)
+        assert np.max(np.abs(J[Jr == 0])) <= 1e-9 * scale
+        assert np.all(J[np.abs(Jr) > 1e-6 * scale] != 0)
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("solver_type", [abi.SOLVER_TYPE_CMINPACK_LMDER,
+                                         abi.SOLVER_TYPE_CMINPACK_LMDIF])
+@pytest.mark.parametrize("mode", MODES)
+def test_rs_solve_matches_oracle(solver_type, mode, oracle, gpu_ctx):
+    prob = rs_scene()
+    opt = S.config_options(prob, scene_graph_mode=mode, solver_type=solver_type)
+    out, (xr, rr) = check_solve(prob, opt, oracle, gpu_ctx)
+    assert rr.reason_number in (1, 2, 3, 5)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(frames=24, scale=0.2, rs=0.5),              # band through every frame
+    dict(frames=12, scale=0.1, rs=-0.8),             # bottom scanline first
+    dict(frames=8, scale=0.05, rs=0.5, lens_model="radial"),
+    dict(frames=8, scale=0.05, rs=0.5, lens_model="classic_animated"),
+])
+def test_rs_variants_match_oracle(kw, oracle, gpu_ctx):
+    prob = rs_scene(**kw)
+    opt = S.config_options(prob)
+    check_solve(prob, opt, oracle, gpu_ctx)
+
+
+def test_rs_one_camera_only(oracle, gpu_ctx):
+    """One camera with a rolling shutter, the other a global shutter."""
+    prob = rs_scene(frames=10, scale=0.08)
+    prob.cam_rs_value = np.array([0.7, 0.0])
+    opt = S.config_options(prob)
+    check_solve(prob, opt, oracle, gpu_ctx)
+
+
+def test_rs_zero_equals_global_shutter(gpu_ctx):
+    """cam_rs_value all 0 is the reference path, bit for bit."""
+    prob = rs_scene()
+    opt = S.config_options(prob)
+    outs = []
+    for rs in (np.zeros(prob.num_cameras), None):
+        prob.cam_rs_value = rs
+        s = Solver(prob, opt, context=gpu_ctx)
+        try:
+            outs.append(s.solve())
+        finally:
+            s.close()
+    np.testing.assert_array_equal(outs[0].x, outs[1].x)
+    np.testing.assert_array_equal(outs[0].fnorm_trace, outs[1].fnorm_trace)
+
+
+def test_rs_refuses_solved_bundles(gpu_ctx):
+    """Outside the supported scope (solved bundles) the plan is refused with
+    MMBA_ERR_UNSUPPORTED, never silently solved without the blend."""
+    prob = S.make_config(3, frames=8, scale=0.001)
+    prob.cam_rs_value = np.full(prob.num_cameras, 0.5)
+    opt = S.config_options(prob)
+    with pytest.raises(MmbaError) as e:
+        Solver(prob, opt, context=gpu_ctx)
+    assert e.value.code == abi.MMBA_ERR_UNSUPPORTED

@@ -1,0 +1,150 @@
+"""The Maya-free half of the plug-in shim (integration/adjust_mmba_core.cpp,
+VERDICT r2 "next" 9), compiled here with g++ and driven through the C ABI by
+tests/shim/shim_core_test.cpp on known scenes.
+
+CPU: the core's flattening of SolverData (SolverInputs + the scene reads) is
+checked against the Python-built problem of the same scene through the CPU
+oracle (identical residuals and solves, bit for bit: only the attribute
+numbering may differ), the known answers of test1 / test3 are reached from the
+shim's problem, and without a gfx950 device the core hands the solve back to
+cminpack (the executable's own checks).  The -m gpu leg (test_gpu_shim in
+this file) runs the same executable and entry on the device.
+Match: adjust_base.cpp:1167-1190 (the dispatch), adjust_data.h:188-261
+(SolverData)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import abi, synthetic as S
+from mayamatchmovesolver_amd.problem import SceneBuilder
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SHIM = os.path.join(HERE, "shim")
+
+
+@pytest.fixture(scope="module")
+def shim():
+    subprocess.check_call(["make", "-s", "-C", SHIM])
+    L = C.CDLL(os.path.join(SHIM, "libshimtest.so"))
+    L.shim_demo_problem.argtypes = [C.c_int, C.POINTER(abi.MmbaProblem)]
+    L.shim_demo_num_params.argtypes = [C.c_int]
+    L.shim_demo_x0.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(abi.MmbaOptions)]
+    L.shim_demo_solve.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]
+    return L
+
+
+def shim_problem(L, which):
+    p = abi.MmbaProblem()
+    assert L.shim_demo_problem(which, C.byref(p)) == 0
+    n = L.shim_demo_num_params(which)
+    x0 = np.zeros(n)
+    opt = abi.MmbaOptions()
+    assert L.shim_demo_x0(which, x0.ctypes.data_as(C.POINTER(C.c_double)), C.byref(opt)) == 0
+    return p, x0, opt
+
+
+def python_scene(which):
+    """The same scenes built by the Python SceneBuilder (attribute ids in its
+    own order)."""
+    if which == 0:
+        return S.known_scene("test1")
+    if which == 1:
+        return S.known_scene("test3")
+    F = 4
+    f = np.arange(F, dtype=np.float64)
+    b = SceneBuilder(F)
+    tfm, tids = b.transform(t=[0.1 * f, 1.0, -0.05 * f],
+                            r=[1.0 + 0.5 * f, -2.0 + 0.3 * f, 0.2 * f])
+    lens, lids = b.lens_3de_classic(distortion=0.02)
+    cam, _ = b.camera(tfm, lens=lens)
+    for k in range(5):
+        bt, _ = b.transform(t=(-4.0 + 2.0 * k, 1.0 + 0.5 * k, -20.0 - 3.0 * k))
+        b.bundle(bt)
+        b.marker(cam, k, np.stack([-0.3 + 0.15 * k + 0.01 * f, 0.2 - 0.1 * k + 0.005 * f], 1))
+    for a in tids[3:6]:
+        b.solve(a)
+    b.solve(lids[0])
+    prob = b.build()
+    prob.cam_rs_value = np.array([0.5])
+    return prob
+
+
+def oracle_run(oracle, pstruct, opt, x0, m, M):
+    """ref_measure + ref_solve on a raw mmba_problem."""
+    L = oracle.lib()
+    dp = C.POINTER(C.c_double)
+    xx = np.ascontiguousarray(x0, dtype=np.float64)
+    f, eu, ed, st = np.zeros(m), np.zeros(m), np.zeros(M), np.zeros(3)
+    assert L.ref_measure(C.byref(pstruct), C.byref(opt), xx.ctypes.data_as(dp),
+                         f.ctypes.data_as(dp), eu.ctypes.data_as(dp), ed.ctypes.data_as(dp),
+                         st.ctypes.data_as(dp)) == 0
+    x = xx.copy()
+    fv, eu2, ed2 = np.zeros(m), np.zeros(m), np.zeros(M)
+    res = abi.MmbaResult()
+    tb = np.zeros(4096)
+    tr = abi.MmbaTrace(tb.ctypes.data_as(dp), 4096, 0)
+    assert L.ref_solve(C.byref(pstruct), C.byref(opt), x.ctypes.data_as(dp),
+                       fv.ctypes.data_as(dp), eu2.ctypes.data_as(dp), ed2.ctypes.data_as(dp),
+                       C.byref(res), C.byref(tr)) == 0
+    return f, x, fv, tb[:tr.count].copy(), res
+
+
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_shim_problem_equals_python_scene(which, shim, oracle):
+    p, x0, opt = shim_problem(shim, which)
+    q = python_scene(which)
+    assert p.num_params == q.num_params and p.num_obs == q.num_obs
+    assert p.num_cameras == q.num_cameras and p.num_bundles == q.num_bundles
+    np.testing.assert_array_equal(x0, q.x0)
+    m, M = 2 * p.num_obs, p.num_obs
+    qs, keep = q.to_ctypes()
+    a = oracle_run(oracle, p, opt, x0, m, M)
+    b = oracle_run(oracle, qs, opt, q.x0, m, M)
+    np.testing.assert_array_equal(a[0], b[0])   # residuals at x0
+    np.testing.assert_array_equal(a[1], b[1])   # solved x
+    np.testing.assert_array_equal(a[3], b[3])   # ||f|| trace
+    assert a[4].reason_number == b[4].reason_number
+
+
+@pytest.mark.parametrize("which,name", [(0, "test1"), (1, "test3")])
+def test_shim_problem_known_answer(which, name, shim, oracle):
+    p, x0, opt = shim_problem(shim, which)
+    x = oracle_run(oracle, p, opt, x0, 2 * p.num_obs, p.num_obs)[1]
+    expected, tol = S.KNOWN_ANSWERS[name]
+    assert np.all(np.abs(x - np.array(expected)) <= tol), (x, expected)
+
+
+def test_shim_executable(shim):
+    """The C++ test: without a device every scene falls back to cminpack
+    (MMBA_ERR_NO_DEVICE is never a failed solve); with one, every scene
+    solves, test1 / test3 reach their known answers and the second round of
+    solves re-uses the cached plans."""
+    out = subprocess.run([os.path.join(SHIM, "shim_core_test")], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "PASSED" in out.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_gpu_shim(which, shim, oracle):
+    """mmba_shim::solve on the device, through the plan cache: x and ||f||
+    against the oracle at 1e-6 (the north star's bar)."""
+    p, x0, opt = shim_problem(shim, which)
+    n, m = p.num_params, 2 * p.num_obs
+    x, fv = np.zeros(n), np.zeros(m)
+    reason, fe = C.c_int(0), C.c_int(0)
+    msg = C.create_string_buffer(256)
+    dp = C.POINTER(C.c_double)
+    st = shim.shim_demo_solve(which, x.ctypes.data_as(dp), fv.ctypes.data_as(dp), C.byref(reason),
+                              C.byref(fe), msg, 256)
+    assert st == 1, msg.value
+    _f, xr, fr, trr, rr = oracle_run(oracle, p, opt, x0, m, p.num_obs)
+    assert reason.value == rr.reason_number
+    assert fe.value == rr.function_evals
+    assert np.max(np.abs(x - xr) / np.maximum(np.abs(xr), 1e-3)) <= 1e-6
+    assert abs(np.linalg.norm(fv) - rr.error_final) <= 1e-6 * rr.error_final + 1e-12
