@@ -5,11 +5,17 @@
 //   LocalComm  N shards driven by N host threads in one process (tests on a
 //              one-GPU box run the sharded code path against the unsharded
 //              one): every shard sums all shards' buffers in rank order, so
-//              all shards get bitwise identical results.
+//              all shards get bitwise identical results; MMBA_LOCAL_RING=1 at
+//              creation sums in ring order instead -- the order of a ring
+//              reduce-scatter (RCCL's ring all-reduce): the buffer is cut into
+//              N chunks and chunk c is accumulated starting at rank c + 1 and
+//              ending at rank c (mod N), so the sharded tests also see a
+//              summation order other than rank order.
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -44,6 +50,7 @@ struct LocalGroup {
     std::condition_variable cv;
     int arrived = 0;
     long gen = 0;
+    bool ring = false;
     double *bufs[LOCAL_MAX] = {};
     void barrier() {
         std::unique_lock<std::mutex> lk(m);
@@ -62,11 +69,16 @@ struct BufSet {
     const double *p[LOCAL_MAX];
 };
 
-__global__ void k_group_reduce(BufSet b, int n, size_t count, int max_op, double *out) {
+__global__ void k_group_reduce(BufSet b, int n, size_t count, int max_op, int ring, double *out) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
          i += (size_t)gridDim.x * blockDim.x) {
-        double s = b.p[0][i];
-        for (int k = 1; k < n; ++k) s = max_op ? fmax(s, b.p[k][i]) : s + b.p[k][i];
+        // ring: chunk c = floor(i n / count) starts at rank c + 1
+        const int r0 = ring ? (int)((i * (size_t)n / count + 1) % n) : 0;
+        double s = b.p[r0][i];
+        for (int k = 1; k < n; ++k) {
+            const double v = b.p[(r0 + k) % n][i];
+            s = max_op ? fmax(s, v) : s + v;
+        }
         out[i] = s;
     }
 }
@@ -91,7 +103,8 @@ struct LocalComm : Comm {
         BufSet b{};
         for (int k = 0; k < g->n; ++k) b.p[k] = g->bufs[k];
         const int blocks = (int)std::min<size_t>((count + 255) / 256, 1024);
-        k_group_reduce<<<blocks, 256, 0, s>>>(b, g->n, count, op == ReduceOp::Max, tmp);
+        k_group_reduce<<<blocks, 256, 0, s>>>(b, g->n, count, op == ReduceOp::Max,
+                                              g->ring ? 1 : 0, tmp);
         MMBA_HIP(hipStreamSynchronize(s));
         g->barrier();  // nobody reads a shard's buffer any more
         MMBA_HIP(hipMemcpyAsync(buf, tmp, count * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -143,6 +156,7 @@ int mmba_comm_create_local(int nranks, mmba_comm **out) {
     if (!out || nranks < 1 || nranks > LOCAL_MAX) return MMBA_ERR_INVALID;
     auto g = std::make_shared<LocalGroup>();
     g->n = nranks;
+    if (const char *e = std::getenv("MMBA_LOCAL_RING")) g->ring = std::atoi(e) != 0;
     for (int r = 0; r < nranks; ++r) {
         auto *c = new LocalComm();
         c->rank = r;

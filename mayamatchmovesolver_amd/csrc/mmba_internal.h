@@ -269,6 +269,15 @@ struct DevProblem {
     // the CF parameters of cf_rs_nb[0], then those of cf_rs_nb[1], then the
     // lens parameters.  rs_Aoff[(2 cf + d - 1) PCMAX^2]: the camera-frame
     // coupling blocks A(cf, next^d(cf)), d = 1, 2.
+    // attribute-value index of every parameter (setParameters' target;
+    // one load instead of the parameter -> attribute -> offset chain)
+    const long long *p_vidx;
+    // fast parentless bundles whose parameters are their own translate
+    // attributes: value indices of tx ty tz (w unused) and the translate
+    // component of each of the bundle's (up to 3) parameters, 2 bits each
+    // (nullptr: some fast bundle needs the transform-table walk)
+    const int4 *bnd_vx;
+    const int *bnd_pcomp;
     int rs;
     const double *obs_tau;
     const int *cf_rs_nb, *cf_rs_vidx;

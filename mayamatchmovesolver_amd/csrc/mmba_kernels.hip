@@ -87,10 +87,7 @@ __device__ __forceinline__ void param_prep_one(const DevProblem &P, int p, doubl
 }
 
 __device__ __forceinline__ void set_attr_one(const DevProblem &P, int p, double value) {
-    const int a = P.p_attr[p];
-    const int f = P.p_frame[p];
-    const int64_t idx = P.attr_off[a] + (P.attr_anim[a] ? (f < 0 ? 0 : f) : 0);
-    P.attr_val[idx] = value;
+    P.attr_val[P.p_vidx[p]] = value;
 }
 
 __global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double *ext,
@@ -171,10 +168,7 @@ __device__ __forceinline__ void cam_record_thread(const DevProblem &P, int t,
     }
     if (P.cf_aidx) {
         long long ov_idx = -1;
-        if (p >= 0) {
-            const int f = P.cf_frame[cf];
-            ov_idx = P.attr_off[ov.attr] + (P.attr_anim[ov.attr] ? (f < 0 ? 0 : f) : 0);
-        }
+        if (p >= 0) ov_idx = P.p_vidx[p];  // the variant's parameter (at this frame)
         camera_record_fast(P, cf, ov_idx, ov.value, &recs[(size_t)idx * CAMREC]);
         return;
     }
@@ -193,6 +187,28 @@ __device__ __forceinline__ void bnd_record_thread(const DevProblem &P, int b,
     const int4 p4 = P.bnd_p4[b];
     if (p4.w < 0) return;
     double *br = &brec[(size_t)b * BREC];
+    if (P.bnd_vx) {
+        // parentless: the position is (tx, ty, tz) and parameter a replaces
+        // one component (bundle_position's values, without the table walk)
+        const int4 vx = P.bnd_vx[b];
+        const double base[3] = {vx.x >= 0 ? P.attr_val[vx.x] : 0., vx.y >= 0 ? P.attr_val[vx.y] : 0.,
+                                vx.z >= 0 ? P.attr_val[vx.z] : 0.};
+        br[0] = base[0];
+        br[1] = base[1];
+        br[2] = base[2];
+        if (base_only) return;
+        const int pcm = P.bnd_pcomp[b];
+        for (int a = 0; a < p4.w; ++a) {
+            const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
+            const int comp = (pcm >> (2 * a)) & 3;
+            const double v = ext_pert[p];
+            br[3 + 3 * a] = comp == 0 ? v : base[0];
+            br[4 + 3 * a] = comp == 1 ? v : base[1];
+            br[5 + 3 * a] = comp == 2 ? v : base[2];
+            br[12 + a] = step[p];
+        }
+        return;
+    }
     const Override none{-1, 0.};
     double bp[3];
     bundle_position(P, b, 0, none, bp);  // frame-independent: any frame

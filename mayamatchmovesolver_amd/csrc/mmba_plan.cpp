@@ -930,6 +930,49 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.row_w = upload(row_w);
     D.row_var = upload(row_var);
     D.row_val = upload(row_val);
+    D.p_vidx = upload(param_vidx);
+    D.bnd_vx = nullptr;
+    D.bnd_pcomp = nullptr;
+    {
+        // fast parentless bundles: value indices of the translate and the
+        // component each parameter sets (MMBA_BND_TABLE=0 keeps the walk)
+        bool ok = nB > 0;
+        const char *e = std::getenv("MMBA_BND_TABLE");
+        if (e && std::atoi(e) == 0) ok = false;
+        std::vector<int4> vx(std::max(nB, 1), make_int4(-1, -1, -1, 0));
+        std::vector<int> pcomp(std::max(nB, 1), 0);
+        for (int b = 0; b < nB && ok; ++b) {
+            const int t = pr->bnd_tfm[b];
+            if (pr->tfm_parent[t] >= 0) {
+                ok = false;
+                break;
+            }
+            int ix[3];
+            for (int k = 0; k < 3; ++k) {
+                const int a = pr->tfm_attrs[9 * t + k];
+                if (a >= 0 && pr->attr_animated[a]) ok = false;
+                const long long v = a < 0 ? -1 : (long long)pr->attr_offset[a];
+                if (v > INT32_MAX) ok = false;
+                ix[k] = (int)v;
+            }
+            vx[b] = make_int4(ix[0], ix[1], ix[2], 0);
+            const int4 p4 = bnd_p4[b];
+            if (p4.w < 0) continue;  // generic bundle: not read through the table
+            const int ps[3] = {p4.x, p4.y, p4.z};
+            for (int a = 0; a < p4.w && ok; ++a) {
+                const int pa = pr->param_attr[ps[a]];
+                int comp = -1;
+                for (int k = 0; k < 3; ++k)
+                    if (pr->tfm_attrs[9 * t + k] == pa) comp = k;
+                if (comp < 0) ok = false;
+                else pcomp[b] |= comp << (2 * a);
+            }
+        }
+        if (ok) {
+            D.bnd_vx = upload(vx);
+            D.bnd_pcomp = upload(pcomp);
+        }
+    }
     D.rs = rs_on ? 1 : 0;
     D.obs_tau = nullptr;
     D.cf_rs_nb = nullptr;

@@ -25,11 +25,7 @@ namespace mmba {
 
 static inline int nblk_rs(long n, int bs) { return (int)((n + bs - 1) / bs); }
 
-__device__ __forceinline__ long long param_vidx(const DevProblem &P, int p) {
-    const int a = P.p_attr[p];
-    const int f = P.p_frame[p];
-    return P.attr_off[a] + (P.attr_anim[a] ? (f < 0 ? 0 : f) : 0);
-}
+__device__ __forceinline__ long long param_vidx(const DevProblem &P, int p) { return P.p_vidx[p]; }
 
 // ---------------------------------------------------------------------------
 // FD Jacobian rows (solveFunc_calculateJacobianMatrixForParameter restated per

@@ -70,10 +70,17 @@ def check_shards_agree(outs):
 SOLVES = {"bcr": "1", "partitioned": "0"}
 
 
+# summation order of the in-process all-reduce: rank order, or the ring
+# reduce-scatter order RCCL's ring all-reduce uses (mmba_comm.cpp)
+ORDERS = {"rank": "0", "ring": "1"}
+
+
+@pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("solve", list(SOLVES))
 @pytest.mark.parametrize("idx,kw,nshards", CASES)
-def test_sharded_matches_oracle(idx, kw, nshards, solve, oracle, monkeypatch):
+def test_sharded_matches_oracle(idx, kw, nshards, solve, order, oracle, monkeypatch):
     monkeypatch.setenv("MMBA_SHARD_BCR", SOLVES[solve])
+    monkeypatch.setenv("MMBA_LOCAL_RING", ORDERS[order])
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
     xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt)
@@ -143,9 +150,10 @@ def test_sharded_ba_many_shards(nshards, gpu_ctx):
         1e-3 * ref.result["error_final"]
 
 
+@pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("nshards", [2, 4, 8])
 @pytest.mark.parametrize("scene", ["c4", "wc"])
-def test_sharded_ba_x_before_the_valley(scene, nshards, gpu_ctx):
+def test_sharded_ba_x_before_the_valley(scene, nshards, order, gpu_ctx, monkeypatch):
     """x itself, on the headline C4 structure (4-frame tracks at depth
     20-200) and on the 6-frame variant, sharded against unsharded, with the
     evaluation budget capped at 2 (x0 and one full LM step): past that the
@@ -154,6 +162,7 @@ def test_sharded_ba_x_before_the_valley(scene, nshards, gpu_ctx):
     Schur / reduced solve across every shard boundary, so a wrong block, a
     missing halo term or a wrong separator shows up in x at 1e-3..1e-2; the
     bar here is 1e-6 relative on every component."""
+    monkeypatch.setenv("MMBA_LOCAL_RING", ORDERS[order])
     kw = WC if scene == "wc" else {}
     prob = S.make_config(3, frames=20 * nshards, scale=0.002 * nshards, **kw)
     opt = S.config_options(prob, iterations=2)
@@ -192,11 +201,13 @@ def test_rccl_communicator_one_rank(gpu_ctx):
         c.close()
 
 
+@pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("n", [2, 3, 8])
-def test_local_group_allreduce(n):
-    """The in-process group's all-reduce (sum in rank order, max) on n host
-    threads, each with its own stream: every rank gets the same bits, equal to
-    the rank-ordered numpy sum."""
+def test_local_group_allreduce(n, order, monkeypatch):
+    """The in-process group's all-reduce (sum in rank or ring order, max) on
+    n host threads, each with its own stream: every rank gets the same bits,
+    equal to the numpy sum in that order."""
+    monkeypatch.setenv("MMBA_LOCAL_RING", ORDERS[order])
     comms = Comm.local_group(n)
     ctxs = [Context(0) for _ in range(n)]
     rng = np.random.default_rng(7)
@@ -221,9 +232,14 @@ def test_local_group_allreduce(n):
     for c in ctxs:
         c.close()
     assert errs == [None] * n, errs
-    ref = vals[0].copy()
-    for v in vals[1:]:
-        ref = ref + v
+    cnt = vals[0].size
+    ref = np.empty(cnt)
+    for i in range(cnt):
+        r0 = (i * n // cnt + 1) % n if order == "ring" else 0
+        acc = vals[r0][i]
+        for k in range(1, n):
+            acc = acc + vals[(r0 + k) % n][i]
+        ref[i] = acc
     for s, m in outs:
         np.testing.assert_array_equal(s, ref)
         np.testing.assert_array_equal(m, np.max(np.stack(vals), axis=0))

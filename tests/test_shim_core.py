@@ -147,4 +147,6 @@ def test_gpu_shim(which, shim, oracle):
     assert reason.value == rr.reason_number
     assert fe.value == rr.function_evals
     assert np.max(np.abs(x - xr) / np.maximum(np.abs(xr), 1e-3)) <= 1e-6
-    assert abs(np.linalg.norm(fv) - rr.error_final) <= 1e-6 * rr.error_final + 1e-12
+    # exact-fit scenes (test3) stop at ||f|| ~ 1e-7, roundoff of the initial
+    # ||f||: an absolute floor of 1e-9 ||f0|| as in test_gpu_parity.check_solve
+    assert abs(np.linalg.norm(fv) - rr.error_final) <= 1e-6 * rr.error_final + 1e-9 * trr[0]
