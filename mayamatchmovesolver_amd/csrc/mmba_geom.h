@@ -390,44 +390,163 @@ MMBA_DEV void camera_record_fast(const DevProblem &P, int cf, long long ov_idx, 
 }
 
 // Rolling shutter (mmba.h ABI 3): the camera-frame record as an observation
-// at scanline time tau sees it -- camera_record_fast with the transform's
-// translate / rotate values replaced by the 3DE exporter's three-frame blend
-// (uvtrack_format.py:186-203, end frames extrapolated as at :311-314); the
-// same operations as oracle/refcpu.c rs_blend.  The override (ov_idx,
-// ov_val) applies to every value read, the neighbouring frames' included.
-MMBA_DEV double rs_val(const DevProblem &P, int ix, long long ov_idx, double ov_val) {
-    return ix == ov_idx ? ov_val : P.attr_val[ix];
+// at scanline time tau sees it -- the transform's translate / rotate values
+// replaced by the 3DE exporter's three-frame blend (uvtrack_format.py:186-203,
+// end frames extrapolated as at :311-314; the operations of oracle/refcpu.c
+// rs_blend).  The override (ov_idx, ov_val) applies to every value read, the
+// neighbouring frames' included.
+// The same record for the FD columns of one observation, cheaper per column:
+// RsCam holds what every column shares (the camera attribute values at the
+// frame and their projection part, the translate / rotate values at f - 1, f,
+// f + 1 with their value indices); rs_record then forms a column's record
+// from the overridden values with the rigid inverse of T R S (the 3 x 3 block
+// inverted as S^-1 R^T, the translation as -S^-1 R^T t) and only the non-zero
+// entries of the projection (rows 0, 1, 3 of P C^-1).  Equal to
+// camera_record_fast's arithmetic up to roundoff: the reference's general
+// 4 x 4 inverse (oracle/refcpu.c) rounds differently, so RS residuals match
+// the oracle to ~1e-15 relative, not bit for bit.
+struct RsCam {
+    int c, roo;
+    int ix[7];              // value indices of the 7 camera attributes (-1: default)
+    int tx[6], px[6], nx[6];  // translate / rotate value indices at f, f - 1, f + 1
+    double cam[7];          // camera attribute values
+    double v[6][3];         // translate / rotate values at f - 1, f, f + 1 (raw)
+    double s[3];            // scale at f
+    double p00, p02, p11, p12, p32, sx, sy;  // projection part of the base record
+};
+
+MMBA_DEV void rs_proj(const DevProblem &P, int c, const double *cv, double &p00, double &p02,
+                      double &p11, double &p12, double &p32, double &sx, double &sy) {
+    double fbw, fbh, offx, offy, fa;
+    if (P.mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        double w_mm = cv[0] * 25.4, h_mm = cv[1] * 25.4;
+        fbw = w_mm * MM_TO_INCH;
+        fbh = h_mm * MM_TO_INCH;
+        offx = (cv[2] * 25.4) * MM_TO_INCH;
+        offy = (cv[3] * 25.4) * MM_TO_INCH;
+        fa = w_mm / h_mm;
+    } else {
+        fbw = cv[0];
+        fbh = cv[1];
+        offx = cv[2];
+        offy = cv[3];
+        fa = cv[0] / cv[1];
+    }
+    const double iw = (double)P.cam_size[2 * c], ih = (double)P.cam_size[2 * c + 1];
+    double Pm[16];
+    const int fit = P.cam_fit[c];
+    projection_matrix(P.mode, cv[4], fbw, fbh, offx, offy, iw, ih, fit, cv[5], cv[6], Pm);
+    p00 = Pm[0];
+    p02 = Pm[2];
+    p11 = Pm[5];
+    p12 = Pm[6];
+    p32 = Pm[14];
+    const double ra = iw / ih;
+    sx = 1.0;
+    sy = 1.0;
+    switch (fit) {
+        case MMBA_FILM_FIT_HORIZONTAL: sy = ra / fa; break;
+        case MMBA_FILM_FIT_VERTICAL: sx = 1.0 / (ra / fa); break;
+        case MMBA_FILM_FIT_FILL:
+            if (fa > ra) sx = fa / ra; else sy = ra / fa;
+            break;
+        case MMBA_FILM_FIT_OVERSCAN:
+            if (fa > ra) sy = ra / fa; else sx = fa / ra;
+            break;
+        default: break;
+    }
 }
 
-MMBA_DEV void camera_record_rs(const DevProblem &P, int cf, double tau, long long ov_idx,
-                               double ov_val, double *rec) {
+MMBA_DEV void rs_cam_load(const DevProblem &P, int cf, RsCam &R) {
     const int *ix = &P.cf_aidx[(size_t)CF_AIDX * cf];
-    const int *nx = &P.cf_rs_vidx[(size_t)12 * cf];
+    const int *nb = &P.cf_rs_vidx[(size_t)12 * cf];
     const double dflt[CF_AIDX] = {36.0 / 25.4, 24.0 / 25.4, 0., 0., 35.0, 10000.0, 1.0,
                                   0., 0., 0., 0., 0., 0., 1., 1., 1.};
-    double v[CF_AIDX];
+    R.c = P.cf_cam[cf];
+    R.roo = P.tfm_roo[P.cam_tfm[R.c]];
 #pragma unroll
-    for (int k = 0; k < CF_AIDX; ++k) {
-        const int a = ix[k];
-        v[k] = a < 0 ? dflt[k] : (a == ov_idx ? ov_val : P.attr_val[a]);
+    for (int k = 0; k < 7; ++k) {
+        R.ix[k] = ix[k];
+        R.cam[k] = ix[k] < 0 ? dflt[k] : P.attr_val[ix[k]];
     }
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const double cv = v[7 + k];
-        const int ip = nx[k], in = nx[6 + k];
-        double pv = ip >= 0 ? rs_val(P, ip, ov_idx, ov_val) : 0.;
-        double nv = in >= 0 ? rs_val(P, in, ov_idx, ov_val) : 0.;
-        if (ip == -2) pv = cv + (cv - nv);
-        if (in == -2) nv = cv + (cv - pv);
+        R.tx[k] = ix[7 + k];
+        R.px[k] = nb[k];
+        R.nx[k] = nb[6 + k];
+        R.v[k][1] = ix[7 + k] < 0 ? 0. : P.attr_val[ix[7 + k]];
+        R.v[k][0] = nb[k] >= 0 ? P.attr_val[nb[k]] : 0.;
+        R.v[k][2] = nb[6 + k] >= 0 ? P.attr_val[nb[6 + k]] : 0.;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) R.s[k] = ix[13 + k] < 0 ? 1. : P.attr_val[ix[13 + k]];
+    rs_proj(P, R.c, R.cam, R.p00, R.p02, R.p11, R.p12, R.p32, R.sx, R.sy);
+}
+
+MMBA_DEV void rs_record(const DevProblem &P, const RsCam &R, double tau, long long ov_idx,
+                        double ov_val, double *rec) {
+    // projection part: recomputed only when a camera attribute is the override
+    double p00 = R.p00, p02 = R.p02, p11 = R.p11, p12 = R.p12, p32 = R.p32, sx = R.sx, sy = R.sy;
+    bool cam_ov = false;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) cam_ov |= R.ix[k] >= 0 && R.ix[k] == ov_idx;
+    if (cam_ov) {
+        double cv[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) cv[k] = (R.ix[k] >= 0 && R.ix[k] == ov_idx) ? ov_val : R.cam[k];
+        rs_proj(P, R.c, cv, p00, p02, p11, p12, p32, sx, sy);
+    }
+    // blended translate / rotate (rs_blend of oracle/refcpu.c)
+    double b6[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const double cv = (R.tx[k] >= 0 && R.tx[k] == ov_idx) ? ov_val : R.v[k][1];
+        double pv = (R.px[k] >= 0 && R.px[k] == ov_idx) ? ov_val : R.v[k][0];
+        double nv = (R.nx[k] >= 0 && R.nx[k] == ov_idx) ? ov_val : R.v[k][2];
+        if (R.px[k] == -2) pv = cv + (cv - nv);
+        if (R.nx[k] == -2) nv = cv + (cv - pv);
         const double b = (nv - pv) / 2.0;
         const double c = -cv + ((nv + pv) / 2.0);
-        v[7 + k] = (cv + tau * b) + (tau * tau) * c;
+        b6[k] = (cv + tau * b) + (tau * tau) * c;
     }
-    const int c = P.cf_cam[cf];
     double W[16];
-    trs_matrix(v[7], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15],
-               P.tfm_roo[P.cam_tfm[c]], W);
-    camera_record_tail(P, c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], W, rec);
+    trs_matrix(b6[0], b6[1], b6[2], b6[3], b6[4], b6[5], R.s[0], R.s[1], R.s[2], R.roo, W);
+    // C^-1 of W = T R S: rows k = (R S)^-1 = S^-1 R^T, column 3 = -S^-1 R^T t
+    double Ci[12];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) Ci[k * 4 + r] = (W[r * 4 + k] / R.s[k]) / R.s[k];
+        Ci[k * 4 + 3] = -(Ci[k * 4 + 0] * W[3] + Ci[k * 4 + 1] * W[7] + Ci[k * 4 + 2] * W[11]);
+    }
+    // rows 0, 1, 3 of P C^-1 (P: p00 / p02 in row 0, p11 / p12 in row 1, p32
+    // in row 3; row 3 of C^-1 is 0 0 0 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rec[k] = p00 * Ci[k] + p02 * Ci[8 + k];
+        rec[4 + k] = p11 * Ci[4 + k] + p12 * Ci[8 + k];
+        rec[8 + k] = p32 * Ci[8 + k];
+    }
+    rec[12] = W[3];
+    rec[13] = W[7];
+    rec[14] = W[11];
+    const double cdir[3] = {-W[2], -W[6], -W[10]};
+    const double cl = sqrt(cdir[0] * cdir[0] + cdir[1] * cdir[1] + cdir[2] * cdir[2]);
+    rec[15] = cdir[0] / cl;
+    rec[16] = cdir[1] / cl;
+    rec[17] = cdir[2] / cl;
+    rec[18] = sx;
+    rec[19] = sy;
+}
+
+// One observation's record at scanline time tau (residual / reprojection
+// kernels): the same arithmetic as the FD columns of k_jacobian_rs, so fvec
+// and the Jacobian's base point agree bit for bit.
+MMBA_DEV void camera_record_rs(const DevProblem &P, int cf, double tau, long long ov_idx,
+                               double ov_val, double *rec) {
+    RsCam R;
+    rs_cam_load(P, cf, R);
+    rs_record(P, R, tau, ov_idx, ov_val, rec);
 }
 
 // ---- LDPK classic 3DE model (undistort polynomial + fixed-point inverse) ----

@@ -281,6 +281,10 @@ struct DevProblem {
     int rs;
     const double *obs_tau;
     const int *cf_rs_nb, *cf_rs_vidx;
+    // per camera-frame: the global-parameter columns of its observations'
+    // Jacobian rows (same for every observation of the segment): count, then
+    // (column, global index) pairs, NGMAX slots each
+    const int *cf_rs_gcnt, *cf_rs_gcol, *cf_rs_gidx;
     double *rs_Aoff;
 };
 

@@ -297,13 +297,30 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             p_class[p] = PC_G;
         }
     }
-    // number the camera-frames (camera-major, frame-minor)
+    // number the camera-frames: frame-major (the keys' order), so a bundle
+    // tracked over a window of frames couples a contiguous band; with a
+    // rolling shutter and no solved bundle, camera-major instead: the
+    // coupling is then only between a camera's consecutive frames, and the
+    // band is 3 camera-frame blocks wide whatever the number of cameras
+    // (C5-RS: half bandwidth 17 instead of 29)
     ncf = 0;
     std::vector<int> cf_cam, cf_frame;
-    for (auto &kv : cf_id) {
-        kv.second = ncf++;
-        cf_frame.push_back(kv.first.first);
-        cf_cam.push_back(kv.first.second);
+    {
+        bool any_b = false;
+        for (int p = 0; p < n && !any_b; ++p) any_b = p_class[p] == PC_B;
+        std::vector<std::pair<int, int>> keys;
+        for (auto &kv : cf_id) keys.push_back(kv.first);
+        if (rs_on && !any_b)
+            std::stable_sort(keys.begin(), keys.end(),
+                             [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
+                                 return a.second != b.second ? a.second < b.second
+                                                             : a.first < b.first;
+                             });
+        for (auto &k : keys) {
+            cf_id[k] = ncf++;
+            cf_frame.push_back(k.first);
+            cf_cam.push_back(k.second);
+        }
     }
     // CF blocks
     std::vector<std::vector<int>> cf_params(ncf);
@@ -977,6 +994,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.obs_tau = nullptr;
     D.cf_rs_nb = nullptr;
     D.cf_rs_vidx = nullptr;
+    D.cf_rs_gcnt = D.cf_rs_gcol = D.cf_rs_gidx = nullptr;
     D.rs_Aoff = nullptr;
     if (rs_on) {
         if (!D.cf_aidx) throw Unsupported{"rolling shutter needs the camera-frame table"};
@@ -1002,6 +1020,35 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             }
         }
         D.cf_rs_vidx = upload(vx);
+        // the global columns of each segment's rows, in k_jacobian_rs's
+        // column order: variants (CF params, camera-side globals), the
+        // neighbours' CF params, the lens params reaching the frame
+        std::vector<int> gcnt(std::max(ncf, 1), 0), gcol((size_t)NGMAX * std::max(ncf, 1), -1),
+            gidx((size_t)NGMAX * std::max(ncf, 1), -1);
+        for (int cf = 0; cf < ncf; ++cf) {
+            std::vector<int> cols;
+            for (int v = cf_var_off[cf] + 1; v < cf_var_off[cf + 1]; ++v) cols.push_back(cf_var_param[v]);
+            for (int side = 0; side < 2; ++side) {
+                const int cn = cf_nb[2 * cf + side];
+                if (cn >= 0)
+                    for (int p : cf_params[cn]) cols.push_back(p);
+            }
+            const int c = cf_cam[cf], f = cf_frame[cf];
+            for (int q = cam_lpar_off[c]; q < cam_lpar_off[c + 1]; ++q) {
+                const int p = cam_lpar[q];
+                if (pr->param_frame[p] >= 0 && pr->param_frame[p] != f) continue;
+                cols.push_back(p);
+            }
+            for (int l = 0; l < (int)cols.size() && l < LMAX; ++l)
+                if (p_class[cols[l]] == PC_G && gcnt[cf] < NGMAX) {
+                    gcol[(size_t)NGMAX * cf + gcnt[cf]] = l;
+                    gidx[(size_t)NGMAX * cf + gcnt[cf]] = p_pos[cols[l]] - nCF;
+                    ++gcnt[cf];
+                }
+        }
+        D.cf_rs_gcnt = upload(gcnt);
+        D.cf_rs_gcol = upload(gcol);
+        D.cf_rs_gidx = upload(gidx);
         D.rs_Aoff = dalloc<double>((size_t)2 * ncf * PCMAX * PCMAX);
         MMBA_HIP(hipMemsetAsync(D.rs_Aoff, 0, sizeof(double) * 2 * ncf * PCMAX * PCMAX, s));
     }

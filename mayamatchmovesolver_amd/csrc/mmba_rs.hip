@@ -23,6 +23,10 @@
 
 namespace mmba {
 
+#ifndef MMBA_RS_WAVES
+#define MMBA_RS_WAVES 1
+#endif
+
 static inline int nblk_rs(long n, int bs) { return (int)((n + bs - 1) / bs); }
 
 __device__ __forceinline__ long long param_vidx(const DevProblem &P, int p) { return P.p_vidx[p]; }
@@ -35,7 +39,13 @@ __device__ __forceinline__ long long param_vidx(const DevProblem &P, int p) { re
 // rotate values leaves the observation unchanged: its entry is exactly 0
 // (what f(x + d e_p) - f(x) gives), written without an evaluation.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) k_jacobian_rs(DevProblem P, const double *__restrict__ ext_pert,
+// The columns are listed first (parameter, kind), then evaluated by one code
+// site: kind 0 = a camera-side value (this frame or a blended neighbour),
+// 1 = a neighbouring frame's parameter the blend does not read (entry 0,
+// no evaluation), 2 = a lens coefficient.  One evaluation site keeps the
+// inlined record + lens code (the register-heavy part) once.
+template <int TPB>
+__global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P, const double *__restrict__ ext_pert,
                                                      const double *__restrict__ step,
                                                      int solver_type, double *J, int *jcol,
                                                      int *nloc, const int *__restrict__ stale_param,
@@ -52,70 +62,95 @@ __global__ void __launch_bounds__(128) k_jacobian_rs(DevProblem P, const double 
     const Override none{-1, 0.};
     double bp0[3];
     base_bundle(P, b, fr, bp0);
-    double lc0[MMBA_LENS_NUM_ATTRS];
     int lens = -1;
     const int hl = obs_lens(P, cam, lens);
-    if (hl) lens_coeffs(P, lens, fr, none, lc0);
-    double rec[CAMREC];
-    camera_record_rs(P, cf, tau, -1, 0., rec);
-    const Resid r0 = residual_l(P, rec, bp0, mx, my, sw, hl, lc0);
-    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
-    const int pstale = stale_param[fr];
-    Resid rs = r0;
-    int l = 0;
-    auto emit = [&](int p, double jx, double jy) {
-        J[(size_t)(2 * l) * M + i] = jx;
-        J[(size_t)(2 * l + 1) * M + i] = jy;
-        jcol[(size_t)l * M + i] = p;
-        ++l;
-    };
-    auto fd = [&](int p, const Resid &r) {
-        const double st = step[p];
-        if (p == pstale) rs = r;
-        if (lmder)  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
-            emit(p, (r.ex - r0.ex) * st, (r.ey - r0.ey) * st);
-        else        // st = h, divided (fdjac2)
-            emit(p, (r.ex - r0.ex) / st, (r.ey - r0.ey) / st);
-    };
-    auto cam_col = [&](int p) {
-        camera_record_rs(P, cf, tau, param_vidx(P, p), ext_pert[p], rec);
-        fd(p, residual_l(P, rec, bp0, mx, my, sw, hl, lc0));
-    };
-    // this camera-frame's variants (its CF parameters, camera-side globals)
+    // the column list
+    int cp[LMAX];
+    unsigned char ck[LMAX];
+    int nl = 0;
     const int voff = P.cf_var_off[cf];
     const int nvar = P.cf_var_off[cf + 1] - voff;
-    for (int v = 1; v < nvar && l < LMAX; ++v) cam_col(P.cf_var_param[voff + v]);
-    // the neighbouring frames' CF parameters
+    for (int v = 1; v < nvar && nl < LMAX; ++v) {
+        cp[nl] = P.cf_var_param[voff + v];
+        ck[nl++] = 0;
+    }
     const int *nx = &P.cf_rs_vidx[(size_t)12 * cf];
     for (int side = 0; side < 2; ++side) {
         const int cn = P.cf_rs_nb[2 * cf + side];
         if (cn < 0) continue;
         const int vo = P.cf_var_off[cn] + 1;
-        for (int a = 0; a < P.cf_pc[cn] && l < LMAX; ++a) {
+        for (int a = 0; a < P.cf_pc[cn] && nl < LMAX; ++a) {
             const int p = P.cf_var_param[vo + a];
             const long long vi = param_vidx(P, p);
             bool blended = false;
 #pragma unroll
             for (int k = 0; k < 6; ++k) blended |= nx[6 * side + k] == vi;
-            if (blended) {
-                cam_col(p);
-            } else {
-                emit(p, 0., 0.);  // f(x + d e_p) = f(x): the column's entry is 0
-            }
+            cp[nl] = p;
+            ck[nl++] = blended ? 0 : 1;
         }
     }
-    // lens parameters of this camera's lens
-    if (hl) {
-        camera_record_rs(P, cf, tau, -1, 0., rec);
-        for (int q = P.cam_lpar_off[cam]; q < P.cam_lpar_off[cam + 1] && l < LMAX; ++q) {
+    if (hl)
+        for (int q = P.cam_lpar_off[cam]; q < P.cam_lpar_off[cam + 1] && nl < LMAX; ++q) {
             const int p = P.cam_lpar[q];
             if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
-            double lc[MMBA_LENS_NUM_ATTRS];
-            lens_coeffs(P, lens, fr, Override{P.p_attr[p], ext_pert[p]}, lc);
-            fd(p, residual_l(P, rec, bp0, mx, my, sw, hl, lc));
+            cp[nl] = p;
+            ck[nl++] = 2;
         }
+    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
+    const int pstale = stale_param[fr];
+    RsCam RC;
+    rs_cam_load(P, cf, RC);
+    // the lens coefficients at x once; a lens column replaces its slot(s)
+    // (lens_coeffs with the override, without re-reading the table)
+    double lc0[MMBA_LENS_NUM_ATTRS];
+    int la[MMBA_LENS_NUM_ATTRS];
+    int ltype = MMBA_LENS_NONE;
+    if (hl) {
+        lens_coeffs(P, lens, fr, none, lc0);
+        ltype = P.lens_type[lens];
+#pragma unroll
+        for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) la[k] = P.lens_attrs[MMBA_LENS_NUM_ATTRS * lens + k];
     }
-    nloc[i] = l;
+    // column -1: the base point; then every column that needs an evaluation
+    Resid r0{}, rs{};
+    for (int l = -1; l < nl; ++l) {
+        const int kind = l < 0 ? 0 : ck[l];
+        const int p = l < 0 ? -1 : cp[l];
+        double jx = 0., jy = 0.;
+        if (kind != 1) {
+            double rec[CAMREC];
+            rs_record(P, RC, tau, kind == 0 && p >= 0 ? param_vidx(P, p) : -1,
+                      p >= 0 ? ext_pert[p] : 0., rec);
+            double lc[MMBA_LENS_NUM_ATTRS];
+            if (hl) {
+                const int oa = kind == 2 ? P.p_attr[p] : -2;
+                const double ov = kind == 2 ? ext_pert[p] : 0.;
+#pragma unroll
+                for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
+                    lc[k] = (la[k] >= 0 && la[k] == oa) ? ov : lc0[k];
+                if (ltype == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) lc[13] = 1.;  // lens_coeffs' rule
+            }
+            const Resid r = residual_l(P, rec, bp0, mx, my, sw, hl, lc);
+            if (l < 0) {
+                r0 = r;
+                rs = r;
+                continue;
+            }
+            if (p == pstale) rs = r;
+            const double st = step[p];
+            if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
+                jx = (r.ex - r0.ex) * st;
+                jy = (r.ey - r0.ey) * st;
+            } else {      // st = h, divided (fdjac2)
+                jx = (r.ex - r0.ex) / st;
+                jy = (r.ey - r0.ey) / st;
+            }
+        }
+        J[(size_t)(2 * l) * M + i] = jx;
+        J[(size_t)(2 * l + 1) * M + i] = jy;
+        jcol[(size_t)l * M + i] = p;
+    }
+    nloc[i] = nl;
     // errorList / errorDistanceList as left by the last FD column (B13)
     if (eu) {
         eu[2 * i] = rs.ux;
@@ -150,7 +185,9 @@ __global__ void __launch_bounds__(256) k_ne_rs(DevProblem P, const double *__res
                                                const int *__restrict__ nloc,
                                                const double *__restrict__ f, double *Acc,
                                                double *Acg, double *g, double *Aoff) {
-    __shared__ double sJ[2 * LMAX][RS_CHUNK];
+    // rows padded to RS_CHUNK + 1: the threads of a wave read different rows
+    // at one column (a 512-B row stride put them all on one LDS bank)
+    __shared__ double sJ[2 * LMAX][RS_CHUNK + 1];
     __shared__ int sG[NGMAX][RS_CHUNK];
     __shared__ double sF[2][RS_CHUNK];
     const int cf = blockIdx.x / 3, d = blockIdx.x % 3;
@@ -264,6 +301,140 @@ __global__ void __launch_bounds__(256) k_ne_rs(DevProblem P, const double *__res
     }
 }
 
+// Uniform block size PC and at most NG global parameters: the same blocks
+// with per-lane accumulators (lane o takes the segment's observations o, o +
+// 256, ...), a fixed xor-shuffle tree per wave and the 4 wave sums added in
+// wave order -- deterministic, no LDS staging of J.  The global columns of an
+// observation are its camera-side globals (variant columns pc .. nvar) and
+// its lens columns (after the neighbours' blocks), found through jcol.
+template <int PC, int NG>
+__global__ void __launch_bounds__(256) k_ne_rs_u(DevProblem P, const double *__restrict__ J,
+                                                 const int *__restrict__ jcol,
+                                                 const int *__restrict__ nloc,
+                                                 const double *__restrict__ f, double *Acc,
+                                                 double *Acg, double *g, double *Aoff) {
+    constexpr int NCC = PC * (PC + 1) / 2, N0 = NCC + PC + PC * NG, N1 = PC * PC;
+    constexpr int NA = N0 > N1 ? N0 : N1;
+    __shared__ double wsum[4][NA];
+    const int cf = blockIdx.x / 3, d = blockIdx.x % 3;
+    if (P.cf_pc[cf] != PC) return;
+    const int n1 = P.cf_rs_nb[2 * cf + 1];
+    int B = cf;
+    if (d >= 1) B = n1;
+    if (d == 2 && B >= 0) B = P.cf_rs_nb[2 * B + 1];
+    if (B < 0 || P.cf_pc[B] != PC) return;
+    const size_t M = P.M;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double acc[NA];
+#pragma unroll
+    for (int e = 0; e < NA; ++e) acc[e] = 0.;
+    int segs[3] = {-1, -1, -1};
+    if (d == 0) {
+        segs[0] = P.cf_rs_nb[2 * cf];
+        segs[1] = cf;
+        segs[2] = n1;
+    } else if (d == 1) {
+        segs[0] = cf;
+        segs[1] = n1;
+    } else {
+        segs[0] = n1;
+    }
+    for (int q = 0; q < 3; ++q) {
+        const int sg = segs[q];
+        if (sg < 0) continue;
+        const int oA = rs_block_off(P, sg, cf), oB = rs_block_off(P, sg, B);
+        // this segment's global columns (the same for all its observations)
+        int gl[NG > 0 ? NG : 1], gi[NG > 0 ? NG : 1];
+        const int ngc = NG > 0 ? min(P.cf_rs_gcnt[sg], NG) : 0;
+#pragma unroll
+        for (int t = 0; t < (NG > 0 ? NG : 1); ++t) {
+            gl[t] = t < ngc ? P.cf_rs_gcol[(size_t)NGMAX * sg + t] : 0;
+            gi[t] = t < ngc ? P.cf_rs_gidx[(size_t)NGMAX * sg + t] : -1;
+        }
+        const int o0 = P.cf_obs_off[sg], o1 = P.cf_obs_off[sg + 1];
+        for (int i = o0 + tid; i < o1; i += 256) {
+            double ax[PC], ay[PC];
+#pragma unroll
+            for (int a = 0; a < PC; ++a) {
+                ax[a] = J[(size_t)(2 * (oA + a)) * M + i];
+                ay[a] = J[(size_t)(2 * (oA + a) + 1) * M + i];
+            }
+            if (d != 0) {
+                double bx[PC], by[PC];
+#pragma unroll
+                for (int c = 0; c < PC; ++c) {
+                    bx[c] = J[(size_t)(2 * (oB + c)) * M + i];
+                    by[c] = J[(size_t)(2 * (oB + c) + 1) * M + i];
+                }
+#pragma unroll
+                for (int a = 0; a < PC; ++a)
+#pragma unroll
+                    for (int c = 0; c < PC; ++c) acc[a * PC + c] += ax[a] * bx[c] + ay[a] * by[c];
+                continue;
+            }
+            const double fx = f[2 * i], fy = f[2 * i + 1];
+            int e = 0;
+#pragma unroll
+            for (int a = 0; a < PC; ++a)
+#pragma unroll
+                for (int c = a; c < PC; ++c) acc[e++] += ax[a] * ax[c] + ay[a] * ay[c];
+#pragma unroll
+            for (int a = 0; a < PC; ++a) acc[NCC + a] += ax[a] * fx + ay[a] * fy;
+            if constexpr (NG > 0) {
+                double gx[NG], gy[NG];
+#pragma unroll
+                for (int t = 0; t < NG; ++t) gx[t] = gy[t] = 0.;
+#pragma unroll
+                for (int t = 0; t < NG; ++t) {
+                    if (t >= ngc) break;
+                    const int l = gl[t];
+                    const double ux = J[(size_t)(2 * l) * M + i], uy = J[(size_t)(2 * l + 1) * M + i];
+#pragma unroll
+                    for (int u = 0; u < NG; ++u) {
+                        gx[u] = (gi[t] == u) ? ux : gx[u];
+                        gy[u] = (gi[t] == u) ? uy : gy[u];
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < PC; ++a)
+#pragma unroll
+                    for (int t = 0; t < NG; ++t) acc[NCC + PC + a * NG + t] += ax[a] * gx[t] + ay[a] * gy[t];
+            }
+        }
+    }
+    const int ne = d == 0 ? N0 : N1;
+#pragma unroll
+    for (int e = 0; e < NA; ++e) {
+        double v = acc[e];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) wsum[wv][e] = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < ne; e += 256) {
+        const double v = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
+        if (d != 0) {
+            Aoff[(size_t)(2 * cf + d - 1) * PCMAX * PCMAX + (e / PC) * PCMAX + e % PC] = v;
+        } else if (e < NCC) {
+            int a = 0, rem = e;
+            while (rem >= PC - a) {
+                rem -= PC - a;
+                ++a;
+            }
+            const int c = a + rem;
+            double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
+            A[a * PCMAX + c] = v;
+            A[c * PCMAX + a] = v;
+        } else if (e < NCC + PC) {
+            g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
+        } else {
+            constexpr int NGd = NG > 0 ? NG : 1;
+            const int a = (e - NCC - PC) / NGd, t = (e - NCC - PC) % NGd;
+            if (t < P.nG) Acg[((size_t)cf * PCMAX + a) * NGMAX + t] = v;
+        }
+    }
+}
+
 // The coupling blocks into the reduced system (after k_schur_init):
 // S(roff(B) + b, roff(cf) + a) = A(cf, B)_ab, B = next^d(cf), d = 1, 2.
 __global__ void __launch_bounds__(256) k_rs_offdiag(DevProblem P, const double *__restrict__ Aoff,
@@ -287,13 +458,22 @@ __global__ void __launch_bounds__(256) k_rs_offdiag(DevProblem P, const double *
 void launch_jacobian_rs(hipStream_t s, const DevProblem &P, const double *ext_pert,
                         const double *step, int solver_type, double *J, int *jcol, int *nloc,
                         const int *stale_param, double *eu, double *ed) {
-    k_jacobian_rs<<<nblk_rs(P.M, 128), 128, 0, s>>>(P, ext_pert, step, solver_type, J, jcol, nloc,
-                                                    stale_param, eu, ed);
+    k_jacobian_rs<64><<<nblk_rs(P.M, 64), 64, 0, s>>>(P, ext_pert, step, solver_type, J, jcol,
+                                                      nloc, stale_param, eu, ed);
 }
 
 void launch_ne_rs(hipStream_t s, const DevProblem &P, const double *J, const int *jcol,
                   const int *nloc, const double *f, double *Acc, double *Acg, double *g) {
-    if (P.ncf > 0) k_ne_rs<<<3 * P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, P.rs_Aoff);
+    if (P.ncf == 0) return;
+    const int pcu = P.pc_uniform;
+    if (pcu == 6 && P.nG == 0)
+        k_ne_rs_u<6, 0><<<3 * P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, P.rs_Aoff);
+    else if (pcu == 6 && P.nG <= 2)
+        k_ne_rs_u<6, 2><<<3 * P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, P.rs_Aoff);
+    else if (pcu == 6 && P.nG <= 4)
+        k_ne_rs_u<6, 4><<<3 * P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, P.rs_Aoff);
+    else
+        k_ne_rs<<<3 * P.ncf, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, P.rs_Aoff);
 }
 
 void launch_rs_offdiag(hipStream_t s, const DevProblem &P, const SView &V) {
