@@ -426,6 +426,16 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out,
                     mmba_result *res, const mmba_callbacks *cb,
                     mmba_trace *trace);
 
+/* Outputs of the plan's last mmba_plan_solve / mmba_plan_measure, kept in
+ * HBM: a caller that solves with NULL output pointers (device-resident
+ * results) fetches errorList / ud->errorList / errorDistanceList here, in
+ * the same layouts as mmba_plan_solve's.  MMBA_ERR_INVALID when the last
+ * call on the plan was neither (reproject, jacobian and per-frame solves
+ * overwrite the buffers).  Sharded plans: a collective, like the solve.  Any
+ * output may be NULL. */
+int mmba_plan_outputs(mmba_plan *plan, double *fvec_out, double *err_user_out,
+                      double *err_dist_out);
+
 /* Per-frame solve mode (FrameSolveMode::kPerFrame, adjust_base.cpp:1430-1484):
  * one solveFrames per frame over that frame's observations and the
  * parameters keyed at it plus every static parameter; results[num_frames]

@@ -83,6 +83,8 @@ def lib():
         L.mmba_plan_solve.restype = C.c_int
         L.mmba_plan_solve.argtypes = [C.c_void_p, dp, dp, dp, dp, C.POINTER(abi.MmbaResult),
                                       C.POINTER(abi.MmbaCallbacks), C.POINTER(abi.MmbaTrace)]
+        L.mmba_plan_outputs.restype = C.c_int
+        L.mmba_plan_outputs.argtypes = [C.c_void_p, dp, dp, dp]
         L.mmba_solve.restype = C.c_int
         L.mmba_solve.argtypes = [C.c_void_p, C.POINTER(abi.MmbaProblem),
                                  C.POINTER(abi.MmbaOptions), dp, dp, dp, dp,

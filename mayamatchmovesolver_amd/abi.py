@@ -231,6 +231,7 @@ EXPORTED_SYMBOLS = [
     "mmba_plan_set_attr_values",
     "mmba_plan_jacobian",
     "mmba_plan_solve",
+    "mmba_plan_outputs",
     "mmba_solve",
     "mmba_plan_kernel_stats",
     "mmba_debug_band_solve",

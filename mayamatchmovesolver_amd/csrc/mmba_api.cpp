@@ -188,7 +188,11 @@ int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out, double
     if (!plan) return MMBA_ERR_INVALID;
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
-        return plan->impl.measure(x, fvec_out, err_user_out, err_dist_out, avg_min_max_out);
+        plan->impl.outputs_ready = false;
+        const int rc =
+            plan->impl.measure(x, fvec_out, err_user_out, err_dist_out, avg_min_max_out);
+        plan->impl.outputs_ready = rc == MMBA_OK;
+        return rc;
     })
 }
 
@@ -197,6 +201,7 @@ int mmba_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
     if (!plan) return MMBA_ERR_INVALID;
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        plan->impl.outputs_ready = false;
         return plan->impl.reproject(x, point_xy_out, marker_xy_out);
     })
 }
@@ -205,6 +210,7 @@ int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac) {
     if (!plan || !x || !fjac) return MMBA_ERR_INVALID;
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        plan->impl.outputs_ready = false;
         return plan->impl.dense_jacobian(x, fjac);
     })
 }
@@ -215,7 +221,23 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *
     if (!plan || !x_inout) return MMBA_ERR_INVALID;
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
-        return plan->impl.solve(x_inout, fvec_out, err_user_out, err_dist_out, res, cb, trace);
+        plan->impl.outputs_ready = false;
+        const int rc =
+            plan->impl.solve(x_inout, fvec_out, err_user_out, err_dist_out, res, cb, trace);
+        plan->impl.outputs_ready = rc == MMBA_OK || rc == MMBA_ERR_INTERRUPTED;
+        return rc;
+    })
+}
+
+int mmba_plan_outputs(mmba_plan *plan, double *fvec_out, double *err_user_out,
+                      double *err_dist_out) {
+    if (!plan || !plan->impl.outputs_ready) return MMBA_ERR_INVALID;
+    MMBA_GUARD({
+        Plan &p = plan->impl;
+        MMBA_HIP(hipSetDevice(p.ctx->device));
+        if (fvec_out || err_user_out || err_dist_out)
+            p.download_ref_order(p.d_f, p.d_eu, p.d_ed, fvec_out, err_user_out, err_dist_out);
+        return MMBA_OK;
     })
 }
 
@@ -237,6 +259,7 @@ int mmba_plan_solve_per_frame(mmba_plan *plan, double *x_inout, mmba_result *res
     if (!plan || !x_inout || !results) return MMBA_ERR_INVALID;
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
+        plan->impl.outputs_ready = false;
         return plan->impl.solve_frames(x_inout, results, cb);
     })
 }

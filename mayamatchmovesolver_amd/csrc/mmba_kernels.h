@@ -24,14 +24,15 @@ struct RedSpec {
     RedRow row[8];
 };
 void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
-                         double *scalar, int *flag = nullptr);
+                         double *scalar, int *flag = nullptr, double *host = nullptr,
+                         int host_n = 0, unsigned *ticket = nullptr);
 // lmder bookkeeping after the normal equations (column norms, rank test, diag
 // update, ||D x||, gnorm): partial rows 0 / 1 / 2 (rstride apart, nparts each)
 void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
                          const double *Abb, const double *aggbuf, double *acnorm, double *g,
                          double *diag, const double *x, int first, int mode, double fnorm,
-                         int do_xn, int do_gn, const int *mask, double *partial, int nparts,
-                         int rstride);
+                         const double *fnorm_sq, int do_xn, int do_gn, const int *mask,
+                         double *partial, int nparts, int rstride);
 // lmder trial point x - xs with setParameters at it; partial rows 0 (pnorm^2)
 // and 1 (||D x_new||^2)
 void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
@@ -98,6 +99,7 @@ struct NeEpi {
     int on = 0;
     int first = 0, mode = 1, do_xn = 0, do_gn = 0;
     double fnorm = 0.;
+    const double *fnorm_sq = nullptr;  // non-null: fnorm = sqrt(*fnorm_sq) (device slot)
     const double *x = nullptr;
     double *diag = nullptr, *acnorm = nullptr, *partial = nullptr;
     int rstride = 0, cf_base = 0, bnd_base = 0;
@@ -143,10 +145,18 @@ void launch_trsv_bwd_all(hipStream_t s, const double *S, const int *slot, int NT
                          double *x);
 // Returns true when the right-hand side update rhs_R -= sum W_i t_b(i) was
 // fused into the diagonal destinations (uniform path; else launch_schur_rhs).
+// k_schur_init's camera-frame rows folded into the diagonal destinations
+// (unsharded, nG == 0, every solved camera-frame has a diagonal destination):
+// those blocks are assigned Acc + lam D^2 - sum W W^T and rhs = g - sum W t.
+struct SchurInitFold {
+    int on;
+    const double *Acc, *g, *diag;
+    double lam;
+};
 bool launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
                        int pc_uniform, int assign_off, const double *tb = nullptr,
-                       double *rhs = nullptr);
+                       double *rhs = nullptr, SchurInitFold fold = SchurInitFold{});
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs);
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,

@@ -752,7 +752,12 @@ __device__ __forceinline__ void epi_param(const NeEpi &E, int p, double d, doubl
         const double v = dg * E.x[p];
         xn += v * v;
     }
-    if (E.do_gn && an != 0.) gm = fmax(gm, fabs((gp / E.fnorm) / an));
+    if (E.do_gn && an != 0.) {
+        // a device-side ||f||^2 (first Jacobian): gnorm only when ||f|| != 0,
+        // as lmder decides on the host otherwise
+        const double fn = E.fnorm_sq ? sqrt(*E.fnorm_sq) : E.fnorm;
+        if (fn != 0.) gm = fmax(gm, fabs((gp / fn) / an));
+    }
 }
 
 __device__ __forceinline__ void epi_store(const NeEpi &E, int col, double zf, double xn,
@@ -1221,9 +1226,14 @@ __device__ __forceinline__ void block_partial(double v, double *red, double *par
 __global__ void __launch_bounds__(256) k_jac_epilogue(
     DevProblem P, const double *__restrict__ Acc, const double *__restrict__ Abb,
     const double *__restrict__ Agg, const double *__restrict__ gG, double *acnorm, double *g,
-    double *diag, const double *__restrict__ x, int first, int mode, double fnorm, int do_xn,
-    int do_gn, const int *__restrict__ mask, double *partial, int rstride) {
+    double *diag, const double *__restrict__ x, int first, int mode, double fnorm,
+    const double *__restrict__ fnorm_sq, int do_xn, int do_gn, const int *__restrict__ mask,
+    double *partial, int rstride) {
     __shared__ double red[256];
+    if (fnorm_sq) {
+        fnorm = sqrt(*fnorm_sq);
+        do_gn = do_gn && fnorm != 0.;
+    }
     double zf = 0., xn = 0., gm = 0.;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.n; p += gridDim.x * blockDim.x) {
         const int cls = P.p_class[p];
@@ -1304,8 +1314,13 @@ __global__ void __launch_bounds__(256) k_trial_prep(
 // Several partial rows reduced in one launch, block r for row r, in the
 // order of k_reduce_sum / k_reduce_max; block 0 also converts the
 // factorisation fail flag to a scalar and clears it (k_flag_to_scalar).
+// host (optional): the last block to finish copies scalar[0, host_n) into
+// that page-locked host mirror (the LM control thread's slots), so the
+// decision point needs no separate device-to-host copy launch.
 __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__ partial,
-                                                      RedSpec spec, double *scalar, int *flag) {
+                                                      RedSpec spec, double *scalar, int *flag,
+                                                      double *host, int host_n,
+                                                      unsigned *ticket) {
     __shared__ double red[256];
     const RedRow rw = spec.row[blockIdx.x];
     const bool mx = rw.is_max != 0;
@@ -1329,6 +1344,21 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
             *flag = 0;
         }
     }
+    if (!host) return;
+    __shared__ unsigned last;
+    if (threadIdx.x == 0) {
+        // release this block's slots, count it in; the last arrival acquires
+        // every block's slots (agent scope: the blocks may sit on other XCDs)
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int i = threadIdx.x; i < host_n; i += blockDim.x)
+        host[i] = __hip_atomic_load(&scalar[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // -------------------------------------------------------------------------
@@ -1685,7 +1715,8 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
                                                      const int *__restrict__ dest_off,
                                                      const int2 *__restrict__ pairs,
                                                      const SView V, int assign_off, int ndest,
-                                                     const double *__restrict__ tb, double *rhs) {
+                                                     const double *__restrict__ tb, double *rhs,
+                                                     const SchurInitFold fold) {
     // diagonal destinations (cf, cf) hold exactly the pairs (i, i) of the
     // camera-frame's observations with a bundle block, so they also form
     // rhs_R -= sum_i W_i t_b(i) (k_schur_rhs) in the same loop
@@ -1773,17 +1804,38 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
             for (int a = 0; a < PC; ++a) red[PC * PC + a][lane] += accr[a];
     }
     __syncthreads();
+    // folded k_schur_init (diagonal destinations): the entries it would have
+    // written, with its operations, then the same subtraction
+    const bool init = fold.on && cc.x == cc.y;
+    const double *Ablk = &fold.Acc[(size_t)cc.x * PCMAX * PCMAX];
+    const int v0 = P.cf_var_off[cc.x] + 1;
     for (int e = lane; e < PC * PC + (diag ? PC : 0); e += 64) {
         double v = 0.;
         for (int l = 0; l < 32; ++l) v += red[e][l];
         if (e >= PC * PC) {
-            rhs[ri + e - PC * PC] -= v;
+            const int a = e - PC * PC;
+            if (init) {
+                const double ga = fold.g[P.cf_var_param[v0 + a]];
+                rhs[ri + a] = ((Ablk[a * PCMAX + a] == 0. && fold.lam == 0.) ? 0. : ga) - v;
+            } else {
+                rhs[ri + a] -= v;
+            }
             continue;
         }
         const int a = e / PC, c = e % PC;
         if (ri + a >= rj + c) {
             double *dd = s_at(V, ri + a, rj + c);
-            *dd = (assign_off && cc.x != cc.y) ? -v : *dd - v;  // see k_schur_dest
+            if (init) {
+                double b = Ablk[a * PCMAX + c];
+                if (c == a) {
+                    const double d = fold.diag[P.cf_var_param[v0 + a]];
+                    b += fold.lam * (d * d);
+                    if (b == 0.) b = 1.;
+                }
+                *dd = b - v;
+            } else {
+                *dd = (assign_off && cc.x != cc.y) ? -v : *dd - v;  // see k_schur_dest
+            }
         }
     }
 }
@@ -2280,11 +2332,11 @@ void launch_param_set(hipStream_t s, const DevProblem &P, const double *x, doubl
 void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
                          const double *Abb, const double *aggbuf, double *acnorm, double *g,
                          double *diag, const double *x, int first, int mode, double fnorm,
-                         int do_xn, int do_gn, const int *mask, double *partial, int nparts,
-                         int rstride) {
+                         const double *fnorm_sq, int do_xn, int do_gn, const int *mask,
+                         double *partial, int nparts, int rstride) {
     k_jac_epilogue<<<nparts, 256, 0, s>>>(P, Acc, Abb, aggbuf, aggbuf + NGMAX * NGMAX, acnorm,
-                                          g, diag, x, first, mode, fnorm, do_xn, do_gn, mask,
-                                          partial, rstride);
+                                          g, diag, x, first, mode, fnorm, fnorm_sq, do_xn, do_gn,
+                                          mask, partial, rstride);
 }
 void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
                        const double *diag, double *wa1, double *wa2, double *wa3, double *ext,
@@ -2295,8 +2347,10 @@ void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, con
                                         solver_type, delta, eps_dif, mask, partial, rstride);
 }
 void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
-                         double *scalar, int *flag) {
-    if (spec.nrows > 0) k_reduce_multi<<<spec.nrows, 256, 0, s>>>(partial, spec, scalar, flag);
+                         double *scalar, int *flag, double *host, int host_n, unsigned *ticket) {
+    if (spec.nrows > 0)
+        k_reduce_multi<<<spec.nrows, 256, 0, s>>>(partial, spec, scalar, flag, host, host_n,
+                                                   ticket);
 }
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);
@@ -2612,16 +2666,18 @@ void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, con
 }
 bool launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
-                       int pc_uniform, int assign_off, const double *tb, double *rhs) {
+                       int pc_uniform, int assign_off, const double *tb, double *rhs,
+                       SchurInitFold fold) {
     if (ndest <= 0) return false;
+    // fold.on only comes with rhs and pc_uniform 6 / 7 (Plan::fold_init)
     if (pc_uniform == 6) {
         k_schur_dest_u<6><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
-                                                                assign_off, ndest, tb, rhs);
+                                                                assign_off, ndest, tb, rhs, fold);
         return rhs != nullptr;
     }
     if (pc_uniform == 7) {
         k_schur_dest_u<7><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
-                                                                assign_off, ndest, tb, rhs);
+                                                                assign_off, ndest, tb, rhs, fold);
         return rhs != nullptr;
     }
     k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);

@@ -82,8 +82,11 @@ void Plan::collect_spans() {
 
 // ---- scalar slots ----
 void Plan::read_slots(int lo, int hi) {
-    MMBA_HIP(hipMemcpyAsync(h_scalar + lo, d_scalar + lo, sizeof(double) * (hi - lo + 1),
-                            hipMemcpyDeviceToHost, s));
+    const bool mirrored = mirror_pending && lo == 0 && hi == SL_LAST;
+    mirror_pending = false;
+    if (!mirrored)
+        MMBA_HIP(hipMemcpyAsync(h_scalar + lo, d_scalar + lo, sizeof(double) * (hi - lo + 1),
+                                hipMemcpyDeviceToHost, s));
     if (!spin_wait) {
         MMBA_HIP(hipStreamSynchronize(s));
         return;
@@ -127,16 +130,20 @@ double Plan::dnorm(const double *dv) {
 }
 
 // iflag = 1: setParameters + measureErrors; ||f||^2 -> SL_FNORM.
-void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed, double *dist) {
-    launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, 1.0);
+void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed, double *dist,
+                       int slot) {
+    // ext_pert / step with the Jacobian's eps: a Jacobian at dx that follows
+    // reuses this parameter pass (params_at)
+    launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, fd_eps());
+    params_at = dx;
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin(SPAN_RESID);
     // stiffness / smoothness rows: their partial goes after the residual blocks
     launch_rows_eval(s, P, df + 2 * (size_t)M, eu ? eu + 2 * (size_t)M : nullptr, d_partial,
                      (M + 255) / 256);
-    launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + SL_FNORM, d_ticket, dist);
+    launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + slot, d_ticket, dist);
     span_end(SPAN_RESID);
-    allreduce(d_scalar + SL_FNORM, 1);
+    allreduce(d_scalar + slot, 1);
 }
 
 double Plan::fun(const double *dx, double *df, double *eu, double *ed, double *dist) {
@@ -150,9 +157,14 @@ double Plan::fun(const double *dx, double *df, double *eu, double *ed, double *d
 // iflag = 2: FD Jacobian blocks + normal equations + column norms at x.
 void Plan::jac(const double *dx, const JacLM *lm) {
     const double t0 = wall_now();
-    const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
+    const double eps_dif = fd_eps();
     const bool lmder = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER;
-    launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
+    // the accepted trial point (or the last evaluation) already set the
+    // parameters at dx: external values, FD points and steps are those
+    // k_param_set would write, bit for bit (same inputs, same kernel code)
+    if (params_at != dx)
+        launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
+    params_at = dx;
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
     CentralB CB;
     if (central) {  // the deltaB pass of the central columns
@@ -176,8 +188,9 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.first = lm->first;
         epi.mode = lm->mode;
         epi.fnorm = lm->fnorm;
+        epi.fnorm_sq = lm->fnorm_sq;
         epi.do_xn = lm->first;
-        epi.do_gn = lm->fnorm != 0.;
+        epi.do_gn = lm->fnorm_sq || lm->fnorm != 0.;
         epi.x = dx;
         epi.diag = d_diag;
         epi.acnorm = d_acnorm;
@@ -228,9 +241,10 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
         span_end(SPAN_JAC);
     } else {
-        const int do_xn = lm->first, do_gn = lm->fnorm != 0.;
+        const int do_xn = lm->first, do_gn = lm->fnorm_sq || lm->fnorm != 0.;
         launch_jac_epilogue(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g, d_diag, dx, lm->first,
-                            lm->mode, lm->fnorm, do_xn, do_gn, d_p_own, d_partial, nparts, pw);
+                            lm->mode, lm->fnorm, lm->fnorm_sq, do_xn, do_gn, d_p_own, d_partial,
+                            nparts, pw);
         span_end(SPAN_JAC);
         RedSpec rs{};
         rs.flag_slot = -1;
@@ -263,7 +277,8 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
-                      opt.solver_type, opt.delta, 1.0, d_p_own, pr, nparts, pw);
+                      opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
+    params_at = d_wa2;  // x <- wa2 on acceptance: the next Jacobian skips k_param_set
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     span_begin(SPAN_RESID);
     launch_rows_eval(s, P, d_ftrial + 2 * (size_t)M, eu + 2 * (size_t)M, pr + 2 * (size_t)pw,
@@ -281,7 +296,12 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
         rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_DNORM};
         rs.flag_slot = SL_FAIL;
     }
-    launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr);
+    // unsharded: the LM decision after this trial reads slots [0, SL_LAST],
+    // which the reduction's last block mirrors to the host itself
+    const bool mirror = host_mirror && nranks == 1;
+    launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr,
+                        mirror ? h_scalar : nullptr, SL_LAST + 1, d_mticket);
+    mirror_pending = mirror;
     // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
     allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
     t_func += wall_now() - t0;
@@ -327,15 +347,20 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         } else if (!band) {
             MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         }
-        launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
+        const bool fold = fold_init && nB_solved > 0;
+        if (!fold)
+            launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
         if (nB_solved > 0) {
             if (use_dest) {
                 // unsharded uniform plans fold the rhs update into the
-                // diagonal destinations
+                // diagonal destinations (and, with fold, the whole of
+                // k_schur_init: one launch less per damped solve)
+                SchurInitFold fi{};
+                if (fold) fi = SchurInitFold{1, d_Acc, d_g, d_diag, lam};
                 const bool rhs_done =
                     launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V,
                                       pc_uniform, band && bs.use_bcr, d_tb,
-                                      nranks > 1 ? nullptr : d_rhs);
+                                      nranks > 1 ? nullptr : d_rhs, fi);
                 if (!rhs_done) launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
                 launch_schur_glob(s, P, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
@@ -589,10 +614,10 @@ void Plan::download_params(const double *dx, double *x_out) {
     MMBA_HIP(hipStreamSynchronize(s));
 }
 
-void Plan::error_stats_enqueue(const double *ed) {
-    launch_dist_stats(s, P, ed, d_partial, nparts, pw, d_scalar + SL_ESUM);
-    allreduce(d_scalar + SL_ESUM, 1);
-    allreduce(d_scalar + SL_ENMIN, 2, ReduceOp::Max);
+void Plan::error_stats_enqueue(const double *ed, int base) {
+    launch_dist_stats(s, P, ed, d_partial, nparts, pw, d_scalar + base);
+    allreduce(d_scalar + base, 1);
+    allreduce(d_scalar + base + 1, 2, ReduceOp::Max);
 }
 
 void Plan::error_stats_device(const double *ed, double *avg, double *mn, double *mx) {
@@ -620,7 +645,7 @@ static void error_stats(const double *dist, int M, double *avg, double *mn, doub
 
 int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
                   double *stats) {
-    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    attrs_reset();
     if (x) {
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_x, d_f, d_eu, d_ed);
@@ -641,7 +666,7 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
 // Per-observation reprojected point and corrected marker at x (caller's
 // observation order); the scratch trial buffers carry them (no solve runs).
 int Plan::reproject(const double *x, double *point_out, double *marker_out) {
-    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    attrs_reset();
     if (x) {
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_x, d_f, d_eu, d_ed);  // parameters set, records current
@@ -657,7 +682,7 @@ int Plan::reproject(const double *x, double *point_out, double *marker_out) {
 // and small problems only.
 int Plan::dense_jacobian(const double *x, double *fjac) {
     if (nranks > 1) throw Unsupported{"dense Jacobian of a sharded plan"};
-    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    attrs_reset();
     MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
     fun(d_x, d_f, d_eu, d_ed);
     const int implicit = P.jcol_implicit;
@@ -710,8 +735,9 @@ void Plan::jac_partial_stale(const double *dx, int k) {
             }
     }
     MMBA_HIP(hipMemcpyAsync(d_stale, st.data(), sizeof(int) * F, hipMemcpyHostToDevice, s));
-    const double eps_dif = std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON));
+    const double eps_dif = fd_eps();
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
+    params_at = dx;
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
     CentralB CB;
     if (central) {
@@ -748,30 +774,26 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         }
     };
     // fresh attribute block (the scene's current values)
-    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
-    double init_avg = 0., init_min = 0., init_max = 0., init_fnorm = 0.;
+    attrs_reset();
+    double init_avg = 0.;
     bool measured = false;
     if (opt.accept_only_better && !opt.initial_error_given) {
         // measureErrors before any parameter is set (adjust_base.cpp:1080-1103);
         // it writes errorList (lmder's fvec), ud->errorList and
-        // errorDistanceList, which an immediate interrupt leaves in place
+        // errorDistanceList, which an immediate interrupt leaves in place.
+        // Its ||f|| and statistics stay in device slots until the solve's
+        // last synchronisation (only the accept-only-better test reads them)
         launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
         launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
                          (M + 255) / 256);
-        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FNORM, nullptr,
+        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FI, nullptr,
                         d_dist_x);
-        allreduce(d_scalar + SL_FNORM, 1);
-        error_stats_enqueue(d_ed);
-        read_slots(SL_FNORM, SL_EMAX);  // one synchronisation for both
-        init_avg = h_scalar[SL_ESUM] / Mg;
-        init_min = -h_scalar[SL_ENMIN];
-        init_max = h_scalar[SL_EMAX];
-        init_fnorm = std::sqrt(h_scalar[SL_FNORM]);
+        allreduce(d_scalar + SL_FI, 1);
+        error_stats_enqueue(d_ed, SL_IESUM);
         measured = true;
     } else if (opt.accept_only_better) {
         init_avg = opt.initial_error_avg;  // the caller measured it
     }
-    r.error_initial_avg = init_avg;
 
     // x0 through the pinned stage: no blocking pageable copy (the previous
     // solve's last synchronisation released the stage)
@@ -789,18 +811,20 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     const bool polls = cb && cb->interrupt;
     int info = 0, nfev = 0, njev = 0, func_evals = 0, jac_evals = 0;
     bool interrupted = false;
-    bool dist_ok = false;  // d_dist_x holds the distances at d_x
-    double delta = 0., xnorm = 0., par = 0., fnorm = init_fnorm, gnorm = 0., ratio = 0.;
+    bool dist_ok = false;     // d_dist_x holds the distances at d_x
+    bool f0_pending = false;  // x0's ||f||^2 is in SL_F0, not yet read
+    bool x0_eval = false;     // x0's evaluation was enqueued
+    double delta = 0., xnorm = 0., par = 0., fnorm = 0., gnorm = 0., ratio = 0.;
 
     if (n <= 0 || mg < n || ftol < 0. || xtol < 0. || gtol < 0. || maxfev <= 0 || factor <= 0.)
         goto TERMINATE;
     if (mode == 2) {
         // diag = paramWeightList (adjust_cminpack_lmder.cpp:151); lmder
-        // rejects a non-positive entry before the first evaluation
-        for (int j = 0; j < n; ++j)
-            if (param_weight[j] <= 0.) goto TERMINATE;
-        MMBA_HIP(hipMemcpyAsync(d_diag, param_weight.data(), sizeof(double) * n,
-                                hipMemcpyHostToDevice, s));
+        // rejects a non-positive entry before the first evaluation (both
+        // checked and uploaded once, at plan build)
+        if (!pweight_ok) goto TERMINATE;
+        MMBA_HIP(hipMemcpyAsync(d_diag, d_pweight, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                                s));
     }
     // iflag = 1 at x0: incrementNormalIteration, then the interrupt poll
     // (adjust_solveFunc.cpp:551-571)
@@ -811,24 +835,13 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         info = -1;
         goto TERMINATE;
     }
-    {
-        // When setParameters(x0) writes back exactly the scene's values (every
-        // int_to_ext(x0_p) equals the attribute value bit for bit), the first
-        // evaluation repeats the initial measurement: reuse it
-        bool same = measured;
-        for (int p = 0; p < n && same; ++p)
-            same = int_to_ext(x_inout[p], pmin_h[p], pmax_h[p], poff_h[p], pscale_h[p]) ==
-                   host_attr0[(size_t)param_vidx[p]];
-        if (same) {
-            launch_param_set(s, P, d_x, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta,
-                             1.0);  // d_ext for the trial / Jacobian bookkeeping
-            fnorm = init_fnorm;
-        } else {
-            fnorm = fun(d_x, d_f, d_eu, d_ed, d_dist_x);
-        }
-        dist_ok = true;
-    }
-    push_trace(fnorm);
+    // x0's evaluation, enqueued: its ||f|| reaches the host with the first
+    // decision point's slots, and the first Jacobian's gnorm reads it on the
+    // device (JacLM::fnorm_sq) -- no synchronisation before the Jacobian
+    fun_enqueue(d_x, d_f, d_eu, d_ed, d_dist_x, SL_F0);
+    dist_ok = true;
+    f0_pending = true;
+    x0_eval = true;
     {
         int iter = 1;
         for (;;) {
@@ -867,7 +880,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 if (lmdif) jac_evals -= n;  // counted below with the rest
             }
             {
-                const JacLM lm{iter == 1, mode, fnorm};
+                const JacLM lm{iter == 1, mode, fnorm, f0_pending ? d_scalar + SL_F0 : nullptr};
                 jac(d_x, &lm);
             }
             ++njev;
@@ -896,6 +909,11 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 const double t0 = wall_now();
                 read_slots(0, SL_LAST);
                 t_jac += wall_now() - t0;
+            }
+            if (f0_pending) {  // lmder's fnorm at x0, first entry of the trace
+                fnorm = std::sqrt(h_scalar[SL_F0]);
+                push_trace(fnorm);
+                f0_pending = false;
             }
             if (central) jac_evals += (int)h_scalar[SL_NCENT];
             rank_deficient = h_scalar[SL_ZERO] != 0.;
@@ -998,7 +1016,6 @@ TERMINATE:
     r.outer_iterations = njev;
     r.user_interrupted = interrupted ? 1 : 0;
     r.success = func_evals > 0;
-    r.error_final = fnorm;  // enorm(fvec) at the returned x
     {
         // lmder leaves the solved x in paramList (adjust_cminpack_lmder.cpp:128);
         // solveFrames writes it back only when the error got better
@@ -1016,7 +1033,16 @@ TERMINATE:
         const bool staged = nranks == 1 && n > 0;
         if (staged)
             MMBA_HIP(hipMemcpyAsync(h_xstage, d_x, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-        read_slots(SL_RMS, SL_EMAX);
+        read_slots(SL_RMS, SL_IEMAX);  // also x0's ||f|| and the initial measurement's
+        if (f0_pending) {  // stopped between x0's evaluation and the first decision
+            fnorm = std::sqrt(h_scalar[SL_F0]);
+            push_trace(fnorm);
+        } else if (!x0_eval) {
+            fnorm = measured ? std::sqrt(h_scalar[SL_FI]) : 0.;  // no evaluation at x0
+        }
+        r.error_final = fnorm;  // enorm(fvec) at the returned x
+        if (measured) init_avg = h_scalar[SL_IESUM] / Mg;
+        r.error_initial_avg = init_avg;
         const double avg = h_scalar[SL_ESUM] / Mg;
         r.error_avg = avg;
         r.error_min = -h_scalar[SL_ENMIN];

@@ -52,7 +52,7 @@ int Plan::solve_frames(double *x_inout, mmba_result *results, const mmba_callbac
     const bool polls = cb && cb->interrupt;
     // a request already pending stops every frame at its first poll
     __atomic_store_n(h_bflag, polls && cb->interrupt(cb->user) ? 1 : 0, __ATOMIC_SEQ_CST);
-    MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+    attrs_reset();
     // bundle records (no bundle is solved: computed once per call)
     launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
     MMBA_HIP(hipMemcpyAsync(d_bx, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));

@@ -775,6 +775,14 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             }
             dest_off_h.push_back((int)recs.size());
             ndest = (int)dest_h.size();
+            // k_schur_init folds into the diagonal destinations when every
+            // solved camera-frame has one (its rows are then all written)
+            std::vector<char> hasd(ncf, 0);
+            for (const int2 &d : dest_h)
+                if (d.x == d.y) hasd[d.x] = 1;
+            dest_diag_all = true;
+            for (int cf = 0; cf < ncf; ++cf)
+                if (cf_pc[cf] > 0 && !hasd[cf]) dest_diag_all = false;
         }
     }
     {
@@ -1264,6 +1272,16 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipMemsetAsync(d_Abb, 0, sizeof(double) * (size_t)nB * 9, s));
     MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
     MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
+    d_mticket = dalloc<unsigned>(1);
+    d_pweight = upload(param_weight);
+    pweight_ok = true;
+    for (int j = 0; j < n; ++j)
+        if (param_weight[j] <= 0.) pweight_ok = false;
+    MMBA_HIP(hipMemsetAsync(d_mticket, 0, sizeof(unsigned), s));
+    if (const char *e = std::getenv("MMBA_HOST_MIRROR")) host_mirror = std::atoi(e) != 0;
+    fold_init = dest_diag_all && use_dest && nranks == 1 && nG == 0 && !rs_on && nRpad == nR &&
+                (pc_uniform == 6 || pc_uniform == 7);
+    if (const char *e = std::getenv("MMBA_FOLD_SCHUR_INIT")) fold_init = fold_init && std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_K2_FUSED")) k2_split = std::atoi(e) == 0;
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));

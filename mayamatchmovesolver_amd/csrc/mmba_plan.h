@@ -3,6 +3,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -144,6 +147,8 @@ struct Plan {
     bool rs_on = false;
     double *d_ext_pertB = nullptr, *d_stepB = nullptr, *d_recsB = nullptr, *d_brecB = nullptr;
     std::vector<double> param_weight;  // paramWeightList (diag in mode 2)
+    double *d_pweight = nullptr;       // ... on the device
+    bool pweight_ok = true;            // every weight > 0 (lmder's mode-2 check)
     std::vector<int> stale_host;       // stale-column table (B13), host copy
     std::vector<int> param_frame_host;
     // solved camera-frame blocks (reduced rows [roff, roff + pc)), for the
@@ -162,6 +167,15 @@ struct Plan {
     int *d_fail = nullptr;
     unsigned int *d_ticket = nullptr;  // single-launch reduction ticket (zero between uses)
     double *h_scalar = nullptr;  // pinned
+    // MMBA_HOST_MIRROR=1: trial reductions write slots [0, SL_LAST] straight
+    // into h_scalar (the last k_reduce_multi block) and read_slots skips its
+    // copy launch.  Off by default: measured 3 % slower per C4 solve (the
+    // device's writes to host memory delay the completion the host polls)
+    unsigned *d_mticket = nullptr;
+    bool host_mirror = false, mirror_pending = false;
+    // every solved camera-frame has a diagonal Schur destination; fold_init:
+    // k_schur_init rides in k_schur_dest_u (SchurInitFold)
+    bool dest_diag_all = false, fold_init = false;
     double *h_xstage = nullptr;  // pinned [n]: x in / out without a blocking pageable copy
     int *h_fail = nullptr;       // pinned
 
@@ -240,11 +254,17 @@ struct Plan {
         SL_GNORM = 11,  // lmder gnorm (max)
         SL_RMS = 12,
         SL_NCENT = 13,  // central FD columns of the last Jacobian (second evaluations)
-        SL_LAST = 13,
+        SL_F0 = 14,     // ||f||^2 at x0 (lmder's first evaluation; read with the first decision)
+        SL_LAST = 14,
+        SL_FI = 15,     // ||f||^2 of the initial measurement (read at the end)
         // errorDistanceList statistics (launch_dist_stats): sum, -min, max
         SL_ESUM = 16,
         SL_ENMIN = 17,
         SL_EMAX = 18,
+        // ... of the initial measurement (read at the end)
+        SL_IESUM = 19,
+        SL_IENMIN = 20,
+        SL_IEMAX = 21,
         NSLOT = 24
     };
     void read_slots(int lo, int hi);
@@ -254,7 +274,7 @@ struct Plan {
     void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
     double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
     void fun_enqueue(const double *dx, double *df, double *eu, double *ed,
-                     double *dist = nullptr);
+                     double *dist = nullptr, int slot = SL_FNORM);
     double fun(const double *dx, double *df, double *eu, double *ed, double *dist = nullptr);
     // errorDistanceList of the accepted x and of the pending trial point
     // (swapped on acceptance): the RMS at the returned x needs no extra
@@ -264,13 +284,17 @@ struct Plan {
     std::vector<double> pmin_h, pmax_h, poff_h, pscale_h;  // bound transform (host)
     // compute_error_stats of ed on the device -> avg, min, max (host)
     void error_stats_device(const double *ed, double *avg, double *mn, double *mx);
-    void error_stats_enqueue(const double *ed);  // -> SL_ESUM, SL_ENMIN, SL_EMAX
+    // -> slots base .. base + 2 (sum, -min, max): SL_ESUM or SL_IESUM
+    void error_stats_enqueue(const double *ed, int base = SL_ESUM);
     // with lm: the lmder bookkeeping after the normal equations is fused
     // into the column-norm launch (k_jac_epilogue); scalars -> SL_ZERO,
     // SL_XN2 (first pass), SL_GNORM (fnorm != 0)
     struct JacLM {
         int first, mode;
         double fnorm;
+        // non-null: ||f||^2 in a device slot (the first Jacobian, before the
+        // host has read x0's evaluation); the kernels take its square root
+        const double *fnorm_sq = nullptr;
     };
     void jac(const double *dx, const JacLM *lm = nullptr);
     // interrupt polls of the reference (MComputation::isInterruptRequested):
@@ -294,6 +318,18 @@ struct Plan {
     // swapped in when lmpar accepts that step
     double *d_eu_s = nullptr, *d_ed_s = nullptr;
     bool spec_ok = true;  // last lmpar accepted its undamped step
+    // d_f / d_eu / d_ed hold the last solve's (or measure's) outputs
+    // (mmba_plan_outputs); other evaluations clear it
+    bool outputs_ready = false;
+    // the device x vector whose parameters (attribute values, d_ext,
+    // d_ext_pert, d_step) are currently set; nullptr: none
+    const double *params_at = nullptr;
+    void attrs_reset() {  // the scene's own attribute values
+        MMBA_HIP(hipMemcpyAsync(P.attr_val, d_attr0, attr_bytes, hipMemcpyDeviceToDevice, s));
+        params_at = nullptr;
+    }
+    // forward-difference eps of lmdif's fdjac2 (unused by lmder's steps)
+    double fd_eps() const { return std::sqrt(std::max(std::fabs(opt.delta), DBL_EPSILON)); }
     int pw = 0;           // partial-row stride of d_partial (8 rows)
     // dnorm_slot >= 0: also ||D xs||^2 -> that slot (one reduction launch
     // with the fail flag)

@@ -266,18 +266,24 @@ class Solver:
         check(lib().mmba_plan_jacobian(self._h, _dp(xx), _dp(fjac)))
         return fjac.reshape(n, m).T
 
-    def solve(self, x0=None, trace_capacity=4096, interrupt=None, out=None) -> SolveResult:
+    def solve(self, x0=None, trace_capacity=4096, interrupt=None, out=None,
+              fetch=True) -> SolveResult:
         """LM solve from x0 (internal parameters).  ``SolveResult.x`` is the
         solved x as lmder leaves paramList; ``result["error_is_better"]`` says
         whether solveFrames would write it back (``accepted_x``).
         ``interrupt``: a callable polled where the reference polls
         MComputation::isInterruptRequested (non-zero / True stops).
         ``out``: (fvec, err_user, err_dist) float64 arrays to fill instead of
-        fresh ones (a caller solving repeatedly keeps its buffers)."""
+        fresh ones (a caller solving repeatedly keeps its buffers).
+        ``fetch=False``: the per-residual outputs stay in HBM (NULL output
+        pointers; ``fvec`` / ``err_user`` / ``err_dist`` are None) until
+        ``outputs()`` fetches them."""
         p = self.problem
         m, M = p.num_residuals, p.num_obs
         x = np.array(p.x0 if x0 is None else x0, dtype=np.float64)
-        if out is None:
+        if not fetch:
+            fvec = eu = ed = None
+        elif out is None:
             fvec, eu, ed = np.zeros(m), np.zeros(m), np.zeros(M)
         else:
             fvec, eu, ed = out
@@ -296,6 +302,16 @@ class Solver:
                            fnorm_trace=tbuf[:min(tr.count, trace_capacity)].copy(), problem=p,
                            x0=np.array(p.x0 if x0 is None else x0, dtype=np.float64))
 
+
+    def outputs(self, out=None):
+        """(fvec, err_user, err_dist) of the last ``solve`` / ``measure``
+        (``mmba_plan_outputs``): the fetch a ``solve(fetch=False)`` left in
+        HBM.  ``out``: arrays to fill (e.g. ``host_array`` page-locked ones)."""
+        p = self.problem
+        m, M = p.num_residuals, p.num_obs
+        fvec, eu, ed = out if out is not None else (np.zeros(m), np.zeros(m), np.zeros(M))
+        check(lib().mmba_plan_outputs(self._h, _dp(fvec), _dp(eu), _dp(ed)))
+        return fvec, eu, ed
 
     def set_attr_values(self, attr_values):
         """Replace the scene's attribute values of this plan

@@ -7,6 +7,7 @@
 #   benchcfg:I        bench line of configs[I] (no CPU baseline)
 #   prof              rocprofv3 --kernel-trace --stats of the default bench
 #   pmc               FETCH_SIZE / WRITE_SIZE passes of the default bench
+#   iter              kernel traces + one-iteration timelines of C2 / C4 / C5
 set -o pipefail
 OUT=${1:?out dir}
 shift
@@ -40,6 +41,8 @@ for step in "$@"; do
       for ctr in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$OUT/pmc_$ctr" -o c4 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/pmc_$ctr.json" 2> "$OUT/pmc_$ctr.err" || exit 1
       done ;;
+    iter)
+      bash tools/gpu_iter.sh "$OUT/iter" || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
