@@ -46,6 +46,11 @@ void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
                     const double *ext_pert, const double *step, double *recs, int nvar,
                     double *brec, int base_only);
 int residual_blocks(const DevProblem &P);
+// Partial count of the trial point's residual pass (launch_residual_jp):
+// one per camera-frame where trial_cf_fusable, else residual_blocks.
+bool &trial_cf_off();
+bool trial_cf_fusable(const DevProblem &P);
+int trial_blocks(const DevProblem &P);
 // Reductions: with a ticket (a zero-initialised device counter) the partial
 // sums are combined inside the same launch, otherwise by a second kernel.
 void launch_reproject(hipStream_t s, const DevProblem &P, const double *recs, double *pts,
@@ -59,10 +64,23 @@ void launch_dist_stats(hipStream_t s, const DevProblem &P, const double *ed, dou
                        int nparts, int rstride, double *out);
 // launch_residual (partials only) plus ||J p||^2 partials of the same blocks
 // into partial_jp (k_jp_sumsq's sum, one launch)
+// Reduction launch folded into a producer (unsharded trial point): the
+// producer's last workgroup (ticket) runs k_reduce_multi's work -- the rows
+// of spec (offsets into partial), the fail flag and the host mirror.
+struct RedTail {
+    int on = 0;
+    RedSpec spec{};
+    const double *partial = nullptr;
+    double *scalar = nullptr;
+    int *flag = nullptr;
+    double *host = nullptr;
+    int host_n = 0;
+    unsigned *ticket = nullptr;
+};
 void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,
-                        double *partial_jp, double *dist = nullptr);
+                        double *partial_jp, double *dist = nullptr, const RedTail &T = RedTail());
 // Second evaluation of central FD columns (lmder, autoDiffType central):
 // records / bundle records / perturbed values at x + deltaB and the column
 // factor 0.5 / (|dA| + |dB|) (0: forward column).  recs == nullptr: forward.
@@ -103,6 +121,17 @@ struct NeEpi {
     const double *x = nullptr;
     double *diag = nullptr, *acnorm = nullptr, *partial = nullptr;
     int rstride = 0, cf_base = 0, bnd_base = 0;
+    // fold (unsharded k_ne_bnd_jb): the bundle pass's last workgroup (ticket)
+    // reduces the epilogue rows of spec into scalar with k_reduce_multi's
+    // arithmetic -- no separate reduction launch
+    int fold = 0;
+    RedSpec spec{};
+    double *scalar = nullptr;
+    unsigned *ticket = nullptr;
+    // Lb != nullptr: the bundle pass also factors Abb at lam = 0
+    // (k_bundle_factor's arithmetic) for the undamped solve that follows
+    double *Lb = nullptr, *tb = nullptr;
+    int *fail = nullptr;
 };
 // Fused K2 (k_jac_ne_u): FD Jacobian + camera-frame normal equations in one
 // pass for uniform fast plans without global parameters (ncv = jac_ncv).

@@ -71,6 +71,191 @@ __device__ __forceinline__ void finish_blocks(double v, double *partial, double 
     }
 }
 
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void st_sc1(double *p, double v) {  // write-through store
+    __hip_atomic_store((gu64_t *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {  // L1-bypassing load
+    return __longlong_as_double((long long)__hip_atomic_load(
+        (gu64_t *)const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// 3 x 3 damped bundle factor of one bundle (k_bundle_factor's arithmetic):
+// A (pb x pb block, identity padding), rhs = gB (0 on padding), dd = diag of
+// the bundle's parameters -> Lb, tb = Lb^-1 rhs; L / il returned for the
+// arrow columns.
+__device__ __forceinline__ void bundle_chol3(double (&A)[3][3], double (&rhs)[3],
+                                             const double (&dd)[3], int pb, double lam, int b,
+                                             double *Lb, double *tb, int *fail,
+                                             double (*Lo)[3] = nullptr, double *ilo = nullptr) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (a < pb) {
+            const double d = dd[a];
+            A[a][a] += lam * (d * d);
+            if (A[a][a] == 0.) {
+                A[a][a] = 1.;
+                rhs[a] = 0.;
+            }
+        }
+    }
+    double L[3][3] = {}, il[3];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double s = A[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+        if (!(s > 0.)) {
+            ok = false;
+            s = 1.;
+        }
+        L[j][j] = sqrt(s);
+        il[j] = 1.0 / L[j][j];
+#pragma unroll
+        for (int i = j + 1; i < 3; ++i) {
+            double t = A[i][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
+            L[i][j] = t * il[j];
+        }
+    }
+    if (!ok) atomicOr(fail, 1);
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Lb[(size_t)b * 9 + a * 3 + c] = (a < pb) ? L[a][c] : 0.;
+    double t[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double s = rhs[a];
+#pragma unroll
+        for (int k = 0; k < a; ++k) s -= L[a][k] * t[k];
+        t[a] = s * il[a];  // zero on padding rows (rhs 0)
+    }
+    for (int a = 0; a < 3; ++a) tb[(size_t)b * 3 + a] = t[a];
+    if (Lo) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            ilo[a] = il[a];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Lo[a][c] = L[a][c];
+        }
+    }
+}
+
+// One partial row reduced by one 256-thread workgroup: k_reduce_multi's
+// arithmetic (thread t sums entries t, t + 256, ..., then the fixed tree).
+template <bool SC1>
+__device__ __forceinline__ double reduce_row_block(const double *partial, const RedRow &rw,
+                                                   double *red) {
+    const bool mx = rw.is_max != 0;
+    double s = 0.;
+    for (int i = threadIdx.x; i < rw.n; i += blockDim.x) {
+        const double q = SC1 ? ld_sc1(&partial[rw.off + i]) : partial[rw.off + i];
+        s = mx ? fmax(s, q) : s + q;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            red[threadIdx.x] = mx ? fmax(red[threadIdx.x], red[threadIdx.x + w])
+                                  : red[threadIdx.x] + red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const double v = red[0];
+    __syncthreads();
+    return v;
+}
+
+// Every row of spec at once (the last workgroup of a folded launch): each
+// thread issues its loads of all rows before any sum, then one fixed tree
+// per row, level by level for all rows -- per row the arithmetic of
+// reduce_row_block (and so of k_reduce_multi).
+constexpr int RED_ROWS = 8;
+__device__ __forceinline__ void reduce_rows_sc1(const RedSpec &spec, const double *partial,
+                                                double *scalar) {
+    __shared__ double red[RED_ROWS][256];
+    const int nr = spec.nrows;
+    double sv[RED_ROWS];
+#pragma unroll
+    for (int r = 0; r < RED_ROWS; ++r) {
+        sv[r] = 0.;
+        if (r < nr) {
+            const RedRow rw = spec.row[r];
+            const bool mx = rw.is_max != 0;
+            for (int i = threadIdx.x; i < rw.n; i += blockDim.x) {
+                const double q = ld_sc1(&partial[rw.off + i]);
+                sv[r] = mx ? fmax(sv[r], q) : sv[r] + q;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RED_ROWS; ++r)
+        if (r < nr) red[r][threadIdx.x] = sv[r];
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+#pragma unroll
+            for (int r = 0; r < RED_ROWS; ++r) {
+                if (r >= nr) break;
+                const bool mx = spec.row[r].is_max != 0;
+                red[r][threadIdx.x] = mx ? fmax(red[r][threadIdx.x], red[r][threadIdx.x + w])
+                                         : red[r][threadIdx.x] + red[r][threadIdx.x + w];
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < nr) scalar[spec.row[threadIdx.x].slot] = red[threadIdx.x][0];
+    __syncthreads();
+}
+
+// Last-workgroup epilogue of a launch whose workgroups stored partials with
+// st_sc1 (or an earlier launch stored them): every storing wave drains, one
+// lane adds to the ticket (agent scope), the workgroup whose add came last
+// loads every partial sc1 (MI355X guide, valid forms, first table row) and
+// reduces the rows of spec into scalar; the ticket is reset for the next
+// user.  256 threads per workgroup.
+__device__ __forceinline__ void tail_reduce(const RedSpec &spec, const double *partial,
+                                            double *scalar, unsigned *ticket) {
+    __shared__ unsigned last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    reduce_rows_sc1(spec, partial, scalar);
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// tail_reduce plus the rest of k_reduce_multi's work: the fail flag to its
+// slot (then cleared) and the host mirror of scalar[0, host_n).
+__device__ __forceinline__ void tail_reduce_full(const RedTail &T) {
+    __shared__ unsigned last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(T.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    reduce_rows_sc1(T.spec, T.partial, T.scalar);
+    if (threadIdx.x == 0 && T.flag && T.spec.flag_slot >= 0) {
+        T.scalar[T.spec.flag_slot] = (double)*T.flag;  // bit 1 pivot, bit 2 dataflow timeout
+        *T.flag = 0;
+    }
+    if (T.host) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int i = threadIdx.x; i < T.host_n; i += blockDim.x) T.host[i] = ld_sc1(&T.scalar[i]);
+    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(T.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // -------------------------------------------------------------------------
 // Parameters: external values, FD perturbations (adjust_solveFunc.cpp:148-180,
 // cminpack fdjac2), setParameters (adjust_setParameters.cpp:174-250).
@@ -264,7 +449,8 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
                                                   const int *__restrict__ jcol,
                                                   const int *__restrict__ nloc,
                                                   const double *__restrict__ pstep,
-                                                  double *partial_jp, double *dist) {
+                                                  double *partial_jp, double *dist,
+                                                  const RedTail T) {
     __shared__ double red[256];
     const int lb = xcd_remap(blockIdx.x, gridDim.x);  // logical block (XCD-contiguous)
     const int i = lb * blockDim.x + threadIdx.x;
@@ -342,7 +528,12 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
             if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
             __syncthreads();
         }
-        if (threadIdx.x == 0) partial_jp[lb] = red[0];
+        if (threadIdx.x == 0) {
+            if (T.on)
+                st_sc1(&partial_jp[lb], red[0]);  // read by this launch's last workgroup
+            else
+                partial_jp[lb] = red[0];
+        }
         __syncthreads();
     }
     red[threadIdx.x] = s;
@@ -351,7 +542,90 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
+    if (T.on) {
+        if (threadIdx.x == 0) st_sc1(&partial[lb], red[0]);
+        tail_reduce_full(T);
+        return;
+    }
     finish_blocks<false>(red[0], partial, out, ticket, lb);
+}
+
+// Trial point on uniform fast plans (one workgroup per camera-frame
+// segment, the plans of k_jac_ne_u): the camera-frame's base record and the
+// steps p of its camera parameters are staged once in LDS, where
+// k_residual<JP, FAST> reaches them per observation through three dependent
+// tables (obs_cf -> cf_var_off -> cf_var_param -> p).  Per observation the
+// same residual and (J p) arithmetic as k_residual<true, true>; one partial
+// per camera-frame (stored at the camera-frame index), in the
+// XCD-contiguous order of k_jac_ne_u, whose records and J rows it reads.
+template <int PC>
+__global__ void __launch_bounds__(256) k_residual_jp_cf(
+    DevProblem P, const double *__restrict__ recs, double *f, double *eu, double *ed,
+    double *partial, const double *__restrict__ J, const int *__restrict__ nloc,
+    const double *__restrict__ pstep, double *partial_jp, double *dist) {
+    __shared__ double sRec[CAMREC];
+    __shared__ double sP[PC];
+    __shared__ int sNv;
+    __shared__ double red[2][256];
+    const int cf = xcd_remap(blockIdx.x, gridDim.x);
+    const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
+    const int tid = threadIdx.x;
+    {
+        const int voff = P.cf_var_off[cf];
+        const int nv = P.cf_var_off[cf + 1] - voff - 1;
+        if (tid < CAMREC) sRec[tid] = recs[(size_t)voff * CAMREC + tid];
+        if (tid < PC) sP[tid] = tid < nv ? pstep[P.cf_var_param[voff + 1 + tid]] : 0.;
+        if (tid == 0) sNv = nv;
+    }
+    __syncthreads();
+    const int nv = sNv;
+    const int M = P.M;
+    double s = 0., sj = 0.;
+    for (int i = o0 + tid; i < o1; i += 256) {
+        const int b = P.obs_bnd[i];
+        const double *br = &P.brec[(size_t)b * BREC];
+        const double bp[3] = {br[0], br[1], br[2]};
+        const int4 p4 = P.bnd_p4[b];
+        const int nl = nloc[i];
+        const Resid r = residual_l(P, sRec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1],
+                                   P.obs_sqrtw[i], MMBA_LENS_NONE, nullptr);
+        f[2 * i] = r.ex;
+        f[2 * i + 1] = r.ey;
+        if (eu) {
+            eu[2 * i] = r.ux;
+            eu[2 * i + 1] = r.uy;
+            ed[i] = r.dist;
+        }
+        if (dist) dist[i] = r.dist;
+        if (own_obs(P, i)) {
+            s += r.ex * r.ex + r.ey * r.ey;
+            // column l is camera variant l (l < nv), then the bundle's
+            // parameters (k_residual<JP>'s implicit-jcol order)
+            double ax = 0., ay = 0.;
+            for (int l = 0; l < nl; ++l) {
+                const int a = l - nv;
+                const double pv = l < nv ? sP[l]
+                                         : pstep[a == 0 ? p4.x : (a == 1 ? p4.y : p4.z)];
+                ax += J[(size_t)(2 * l) * M + i] * pv;
+                ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+            }
+            sj += ax * ax + ay * ay;
+        }
+    }
+    red[0][tid] = s;
+    red[1][tid] = sj;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) {
+            red[0][tid] += red[0][tid + w];
+            red[1][tid] += red[1][tid + w];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        partial[cf] = red[0][0];
+        partial_jp[cf] = red[1][0];
+    }
 }
 
 // -------------------------------------------------------------------------
@@ -496,34 +770,54 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     }
 }
 
+// Camera-frame-uniform inputs of one observation's fast Jacobian: the
+// camera-frame's record block (base record, then variant v at (1 + v) *
+// CAMREC), its variant parameters and steps, and the stale column of its
+// frame.  k_jac_ne_u (one workgroup per camera-frame) stages them once in
+// LDS; k_jacobian_u (one thread per observation) loads them per thread.
+template <int NCV>
+struct JacCf {
+    const double *rcf;
+    int pv[NCV];
+    double st[NCV];
+    int nv, fr, pstale;
+};
+
+template <int NCV>
+__device__ __forceinline__ JacCf<NCV> jac_cf_load(const DevProblem &P, int cf,
+                                                  const double *__restrict__ recs,
+                                                  const double *__restrict__ step,
+                                                  const int *__restrict__ stale_param) {
+    JacCf<NCV> C;
+    const int voff = P.cf_var_off[cf];
+    C.nv = min(P.cf_var_off[cf + 1] - voff - 1, NCV);
+#pragma unroll
+    for (int v = 0; v < NCV; ++v) C.pv[v] = v < C.nv ? P.cf_var_param[voff + 1 + v] : -1;
+#pragma unroll
+    for (int v = 0; v < NCV; ++v) C.st[v] = v < C.nv ? step[C.pv[v]] : 1.;
+    C.rcf = &recs[(size_t)voff * CAMREC];
+    C.fr = P.cf_frame[cf];
+    C.pstale = stale_param[C.fr];
+    return C;
+}
+
 // One observation of the uniform fast Jacobian: writes its J columns (and
 // jcol / the bundle block record / the stale errorList) and returns the
 // camera columns and f at x for a fused normal-equation accumulation.
 template <int NCV, bool GEN>  // GEN: some bundle needs the transform-chain path
-__device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i,
-                                          const double *__restrict__ recs,
-                                          const double *__restrict__ step, bool lmder,
-                                          double *__restrict__ J, int *__restrict__ jcol,
-                                          int *__restrict__ nloc,
-                                          const int *__restrict__ stale_param,
+__device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i, const JacCf<NCV> &C,
+                                          bool lmder, double *__restrict__ J,
+                                          int *__restrict__ jcol, int *__restrict__ nloc,
                                           double *__restrict__ eu, double *__restrict__ ed,
                                           double (&cx)[NCV], double (&cy)[NCV], double &fx,
                                           double &fy) {
     const int M = P.M;
-    const int cf = P.obs_cf[i];
     const int b = P.obs_bnd[i];
-    const int fr = P.obs_frame[i];
+    const int fr = C.fr;
     const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
     const int4 p4 = P.bnd_p4[b];
-    const int voff = P.cf_var_off[cf];
-    const int nv = min(P.cf_var_off[cf + 1] - voff - 1, NCV);
-    const int pstale = stale_param[fr];
-    int pv[NCV];
-    double st[NCV];
-#pragma unroll
-    for (int v = 0; v < NCV; ++v) pv[v] = v < nv ? P.cf_var_param[voff + 1 + v] : -1;
-#pragma unroll
-    for (int v = 0; v < NCV; ++v) st[v] = v < nv ? step[pv[v]] : 1.;
+    const int nv = C.nv;
+    const int pstale = C.pstale;
     double bp0[3];
     if (GEN) {
         base_bundle(P, b, fr, bp0);
@@ -535,7 +829,7 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i,
     }
     const int nb = p4.w > 0 ? p4.w : 0;
     const double *__restrict__ br = &P.brec[(size_t)b * BREC];
-    const double *__restrict__ rec0 = &recs[(size_t)voff * CAMREC];
+    const double *__restrict__ rec0 = C.rcf;
     const Resid r0 = residual(rec0, bp0, mx, my, sw, P.mode, P.image_width, MMBA_LENS_NONE, nullptr);
     fx = r0.ex;
     fy = r0.ey;
@@ -566,9 +860,9 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i,
         cx[v] = 0.;
         cy[v] = 0.;
         if (v < nv) {
-            const double *__restrict__ rec = &recs[(size_t)(voff + 1 + v) * CAMREC];
+            const double *__restrict__ rec = C.rcf + (1 + v) * CAMREC;
             const double2 j =
-                emit(pv[v], residual_e(rec, bp0, mx, my, sw, P.mode, P.image_width), st[v], v);
+                emit(C.pv[v], residual_e(rec, bp0, mx, my, sw, P.mode, P.image_width), C.st[v], v);
             cx[v] = j.x;
             cy[v] = j.y;
         }
@@ -586,7 +880,7 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i,
     }
     double rsx = r0.ux, rsy = r0.uy, rsd = r0.dist;  // errorList of the stale column
     if (hit >= 0) {
-        const double *rec = hit < NCV ? &recs[(size_t)(voff + 1 + hit) * CAMREC] : rec0;
+        const double *rec = hit < NCV ? C.rcf + (1 + hit) * CAMREC : rec0;
         double bq[3] = {bp0[0], bp0[1], bp0[2]};
         if (hit >= NCV) {
             const int a = hit - NCV;
@@ -630,8 +924,9 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     const int i = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     if (i >= P.M) return;
     double cx[NCV], cy[NCV], fx, fy;
-    jac_obs_u<NCV, GEN>(P, i, recs, step, solver_type == MMBA_SOLVER_CMINPACK_LMDER, J, jcol,
-                        nloc, stale_param, eu, ed, cx, cy, fx, fy);
+    const JacCf<NCV> C = jac_cf_load<NCV>(P, P.obs_cf[i], recs, step, stale_param);
+    jac_obs_u<NCV, GEN>(P, i, C, solver_type == MMBA_SOLVER_CMINPACK_LMDER, J, jcol, nloc, eu,
+                        ed, cx, cy, fx, fy);
 }
 
 // -------------------------------------------------------------------------
@@ -737,7 +1032,7 @@ __global__ void __launch_bounds__(256) k_ne_cf(DevProblem P, const double *__res
 // One parameter's share of the lmder bookkeeping (k_jac_epilogue, same
 // operations): acnorm, diag update, and its contributions to the rank flag,
 // ||D x||^2 and gnorm.
-__device__ __forceinline__ void epi_param(const NeEpi &E, int p, double d, double gp, double &zf,
+__device__ __forceinline__ double epi_param(const NeEpi &E, int p, double d, double gp, double &zf,
                                           double &xn, double &gm) {
     const double an = sqrt(d);
     E.acnorm[p] = an;
@@ -758,6 +1053,7 @@ __device__ __forceinline__ void epi_param(const NeEpi &E, int p, double d, doubl
         const double fn = E.fnorm_sq ? sqrt(*E.fnorm_sq) : E.fnorm;
         if (fn != 0.) gm = fmax(gm, fabs((gp / fn) / an));
     }
+    return dg;  // diag[p] as stored (what k_bundle_factor reads next)
 }
 
 __device__ __forceinline__ void epi_store(const NeEpi &E, int col, double zf, double xn,
@@ -766,6 +1062,7 @@ __device__ __forceinline__ void epi_store(const NeEpi &E, int col, double zf, do
     E.partial[E.rstride + col] = xn;
     E.partial[2 * E.rstride + col] = gm;
 }
+
 
 template <int PC, int NW, int NG>
 __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
@@ -899,18 +1196,57 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
     double *Acc, double *g, NeEpi E) {
     constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC;
     __shared__ double wsum[NW][NE];
+    // the camera-frame's records, variant parameters and steps: staged once
+    // (every observation of the segment reads the same ones)
+    __shared__ double sRec[(PC + 1) * CAMREC];
+    __shared__ int sPv[PC];
+    __shared__ double sSt[PC];
+    __shared__ int sHdr[3];  // nv, frame, stale column
     const int cf = xcd_remap(blockIdx.x, gridDim.x);
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     const bool solved = P.cf_pc[cf] == PC && own_cf(P, cf);  // sharded: owner's blocks only
+    {
+        const int voff = P.cf_var_off[cf];
+        const int nv = min(P.cf_var_off[cf + 1] - voff - 1, PC);
+        for (int t = tid; t < (nv + 1) * CAMREC; t += 64 * NW)
+            sRec[t] = recs[(size_t)voff * CAMREC + t];
+        if (tid < PC) {
+            const int p = tid < nv ? P.cf_var_param[voff + 1 + tid] : -1;
+            sPv[tid] = p;
+            sSt[tid] = tid < nv ? step[p] : 1.;
+        }
+        if (tid == 0) {
+            const int fr = P.cf_frame[cf];
+            sHdr[0] = nv;
+            sHdr[1] = fr;
+            sHdr[2] = stale_param[fr];
+        }
+    }
+    __syncthreads();
+    JacCf<PC> C;
+    C.rcf = sRec;
+#pragma unroll
+    for (int v = 0; v < PC; ++v) {
+        C.pv[v] = sPv[v];
+        C.st[v] = sSt[v];
+    }
+    C.nv = sHdr[0];
+    C.fr = sHdr[1];
+    C.pstale = sHdr[2];
     double acc[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) acc[e] = 0.;
     for (int i = o0 + tid; i < o1; i += 64 * NW) {
         double jx[PC], jy[PC], fx, fy;
-        jac_obs_u<PC, GEN>(P, i, recs, step, lmder, J, jcol, nloc, stale_param, eu, ed, jx, jy,
-                           fx, fy);
+        // the record reads stay inside the loop (LDS broadcasts): an opaque
+        // zero offset keeps the compiler from hoisting 140 loop-invariant
+        // doubles into registers
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        C.rcf = sRec + z;
+        jac_obs_u<PC, GEN>(P, i, C, lmder, J, jcol, nloc, eu, ed, jx, jy, fx, fy);
         int e = 0;
 #pragma unroll
         for (int a = 0; a < PC; ++a)
@@ -998,18 +1334,32 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
         g[p4.x] = gb[0];
         if (pb > 1) g[p4.y] = gb[1];
         if (pb > 2) g[p4.z] = gb[2];
+        double dd[3] = {0., 0., 0.};  // diag after the epilogue (read by the factor)
         if (E.on) {
             // sharded: every bundle of the shard gets acnorm / diag, only the
             // owned ones enter the rank-summed scalars
             double zo = 0., xo = 0., go = 0.;
-            epi_param(E, p4.x, A[0][0], gb[0], zo, xo, go);
-            if (pb > 1) epi_param(E, p4.y, A[1][1], gb[1], zo, xo, go);
-            if (pb > 2) epi_param(E, p4.z, A[2][2], gb[2], zo, xo, go);
+            dd[0] = epi_param(E, p4.x, A[0][0], gb[0], zo, xo, go);
+            if (pb > 1) dd[1] = epi_param(E, p4.y, A[1][1], gb[1], zo, xo, go);
+            if (pb > 2) dd[2] = epi_param(E, p4.z, A[2][2], gb[2], zo, xo, go);
             if (own_bnd(P, b)) {
                 zf = zo;
                 xn = xo;
                 gm = go;
             }
+        }
+        if (E.Lb) {
+            // the undamped solve's bundle factor (k_bundle_factor at lam = 0,
+            // same operands and operations: Abb and gB as stored above)
+            double Af[3][3], rhs[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    Af[a][c] = (a < pb && c < pb) ? A[a][c] : (a == c ? 1. : 0.);
+                rhs[a] = a < pb ? gb[a] : 0.;
+            }
+            bundle_chol3(Af, rhs, dd, pb, 0.0, b, E.Lb, E.tb, E.fail);
         }
     }
     if (!E.on) return;
@@ -1025,9 +1375,17 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0)
-        epi_store(E, E.bnd_base + xcd_remap(blockIdx.x, gridDim.x), red[0][0], red[1][0],
-                  red[2][0]);
+    if (threadIdx.x == 0) {
+        const int col = E.bnd_base + xcd_remap(blockIdx.x, gridDim.x);
+        if (E.fold) {  // read by this launch's last workgroup: write-through
+            st_sc1(&E.partial[col], red[0][0]);
+            st_sc1(&E.partial[E.rstride + col], red[1][0]);
+            st_sc1(&E.partial[2 * E.rstride + col], red[2][0]);
+        } else {
+            epi_store(E, col, red[0][0], red[1][0], red[2][0]);
+        }
+    }
+    if (E.fold) tail_reduce(E.spec, E.partial, E.scalar, E.ticket);
 }
 
 // Per bundle: Abb (pb x pb), gB, Abg (pb x nG).  One thread per bundle.
@@ -1323,22 +1681,9 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
                                                       unsigned *ticket) {
     __shared__ double red[256];
     const RedRow rw = spec.row[blockIdx.x];
-    const bool mx = rw.is_max != 0;
-    double s = 0.;
-    for (int i = threadIdx.x; i < rw.n; i += blockDim.x) {
-        const double q = partial[rw.off + i];
-        s = mx ? fmax(s, q) : s + q;
-    }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            red[threadIdx.x] = mx ? fmax(red[threadIdx.x], red[threadIdx.x + w])
-                                  : red[threadIdx.x] + red[threadIdx.x + w];
-        __syncthreads();
-    }
+    const double v = reduce_row_block<false>(partial, rw, red);
     if (threadIdx.x == 0) {
-        scalar[rw.slot] = red[0];
+        scalar[rw.slot] = v;
         if (blockIdx.x == 0 && flag && spec.flag_slot >= 0) {
             scalar[spec.flag_slot] = (double)*flag;  // bit 1 pivot, bit 2 dataflow timeout
             *flag = 0;
@@ -1377,59 +1722,22 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
     if (pb == 0) return;
     const int po = P.bnd_par_off[b];
     // every index static (no scratch); rows a >= pb are identity padding
-    double A[3][3], rhs[3];
+    double A[3][3], rhs[3], dd[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
 #pragma unroll
         for (int c = 0; c < 3; ++c)
             A[a][c] = (a < pb && c < pb) ? Abb[(size_t)b * 9 + a * 3 + c] : (a == c ? 1. : 0.);
         rhs[a] = 0.;
+        dd[a] = 0.;
         if (a < pb) {
             const int p = P.bnd_par[po + a];
-            const double d = diag[p];
-            A[a][a] += lam * (d * d);
+            dd[a] = diag[p];
             rhs[a] = g[p];
-            if (A[a][a] == 0.) {
-                A[a][a] = 1.;
-                rhs[a] = 0.;
-            }
         }
     }
-    double L[3][3] = {}, il[3];
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        double s = A[j][j];
-#pragma unroll
-        for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
-        if (!(s > 0.)) {
-            ok = false;
-            s = 1.;
-        }
-        L[j][j] = sqrt(s);
-        il[j] = 1.0 / L[j][j];
-#pragma unroll
-        for (int i = j + 1; i < 3; ++i) {
-            double t = A[i][j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
-            L[i][j] = t * il[j];
-        }
-    }
-    if (!ok) atomicOr(fail, 1);
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) Lb[(size_t)b * 9 + a * 3 + c] = (a < pb) ? L[a][c] : 0.;
-    double t[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        double s = rhs[a];
-#pragma unroll
-        for (int k = 0; k < a; ++k) s -= L[a][k] * t[k];
-        t[a] = s * il[a];  // zero on padding rows (rhs 0)
-    }
-    for (int a = 0; a < 3; ++a) tb[(size_t)b * 3 + a] = t[a];
+    double L[3][3], il[3];
+    bundle_chol3(A, rhs, dd, pb, lam, b, Lb, tb, fail, L, il);
     for (int q = 0; q < P.nG; ++q) {
         // row q of Abg^T, forward-solve against L: w L^T = a  ->  L w^T = a^T
         double w[3];
@@ -2358,6 +2666,21 @@ void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
 // Partial sums of a residual evaluation: one per 256 observations, plus one
 // for the attribute rows (k_rows_eval writes entry nblk(M, 256)).
 int residual_blocks(const DevProblem &P) { return nblk(P.M, 256) + (P.nrows > 0 ? 1 : 0); }
+// The trial point's residual pass runs per camera-frame (k_residual_jp_cf)
+// on the uniform fast plans of the fused K2: no attribute rows, no lens, no
+// rolling shutter, implicit Jacobian columns.
+bool trial_cf_fusable(const DevProblem &P) {
+    return jac_ne_fusable(P, P.pc_uniform) && P.all_bnd_fast && P.no_lens && P.jcol_implicit &&
+           !trial_cf_off();
+}
+bool &trial_cf_off() {  // MMBA_TRIAL_CF=0: the per-256-observation kernel (A/B)
+    static bool off = [] {
+        const char *e = std::getenv("MMBA_TRIAL_CF");
+        return e && std::atoi(e) == 0;
+    }();
+    return off;
+}
+int trial_blocks(const DevProblem &P) { return trial_cf_fusable(P) ? P.ncf : residual_blocks(P); }
 void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, double *f, double *eu,
                      double *ed, double *partial, double *out, unsigned int *ticket, double *dist) {
     // the ticket epilogue sums the residual kernel's own nblk(M) partials
@@ -2367,15 +2690,15 @@ void launch_residual(hipStream_t s, const DevProblem &P, const double *recs, dou
     if (P.rs)
         k_residual<false, false, true><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
-            dist);
+            dist, RedTail());
     else if (P.all_bnd_fast && P.no_lens)
         k_residual<false, true><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
-            dist);
+            dist, RedTail());
     else
         k_residual<false, false><<<nblk(P.M, 256), 256, 0, s>>>(
             P, recs, f, eu, ed, partial, out, ticket, nullptr, nullptr, nullptr, nullptr, nullptr,
-            dist);
+            dist, RedTail());
     if (!ticket && out) k_reduce_sum<<<1, 256, 0, s>>>(partial, residual_blocks(P), out);
 }
 // Per-observation reprojection (FlatScene::evaluate's out_point_list /
@@ -2414,16 +2737,25 @@ void launch_reproject(hipStream_t s, const DevProblem &P, const double *recs, do
 void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, double *f,
                         double *eu, double *ed, double *partial, const double *J,
                         const int *jcol, const int *nloc, const double *pstep,
-                        double *partial_jp, double *dist) {
+                        double *partial_jp, double *dist, const RedTail &T) {
+    if (!T.on && trial_cf_fusable(P)) {  // partials per camera-frame (trial_blocks)
+        if (P.pc_uniform == 6)
+            k_residual_jp_cf<6><<<P.ncf, 256, 0, s>>>(P, recs, f, eu, ed, partial, J, nloc, pstep,
+                                                      partial_jp, dist);
+        else
+            k_residual_jp_cf<7><<<P.ncf, 256, 0, s>>>(P, recs, f, eu, ed, partial, J, nloc, pstep,
+                                                      partial_jp, dist);
+        return;
+    }
     if (P.rs)
         k_residual<true, false, true><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
+            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist, T);
     else if (P.all_bnd_fast && P.no_lens)
         k_residual<true, true><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
+            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist, T);
     else
         k_residual<true, false><<<nblk(P.M, 256), 256, 0, s>>>(
-            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist);
+            P, recs, f, eu, ed, partial, nullptr, nullptr, J, jcol, nloc, pstep, partial_jp, dist, T);
 }
 
 // compute_error_stats (adjust_base.cpp:346-372) on the device: per block the

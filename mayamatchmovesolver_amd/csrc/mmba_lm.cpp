@@ -129,6 +129,11 @@ double Plan::dnorm(const double *dv) {
     return std::sqrt(read_scalar(SL_DNORM));
 }
 
+void Plan::records_enqueue(const double *xat, int base_only) {
+    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, base_only);
+    recs_full_at = base_only ? nullptr : xat;
+}
+
 // iflag = 1: setParameters + measureErrors; ||f||^2 -> SL_FNORM.
 void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed, double *dist,
                        int slot) {
@@ -136,7 +141,9 @@ void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed, dou
     // reuses this parameter pass (params_at)
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, fd_eps());
     params_at = dx;
-    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+    // the full record set (same launch; the variants and perturbed bundle
+    // positions are what a Jacobian at dx reads next)
+    records_enqueue(dx, 0);
     span_begin(SPAN_RESID);
     // stiffness / smoothness rows: their partial goes after the residual blocks
     launch_rows_eval(s, P, df + 2 * (size_t)M, eu ? eu + 2 * (size_t)M : nullptr, d_partial,
@@ -162,10 +169,12 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     // the accepted trial point (or the last evaluation) already set the
     // parameters at dx: external values, FD points and steps are those
     // k_param_set would write, bit for bit (same inputs, same kernel code)
-    if (params_at != dx)
+    if (params_at != dx) {
         launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
+        recs_full_at = nullptr;
+    }
     params_at = dx;
-    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
+    if (recs_full_at != dx) records_enqueue(dx, 0);  // else built by the evaluation at dx
     CentralB CB;
     if (central) {  // the deltaB pass of the central columns
         MMBA_HIP(hipMemsetAsync(d_scalar + SL_NCENT, 0, sizeof(double), s));
@@ -199,6 +208,30 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.cf_base = 0;
         epi.bnd_base = ncf;
     }
+    // unsharded plans with fast bundles: the bundle pass forms the lam = 0
+    // bundle factor the undamped solve reads next (no k_bundle_factor
+    // launch); with MMBA_TAIL_REDUCE=1 its last workgroup also reduces the
+    // epilogue rows
+    const bool fold = fuse && nranks == 1 && P.nbs > 0 && P.JB != nullptr && fold_ok;
+    const bool tail = fold && tail_reduce;
+    lb0_valid = false;
+    if (tail) {
+        epi.fold = 1;
+        epi.scalar = d_scalar;
+        epi.ticket = d_mticket;
+        RedSpec &rf = epi.spec;
+        rf.flag_slot = -1;
+        const int ncol = ncf + (nB_solved > 0 ? (nB + 255) / 256 : 0);  // as below
+        rf.row[rf.nrows++] = {0, ncol, 1, SL_ZERO};
+        if (epi.do_xn) rf.row[rf.nrows++] = {pw, ncol, 0, SL_XN2};
+        if (epi.do_gn) rf.row[rf.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
+    }
+    if (fold && nB_solved > 0) {
+        epi.Lb = d_Lb;
+        epi.tb = d_tb;
+        epi.fail = d_fail;
+        lb0_valid = true;
+    }
     const bool k2_fused = !central && jac_ne_fusable(P, jac_ncv) && !k2_split;
     if (k2_fused) {
         // the local column counts are a property of the plan: stored once
@@ -231,7 +264,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
             launch_reduce_multi(s, d_partial, rs, tail);
             allreduce(tail, 2 + nranks);
             launch_fold_ranks(s, tail, nranks, d_scalar + SL_ZERO, epi.do_xn, epi.do_gn);
-        } else {
+        } else if (!tail) {
             rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
             if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, SL_XN2};
             if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
@@ -279,19 +312,16 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
                       opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
     params_at = d_wa2;  // x <- wa2 on acceptance: the next Jacobian skips k_param_set
-    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+    records_enqueue(d_wa2, 0);  // ... and k_records
     span_begin(SPAN_RESID);
     launch_rows_eval(s, P, d_ftrial + 2 * (size_t)M, eu + 2 * (size_t)M, pr + 2 * (size_t)pw,
                      (M + 255) / 256, d_Jrow, d_wa1, pr + 3 * (size_t)pw);
-    launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
-                       d_wa1, pr + 3 * (size_t)pw, d_dist_t);
-    span_end(SPAN_RESID);
     RedSpec rs{};
     rs.flag_slot = -1;
     rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_PNORM};
     rs.row[rs.nrows++] = {4 * pw, nparts, 0, SL_XN2T};
-    rs.row[rs.nrows++] = {5 * pw, residual_blocks(P), 0, SL_FNORM};
-    rs.row[rs.nrows++] = {6 * pw, residual_blocks(P), 0, SL_JP};
+    rs.row[rs.nrows++] = {5 * pw, trial_blocks(P), 0, SL_FNORM};
+    rs.row[rs.nrows++] = {6 * pw, trial_blocks(P), 0, SL_JP};
     if (fill_dnorm) {  // the undamped solve's ||D xs||^2 and fail flag (solve_damped_enqueue)
         rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_DNORM};
         rs.flag_slot = SL_FAIL;
@@ -299,8 +329,26 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     // unsharded: the LM decision after this trial reads slots [0, SL_LAST],
     // which the reduction's last block mirrors to the host itself
     const bool mirror = host_mirror && nranks == 1;
-    launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr,
-                        mirror ? h_scalar : nullptr, SL_LAST + 1, d_mticket);
+    // MMBA_TAIL_REDUCE=1 (unsharded): the residual pass's last workgroup
+    // runs the reduction launch's work itself (RedTail: same rows, flag and
+    // mirror) -- off by default, see Plan::tail_reduce
+    RedTail T;
+    if (nranks == 1 && tail_reduce) {
+        T.on = 1;
+        T.spec = rs;
+        T.partial = d_partial;
+        T.scalar = d_scalar;
+        T.flag = fill_dnorm ? d_fail : nullptr;
+        T.host = mirror ? h_scalar : nullptr;
+        T.host_n = SL_LAST + 1;
+        T.ticket = d_mticket;
+    }
+    launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
+                       d_wa1, pr + 3 * (size_t)pw, d_dist_t, T);
+    span_end(SPAN_RESID);
+    if (!T.on)
+        launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr,
+                            mirror ? h_scalar : nullptr, SL_LAST + 1, d_mticket);
     mirror_pending = mirror;
     // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
     allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
@@ -324,7 +372,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         // (folding the 3 x 3 factor into k_schur_obs, one factor per
         // observation, measured 34 us against 16 + 6 us: the per-observation
         // square roots and divisions lengthen the latency-bound pass)
-        launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
+        if (!(lam == 0. && lb0_valid))  // else formed by the Jacobian's bundle pass
+            launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
+        lb0_valid = false;
         launch_schur_obs(s, P, d_J, d_Lb, d_W);
     }
     if (nR > 0) {
@@ -650,7 +700,7 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_x, d_f, d_eu, d_ed);
     } else {
-        launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+        records_enqueue(nullptr, 1);
         launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
                          (M + 255) / 256);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
@@ -671,7 +721,7 @@ int Plan::reproject(const double *x, double *point_out, double *marker_out) {
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_x, d_f, d_eu, d_ed);  // parameters set, records current
     } else {
-        launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+        records_enqueue(nullptr, 1);
     }
     launch_reproject(s, P, d_recs, d_ftrial, d_eu_s);
     download_ref_order(d_ftrial, d_eu_s, d_ed_s, point_out, marker_out, nullptr);
@@ -738,7 +788,7 @@ void Plan::jac_partial_stale(const double *dx, int k) {
     const double eps_dif = fd_eps();
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, eps_dif);
     params_at = dx;
-    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 0);
+    records_enqueue(dx, 0);
     CentralB CB;
     if (central) {
         MMBA_HIP(hipMemsetAsync(d_scalar + SL_NCENT, 0, sizeof(double), s));
@@ -783,7 +833,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         // errorDistanceList, which an immediate interrupt leaves in place.
         // Its ||f|| and statistics stay in device slots until the solve's
         // last synchronisation (only the accept-only-better test reads them)
-        launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+        records_enqueue(nullptr, 1);
         launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
                          (M + 255) / 256);
         launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FI, nullptr,

@@ -54,7 +54,7 @@ int Plan::solve_frames(double *x_inout, mmba_result *results, const mmba_callbac
     __atomic_store_n(h_bflag, polls && cb->interrupt(cb->user) ? 1 : 0, __ATOMIC_SEQ_CST);
     attrs_reset();
     // bundle records (no bundle is solved: computed once per call)
-    launch_records(s, P, d_var_cf, d_ext_pert, d_step, d_recs, nvar, d_brec, 1);
+    records_enqueue(nullptr, 1);
     MMBA_HIP(hipMemcpyAsync(d_bx, x_inout, sizeof(double) * n, hipMemcpyHostToDevice, s));
     BatchArgs B{};
     B.nf = batch_nf;

@@ -1284,6 +1284,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     if (const char *e = std::getenv("MMBA_FOLD_SCHUR_INIT")) fold_init = fold_init && std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_K2_FUSED")) k2_split = std::atoi(e) == 0;
+    if (const char *e = std::getenv("MMBA_NE_FOLD")) fold_ok = std::atoi(e) != 0;
+    if (const char *e = std::getenv("MMBA_TAIL_REDUCE")) tail_reduce = std::atoi(e) != 0;
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
     MMBA_HIP(hipHostMalloc(&h_xstage, sizeof(double) * std::max(n, 1)));
     MMBA_HIP(hipStreamSynchronize(s));
