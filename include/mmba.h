@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 3
+#define MMBA_ABI_VERSION 4
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -500,6 +500,9 @@ typedef struct mmba_kernel_stats {
     int32_t dataflow_fallback; /* 1 once a timed-out dataflow wait in the block
                                cyclic reduction switched this plan to the
                                per-level launches (ABI 3)                  */
+    int32_t solve_launch;   /* 1 when this plan runs a solve as ONE
+                               cooperative launch (block-diagonal plans
+                               without callbacks; ABI 4)                  */
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -196,6 +196,7 @@ class MmbaKernelStats(C.Structure):
         ("reduced_dim", C.c_int32),
         ("reduced_kind", C.c_int32),
         ("dataflow_fallback", C.c_int32),
+        ("solve_launch", C.c_int32),
     ]
 
     def as_dict(self):

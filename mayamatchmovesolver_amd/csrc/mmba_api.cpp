@@ -289,6 +289,7 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         out->reduced_dim = p.nR;
         out->reduced_kind = p.band ? (p.bs.use_bd ? 3 : 0) : (p.dense ? 2 : 1);
         out->dataflow_fallback = p.bs.df_off ? 1 : 0;
+        out->solve_launch = p.coop_ok ? 1 : 0;
         // Algorithmic bytes: B_J = 48 + 8 p_c p_b per observation
         // for the Jacobian + normal-equation pass, B_f = 48 per observation for
         // the residual pass.

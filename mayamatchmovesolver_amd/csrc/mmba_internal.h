@@ -133,6 +133,25 @@ struct BatchArgs {
     double delta, factor, ftol, xtol, gtol, initial_error_avg;
 };
 
+// Whole-solve cooperative launch for block-diagonal plans (mmba_lmcoop.hip).
+struct CoopOut {
+    double fnorm;
+    int info, nfev, njev, func_evals, jac_evals, ntrace, failed, aborted;
+};
+struct CoopArgs {
+    const int *cf_off;   // workgroup g owns camera-frames [cf_off[g], cf_off[g + 1])
+    const int *stale;    // stale FD column per frame (B13)
+    const double *pweight;
+    double *x;           // internal parameters, in / out
+    double *f, *ft, *eu, *ed, *dist, *distt, *J;
+    double *part;        // [2][G][8] grid-reduction partials
+    unsigned *ctr, *abort;
+    double *trace;
+    int trace_cap;
+    CoopOut *out;
+    int solver_type, mode, maxfev;
+    double delta, factor, ftol, xtol, gtol;
+};
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
     bool use_bd = false;                     // block diagonal + arrow (no solved bundle)
@@ -210,6 +229,9 @@ struct DevProblem {
     // destination-sorted gathers of k_schur_dest read 2-3 cache lines per
     // observation instead of one line per entry
     int wst;
+    // every pair of a diagonal Schur destination (cf, cf) is (i, i)
+    // (k_schur_dest_u loads one W row for both sides)
+    int dest_diag_ii;
     // bundle-side parameter lists (B-class first, then bundle-side globals)
     const int *bnd_par_off, *bnd_par;
     const int *bnd_pb;     // B-block size

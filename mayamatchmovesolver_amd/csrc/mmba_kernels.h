@@ -1,6 +1,8 @@
 // mmba_kernels.h -- host launch wrappers for the kernels in mmba_kernels.hip.
 #pragma once
 
+#include <vector>
+
 #include "mmba_internal.h"
 
 namespace mmba {
@@ -64,6 +66,12 @@ void launch_dist_stats(hipStream_t s, const DevProblem &P, const double *ed, dou
                        int nparts, int rstride, double *out);
 // launch_residual (partials only) plus ||J p||^2 partials of the same blocks
 // into partial_jp (k_jp_sumsq's sum, one launch)
+// Whole-solve cooperative launch for block-diagonal plans (mmba_lmcoop.hip;
+// CoopArgs / CoopOut in mmba_internal.h).
+bool lm_coop_layout(int ncf, std::vector<int> &cf_off);
+int lm_coop_nfc();
+bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G);
+
 // Reduction launch folded into a producer (unsharded trial point): the
 // producer's last workgroup (ticket) runs k_reduce_multi's work -- the rows
 // of spec (offsets into partial), the fail flag and the host mirror.

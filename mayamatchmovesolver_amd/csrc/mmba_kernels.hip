@@ -2041,6 +2041,9 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
     const int lane = threadIdx.x;
     const bool diag = rhs && cc.x == cc.y && own_cf(P, cc.x);
+    // pairs of a diagonal destination are (i, i) when no observation's
+    // bundle is seen twice in one camera-frame (plan flag, host-checked)
+    const bool same = cc.x == cc.y && P.dest_diag_ii;
     double acc[PC * PC], accr[PC];
 #pragma unroll
     for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
@@ -2062,7 +2065,22 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
         const int2 pr = prk[k];
         if (pr.x < 0) continue;
         double wi[3 * PC], wj[3 * PC];
-        if constexpr ((3 * PC) % 2 == 0) {  // wst = 3 PC: 16-B aligned records
+        if (same) {
+            // diagonal destination: every pair is (i, i) (a bundle is seen
+            // once per camera-frame), so one W row is loaded for both sides
+            if constexpr ((3 * PC) % 2 == 0) {
+                const double2 *pi = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.x)]);
+#pragma unroll
+                for (int k = 0; k < 3 * PC / 2; ++k) {
+                    const double2 a = pi[k];
+                    wi[2 * k] = wj[2 * k] = a.x;
+                    wi[2 * k + 1] = wj[2 * k + 1] = a.y;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3 * PC; ++k) wi[k] = wj[k] = W[widx(P, k, pr.x)];
+            }
+        } else if constexpr ((3 * PC) % 2 == 0) {  // wst = 3 PC: 16-B aligned records
             const double2 *pi = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.x)]);
             const double2 *pj = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.y)]);
 #pragma unroll

@@ -885,6 +885,70 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         info = -1;
         goto TERMINATE;
     }
+    // block-diagonal plans: the whole solve as one cooperative launch (no
+    // host decision point per iteration); callbacks keep the host loop
+    if (coop_ok && !central && !polls && !(cb && cb->progress)) {
+        if (!measured) records_enqueue(nullptr, 1);  // bundle positions at the scene's values
+        CoopArgs A{};
+        A.cf_off = d_coop_cf_off;
+        A.stale = d_stale;
+        A.pweight = d_pweight;
+        A.x = d_x;
+        A.f = d_f;
+        A.ft = d_ftrial;
+        A.eu = d_eu;
+        A.ed = d_ed;
+        A.dist = d_dist_x;
+        A.distt = d_dist_t;
+        A.J = d_J;
+        A.part = d_coop_part;
+        A.ctr = d_coop_sync;
+        A.abort = d_coop_sync + 1;
+        A.trace = d_coop_trace;
+        A.trace_cap = COOP_TRACE;
+        A.out = d_coop_out;
+        A.solver_type = opt.solver_type;
+        A.mode = mode;
+        A.maxfev = maxfev;
+        A.delta = opt.delta;
+        A.factor = factor;
+        A.ftol = ftol;
+        A.xtol = xtol;
+        A.gtol = gtol;
+        MMBA_HIP(hipMemsetAsync(d_coop_sync, 0, 2 * sizeof(unsigned), s));
+        const double t0 = wall_now();
+        if (launch_lm_coop(s, P, A, coop_G)) {
+            MMBA_HIP(hipMemcpyAsync(h_coop_out, d_coop_out, sizeof(CoopOut), hipMemcpyDeviceToHost,
+                                    s));
+            MMBA_HIP(hipStreamSynchronize(s));
+            const CoopOut o = *h_coop_out;
+            t_jac += wall_now() - t0;
+            if (o.aborted) {
+                set_error("cooperative solve: a grid reduction timed out");
+                throw DeviceError();
+            }
+            if (o.failed) {
+                set_error("damped normal-equation factorisation failed (cooperative solve)");
+                throw DeviceError();
+            }
+            if (trace && o.ntrace > 0) {
+                std::vector<double> tr(std::min(o.ntrace, COOP_TRACE));
+                MMBA_HIP(hipMemcpy(tr.data(), d_coop_trace, sizeof(double) * tr.size(),
+                                   hipMemcpyDeviceToHost));
+                for (int k = 0; k < o.ntrace; ++k) push_trace(k < (int)tr.size() ? tr[k] : 0.);
+            }
+            info = o.info;
+            nfev = o.nfev;
+            njev = o.njev;
+            func_evals = o.func_evals;
+            jac_evals = o.jac_evals;
+            fnorm = o.fnorm;
+            dist_ok = true;
+            x0_eval = true;
+            goto TERMINATE;
+        }
+        coop_ok = false;  // not co-resident on this device: the host loop from now on
+    }
     // x0's evaluation, enqueued: its ||f|| reaches the host with the first
     // decision point's slots, and the first Jacobian's gnorm reads it on the
     // device (JacLM::fnorm_sq) -- no synchronisation before the Jacobian

@@ -82,6 +82,7 @@ Plan::~Plan() {
     if (h_fail) (void)hipHostFree(h_fail);
     if (h_bflag) (void)hipHostFree(h_bflag);
     if (h_xstage) (void)hipHostFree(h_xstage);
+    if (h_coop_out) (void)hipHostFree(h_coop_out);
 }
 
 static void require(bool c, const char *what) {
@@ -783,6 +784,14 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             dest_diag_all = true;
             for (int cf = 0; cf < ncf; ++cf)
                 if (cf_pc[cf] > 0 && !hasd[cf]) dest_diag_all = false;
+            dest_diag_ii = true;
+            for (size_t d = 0; d < dest_h.size() && dest_diag_ii; ++d)
+                if (dest_h[d].x == dest_h[d].y)
+                    for (int q = dest_off_h[d]; q < dest_off_h[d + 1]; ++q)
+                        if (dpairs_h[q].x != dpairs_h[q].y) {
+                            dest_diag_ii = false;
+                            break;
+                        }
         }
     }
     {
@@ -885,6 +894,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         }
     }
     D.nbs = nB_solved;
+    D.dest_diag_ii = dest_diag_ii ? 1 : 0;
     D.all_bnd_fast = 1;
     for (int b = 0; b < nB; ++b)
         if (bnd_p4[b].w < 0) D.all_bnd_fast = 0;
@@ -1286,6 +1296,35 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     if (const char *e = std::getenv("MMBA_K2_FUSED")) k2_split = std::atoi(e) == 0;
     if (const char *e = std::getenv("MMBA_NE_FOLD")) fold_ok = std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_TAIL_REDUCE")) tail_reduce = std::atoi(e) != 0;
+    {
+        // the cooperative whole-solve launch (mmba_lmcoop.hip): every
+        // parameter is a camera-frame parameter of its own block, no
+        // bundle-side variants, blocks of <= 8 parameters, <= 4 camera-frames
+        // per workgroup on <= 256 workgroups
+        bool ok = nG == 0 && nB_solved == 0 && nrows == 0 && !rs_on && nranks == 1 && n > 0 &&
+                  n == nCF;
+        for (int p = 0; p < n && ok; ++p) ok = p_class[p] == PC_CF;
+        for (size_t t = 0; t < cf_var_flags.size() && ok; ++t) ok = cf_var_flags[t] == 0;
+        for (int cf = 0; cf < ncf && ok; ++cf)
+            ok = cf_var_off[cf + 1] - cf_var_off[cf] - 1 == cf_pc[cf] && cf_pc[cf] <= lm_coop_nfc();
+        std::vector<int> off;
+        if (ok) ok = lm_coop_layout(ncf, off);
+        // opt-in while the one-workgroup-per-camera-frame layout is slower
+        // than the host loop on C2 (1.38 vs ~0.8 ms per solve: 120
+        // workgroups of 1,656 observations each leave half the chip idle)
+        const char *e = std::getenv("MMBA_LM_COOP");
+        ok = ok && e && std::atoi(e) != 0;
+        if (ok) {
+            coop_ok = true;
+            coop_G = (int)off.size() - 1;
+            d_coop_cf_off = upload(off);
+            d_coop_part = dalloc<double>((size_t)2 * coop_G * 8);
+            d_coop_trace = dalloc<double>(COOP_TRACE);
+            d_coop_sync = dalloc<unsigned>(2);
+            d_coop_out = dalloc<CoopOut>(1);
+            MMBA_HIP(hipHostMalloc(&h_coop_out, sizeof(CoopOut)));
+        }
+    }
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
     MMBA_HIP(hipHostMalloc(&h_xstage, sizeof(double) * std::max(n, 1)));
     MMBA_HIP(hipStreamSynchronize(s));

@@ -104,6 +104,16 @@ struct Plan {
     // +7 us): 782 / 196 arrivals on one device-scope counter cost more than
     // the launch they save (MI355X guide "fanin", ~12 ns per atomic)
     bool tail_reduce = false;
+    // block-diagonal plans (every parameter on one camera-frame, no solved
+    // bundle, no global): the whole solve as one cooperative launch
+    // (mmba_lmcoop.hip); MMBA_LM_COOP=0 keeps the host-driven loop
+    bool coop_ok = false;
+    int coop_G = 0;
+    int *d_coop_cf_off = nullptr;
+    double *d_coop_part = nullptr, *d_coop_trace = nullptr;
+    unsigned *d_coop_sync = nullptr;
+    CoopOut *d_coop_out = nullptr, *h_coop_out = nullptr;
+    static constexpr int COOP_TRACE = 4096;
     int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
@@ -182,7 +192,7 @@ struct Plan {
     bool host_mirror = false, mirror_pending = false;
     // every solved camera-frame has a diagonal Schur destination; fold_init:
     // k_schur_init rides in k_schur_dest_u (SchurInitFold)
-    bool dest_diag_all = false, fold_init = false;
+    bool dest_diag_all = false, fold_init = false, dest_diag_ii = false;
     double *h_xstage = nullptr;  // pinned [n]: x in / out without a blocking pageable copy
     int *h_fail = nullptr;       // pinned
 
