@@ -139,7 +139,13 @@ struct CoopOut {
     int info, nfev, njev, func_evals, jac_evals, ntrace, failed, aborted;
 };
 struct CoopArgs {
-    const int *cf_off;   // workgroup g owns camera-frames [cf_off[g], cf_off[g + 1])
+    // workgroup g: observations [slice_off[g], slice_off[g + 1]) over the
+    // slice_ncf[g] camera-frames from slice_cf[g]; it owns camera-frames g,
+    // g + G, ...; cf_src[cf_src_off[cf] ..] = the slots (g * SLM + local
+    // camera-frame) holding camera-frame cf's normal-equation partials
+    const int *slice_off, *slice_cf, *slice_ncf, *cf_src_off, *cf_src;
+    double *nep;         // [G * SLM][KJC] normal-equation partials
+    double *xs;          // [n] damped step (owners -> slices)
     const int *stale;    // stale FD column per frame (B13)
     const double *pweight;
     double *x;           // internal parameters, in / out
@@ -150,6 +156,7 @@ struct CoopArgs {
     int trace_cap;
     CoopOut *out;
     int solver_type, mode, maxfev;
+    int pad;
     double delta, factor, ftol, xtol, gtol;
 };
 // Device buffers of the (partitioned) band factorisation.

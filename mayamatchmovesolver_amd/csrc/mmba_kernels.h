@@ -25,9 +25,13 @@ struct RedSpec {
     int flag_slot;
     RedRow row[8];
 };
+// host (optional): the last block copies scalar[0, host_n) into that
+// page-locked mirror and then stores seq into *host_seq (system scope,
+// release): the LM thread polls that word instead of a stream event.
 void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
                          double *scalar, int *flag = nullptr, double *host = nullptr,
-                         int host_n = 0, unsigned *ticket = nullptr);
+                         int host_n = 0, unsigned *ticket = nullptr,
+                         unsigned *host_seq = nullptr, unsigned seq = 0);
 // lmder bookkeeping after the normal equations (column norms, rank test, diag
 // update, ||D x||, gnorm): partial rows 0 / 1 / 2 (rstride apart, nparts each)
 void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
@@ -68,9 +72,15 @@ void launch_dist_stats(hipStream_t s, const DevProblem &P, const double *ed, dou
 // into partial_jp (k_jp_sumsq's sum, one launch)
 // Whole-solve cooperative launch for block-diagonal plans (mmba_lmcoop.hip;
 // CoopArgs / CoopOut in mmba_internal.h).
-bool lm_coop_layout(int ncf, std::vector<int> &cf_off);
+struct CoopLayout {
+    int G = 0;
+    std::vector<int> slice_off, slice_cf, slice_ncf, cf_src_off, cf_src;
+};
+bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, CoopLayout &L);
 int lm_coop_nfc();
-bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G);
+int lm_coop_slots();
+int lm_coop_kj();
+bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G, bool lens);
 
 // Reduction launch folded into a producer (unsharded trial point): the
 // producer's last workgroup (ticket) runs k_reduce_multi's work -- the rows

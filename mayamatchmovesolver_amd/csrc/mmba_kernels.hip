@@ -1678,7 +1678,8 @@ __global__ void __launch_bounds__(256) k_trial_prep(
 __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__ partial,
                                                       RedSpec spec, double *scalar, int *flag,
                                                       double *host, int host_n,
-                                                      unsigned *ticket) {
+                                                      unsigned *ticket, unsigned *host_seq,
+                                                      unsigned seq) {
     __shared__ double red[256];
     const RedRow rw = spec.row[blockIdx.x];
     const double v = reduce_row_block<false>(partial, rw, red);
@@ -1703,6 +1704,15 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     for (int i = threadIdx.x; i < host_n; i += blockDim.x)
         host[i] = __hip_atomic_load(&scalar[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host_seq) {
+        // the mirror's writes, then its sequence word (the host polls it)
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2673,10 +2683,11 @@ void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, con
                                         solver_type, delta, eps_dif, mask, partial, rstride);
 }
 void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
-                         double *scalar, int *flag, double *host, int host_n, unsigned *ticket) {
+                         double *scalar, int *flag, double *host, int host_n, unsigned *ticket,
+                         unsigned *host_seq, unsigned seq) {
     if (spec.nrows > 0)
         k_reduce_multi<<<spec.nrows, 256, 0, s>>>(partial, spec, scalar, flag, host, host_n,
-                                                   ticket);
+                                                   ticket, host_seq, seq);
 }
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);

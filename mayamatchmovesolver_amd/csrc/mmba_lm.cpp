@@ -84,6 +84,26 @@ void Plan::collect_spans() {
 void Plan::read_slots(int lo, int hi) {
     const bool mirrored = mirror_pending && lo == 0 && hi == SL_LAST;
     mirror_pending = false;
+    const bool by_seq = mirrored && seq_pending;
+    seq_pending = false;
+    if (by_seq) {
+        // the reduction's last block wrote the mirror, then the sequence
+        // word (system-scope release): poll page-locked memory directly --
+        // a stream event query costs microseconds per call.  The stream is
+        // checked now and then, so a failed launch ends the wait.
+        for (unsigned spins = 1;; ++spins) {
+            if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq_next) return;
+            if ((spins & 4095u) == 0) {
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipSuccess) {
+                    if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq_next) return;
+                    set_error("mirrored reduction finished without its sequence word");
+                    throw DeviceError();
+                }
+                if (e != hipErrorNotReady) MMBA_HIP(e);
+            }
+        }
+    }
     if (!mirrored)
         MMBA_HIP(hipMemcpyAsync(h_scalar + lo, d_scalar + lo, sizeof(double) * (hi - lo + 1),
                                 hipMemcpyDeviceToHost, s));
@@ -346,9 +366,14 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
                        d_wa1, pr + 3 * (size_t)pw, d_dist_t, T);
     span_end(SPAN_RESID);
-    if (!T.on)
+    if (!T.on) {
+        const bool sq = mirror && seq_poll;
+        if (sq) ++seq_next;
         launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr,
-                            mirror ? h_scalar : nullptr, SL_LAST + 1, d_mticket);
+                            mirror ? h_scalar : nullptr, SL_LAST + 1, d_mticket,
+                            sq ? h_seq : nullptr, seq_next);
+        seq_pending = sq;
+    }
     mirror_pending = mirror;
     // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
     allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
@@ -890,7 +915,13 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     if (coop_ok && !central && !polls && !(cb && cb->progress)) {
         if (!measured) records_enqueue(nullptr, 1);  // bundle positions at the scene's values
         CoopArgs A{};
-        A.cf_off = d_coop_cf_off;
+        A.slice_off = d_coop_slice_off;
+        A.slice_cf = d_coop_slice_cf;
+        A.slice_ncf = d_coop_slice_ncf;
+        A.cf_src_off = d_coop_src_off;
+        A.cf_src = d_coop_src;
+        A.nep = d_coop_nep;
+        A.xs = d_coop_xs;
         A.stale = d_stale;
         A.pweight = d_pweight;
         A.x = d_x;
@@ -917,7 +948,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         A.gtol = gtol;
         MMBA_HIP(hipMemsetAsync(d_coop_sync, 0, 2 * sizeof(unsigned), s));
         const double t0 = wall_now();
-        if (launch_lm_coop(s, P, A, coop_G)) {
+        if (launch_lm_coop(s, P, A, coop_G, coop_lens)) {
             MMBA_HIP(hipMemcpyAsync(h_coop_out, d_coop_out, sizeof(CoopOut), hipMemcpyDeviceToHost,
                                     s));
             MMBA_HIP(hipStreamSynchronize(s));

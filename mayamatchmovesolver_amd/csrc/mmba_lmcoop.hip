@@ -34,9 +34,11 @@ namespace mmba {
 namespace {
 
 constexpr int CT = 256;    // threads per workgroup
-constexpr int CPB = 4;     // camera-frames per workgroup (one wave each in lmpar)
+constexpr int CPB = 4;     // camera-frames owned per workgroup (one wave each in lmpar)
+constexpr int SLM = 4;     // camera-frames touched by one workgroup's observation slice
 constexpr int NFC = 8;     // parameters per camera-frame (lanes of the solve)
 constexpr int NRED = 8;    // values per grid reduction
+constexpr int KJC = NFC * (NFC + 1) / 2 + NFC;  // J^T J lower triangle + J^T f
 
 typedef __attribute__((address_space(1))) unsigned long long cg_u64;
 typedef __attribute__((address_space(1))) unsigned int cg_u32;
@@ -112,14 +114,32 @@ __device__ __forceinline__ void cg_block_reduce(const double (&v)[NV], double (*
 // One cooperative launch: the solve of Plan::solve from x0's evaluation to
 // termination.  The caller has reset the attribute block, built the bundle
 // records and (accept-only-better) enqueued the initial measurement.
+//
+// Two roles per workgroup g:
+//   slice  observations [slice_off[g], slice_off[g + 1]) (balanced, cut
+//          anywhere; <= SLM camera-frames): setParameters of their
+//          camera-frames, their camera records, residuals, FD Jacobian rows,
+//          and J^T J / J^T f partials per camera-frame slot -> A.nep
+//   owner  camera-frames g, g + G, ... (<= CPB): sums the slots of each
+//          (A.cf_src, in workgroup order), the lmder epilogue of its
+//          parameters and the damped solves (one wave per camera-frame);
+//          its steps xs go to A.xs for the slices' trial points.
+// Both roles keep their own copy of the parameters they touch and update it
+// with the same operations, so no owner-to-slice hand-off of x is needed.
+template <bool LENS>
 __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
-    constexpr int KA = NFC * (NFC + 1) / 2, KJ = KA + NFC;
-    __shared__ double s_rec[CPB][NFC + 1][CAMREC];
+    constexpr int KA = NFC * (NFC + 1) / 2, KJ = KJC;
+    // slice role
+    __shared__ double s_rec[SLM][NFC + 1][CAMREC];
+    __shared__ double s_sx[SLM * NFC], s_swa2[SLM * NFC], s_swa1[SLM * NFC];
+    __shared__ double s_extp[SLM * NFC], s_step[SLM * NFC];
+    __shared__ int s_sp[SLM * NFC];
+    __shared__ long long s_vidx[SLM * NFC];
+    // owner role
     __shared__ double s_A[CPB][NFC * NFC];
-    __shared__ double s_g[CPB * NFC], s_x[CPB * NFC], s_diag[CPB * NFC], s_xs[CPB * NFC];
-    __shared__ double s_wa1[CPB * NFC], s_wa2[CPB * NFC], s_extp[CPB * NFC], s_step[CPB * NFC];
-    __shared__ int s_p[CPB * NFC];
-    __shared__ long long s_vidx[CPB * NFC];
+    __shared__ double s_g[CPB * NFC], s_ox[CPB * NFC], s_diag[CPB * NFC], s_xs[CPB * NFC];
+    __shared__ double s_owa2[CPB * NFC];
+    __shared__ int s_op[CPB * NFC];
     static_assert(KJ <= 4 * NRED + 12, "reduction scratch");
     __shared__ double s_red[4][4 * NRED + 12];
     __shared__ double s_gv[NRED];  // this workgroup's grid-reduction partials, then the totals
@@ -127,32 +147,42 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
 
     const int G = gridDim.x, g = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int cf0 = A.cf_off[g], ncl = A.cf_off[g + 1] - cf0;  // ncl <= CPB
+    const int scf0 = A.slice_cf[g], nsl = A.slice_ncf[g];  // slice camera-frames
+    const int so0 = A.slice_off[g], so1 = A.slice_off[g + 1];
+    const int ncf = P.ncf;
+    int nown = 0;  // owned camera-frames g, g + G, ...
+    for (int c = g; c < ncf && nown < CPB; c += G) ++nown;
     const bool lmder = A.solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     const double eps_dif = sqrt(fmax(fabs(A.delta), DBL_EPSILON));
     const Override none{-1, 0.};
 
-    // local parameter k = c * NFC + a: parameter a of camera-frame cf0 + c
-    if (tid < CPB * NFC) {
+    // parameter a of local camera-frame c at index c * NFC + a (both roles)
+    if (tid < SLM * NFC) {
         const int c = tid / NFC, a = tid % NFC;
         int p = -1;
-        if (c < ncl && a < P.cf_pc[cf0 + c]) p = P.cf_var_param[P.cf_var_off[cf0 + c] + 1 + a];
-        s_p[tid] = p;
+        if (c < nsl && a < P.cf_pc[scf0 + c]) p = P.cf_var_param[P.cf_var_off[scf0 + c] + 1 + a];
+        s_sp[tid] = p;
+        s_vidx[tid] = -1;
+        s_sx[tid] = 0.;
         if (p >= 0) {
             const int at = P.p_attr[p];
             s_vidx[tid] = P.attr_off[at] + (P.attr_anim[at] ? P.p_frame[p] : 0);
-            s_x[tid] = A.x[p];
-            s_diag[tid] = A.mode == 2 ? A.pweight[p] : 0.;
-        } else {
-            s_vidx[tid] = -1;
-            s_x[tid] = 0.;
-            s_diag[tid] = 0.;
+            s_sx[tid] = A.x[p];
         }
+    } else if (tid >= 64 && tid < 64 + CPB * NFC) {
+        const int k = tid - 64, c = k / NFC, a = k % NFC;
+        const int cf = g + c * G;
+        int p = -1;
+        if (c < nown && a < P.cf_pc[cf]) p = P.cf_var_param[P.cf_var_off[cf] + 1 + a];
+        s_op[k] = p;
+        s_ox[k] = p >= 0 ? A.x[p] : 0.;
+        s_diag[k] = (p >= 0 && A.mode == 2) ? A.pweight[p] : 0.;
     }
     if (tid == 0) s_abort = 0;
     __syncthreads();
 
-    // ---- grid reduction: nv values in s_gv (sum, or max where is_max) ----
+    // ---- grid reduction of nv values in s_gv (sum, or max where bit v of
+    // maxmask); nv = 0: a plain grid barrier ----
     unsigned round = 0;
     auto grid_reduce = [&](int nv, unsigned maxmask) {
         double *part = A.part + (size_t)(round & 1) * G * NRED;
@@ -193,31 +223,40 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         ++round;
         return s_abort != 0;
     };
+
     auto record = [&](int c, int k, double *rec) {
-        const int cf = cf0 + c;
+        const int cf = scf0 + c;
         if (P.cf_aidx) {
             camera_record_fast(P, cf, k < 0 ? -1ll : s_vidx[k], k < 0 ? 0. : s_extp[k], rec);
         } else {
-            const Override ov = k < 0 ? none : Override{P.p_attr[s_p[k]], s_extp[k]};
+            const Override ov = k < 0 ? none : Override{P.p_attr[s_sp[k]], s_extp[k]};
             camera_record(P, P.cf_cam[cf], P.cf_frame[cf], ov, rec);
         }
     };
     auto resid_at = [&](int i, const double *rec) {
-        const int b = P.obs_bnd[i], fr = P.obs_frame[i], cam = P.obs_cam[i];
+        const int b = P.obs_bnd[i], fr = P.obs_frame[i];
         double bp[3];
         base_bundle(P, b, fr, bp);
-        double lc[MMBA_LENS_NUM_ATTRS];
-        int lens = -1;
-        const int hl = obs_lens(P, cam, lens);
-        if (hl) lens_coeffs(P, lens, fr, none, lc);
-        return residual_l(P, rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i], hl,
-                          lc);
+        if constexpr (LENS) {
+            double lc[MMBA_LENS_NUM_ATTRS];
+            int lens = -1;
+            const int hl = obs_lens(P, P.obs_cam[i], lens);
+            if (hl) lens_coeffs(P, lens, fr, none, lc);
+            return residual_l(P, rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i],
+                              hl, lc);
+        } else {
+            return residual_l(P, rec, bp, P.obs_xy[2 * i], P.obs_xy[2 * i + 1], P.obs_sqrtw[i],
+                              MMBA_LENS_NONE, nullptr);
+        }
     };
-    // setParameters of this workgroup's parameters at xv (its records read
-    // them next; no other workgroup reads them)
+    // the slice's observations of local camera-frame c
+    auto obs_lo = [&](int c) { return max(so0, P.cf_obs_off[scf0 + c]); };
+    auto obs_hi = [&](int c) { return min(so1, P.cf_obs_off[scf0 + c + 1]); };
+    // setParameters of the slice's camera-frames at xv (its own records read
+    // them next; other workgroups write the same values for shared ones)
     auto set_params = [&](const double *xv) {
-        if (tid < CPB * NFC && s_p[tid] >= 0) {
-            const int p = s_p[tid];
+        if (tid < SLM * NFC && s_sp[tid] >= 0) {
+            const int p = s_sp[tid];
             P.attr_val[s_vidx[tid]] =
                 int_to_ext(xv[tid], P.p_min[p], P.p_max[p], P.p_off[p], P.p_scale[p]);
         }
@@ -226,17 +265,16 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         __threadfence();
     };
 
-    // measureErrors at xv: fvec -> fo, errorList -> eu / ed, distances -> dist;
-    // partials [||f||^2, ||J p||^2 (pv)] -> s_gv[0, 1]
+    // measureErrors of the slice at xv: fvec -> fo, errorList -> eu / ed,
+    // distances -> dist; partials [||f||^2, ||J p||^2 (pv)] -> s_gv[0, 1]
     auto eval = [&](const double *xv, const double *pv, double *fo, double *dist) {
         set_params(xv);
-        if (tid < ncl) record(tid, -1, s_rec[tid][0]);
+        if (tid < nsl) record(tid, -1, s_rec[tid][0]);
         __syncthreads();
         double v[2] = {0., 0.};
-        for (int c = 0; c < ncl; ++c) {
-            const int cf = cf0 + c;
-            const int pc = P.cf_pc[cf];
-            for (int i = P.cf_obs_off[cf] + tid; i < P.cf_obs_off[cf + 1]; i += CT) {
+        for (int c = 0; c < nsl; ++c) {
+            const int pc = P.cf_pc[scf0 + c];
+            for (int i = obs_lo(c) + tid; i < obs_hi(c); i += CT) {
                 const Resid r = resid_at(i, s_rec[c][0]);
                 fo[2 * i] = r.ex;
                 fo[2 * i + 1] = r.ey;
@@ -259,12 +297,14 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         cg_block_reduce<2, 0u>(v, s_red, s_gv);
     };
 
-    // FD Jacobian at s_x: J^T J blocks -> s_A, J^T f -> s_g, rows -> A.J;
-    // errorList / errorDistanceList of the frame's stale column (B13)
+    // FD Jacobian rows of the slice at s_sx -> A.J; J^T J / J^T f of each
+    // slice camera-frame -> A.nep[g * SLM + c] (write-through: the owners read
+    // them after the next grid barrier); errorList / errorDistanceList of the
+    // frame's stale column (B13)
     auto jacobian = [&]() {
-        if (tid < CPB * NFC && s_p[tid] >= 0) {
-            const int p = s_p[tid];
-            const double v = s_x[tid], xmin = P.p_min[p], xmax = P.p_max[p];
+        if (tid < SLM * NFC && s_sp[tid] >= 0) {
+            const int p = s_sp[tid];
+            const double v = s_sx[tid], xmin = P.p_min[p], xmax = P.p_max[p];
             const double off = P.p_off[p], sc = P.p_scale[p];
             double st;
             const double xp = fd_point(v, xmin, xmax, A.solver_type, A.delta, eps_dif, st);
@@ -276,22 +316,20 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         __syncthreads();
         __threadfence();
         // records: thread c (1 + NFC) + k: camera-frame c, k = 0 base, k > 0 variant k - 1
-        if (tid < CPB * (NFC + 1)) {
+        if (tid < SLM * (NFC + 1)) {
             const int c = tid / (NFC + 1), k = tid % (NFC + 1);
-            if (c < ncl && (k == 0 || s_p[c * NFC + k - 1] >= 0))
+            if (c < nsl && (k == 0 || s_sp[c * NFC + k - 1] >= 0))
                 record(c, k == 0 ? -1 : c * NFC + k - 1, s_rec[c][k]);
         }
-        for (int t = tid; t < CPB * NFC * NFC; t += CT) s_A[t / (NFC * NFC)][t % (NFC * NFC)] = 0.;
-        if (tid < CPB * NFC) s_g[tid] = 0.;
         __syncthreads();
-        for (int c = 0; c < ncl; ++c) {
-            const int cf = cf0 + c;
+        for (int c = 0; c < nsl; ++c) {
+            const int cf = scf0 + c;
             const int pc = P.cf_pc[cf];
             const int pstale = A.stale[P.cf_frame[cf]];
             double acc[KJ];
 #pragma unroll
             for (int q = 0; q < KJ; ++q) acc[q] = 0.;
-            for (int i = P.cf_obs_off[cf] + tid; i < P.cf_obs_off[cf + 1]; i += CT) {
+            for (int i = obs_lo(c) + tid; i < obs_hi(c); i += CT) {
                 const Resid r0 = resid_at(i, s_rec[c][0]);
                 Resid rs = r0;
                 double jx[NFC], jy[NFC];
@@ -310,7 +348,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                             jx[a] = (r.ex - r0.ex) / st;
                             jy[a] = (r.ey - r0.ey) / st;
                         }
-                        if (s_p[k] == pstale) rs = r;
+                        if (s_sp[k] == pstale) rs = r;
                     }
                 }
                 double *Jr = &A.J[(size_t)i * 2 * NFC];
@@ -339,8 +377,26 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
             __syncthreads();
             if (tid < KJ) {
                 const double v = (s_red[0][tid] + s_red[1][tid]) + (s_red[2][tid] + s_red[3][tid]);
-                if (tid < KA) {
-                    int a = 0, t = tid;
+                cg_st(&A.nep[((size_t)g * SLM + c) * KJ + tid], v);
+            }
+            __syncthreads();
+        }
+    };
+
+    // owner: J^T J / J^T f of the owned camera-frames from the slices' slots
+    // (in workgroup order) -> s_A, s_g
+    auto assemble = [&]() {
+        for (int t = tid; t < CPB * NFC * NFC; t += CT) s_A[t / (NFC * NFC)][t % (NFC * NFC)] = 0.;
+        __syncthreads();
+        if (tid < CPB * KJ) {
+            const int c = tid / KJ, q = tid % KJ;
+            if (c < nown) {
+                const int cf = g + c * G, pc = P.cf_pc[cf];
+                double v = 0.;
+                for (int u = A.cf_src_off[cf]; u < A.cf_src_off[cf + 1]; ++u)
+                    v += cg_ld(&A.nep[(size_t)A.cf_src[u] * KJ + q]);
+                if (q < KA) {
+                    int a = 0, t = q;
                     while (t > a) {
                         t -= a + 1;
                         ++a;
@@ -349,25 +405,26 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                         s_A[c][a * NFC + t] = v;
                         s_A[c][t * NFC + a] = v;
                     }
-                } else if (tid - KA < pc) {
-                    s_g[c * NFC + tid - KA] = v;
+                } else if (q - KA < pc) {
+                    s_g[c * NFC + q - KA] = v;
                 }
             }
-            __syncthreads();
         }
+        __syncthreads();
     };
 
-    // damped solve of every local camera-frame block (wave c): (A_c + lam
-    // D_c^2) xs_c = g_c; partials [||D xs||^2, pivot failure] -> s_gv[0, 1].
-    // The factor stays in the wave's registers for newton().
+    // owner: damped solve of every owned camera-frame block (wave c):
+    // (A_c + lam D_c^2) xs_c = g_c -> s_xs and A.xs (write-through);
+    // partials [||D xs||^2, pivot failure] -> s_gv[0, 1].  The factor stays
+    // in the wave's registers for newton().
     double fa[NFC];
     double frs = 0., fxs = 0.;
     auto solve = [&](double lam) {
         bool bad = false;
         double dn = 0.;
-        if (wv < ncl) {
+        if (wv < nown) {
             const int c = wv;
-            const int pc = P.cf_pc[cf0 + c];
+            const int pc = P.cf_pc[g + c * G];
             const double dk = lane < pc ? s_diag[c * NFC + lane] : 0.;
 #pragma unroll
             for (int col = 0; col < NFC; ++col) {
@@ -405,7 +462,10 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                 }
             }
             fxs = lane < pc ? acc : 0.;
-            if (lane < NFC) s_xs[c * NFC + lane] = fxs;
+            if (lane < NFC) {
+                s_xs[c * NFC + lane] = fxs;
+                if (lane < pc) cg_st(&A.xs[s_op[c * NFC + lane]], fxs);
+            }
             const double v = dk * fxs;
             dn = cg_wsum(lane < pc ? v * v : 0.);
             bad = __builtin_amdgcn_ballot_w64(bad) != 0;
@@ -418,7 +478,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         if (tid == 0) {
             double d = 0., b = 0.;
             for (int w = 0; w < CT / 64; ++w)
-                if (w < ncl) {
+                if (w < nown) {
                     d += s_red[w][0];
                     b = fmax(b, s_red[w][1]);
                 }
@@ -427,13 +487,13 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         }
         __syncthreads();
     };
-    // sum over local blocks of ||C^-1 v||^2, v = D (D xs / dxnorm), with the
-    // factors of the last solve -> s_gv[0]
+    // owner: sum over owned blocks of ||C^-1 v||^2, v = D (D xs / dxnorm),
+    // with the factors of the last solve -> s_gv[0]
     auto newton = [&](double dxn) {
         double nsq = 0.;
-        if (wv < ncl) {
+        if (wv < nown) {
             const int c = wv;
-            const int pc = P.cf_pc[cf0 + c];
+            const int pc = P.cf_pc[g + c * G];
             const double dk = lane < pc ? s_diag[c * NFC + lane] : 0.;
             double acc = lane < pc ? dk * ((dk * fxs) / dxn) : 0.;
 #pragma unroll
@@ -451,7 +511,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         if (tid == 0) {
             double d = 0.;
             for (int w = 0; w < CT / 64; ++w)
-                if (w < ncl) d += s_red[w][0];
+                if (w < nown) d += s_red[w][0];
             s_gv[0] = d;
         }
         __syncthreads();
@@ -470,7 +530,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
 
     nfev = 1;
     fe = 1;
-    eval(s_x, nullptr, A.f, A.dist);  // x0 (lmder's first fcn call)
+    eval(s_sx, nullptr, A.f, A.dist);  // x0 (lmder's first fcn call)
     aborted = grid_reduce(1, 0u);
     fnorm = sqrt(s_gv[0]);
     trace(fnorm);
@@ -481,10 +541,15 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         je += P.n;
         if (!lmder) nfev += P.n;
         const bool first = iter == 1;
+        aborted = grid_reduce(0, 0u);  // every slot stored
+        if (aborted) break;
+        assemble();
         {
-            // lmder after qrfac: column norms, diag, ||D x||, gnorm, rank flag
+            // lmder after qrfac: column norms, diag, ||D x||, gnorm, rank
+            // flag -- and the undamped solve lmpar starts from, in the same
+            // reduction
             double xn = 0., gm = 0., zf = 0.;
-            if (tid < CPB * NFC && s_p[tid] >= 0) {
+            if (tid < CPB * NFC && s_op[tid] >= 0) {
                 const int c = tid / NFC, a = tid % NFC;
                 const double an = sqrt(s_A[c][a * NFC + a]);
                 double dg = s_diag[tid];
@@ -493,14 +558,25 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                     dg = fmax(dg, an);
                     s_diag[tid] = dg;
                 }
-                const double v = dg * s_x[tid];
+                const double v = dg * s_ox[tid];
                 xn = v * v;
                 if (an == 0.) zf = 1.;
                 if (fnorm != 0. && an != 0.) gm = fabs((s_g[tid] / fnorm) / an);
             }
             const double vv[3] = {xn, gm, zf};
             cg_block_reduce<3, 6u>(vv, s_red, s_gv);
-            aborted = grid_reduce(3, 6u);
+            const double b0 = s_gv[0], b1 = s_gv[1], b2 = s_gv[2];
+            __syncthreads();
+            solve(0.);
+            if (tid == 0) {
+                s_gv[3] = s_gv[0];  // ||D xs||^2 of the undamped step
+                s_gv[4] = s_gv[1];  // its pivot flag
+                s_gv[0] = b0;
+                s_gv[1] = b1;
+                s_gv[2] = b2;
+            }
+            __syncthreads();
+            aborted = grid_reduce(5, 2u | 4u | 16u);
         }
         if (aborted) break;
         const bool rank_def = s_gv[2] != 0.;
@@ -510,6 +586,8 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
             if (delta == 0.) delta = A.factor;
         }
         gnorm = fnorm != 0. ? s_gv[1] : 0.;
+        double dn0 = s_gv[3], bad0 = s_gv[4];
+        bool pre = true;  // the undamped solve of this Jacobian is current
         __syncthreads();
         if (gnorm <= A.gtol) info = 4;
         if (info != 0) break;
@@ -517,11 +595,16 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
             // ---- lmpar (lmpar_ne, mmba_lm.cpp) ----
             const double dwarf = DBL_MIN;
             int it = 0;
-            solve(0.);
-            aborted = grid_reduce(2, 2u);
-            if (aborted) break;
-            const bool ok0 = s_gv[1] == 0.;
-            double dxnorm = ok0 ? sqrt(s_gv[0]) : HUGE_VAL;
+            if (!pre) {
+                solve(0.);
+                aborted = grid_reduce(2, 2u);
+                if (aborted) break;
+                dn0 = s_gv[0];
+                bad0 = s_gv[1];
+            }
+            pre = false;
+            const bool ok0 = bad0 == 0.;
+            double dxnorm = ok0 ? sqrt(dn0) : HUGE_VAL;
             double fp = dxnorm - delta;
             if (fp <= p1 * delta) {
                 par = 0.;
@@ -535,7 +618,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                     nsq = s_gv[0];
                 }
                 double gd = 0.;
-                if (tid < CPB * NFC && s_p[tid] >= 0) {
+                if (tid < CPB * NFC && s_op[tid] >= 0) {
                     const double q = s_g[tid] / s_diag[tid];
                     gd = q * q;
                 }
@@ -592,16 +675,15 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                     par = fmax(parl, par + parc);
                 }
                 if (aborted || failed) break;
-                if (it == 0) par = 0.;
             }
             // ---- trial point: p = -xs, wa2 = x + p ----
+            // owners: ||D p||^2, ||D wa2||^2 of their parameters
             double pn = 0., xn = 0.;
-            if (tid < CPB * NFC && s_p[tid] >= 0) {
+            if (tid < CPB * NFC && s_op[tid] >= 0) {
                 const double st = -s_xs[tid];
-                const double w2 = s_x[tid] + st;
+                const double w2 = s_ox[tid] + st;
                 const double dk = s_diag[tid];
-                s_wa1[tid] = st;
-                s_wa2[tid] = w2;
+                s_owa2[tid] = w2;
                 pn = dk * st;
                 pn *= pn;
                 xn = dk * w2;
@@ -612,10 +694,18 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                 cg_block_reduce<2, 0u>(vv, s_red, s_gv);
             }
             const double bpn = s_gv[0], bxn = s_gv[1];
+            // slices: the same trial point from the owners' steps (stored
+            // write-through before the last grid reduction)
+            if (tid < SLM * NFC) {
+                double st = 0.;
+                if (s_sp[tid] >= 0) st = -cg_ld(&A.xs[s_sp[tid]]);
+                s_swa1[tid] = st;
+                s_swa2[tid] = s_sx[tid] + st;
+            }
             __syncthreads();
             ++nfev;
             ++fe;
-            eval(s_wa2, s_wa1, fsel ? A.f : A.ft, fsel ? A.dist : A.distt);
+            eval(s_swa2, s_swa1, fsel ? A.f : A.ft, fsel ? A.dist : A.distt);
             // [||f||^2, ||J p||^2, ||D p||^2, ||D wa2||^2]
             if (tid == 0) {
                 s_gv[2] = bpn;
@@ -653,7 +743,8 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                 par = p5 * par;
             }
             if (ratio >= p0001) {
-                if (tid < CPB * NFC) s_x[tid] = s_wa2[tid];
+                if (tid < SLM * NFC) s_sx[tid] = s_swa2[tid];
+                if (tid < CPB * NFC) s_ox[tid] = s_owa2[tid];
                 fsel = 1 - fsel;
                 xnorm = sqrt(s_gv[3]);
                 fnorm = fnorm1;
@@ -675,16 +766,13 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
     }
     // the accepted point's fvec and distances end in A.f / A.dist, x in A.x
     if (fsel) {
-        for (int c = 0; c < ncl; ++c) {
-            const int cf = cf0 + c;
-            for (int i = P.cf_obs_off[cf] + tid; i < P.cf_obs_off[cf + 1]; i += CT) {
-                A.f[2 * i] = A.ft[2 * i];
-                A.f[2 * i + 1] = A.ft[2 * i + 1];
-                A.dist[i] = A.distt[i];
-            }
+        for (int i = so0 + tid; i < so1; i += CT) {
+            A.f[2 * i] = A.ft[2 * i];
+            A.f[2 * i + 1] = A.ft[2 * i + 1];
+            A.dist[i] = A.distt[i];
         }
     }
-    if (tid < CPB * NFC && s_p[tid] >= 0) A.x[s_p[tid]] = s_x[tid];
+    if (tid < CPB * NFC && s_op[tid] >= 0) A.x[s_op[tid]] = s_ox[tid];
     if (g == 0 && tid == 0) {
         CoopOut o;
         o.fnorm = fnorm;
@@ -700,28 +788,59 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
     }
 }
 
-// Camera-frame ranges of the workgroups (<= CPB each, G <= 256); false when
+// Observation slices (balanced, one per workgroup, <= SLM camera-frames
+// each), camera-frame owners (g, g + G, ...: <= CPB per workgroup) and the
+// normal-equation slots of every camera-frame in workgroup order; false when
 // the plan does not fit the cooperative launch.
-bool lm_coop_layout(int ncf, std::vector<int> &cf_off) {
-    if (ncf <= 0) return false;
-    const int per = (ncf + 255) / 256;
-    if (per > CPB) return false;
-    const int G = (ncf + per - 1) / per;
-    cf_off.resize(G + 1);
-    for (int g = 0; g <= G; ++g) cf_off[g] = std::min(ncf, g * per);
+bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, CoopLayout &L) {
+    const int M = cf_obs_off[ncf];
+    if (ncf <= 0 || M <= 0) return false;
+    int G = std::min(256, std::max(1, (M + 511) / 512));
+    G = std::max(G, (ncf + CPB - 1) / CPB);
+    if (G > 256) return false;
+    L.G = G;
+    L.slice_off.assign(G + 1, 0);
+    L.slice_cf.assign(G, 0);
+    L.slice_ncf.assign(G, 0);
+    for (int g = 0; g <= G; ++g) L.slice_off[g] = (int)((long long)M * g / G);
+    std::vector<std::vector<int>> src(ncf);
+    int cf = 0;
+    for (int g = 0; g < G; ++g) {
+        const int o0 = L.slice_off[g], o1 = L.slice_off[g + 1];
+        while (cf < ncf && cf_obs_off[cf + 1] <= o0) ++cf;
+        L.slice_cf[g] = cf;
+        int n = 0;
+        for (int c = cf; c < ncf && cf_obs_off[c] < o1; ++c) {
+            if (cf_obs_off[c + 1] <= o0) continue;
+            src[c].push_back(g * SLM + n);
+            ++n;
+        }
+        if (n > SLM) return false;
+        L.slice_ncf[g] = n;
+    }
+    L.cf_src_off.assign(ncf + 1, 0);
+    L.cf_src.clear();
+    for (int c = 0; c < ncf; ++c) {
+        L.cf_src_off[c] = (int)L.cf_src.size();
+        for (int u : src[c]) L.cf_src.push_back(u);
+    }
+    L.cf_src_off[ncf] = (int)L.cf_src.size();
     return true;
 }
 
 int lm_coop_nfc() { return NFC; }
+int lm_coop_slots() { return SLM; }
+int lm_coop_kj() { return KJC; }
 
-bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G) {
+bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G, bool lens) {
     // every workgroup must be resident (grid reductions): a cooperative
     // launch fails instead of deadlocking when they are not
     DevProblem Pc = P;
     CoopArgs Ac = A;
     void *args[] = {&Pc, &Ac};
-    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&k_lm_coop),
-                                                    dim3(G), dim3(CT), args, 0, s);
+    const void *fn = lens ? reinterpret_cast<const void *>(&k_lm_coop<true>)
+                          : reinterpret_cast<const void *>(&k_lm_coop<false>);
+    const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(G), dim3(CT), args, 0, s);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return false;

@@ -83,6 +83,7 @@ Plan::~Plan() {
     if (h_bflag) (void)hipHostFree(h_bflag);
     if (h_xstage) (void)hipHostFree(h_xstage);
     if (h_coop_out) (void)hipHostFree(h_coop_out);
+    if (h_seq) (void)hipHostFree(h_seq);
 }
 
 static void require(bool c, const char *what) {
@@ -1282,6 +1283,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipMemsetAsync(d_Abb, 0, sizeof(double) * (size_t)nB * 9, s));
     MMBA_HIP(hipMemsetAsync(d_Acc, 0, sizeof(double) * (size_t)ncf * PCMAX * PCMAX, s));
     MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
+    MMBA_HIP(hipHostMalloc(&h_seq, sizeof(unsigned)));
+    *h_seq = 0;
+    if (const char *e = std::getenv("MMBA_SEQ_POLL")) seq_poll = std::atoi(e) != 0;
     d_mticket = dalloc<unsigned>(1);
     d_pweight = upload(param_weight);
     pweight_ok = true;
@@ -1307,8 +1311,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (size_t t = 0; t < cf_var_flags.size() && ok; ++t) ok = cf_var_flags[t] == 0;
         for (int cf = 0; cf < ncf && ok; ++cf)
             ok = cf_var_off[cf + 1] - cf_var_off[cf] - 1 == cf_pc[cf] && cf_pc[cf] <= lm_coop_nfc();
-        std::vector<int> off;
-        if (ok) ok = lm_coop_layout(ncf, off);
+        CoopLayout L;
+        if (ok) ok = lm_coop_layout(ncf, cf_obs_off, L);
         // opt-in while the one-workgroup-per-camera-frame layout is slower
         // than the host loop on C2 (1.38 vs ~0.8 ms per solve: 120
         // workgroups of 1,656 observations each leave half the chip idle)
@@ -1316,8 +1320,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         ok = ok && e && std::atoi(e) != 0;
         if (ok) {
             coop_ok = true;
-            coop_G = (int)off.size() - 1;
-            d_coop_cf_off = upload(off);
+            coop_G = L.G;
+            coop_lens = D.no_lens == 0;
+            d_coop_slice_off = upload(L.slice_off);
+            d_coop_slice_cf = upload(L.slice_cf);
+            d_coop_slice_ncf = upload(L.slice_ncf);
+            d_coop_src_off = upload(L.cf_src_off);
+            d_coop_src = upload(L.cf_src.empty() ? std::vector<int>(1, 0) : L.cf_src);
+            d_coop_nep = dalloc<double>((size_t)coop_G * lm_coop_slots() * lm_coop_kj());
+            d_coop_xs = dalloc<double>(std::max(n, 1));
             d_coop_part = dalloc<double>((size_t)2 * coop_G * 8);
             d_coop_trace = dalloc<double>(COOP_TRACE);
             d_coop_sync = dalloc<unsigned>(2);

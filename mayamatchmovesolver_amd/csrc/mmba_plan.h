@@ -107,10 +107,19 @@ struct Plan {
     // block-diagonal plans (every parameter on one camera-frame, no solved
     // bundle, no global): the whole solve as one cooperative launch
     // (mmba_lmcoop.hip); MMBA_LM_COOP=0 keeps the host-driven loop
+    // page-locked sequence word of the mirrored reductions (read_slots
+    // polls it, MMBA_SEQ_POLL=0: stream events)
+    unsigned *h_seq = nullptr;
+    unsigned seq_next = 0;
+    bool seq_pending = false;  // the next mirrored read_slots polls h_seq
+    bool seq_poll = false;  // MMBA_SEQ_POLL=1 (pending its GPU A/B)
     bool coop_ok = false;
     int coop_G = 0;
-    int *d_coop_cf_off = nullptr;
-    double *d_coop_part = nullptr, *d_coop_trace = nullptr;
+    bool coop_lens = false;
+    int *d_coop_slice_off = nullptr, *d_coop_slice_cf = nullptr, *d_coop_slice_ncf = nullptr;
+    int *d_coop_src_off = nullptr, *d_coop_src = nullptr;
+    double *d_coop_part = nullptr, *d_coop_trace = nullptr, *d_coop_nep = nullptr;
+    double *d_coop_xs = nullptr;
     unsigned *d_coop_sync = nullptr;
     CoopOut *d_coop_out = nullptr, *h_coop_out = nullptr;
     static constexpr int COOP_TRACE = 4096;
