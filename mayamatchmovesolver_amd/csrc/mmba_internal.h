@@ -159,6 +159,23 @@ struct CoopArgs {
     int pad;
     double delta, factor, ftol, xtol, gtol;
 };
+// The MINPACK decision after a trial point, restated on the device (the
+// last k_reduce_multi block, one thread) so that the next Jacobian can be
+// enqueued before the host has read the trial: *gate = 1 exactly when the
+// host's lmder loop will take this trial, accept it and go on (Plan::solve
+// checks its own decision against the record in slots out[0..4]).
+struct LmDec {
+    int on = 0;
+    int spec = 0;    // the speculative trial: lmpar's undamped test decides whether it is used
+    int first = 0;   // iter == 1 (delta from ||D x||, delta = min(delta, pnorm))
+    int f0 = 0;      // fnorm is x0's: sqrt(scalar[s_f0])
+    int nfev = 0, maxfev = 0;
+    double fnorm = 0., par = 0., delta = 0., xnorm = 0., gnorm = 0.;
+    double factor = 0., ftol = 0., xtol = 0., gtol = 0.;
+    int s_pnorm = 0, s_xn2t = 0, s_fnorm = 0, s_jp = 0, s_dnorm = 0, s_fail = 0;
+    int s_xn2 = 0, s_gnorm = 0, s_f0 = 0, s_out = 0;
+    int *gate = nullptr;
+};
 // Device buffers of the (partitioned) band factorisation.
 struct BandSolver {
     bool use_bd = false;                     // block diagonal + arrow (no solved bundle)

@@ -25,13 +25,15 @@ struct RedSpec {
     int flag_slot;
     RedRow row[8];
 };
+// LmDec (mmba_internal.h): the decision after a trial point, restated on the device.
 // host (optional): the last block copies scalar[0, host_n) into that
 // page-locked mirror and then stores seq into *host_seq (system scope,
 // release): the LM thread polls that word instead of a stream event.
 void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
                          double *scalar, int *flag = nullptr, double *host = nullptr,
                          int host_n = 0, unsigned *ticket = nullptr,
-                         unsigned *host_seq = nullptr, unsigned seq = 0);
+                         unsigned *host_seq = nullptr, unsigned seq = 0,
+                         const LmDec &dec = LmDec());
 // lmder bookkeeping after the normal equations (column norms, rank test, diag
 // update, ||D x||, gnorm): partial rows 0 / 1 / 2 (rstride apart, nparts each)
 void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
@@ -76,7 +78,8 @@ struct CoopLayout {
     int G = 0;
     std::vector<int> slice_off, slice_cf, slice_ncf, cf_src_off, cf_src;
 };
-bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, CoopLayout &L);
+bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, int gmax, CoopLayout &L);
+int lm_coop_max_grid(bool lens);
 int lm_coop_nfc();
 int lm_coop_slots();
 int lm_coop_kj();
@@ -150,6 +153,9 @@ struct NeEpi {
     // (k_bundle_factor's arithmetic) for the undamped solve that follows
     double *Lb = nullptr, *tb = nullptr;
     int *fail = nullptr;
+    // gate != nullptr: the launch runs only when *gate != 0 (a Jacobian
+    // enqueued ahead of the host's decision, LmDec)
+    const int *gate = nullptr;
 };
 // Fused K2 (k_jac_ne_u): FD Jacobian + camera-frame normal equations in one
 // pass for uniform fast plans without global parameters (ncv = jac_ncv).

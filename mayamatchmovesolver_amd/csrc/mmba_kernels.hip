@@ -1202,6 +1202,10 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
     __shared__ int sPv[PC];
     __shared__ double sSt[PC];
     __shared__ int sHdr[3];  // nv, frame, stale column
+    // a Jacobian enqueued ahead of the host's decision runs only when the
+    // device's restatement of that decision (lm_decide) let it
+    if (E.gate && __hip_atomic_load(E.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        return;
     const int cf = xcd_remap(blockIdx.x, gridDim.x);
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1669,6 +1673,85 @@ __global__ void __launch_bounds__(256) k_trial_prep(
     block_partial<false>(xn, red, partial + rstride);
 }
 
+// lmder after a trial point (oracle/refcpu.c lm_core; mmba_lm.cpp
+// Plan::solve and lmpar_ne's undamped test), the same operations in the same
+// order as the host's, from the slots this reduction just wrote.
+__device__ void lm_decide(const LmDec &d, double *scalar) {
+    const double p1 = .1, p5 = .5, p25 = .25, p75 = .75, p0001 = 1e-4;
+    const double epsmch = DBL_EPSILON;
+    double fnorm = d.f0 ? sqrt(scalar[d.s_f0]) : d.fnorm;
+    double delta = d.delta, xnorm = d.xnorm, par = d.par, gnorm = d.gnorm;
+    int info = 0, go = 0;
+    double ratio = 0.;
+    bool taken = true;
+    if (d.spec) {
+        if (d.first) {
+            xnorm = sqrt(scalar[d.s_xn2]);
+            delta = d.factor * xnorm;
+            if (delta == 0.) delta = d.factor;
+        }
+        gnorm = fnorm != 0. ? scalar[d.s_gnorm] : 0.;
+        if (gnorm <= d.gtol) {
+            info = 4;
+            taken = false;
+        } else {
+            const double fl = scalar[d.s_fail];
+            const bool ok0 = fl == 0.;
+            const double dxnorm = ok0 ? sqrt(scalar[d.s_dnorm]) : HUGE_VAL;
+            const double fp = dxnorm - delta;
+            // a dataflow timeout (flag >= 2) makes the host solve again
+            taken = fl < 2. && fp <= p1 * delta;
+            par = 0.;
+        }
+    }
+    if (taken) {
+        const double pnorm = sqrt(scalar[d.s_pnorm]);
+        if (d.first) delta = fmin(delta, pnorm);
+        const double fnorm1 = sqrt(scalar[d.s_fnorm]);
+        double actred = -1.;
+        if (p1 * fnorm1 < fnorm) {
+            const double d1 = fnorm1 / fnorm;
+            actred = 1. - d1 * d1;
+        }
+        const double temp1 = sqrt(scalar[d.s_jp]) / fnorm;
+        const double temp2 = (sqrt(par) * pnorm) / fnorm;
+        const double prered = temp1 * temp1 + temp2 * temp2 / p5;
+        const double dirder = -(temp1 * temp1 + temp2 * temp2);
+        if (prered != 0.) ratio = actred / prered;
+        if (ratio <= p25) {
+            double temp;
+            if (actred >= 0.)
+                temp = p5;
+            else
+                temp = p5 * dirder / (dirder + p5 * actred);
+            if (p1 * fnorm1 >= fnorm || temp < p1) temp = p1;
+            delta = temp * fmin(delta, pnorm / p1);
+            par /= temp;
+        } else if (par == 0. || ratio >= p75) {
+            delta = pnorm / p5;
+            par = p5 * par;
+        }
+        const bool accept = ratio >= p0001;
+        if (accept) xnorm = sqrt(scalar[d.s_xn2t]);
+        if (fabs(actred) <= d.ftol && prered <= d.ftol && p5 * ratio <= 1.) info = 1;
+        if (delta <= d.xtol * xnorm) info = 2;
+        if (fabs(actred) <= d.ftol && prered <= d.ftol && p5 * ratio <= 1. && info == 2) info = 3;
+        if (info == 0) {
+            if (d.nfev >= d.maxfev) info = 5;
+            if (fabs(actred) <= epsmch && prered <= epsmch && p5 * ratio <= 1.) info = 6;
+            if (delta <= epsmch * xnorm) info = 7;
+            if (gnorm <= epsmch) info = 8;
+        }
+        go = (accept && info == 0) ? 1 : 0;
+    }
+    scalar[d.s_out] = go;
+    scalar[d.s_out + 1] = ratio;
+    scalar[d.s_out + 2] = delta;
+    scalar[d.s_out + 3] = par;
+    scalar[d.s_out + 4] = taken ? info : -100 - info;
+    __hip_atomic_store(d.gate, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Several partial rows reduced in one launch, block r for row r, in the
 // order of k_reduce_sum / k_reduce_max; block 0 also converts the
 // factorisation fail flag to a scalar and clears it (k_flag_to_scalar).
@@ -1679,7 +1762,7 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
                                                       RedSpec spec, double *scalar, int *flag,
                                                       double *host, int host_n,
                                                       unsigned *ticket, unsigned *host_seq,
-                                                      unsigned seq) {
+                                                      unsigned seq, const LmDec dec) {
     __shared__ double red[256];
     const RedRow rw = spec.row[blockIdx.x];
     const double v = reduce_row_block<false>(partial, rw, red);
@@ -1690,7 +1773,7 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
             *flag = 0;
         }
     }
-    if (!host) return;
+    if (!host && !dec.on) return;
     __shared__ unsigned last;
     if (threadIdx.x == 0) {
         // release this block's slots, count it in; the last arrival acquires
@@ -1702,6 +1785,16 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
     __syncthreads();
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (dec.on) {
+        if (threadIdx.x == 0) lm_decide(dec, scalar);
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    if (!host) {
+        if (threadIdx.x == 0)
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     for (int i = threadIdx.x; i < host_n; i += blockDim.x)
         host[i] = __hip_atomic_load(&scalar[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (host_seq) {
@@ -2684,10 +2777,10 @@ void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, con
 }
 void launch_reduce_multi(hipStream_t s, const double *partial, const RedSpec &spec,
                          double *scalar, int *flag, double *host, int host_n, unsigned *ticket,
-                         unsigned *host_seq, unsigned seq) {
+                         unsigned *host_seq, unsigned seq, const LmDec &dec) {
     if (spec.nrows > 0)
         k_reduce_multi<<<spec.nrows, 256, 0, s>>>(partial, spec, scalar, flag, host, host_n,
-                                                   ticket, host_seq, seq);
+                                                   ticket, host_seq, seq, dec);
 }
 void launch_set_attrs(hipStream_t s, const DevProblem &P, const double *ext) {
     k_set_attrs<<<nblk(P.n, 256), 256, 0, s>>>(P, ext);

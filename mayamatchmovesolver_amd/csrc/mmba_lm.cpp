@@ -81,11 +81,46 @@ void Plan::collect_spans() {
 }
 
 // ---- scalar slots ----
+// The trial's slots on their way to the host before anything else is
+// enqueued behind them (the pre-enqueued Jacobian): the D2H copy (unless the
+// reduction mirrors them) and the event read_slots waits on.
+void Plan::stage_slots() {
+    const bool mirrored = mirror_pending;
+    if (!mirrored)
+        MMBA_HIP(hipMemcpyAsync(h_scalar, d_scalar, sizeof(double) * (SL_LAST + 1),
+                                hipMemcpyDeviceToHost, s));
+    if (!(mirrored && seq_pending)) {
+        if (!ev_sync) MMBA_HIP(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
+        MMBA_HIP(hipEventRecord(ev_sync, s));
+    }
+    slots_staged = true;
+}
+
+void Plan::wait_event() {
+    if (!spin_wait) {
+        MMBA_HIP(hipEventSynchronize(ev_sync));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev_sync);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) MMBA_HIP(e);
+    }
+}
+
 void Plan::read_slots(int lo, int hi) {
     const bool mirrored = mirror_pending && lo == 0 && hi == SL_LAST;
     mirror_pending = false;
     const bool by_seq = mirrored && seq_pending;
     seq_pending = false;
+    if (slots_staged && lo == 0 && hi == SL_LAST) {
+        slots_staged = false;
+        if (!by_seq) {
+            wait_event();
+            return;
+        }
+    }
+    slots_staged = false;
     if (by_seq) {
         // the reduction's last block wrote the mirror, then the sequence
         // word (system-scope release): poll page-locked memory directly --
@@ -181,6 +216,40 @@ double Plan::fun(const double *dx, double *df, double *eu, double *ed, double *d
     return r;
 }
 
+// The pre-enqueued Jacobian applies where jac() takes the fused path whose
+// only launch before the host-visible epilogue is k_jac_ne_u (uniform fast
+// unsharded plans, forward differences, no attribute rows), no callback can
+// end the solve between the trial and the Jacobian, and no timing spans run.
+bool Plan::pre_jac_ok() const {
+    return pre_jac && nranks == 1 && !central && nrows == 0 && !timing && !k2_split &&
+           ne_epilogue_fusable(P) && jac_ne_fusable(P, jac_ncv) && !(cbk && cbk->interrupt) &&
+           !(cbk && cbk->progress);
+}
+
+void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
+    NeEpi epi;
+    epi.on = 1;
+    epi.first = 0;  // a later iteration: the first Jacobian is never enqueued ahead
+    epi.mode = opt.auto_param_scale == 1 ? 1 : 2;
+    epi.fnorm = 0.;
+    epi.fnorm_sq = d_scalar + SL_FNORM;  // the trial's ||f||^2 = the accepted fnorm^2
+    epi.do_xn = 0;
+    epi.do_gn = 1;
+    epi.x = dx;
+    epi.diag = d_diag;
+    epi.acnorm = d_acnorm;
+    epi.partial = d_partial;
+    epi.rstride = pw;
+    epi.cf_base = 0;
+    epi.bnd_base = ncf;
+    epi.gate = d_gate;
+    launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, nloc_set ? nullptr : d_nloc,
+                  d_stale, eu, ed, d_Acc, d_g, epi);
+    nloc_set = true;
+    pre_jac_pending = true;
+    pre_jac_x = dx;
+}
+
 // iflag = 2: FD Jacobian blocks + normal equations + column norms at x.
 void Plan::jac(const double *dx, const JacLM *lm) {
     const double t0 = wall_now();
@@ -253,7 +322,12 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         lb0_valid = true;
     }
     const bool k2_fused = !central && jac_ne_fusable(P, jac_ncv) && !k2_split;
-    if (k2_fused) {
+    const bool pre_done = pre_jac_pending && pre_jac_x == dx && k2_fused && fuse;
+    pre_jac_pending = false;
+    if (pre_done) {
+        // k_jac_ne_u ran ahead at this x (its gate was open: the device took
+        // this trial point, as the host did)
+    } else if (k2_fused) {
         // the local column counts are a property of the plan: stored once
         launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, nloc_set ? nullptr : d_nloc,
                       d_stale, d_eu, d_ed, d_Acc, d_g, epi);
@@ -326,7 +400,8 @@ void Plan::jac(const double *dx, const JacLM *lm) {
 
 // Trial point x + p, p = -xs (lmder): one parameter pass (step, norms,
 // setParameters), measureErrors, ||J p||, one reduction launch.
-void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnorm) {
+void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnorm,
+                         const LmDec *dec) {
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
@@ -366,15 +441,35 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
                        d_wa1, pr + 3 * (size_t)pw, d_dist_t, T);
     span_end(SPAN_RESID);
+    LmDec D;
+    if (dec) {
+        D = *dec;
+        D.on = 1;
+        D.s_pnorm = SL_PNORM;
+        D.s_xn2t = SL_XN2T;
+        D.s_fnorm = SL_FNORM;
+        D.s_jp = SL_JP;
+        D.s_dnorm = SL_DNORM;
+        D.s_fail = SL_FAIL;
+        D.s_xn2 = SL_XN2;
+        D.s_gnorm = SL_GNORM;
+        D.s_f0 = SL_F0;
+        D.s_out = SL_DGO;
+        D.gate = d_gate;
+    }
     if (!T.on) {
         const bool sq = mirror && seq_poll;
         if (sq) ++seq_next;
         launch_reduce_multi(s, d_partial, rs, d_scalar, fill_dnorm ? d_fail : nullptr,
                             mirror ? h_scalar : nullptr, SL_LAST + 1, d_mticket,
-                            sq ? h_seq : nullptr, seq_next);
+                            sq ? h_seq : nullptr, seq_next, D);
         seq_pending = sq;
     }
     mirror_pending = mirror;
+    if (dec) {  // the next Jacobian's first launch, gated on the device's decision
+        stage_slots();
+        pre_jac_enqueue(d_wa2, eu, ed);
+    }
     // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
     allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
     t_func += wall_now() - t0;
@@ -848,6 +943,21 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             trace->count++;
         }
     };
+    // the host's decision on a trial point against the device's (LmDec):
+    // a Jacobian the device ran ahead must be one the host takes
+    pre_jac_pending = false;
+    auto settle_pre = [&](bool go_host) {
+        if (!pre_jac_pending) return;
+        const bool go_dev = h_scalar[SL_DGO] != 0.;
+        if (go_dev && !go_host) {
+            pre_jac_pending = false;
+            set_error("device and host decisions differ after a trial point (device ratio " +
+                      std::to_string(h_scalar[SL_DRATIO]) + ")");
+            throw DeviceError();
+        }
+        // !go_dev: the gated launch did nothing (jac() launches it itself)
+        if (!go_dev || !go_host) pre_jac_pending = false;
+    };
     // fresh attribute block (the scene's current values)
     attrs_reset();
     double init_avg = 0.;
@@ -1049,7 +1159,27 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             // trial's all-reduce
             const bool by_trial = spec && !(band && bs.use_bd && nG == 0 && nranks == 1);
             lmpar_first_enqueue(*this, spec && nranks > 1, by_trial);
-            if (spec) trial_enqueue(d_eu_s, d_ed_s, nranks > 1, by_trial);
+            // the next Jacobian is enqueued behind the trial, gated on the
+            // device's restatement of the decision the host takes below
+            const bool pj = pre_jac_ok();
+            LmDec dec;
+            if (pj) {
+                dec.spec = 1;
+                dec.first = iter == 1;
+                dec.f0 = f0_pending;
+                dec.fnorm = fnorm;
+                dec.delta = delta;
+                dec.xnorm = xnorm;
+                dec.par = par;
+                dec.gnorm = gnorm;
+                dec.nfev = nfev + 1;
+                dec.maxfev = maxfev;
+                dec.factor = factor;
+                dec.ftol = ftol;
+                dec.xtol = xtol;
+                dec.gtol = gtol;
+            }
+            if (spec) trial_enqueue(d_eu_s, d_ed_s, nranks > 1, by_trial, pj ? &dec : nullptr);
             {
                 const double t0 = wall_now();
                 read_slots(0, SL_LAST);
@@ -1069,7 +1199,10 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             }
             gnorm = fnorm != 0. ? h_scalar[SL_GNORM] : 0.;
             if (gnorm <= gtol) info = 4;
-            if (info != 0) goto TERMINATE;
+            if (info != 0) {
+                settle_pre(false);
+                goto TERMINATE;
+            }
             bool pre = true;
             do {
                 bool undamped = false;
@@ -1089,9 +1222,26 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                     std::swap(d_eu, d_eu_s);
                     std::swap(d_ed, d_ed_s);
                 } else {
+                    settle_pre(false);  // a speculative trial lmpar did not take
+                    LmDec dec2;
+                    if (pj) {
+                        dec2.spec = 0;
+                        dec2.first = iter == 1;
+                        dec2.fnorm = fnorm;
+                        dec2.delta = delta;
+                        dec2.xnorm = xnorm;
+                        dec2.par = par;
+                        dec2.gnorm = gnorm;
+                        dec2.nfev = nfev;
+                        dec2.maxfev = maxfev;
+                        dec2.factor = factor;
+                        dec2.ftol = ftol;
+                        dec2.xtol = xtol;
+                        dec2.gtol = gtol;
+                    }
                     // trial point: ||D p||, f(x + p), ||J p|| and the
                     // candidate ||D x_new|| -- one synchronisation
-                    trial_enqueue(d_eu, d_ed);
+                    trial_enqueue(d_eu, d_ed, false, false, pj ? &dec2 : nullptr);
                     const double t0 = wall_now();
                     read_slots(0, SL_LAST);
                     t_func += wall_now() - t0;
@@ -1137,12 +1287,19 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
                 if (delta <= xtol * xnorm) info = 2;
                 if (std::fabs(actred) <= ftol && prered <= ftol && p5 * ratio <= 1. && info == 2)
                     info = 3;
-                if (info != 0) goto TERMINATE;
+                if (info != 0) {
+                    settle_pre(false);
+                    goto TERMINATE;
+                }
                 if (nfev >= maxfev) info = 5;
                 if (std::fabs(actred) <= epsmch && prered <= epsmch && p5 * ratio <= 1.) info = 6;
                 if (delta <= epsmch * xnorm) info = 7;
                 if (gnorm <= epsmch) info = 8;
-                if (info != 0) goto TERMINATE;
+                if (info != 0) {
+                    settle_pre(false);
+                    goto TERMINATE;
+                }
+                settle_pre(ratio >= p0001);
             } while (ratio < p0001);
         }
     }

@@ -24,6 +24,8 @@
 // and every poll ends; each poll is also bounded (a timeout aborts the
 // solve on every workgroup through an abort word and is reported).
 #include <cfloat>
+#include <cstdio>
+#include <cstdlib>
 
 #include "mmba_geom.h"
 #include "mmba_kernels.h"
@@ -35,7 +37,7 @@ namespace {
 
 constexpr int CT = 256;    // threads per workgroup
 constexpr int CPB = 4;     // camera-frames owned per workgroup (one wave each in lmpar)
-constexpr int SLM = 4;     // camera-frames touched by one workgroup's observation slice
+constexpr int SLM = 8;     // camera-frames touched by one workgroup's observation slice
 constexpr int NFC = 8;     // parameters per camera-frame (lanes of the solve)
 constexpr int NRED = 8;    // values per grid reduction
 constexpr int KJC = NFC * (NFC + 1) / 2 + NFC;  // J^T J lower triangle + J^T f
@@ -117,7 +119,8 @@ __device__ __forceinline__ void cg_block_reduce(const double (&v)[NV], double (*
 //
 // Two roles per workgroup g:
 //   slice  observations [slice_off[g], slice_off[g + 1]) (balanced, cut
-//          anywhere; <= SLM camera-frames): setParameters of their
+//          anywhere; <= SLM camera-frames: C2's frames hold 63 to 2,643
+//          observations): setParameters of their
 //          camera-frames, their camera records, residuals, FD Jacobian rows,
 //          and J^T J / J^T f partials per camera-frame slot -> A.nep
 //   owner  camera-frames g, g + G, ... (<= CPB): sums the slots of each
@@ -330,7 +333,13 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
 #pragma unroll
             for (int q = 0; q < KJ; ++q) acc[q] = 0.;
             for (int i = obs_lo(c) + tid; i < obs_hi(c); i += CT) {
-                const Resid r0 = resid_at(i, s_rec[c][0]);
+                // the records stay in LDS (an opaque zero offset keeps the
+                // compiler from hoisting 180 loop-invariant doubles into
+                // registers)
+                int z = 0;
+                asm volatile("" : "+s"(z));
+                const double *rc = &s_rec[c][0][0] + z;
+                const Resid r0 = resid_at(i, rc);
                 Resid rs = r0;
                 double jx[NFC], jy[NFC];
 #pragma unroll
@@ -339,7 +348,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                     jy[a] = 0.;
                     if (a < pc) {
                         const int k = c * NFC + a;
-                        const Resid r = resid_at(i, s_rec[c][1 + a]);
+                        const Resid r = resid_at(i, rc + (1 + a) * CAMREC);
                         const double st = s_step[k];
                         if (lmder) {  // inv_delta, multiplied (adjust_solveFunc.cpp:395-402)
                             jx[a] = (r.ex - r0.ex) * st;
@@ -792,40 +801,77 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
 // each), camera-frame owners (g, g + G, ...: <= CPB per workgroup) and the
 // normal-equation slots of every camera-frame in workgroup order; false when
 // the plan does not fit the cooperative launch.
-bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, CoopLayout &L) {
+bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, int gmax, CoopLayout &L) {
     const int M = cf_obs_off[ncf];
-    if (ncf <= 0 || M <= 0) return false;
-    int G = std::min(256, std::max(1, (M + 511) / 512));
-    G = std::max(G, (ncf + CPB - 1) / CPB);
-    if (G > 256) return false;
-    L.G = G;
-    L.slice_off.assign(G + 1, 0);
-    L.slice_cf.assign(G, 0);
-    L.slice_ncf.assign(G, 0);
-    for (int g = 0; g <= G; ++g) L.slice_off[g] = (int)((long long)M * g / G);
-    std::vector<std::vector<int>> src(ncf);
-    int cf = 0;
-    for (int g = 0; g < G; ++g) {
-        const int o0 = L.slice_off[g], o1 = L.slice_off[g + 1];
-        while (cf < ncf && cf_obs_off[cf + 1] <= o0) ++cf;
-        L.slice_cf[g] = cf;
-        int n = 0;
-        for (int c = cf; c < ncf && cf_obs_off[c] < o1; ++c) {
-            if (cf_obs_off[c + 1] <= o0) continue;
-            src[c].push_back(g * SLM + n);
+    if (ncf <= 0 || M <= 0 || gmax <= 0) return false;
+    // slices of ~M / G observations, also cut where a slice would touch a
+    // (SLM + 1)-th camera-frame; fewer, longer slices when that needs more
+    // workgroups than fit
+    const int gmin = (ncf + CPB - 1) / CPB;  // owners: <= CPB camera-frames each
+    if (gmin > gmax) return false;
+    for (int target = std::max(512, (M + gmax - 1) / gmax);; target += target / 4 + 1) {
+        std::vector<int> off{0}, first{0}, cnt;
+        int cf = 0, n = 0;  // current slice: first camera-frame, camera-frames touched
+        for (int o = 0; o < M;) {
+            while (cf_obs_off[cf + 1] <= o) ++cf;
+            const int start = off.back();
+            if (n == 0) first.back() = cf;
             ++n;
+            const int end = std::min(cf_obs_off[cf + 1], start + target);
+            o = end;
+            if (end == start + target || n == SLM || o == M) {
+                off.push_back(o);
+                cnt.push_back(n);
+                if (o < M) first.push_back(0);
+                n = 0;
+            }
         }
-        if (n > SLM) return false;
-        L.slice_ncf[g] = n;
+        int G = (int)cnt.size();
+        if (G > gmax) {
+            if (target >= M) return false;
+            continue;
+        }
+        // every owner slot exists: pad with empty slices up to gmin
+        while (G < gmin) {
+            off.push_back(M);
+            first.push_back(ncf - 1);
+            cnt.push_back(0);
+            ++G;
+        }
+        L.G = G;
+        L.slice_off = off;
+        L.slice_cf = first;
+        L.slice_ncf = cnt;
+        std::vector<std::vector<int>> src(ncf);
+        for (int g = 0; g < G; ++g)
+            for (int c = 0; c < cnt[g]; ++c) src[first[g] + c].push_back(g * SLM + c);
+        L.cf_src_off.assign(ncf + 1, 0);
+        L.cf_src.clear();
+        for (int c = 0; c < ncf; ++c) {
+            L.cf_src_off[c] = (int)L.cf_src.size();
+            for (int u : src[c]) L.cf_src.push_back(u);
+        }
+        L.cf_src_off[ncf] = (int)L.cf_src.size();
+        return true;
     }
-    L.cf_src_off.assign(ncf + 1, 0);
-    L.cf_src.clear();
-    for (int c = 0; c < ncf; ++c) {
-        L.cf_src_off[c] = (int)L.cf_src.size();
-        for (int u : src[c]) L.cf_src.push_back(u);
+}
+
+// Workgroups a cooperative launch of k_lm_coop can keep resident on the
+// current device (occupancy x compute units), 0 when it cannot launch.
+int lm_coop_max_grid(bool lens) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const void *fn = lens ? reinterpret_cast<const void *>(&k_lm_coop<true>)
+                          : reinterpret_cast<const void *>(&k_lm_coop<false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, CT, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
     }
-    L.cf_src_off[ncf] = (int)L.cf_src.size();
-    return true;
+    if (std::getenv("MMBA_COOP_DEBUG"))
+        std::fprintf(stderr, "[mmba coop] %d compute units x %d resident workgroups\n", cus, per);
+    return std::min(256, per * cus);
 }
 
 int lm_coop_nfc() { return NFC; }
@@ -843,6 +889,9 @@ bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G
     const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(G), dim3(CT), args, 0, s);
     if (e != hipSuccess) {
         (void)hipGetLastError();
+        if (std::getenv("MMBA_COOP_DEBUG"))
+            std::fprintf(stderr, "[mmba coop] cooperative launch of %d workgroups failed: %s\n", G,
+                         hipGetErrorString(e));
         return false;
     }
     return true;

@@ -1286,6 +1286,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipHostMalloc(&h_seq, sizeof(unsigned)));
     *h_seq = 0;
     if (const char *e = std::getenv("MMBA_SEQ_POLL")) seq_poll = std::atoi(e) != 0;
+    if (const char *e = std::getenv("MMBA_PRE_JAC")) pre_jac = std::atoi(e) != 0;
+    d_gate = dalloc<int>(1);
+    MMBA_HIP(hipMemsetAsync(d_gate, 0, sizeof(int), s));
     d_mticket = dalloc<unsigned>(1);
     d_pweight = upload(param_weight);
     pweight_ok = true;
@@ -1312,7 +1315,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int cf = 0; cf < ncf && ok; ++cf)
             ok = cf_var_off[cf + 1] - cf_var_off[cf] - 1 == cf_pc[cf] && cf_pc[cf] <= lm_coop_nfc();
         CoopLayout L;
-        if (ok) ok = lm_coop_layout(ncf, cf_obs_off, L);
+        const int gmax = ok ? lm_coop_max_grid(D.no_lens == 0) : 0;
+        if (ok) ok = gmax > 0 && lm_coop_layout(ncf, cf_obs_off, gmax, L);
         // opt-in while the one-workgroup-per-camera-frame layout is slower
         // than the host loop on C2 (1.38 vs ~0.8 ms per solve: 120
         // workgroups of 1,656 observations each leave half the chip idle)

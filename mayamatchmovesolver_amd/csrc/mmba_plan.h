@@ -281,17 +281,25 @@ struct Plan {
         SL_RMS = 12,
         SL_NCENT = 13,  // central FD columns of the last Jacobian (second evaluations)
         SL_F0 = 14,     // ||f||^2 at x0 (lmder's first evaluation; read with the first decision)
-        SL_LAST = 14,
-        SL_FI = 15,     // ||f||^2 of the initial measurement (read at the end)
+        // the device's restatement of the decision after a trial point
+        // (LmDec, k_reduce_multi): gate of the pre-enqueued Jacobian, then
+        // ratio, delta, par, info -- the host checks its own against them
+        SL_DGO = 15,
+        SL_DRATIO = 16,
+        SL_DDELTA = 17,
+        SL_DPAR = 18,
+        SL_DINFO = 19,
+        SL_LAST = 19,
+        SL_FI = 20,     // ||f||^2 of the initial measurement (read at the end)
         // errorDistanceList statistics (launch_dist_stats): sum, -min, max
-        SL_ESUM = 16,
-        SL_ENMIN = 17,
-        SL_EMAX = 18,
+        SL_ESUM = 21,
+        SL_ENMIN = 22,
+        SL_EMAX = 23,
         // ... of the initial measurement (read at the end)
-        SL_IESUM = 19,
-        SL_IENMIN = 20,
-        SL_IEMAX = 21,
-        NSLOT = 24
+        SL_IESUM = 24,
+        SL_IENMIN = 25,
+        SL_IEMAX = 26,
+        NSLOT = 28
     };
     void read_slots(int lo, int hi);
     bool spin_wait = true;  // MMBA_SPIN_WAIT=0: blocking synchronisation
@@ -338,7 +346,24 @@ struct Plan {
     // FAIL] ride in the trial's all-reduce (slots 0..5, one collective)
     // fill_dnorm: this trial's ||D p||^2 also fills SL_DNORM and the fail
     // flag SL_FAIL of the undamped solve enqueued with dnorm_by_trial
-    void trial_enqueue(double *eu, double *ed, bool with_dnorm = false, bool fill_dnorm = false);
+    void trial_enqueue(double *eu, double *ed, bool with_dnorm = false, bool fill_dnorm = false,
+                       const LmDec *dec = nullptr);
+    // The next Jacobian's first launch (k_jac_ne_u at the trial point),
+    // enqueued behind a trial whose reduction restates the host's decision
+    // (LmDec): it runs only when that decision takes the trial and goes on,
+    // so the GPU starts the next iteration while the host reads the trial.
+    // MMBA_PRE_JAC=0: off.
+    bool pre_jac = true;
+    bool pre_jac_pending = false;   // enqueued, the host has not decided yet
+    const double *pre_jac_x = nullptr;
+    int *d_gate = nullptr;
+    bool pre_jac_ok() const;
+    void pre_jac_enqueue(const double *dx, double *eu, double *ed);
+    // the trial's slots staged (D2H copy unless mirrored, then an event)
+    // before the pre-enqueued Jacobian: read_slots(0, SL_LAST) only waits
+    bool slots_staged = false;
+    void stage_slots();
+    void wait_event();
     // speculative trial (lmpar's first, undamped, step taken before the
     // host has read it): its errorList / errorDistanceList land here and are
     // swapped in when lmpar accepts that step
