@@ -136,7 +136,7 @@ struct BatchArgs {
 // Whole-solve cooperative launch for block-diagonal plans (mmba_lmcoop.hip).
 struct CoopOut {
     double fnorm;
-    int info, nfev, njev, func_evals, jac_evals, ntrace, failed, aborted;
+    int info, nfev, njev, func_evals, jac_evals, ntrace, failed, aborted, nprobe, pad;
 };
 struct CoopArgs {
     // workgroup g: observations [slice_off[g], slice_off[g + 1]) over the
@@ -155,6 +155,7 @@ struct CoopArgs {
     double *trace;
     int trace_cap;
     CoopOut *out;
+    long long *probe;    // MMBA_COOP_DEBUG: workgroup 0's wall clock at phase ends (64)
     int solver_type, mode, maxfev;
     int pad;
     double delta, factor, ftol, xtol, gtol;

@@ -40,7 +40,8 @@ void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
                          const double *Abb, const double *aggbuf, double *acnorm, double *g,
                          double *diag, const double *x, int first, int mode, double fnorm,
                          const double *fnorm_sq, int do_xn, int do_gn, const int *mask,
-                         double *partial, int nparts, int rstride);
+                         double *partial, int nparts, int rstride, const double *c15 = nullptr,
+                         const double *s15 = nullptr, double *gfull = nullptr);
 // lmder trial point x - xs with setParameters at it; partial rows 0 (pnorm^2)
 // and 1 (||D x_new||^2)
 void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
@@ -107,9 +108,29 @@ void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, 
 // factor 0.5 / (|dA| + |dB|) (0: forward column).  recs == nullptr: forward.
 struct CentralB {
     const double *recs = nullptr, *brec = nullptr, *ext_pert = nullptr, *step = nullptr;
+    // B15: animated central columns leave out f c (the rows other frames
+    // skip carry f c^T, applied as a rank-one term: Plan::b15)
+    int b15 = 0;
 };
+// c15 (optional): c_p = 0.5 / (|dA| + |dB|) of animated central columns, else 0
 void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
-                          double *stepB, double delta, double *count);
+                          double *stepB, double delta, double *count, double *c15 = nullptr);
+// B15 rank-one Jacobian term J = J_s + f c^T (Plan::b15): s = ||f||^2 at the
+// Jacobian's point (*fsq, or fn^2) -> *out
+void launch_b15_s(hipStream_t s, const double *fsq, double fn, double *out);
+// xs = (M + U B U^T)^-1 (u + s c) from z_u = M^-1 u, z_c = M^-1 c (Woodbury,
+// U = [u c], B = [0 1; 1 s]); K^-1 -> kinv[0..3]; ||D xs||^2 -> scalar[dnorm_slot]
+// (dnorm_slot >= 0); scalar[fail_slot] = max(itself, *fail_prev, singular K)
+void launch_b15_combine(hipStream_t s, int n, const double *u, const double *c, const double *zu,
+                        const double *zc, const double *sp, const double *diag, double *xs,
+                        double *kinv, double *scalar, int dnorm_slot, int fail_slot,
+                        const double *fail_prev);
+// *out -= w^T K^-1 w, w = [z_u . v, z_c . v] (lmpar's v^T (A + lam D^2)^-1 v)
+void launch_b15_newton(hipStream_t s, int n, const double *v, const double *zu, const double *zc,
+                       const double *kinv, double *out);
+// *out += 2 (c . xs)(u . xs) + s (c . xs)^2 (||J p||^2 of the rank-one term)
+void launch_b15_jp(hipStream_t s, int n, const double *xs, const double *u, const double *c,
+                   const double *sp, double *out);
 void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
                      const double *ext_pert, const double *step, int solver_type, double *J,
                      int *jcol, int *nloc, const int *stale_param, double *eu, double *ed,
@@ -217,6 +238,27 @@ void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, cons
 void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                            const double *tb, const double *Lb, const double *xR, double *U,
                            double *x);
+// The trial point's parameter pass (k_trial_prep's operations) fused into
+// the bundle back substitution: bundle parameters as their step is formed,
+// the other parameters (other[0, nother)) by extra workgroups; partial rows
+// pn / xn (rstride apart) get one entry per workgroup (trial_fold_parts).
+struct TrialFold {
+    const double *x = nullptr, *diag = nullptr;
+    double *wa1 = nullptr, *wa2 = nullptr, *wa3 = nullptr;
+    double *ext = nullptr, *ext_pert = nullptr, *step = nullptr;
+    int solver_type = 0;
+    double delta = 0., eps_dif = 0.;
+    const int *other = nullptr;
+    int nother = 0;
+    double *partial = nullptr;
+    int rstride = 0;
+};
+int trial_fold_parts(const DevProblem &P, int nother);
+void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,
+                    double *U);
+void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,
+                          const double *Lb, const double *xR, const double *U, double *x,
+                          const TrialFold &T);
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                           const double *Lb, const double *v, double *wR, double *usq,

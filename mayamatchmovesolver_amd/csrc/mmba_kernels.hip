@@ -291,7 +291,7 @@ __global__ void k_param_prep(DevProblem P, const double *__restrict__ x, double 
 // stepB holding that factor.  count += number of central columns (each one
 // is a second incrementJacobianIteration).
 __global__ void k_param_central(DevProblem P, const double *__restrict__ x, double *ext_pertB,
-                                double *stepB, double delta, double *count) {
+                                double *stepB, double delta, double *count, double *c15) {
     int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
     const double v = x[p];
@@ -303,9 +303,14 @@ __global__ void k_param_central(DevProblem P, const double *__restrict__ x, doub
     if (dA == dB) {
         stepB[p] = 0.;
         ext_pertB[p] = 0.;
+        if (c15) c15[p] = 0.;
         return;
     }
     stepB[p] = 0.5 / (fabs(dA) + fabs(dB));
+    // B15: an animated column's measureErrors skips the other frames, whose
+    // rows keep errorListA = errors and errorListB = 0
+    // (adjust_solveFunc.cpp:331-333, 412, 468-471): J_jp = f_j c_p there
+    if (c15) c15[p] = P.p_frame[p] >= 0 ? stepB[p] : 0.;
     ext_pertB[p] = int_to_ext(v + dB, xmin, xmax, P.p_off[p], P.p_scale[p]);
     atomicAdd(count, 1.0);
 }
@@ -674,6 +679,12 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
             const Resid rb = evalB();
             jx = (r.ex - rb.ex) * sB;
             jy = (r.ey - rb.ey) * sB;
+            if (CB.b15 && P.p_frame[p] >= 0) {
+                // B15: J = J_s + f c^T, so the column's own rows keep
+                // (eA - eB - f) c (the rank-one term adds f c back)
+                jx -= r0.ex * sB;
+                jy -= r0.ey * sB;
+            }
             if (p == pstale) rs = rb;  // the column's last measureErrors
         } else {
             if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
@@ -1590,12 +1601,14 @@ __global__ void __launch_bounds__(256) k_jac_epilogue(
     const double *__restrict__ Agg, const double *__restrict__ gG, double *acnorm, double *g,
     double *diag, const double *__restrict__ x, int first, int mode, double fnorm,
     const double *__restrict__ fnorm_sq, int do_xn, int do_gn, const int *__restrict__ mask,
-    double *partial, int rstride) {
+    double *partial, int rstride, const double *__restrict__ c15, const double *__restrict__ s15,
+    double *gfull) {
     __shared__ double red[256];
     if (fnorm_sq) {
         fnorm = sqrt(*fnorm_sq);
         do_gn = do_gn && fnorm != 0.;
     }
+    const double s15v = c15 ? *s15 : 0.;
     double zf = 0., xn = 0., gm = 0.;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.n; p += gridDim.x * blockDim.x) {
         const int cls = P.p_class[p];
@@ -1616,6 +1629,14 @@ __global__ void __launch_bounds__(256) k_jac_epilogue(
             d = Agg[gi * NGMAX + gi];
             gp = gG[gi];
             g[p] = gp;
+        }
+        if (c15) {
+            // B15: ||J_p||^2 and (J^T f)_p of J = J_s + f c^T, with
+            // u = J_s^T f in g: A_pp + 2 c_p u_p + s c_p^2, u_p + s c_p
+            const double cp = c15[p];
+            d = fmax(d + 2. * cp * gp + s15v * cp * cp, 0.);
+            gp = gp + s15v * cp;
+            gfull[p] = gp;
         }
         const double an = sqrt(d);
         acnorm[p] = an;
@@ -2436,6 +2457,99 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
         if (a < pb) x[P.bnd_par[po + a]] = xb[a];
 }
 
+// k_trial_prep's operations for parameter j with step xs_j.
+__device__ __forceinline__ void trial_one(const DevProblem &P, const TrialFold &T, int j,
+                                          double xsj, double &pn, double &xn) {
+    const double st = -xsj;
+    const double dj = T.diag[j];
+    const double xj = T.x[j] + st;
+    const double w3 = dj * st;
+    T.wa1[j] = st;
+    T.wa2[j] = xj;
+    T.wa3[j] = w3;
+    param_prep_one(P, j, xj, T.ext, T.ext_pert, T.step, T.solver_type, T.delta, T.eps_dif);
+    set_attr_one(P, j, T.ext[j]);
+    pn += w3 * w3;
+    const double v = dj * xj;
+    xn += v * v;
+}
+
+// k_backsub_bundle (two-pass form: u_i from k_obs_wtx) + the trial point's
+// parameter pass: workgroups [0, nbb) back-substitute their bundles and
+// prepare those parameters from the step just formed; workgroups [nbb, ..)
+// prepare the other parameters from xs (the reduced solve's scatter).
+// Unsharded plans only (every parameter owned).
+__global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double *__restrict__ U,
+                                                      const double *__restrict__ Wg,
+                                                      const double *__restrict__ tb,
+                                                      const double *__restrict__ Lb,
+                                                      const double *__restrict__ xR, double *x,
+                                                      int nbb, TrialFold T) {
+    __shared__ double red[256];
+    double pn = 0., xn = 0.;
+    if ((int)blockIdx.x < nbb) {
+        const int b = xcd_remap(blockIdx.x, nbb) * blockDim.x + threadIdx.x;
+        const int pb = b < P.nB ? P.bnd_pb[b] : 0;
+        if (pb > 0) {
+            const int nG = P.nG;
+            const int nCF = P.nR - nG;
+            double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
+            for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
+                const double4 uu = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
+                s[0] -= uu.x;
+                s[1] -= uu.y;
+                s[2] -= uu.z;
+            }
+            for (int q = 0; q < nG; ++q) {
+                const double xv = xR[nCF + q];
+                for (int c = 0; c < 3; ++c) s[c] -= Wg[((size_t)b * NGMAX + q) * 3 + c] * xv;
+            }
+            double L[3][3];
+            for (int a = 0; a < 3; ++a)
+                for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+            double xb[3] = {0., 0., 0.};
+#pragma unroll
+            for (int a = 2; a >= 0; --a) {
+                if (a >= pb) continue;
+                double t = s[a];
+#pragma unroll
+                for (int k = a + 1; k < 3; ++k)
+                    if (k < pb) t -= L[k][a] * xb[k];
+                xb[a] = t / L[a][a];
+            }
+            const int po = P.bnd_par_off[b];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                if (a < pb) {
+                    const int j = P.bnd_par[po + a];
+                    x[j] = xb[a];
+                    trial_one(P, T, j, xb[a], pn, xn);
+                }
+        }
+    } else {
+        const int k = (blockIdx.x - nbb) * blockDim.x + threadIdx.x;
+        if (k < T.nother) {
+            const int j = T.other[k];
+            trial_one(P, T, j, x[j], pn, xn);
+        }
+    }
+    // one partial per workgroup, 64-lane fixed tree
+    red[threadIdx.x] = pn;
+    red[64 + threadIdx.x] = xn;
+    __syncthreads();
+    for (int w = 32; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            red[threadIdx.x] += red[threadIdx.x + w];
+            red[64 + threadIdx.x] += red[64 + threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        T.partial[blockIdx.x] = red[0];
+        T.partial[T.rstride + blockIdx.x] = red[64];
+    }
+}
+
 // Reduced-system solution (R order) -> parameter order.
 __global__ void k_scatter_xR(DevProblem P, const double *__restrict__ xR, double *x) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2721,6 +2835,23 @@ __global__ void k_unpermute(int M, const int *__restrict__ ref_of_dev,
 namespace mmba {
 
 static inline int nblk(long n, int bs) { return (int)((n + bs - 1) / bs); }
+int trial_fold_parts(const DevProblem &P, int nother) {
+    return nblk(P.nB, 64) + nblk(nother, 64);
+}
+
+void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,
+                          const double *Lb, const double *xR, const double *U, double *x,
+                          const TrialFold &T) {
+    const int nbb = nblk(P.nB, 64);
+    const int g = nbb + nblk(T.nother, 64);
+    if (g > 0) k_backsub_trial<<<g, 64, 0, s>>>(P, U, Wg, tb, Lb, xR, x, nbb, T);
+}
+
+void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,
+                    double *U) {
+    if (P.nB == 0) return;
+    k_obs_wtx<<<nblk(P.M, 64), 64, sizeof(double) * 64 * P.wst, s>>>(P, W, xR, U);
+}
 
 void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, double *ext,
                        double *ext_pert, double *step, int solver_type, double delta,
@@ -2762,10 +2893,11 @@ void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
                          const double *Abb, const double *aggbuf, double *acnorm, double *g,
                          double *diag, const double *x, int first, int mode, double fnorm,
                          const double *fnorm_sq, int do_xn, int do_gn, const int *mask,
-                         double *partial, int nparts, int rstride) {
+                         double *partial, int nparts, int rstride, const double *c15,
+                         const double *s15, double *gfull) {
     k_jac_epilogue<<<nparts, 256, 0, s>>>(P, Acc, Abb, aggbuf, aggbuf + NGMAX * NGMAX, acnorm,
                                           g, diag, x, first, mode, fnorm, fnorm_sq, do_xn, do_gn,
-                                          mask, partial, rstride);
+                                          mask, partial, rstride, c15, s15, gfull);
 }
 void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
                        const double *diag, double *wa1, double *wa2, double *wa3, double *ext,
@@ -3032,9 +3164,131 @@ void launch_fold_ranks(hipStream_t s, const double *t, int nranks, double *out, 
     k_fold_ranks<<<1, 64, 0, s>>>(t, nranks, out, do_xn, do_gn);
 }
 void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
-                          double *stepB, double delta, double *count) {
+                          double *stepB, double delta, double *count, double *c15) {
     if (P.n > 0)
-        k_param_central<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext_pertB, stepB, delta, count);
+        k_param_central<<<nblk(P.n, 256), 256, 0, s>>>(P, x, ext_pertB, stepB, delta, count,
+                                                        c15);
+}
+
+// ---------------------------------------------------------------------------
+// B15: the reference's central Jacobian of animated parameters over several
+// frames is J = J_s + f c^T (Plan::b15).  Its normal matrix is
+// A = M + U B U^T with M = J_s^T J_s (+ lam D^2), U = [u c], u = J_s^T f,
+// B = [0 1; 1 s], s = ||f||^2, and J^T f = u + s c.  One workgroup per call,
+// fixed-order sums (bit-reproducible); the vectors are n long.
+// ---------------------------------------------------------------------------
+template <int NV>
+__device__ __forceinline__ void b15_block_sum(double (&v)[NV], double (*red)[1024]) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[k][tid] = v[k];
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if (tid < w) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) red[k][tid] += red[k][tid + w];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = red[k][0];
+    __syncthreads();
+}
+
+__global__ void k_b15_s(const double *fsq, double fn, double *out) {
+    if (threadIdx.x == 0) *out = fsq ? *fsq : fn * fn;
+}
+
+__global__ void __launch_bounds__(1024) k_b15_combine(
+    int n, const double *__restrict__ u, const double *__restrict__ c,
+    const double *__restrict__ zu, const double *__restrict__ zc, const double *__restrict__ sp,
+    const double *__restrict__ diag, double *xs, double *kinv, double *scalar, int dnorm_slot,
+    int fail_slot, const double *__restrict__ fail_prev) {
+    __shared__ double red[4][1024];
+    double d[4] = {0., 0., 0., 0.};
+    for (int j = threadIdx.x; j < n; j += 1024) {
+        d[0] += u[j] * zu[j];
+        d[1] += u[j] * zc[j];
+        d[2] += c[j] * zu[j];
+        d[3] += c[j] * zc[j];
+    }
+    b15_block_sum<4>(d, red);
+    const double s = *sp;
+    // K = B^-1 + U^T M^-1 U, B^-1 = [-s 1; 1 0]
+    const double k00 = d[0] - s, k01 = 1. + d[1], k10 = 1. + d[2], k11 = d[3];
+    const double det = k00 * k11 - k01 * k10;
+    const bool sing = !(fabs(det) > 0.) || !isfinite(det);
+    const double i00 = k11 / det, i01 = -k01 / det, i10 = -k10 / det, i11 = k00 / det;
+    // U^T M^-1 g, g = u + s c, M^-1 g = z_u + s z_c
+    const double r0 = d[0] + s * d[1], r1 = d[2] + s * d[3];
+    const double al = i00 * r0 + i01 * r1, be = i10 * r0 + i11 * r1;
+    const double cu = 1. - al, cc = s - be;
+    double dn[1] = {0.};
+    for (int j = threadIdx.x; j < n; j += 1024) {
+        const double v = cu * zu[j] + cc * zc[j];
+        xs[j] = v;
+        const double w = diag[j] * v;
+        dn[0] += w * w;
+    }
+    b15_block_sum<1>(dn, red);
+    if (threadIdx.x == 0) {
+        kinv[0] = i00;
+        kinv[1] = i01;
+        kinv[2] = i10;
+        kinv[3] = i11;
+        if (dnorm_slot >= 0) scalar[dnorm_slot] = dn[0];
+        double f = fmax(scalar[fail_slot], *fail_prev);
+        if (sing) f = fmax(f, 1.);
+        scalar[fail_slot] = f;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_b15_newton(int n, const double *__restrict__ v,
+                                                     const double *__restrict__ zu,
+                                                     const double *__restrict__ zc,
+                                                     const double *__restrict__ kinv, double *out) {
+    __shared__ double red[2][1024];
+    double w[2] = {0., 0.};
+    for (int j = threadIdx.x; j < n; j += 1024) {
+        w[0] += zu[j] * v[j];
+        w[1] += zc[j] * v[j];
+    }
+    b15_block_sum<2>(w, red);
+    if (threadIdx.x == 0)
+        *out -= w[0] * (kinv[0] * w[0] + kinv[1] * w[1]) + w[1] * (kinv[2] * w[0] + kinv[3] * w[1]);
+}
+
+__global__ void __launch_bounds__(1024) k_b15_jp(int n, const double *__restrict__ xs,
+                                                 const double *__restrict__ u,
+                                                 const double *__restrict__ c,
+                                                 const double *__restrict__ sp, double *out) {
+    __shared__ double red[2][1024];
+    double w[2] = {0., 0.};
+    for (int j = threadIdx.x; j < n; j += 1024) {
+        w[0] += c[j] * xs[j];
+        w[1] += u[j] * xs[j];
+    }
+    b15_block_sum<2>(w, red);
+    if (threadIdx.x == 0) *out += 2. * w[0] * w[1] + *sp * w[0] * w[0];
+}
+
+void launch_b15_s(hipStream_t s, const double *fsq, double fn, double *out) {
+    k_b15_s<<<1, 64, 0, s>>>(fsq, fn, out);
+}
+void launch_b15_combine(hipStream_t s, int n, const double *u, const double *c, const double *zu,
+                        const double *zc, const double *sp, const double *diag, double *xs,
+                        double *kinv, double *scalar, int dnorm_slot, int fail_slot,
+                        const double *fail_prev) {
+    k_b15_combine<<<1, 1024, 0, s>>>(n, u, c, zu, zc, sp, diag, xs, kinv, scalar, dnorm_slot,
+                                     fail_slot, fail_prev);
+}
+void launch_b15_newton(hipStream_t s, int n, const double *v, const double *zu, const double *zc,
+                       const double *kinv, double *out) {
+    k_b15_newton<<<1, 1024, 0, s>>>(n, v, zu, zc, kinv, out);
+}
+void launch_b15_jp(hipStream_t s, int n, const double *xs, const double *u, const double *c,
+                   const double *sp, double *out) {
+    k_b15_jp<<<1, 1024, 0, s>>>(n, xs, u, c, sp, out);
 }
 bool ne_epilogue_fusable(const DevProblem &P) {
     return P.nG == 0 && (P.JB || P.nbs == 0) && (P.pc_uniform == 6 || P.pc_uniform == 7) &&

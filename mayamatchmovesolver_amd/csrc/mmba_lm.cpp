@@ -16,6 +16,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 #include "mmba_geom.h"
@@ -267,19 +268,21 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     CentralB CB;
     if (central) {  // the deltaB pass of the central columns
         MMBA_HIP(hipMemsetAsync(d_scalar + SL_NCENT, 0, sizeof(double), s));
-        launch_param_central(s, P, dx, d_ext_pertB, d_stepB, opt.delta, d_scalar + SL_NCENT);
+        launch_param_central(s, P, dx, d_ext_pertB, d_stepB, opt.delta, d_scalar + SL_NCENT,
+                             b15 ? d_c15 : nullptr);
         launch_records(s, P, d_var_cf, d_ext_pertB, d_stepB, d_recsB, nvar, d_brecB, 0);
         CB.recs = d_recsB;
         CB.brec = d_brecB;
         CB.ext_pert = d_ext_pertB;
         CB.step = d_stepB;
+        CB.b15 = b15 ? 1 : 0;
     }
     span_begin(SPAN_JAC);
     // uniform unsharded plans: the lmder bookkeeping rides in the
     // normal-equation kernels (no k_jac_epilogue launch), and with one
     // block size the camera-frame normal equations ride in the Jacobian
     // pass itself (k_jac_ne_u: J is written once and not re-read)
-    const bool fuse = lm && ne_epilogue_fusable(P) && nrows == 0;
+    const bool fuse = lm && ne_epilogue_fusable(P) && nrows == 0 && !b15;
     NeEpi epi;
     if (fuse) {
         epi.on = 1;
@@ -369,9 +372,10 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         span_end(SPAN_JAC);
     } else {
         const int do_xn = lm->first, do_gn = lm->fnorm_sq || lm->fnorm != 0.;
+        if (b15) launch_b15_s(s, lm->fnorm_sq, lm->fnorm, d_b15k + 4);
         launch_jac_epilogue(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g, d_diag, dx, lm->first,
                             lm->mode, lm->fnorm, lm->fnorm_sq, do_xn, do_gn, d_p_own, d_partial,
-                            nparts, pw);
+                            nparts, pw, b15 ? d_c15 : nullptr, d_b15k + 4, d_g15);
         span_end(SPAN_JAC);
         RedSpec rs{};
         rs.flag_slot = -1;
@@ -404,8 +408,11 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
                          const LmDec *dec) {
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
-    launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
-                      opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
+    // the parameter pass ran in the damped solve's back substitution, or here
+    const int tparts = trial_folded ? trial_fold_parts(P, n_trial_other) : nparts;
+    if (!trial_folded)
+        launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
+                          opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
     params_at = d_wa2;  // x <- wa2 on acceptance: the next Jacobian skips k_param_set
     records_enqueue(d_wa2, 0);  // ... and k_records
     span_begin(SPAN_RESID);
@@ -413,12 +420,12 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
                      (M + 255) / 256, d_Jrow, d_wa1, pr + 3 * (size_t)pw);
     RedSpec rs{};
     rs.flag_slot = -1;
-    rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_PNORM};
-    rs.row[rs.nrows++] = {4 * pw, nparts, 0, SL_XN2T};
+    rs.row[rs.nrows++] = {3 * pw, tparts, 0, SL_PNORM};
+    rs.row[rs.nrows++] = {4 * pw, tparts, 0, SL_XN2T};
     rs.row[rs.nrows++] = {5 * pw, trial_blocks(P), 0, SL_FNORM};
     rs.row[rs.nrows++] = {6 * pw, trial_blocks(P), 0, SL_JP};
     if (fill_dnorm) {  // the undamped solve's ||D xs||^2 and fail flag (solve_damped_enqueue)
-        rs.row[rs.nrows++] = {3 * pw, nparts, 0, SL_DNORM};
+        rs.row[rs.nrows++] = {3 * pw, tparts, 0, SL_DNORM};
         rs.flag_slot = SL_FAIL;
     }
     // unsharded: the LM decision after this trial reads slots [0, SL_LAST],
@@ -465,6 +472,8 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
                             sq ? h_seq : nullptr, seq_next, D);
         seq_pending = sq;
     }
+    if (b15)  // ||J p||^2 of J = J_s + f c^T (no host mirror on these plans)
+        launch_b15_jp(s, n, d_xs, d_g, d_c15, d_b15k + 4, d_scalar + SL_JP);
     mirror_pending = mirror;
     if (dec) {  // the next Jacobian's first launch, gated on the device's decision
         stage_slots();
@@ -477,7 +486,29 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
 void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dnorm_by_trial) {
+    if (b15 && !b15_inner) {
+        // B15: (M + U B U^T) xs = u + s c from M z_u = u and M z_c = c, the
+        // same damped factorisation formed twice (the right-hand side rides
+        // in every stage of the solve); the host loop never asks these plans
+        // for a by-trial norm (Plan::solve)
+        b15_inner = true;
+        solve_damped_enqueue(lam, -1, false, false);
+        MMBA_HIP(hipMemcpyAsync(d_z15u, d_xs, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        MMBA_HIP(hipMemcpyAsync(d_b15k + 5, d_scalar + SL_FAIL, sizeof(double),
+                                hipMemcpyDeviceToDevice, s));
+        std::swap(d_g, d_c15);
+        solve_damped_enqueue(lam, -1, false, false);
+        std::swap(d_g, d_c15);
+        MMBA_HIP(hipMemcpyAsync(d_z15c, d_xs, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        b15_inner = false;
+        launch_b15_combine(s, n, d_g, d_c15, d_z15u, d_z15c, d_b15k + 4, d_diag, d_xs, d_b15k,
+                           d_scalar, dnorm_slot, SL_FAIL, d_b15k + 5);
+        (void)defer;
+        (void)dnorm_by_trial;
+        return;
+    }
     const double t0 = wall_now();
+    trial_folded = false;
     // d_fail is zero here: launch_flag_to_scalar clears it after every use
     if (band && bs.use_bd && nG == 0 && nranks == 1 && dnorm_slot >= 0) {
         // the whole damped solve, ||D xs||^2 and the flag in one launch
@@ -581,7 +612,36 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         if (!(band && ((bs.use_bcr && bs.bcr.xs) || bs.use_bd)))
             launch_scatter_xR(s, P, d_xR, d_xs);
     }
-    if (nB_solved > 0) launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
+    trial_folded = false;
+    if (nB_solved > 0) {
+        if (trial_fold_ok) {
+            // the trial point's parameter pass rides in the back substitution
+            // (the last damped solve before a trial is the one it keeps)
+            launch_obs_wtx(s, P, d_W, d_xR, d_U);
+            TrialFold T;
+            T.x = d_x;
+            T.diag = d_diag;
+            T.wa1 = d_wa1;
+            T.wa2 = d_wa2;
+            T.wa3 = d_wa3;
+            T.ext = d_ext;
+            T.ext_pert = d_ext_pert;
+            T.step = d_step;
+            T.solver_type = opt.solver_type;
+            T.delta = opt.delta;
+            T.eps_dif = fd_eps();
+            T.other = d_trial_other;
+            T.nother = n_trial_other;
+            T.partial = d_partial + 3 * (size_t)pw;
+            T.rstride = pw;
+            launch_backsub_trial(s, P, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
+            trial_folded = true;
+            params_at = nullptr;  // the attribute block now holds the trial point
+            recs_full_at = nullptr;
+        } else {
+            launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
+        }
+    }
     if (dnorm_by_trial) {
         // the speculative trial's ||D p||^2 (p = -xs, same partial blocks and
         // order as k_sumsq: bit-identical) becomes ||D xs||^2, and its
@@ -643,6 +703,9 @@ void Plan::newton_enqueue(double dxnorm) {
         launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R, d_ymask,
                      d_ticket);
     }
+    // B15: v^T (M + U B U^T)^-1 v = v^T M^-1 v - w^T K^-1 w (the factor and
+    // z_u, z_c of the last damped solve)
+    if (b15) launch_b15_newton(s, n, d_v, d_z15u, d_z15c, d_b15k, d_scalar + SL_NEWT_B);
     allreduce(d_scalar + SL_NEWT_B, 2);
     t_linear += wall_now() - t0;
 }
@@ -685,7 +748,7 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *und
     double parl = 0.;
     const bool newton0 = !pl.rank_deficient && ok0;
     if (newton0) pl.newton_enqueue(dxnorm);
-    launch_sumsq_div(pl.s, pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts,
+    launch_sumsq_div(pl.s, pl.b15 ? pl.d_g15 : pl.d_g, pl.d_diag, pl.n, pl.d_partial, pl.nparts,
                      pl.d_scalar + Plan::SL_GDIV, pl.d_p_own, pl.d_ticket);
     pl.allreduce(pl.d_scalar + Plan::SL_GDIV, 1);
     pl.read_slots(Plan::SL_NEWT_B, Plan::SL_GDIV);
@@ -883,6 +946,19 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
     }
     for (int r = 0; r < nrows; ++r)
         if (rp[r] >= 0) fjac[(size_t)rp[r] * m + 2 * (size_t)M + r] = Jr[r];
+    if (b15) {  // J = J_s + f c^T
+        std::vector<double> c(n), f(2 * (size_t)M);
+        MMBA_HIP(hipMemcpy(c.data(), d_c15, sizeof(double) * n, hipMemcpyDeviceToHost));
+        MMBA_HIP(hipMemcpy(f.data(), d_f, sizeof(double) * f.size(), hipMemcpyDeviceToHost));
+        for (int p = 0; p < n; ++p) {
+            if (c[p] == 0.) continue;
+            for (int i = 0; i < M; ++i) {
+                const int r = ref_of_dev[i];
+                fjac[(size_t)p * m + 2 * r] += f[2 * (size_t)i] * c[p];
+                fjac[(size_t)p * m + 2 * r + 1] += f[2 * (size_t)i + 1] * c[p];
+            }
+        }
+    }
     return MMBA_OK;
 }
 
@@ -1048,6 +1124,8 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         A.trace = d_coop_trace;
         A.trace_cap = COOP_TRACE;
         A.out = d_coop_out;
+        static const bool coop_dbg = std::getenv("MMBA_COOP_DEBUG") != nullptr;
+        A.probe = coop_dbg ? reinterpret_cast<long long *>(d_coop_trace + COOP_TRACE - 64) : nullptr;
         A.solver_type = opt.solver_type;
         A.mode = mode;
         A.maxfev = maxfev;
@@ -1071,6 +1149,15 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             if (o.failed) {
                 set_error("damped normal-equation factorisation failed (cooperative solve)");
                 throw DeviceError();
+            }
+            if (A.probe) {  // phase ends of workgroup 0 (100 MHz ticks)
+                std::vector<long long> pr(64);
+                MMBA_HIP(hipMemcpy(pr.data(), A.probe, sizeof(long long) * 64,
+                                   hipMemcpyDeviceToHost));
+                std::fprintf(stderr, "[mmba coop] %d phases (us):", o.nprobe);
+                for (int k = 1; k < std::min(o.nprobe, 64); ++k)
+                    std::fprintf(stderr, " %.1f", (pr[k] - pr[k - 1]) / 100.);
+                std::fprintf(stderr, "\n");
             }
             if (trace && o.ntrace > 0) {
                 std::vector<double> tr(std::min(o.ntrace, COOP_TRACE));
@@ -1157,7 +1244,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
             // ||D xs|| comes from the trial's ||D p|| reduction (no separate
             // norm launches), and sharded plans fold [DNORM, FAIL] into the
             // trial's all-reduce
-            const bool by_trial = spec && !(band && bs.use_bd && nG == 0 && nranks == 1);
+            const bool by_trial = spec && !(band && bs.use_bd && nG == 0 && nranks == 1) && !b15;
             lmpar_first_enqueue(*this, spec && nranks > 1, by_trial);
             // the next Jacobian is enqueued behind the trial, gated on the
             // device's restatement of the decision the host takes below

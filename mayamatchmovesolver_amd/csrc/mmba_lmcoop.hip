@@ -537,6 +537,12 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         ++ntr;
     };
 
+    int npr = 0;
+    auto stamp = [&]() {
+        if (A.probe && g == 0 && tid == 0 && npr < 64) A.probe[npr] = (long long)wall_clock64();
+        ++npr;
+    };
+    stamp();
     nfev = 1;
     fe = 1;
     eval(s_sx, nullptr, A.f, A.dist);  // x0 (lmder's first fcn call)
@@ -545,12 +551,15 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
     trace(fnorm);
     int iter = 1;
     while (!aborted) {
+        stamp();
         jacobian();
+        stamp();
         ++njev;
         je += P.n;
         if (!lmder) nfev += P.n;
         const bool first = iter == 1;
         aborted = grid_reduce(0, 0u);  // every slot stored
+        stamp();
         if (aborted) break;
         assemble();
         {
@@ -585,7 +594,9 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
                 s_gv[2] = b2;
             }
             __syncthreads();
+            stamp();
             aborted = grid_reduce(5, 2u | 4u | 16u);
+            stamp();
         }
         if (aborted) break;
         const bool rank_def = s_gv[2] != 0.;
@@ -714,7 +725,9 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
             __syncthreads();
             ++nfev;
             ++fe;
+            stamp();
             eval(s_swa2, s_swa1, fsel ? A.f : A.ft, fsel ? A.dist : A.distt);
+            stamp();
             // [||f||^2, ||J p||^2, ||D p||^2, ||D wa2||^2]
             if (tid == 0) {
                 s_gv[2] = bpn;
@@ -722,6 +735,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
             }
             __syncthreads();
             aborted = grid_reduce(4, 0u);
+            stamp();
             if (aborted) break;
             const double fnorm1 = sqrt(s_gv[0]);
             const double pnorm = sqrt(s_gv[2]);
@@ -793,6 +807,7 @@ __global__ void __launch_bounds__(CT) k_lm_coop(DevProblem P, CoopArgs A) {
         o.ntrace = ntr;
         o.failed = failed ? 1 : 0;
         o.aborted = aborted ? 1 : 0;
+        o.nprobe = npr;
         *A.out = o;
     }
 }

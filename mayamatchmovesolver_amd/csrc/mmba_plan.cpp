@@ -573,12 +573,17 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     };
     for (int i = 0; i < M; ++i)
         if (obs_cols(i) > LMAX) throw Unsupported{"more than 20 parameters reach one observation"};
-    // Central differences and the robust loss are only well defined where
-    // every lmder FD column re-measures every marker row: the reference
-    // zero-initialises errorListB (adjust_solveFunc.cpp:412) and re-applies
-    // the loss to the whole buffer (adjust_measureErrors.cpp:553-558), so a
-    // row a column skips (another frame than an animated parameter's, or an
-    // observation no parameter reaches) would get a dense garbage entry.
+    // Central differences and the robust loss where an lmder FD column skips
+    // marker rows (another frame than an animated parameter's): the
+    // reference zero-initialises errorListB (adjust_solveFunc.cpp:412), so a
+    // skipped row j of an animated central column p gets f_j c_p,
+    // c_p = 0.5 / (|dA| + |dB|) (errorListA keeps f, :331-333, 468-471) --
+    // J = J_s + f c^T, a rank-one term (B15, Plan::b15).  That needs every
+    // row of the column's own frame to be one the column reaches (else J_s
+    // would gain entries outside the block structure); the robust loss
+    // re-applies the loss to the whole buffer (adjust_measureErrors.cpp:
+    // 553-558) and stays refused there.
+    b15 = false;
     if (lmder_opt && (central || opt.robust_loss)) {
         int fmin = F, fmax = -1;
         for (int i = 0; i < Mg; ++i) {
@@ -589,6 +594,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int p = 0; p < n && !masked; ++p)
             if (pr->param_frame[p] >= 0 && (fmin != pr->param_frame[p] || fmax != fmin))
                 masked = true;
+        const bool skips = masked;  // some animated column skips another frame's rows
         for (int i = 0; i < M && !masked; ++i) {
             const int cf = d_cf[i];
             const int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
@@ -596,11 +602,39 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                            (cam_lpar_off[d_cam[i] + 1] - cam_lpar_off[d_cam[i]]);
             if (nl == 0) masked = true;
         }
+        if (masked && central && !opt.robust_loss && nranks == 1 && nrows == 0 && !rs_on) {
+            // every observation of an animated parameter's frame reached by it
+            std::vector<std::vector<int>> anim_at(F);
+            for (int p = 0; p < n; ++p)
+                if (pr->param_frame[p] >= 0) anim_at[pr->param_frame[p]].push_back(p);
+            bool cover = true;
+            std::vector<int> reach;
+            for (int i = 0; i < M && cover; ++i) {
+                const auto &need = anim_at[d_frame[i]];
+                if (need.empty()) continue;
+                reach.clear();
+                const int cf = d_cf[i];
+                for (int t = cf_var_off[cf] + 1; t < cf_var_off[cf + 1]; ++t)
+                    reach.push_back(cf_var_param[t]);
+                for (int t = bnd_par_off[d_bnd[i]]; t < bnd_par_off[d_bnd[i] + 1]; ++t)
+                    reach.push_back(bnd_par[t]);
+                const int c = d_cam[i];
+                for (int q = cam_lpar_off[c]; q < cam_lpar_off[c + 1]; ++q)
+                    reach.push_back(cam_lpar[q]);
+                for (int p : need)
+                    if (std::find(reach.begin(), reach.end(), p) == reach.end()) cover = false;
+            }
+            if (cover) {  // (rows no column reaches stay zero rows of J)
+                b15 = skips;
+                masked = false;
+            }
+        }
         if (masked)
             throw Unsupported{std::string(central ? "central differences" : "robust loss") +
                               " with lmder where an FD column skips marker rows (animated "
-                              "parameters over several frames, or observations no parameter "
-                              "reaches): the reference's Jacobian is not defined there (B15)"};
+                              "parameters over several frames) and its own frame holds rows it "
+                              "does not reach, or with the robust loss, attribute rows, the "
+                              "rolling shutter or shards (B15)"};
     }
     // observations grouped by bundle
     std::vector<int> bobs_off(nB + 1, 0), bobs(M);
@@ -1168,6 +1202,14 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_recsB = dalloc<double>((size_t)nvar * CAMREC);
         d_brecB = dalloc<double>((size_t)nB * BREC);
     }
+    if (b15) {
+        d_c15 = dalloc<double>(n);
+        d_g15 = dalloc<double>(n);
+        d_z15u = dalloc<double>(n);
+        d_z15c = dalloc<double>(n);
+        d_b15k = dalloc<double>(8);
+        MMBA_HIP(hipMemsetAsync(d_b15k, 0, sizeof(double) * 8, s));
+    }
     d_J = dalloc<double>(std::max((size_t)2 * LMAX * M, (size_t)m + M));
     d_jcol = dalloc<int>((size_t)LMAX * M);
     d_nloc = dalloc<int>(M);
@@ -1193,6 +1235,19 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_nu = dalloc<double>((size_t)3 * std::max(nB, 1));
     d_ngp = dalloc<double>((size_t)std::max(nG, 1) * std::max(nB, 1));
     pw = std::max(std::max(nparts, residual_blocks(P)), ncf + (nB + 255) / 256);
+    {
+        // parameters outside every solved bundle: the extra workgroups of
+        // the fused back substitution + trial pass
+        std::vector<char> inb(n, 0);
+        for (int b = 0; b < nB; ++b)  // a bundle's own parameters come first (bnd_pb of them)
+            for (int a = 0; a < bnd_pb[b]; ++a) inb[bnd_par[bnd_par_off[b] + a]] = 1;
+        std::vector<int> other;
+        for (int j = 0; j < n; ++j)
+            if (!inb[j]) other.push_back(j);
+        n_trial_other = (int)other.size();
+        d_trial_other = upload(other.empty() ? std::vector<int>(1, 0) : other);
+        pw = std::max(pw, trial_fold_parts(P, n_trial_other));
+    }
     d_partial = dalloc<double>((size_t)8 * pw);  // rows 0..7 (launch_dist_stats: 0..2)
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
@@ -1287,6 +1342,10 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     *h_seq = 0;
     if (const char *e = std::getenv("MMBA_SEQ_POLL")) seq_poll = std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_PRE_JAC")) pre_jac = std::atoi(e) != 0;
+    trial_fold_ok = nranks == 1 && nB_solved > 0;
+    if (const char *e = std::getenv("MMBA_TRIAL_FOLD")) trial_fold_ok = trial_fold_ok && std::atoi(e) != 0;
+    if (const char *e = std::getenv("MMBA_BACKSUB_WTX"))  // the fused form needs the two-pass u_i
+        trial_fold_ok = trial_fold_ok && std::atoi(e) != 0;
     d_gate = dalloc<int>(1);
     MMBA_HIP(hipMemsetAsync(d_gate, 0, sizeof(int), s));
     d_mticket = dalloc<unsigned>(1);
@@ -1296,6 +1355,10 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         if (param_weight[j] <= 0.) pweight_ok = false;
     MMBA_HIP(hipMemsetAsync(d_mticket, 0, sizeof(unsigned), s));
     if (const char *e = std::getenv("MMBA_HOST_MIRROR")) host_mirror = std::atoi(e) != 0;
+    if (b15) {  // the rank-one term corrects ||J p|| after the trial's reduction
+        host_mirror = false;
+        trial_fold_ok = false;
+    }
     fold_init = dest_diag_all && use_dest && nranks == 1 && nG == 0 && !rs_on && nRpad == nR &&
                 (pc_uniform == 6 || pc_uniform == 7);
     if (const char *e = std::getenv("MMBA_FOLD_SCHUR_INIT")) fold_init = fold_init && std::atoi(e) != 0;

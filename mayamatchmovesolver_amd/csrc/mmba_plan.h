@@ -112,7 +112,7 @@ struct Plan {
     unsigned *h_seq = nullptr;
     unsigned seq_next = 0;
     bool seq_pending = false;  // the next mirrored read_slots polls h_seq
-    bool seq_poll = false;  // MMBA_SEQ_POLL=1 (pending its GPU A/B)
+    bool seq_poll = true;  // MMBA_SEQ_POLL=0: stream events
     bool coop_ok = false;
     int coop_G = 0;
     bool coop_lens = false;
@@ -169,6 +169,18 @@ struct Plan {
     double *d_Jrow = nullptr;      // their Jacobian entries (one column each)
     // central differences (lmder, autoDiffType central): the deltaB pass
     bool central = false;
+    // B15: central differences where animated columns skip the other
+    // frames' rows.  The reference's Jacobian is then J = J_s + f c^T (f at
+    // the Jacobian's point, c_p = 0.5 / (|dA| + |dB|) of animated central
+    // columns): J_s is the sparse Jacobian the kernels store, the rank-one
+    // term rides in the epilogue (column norms, J^T f), the damped solve
+    // (Woodbury over two right-hand sides, u = J_s^T f and c, with one
+    // factorisation each), lmpar's Newton term and ||J p||.
+    bool b15 = false, b15_inner = false;
+    double *d_c15 = nullptr;   // c (n)
+    double *d_g15 = nullptr;   // J^T f = u + s c (n): gnorm, lmpar's ||D^-1 g||
+    double *d_z15u = nullptr, *d_z15c = nullptr;  // M^-1 u, M^-1 c of the last damped solve
+    double *d_b15k = nullptr;  // [K^-1 (4), s, fail of the first solve]
     // rolling shutter (mmba.h ABI 3, mmba_rs.hip)
     bool rs_on = false;
     double *d_ext_pertB = nullptr, *d_stepB = nullptr, *d_recsB = nullptr, *d_brecB = nullptr;
@@ -195,10 +207,11 @@ struct Plan {
     double *h_scalar = nullptr;  // pinned
     // MMBA_HOST_MIRROR=1: trial reductions write slots [0, SL_LAST] straight
     // into h_scalar (the last k_reduce_multi block) and read_slots skips its
-    // copy launch.  Off by default: measured 3 % slower per C4 solve (the
-    // device's writes to host memory delay the completion the host polls)
+    // copy launch.  With a stream-event wait it measured 3 % slower per C4
+    // solve (round 2); with the page-locked sequence word the LM thread polls
+    // (seq_poll) it is 4 % faster (C4 14.48 -> 13.90 ms, profiles/r3_prejac)
     unsigned *d_mticket = nullptr;
-    bool host_mirror = false, mirror_pending = false;
+    bool host_mirror = true, mirror_pending = false;
     // every solved camera-frame has a diagonal Schur destination; fold_init:
     // k_schur_init rides in k_schur_dest_u (SchurInitFold)
     bool dest_diag_all = false, fold_init = false, dest_diag_ii = false;
@@ -353,6 +366,12 @@ struct Plan {
     // (LmDec): it runs only when that decision takes the trial and goes on,
     // so the GPU starts the next iteration while the host reads the trial.
     // MMBA_PRE_JAC=0: off.
+    // the trial point's parameter pass fused into the bundle back
+    // substitution of the damped solve (launch_backsub_trial);
+    // MMBA_TRIAL_FOLD=0: k_trial_prep
+    bool trial_fold_ok = false, trial_folded = false;
+    int *d_trial_other = nullptr;
+    int n_trial_other = 0;
     bool pre_jac = true;
     bool pre_jac_pending = false;   // enqueued, the host has not decided yet
     const double *pre_jac_x = nullptr;

@@ -188,17 +188,6 @@ def test_central_static_rig(kw, mode, oracle, gpu_ctx):
     check(prob, opt, oracle, gpu_ctx)
 
 
-def test_central_refused_where_undefined(gpu_ctx):
-    """Animated parameters over several frames: the reference's central
-    Jacobian has dense garbage rows there (errorListB zero-initialised, B15),
-    so the library refuses instead of computing something else."""
-    prob = S.edge_scene()
-    opt = make_options(auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL)
-    with pytest.raises(MmbaError) as e:
-        Solver(prob, opt, context=gpu_ctx)
-    assert e.value.code == abi.MMBA_ERR_UNSUPPORTED
-
-
 # --- stiffness / smoothness rows, robust loss, paramWeightList ---------------
 
 @pytest.mark.parametrize("solver_type", [LMDER, LMDIF])

@@ -31,7 +31,7 @@ for step in "$@"; do
       cat "$OUT/bench.json" ;;
     benchcfg:*)
       c=${step#benchcfg:}
-      timeout -k 10 400 python -u bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
+      timeout -k 10 400 python -u bench.py --config "$c" --steps 8 --warmup 3 --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
       cat "$OUT/bench_$c.json" ;;
     prof)
       cd /tmp && cd "$ROOT"
