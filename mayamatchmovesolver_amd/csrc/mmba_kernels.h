@@ -41,7 +41,8 @@ void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
                          double *diag, const double *x, int first, int mode, double fnorm,
                          const double *fnorm_sq, int do_xn, int do_gn, const int *mask,
                          double *partial, int nparts, int rstride, const double *c15 = nullptr,
-                         const double *s15 = nullptr, double *gfull = nullptr);
+                         const double *s15 = nullptr, double *gfull = nullptr,
+                         const double *adiag15 = nullptr, const double *u15 = nullptr);
 // lmder trial point x - xs with setParameters at it; partial rows 0 (pnorm^2)
 // and 1 (||D x_new||^2)
 void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
@@ -108,9 +109,9 @@ void launch_residual_jp(hipStream_t s, const DevProblem &P, const double *recs, 
 // factor 0.5 / (|dA| + |dB|) (0: forward column).  recs == nullptr: forward.
 struct CentralB {
     const double *recs = nullptr, *brec = nullptr, *ext_pert = nullptr, *step = nullptr;
-    // B15: animated central columns leave out f c (the rows other frames
-    // skip carry f c^T, applied as a rank-one term: Plan::b15)
-    int b15 = 0;
+    // B15 (Plan::b15): camera-frame block columns stored in the basis Q_cf
+    // (q15: ncf x PCMAX x PCMAX) less f kappa_cf on the first (kap15)
+    const double *q15 = nullptr, *kap15 = nullptr;
 };
 // c15 (optional): c_p = 0.5 / (|dA| + |dB|) of animated central columns, else 0
 void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, double *ext_pertB,
@@ -119,12 +120,28 @@ void launch_param_central(hipStream_t s, const DevProblem &P, const double *x, d
 // Jacobian's point (*fsq, or fn^2) -> *out
 void launch_b15_s(hipStream_t s, const double *fsq, double fn, double *out);
 // xs = (M + U B U^T)^-1 (u + s c) from z_u = M^-1 u, z_c = M^-1 c (Woodbury,
-// U = [u c], B = [0 1; 1 s]); K^-1 -> kinv[0..3]; ||D xs||^2 -> scalar[dnorm_slot]
-// (dnorm_slot >= 0); scalar[fail_slot] = max(itself, *fail_prev, singular K)
+// U = [u c], B = [0 1; 1 s]); K^-1 -> kinv[0..3]; scalar[fail_slot] =
+// max(itself, *fail_prev, singular K)
 void launch_b15_combine(hipStream_t s, int n, const double *u, const double *c, const double *zu,
-                        const double *zc, const double *sp, const double *diag, double *xs,
-                        double *kinv, double *scalar, int dnorm_slot, int fail_slot,
-                        const double *fail_prev);
+                        const double *zc, const double *sp, double *xs, double *kinv,
+                        double *scalar, int fail_slot, const double *fail_prev);
+// per camera-frame Householder basis Q (Q c_cf = kappa e_0) -> q15, kap15;
+// c in that basis -> cr
+void launch_b15_q(hipStream_t s, const DevProblem &P, const double *c, double *q15, double *kap15,
+                  double *cr);
+// out = Q x on camera-frame parameters (its own inverse), copy elsewhere
+void launch_b15_rot(hipStream_t s, const DevProblem &P, const double *q15, const double *x,
+                    double *out);
+// AccL = Acc + lam Q D^2 Q per camera-frame block; diagL = diag, 0 on
+// camera-frame parameters
+void launch_b15_accl(hipStream_t s, const DevProblem &P, const double *Acc, const double *q15,
+                     const double *diag, double lam, double *AccL, double *diagL);
+// diag(Q A Q) -> adiag and Q g -> u on camera-frame parameters (g copied elsewhere)
+void launch_b15_unrot(hipStream_t s, const DevProblem &P, const double *Acc, const double *g,
+                      const double *q15, double *adiag, double *u);
+void launch_b15_unrot_J(hipStream_t s, const DevProblem &P, double *J, const double *q15);
+// ||D x||^2 -> *out (one workgroup, fixed order)
+void launch_b15_dnorm(hipStream_t s, int n, const double *x, const double *diag, double *out);
 // *out -= w^T K^-1 w, w = [z_u . v, z_c . v] (lmpar's v^T (A + lam D^2)^-1 v)
 void launch_b15_newton(hipStream_t s, int n, const double *v, const double *zu, const double *zc,
                        const double *kinv, double *out);

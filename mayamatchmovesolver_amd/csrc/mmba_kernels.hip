@@ -679,12 +679,6 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
             const Resid rb = evalB();
             jx = (r.ex - rb.ex) * sB;
             jy = (r.ey - rb.ey) * sB;
-            if (CB.b15 && P.p_frame[p] >= 0) {
-                // B15: J = J_s + f c^T, so the column's own rows keep
-                // (eA - eB - f) c (the rank-one term adds f c back)
-                jx -= r0.ex * sB;
-                jy -= r0.ey * sB;
-            }
             if (p == pstale) rs = rb;  // the column's last measureErrors
         } else {
             if (lmder) {  // st = 1/delta, multiplied (adjust_solveFunc.cpp:395-402)
@@ -716,6 +710,38 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
                    if (bside) bundle_position(P, b, fr, Override{P.p_attr[p], CB.ext_pert[p]}, bq);
                    return residual_l(P, &CB.recs[(size_t)t * CAMREC], bq, mx, my, sw, hl, lc0);
                });
+    }
+    if (CB.q15) {
+        // B15 (Plan::b15): the camera-frame block's columns (the first pc
+        // emitted) in the basis Q_cf (Q c = kappa e_0): J_s Q = J Q - f kappa
+        // e_0^T with J the central differences of the block's own frame.  The
+        // large f c part of the block lands in one column, so the block's
+        // normal equations keep the accuracy of its differences.
+        const int pc = P.cf_pc[cf];
+        const double *Q = CB.q15 + (size_t)cf * PCMAX * PCMAX;
+        const double kap = CB.kap15[cf];
+        double ax[PCMAX], ay[PCMAX];
+#pragma unroll
+        for (int a = 0; a < PCMAX; ++a) {
+            ax[a] = a < pc ? J[(size_t)(2 * a) * M + i] : 0.;
+            ay[a] = a < pc ? J[(size_t)(2 * a + 1) * M + i] : 0.;
+        }
+#pragma unroll
+        for (int a2 = 0; a2 < PCMAX; ++a2) {
+            if (a2 >= pc) break;
+            double sx = 0., sy = 0.;
+#pragma unroll
+            for (int a = 0; a < PCMAX; ++a) {
+                sx = fma(ax[a], Q[a * PCMAX + a2], sx);
+                sy = fma(ay[a], Q[a * PCMAX + a2], sy);
+            }
+            if (a2 == 0) {
+                sx -= r0.ex * kap;
+                sy -= r0.ey * kap;
+            }
+            J[(size_t)(2 * a2) * M + i] = sx;
+            J[(size_t)(2 * a2 + 1) * M + i] = sy;
+        }
     }
     // bundle-side parameters not already covered by a camera variant
     if (p4.w >= 0) {  // fast bundle: perturbed positions from the record
@@ -1602,7 +1628,7 @@ __global__ void __launch_bounds__(256) k_jac_epilogue(
     double *diag, const double *__restrict__ x, int first, int mode, double fnorm,
     const double *__restrict__ fnorm_sq, int do_xn, int do_gn, const int *__restrict__ mask,
     double *partial, int rstride, const double *__restrict__ c15, const double *__restrict__ s15,
-    double *gfull) {
+    double *gfull, const double *__restrict__ adiag15, const double *__restrict__ u15) {
     __shared__ double red[256];
     if (fnorm_sq) {
         fnorm = sqrt(*fnorm_sq);
@@ -1632,7 +1658,12 @@ __global__ void __launch_bounds__(256) k_jac_epilogue(
         }
         if (c15) {
             // B15: ||J_p||^2 and (J^T f)_p of J = J_s + f c^T, with
-            // u = J_s^T f in g: A_pp + 2 c_p u_p + s c_p^2, u_p + s c_p
+            // u = J_s^T f: A_pp + 2 c_p u_p + s c_p^2, u_p + s c_p (camera-frame
+            // parameters: A_pp and u_p back from the rotated block, adiag15 / u15)
+            if (cls == PC_CF) {
+                d = adiag15[p];
+                gp = u15[p];
+            }
             const double cp = c15[p];
             d = fmax(d + 2. * cp * gp + s15v * cp * cp, 0.);
             gp = gp + s15v * cp;
@@ -2894,10 +2925,11 @@ void launch_jac_epilogue(hipStream_t s, const DevProblem &P, const double *Acc,
                          double *diag, const double *x, int first, int mode, double fnorm,
                          const double *fnorm_sq, int do_xn, int do_gn, const int *mask,
                          double *partial, int nparts, int rstride, const double *c15,
-                         const double *s15, double *gfull) {
+                         const double *s15, double *gfull, const double *adiag15,
+                         const double *u15) {
     k_jac_epilogue<<<nparts, 256, 0, s>>>(P, Acc, Abb, aggbuf, aggbuf + NGMAX * NGMAX, acnorm,
                                           g, diag, x, first, mode, fnorm, fnorm_sq, do_xn, do_gn,
-                                          mask, partial, rstride, c15, s15, gfull);
+                                          mask, partial, rstride, c15, s15, gfull, adiag15, u15);
 }
 void launch_trial_prep(hipStream_t s, const DevProblem &P, const double *xs, const double *x,
                        const double *diag, double *wa1, double *wa2, double *wa3, double *ext,
@@ -3202,8 +3234,7 @@ __global__ void k_b15_s(const double *fsq, double fn, double *out) {
 __global__ void __launch_bounds__(1024) k_b15_combine(
     int n, const double *__restrict__ u, const double *__restrict__ c,
     const double *__restrict__ zu, const double *__restrict__ zc, const double *__restrict__ sp,
-    const double *__restrict__ diag, double *xs, double *kinv, double *scalar, int dnorm_slot,
-    int fail_slot, const double *__restrict__ fail_prev) {
+    double *xs, double *kinv, double *scalar, int fail_slot, const double *__restrict__ fail_prev) {
     __shared__ double red[4][1024];
     double d[4] = {0., 0., 0., 0.};
     for (int j = threadIdx.x; j < n; j += 1024) {
@@ -3223,20 +3254,12 @@ __global__ void __launch_bounds__(1024) k_b15_combine(
     const double r0 = d[0] + s * d[1], r1 = d[2] + s * d[3];
     const double al = i00 * r0 + i01 * r1, be = i10 * r0 + i11 * r1;
     const double cu = 1. - al, cc = s - be;
-    double dn[1] = {0.};
-    for (int j = threadIdx.x; j < n; j += 1024) {
-        const double v = cu * zu[j] + cc * zc[j];
-        xs[j] = v;
-        const double w = diag[j] * v;
-        dn[0] += w * w;
-    }
-    b15_block_sum<1>(dn, red);
+    for (int j = threadIdx.x; j < n; j += 1024) xs[j] = cu * zu[j] + cc * zc[j];
     if (threadIdx.x == 0) {
         kinv[0] = i00;
         kinv[1] = i01;
         kinv[2] = i10;
         kinv[3] = i11;
-        if (dnorm_slot >= 0) scalar[dnorm_slot] = dn[0];
         double f = fmax(scalar[fail_slot], *fail_prev);
         if (sing) f = fmax(f, 1.);
         scalar[fail_slot] = f;
@@ -3276,11 +3299,204 @@ void launch_b15_s(hipStream_t s, const double *fsq, double fn, double *out) {
     k_b15_s<<<1, 64, 0, s>>>(fsq, fn, out);
 }
 void launch_b15_combine(hipStream_t s, int n, const double *u, const double *c, const double *zu,
-                        const double *zc, const double *sp, const double *diag, double *xs,
-                        double *kinv, double *scalar, int dnorm_slot, int fail_slot,
-                        const double *fail_prev) {
-    k_b15_combine<<<1, 1024, 0, s>>>(n, u, c, zu, zc, sp, diag, xs, kinv, scalar, dnorm_slot,
-                                     fail_slot, fail_prev);
+                        const double *zc, const double *sp, double *xs, double *kinv,
+                        double *scalar, int fail_slot, const double *fail_prev) {
+    k_b15_combine<<<1, 1024, 0, s>>>(n, u, c, zu, zc, sp, xs, kinv, scalar, fail_slot, fail_prev);
+}
+
+// Q_cf = I - beta v v^T with v = c_cf + sign(c_0) |c_cf| e_0 (Householder:
+// Q c_cf = kappa e_0, kappa = -sign(c_0) |c_cf|; Q = I where c_cf = 0), and
+// c in that basis (kappa at the block's first parameter, 0 elsewhere).
+__global__ void k_b15_q(DevProblem P, const double *__restrict__ c, double *q15, double *kap15,
+                        double *cr) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < P.n) {
+        double v = c[t];
+        if (P.p_class[t] == PC_CF) {  // kappa at the block's first parameter, else 0
+            const int cf = P.p_blk[t], pc = P.cf_pc[cf], voff = P.cf_var_off[cf];
+            v = 0.;
+            if (P.p_pos[t] == P.cf_roff[cf]) {
+                double n2 = 0.;
+                for (int a = 0; a < pc; ++a) {
+                    const double ca = c[P.cf_var_param[voff + 1 + a]];
+                    n2 += ca * ca;
+                }
+                if (n2 > 0.) v = (c[t] < 0. ? 1. : -1.) * sqrt(n2);
+            }
+        }
+        cr[t] = v;
+    }
+    if (t >= P.ncf) return;
+    const int cf = t, pc = P.cf_pc[cf], voff = P.cf_var_off[cf];
+    double v[PCMAX];
+    double nrm2 = 0.;
+#pragma unroll
+    for (int a = 0; a < PCMAX; ++a) {
+        v[a] = a < pc ? c[P.cf_var_param[voff + 1 + a]] : 0.;
+        nrm2 += v[a] * v[a];
+    }
+    double *Q = q15 + (size_t)cf * PCMAX * PCMAX;
+    double kap = 0.;
+    if (nrm2 > 0.) {
+        const double nrm = sqrt(nrm2), sg = v[0] < 0. ? -1. : 1.;
+        kap = -sg * nrm;
+        v[0] += sg * nrm;
+        double vv = 0.;
+#pragma unroll
+        for (int a = 0; a < PCMAX; ++a) vv += v[a] * v[a];
+        const double beta = 2. / vv;
+#pragma unroll
+        for (int a = 0; a < PCMAX; ++a)
+#pragma unroll
+            for (int b = 0; b < PCMAX; ++b) Q[a * PCMAX + b] = (a == b ? 1. : 0.) - beta * v[a] * v[b];
+    } else {
+#pragma unroll
+        for (int a = 0; a < PCMAX; ++a)
+#pragma unroll
+            for (int b = 0; b < PCMAX; ++b) Q[a * PCMAX + b] = a == b ? 1. : 0.;
+    }
+    kap15[cf] = kap;
+}
+
+// out = Q x per camera-frame block (Q symmetric orthogonal: its own inverse),
+// other parameters copied
+__global__ void k_b15_rot(DevProblem P, const double *__restrict__ q15,
+                          const double *__restrict__ x, double *out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    if (P.p_class[p] != PC_CF) {
+        out[p] = x[p];
+        return;
+    }
+    const int cf = P.p_blk[p], a = P.p_pos[p] - P.cf_roff[cf];
+    const int pc = P.cf_pc[cf], voff = P.cf_var_off[cf];
+    const double *Q = q15 + (size_t)cf * PCMAX * PCMAX + a * PCMAX;
+    double acc = 0.;
+    for (int b = 0; b < pc; ++b) acc = fma(Q[b], x[P.cf_var_param[voff + 1 + b]], acc);
+    out[p] = acc;
+}
+
+// Damped block of the rotated system: AccL = Acc + lam Q D^2 Q per camera-frame
+// (the solve then adds nothing there: diagL = 0 on camera-frame parameters)
+__global__ void k_b15_accl(DevProblem P, const double *__restrict__ Acc,
+                           const double *__restrict__ q15, const double *__restrict__ diag,
+                           double lam, double *AccL, double *diagL) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < P.n) diagL[t] = P.p_class[t] == PC_CF ? 0. : diag[t];
+    if (t >= P.ncf) return;
+    const int cf = t, pc = P.cf_pc[cf], voff = P.cf_var_off[cf];
+    const double *Q = q15 + (size_t)cf * PCMAX * PCMAX;
+    const double *A = Acc + (size_t)cf * PCMAX * PCMAX;
+    double *AL = AccL + (size_t)cf * PCMAX * PCMAX;
+    double d2[PCMAX];
+    for (int k = 0; k < pc; ++k) {
+        const double d = diag[P.cf_var_param[voff + 1 + k]];
+        d2[k] = d * d;
+    }
+    for (int a = 0; a < PCMAX; ++a)
+        for (int b = 0; b < PCMAX; ++b) {
+            double v = A[a * PCMAX + b];
+            if (a < pc && b < pc) {
+                double w = 0.;
+                for (int k = 0; k < pc; ++k) w = fma(Q[k * PCMAX + a] * d2[k], Q[k * PCMAX + b], w);
+                v += lam * w;
+            }
+            AL[a * PCMAX + b] = v;
+        }
+}
+
+// The camera-frame parameters' A_pp and u_p in the original basis:
+// diag(Q A Q), Q u (epilogue of a rotated Jacobian)
+__global__ void k_b15_unrot(DevProblem P, const double *__restrict__ Acc,
+                            const double *__restrict__ g, const double *__restrict__ q15,
+                            double *adiag, double *u) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    if (P.p_class[p] != PC_CF) {
+        u[p] = g[p];
+        adiag[p] = 0.;
+        return;
+    }
+    const int cf = P.p_blk[p], a = P.p_pos[p] - P.cf_roff[cf];
+    const int pc = P.cf_pc[cf], voff = P.cf_var_off[cf];
+    const double *Q = q15 + (size_t)cf * PCMAX * PCMAX + a * PCMAX;
+    const double *A = Acc + (size_t)cf * PCMAX * PCMAX;
+    double ua = 0., da = 0.;
+    for (int k = 0; k < pc; ++k) {
+        ua = fma(Q[k], g[P.cf_var_param[voff + 1 + k]], ua);
+        double r = 0.;
+        for (int l = 0; l < pc; ++l) {
+            const int hi = k > l ? k : l, lo = k > l ? l : k;  // lower triangle
+            r = fma(A[hi * PCMAX + lo], Q[l], r);
+        }
+        da = fma(Q[k], r, da);
+    }
+    u[p] = ua;
+    adiag[p] = da;
+}
+
+// Dense-Jacobian readback of a rotated J: the camera-frame block's first pc
+// columns back to the original basis (J_s = (J_s Q) Q)
+__global__ void k_b15_unrot_J(DevProblem P, double *J, const double *__restrict__ q15) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.M) return;
+    const int M = P.M, cf = P.obs_cf[i], pc = P.cf_pc[cf];
+    const double *Q = q15 + (size_t)cf * PCMAX * PCMAX;
+    double ax[PCMAX], ay[PCMAX];
+#pragma unroll
+    for (int a = 0; a < PCMAX; ++a) {
+        ax[a] = a < pc ? J[(size_t)(2 * a) * M + i] : 0.;
+        ay[a] = a < pc ? J[(size_t)(2 * a + 1) * M + i] : 0.;
+    }
+#pragma unroll
+    for (int a2 = 0; a2 < PCMAX; ++a2) {
+        if (a2 >= pc) break;
+        double sx = 0., sy = 0.;
+#pragma unroll
+        for (int a = 0; a < PCMAX; ++a) {
+            sx = fma(ax[a], Q[a * PCMAX + a2], sx);
+            sy = fma(ay[a], Q[a * PCMAX + a2], sy);
+        }
+        J[(size_t)(2 * a2) * M + i] = sx;
+        J[(size_t)(2 * a2 + 1) * M + i] = sy;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_b15_dnorm(int n, const double *__restrict__ x,
+                                                    const double *__restrict__ diag, double *out) {
+    __shared__ double red[1][1024];
+    double v[1] = {0.};
+    for (int j = threadIdx.x; j < n; j += 1024) {
+        const double w = diag[j] * x[j];
+        v[0] += w * w;
+    }
+    b15_block_sum<1>(v, red);
+    if (threadIdx.x == 0) *out = v[0];
+}
+
+void launch_b15_q(hipStream_t s, const DevProblem &P, const double *c, double *q15, double *kap15,
+                  double *cr) {
+    const int nt = P.n > P.ncf ? P.n : P.ncf;
+    if (nt > 0) k_b15_q<<<nblk(nt, 256), 256, 0, s>>>(P, c, q15, kap15, cr);
+}
+void launch_b15_rot(hipStream_t s, const DevProblem &P, const double *q15, const double *x,
+                    double *out) {
+    if (P.n > 0) k_b15_rot<<<nblk(P.n, 256), 256, 0, s>>>(P, q15, x, out);
+}
+void launch_b15_accl(hipStream_t s, const DevProblem &P, const double *Acc, const double *q15,
+                     const double *diag, double lam, double *AccL, double *diagL) {
+    const int nt = P.n > P.ncf ? P.n : P.ncf;
+    if (nt > 0) k_b15_accl<<<nblk(nt, 256), 256, 0, s>>>(P, Acc, q15, diag, lam, AccL, diagL);
+}
+void launch_b15_unrot(hipStream_t s, const DevProblem &P, const double *Acc, const double *g,
+                      const double *q15, double *adiag, double *u) {
+    if (P.n > 0) k_b15_unrot<<<nblk(P.n, 256), 256, 0, s>>>(P, Acc, g, q15, adiag, u);
+}
+void launch_b15_unrot_J(hipStream_t s, const DevProblem &P, double *J, const double *q15) {
+    if (P.M > 0) k_b15_unrot_J<<<nblk(P.M, 128), 128, 0, s>>>(P, J, q15);
+}
+void launch_b15_dnorm(hipStream_t s, int n, const double *x, const double *diag, double *out) {
+    k_b15_dnorm<<<1, 1024, 0, s>>>(n, x, diag, out);
 }
 void launch_b15_newton(hipStream_t s, int n, const double *v, const double *zu, const double *zc,
                        const double *kinv, double *out) {

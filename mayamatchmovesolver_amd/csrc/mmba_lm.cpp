@@ -275,7 +275,11 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         CB.brec = d_brecB;
         CB.ext_pert = d_ext_pertB;
         CB.step = d_stepB;
-        CB.b15 = b15 ? 1 : 0;
+        if (b15) {
+            launch_b15_q(s, P, d_c15, d_q15, d_kap15, d_c15r);
+            CB.q15 = d_q15;
+            CB.kap15 = d_kap15;
+        }
     }
     span_begin(SPAN_JAC);
     // uniform unsharded plans: the lmder bookkeeping rides in the
@@ -372,10 +376,14 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         span_end(SPAN_JAC);
     } else {
         const int do_xn = lm->first, do_gn = lm->fnorm_sq || lm->fnorm != 0.;
-        if (b15) launch_b15_s(s, lm->fnorm_sq, lm->fnorm, d_b15k + 4);
+        if (b15) {
+            launch_b15_s(s, lm->fnorm_sq, lm->fnorm, d_b15k + 4);
+            launch_b15_unrot(s, P, d_Acc, d_g, d_q15, d_adiag15, d_u15);
+        }
         launch_jac_epilogue(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g, d_diag, dx, lm->first,
                             lm->mode, lm->fnorm, lm->fnorm_sq, do_xn, do_gn, d_p_own, d_partial,
-                            nparts, pw, b15 ? d_c15 : nullptr, d_b15k + 4, d_g15);
+                            nparts, pw, b15 ? d_c15 : nullptr, d_b15k + 4, d_g15, d_adiag15,
+                            d_u15);
         span_end(SPAN_JAC);
         RedSpec rs{};
         rs.flag_slot = -1;
@@ -413,6 +421,7 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     if (!trial_folded)
         launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
                           opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
+    if (b15) launch_b15_rot(s, P, d_q15, d_wa1, d_p15);  // p in the rotated basis of J
     params_at = d_wa2;  // x <- wa2 on acceptance: the next Jacobian skips k_param_set
     records_enqueue(d_wa2, 0);  // ... and k_records
     span_begin(SPAN_RESID);
@@ -446,7 +455,7 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
         T.ticket = d_mticket;
     }
     launch_residual_jp(s, P, d_recs, d_ftrial, eu, ed, pr + 2 * (size_t)pw, d_J, d_jcol, d_nloc,
-                       d_wa1, pr + 3 * (size_t)pw, d_dist_t, T);
+                       b15 ? d_p15 : d_wa1, pr + 3 * (size_t)pw, d_dist_t, T);
     span_end(SPAN_RESID);
     LmDec D;
     if (dec) {
@@ -472,8 +481,8 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
                             sq ? h_seq : nullptr, seq_next, D);
         seq_pending = sq;
     }
-    if (b15)  // ||J p||^2 of J = J_s + f c^T (no host mirror on these plans)
-        launch_b15_jp(s, n, d_xs, d_g, d_c15, d_b15k + 4, d_scalar + SL_JP);
+    if (b15)  // ||J p||^2 of J = J_s + f c^T (no host mirror on these plans; rotated basis)
+        launch_b15_jp(s, n, d_xs15r, d_g, d_c15r, d_b15k + 4, d_scalar + SL_JP);
     mirror_pending = mirror;
     if (dec) {  // the next Jacobian's first launch, gated on the device's decision
         stage_slots();
@@ -491,18 +500,26 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         // same damped factorisation formed twice (the right-hand side rides
         // in every stage of the solve); the host loop never asks these plans
         // for a by-trial norm (Plan::solve)
+        // (rotated basis: the camera-frame blocks carry lam Q D^2 Q)
         b15_inner = true;
+        launch_b15_accl(s, P, d_Acc, d_q15, d_diag, lam, d_AccL, d_diagL);
+        std::swap(d_Acc, d_AccL);
+        std::swap(d_diag, d_diagL);
         solve_damped_enqueue(lam, -1, false, false);
         MMBA_HIP(hipMemcpyAsync(d_z15u, d_xs, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         MMBA_HIP(hipMemcpyAsync(d_b15k + 5, d_scalar + SL_FAIL, sizeof(double),
                                 hipMemcpyDeviceToDevice, s));
-        std::swap(d_g, d_c15);
+        std::swap(d_g, d_c15r);
         solve_damped_enqueue(lam, -1, false, false);
-        std::swap(d_g, d_c15);
+        std::swap(d_g, d_c15r);
+        std::swap(d_Acc, d_AccL);
+        std::swap(d_diag, d_diagL);
         MMBA_HIP(hipMemcpyAsync(d_z15c, d_xs, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         b15_inner = false;
-        launch_b15_combine(s, n, d_g, d_c15, d_z15u, d_z15c, d_b15k + 4, d_diag, d_xs, d_b15k,
-                           d_scalar, dnorm_slot, SL_FAIL, d_b15k + 5);
+        launch_b15_combine(s, n, d_g, d_c15r, d_z15u, d_z15c, d_b15k + 4, d_xs15r, d_b15k,
+                           d_scalar, SL_FAIL, d_b15k + 5);
+        launch_b15_rot(s, P, d_q15, d_xs15r, d_xs);
+        if (dnorm_slot >= 0) launch_b15_dnorm(s, n, d_xs, d_diag, d_scalar + dnorm_slot);
         (void)defer;
         (void)dnorm_by_trial;
         return;
@@ -679,6 +696,10 @@ bool Plan::solve_damped(double lam) {
 void Plan::newton_enqueue(double dxnorm) {
     const double t0 = wall_now();
     launch_newton_v(s, n, d_diag, d_xs, dxnorm, d_v);
+    if (b15) {  // v in the rotated basis of the factorisation
+        launch_b15_rot(s, P, d_q15, d_v, d_v15);
+        std::swap(d_v, d_v15);
+    }
     MMBA_HIP(hipMemsetAsync(d_scalar + SL_NEWT_B, 0, 2 * sizeof(double), s));
     if (nR > 0) launch_gather_R(s, P, d_v, d_wR, nRpad);
     if (nB_solved > 0) {
@@ -705,7 +726,10 @@ void Plan::newton_enqueue(double dxnorm) {
     }
     // B15: v^T (M + U B U^T)^-1 v = v^T M^-1 v - w^T K^-1 w (the factor and
     // z_u, z_c of the last damped solve)
-    if (b15) launch_b15_newton(s, n, d_v, d_z15u, d_z15c, d_b15k, d_scalar + SL_NEWT_B);
+    if (b15) {
+        launch_b15_newton(s, n, d_v, d_z15u, d_z15c, d_b15k, d_scalar + SL_NEWT_B);
+        std::swap(d_v, d_v15);  // back to the original basis buffer
+    }
     allreduce(d_scalar + SL_NEWT_B, 2);
     t_linear += wall_now() - t0;
 }
@@ -930,6 +954,7 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
         MMBA_HIP(hipMemcpyAsync(rp.data(), P.row_param, sizeof(int) * nrows,
                                 hipMemcpyDeviceToHost, s));
     }
+    if (b15) launch_b15_unrot_J(s, P, d_J, d_q15);  // back to the original basis
     MMBA_HIP(hipMemcpyAsync(J.data(), d_J, sizeof(double) * J.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(jc.data(), d_jcol, sizeof(int) * jc.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(nl.data(), d_nloc, sizeof(int) * M, hipMemcpyDeviceToHost, s));

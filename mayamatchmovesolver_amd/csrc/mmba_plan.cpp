@@ -607,7 +607,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             std::vector<std::vector<int>> anim_at(F);
             for (int p = 0; p < n; ++p)
                 if (pr->param_frame[p] >= 0) anim_at[pr->param_frame[p]].push_back(p);
+            // ... and every animated parameter a camera-frame block parameter
+            // (the rotated basis lives in those blocks)
             bool cover = true;
+            for (int p = 0; p < n; ++p)
+                if (pr->param_frame[p] >= 0 && p_class[p] != PC_CF) cover = false;
             std::vector<int> reach;
             for (int i = 0; i < M && cover; ++i) {
                 const auto &need = anim_at[d_frame[i]];
@@ -1204,9 +1208,19 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     if (b15) {
         d_c15 = dalloc<double>(n);
+        d_c15r = dalloc<double>(n);
         d_g15 = dalloc<double>(n);
         d_z15u = dalloc<double>(n);
         d_z15c = dalloc<double>(n);
+        d_q15 = dalloc<double>((size_t)ncf * PCMAX * PCMAX);
+        d_kap15 = dalloc<double>(ncf);
+        d_AccL = dalloc<double>((size_t)ncf * PCMAX * PCMAX);
+        d_diagL = dalloc<double>(n);
+        d_xs15r = dalloc<double>(n);
+        d_p15 = dalloc<double>(n);
+        d_v15 = dalloc<double>(n);
+        d_adiag15 = dalloc<double>(n);
+        d_u15 = dalloc<double>(n);
         d_b15k = dalloc<double>(8);
         MMBA_HIP(hipMemsetAsync(d_b15k, 0, sizeof(double) * 8, s));
     }

@@ -176,10 +176,21 @@ struct Plan {
     // term rides in the epilogue (column norms, J^T f), the damped solve
     // (Woodbury over two right-hand sides, u = J_s^T f and c, with one
     // factorisation each), lmpar's Newton term and ||J p||.
+    // The c f part of an animated block is one direction per camera-frame:
+    // the block's columns are stored in the Householder basis Q_cf with
+    // Q c_cf = kappa e_0, so the normal equations keep the accuracy of the
+    // differences (in the original basis the block's columns are nearly
+    // parallel and the squared condition loses ~5 digits); every
+    // parameter-space vector crosses Q at the solve's boundary.
     bool b15 = false, b15_inner = false;
-    double *d_c15 = nullptr;   // c (n)
-    double *d_g15 = nullptr;   // J^T f = u + s c (n): gnorm, lmpar's ||D^-1 g||
-    double *d_z15u = nullptr, *d_z15c = nullptr;  // M^-1 u, M^-1 c of the last damped solve
+    double *d_c15 = nullptr;   // c (n, original basis)
+    double *d_c15r = nullptr;  // c in the rotated basis
+    double *d_g15 = nullptr;   // J^T f = u + s c (n, original): gnorm, lmpar's ||D^-1 g||
+    double *d_q15 = nullptr, *d_kap15 = nullptr;  // Q_cf (ncf x PCMAX^2), kappa_cf
+    double *d_AccL = nullptr, *d_diagL = nullptr;  // damped rotated blocks, diag off them
+    double *d_z15u = nullptr, *d_z15c = nullptr;  // M^-1 u, M^-1 c (rotated) of the last solve
+    double *d_xs15r = nullptr, *d_p15 = nullptr, *d_v15 = nullptr;  // xs, p, v rotated
+    double *d_adiag15 = nullptr, *d_u15 = nullptr;  // A_pp, u in the original basis
     double *d_b15k = nullptr;  // [K^-1 (4), s, fail of the first solve]
     // rolling shutter (mmba.h ABI 3, mmba_rs.hip)
     bool rs_on = false;
