@@ -95,6 +95,26 @@ __device__ __forceinline__ int potrf_inv(double (&a)[NB], double (&x)[NB]) {
     return badl;
 }
 
+// Corner factor of the arrow, one wave: Ld (lower) and Ld^-1 of the packed
+// lower nc x nc matrix sZ (na rows used, identity padding), NC a power of 2.
+template <int NC>
+__device__ __forceinline__ int band_corner(const double *sZ, int na, double *Gd, double *Gdinv) {
+    const int tid = threadIdx.x, r = tid & (NC - 1);
+    double a[NC], x[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) a[c] = (c <= r && r < na) ? sZ[r * (r + 1) / 2 + c] : 0.;
+    if (r >= na) a[r] = 1.;
+    const int badl = potrf_inv<NC>(a, x);
+    if (tid < NC) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            Gd[r * NGMAX + c] = (c <= r) ? a[c] : 0.;
+            Gdinv[c * NGMAX + r] = x[c];
+        }
+    }
+    return badl;
+}
+
 // ---------------------------------------------------------------------------
 // Stage-1 / corner factorisation, one workgroup per partition.  CORNER: the
 // arrow rows are the nG global rows, Z starts from Gd and is factored at the
@@ -263,21 +283,10 @@ __global__ void __launch_bounds__(256)
         store_rows(jl, r1, tid, blockDim.x);
     }
     if (CORNER) {
-        // Ld Ld^T = D - Y Y^T (accumulated in sZ), na = nG <= 16
+        // Ld Ld^T = D - Y Y^T (accumulated in sZ), na = nG <= NGMAX
         if (na > 0 && tid < 64) {
-            const int r = tid & 15;
-            double a[16], x[16];
-#pragma unroll
-            for (int c = 0; c < 16; ++c) a[c] = (c <= r && r < na) ? sZ[r * (r + 1) / 2 + c] : 0.;
-            if (r >= na) a[r] = 1.;
-            const int badl = potrf_inv<16>(a, x);
-            if (tid < 16) {
-#pragma unroll
-                for (int c = 0; c < 16; ++c) {
-                    Gd[r * NGMAX + c] = (c <= r) ? a[c] : 0.;
-                    Gdinv[c * NGMAX + r] = x[c];
-                }
-            }
+            const int badl = na <= 16 ? band_corner<16>(sZ, na, Gd, Gdinv)
+                                      : band_corner<NGMAX>(sZ, na, Gd, Gdinv);
             if (tid == 0 && badl) bad = 1;
         }
     } else {

@@ -435,14 +435,16 @@ __device__ __forceinline__ void bcr_band_dl(const BcrDev &B, int b, int q, doubl
 // odd neighbours.  band: level 0 of the dataflow factor, operands staged
 // straight from the band layout and the right-hand side rsrc (no load pass).
 // ---------------------------------------------------------------------------
-template <int K, int CH, bool MF>  // CH: pivot chain variant (BcrDev::regchol); MF: MFMA updates
+// GX: arrow capacity (NGLANE: the arrow rides in spare lanes of the augmented
+// pivot chains; NGMAX: wider arrows, the separate triangular solves)
+template <int K, int CH, bool MF, int GX = NGLANE>  // CH: pivot chain variant (BcrDev::regchol); MF: MFMA updates
 __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact, int ping,
                                                const int t, int *fail, long long *probe,
                                                double *y, bool band, const double *rsrc,
                                                int *pub = nullptr, unsigned pub_epoch = 0) {
     constexpr int KS = K + 2;     // even row stride: 16-B aligned rows
     constexpr int CG = K / 4;     // columns per update task
-    constexpr int GS = NGMAX;     // row stride of the K x nG arrays
+    constexpr int GS = GX;        // row stride of the K x nG arrays
     __shared__ double sD[2][K * KS];   // D_o1, D_o2 -> C_o1, C_o2
     // right-hand sides, solved in place: Lo1 -> U1, Le^T -> V1, Lo2 -> U2, Ln^T -> V2
     __shared__ double sB[4][K * KS];
@@ -450,7 +452,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     __shared__ double sR[3][K];        // r_o1 -> y1, r_o2 -> y2, r_e (fused forward solve)
     __shared__ double sRs[2][K];       // 1 / C_jj
     __shared__ double col[4][64 * (MMBA_BCR_PW > 8 ? MMBA_BCR_PW : 8)];  // pivot column (LDS chain) / panel image (blocked chain)
-    __shared__ double sDe[K * KS], sGe[NGMAX * K];
+    __shared__ double sDe[K * KS], sGe[GX * K];
     __shared__ double sZero[2];
     __shared__ int bad_s;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -540,7 +542,7 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
     __syncthreads();
     stamp(0);
     int bad = 0;
-    if constexpr (2 * K + NGMAX <= 64) {
+    if constexpr (2 * K + GX <= 64) {
         // A+B. Cholesky of the two odd neighbours with their triangular
         // solves fused into the pivot chain (bcr_chol_aug_wave): wave w
         // factors neighbour w & 1; waves 0/1 carry U (and y) in lanes K..,
@@ -747,10 +749,11 @@ __device__ __forceinline__ void bcr_level_item(const BcrDev &B, int s, int nact,
 }
 
 // One elimination level.  blockIdx.x = even index / 2 (t = 2 blockIdx.x).
-template <int K, int CH, bool MF>
+template <int K, int CH, bool MF, int GX = NGLANE>
 __global__ void __launch_bounds__(256) k_bcr_level(BcrDev B, int s, int nact, int ping,
                                                    int *fail, long long *probe, double *y) {
-    bcr_level_item<K, CH, MF>(B, s, nact, ping, 2 * blockIdx.x, fail, probe, y, false, nullptr);
+    bcr_level_item<K, CH, MF, GX>(B, s, nact, ping, 2 * blockIdx.x, fail, probe, y, false,
+                                  nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1318,7 +1321,8 @@ static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long lon
                          const double *r, double *y) {
     const BcrDev &D = B.bcr;
     double *yy = r ? y : nullptr;
-    if (D.fflags && D.tick && !B.df_off && D.nblk >= 2 && D.regchol == 2 && D.mfma_upd) {
+    const bool wide = D.nG > NGLANE;  // arrows wider than NGLANE: per-level launches
+    if (D.fflags && D.tick && !B.df_off && D.nblk >= 2 && D.regchol == 2 && D.mfma_upd && !wide) {
         const unsigned ep = bcr_next_epoch();
         // level items (the root is item `items`); G workgroups need not all
         // be resident (tickets), so the grid is the level-0 width (<= 256)
@@ -1341,7 +1345,9 @@ static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long lon
     int ping = 0;
     for (int st = 1, nact = D.nblk; nact > 1; st *= 2, nact = (nact + 1) / 2) {
         const int g = (nact + 1) / 2;
-        if (D.regchol == 2) {
+        if (wide) {
+            k_bcr_level<K, 2, true, NGMAX><<<g, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
+        } else if (D.regchol == 2) {
             if (D.mfma_upd)
                 k_bcr_level<K, 2, true><<<g, 256, 0, s>>>(D, st, nact, ping, fail, probe, yy);
             else
@@ -1360,7 +1366,9 @@ static void bcr_factor_k(hipStream_t s, const BandSolver &B, int *fail, long lon
         case 24: k_bcr_root<24><<<1, 64, 0, s>>>(D, fail, yy); break;
         case 32: k_bcr_root<32><<<1, 64, 0, s>>>(D, fail, yy); break;
         case 40: k_bcr_root<40><<<1, 64, 0, s>>>(D, fail, yy); break;
-        default: k_bcr_root<48><<<1, 64, 0, s>>>(D, fail, yy); break;
+        case 48: k_bcr_root<48><<<1, 64, 0, s>>>(D, fail, yy); break;
+        case 56: k_bcr_root<56><<<1, 64, 0, s>>>(D, fail, yy); break;
+        default: k_bcr_root<64><<<1, 64, 0, s>>>(D, fail, yy); break;
     }
 }
 

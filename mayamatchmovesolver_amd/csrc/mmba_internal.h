@@ -25,9 +25,10 @@ namespace mmba {
 
 constexpr int PCMAX = 10;   // params per camera-frame block
 constexpr int PBMAX = 3;    // params per bundle block
-constexpr int NGMAX = 16;   // global parameters
-constexpr int LMAX = 20;
-constexpr int CF_AIDX = 16;  // camera-frame attribute table: 7 camera + 9 TRS    // local Jacobian columns per observation
+constexpr int NGMAX = 32;   // global parameters (the arrow of the reduced system)
+constexpr int NGLANE = 16;  // arrows up to this width ride in spare lanes of the BCR pivot chains
+constexpr int LMAX = 32;    // local Jacobian columns per observation
+constexpr int CF_AIDX = 16;  // camera-frame attribute table: 7 camera + 9 TRS
 constexpr int TILE = 64;    // reduced-system tile edge
 constexpr int CAMREC = 20;  // doubles per camera-frame record
 constexpr int BREC = 16;    // doubles per bundle record (128 B: one L2 line)

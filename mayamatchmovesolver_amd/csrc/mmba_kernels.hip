@@ -1479,8 +1479,9 @@ __global__ void k_ne_bnd(DevProblem P, const double *__restrict__ J,
 
 // Globals: partial sums of Agg (nG x nG) and gG per block of observations.
 // NG: compile-time bound on the number of global parameters (2, 4, 8 or
-// NGMAX): the per-thread accumulators are NG^2 + NG registers (a 272-double
-// NGMAX array spilled 2 KB per lane to scratch).  Partial rows keep the
+// 16): the per-thread accumulators are NG^2 + NG registers (the 272-double
+// array of NG = 16 spills 2 KB per lane to scratch; wider arrows take
+// k_ne_glob_wide).  Partial rows keep the
 // NGMAX layout.
 template <int NG>
 __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__restrict__ J,
@@ -1544,6 +1545,77 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
             const int e = mat ? a * NG + b : NG * NG + a;
             v = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
         }
+        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = v;
+    }
+}
+
+// Globals wider than 16 (NG^2 + NG accumulators no longer fit a thread's
+// registers): the block stages the dense global Jacobian rows and residuals
+// of 64 observations at a time in LDS, and thread t owns entries t, t + 256,
+// ... of [Agg | gG], summed over the observations in order (deterministic,
+// no atomics).  Same partial-row layout as k_ne_glob.
+__global__ void __launch_bounds__(256) k_ne_glob_wide(DevProblem P, const double *__restrict__ J,
+                                                      const int *__restrict__ jcol,
+                                                      const int *__restrict__ nloc,
+                                                      const double *__restrict__ f,
+                                                      double *partial, int chunk) {
+    constexpr int OB = 64;  // observations per LDS round
+    constexpr int EPT = (NGMAX * NGMAX + NGMAX + 255) / 256;
+    __shared__ double sg[OB][2 * NGMAX + 2];  // gx[NGMAX] | gy[NGMAX] | fx, fy
+    const int nG = P.nG, nCF = P.nR - nG, M = P.M;
+    const int NA = nG * nG + nG;
+    const int i0 = blockIdx.x * chunk, i1 = min(M, i0 + chunk);
+    double acc[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) acc[k] = 0.;
+    for (int b0 = i0; b0 < i1; b0 += OB) {
+        __syncthreads();  // the previous round's reads are done
+        for (int t = threadIdx.x; t < OB * (2 * NGMAX + 2); t += blockDim.x) (&sg[0][0])[t] = 0.;
+        __syncthreads();
+        if (threadIdx.x < OB) {
+            const int o = threadIdx.x, i = b0 + o;
+            if (i < i1 && own_obs(P, i)) {
+                const int nl = nloc[i];
+                for (int l = 0; l < nl; ++l) {
+                    const int p = jcol[(size_t)l * M + i];
+                    if (P.p_class[p] != PC_G) continue;
+                    const int gi = P.p_pos[p] - nCF;
+                    sg[o][gi] = J[(size_t)(2 * l) * M + i];
+                    sg[o][NGMAX + gi] = J[(size_t)(2 * l + 1) * M + i];
+                }
+                sg[o][2 * NGMAX] = f[2 * i];
+                sg[o][2 * NGMAX + 1] = f[2 * i + 1];
+            }
+        }
+        __syncthreads();
+        const int no = min(OB, i1 - b0);
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int e = threadIdx.x + 256 * k;
+            if (e >= NA) continue;
+            const bool mat = e < nG * nG;
+            const int a = mat ? e / nG : e - nG * nG;
+            const int bx = mat ? e % nG : 2 * NGMAX, by = mat ? NGMAX + bx : 2 * NGMAX + 1;
+            double v = acc[k];
+            for (int o = 0; o < no; ++o)
+                v += sg[o][a] * sg[o][bx] + sg[o][NGMAX + a] * sg[o][by];
+            acc[k] = v;
+        }
+    }
+    // compact [Agg | gG] through LDS, then the NGMAX-layout row (zeros beyond nG)
+    double *cmp = &sg[0][0];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const int e = threadIdx.x + 256 * k;
+        if (e < NA) cmp[e] = acc[k];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
+        const bool mat = t < NGMAX * NGMAX;
+        const int a = mat ? t / NGMAX : t - NGMAX * NGMAX, c = mat ? t % NGMAX : 0;
+        double v = 0.;
+        if (a < nG && c < nG) v = cmp[mat ? a * nG + c : nG * nG + a];
         partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = v;
     }
 }
@@ -3556,8 +3628,10 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
             k_ne_glob<4><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
         else if (P.nG <= 8)
             k_ne_glob<8><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+        else if (P.nG <= 16)
+            k_ne_glob<16><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
         else
-            k_ne_glob<NGMAX><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
+            k_ne_glob_wide<<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
         k_ne_glob_reduce<<<1, 256, 0, s>>>(P, glob_partial, nb, Agg, gG);
     }
 }

@@ -346,7 +346,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     for (int p = 0; p < n; ++p)
         if (p_class[p] == PC_G) g_param.push_back(p);
     nG = (int)g_param.size();
-    if (nG > NGMAX) throw Unsupported{"more than 16 global parameters"};
+    if (nG > NGMAX) throw Unsupported{"more than 32 global parameters"};
     for (int q = 0; q < nG; ++q) p_pos[g_param[q]] = nCF + q;
     nR = nCF + nG;
 
@@ -572,7 +572,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         return nl;
     };
     for (int i = 0; i < M; ++i)
-        if (obs_cols(i) > LMAX) throw Unsupported{"more than 20 parameters reach one observation"};
+        if (obs_cols(i) > LMAX) throw Unsupported{"more than 32 parameters reach one observation"};
     // Central differences and the robust loss where an lmder FD column skips
     // marker rows (another frame than an animated parameter's): the
     // reference zero-initialises errorListB (adjust_solveFunc.cpp:412), so a

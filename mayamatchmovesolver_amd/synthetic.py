@@ -884,6 +884,105 @@ def rig_scene(n_cams=2, bundles=10, solve_cam1=True, stiffness=False, seed=11) -
     return b.build(meta={"name": "rig"})
 
 
+def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal=3,
+                  extra_globals=0, window=None, lens=None, seed=17) -> Problem:
+    """Witness-camera rig with a wide arrow of global parameters: a fixed
+    static reference camera 0, ``n_witness`` static witness cameras whose
+    poses are solved as static (global) parameters (witness 1: rotation
+    only -- its fixed translation sets the scale; the others: translate and
+    rotate), static focal lengths solved on the first ``n_focal`` witnesses,
+    one animated camera whose pose is solved per frame (camera-frame blocks),
+    and ``bundles`` bundles (translate solved with ``solve_bundles``).
+    n_witness = 4, n_focal = 3 gives 24 globals; 5 / 5 gives 32, the
+    library's arrow capacity.  ``extra_globals`` adds solved static film back
+    widths on the witnesses (to step past it).  ``window``: the animated
+    camera sees bundle j only on ``window`` consecutive frames (a banded
+    reduced system instead of a dense one).  ``lens="anamorphic"``: every
+    camera shares one 3DE anamorphic deg 4 lens whose ten polynomial
+    coefficients are solved (created and solved first: B3), so a witness
+    observation reaches more than 20 parameters.  Markers camera-major (B4)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    F = int(frames)
+    b = SceneBuilder(F)
+    lens_idx, lens_solve = -1, []
+    if lens == "anamorphic":
+        lens_idx, lids = b.lens_3de_anamorphic_std_deg4()
+        lens_solve = list(lids[:10])
+    elif lens is not None:
+        raise ValueError(lens)
+    B = bundles
+    depth = rng.uniform(12.0, 30.0, size=B)
+    P = np.stack([rng.uniform(-0.3, 0.3, B) * depth, rng.uniform(-0.2, 0.2, B) * depth,
+                  -depth], axis=1)
+    views = []  # (cam index, per-frame t (F,3), per-frame r (F,3), focal)
+    solve_ids = []
+    gl_cams = []
+    for c in range(n_witness + 1):
+        # on an arc around the bundle cloud, each aimed at its centre
+        X = 5.0 * (c - n_witness / 2.0)
+        t = np.array([X, 0.4 * c, 0.5 * (c % 2)])
+        r = np.array([0.5 * c, np.degrees(np.arctan2(X, 20.0)), 0.3 * c])
+        foc = FOCAL_MM * (1.0 + 0.05 * c)
+        solved = c >= 1
+        t0 = t + (rng.uniform(-0.05, 0.05, 3) if c >= 2 else 0.0)
+        r0 = r + (rng.uniform(-1.0, 1.0, 3) if solved else 0.0)
+        f0 = foc * (1.0 + (rng.uniform(-0.03, 0.03) if 1 <= c <= n_focal else 0.0))
+        tfm, tids = b.transform(t=tuple(t0), r=tuple(r0))
+        cam, cids = b.camera(tfm, focal=f0, film_back=(FILM_W_IN, FILM_H_IN),
+                             render_size=RENDER, lens=lens_idx)
+        views.append((cam, np.tile(t, (F, 1)), np.tile(r, (F, 1)), foc))
+        if c == 1:
+            solve_ids += tids[3:6]
+        elif c >= 2:
+            solve_ids += tids[0:6]
+        if 1 <= c <= n_focal:
+            solve_ids.append(cids[abi.CAM_FOCAL_MM])
+        if c >= 1:
+            gl_cams.append(cids)
+    for k in range(int(extra_globals)):
+        solve_ids.append(gl_cams[k % len(gl_cams)][abi.CAM_FILM_BACK_W_INCH])
+    # the animated camera: pose solved per frame
+    fr = np.arange(F, dtype=np.float64)
+    ta = np.stack([0.7 + 0.25 * fr, 0.1 + 0.02 * fr, 0.5 - 0.05 * fr], axis=1)
+    ra = np.stack([0.4 + 0.3 * np.sin(fr), -1.0 + 0.5 * fr, 0.2 * np.cos(fr)], axis=1)
+    ta0 = ta + rng.uniform(-0.05, 0.05, size=ta.shape)
+    ra0 = ra + rng.uniform(-1.0, 1.0, size=ra.shape)
+    tfm, aids = b.transform(t=tuple(ta0[:, k] for k in range(3)),
+                            r=tuple(ra0[:, k] for k in range(3)))
+    cam, _ = b.camera(tfm, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
+                      render_size=RENDER, lens=lens_idx)
+    views.append((cam, ta, ra, FOCAL_MM))
+    P0 = P * (1.0 + rng.uniform(-0.04, 0.04, size=(B, 1))) if solve_bundles else P
+    bids = []
+    for j in range(B):
+        bt, ids = b.transform(t=tuple(P0[j]))
+        b.bundle(bt)
+        bids.append(ids)
+    for cam, tt, rr, foc in views:
+        xy = np.zeros((B, F, 2))
+        for f in range(F):
+            R = _euler_xyz(*rr[f])
+            pc = (P - tt[f]) @ R
+            xy[:, f, 0] = foc * pc[:, 0] / (FILM_W_MM * -pc[:, 2])
+            xy[:, f, 1] = foc * pc[:, 1] / (FILM_H_MM * -pc[:, 2])
+        animated = cam == views[-1][0]
+        for j in range(B):
+            en = None
+            if animated and window is not None:
+                s0 = (j * max(F - window, 0)) // max(B - 1, 1)
+                en = (fr >= s0) & (fr < s0 + window)
+            b.marker(cam, j, _noisy(rng, xy[j]), enable=en)
+    for a in lens_solve + solve_ids:
+        b.solve(a)
+    for a in aids[0:6]:
+        b.solve(a)
+    if solve_bundles:
+        for j in range(B):
+            for a in bids[j][:3]:
+                b.solve(a)
+    return b.build(meta={"name": "witness"})
+
+
 def config_options(prob: Problem, scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH,
                    **overrides):
     """Solver options for a synthetic config (lmder, forward FD,

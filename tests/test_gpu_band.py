@@ -42,6 +42,10 @@ CASES = [
     (1000, 32, 16, -1), (10, 2, 16, -1), (0, 0, 4, -1), (90, 5, 0, -1),
     (7, 3, 0, -1), (777, 31, 1, -1), (1000, 16, 3, -1), (17, 8, 2, -1),
     (2880, 11, 2, -1), (840, 6, 0, -1), (4096, 24, 0, -1), (24 * 65, 24, 1, -1),
+    # arrows wider than 16 (up to NGMAX = 32): band, partitioned, BCR K = 8..32
+    (1000, 23, 24, 1), (1000, 40, 32, 4), (640, 60, 32, 1), (10, 2, 32, 1), (0, 0, 32, 1),
+    (1000, 23, 24, -1), (1000, 32, 32, -1), (300, 6, 32, -1), (500, 16, 17, -1),
+    (24 * 65, 24, 24, -1), (0, 0, 24, -1),
 ]
 
 

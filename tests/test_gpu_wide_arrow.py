@@ -1,0 +1,106 @@
+"""Global parameters beyond 16 (VERDICT r2 "missing" 5, "next" 8): the
+reference has no limit on the global (static, shared) parameters
+(adjust_relationships.cpp:223-337); the library's reduced system carries
+them as an arrow of up to NGMAX = 32 rows (csrc/mmba_internal.h).  Scenes:
+static witness cameras whose poses and focal lengths are solved as static
+parameters beside an animated camera solved per frame (synthetic
+witness_scene), on each reduced-system path: the band + arrow Cholesky
+(every frame coupled), block cyclic reduction (bundles on 3-frame windows),
+the block-diagonal + arrow solve (no solved bundle), and frame shards.  Each
+case: the library through the C ABI against the CPU oracle on the same
+inputs, 1e-6 on x and on every ||f|| of the trace, identical counts."""
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import abi, make_options, synthetic as S
+from mayamatchmovesolver_amd._lib import MmbaError
+from mayamatchmovesolver_amd.solver import Solver
+
+from test_gpu_edge import check, check_measure_jacobian
+from test_gpu_sharded import check_shards_agree, run_sharded
+
+pytestmark = pytest.mark.gpu
+
+DAG, MMSG = abi.SCENE_GRAPH_MODE_MAYA_DAG, abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH
+BAND, BDIAG = 0, 3
+
+
+def reduced_kind(prob, opt, ctx):
+    s = Solver(prob, opt, context=ctx)
+    try:
+        return s.kernel_stats()["reduced_kind"]
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+@pytest.mark.parametrize("kw,ng", [(dict(), 24), (dict(n_witness=5, n_focal=5), 32)])
+def test_wide_arrow_band(kw, ng, mode, oracle, gpu_ctx):
+    """Every frame coupled through the bundles: band + arrow Cholesky."""
+    prob = S.witness_scene(**kw)
+    opt = make_options(scene_graph_mode=mode)
+    assert reduced_kind(prob, opt, gpu_ctx) == BAND
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("kw", [dict(frames=10, window=3, bundles=30),
+                                dict(frames=10, window=3, bundles=30, n_witness=5, n_focal=5)])
+def test_wide_arrow_bcr(kw, oracle, gpu_ctx):
+    """Bundles on 3-frame windows of the animated camera: a banded reduced
+    system, factored by block cyclic reduction with the wide arrow."""
+    prob = S.witness_scene(**kw)
+    opt = make_options()
+    assert reduced_kind(prob, opt, gpu_ctx) == BAND
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+@pytest.mark.parametrize("kw", [dict(solve_bundles=False),
+                                dict(solve_bundles=False, n_witness=5, n_focal=5)])
+def test_wide_arrow_block_diagonal(kw, mode, oracle, gpu_ctx):
+    """No solved bundle: block-diagonal camera-frame blocks + the arrow."""
+    prob = S.witness_scene(**kw)
+    opt = make_options(scene_graph_mode=mode)
+    assert reduced_kind(prob, opt, gpu_ctx) == BDIAG
+    check(prob, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("kw,n", [(dict(n_witness=5, n_focal=5), 2),
+                                  (dict(frames=10, window=3, bundles=30), 3)])
+def test_wide_arrow_sharded(kw, n, oracle):
+    """Frame shards (in-process communicators): the global rows are
+    all-reduced like the narrow arrow's."""
+    prob = S.witness_scene(**kw)
+    opt = make_options()
+    outs = run_sharded(prob, opt, n)
+    check_shards_agree(outs)
+    xr, _f, _eu, _ed, rr, trr = oracle.solve(prob, opt)
+    o = outs[0]
+    assert o.result["iterations"] == rr.iterations
+    np.testing.assert_allclose(o.fnorm_trace, trr, rtol=1e-6, atol=1e-9 * trr[0])
+    xs = np.maximum(np.abs(xr), 1e-3)
+    assert np.max(np.abs(o.x - xr) / xs) <= 1e-6
+
+
+def test_arrow_capacity_refused(gpu_ctx):
+    """33 globals: refused as UNSUPPORTED (the caller keeps cminpack)."""
+    prob = S.witness_scene(n_witness=5, n_focal=5, extra_globals=1)
+    with pytest.raises(MmbaError) as ei:
+        Solver(prob, make_options(), context=gpu_ctx)
+    assert ei.value.code == abi.MMBA_ERR_UNSUPPORTED
+    assert "32 global" in str(ei.value)
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+def test_more_than_20_columns_per_observation(mode, oracle, gpu_ctx):
+    """A shared anamorphic lens with its ten coefficients solved beside the
+    witness poses, focal lengths and film back widths: a witness observation
+    reaches 21 parameters (the library's bound is LMAX = 32).  The lens
+    coefficients are weakly determined by these markers (the oracle's own
+    final x moves by 5e-5 under a 1-ulp change of x0), so the bar is the
+    dense Jacobian and one LM step (1-ulp envelope 6e-9) at 1e-6."""
+    prob = S.witness_scene(n_witness=2, n_focal=2, extra_globals=2, lens="anamorphic")
+    opt = make_options(scene_graph_mode=mode, iterations=2)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)
