@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 4
+#define MMBA_ABI_VERSION 5
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -220,6 +220,24 @@ typedef struct mmba_problem {
      * camera transforms without a parent, without solved bundles, unsharded
      * (MMBA_ERR_UNSUPPORTED otherwise). */
     const double *cam_rs_value;   /* [num_cameras] */
+
+    /* ---- ABI 5 ---- */
+    /* Layered lens nodes.  lens_input[l] = the lens chained as the input of
+     * lens l (-1 = none).  What the reference solver evaluates for a camera
+     * whose lens node has upstream nodes: the per-frame models are clones of
+     * the camera-connected node's plug model (maya_lens_model_utils.cpp:
+     * 655-662), whose input chain the node's compute set from the upstream
+     * nodes' values at the time the plug was read (MMLensModel3deNode.cpp:
+     * 164); connectLensModels never re-points it (its loop, :715, does not
+     * run), so the input layers are constants of the solve and their
+     * attributes, if solved, have zero Jacobian columns.  Distortion applies
+     * the deepest input first, the camera's own lens last
+     * (lens_model_3de_classic.cpp:82-88).  lens_input_values[14*l + k] =
+     * slot k of layer l as read with the plug (absent slots: the model's
+     * default); NULL = each slot's attribute value at frame 0.  At most 4
+     * input layers per lens; lens_input NULL = no layers (ABI <= 4). */
+    const int32_t *lens_input;        /* [num_lenses] */
+    const double *lens_input_values;  /* [14*num_lenses] */
 } mmba_problem;
 
 /* SolverOptions subset that the LM path reads (adjust_data.h:133-185). */

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -106,6 +106,9 @@ class MmbaProblem(C.Structure):
         ("smooth_value", _f64p),
         # ---- ABI 3 ----
         ("cam_rs_value", _f64p),
+        # ---- ABI 5 ----
+        ("lens_input", _i32p),
+        ("lens_input_values", _f64p),
     ]
 
 

@@ -19,9 +19,10 @@
 // GEMMs and trailing updates that produce L also produce row n of the
 // factor of [S r; r^T .], which is y = L^-1 r -- the forward solve costs
 // nothing extra.  The backward solve x = L^-T y (and a stand-alone forward
-// solve for lmpar's Newton term) walk the 64-row blocks with two GEMVs per
-// block (the diagonal block through the stored Linv_kk, then the update of
-// the rest), rocblas_dgemv.  The flops are those of a dense Cholesky, n^3/3,
+// solve for lmpar's Newton term) walk the 64-row blocks with one launch per
+// block (k_dense_fwd_step / k_dense_bwd_step: the diagonal block through the
+// stored Linv_kk, computed by every workgroup, then the workgroup's slice of
+// the update of the rest).  The flops are those of a dense Cholesky, n^3/3,
 // in fp64 MFMA GEMMs; the panel factorisation is the latency-bound part.
 #include <rocblas/rocblas.h>
 
@@ -123,6 +124,69 @@ __global__ void k_dense_row_put(double *A, int ld, int n, const double *r) {
 __global__ void k_dense_row_get(const double *A, int ld, int n, double *y) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j < n) y[j] = A[(size_t)j * ld + n];
+}
+
+// Forward step of block k (rows k..k+63): y_k = Linv_kk t_k (every workgroup
+// forms it in LDS, workgroup 0 stores it), then t_i -= L_i,k y_k for the
+// rows i >= k + 64, one row per thread (grid-stride, coalesced column reads).
+// t_k is only read here and the rows below only written: no race.
+__global__ void __launch_bounds__(256) k_dense_fwd_step(const double *__restrict__ A, int ld,
+                                                        int n, int k,
+                                                        const double *__restrict__ Li,
+                                                        double *t, double *y) {
+    __shared__ double st[64], sy[64];
+    const int tid = threadIdx.x;
+    if (tid < 64) st[tid] = t[k + tid];
+    __syncthreads();
+    if (tid < 64) {
+        double s = 0.;
+        for (int c = 0; c <= tid; ++c) s = fma(Li[(size_t)c * 64 + tid], st[c], s);
+        sy[tid] = s;
+        if (blockIdx.x == 0) y[k + tid] = s;
+    }
+    __syncthreads();
+    for (int i = k + 64 + blockIdx.x * blockDim.x + tid; i < n; i += gridDim.x * blockDim.x) {
+        const double *col = A + (size_t)k * ld + i;
+        double s0 = 0., s1 = 0.;
+#pragma unroll 8
+        for (int c = 0; c < 64; c += 2) {
+            s0 = fma(col[(size_t)c * ld], sy[c], s0);
+            s1 = fma(col[(size_t)(c + 1) * ld], sy[c + 1], s1);
+        }
+        t[i] -= s0 + s1;
+    }
+}
+
+// Backward step of block k: x_k = Linv_kk^T t_k (every workgroup; workgroup 0
+// stores it), then t_j -= L_k,j^T x_k for the columns j < k, one column per
+// thread (the 64 rows of column j are contiguous: double2 loads; ld and k are
+// even).
+__global__ void __launch_bounds__(256) k_dense_bwd_step(const double *__restrict__ A, int ld,
+                                                        int k, const double *__restrict__ Li,
+                                                        double *t, double *x) {
+    __shared__ double st[64], sx[64];
+    const int tid = threadIdx.x;
+    if (tid < 64) st[tid] = t[k + tid];
+    __syncthreads();
+    if (tid < 64) {
+        const double *lc = Li + (size_t)tid * 64;  // column tid of Linv (lower)
+        double s = 0.;
+        for (int i = tid; i < 64; ++i) s = fma(lc[i], st[i], s);
+        sx[tid] = s;
+        if (blockIdx.x == 0) x[k + tid] = s;
+    }
+    __syncthreads();
+    for (int j = blockIdx.x * blockDim.x + tid; j < k; j += gridDim.x * blockDim.x) {
+        const double2 *col = (const double2 *)(A + (size_t)j * ld + k);
+        double s0 = 0., s1 = 0.;
+#pragma unroll 8
+        for (int c = 0; c < 32; ++c) {
+            const double2 v = col[c];
+            s0 = fma(v.x, sx[2 * c], s0);
+            s1 = fma(v.y, sx[2 * c + 1], s1);
+        }
+        t[j] -= s0 + s1;
+    }
 }
 
 #define MMBA_RB(call)                                                                    \
@@ -233,38 +297,23 @@ void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int 
 
 // y = L^-1 r: per 64-row block, y_k = Linv_kk t_k, then t_(k+1..) -= L_(k+1..),k y_k.
 void DenseSolver::forward(hipStream_t s, const double *r, double *y) {
-    init(s);
-    rocblas_handle h = (rocblas_handle)handle;
-    const double one = 1.0, mone = -1.0, zero = 0.0;
     double *t = ws;
     MMBA_HIP(hipMemcpyAsync(t, r, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
     for (int k = 0; k < n; k += 64) {
-        const double *Li = Linv + (size_t)(k / 64) * 64 * 64;
-        MMBA_RB(rocblas_dgemv(h, rocblas_operation_none, 64, 64, &one, Li, 64, t + k, 1, &zero,
-                              y + k, 1));
         const int m = n - (k + 64);
-        if (m > 0)
-            MMBA_RB(rocblas_dgemv(h, rocblas_operation_none, m, 64, &mone,
-                                  A + (size_t)k * ld + k + 64, ld, y + k, 1, &one, t + k + 64,
-                                  1));
+        const int g = std::max(1, std::min((m + 255) / 256, 1024));
+        k_dense_fwd_step<<<g, 256, 0, s>>>(A, ld, n, k, Linv + (size_t)(k / 64) * 64 * 64, t, y);
     }
 }
 
 // x = L^-T y: per 64-row block from the last, x_k = Linv_kk^T t_k, then
 // t_(0..k) -= L_k,(0..k)^T x_k.
 void DenseSolver::backward(hipStream_t s, const double *y, double *x) {
-    init(s);
-    rocblas_handle h = (rocblas_handle)handle;
-    const double one = 1.0, mone = -1.0, zero = 0.0;
     double *t = ws;
     MMBA_HIP(hipMemcpyAsync(t, y, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
     for (int k = n - 64; k >= 0; k -= 64) {
-        const double *Li = Linv + (size_t)(k / 64) * 64 * 64;
-        MMBA_RB(rocblas_dgemv(h, rocblas_operation_transpose, 64, 64, &one, Li, 64, t + k, 1,
-                              &zero, x + k, 1));
-        if (k > 0)
-            MMBA_RB(rocblas_dgemv(h, rocblas_operation_transpose, 64, k, &mone, A + k, ld,
-                                  x + k, 1, &one, t, 1));
+        const int g = std::max(1, std::min((k + 255) / 256, 1024));
+        k_dense_bwd_step<<<g, 256, 0, s>>>(A, ld, k, Linv + (size_t)(k / 64) * 64 * 64, t, x);
     }
 }
 

@@ -701,12 +701,19 @@ MMBA_DEV void project_point(const double *rec, const double *bp, double &point_x
 }
 
 // Lens distortion of a reprojected point; a non-finite result keeps the
-// undistorted coordinate (adjust_measureErrors.cpp:466-472).
+// undistorted coordinate (adjust_measureErrors.cpp:466-472).  chain: the
+// lens's constant input layers, deepest first (mmba.h ABI 5), applied before
+// the lens itself with no check between layers (each model's
+// applyModelDistort runs its input's first, lens_model_3de_classic.cpp:82-88).
 MMBA_DEV void distort_point(int lens_type, const double *lens, double &point_x,
-                            double &point_y) {
+                            double &point_y, const double *chain = nullptr, int nchain = 0) {
     if (lens_type != MMBA_LENS_NONE) {
-        double ox, oy;
-        lens_distort(lens_type, lens, point_x, point_y, ox, oy);
+        double ox, oy, ix = point_x, iy = point_y;
+        for (int k = 0; k < nchain; ++k) {
+            const double *ly = chain + (size_t)k * LENS_LAYER;
+            lens_distort((int)ly[0], ly + 1, ix, iy, ix, iy);
+        }
+        lens_distort(lens_type, lens, ix, iy, ox, oy);
         if (isfinite(ox)) point_x = ox;
         if (isfinite(oy)) point_y = oy;
     }
@@ -715,7 +722,7 @@ MMBA_DEV void distort_point(int lens_type, const double *lens, double &point_x,
 // One observation's residual from a camera record and a bundle position.
 MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, double mkr_y,
                         double sqrtw, int mode, double image_width, int lens_type,
-                        const double *lens) {
+                        const double *lens, const double *chain = nullptr, int nchain = 0) {
     double point_x, point_y;
     project_point(rec, bp, point_x, point_y);
     mkr_x *= rec[18];
@@ -727,7 +734,7 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
         double dot = rec[15] * (bd0 / bl) + rec[16] * (bd1 / bl) + rec[17] * (bd2 / bl);
         if (dot < 0.0) factor = 1e+6;
     }
-    distort_point(lens_type, lens, point_x, point_y);
+    distort_point(lens_type, lens, point_x, point_y, chain, nchain);
     double dx = fabs(mkr_x - point_x), dy = fabs(mkr_y - point_y);
     double dxp = dx * image_width, dyp = dy * image_width;
     Resid r;
@@ -789,7 +796,8 @@ MMBA_DEV double robust_loss(double f, int type, double scale) {
 // solver applies one (fvec only: errorList / errorDistanceList are unscaled).
 MMBA_DEV Resid residual_l(const DevProblem &P, const double *rec, const double *bp, double mkr_x,
                           double mkr_y, double sqrtw, int lens_type, const double *lens) {
-    Resid r = residual(rec, bp, mkr_x, mkr_y, sqrtw, P.mode, P.image_width, lens_type, lens);
+    Resid r = residual(rec, bp, mkr_x, mkr_y, sqrtw, P.mode, P.image_width, lens_type, lens,
+                       P.lens_chain, P.lens_chain_n);
     if (P.loss_on) {
         r.ex = robust_loss(r.ex, P.loss_type, P.loss_scale);
         r.ey = robust_loss(r.ey, P.loss_type, P.loss_scale);

@@ -31,6 +31,8 @@ constexpr int LMAX = 32;    // local Jacobian columns per observation
 constexpr int CF_AIDX = 16;  // camera-frame attribute table: 7 camera + 9 TRS
 constexpr int TILE = 64;    // reduced-system tile edge
 constexpr int CAMREC = 20;  // doubles per camera-frame record
+constexpr int LENS_LAYER = 1 + MMBA_LENS_NUM_ATTRS;  // input lens layer: type, 14 slots
+constexpr int LENS_CHAIN_MAX = 4;                    // input layers per lens
 constexpr int BREC = 16;    // doubles per bundle record (128 B: one L2 line)
 
 // In-place all-reduce of device buffers across the shards of a plan
@@ -242,6 +244,10 @@ struct DevProblem {
     const int *tfm_parent, *tfm_roo, *tfm_attrs;
     const int *cam_tfm, *cam_attrs, *cam_fit, *cam_size, *cam_lens;
     const int *lens_attrs, *lens_type;
+    // input layers of the cameras' lens (deepest first, LENS_LAYER doubles
+    // each: type, 14 slot values), constant for the solve (mmba.h ABI 5)
+    const double *lens_chain;
+    int lens_chain_n;
     const int *bnd_tfm;
     // observations (device order)
     const int *obs_cf, *obs_bnd, *obs_frame, *obs_cam;

@@ -3082,7 +3082,7 @@ __global__ void __launch_bounds__(256) k_reproject(DevProblem P, const double *_
     }
     double px, py;
     project_point(rec, bp, px, py);
-    distort_point(hl, lc, px, py);
+    distort_point(hl, lc, px, py, P.lens_chain, P.lens_chain_n);
     pts[2 * i] = px;
     pts[2 * i + 1] = py;
     mkr[2 * i] = P.obs_xy[2 * i] * rec[18];

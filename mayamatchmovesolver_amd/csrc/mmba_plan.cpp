@@ -236,6 +236,44 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         else if (l != lens_owner)
             throw Unsupported{"cameras with different lens models (B3)"};
     }
+    // ABI 5: the lens's input layers, constants of the solve (mmba.h), deepest
+    // first: type, then the 14 slot values (lens_input_values, or each slot's
+    // attribute at frame 0; absent slots the model's default)
+    std::vector<double> lens_chain_h;
+    if (lens_owner >= 0 && pr->lens_input) {
+        std::vector<int> lay;
+        for (int l = pr->lens_input[lens_owner]; l >= 0; l = pr->lens_input[l]) {
+            require(l < nL, "lens_input");
+            if (l == lens_owner || std::find(lay.begin(), lay.end(), l) != lay.end())
+                throw Unsupported{"cyclic lens input chain"};
+            if ((int)lay.size() >= LENS_CHAIN_MAX)
+                throw Unsupported{"more than 4 input lens layers"};
+            lay.push_back(l);
+        }
+        for (auto it = lay.rbegin(); it != lay.rend(); ++it) {
+            const int l = *it, type = pr->lens_type[l];
+            if (type < MMBA_LENS_3DE_CLASSIC || type > MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED)
+                throw Unsupported{"unknown lens model type"};
+            const bool classic = type == MMBA_LENS_3DE_CLASSIC;
+            const bool anam = type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 ||
+                              type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED;
+            lens_chain_h.push_back((double)type);
+            for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+                double v = ((classic && k == 1) || (anam && k >= 11)) ? 1. : 0.;
+                if (pr->lens_input_values) {
+                    v = pr->lens_input_values[(size_t)MMBA_LENS_NUM_ATTRS * l + k];
+                } else {
+                    const int a = pr->lens_attrs[MMBA_LENS_NUM_ATTRS * l + k];
+                    if (a >= 0) {
+                        require(a < nA, "lens_attrs");
+                        v = pr->attr_values[pr->attr_offset[a]];
+                    }
+                }
+                if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 && k == 13) v = 1.;  // no rescale slot
+                lens_chain_h.push_back(v);
+            }
+        }
+    }
 
     // ---- attribute -> dependent cameras / bundles / lens-cameras ----
     std::vector<std::vector<int>> chain(nT);
@@ -878,6 +916,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.cam_lens = pr->cam_lens ? upload(pr->cam_lens, nC) : nullptr;
     D.lens_attrs = upload(pr->lens_attrs, MMBA_LENS_NUM_ATTRS * (size_t)nL);
     D.lens_type = upload(pr->lens_type, nL);
+    D.lens_chain = lens_chain_h.empty() ? nullptr : upload(lens_chain_h);
+    D.lens_chain_n = (int)(lens_chain_h.size() / LENS_LAYER);
     D.bnd_tfm = upload(pr->bnd_tfm, nB);
     D.obs_cf = upload(d_cf);
     D.obs_bnd = upload(d_bnd);

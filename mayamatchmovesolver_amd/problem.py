@@ -133,6 +133,10 @@ class Problem:
     # ABI 3: per-camera rolling-shutter value in frames (time shift x fps;
     # None = every camera a global shutter, the reference behaviour)
     cam_rs_value: Optional[np.ndarray] = None
+    # ABI 5: layered lens nodes -- the input lens of each lens (-1 none) and
+    # the input layers' plug-read values (None = the attributes at frame 0)
+    lens_input: Optional[np.ndarray] = None
+    lens_input_values: Optional[np.ndarray] = None
 
     def __post_init__(self):
         for name in _FIELDS_I32:
@@ -155,6 +159,11 @@ class Problem:
         if self.cam_rs_value is not None:
             self.cam_rs_value = np.ascontiguousarray(self.cam_rs_value,
                                                      dtype=np.float64).reshape(-1)
+        if self.lens_input is not None:
+            self.lens_input = np.ascontiguousarray(self.lens_input, dtype=np.int32).reshape(-1)
+        if self.lens_input_values is not None:
+            self.lens_input_values = np.ascontiguousarray(self.lens_input_values,
+                                                          dtype=np.float64).reshape(-1)
 
     # sizes -------------------------------------------------------------
     @property
@@ -250,6 +259,11 @@ class Problem:
         p.smooth_value = ptr(self.smooth_value, C.c_double)
         p.cam_rs_value = (ptr(self.cam_rs_value, C.c_double) if self.cam_rs_value is not None
                           else C.cast(None, C.POINTER(C.c_double)))
+        p.lens_input = (ptr(self.lens_input, C.c_int32) if self.lens_input is not None
+                        else C.cast(None, C.POINTER(C.c_int32)))
+        p.lens_input_values = (ptr(self.lens_input_values, C.c_double)
+                               if self.lens_input_values is not None
+                               else C.cast(None, C.POINTER(C.c_double)))
         return p, [self]
 
     # (de)serialisation ---------------------------------------------------
@@ -263,6 +277,9 @@ class Problem:
             d["param_weight"] = self.param_weight
         if self.cam_rs_value is not None:
             d["cam_rs_value"] = self.cam_rs_value
+        for name in ("lens_input", "lens_input_values"):
+            if getattr(self, name) is not None:
+                d[name] = getattr(self, name)
         return d
 
     @classmethod
@@ -274,7 +291,8 @@ class Problem:
             la = np.concatenate([la.reshape(nl, 5), -np.ones((nl, abi.LENS_NUM_ATTRS - 5),
                                                              np.int32)], axis=1).reshape(-1)
             kw["lens_attrs"] = la
-        for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight", "cam_rs_value"]:
+        for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight", "cam_rs_value",
+                                                          "lens_input", "lens_input_values"]:
             if name in d:
                 kw[name] = np.asarray(d[name])
         return cls(num_frames=int(d["num_frames"]), **kw)
@@ -327,6 +345,7 @@ class SceneBuilder:
         self._cam_lens: List[int] = []
         self._lens_type: List[int] = []
         self._lens_attrs: List[List[int]] = []
+        self._lens_input: Dict[int, int] = {}
         self._bnd_tfm: List[int] = []
         self._mkr_cam: List[int] = []
         self._mkr_bnd: List[int] = []
@@ -443,6 +462,12 @@ class SceneBuilder:
         self._lens_type.append(kind)
         self._lens_attrs.append(ids + [-1] * (abi.LENS_NUM_ATTRS - len(ids)))
         return idx, ids
+
+    def lens_input(self, lens: int, input_lens: int):
+        """Layer ``input_lens`` under ``lens`` (a lens node's inLens connection,
+        mmba.h ABI 5): the input layer's values are constants of the solve."""
+        assert 0 <= lens < len(self._lens_type) and 0 <= input_lens < len(self._lens_type)
+        self._lens_input[int(lens)] = int(input_lens)
 
     def bundle(self, tfm: int) -> int:
         self._bnd_tfm.append(int(tfm))
@@ -575,6 +600,11 @@ class SceneBuilder:
             setattr(prob, kind + "_weight", np.array([r[2] for r in use], np.float64))
             setattr(prob, kind + "_variance", np.array([r[3] for r in use], np.float64))
             setattr(prob, kind + "_value", np.array([r[4] for r in use], np.float64))
+        if self._lens_input:
+            li = np.full(len(self._lens_type), -1, np.int32)
+            for k, v in self._lens_input.items():
+                li[k] = v
+            prob.lens_input = li
         prob.meta = dict(meta or {})
         return prob
 

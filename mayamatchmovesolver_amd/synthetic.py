@@ -432,6 +432,11 @@ def _bulk_problem(F, cams_t, cams_r, cams_focal, cam_solve, bnd_init, bnd_solved
             lens_idx, lens_ids = b.lens_3de_anamorphic_std_deg4(*lens["init"])
         else:
             lens_idx, lens_ids = b.lens_3de_classic(*lens["init"])
+        if "input" in lens:
+            kind, vals = lens["input"]
+            assert kind == "radial"
+            in_idx, _ = b.lens_3de_radial_std_deg4(*vals)
+            b.lens_input(lens_idx, in_idx)
     cam_attr_ids = []
     for c in range(len(cams_t)):
         tfm, tids = b.transform(t=[cams_t[c][:, 0], cams_t[c][:, 1], cams_t[c][:, 2]],
@@ -698,6 +703,18 @@ def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0):
         distort = _radial_distort_truth
         lens = {"model": "radial", "init": (0.0,) + lens_true[1:3] + (0.0,) + lens_true[4:],
                 "solve_slots": (0, 3)}
+    elif lens_model == "layered":
+        # the classic lens (distortion + quartic solved) layered over a
+        # static radial deg 4 input lens (mmba.h ABI 5): the input is applied
+        # first, with its values as read (constants of the solve)
+        lens_true = (0.05, 1.0, 0.0, 0.0, 0.01)
+        in_true = (0.03, 0.002, -0.001, 0.008, 0.0, 0.0, 15.0, 0.02)
+
+        def distort(c, x, y):
+            ix, iy = _radial_distort_truth(in_true, x, y)
+            return _lens_distort_truth(c, ix, iy)
+        lens = {"init": (0.0, 1.0, 0.0, 0.0, 0.0), "solve_slots": (0, 4),
+                "input": ("radial", in_true)}
     else:
         lens_true = (0.05, 1.0, 0.0, 0.0, 0.01)
         distort = _lens_distort_truth

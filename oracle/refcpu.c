@@ -1212,6 +1212,47 @@ static void lens_coeffs(const ref_scene *s, int lens, int f, double c[MMBA_LENS_
     if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.; /* no rescale slot */
 }
 
+static void lens_model_distort(int type, const double *c, double x, double y, double *ox,
+                               double *oy) {
+    if (type == MMBA_LENS_3DE_CLASSIC)
+        ref_lens_3de_classic_distort(c, x, y, ox, oy);
+    else if (type == MMBA_LENS_3DE_RADIAL_STD_DEG4)
+        ref_lens_3de_radial_distort(c, x, y, ox, oy);
+    else
+        ref_lens_3de_anamorphic_distort(c, x, y, ox, oy);
+}
+
+/* An input layer of a layered lens (mmba.h ABI 5): the values read with the
+ * camera-connected node's plug (lens_input_values), or each slot's
+ * attribute at frame 0 -- constants of the solve (the reference never
+ * re-points the clones' input chain, maya_lens_model_utils.cpp:715). */
+static void lens_layer_values(const ref_scene *s, int l, double c[MMBA_LENS_NUM_ATTRS]) {
+    const mmba_problem *p = s->p;
+    const int type = p->lens_type[l];
+    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+        if (p->lens_input_values) {
+            c[k] = p->lens_input_values[MMBA_LENS_NUM_ATTRS * l + k];
+        } else {
+            const int a = p->lens_attrs[MMBA_LENS_NUM_ATTRS * l + k];
+            c[k] = a >= 0 ? p->attr_values[p->attr_offset[a]] : lens_default(type, k);
+        }
+    }
+    if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.;
+}
+
+/* The model's applyModelDistort: its input model's first (recursively, so
+ * the deepest layer runs first), no check in between
+ * (lens_model_3de_classic.cpp:82-88 and the other models alike). */
+static void lens_chain_distort(const ref_scene *s, int l, int depth, double x, double y,
+                               double *ox, double *oy) {
+    const mmba_problem *p = s->p;
+    const int in = p->lens_input ? p->lens_input[l] : -1;
+    if (in >= 0 && depth < 8) lens_chain_distort(s, in, depth + 1, x, y, &x, &y);
+    double c[MMBA_LENS_NUM_ATTRS];
+    lens_layer_values(s, l, c);
+    lens_model_distort(p->lens_type[l], c, x, y, ox, oy);
+}
+
 static void apply_lens(const ref_scene *s, int cam, int f, double *px,
                        double *py) {
     const mmba_problem *p = s->p;
@@ -1220,14 +1261,11 @@ static void apply_lens(const ref_scene *s, int cam, int f, double *px,
     if (lens < 0) return;
     const int type = p->lens_type[lens];
     if (type < MMBA_LENS_3DE_CLASSIC || type > MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED) return;
-    double c[MMBA_LENS_NUM_ATTRS], ox = *px, oy = *py;
+    double c[MMBA_LENS_NUM_ATTRS], ox = *px, oy = *py, ix = *px, iy = *py;
     lens_coeffs(s, lens, f, c);
-    if (type == MMBA_LENS_3DE_CLASSIC)
-        ref_lens_3de_classic_distort(c, *px, *py, &ox, &oy);
-    else if (type == MMBA_LENS_3DE_RADIAL_STD_DEG4)
-        ref_lens_3de_radial_distort(c, *px, *py, &ox, &oy);
-    else
-        ref_lens_3de_anamorphic_distort(c, *px, *py, &ox, &oy);
+    const int in = p->lens_input ? p->lens_input[lens] : -1;
+    if (in >= 0) lens_chain_distort(s, in, 1, ix, iy, &ix, &iy);
+    lens_model_distort(type, c, ix, iy, &ox, &oy);
     if (isfinite(ox)) *px = ox; /* adjust_measureErrors.cpp:466-472 */
     if (isfinite(oy)) *py = oy;
 }

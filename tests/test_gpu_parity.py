@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from mayamatchmovesolver_amd import abi, make_options, synthetic as S
+from mayamatchmovesolver_amd.problem import FLOAT_MAX
 from mayamatchmovesolver_amd.solver import Solver
 
 pytestmark = pytest.mark.gpu
@@ -116,6 +117,8 @@ SMALL_CONFIGS = [
     (4, dict(frames=8, scale=0.05, lens_model="anamorphic")),  # 3DE anamorphic std deg 4
     (4, dict(frames=24, scale=0.2, lens_model="anamorphic_rescaled")),
     (4, dict(frames=8, scale=0.05, lens_model="classic_animated")),  # animated lens attr
+    (4, dict(frames=8, scale=0.05, lens_model="layered")),  # classic over a radial input (ABI 5)
+    (4, dict(frames=24, scale=0.2, lens_model="layered")),
 ]
 
 
@@ -160,3 +163,38 @@ def test_reproject_matches_oracle(idx, kw, mode, oracle, gpu_ctx):
             np.testing.assert_allclose(mkr, mr, rtol=1e-15, atol=0)
     finally:
         s.close()
+
+
+def test_layered_lens_measure_jacobian_and_input_attr(oracle, gpu_ctx):
+    """Layered lens nodes (mmba.h ABI 5): the measurement and Jacobian of the
+    C5 subset with its classic lens over a static radial input layer, then the
+    same scene with an input layer's attribute solved -- the reference's
+    column is zero there (the input chain is never re-pointed at the solved
+    clones, maya_lens_model_utils.cpp:715) -- through the whole solve."""
+    prob = S.make_config(4, frames=8, scale=0.05, lens_model="layered")
+    opt = S.config_options(prob)
+    x1 = prob.x0.copy()
+    x1[0], x1[1] = 0.04, 0.008
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        fv, *_ = s.measure(x1)
+        fr, *_ = oracle.measure(prob, opt, x1)
+        assert np.max(np.abs(fv - fr)) <= 1e-9 * max(1.0, np.max(np.abs(fr)))
+        J = s.jacobian(x1)
+        _, J_ref = oracle.jacobian(prob, opt, x1)
+        assert np.max(np.abs(J - J_ref)) <= 1e-7 * np.max(np.abs(J_ref))
+    finally:
+        s.close()
+    # solve the input layer's degree-2 distortion too (a static attribute)
+    a = int(prob.lens_attrs[14 + 0])
+    d = prob.to_npz_dict()
+    v = float(prob.attr_values[prob.attr_offset[a]])
+    for name, val in (("param_attr", a), ("param_frame", -1), ("param_min", -FLOAT_MAX),
+                      ("param_max", FLOAT_MAX), ("param_offset", 0.0),
+                      ("param_scale", 1.0), ("x0", v)):
+        d[name] = np.append(d[name], val)
+    p2 = type(prob).from_npz_dict(d)
+    p2.meta = dict(prob.meta)
+    _, J2 = oracle.jacobian(p2, opt, p2.x0)
+    assert not np.any(J2[:, -1])
+    check_solve(p2, opt, oracle, gpu_ctx)
