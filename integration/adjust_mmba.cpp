@@ -103,26 +103,60 @@ class MayaSceneReader : public SceneReader {
 
     // the lens node on camera.inLens (maya_lens_model_utils.cpp)
     LensRead lens(const std::string &camera_shape) override {
-        LensRead l;
         MSelectionList sel;
         MObject shape_obj;
         if (sel.add(MString(camera_shape.c_str())) != MS::kSuccess ||
             sel.getDependNode(0, shape_obj) != MS::kSuccess)
-            return l;
+            return LensRead{};
+        return lens_on(shape_obj);
+    }
+
+    // a lens node by name: its own inLens is the next layer up the chain
+    LensRead lens_node(const std::string &node) override {
+        MSelectionList sel;
+        MObject obj;
+        if (sel.add(MString(node.c_str())) != MS::kSuccess || sel.getDependNode(0, obj) != MS::kSuccess)
+            return LensRead{};
+        LensRead l;
+        read_lens(obj, l);
+        return l;
+    }
+
+  private:
+    // the lens node connected to node.inLens (connected = false when none)
+    LensRead lens_on(const MObject &node) {
+        LensRead l;
         MStatus status;
-        MFnDependencyNode shape(shape_obj, &status);
-        MPlug in_lens = shape.findPlug("inLens", true, &status);
+        MFnDependencyNode fn(node, &status);
+        MPlug in_lens = fn.findPlug("inLens", true, &status);
         if (!status || in_lens.isNull()) return l;
         MPlugArray src;
         in_lens.connectedTo(src, /*asDst=*/true, /*asSrc=*/false, &status);
         if (src.length() == 0) return l;
-        MFnDependencyNode lens_fn(src[0].node(), &status);
+        read_lens(src[0].node(), l);
+        return l;
+    }
+
+    // the name of the node on obj.inLens ("" when none), not read further
+    std::string upstream_name(const MObject &obj) {
+        MStatus status;
+        MFnDependencyNode fn(obj, &status);
+        MPlug in_lens = fn.findPlug("inLens", true, &status);
+        if (!status || in_lens.isNull()) return std::string();
+        MPlugArray src;
+        in_lens.connectedTo(src, /*asDst=*/true, /*asSrc=*/false, &status);
+        if (src.length() == 0) return std::string();
+        MFnDependencyNode up(src[0].node(), &status);
+        return status ? std::string(up.name().asChar()) : std::string();
+    }
+
+    void read_lens(const MObject &obj, LensRead &l) {
+        MStatus status;
+        MFnDependencyNode lens_fn(obj, &status);
+        if (!status) return;
         l.connected = true;
         l.node = lens_fn.name().asChar();
-        MPlug up = lens_fn.findPlug("inLens", true, &status);
-        MPlugArray up_src;
-        if (status && !up.isNull()) up.connectedTo(up_src, true, false, &status);
-        l.layered = up_src.length() > 0;
+        l.input = upstream_name(obj);
         Attr enable;
         enable.setNodeName(lens_fn.name());
         enable.setAttrName("enable");
@@ -133,10 +167,8 @@ class MayaSceneReader : public SceneReader {
         short m = 0;
         model.getValue(m, mode_);
         l.model = m;
-        return l;
     }
 
-  private:
     const MTimeArray &frames_;
     int mode_;
 };

@@ -104,18 +104,44 @@ int32_t FlatScene::transform_of(const std::string &path, int depth) {
     return id;
 }
 
-// The lens node on camera.inLens, one layer: its model and its coefficients
-// in the MMBA_LENS_* slots (mmlens LensModelType, _cxxbridge.h:414-421).
+// The lens nodes on camera.inLens: the enabled nodes of the chain, top
+// (camera-connected) first, as the reference collects them
+// (maya_lens_model_utils.cpp:405-465); the first is the camera's lens, the
+// others its input layers (mmba.h ABI 5: constants of the solve, evaluated
+// with their attributes at the first solve frame).  Each node's model and
+// coefficients in the MMBA_LENS_* slots (mmlens LensModelType,
+// _cxxbridge.h:414-421).
 int32_t FlatScene::lens_of(const std::string &camera_shape) {
-    const LensRead l = rd_->lens(camera_shape);
-    if (!l.connected) return -1;
-    auto it = lens_id.find(l.node);
-    if (it != lens_id.end()) return it->second;
-    if (l.layered) {
-        why = "layered lens nodes: " + l.node;
-        return -2;
+    LensRead l = rd_->lens(camera_shape);
+    std::vector<LensRead> chain;
+    for (int depth = 0; l.connected; ++depth) {
+        if (depth > 16) {
+            why = "lens input chain deeper than 16 nodes: " + l.node;
+            return -2;
+        }
+        if (l.enabled) chain.push_back(l);
+        if (l.input.empty()) break;
+        l = rd_->lens_node(l.input);
     }
-    if (!l.enabled) return -1;
+    int32_t below = -1;  // the layer under the current one
+    for (auto it = chain.rbegin(); it != chain.rend(); ++it) {
+        const int32_t id = lens_layer(*it, below);
+        if (id == -2) return -2;
+        if (id >= 0) below = id;  // a passthrough layer adds nothing to the chain
+    }
+    return below;
+}
+
+// One lens node as a lens of the flat scene, its input layer `below` (-1 none).
+int32_t FlatScene::lens_layer(const LensRead &l, int32_t below) {
+    auto it = lens_id.find(l.node);
+    if (it != lens_id.end()) {
+        if (lens_input[it->second] != below) {
+            why = "lens node with two different input chains: " + l.node;
+            return -2;
+        }
+        return it->second;
+    }
     int32_t type;
     std::vector<const char *> slots;
     if (l.model == 2) {
@@ -140,7 +166,7 @@ int32_t FlatScene::lens_of(const std::string &camera_shape) {
                  "tdeAnamorphicStdDeg4_squeeze_y"};
         if (l.model == 5) slots.push_back("tdeAnamorphicStdDeg4_rescale");
     } else {
-        return -1;  // passthrough / uninitialised: no distortion
+        return -1;  // passthrough / uninitialised: no distortion of its own
     }
     int32_t ids[MMBA_LENS_NUM_ATTRS];
     for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) ids[k] = -1;
@@ -148,6 +174,7 @@ int32_t FlatScene::lens_of(const std::string &camera_shape) {
     const int32_t id = static_cast<int32_t>(lens_type.size());
     lens_type.push_back(type);
     lens_attrs.insert(lens_attrs.end(), ids, ids + MMBA_LENS_NUM_ATTRS);
+    lens_input.push_back(below);
     lens_id.emplace(l.node, id);
     return id;
 }
@@ -301,6 +328,9 @@ mmba_problem FlatScene::problem() const {
     p.num_lenses = static_cast<int32_t>(lens_type.size());
     p.lens_type = lens_type.data();
     p.lens_attrs = lens_attrs.data();
+    bool layered = false;
+    for (int32_t v : lens_input) layered = layered || v >= 0;
+    p.lens_input = layered ? lens_input.data() : nullptr;  // input values: attributes at frame 0
     p.num_bundles = static_cast<int32_t>(bnd_tfm.size());
     p.bnd_tfm = bnd_tfm.data();
     p.num_markers = static_cast<int32_t>(mkr_cam.size());
@@ -352,6 +382,7 @@ std::vector<uint8_t> FlatScene::plan_key(const mmba_options &o) const {
     put(k, cam_lens);
     put(k, lens_type);
     put(k, lens_attrs);
+    put(k, lens_input);
     put(k, bnd_tfm);
     put(k, mkr_cam);
     put(k, mkr_bnd);

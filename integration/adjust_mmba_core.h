@@ -52,7 +52,7 @@ struct TransformRead {
 struct LensRead {
     bool connected = false;
     std::string node;
-    bool layered = false;         // the lens node has a lens on its own inLens
+    std::string input;            // the lens node on this node's own inLens ("" = none)
     bool enabled = true;
     int model = 0;                // mmLensModel3de lensModel: 2 classic, 3 radial std deg 4,
                                   // 4 anamorphic std deg 4, 5 anamorphic rescaled
@@ -67,6 +67,8 @@ class SceneReader {
                           bool force_animated) = 0;
     virtual TransformRead transform(const std::string &path) = 0;
     virtual LensRead lens(const std::string &camera_shape) = 0;
+    // a lens node by name (the upstream layers of a layered lens)
+    virtual LensRead lens_node(const std::string &node) = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -114,7 +116,7 @@ struct FlatScene {
     std::vector<double> attr_values;
     std::vector<int32_t> tfm_parent, tfm_roo, tfm_attrs;
     std::vector<int32_t> cam_tfm, cam_attrs, cam_fit, cam_size, cam_lens;
-    std::vector<int32_t> lens_type, lens_attrs;
+    std::vector<int32_t> lens_type, lens_attrs, lens_input;
     std::vector<int32_t> bnd_tfm, mkr_cam, mkr_bnd;
     std::vector<int32_t> obs_marker, obs_frame;
     std::vector<double> obs_xy, obs_weight;
@@ -138,6 +140,7 @@ struct FlatScene {
     int32_t attr_of(const std::string &node, const char *attr);
     int32_t transform_of(const std::string &path, int depth = 0);
     int32_t lens_of(const std::string &camera_shape);
+    int32_t lens_layer(const LensRead &l, int32_t below);
 };
 
 // SolverOptions (adjust_data.h:133-185) fields the LM path reads.

@@ -9,7 +9,8 @@
 //   1  test3 (test3.py:55-124): camera rx, ry solved (delta 1e-5), known
 //      answer (7.44014, -32.3891)
 //   2  an animated camera over 4 frames with per-frame rotate solved, a 3DE
-//      classic lens on camera.inLens (distortion solved) and a rolling
+//      classic lens on camera.inLens (distortion solved) layered over a
+//      static radial lens, and a rolling
 //      shutter: keyed attributes, lens slots, rows of several frames
 //
 // Built twice (tests/shim/Makefile): as an executable (main: every scene
@@ -54,6 +55,11 @@ struct MemReader : SceneReader {
     LensRead lens(const std::string &shape) override {
         auto it = lenses.find(shape);
         return it == lenses.end() ? LensRead{} : it->second;
+    }
+    std::map<std::string, LensRead> nodes;  // lens nodes by name (upstream layers)
+    LensRead lens_node(const std::string &node) override {
+        auto it = nodes.find(node);
+        return it == nodes.end() ? LensRead{} : it->second;
     }
 
     void stat(const std::string &na, double v) {
@@ -167,7 +173,21 @@ std::unique_ptr<Scene> make_scene(int which) {
     lens.connected = true;
     lens.node = "lens1";
     lens.model = 2;  // 3DE classic
+    lens.input = "lens0";  // layered over a radial lens (mmba.h ABI 5)
     rd.lenses["|cam|camShape"] = lens;
+    LensRead lens0;
+    lens0.connected = true;
+    lens0.node = "lens0";
+    lens0.model = 3;  // 3DE radial std deg 4, static
+    rd.nodes["lens0"] = lens0;
+    rd.stat("lens0.tdeRadialStdDeg4_degree2_distortion", 0.03);
+    rd.stat("lens0.tdeRadialStdDeg4_degree2_u", 0.002);
+    rd.stat("lens0.tdeRadialStdDeg4_degree2_v", -0.001);
+    rd.stat("lens0.tdeRadialStdDeg4_degree4_distortion", 0.008);
+    rd.stat("lens0.tdeRadialStdDeg4_degree4_u", 0.0);
+    rd.stat("lens0.tdeRadialStdDeg4_degree4_v", 0.0);
+    rd.stat("lens0.tdeRadialStdDeg4_cylindricDirection", 15.0);
+    rd.stat("lens0.tdeRadialStdDeg4_cylindricBending", 0.02);
     rd.stat("lens1.tdeClassic_distortion", 0.02);
     rd.stat("lens1.tdeClassic_anamorphicSqueeze", 1.0);
     rd.stat("lens1.tdeClassic_curvatureX", 0.0);

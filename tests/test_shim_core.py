@@ -60,6 +60,8 @@ def python_scene(which):
     tfm, tids = b.transform(t=[0.1 * f, 1.0, -0.05 * f],
                             r=[1.0 + 0.5 * f, -2.0 + 0.3 * f, 0.2 * f])
     lens, lids = b.lens_3de_classic(distortion=0.02)
+    lens0, _ = b.lens_3de_radial_std_deg4(0.03, 0.002, -0.001, 0.008, 0.0, 0.0, 15.0, 0.02)
+    b.lens_input(lens, lens0)  # the classic lens layered over a static radial one
     cam, _ = b.camera(tfm, lens=lens)
     for k in range(5):
         bt, _ = b.transform(t=(-4.0 + 2.0 * k, 1.0 + 0.5 * k, -20.0 - 3.0 * k))
