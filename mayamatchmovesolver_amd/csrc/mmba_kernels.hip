@@ -953,7 +953,7 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i, const JacC
 // residuals are independent straight-line code, so their fp64 latency
 // chains overlap (the generic loop serialises them behind its dependent
 // variant-table loads).  Emits columns in the generic kernel's order.
-template <int NCV, bool GEN>
+template <int NCV, bool GEN, bool UNI>
 __global__ void __launch_bounds__(128) k_jacobian_u(
     DevProblem P, const double *__restrict__ recs, const double *__restrict__ step,
     int solver_type, double *__restrict__ J, int *__restrict__ jcol, int *__restrict__ nloc,
@@ -961,9 +961,21 @@ __global__ void __launch_bounds__(128) k_jacobian_u(
     const int i = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     if (i >= P.M) return;
     double cx[NCV], cy[NCV], fx, fy;
-    const JacCf<NCV> C = jac_cf_load<NCV>(P, P.obs_cf[i], recs, step, stale_param);
-    jac_obs_u<NCV, GEN>(P, i, C, solver_type == MMBA_SOLVER_CMINPACK_LMDER, J, jcol, nloc, eu,
-                        ed, cx, cy, fx, fy);
+    const int cf = P.obs_cf[i];
+    const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
+    if (UNI) {
+        // every lane of the wave in one camera-frame (C2: 1,656 observations
+        // per frame): the camera-frame index is wave-uniform, so its records,
+        // variant parameters and steps are scalar (broadcast) loads
+        const int cfu = __builtin_amdgcn_readfirstlane(cf);
+        if (__all(cf == cfu)) {
+            const JacCf<NCV> C = jac_cf_load<NCV>(P, cfu, recs, step, stale_param);
+            jac_obs_u<NCV, GEN>(P, i, C, lmder, J, jcol, nloc, eu, ed, cx, cy, fx, fy);
+            return;
+        }
+    }
+    const JacCf<NCV> C = jac_cf_load<NCV>(P, cf, recs, step, stale_param);
+    jac_obs_u<NCV, GEN>(P, i, C, lmder, J, jcol, nloc, eu, ed, cx, cy, fx, fy);
 }
 
 // -------------------------------------------------------------------------
@@ -3195,9 +3207,20 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
         launch_jacobian_rs(s, P, ext_pert, step, solver_type, J, jcol, nloc, stale_param, eu, ed);
         return;
     }
+    // MMBA_JAC_UNI=0: per-lane record loads only (A/B of the wave-uniform path)
+    static const bool uni = [] {
+        const char *e = std::getenv("MMBA_JAC_UNI");
+        return !(e && std::atoi(e) == 0);
+    }();
 #define MMBA_JAC_U(NCV, GEN)                                                                \
-    k_jacobian_u<NCV, GEN><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, step, solver_type, J, jcol, \
-                                                           nloc, stale_param, eu, ed)
+    do {                                                                                    \
+        if (uni)                                                                            \
+            k_jacobian_u<NCV, GEN, true><<<nblk(P.M, 128), 128, 0, s>>>(                    \
+                P, recs, step, solver_type, J, jcol, nloc, stale_param, eu, ed);            \
+        else                                                                                \
+            k_jacobian_u<NCV, GEN, false><<<nblk(P.M, 128), 128, 0, s>>>(                   \
+                P, recs, step, solver_type, J, jcol, nloc, stale_param, eu, ed);            \
+    } while (0)
     if (ncv == 6 || ncv == 7) {
         if (ncv == 6) {
             if (P.all_bnd_fast) MMBA_JAC_U(6, false); else MMBA_JAC_U(6, true);
