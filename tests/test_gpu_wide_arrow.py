@@ -44,11 +44,14 @@ def test_wide_arrow_band(kw, ng, mode, oracle, gpu_ctx):
     check(prob, opt, oracle, gpu_ctx)
 
 
-@pytest.mark.parametrize("kw", [dict(frames=10, window=3, bundles=30),
-                                dict(frames=10, window=3, bundles=30, n_witness=5, n_focal=5)])
+@pytest.mark.parametrize("kw", [dict(frames=4), dict(frames=5, n_witness=5, n_focal=5)])
 def test_wide_arrow_bcr(kw, oracle, gpu_ctx):
-    """Bundles on 3-frame windows of the animated camera: a banded reduced
-    system, factored by block cyclic reduction with the wide arrow."""
+    """Four / five frames of the animated camera: half bandwidth 23 / 29, so
+    the reduced system is factored by block cyclic reduction (K = 24 / 32)
+    with the 24 / 32-wide arrow (roots of order 48 / 64).  (Windowed
+    visibility of the animated camera over more frames leaves these rigs
+    without a parity bar: the oracle's own x moves by O(1) under a 1-ulp
+    change of x0.)"""
     prob = S.witness_scene(**kw)
     opt = make_options()
     assert reduced_kind(prob, opt, gpu_ctx) == BAND
@@ -67,7 +70,7 @@ def test_wide_arrow_block_diagonal(kw, mode, oracle, gpu_ctx):
 
 
 @pytest.mark.parametrize("kw,n", [(dict(n_witness=5, n_focal=5), 2),
-                                  (dict(frames=10, window=3, bundles=30), 3)])
+                                  (dict(frames=5, n_witness=5, n_focal=5), 3)])
 def test_wide_arrow_sharded(kw, n, oracle):
     """Frame shards (in-process communicators): the global rows are
     all-reduced like the narrow arrow's."""

@@ -20,7 +20,7 @@ def globals_and_reach(prob):
 
 @pytest.mark.parametrize("kw,ng", [(dict(), 24), (dict(n_witness=5, n_focal=5), 32),
                                    (dict(n_witness=5, n_focal=5, extra_globals=1), 33),
-                                   (dict(frames=10, window=3, bundles=30), 24),
+                                   (dict(frames=4), 24), (dict(frames=5, n_witness=5, n_focal=5), 32),
                                    (dict(n_witness=2, n_focal=2, extra_globals=2,
                                          lens="anamorphic"), 23)])
 def test_witness_scene_globals(kw, ng):
