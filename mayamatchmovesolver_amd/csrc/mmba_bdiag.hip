@@ -20,7 +20,8 @@ namespace mmba {
 // Lane roles of one block's wave: rows 0..PC-1 of the block, then one
 // right-hand-side lane per arrow row (Y_b columns), then the rhs lane.
 constexpr int BD_G0 = 16;  // first arrow lane
-constexpr int BD_R = 32;   // right-hand-side lane
+constexpr int BD_R = BD_G0 + NGMAX;  // right-hand-side lane (after the widest arrow)
+static_assert(BD_R < 64, "arrow and right-hand-side lanes exceed the wave");
 
 // Augmented Cholesky of one block by one wave (bcr_chol_aug_wave's scheme
 // with a register-only column broadcast: PC <= 10 is short enough for
