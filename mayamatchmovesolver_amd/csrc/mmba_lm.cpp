@@ -204,7 +204,10 @@ void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed, dou
     // stiffness / smoothness rows: their partial goes after the residual blocks
     launch_rows_eval(s, P, df + 2 * (size_t)M, eu ? eu + 2 * (size_t)M : nullptr, d_partial,
                      (M + 255) / 256);
-    launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + slot, d_ticket, dist);
+    // the ticket epilogue sums only the residual kernel's own grid: with
+    // attribute rows the rows' partial would be dropped, so reduce separately
+    launch_residual(s, P, d_recs, df, eu, ed, d_partial, d_scalar + slot,
+                    P.nrows > 0 ? nullptr : d_ticket, dist);
     span_end(SPAN_RESID);
     allreduce(d_scalar + slot, 1);
 }
