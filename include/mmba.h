@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 5
+#define MMBA_ABI_VERSION 6
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -518,9 +518,20 @@ typedef struct mmba_kernel_stats {
     int32_t dataflow_fallback; /* 1 once a timed-out dataflow wait in the block
                                cyclic reduction switched this plan to the
                                per-level launches (ABI 3)                  */
-    int32_t solve_launch;   /* 1 when this plan runs a solve as ONE
-                               cooperative launch (block-diagonal plans
-                               without callbacks; ABI 4)                  */
+    int32_t shards_replicated; /* ABI 6 (the slot of ABI 4's solve_launch,
+                               whose cooperative solve was removed): 1 when
+                               mmba_plan_create_sharded found that the
+                               problem does not shard (too few camera-frame
+                               rows per shard, a band wider than the
+                               partitioned solver takes, rolling shutter,
+                               B15 ...) and every shard solves the whole
+                               problem redundantly, without collectives    */
+    int32_t spec_replays;   /* ABI 6: solves of this plan replayed from x0
+                               because a Jacobian enqueued ahead of the
+                               host's lmder decision was not the one the
+                               host took (expected 0; the replay enqueues
+                               every Jacobian after the decision)          */
+    int32_t pad_ks0;
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);

@@ -108,7 +108,7 @@ int32_t FlatScene::transform_of(const std::string &path, int depth) {
 // (camera-connected) first, as the reference collects them
 // (maya_lens_model_utils.cpp:405-465); the first is the camera's lens, the
 // others its input layers (mmba.h ABI 5: constants of the solve, evaluated
-// with their attributes at the first solve frame).  Each node's model and
+// with their attributes at the current time).  Each node's model and
 // coefficients in the MMBA_LENS_* slots (mmlens LensModelType,
 // _cxxbridge.h:414-421).
 int32_t FlatScene::lens_of(const std::string &camera_shape) {
@@ -175,6 +175,22 @@ int32_t FlatScene::lens_layer(const LensRead &l, int32_t below) {
     lens_type.push_back(type);
     lens_attrs.insert(lens_attrs.end(), ids, ids + MMBA_LENS_NUM_ATTRS);
     lens_input.push_back(below);
+    // the slot values at the current time: what an input layer's plug model
+    // holds when the camera-connected node is read (the reference reads it
+    // at the current Maya time, with no DG context, and clones it per frame,
+    // maya_lens_model_utils.cpp:433-446, 655-662); absent slots take the
+    // model's default (squeeze / rescale 1, the rest 0)
+    const bool classic = type == MMBA_LENS_3DE_CLASSIC;
+    const bool anam = type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 ||
+                      type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED;
+    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+        double v = ((classic && k == 1) || (anam && k >= 11)) ? 1.0 : 0.0;
+        if (ids[k] >= 0) {
+            const int64_t off = attr_offset[ids[k]];
+            v = attr_values[off + (attr_animated[ids[k]] ? cur_frame_ : 0)];
+        }
+        lens_input_values.push_back(v);
+    }
     lens_id.emplace(l.node, id);
     return id;
 }
@@ -186,6 +202,7 @@ bool FlatScene::build(const SolverInputs &in, SceneReader &rd) {
         why = "no solve frames";
         return false;
     }
+    cur_frame_ = std::min(std::max(in.current_frame, 0), num_frames - 1);
     // attributes solved per frame are animated in the flat scene
     for (const auto &pa : in.paramToAttrList) {
         if (pa.first < 0 || pa.first >= static_cast<int>(in.attrs.size())) {
@@ -330,7 +347,8 @@ mmba_problem FlatScene::problem() const {
     p.lens_attrs = lens_attrs.data();
     bool layered = false;
     for (int32_t v : lens_input) layered = layered || v >= 0;
-    p.lens_input = layered ? lens_input.data() : nullptr;  // input values: attributes at frame 0
+    p.lens_input = layered ? lens_input.data() : nullptr;
+    p.lens_input_values = layered ? lens_input_values.data() : nullptr;  // at the current time
     p.num_bundles = static_cast<int32_t>(bnd_tfm.size());
     p.bnd_tfm = bnd_tfm.data();
     p.num_markers = static_cast<int32_t>(mkr_cam.size());
@@ -383,6 +401,16 @@ std::vector<uint8_t> FlatScene::plan_key(const mmba_options &o) const {
     put(k, lens_type);
     put(k, lens_attrs);
     put(k, lens_input);
+    {  // the input layers' values are constants a plan captures (not the
+       // camera lenses' own, which are attribute values refreshed per solve)
+        std::vector<double> layer_vals;
+        for (size_t l = 0; l < lens_input.size(); ++l)
+            if (std::find(lens_input.begin(), lens_input.end(), (int32_t)l) != lens_input.end())
+                layer_vals.insert(layer_vals.end(),
+                                  lens_input_values.begin() + MMBA_LENS_NUM_ATTRS * l,
+                                  lens_input_values.begin() + MMBA_LENS_NUM_ATTRS * (l + 1));
+        put(k, layer_vals);
+    }
     put(k, bnd_tfm);
     put(k, mkr_cam);
     put(k, mkr_bnd);

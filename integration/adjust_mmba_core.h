@@ -117,6 +117,10 @@ struct FlatScene {
     std::vector<int32_t> tfm_parent, tfm_roo, tfm_attrs;
     std::vector<int32_t> cam_tfm, cam_attrs, cam_fit, cam_size, cam_lens;
     std::vector<int32_t> lens_type, lens_attrs, lens_input;
+    // every lens's 14 slot values at the current time (SolverInputs::
+    // current_frame): the plug values the reference's input layers hold
+    // for the whole solve (maya_lens_model_utils.cpp:433-446, mmba.h ABI 5)
+    std::vector<double> lens_input_values;
     std::vector<int32_t> bnd_tfm, mkr_cam, mkr_bnd;
     std::vector<int32_t> obs_marker, obs_frame;
     std::vector<double> obs_xy, obs_weight;
@@ -137,6 +141,7 @@ struct FlatScene {
     std::unordered_map<std::string, int32_t> attr_id, tfm_id, lens_id;
     std::unordered_map<std::string, bool> keyed;
     SceneReader *rd_ = nullptr;
+    int32_t cur_frame_ = 0;  // SolverInputs::current_frame, clamped to the solve frames
     int32_t attr_of(const std::string &node, const char *attr);
     int32_t transform_of(const std::string &path, int depth = 0);
     int32_t lens_of(const std::string &camera_shape);

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -199,7 +199,9 @@ class MmbaKernelStats(C.Structure):
         ("reduced_dim", C.c_int32),
         ("reduced_kind", C.c_int32),
         ("dataflow_fallback", C.c_int32),
-        ("solve_launch", C.c_int32),
+        ("shards_replicated", C.c_int32),
+        ("spec_replays", C.c_int32),
+        ("pad_ks0", C.c_int32),
     ]
 
     def as_dict(self):

@@ -159,24 +159,81 @@ int mmba_plan_create(mmba_context *ctx, const mmba_problem *prob, const mmba_opt
     return mmba_plan_create_sharded(ctx, prob, opt, nullptr, out);
 }
 
+// Every shard of a sharded plan must take the same path, or the first
+// collective of a solve would wait forever: the shards all-reduce (max) a
+// build status word.  0 = built, 1 = this problem does not shard (too few
+// camera-frame rows per shard, a band wider than the partitioned solver
+// takes, rolling shutter, B15 ...: MMBA_ERR_UNSUPPORTED from the sharded
+// build), 2 = any other failure.  On 1 every shard rebuilds the plan
+// unsharded and solves the whole problem redundantly -- no collectives, the
+// same bits on every shard (the reference solveFrames takes any problem,
+// adjust_base.cpp:713-1287, so a sharded caller must not be refused for
+// sharding's sake).  On 2 every shard fails.
+static int agree_build_status(mmba_context *ctx, Comm *c, int mine) {
+    double *d = nullptr;
+    double v = mine;
+    try {
+        MMBA_HIP(hipMalloc(&d, sizeof(double)));
+        MMBA_HIP(hipMemcpyAsync(d, &v, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+        c->allreduce(d, 1, ReduceOp::Max, ctx->stream);
+        MMBA_HIP(hipMemcpyAsync(&v, d, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        MMBA_HIP(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+        if (d) (void)hipFree(d);
+        return 2;
+    }
+    (void)hipFree(d);
+    return (int)v;
+}
+
 int mmba_plan_create_sharded(mmba_context *ctx, const mmba_problem *prob,
                              const mmba_options *opt, mmba_comm *comm, mmba_plan **out) {
     if (!ctx || !prob || !opt || !out) return MMBA_ERR_INVALID;
     *out = nullptr;
-    mmba_plan *p = new mmba_plan();
-    int rc = [&]() -> int {
-        MMBA_GUARD({
-            MMBA_HIP(hipSetDevice(ctx->device));
-            p->impl.ctx = ctx;
-            p->impl.comm = reinterpret_cast<Comm *>(comm);
-            p->impl.build(prob, opt);
+    Comm *c = reinterpret_cast<Comm *>(comm);
+    auto make = [&](bool replicate, mmba_plan **pp) -> int {
+        mmba_plan *p = new mmba_plan();
+        const int rc = [&]() -> int {
+            MMBA_GUARD({
+                MMBA_HIP(hipSetDevice(ctx->device));
+                p->impl.ctx = ctx;
+                p->impl.comm = c;
+                p->impl.replicated = replicate;
+                p->impl.build(prob, opt);
+                return MMBA_OK;
+            })
+        }();
+        if (rc != MMBA_OK) {
+            delete p;
+            return rc;
+        }
+        *pp = p;
+        return MMBA_OK;
+    };
+    mmba_plan *p = nullptr;
+    int rc = make(false, &p);
+    if (c && c->nranks > 1) {
+        const std::string why = rc == MMBA_OK ? std::string() : std::string(mmba_last_error());
+        const int st = agree_build_status(
+            ctx, c, rc == MMBA_OK ? 0 : rc == MMBA_ERR_UNSUPPORTED ? 1 : 2);
+        if (st == 0 && rc == MMBA_OK) {
+            *out = p;
             return MMBA_OK;
-        })
-    }();
-    if (rc != MMBA_OK) {
+        }
         delete p;
-        return rc;
+        p = nullptr;
+        if (st >= 2) {
+            if (rc == MMBA_OK) {
+                set_error("another shard failed to build its plan");
+                return MMBA_ERR_COMM;
+            }
+            set_error(why);
+            return rc;
+        }
+        rc = make(true, &p);  // deterministic: the same outcome on every shard
+        if (rc == MMBA_OK) p->impl.replicate_why = why.empty() ? "another shard's plan" : why;
     }
+    if (rc != MMBA_OK) return rc;
     *out = p;
     return MMBA_OK;
 }
@@ -289,7 +346,8 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         out->reduced_dim = p.nR;
         out->reduced_kind = p.band ? (p.bs.use_bd ? 3 : 0) : (p.dense ? 2 : 1);
         out->dataflow_fallback = p.bs.df_off ? 1 : 0;
-        out->solve_launch = p.coop_ok ? 1 : 0;
+        out->shards_replicated = p.replicated ? 1 : 0;
+        out->spec_replays = p.spec_replays;
         // Algorithmic bytes: B_J = 48 + 8 p_c p_b per observation
         // for the Jacobian + normal-equation pass, B_f = 48 per observation for
         // the residual pass.

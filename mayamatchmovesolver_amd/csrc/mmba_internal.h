@@ -136,33 +136,6 @@ struct BatchArgs {
     double delta, factor, ftol, xtol, gtol, initial_error_avg;
 };
 
-// Whole-solve cooperative launch for block-diagonal plans (mmba_lmcoop.hip).
-struct CoopOut {
-    double fnorm;
-    int info, nfev, njev, func_evals, jac_evals, ntrace, failed, aborted, nprobe, pad;
-};
-struct CoopArgs {
-    // workgroup g: observations [slice_off[g], slice_off[g + 1]) over the
-    // slice_ncf[g] camera-frames from slice_cf[g]; it owns camera-frames g,
-    // g + G, ...; cf_src[cf_src_off[cf] ..] = the slots (g * SLM + local
-    // camera-frame) holding camera-frame cf's normal-equation partials
-    const int *slice_off, *slice_cf, *slice_ncf, *cf_src_off, *cf_src;
-    double *nep;         // [G * SLM][KJC] normal-equation partials
-    double *xs;          // [n] damped step (owners -> slices)
-    const int *stale;    // stale FD column per frame (B13)
-    const double *pweight;
-    double *x;           // internal parameters, in / out
-    double *f, *ft, *eu, *ed, *dist, *distt, *J;
-    double *part;        // [2][G][8] grid-reduction partials
-    unsigned *ctr, *abort;
-    double *trace;
-    int trace_cap;
-    CoopOut *out;
-    long long *probe;    // MMBA_COOP_DEBUG: workgroup 0's wall clock at phase ends (64)
-    int solver_type, mode, maxfev;
-    int pad;
-    double delta, factor, ftol, xtol, gtol;
-};
 // The MINPACK decision after a trial point, restated on the device (the
 // last k_reduce_multi block, one thread) so that the next Jacobian can be
 // enqueued before the host has read the trial: *gate = 1 exactly when the

@@ -74,19 +74,6 @@ void launch_dist_stats(hipStream_t s, const DevProblem &P, const double *ed, dou
                        int nparts, int rstride, double *out);
 // launch_residual (partials only) plus ||J p||^2 partials of the same blocks
 // into partial_jp (k_jp_sumsq's sum, one launch)
-// Whole-solve cooperative launch for block-diagonal plans (mmba_lmcoop.hip;
-// CoopArgs / CoopOut in mmba_internal.h).
-struct CoopLayout {
-    int G = 0;
-    std::vector<int> slice_off, slice_cf, slice_ncf, cf_src_off, cf_src;
-};
-bool lm_coop_layout(int ncf, const std::vector<int> &cf_obs_off, int gmax, CoopLayout &L);
-int lm_coop_max_grid(bool lens);
-int lm_coop_nfc();
-int lm_coop_slots();
-int lm_coop_kj();
-bool launch_lm_coop(hipStream_t s, const DevProblem &P, const CoopArgs &A, int G, bool lens);
-
 // Reduction launch folded into a producer (unsharded trial point): the
 // producer's last workgroup (ticket) runs k_reduce_multi's work -- the rows
 // of spec (offsets into partial), the fail flag and the host mirror.

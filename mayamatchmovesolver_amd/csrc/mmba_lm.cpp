@@ -1033,8 +1033,42 @@ void Plan::jac_partial_stale(const double *dx, int k) {
                             s));
 }
 
+// The solve; a speculative Jacobian that the host's decision does not take
+// (SpecMismatch: the device's restatement of the lmder decision disagreed
+// with the host's, which the kernels are written never to do) is not an
+// error: the solve is replayed from x0 with the Jacobian enqueued only after
+// the host's decisions (same kernels, same bits as an unspeculated solve;
+// no callback can have run, pre_jac_ok requires none) and the event is
+// counted in mmba_kernel_stats.spec_replays.
 int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
                 mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {
+    try {
+        return solve_once(x_inout, fvec_out, eu_out, ed_out, res, cb, trace);
+    } catch (const SpecMismatch &) {
+        MMBA_HIP(hipStreamSynchronize(s));
+        ++spec_replays;
+        pre_jac_pending = false;
+        seq_pending = false;
+        mirror_pending = false;
+        slots_staged = false;
+        params_at = nullptr;
+        recs_full_at = nullptr;
+        const bool keep = pre_jac;
+        pre_jac = false;
+        int rc;
+        try {
+            rc = solve_once(x_inout, fvec_out, eu_out, ed_out, res, cb, trace);
+        } catch (...) {
+            pre_jac = keep;
+            throw;
+        }
+        pre_jac = keep;
+        return rc;
+    }
+}
+
+int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
+                     mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {
     const double t_start = wall_now();
     t_func = t_jac = t_linear = 0.;
     cbk = cb;
@@ -1054,10 +1088,10 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         if (!pre_jac_pending) return;
         const bool go_dev = h_scalar[SL_DGO] != 0.;
         if (go_dev && !go_host) {
+            // the Jacobian ran ahead at a trial point the host rejects (its
+            // epilogue moved diag): replay the solve without speculation
             pre_jac_pending = false;
-            set_error("device and host decisions differ after a trial point (device ratio " +
-                      std::to_string(h_scalar[SL_DRATIO]) + ")");
-            throw DeviceError();
+            throw SpecMismatch{};
         }
         // !go_dev: the gated launch did nothing (jac() launches it itself)
         if (!go_dev || !go_host) pre_jac_pending = false;
@@ -1123,87 +1157,6 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         interrupted = true;
         info = -1;
         goto TERMINATE;
-    }
-    // block-diagonal plans: the whole solve as one cooperative launch (no
-    // host decision point per iteration); callbacks keep the host loop
-    if (coop_ok && !central && !polls && !(cb && cb->progress)) {
-        if (!measured) records_enqueue(nullptr, 1);  // bundle positions at the scene's values
-        CoopArgs A{};
-        A.slice_off = d_coop_slice_off;
-        A.slice_cf = d_coop_slice_cf;
-        A.slice_ncf = d_coop_slice_ncf;
-        A.cf_src_off = d_coop_src_off;
-        A.cf_src = d_coop_src;
-        A.nep = d_coop_nep;
-        A.xs = d_coop_xs;
-        A.stale = d_stale;
-        A.pweight = d_pweight;
-        A.x = d_x;
-        A.f = d_f;
-        A.ft = d_ftrial;
-        A.eu = d_eu;
-        A.ed = d_ed;
-        A.dist = d_dist_x;
-        A.distt = d_dist_t;
-        A.J = d_J;
-        A.part = d_coop_part;
-        A.ctr = d_coop_sync;
-        A.abort = d_coop_sync + 1;
-        A.trace = d_coop_trace;
-        A.trace_cap = COOP_TRACE;
-        A.out = d_coop_out;
-        static const bool coop_dbg = std::getenv("MMBA_COOP_DEBUG") != nullptr;
-        A.probe = coop_dbg ? reinterpret_cast<long long *>(d_coop_trace + COOP_TRACE - 64) : nullptr;
-        A.solver_type = opt.solver_type;
-        A.mode = mode;
-        A.maxfev = maxfev;
-        A.delta = opt.delta;
-        A.factor = factor;
-        A.ftol = ftol;
-        A.xtol = xtol;
-        A.gtol = gtol;
-        MMBA_HIP(hipMemsetAsync(d_coop_sync, 0, 2 * sizeof(unsigned), s));
-        const double t0 = wall_now();
-        if (launch_lm_coop(s, P, A, coop_G, coop_lens)) {
-            MMBA_HIP(hipMemcpyAsync(h_coop_out, d_coop_out, sizeof(CoopOut), hipMemcpyDeviceToHost,
-                                    s));
-            MMBA_HIP(hipStreamSynchronize(s));
-            const CoopOut o = *h_coop_out;
-            t_jac += wall_now() - t0;
-            if (o.aborted) {
-                set_error("cooperative solve: a grid reduction timed out");
-                throw DeviceError();
-            }
-            if (o.failed) {
-                set_error("damped normal-equation factorisation failed (cooperative solve)");
-                throw DeviceError();
-            }
-            if (A.probe) {  // phase ends of workgroup 0 (100 MHz ticks)
-                std::vector<long long> pr(64);
-                MMBA_HIP(hipMemcpy(pr.data(), A.probe, sizeof(long long) * 64,
-                                   hipMemcpyDeviceToHost));
-                std::fprintf(stderr, "[mmba coop] %d phases (us):", o.nprobe);
-                for (int k = 1; k < std::min(o.nprobe, 64); ++k)
-                    std::fprintf(stderr, " %.1f", (pr[k] - pr[k - 1]) / 100.);
-                std::fprintf(stderr, "\n");
-            }
-            if (trace && o.ntrace > 0) {
-                std::vector<double> tr(std::min(o.ntrace, COOP_TRACE));
-                MMBA_HIP(hipMemcpy(tr.data(), d_coop_trace, sizeof(double) * tr.size(),
-                                   hipMemcpyDeviceToHost));
-                for (int k = 0; k < o.ntrace; ++k) push_trace(k < (int)tr.size() ? tr[k] : 0.);
-            }
-            info = o.info;
-            nfev = o.nfev;
-            njev = o.njev;
-            func_evals = o.func_evals;
-            jac_evals = o.jac_evals;
-            fnorm = o.fnorm;
-            dist_ok = true;
-            x0_eval = true;
-            goto TERMINATE;
-        }
-        coop_ok = false;  // not co-resident on this device: the host loop from now on
     }
     // x0's evaluation, enqueued: its ||f|| reaches the host with the first
     // decision point's slots, and the first Jacobian's gnorm reads it on the

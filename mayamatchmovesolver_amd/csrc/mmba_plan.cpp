@@ -82,7 +82,6 @@ Plan::~Plan() {
     if (h_fail) (void)hipHostFree(h_fail);
     if (h_bflag) (void)hipHostFree(h_bflag);
     if (h_xstage) (void)hipHostFree(h_xstage);
-    if (h_coop_out) (void)hipHostFree(h_coop_out);
     if (h_seq) (void)hipHostFree(h_seq);
 }
 
@@ -133,8 +132,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     M = Mg;  // local observations: all of them unless sharded (below)
     n = pr->num_params;
     m = 2 * M + nrows;
-    rank = comm ? comm->rank : 0;
-    nranks = comm ? comm->nranks : 1;
+    rank = comm && !replicated ? comm->rank : 0;
+    nranks = comm && !replicated ? comm->nranks : 1;
     require(F > 0 && M > 0 && n > 0, "empty problem");
     require(n <= m, "more parameters than errors (adjust_base.cpp:864)");
     require(opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER ||
@@ -1420,43 +1419,6 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     if (const char *e = std::getenv("MMBA_K2_FUSED")) k2_split = std::atoi(e) == 0;
     if (const char *e = std::getenv("MMBA_NE_FOLD")) fold_ok = std::atoi(e) != 0;
     if (const char *e = std::getenv("MMBA_TAIL_REDUCE")) tail_reduce = std::atoi(e) != 0;
-    {
-        // the cooperative whole-solve launch (mmba_lmcoop.hip): every
-        // parameter is a camera-frame parameter of its own block, no
-        // bundle-side variants, blocks of <= 8 parameters, <= 4 camera-frames
-        // per workgroup on <= 256 workgroups
-        bool ok = nG == 0 && nB_solved == 0 && nrows == 0 && !rs_on && nranks == 1 && n > 0 &&
-                  n == nCF;
-        for (int p = 0; p < n && ok; ++p) ok = p_class[p] == PC_CF;
-        for (size_t t = 0; t < cf_var_flags.size() && ok; ++t) ok = cf_var_flags[t] == 0;
-        for (int cf = 0; cf < ncf && ok; ++cf)
-            ok = cf_var_off[cf + 1] - cf_var_off[cf] - 1 == cf_pc[cf] && cf_pc[cf] <= lm_coop_nfc();
-        CoopLayout L;
-        const int gmax = ok ? lm_coop_max_grid(D.no_lens == 0) : 0;
-        if (ok) ok = gmax > 0 && lm_coop_layout(ncf, cf_obs_off, gmax, L);
-        // opt-in while the one-workgroup-per-camera-frame layout is slower
-        // than the host loop on C2 (1.38 vs ~0.8 ms per solve: 120
-        // workgroups of 1,656 observations each leave half the chip idle)
-        const char *e = std::getenv("MMBA_LM_COOP");
-        ok = ok && e && std::atoi(e) != 0;
-        if (ok) {
-            coop_ok = true;
-            coop_G = L.G;
-            coop_lens = D.no_lens == 0;
-            d_coop_slice_off = upload(L.slice_off);
-            d_coop_slice_cf = upload(L.slice_cf);
-            d_coop_slice_ncf = upload(L.slice_ncf);
-            d_coop_src_off = upload(L.cf_src_off);
-            d_coop_src = upload(L.cf_src.empty() ? std::vector<int>(1, 0) : L.cf_src);
-            d_coop_nep = dalloc<double>((size_t)coop_G * lm_coop_slots() * lm_coop_kj());
-            d_coop_xs = dalloc<double>(std::max(n, 1));
-            d_coop_part = dalloc<double>((size_t)2 * coop_G * 8);
-            d_coop_trace = dalloc<double>(COOP_TRACE);
-            d_coop_sync = dalloc<unsigned>(2);
-            d_coop_out = dalloc<CoopOut>(1);
-            MMBA_HIP(hipHostMalloc(&h_coop_out, sizeof(CoopOut)));
-        }
-    }
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
     MMBA_HIP(hipHostMalloc(&h_xstage, sizeof(double) * std::max(n, 1)));
     MMBA_HIP(hipStreamSynchronize(s));

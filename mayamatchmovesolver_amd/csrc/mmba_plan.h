@@ -30,6 +30,7 @@ void set_error(const std::string &msg);
     } while (0)
 
 struct DeviceError {};
+struct SpecMismatch {};  // a Jacobian enqueued ahead of a decision the host did not take
 struct Unsupported {
     std::string what;
 };
@@ -104,25 +105,12 @@ struct Plan {
     // +7 us): 782 / 196 arrivals on one device-scope counter cost more than
     // the launch they save (MI355X guide "fanin", ~12 ns per atomic)
     bool tail_reduce = false;
-    // block-diagonal plans (every parameter on one camera-frame, no solved
-    // bundle, no global): the whole solve as one cooperative launch
-    // (mmba_lmcoop.hip); MMBA_LM_COOP=0 keeps the host-driven loop
     // page-locked sequence word of the mirrored reductions (read_slots
     // polls it, MMBA_SEQ_POLL=0: stream events)
     unsigned *h_seq = nullptr;
     unsigned seq_next = 0;
     bool seq_pending = false;  // the next mirrored read_slots polls h_seq
     bool seq_poll = true;  // MMBA_SEQ_POLL=0: stream events
-    bool coop_ok = false;
-    int coop_G = 0;
-    bool coop_lens = false;
-    int *d_coop_slice_off = nullptr, *d_coop_slice_cf = nullptr, *d_coop_slice_ncf = nullptr;
-    int *d_coop_src_off = nullptr, *d_coop_src = nullptr;
-    double *d_coop_part = nullptr, *d_coop_trace = nullptr, *d_coop_nep = nullptr;
-    double *d_coop_xs = nullptr;
-    unsigned *d_coop_sync = nullptr;
-    CoopOut *d_coop_out = nullptr, *h_coop_out = nullptr;
-    static constexpr int COOP_TRACE = 4096;
     int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
@@ -254,6 +242,10 @@ struct Plan {
 
     // multi-GPU
     Comm *comm = nullptr;
+    // a sharded plan whose problem does not shard (mmba_plan_create_sharded):
+    // every shard solves the whole problem, no collectives
+    bool replicated = false;
+    std::string replicate_why;
 
     ~Plan();
 
@@ -435,6 +427,9 @@ struct Plan {
     double dnorm(const double *dv);
     int solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
               mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace);
+    int solve_once(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
+                   mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace);
+    int spec_replays = 0;  // solves replayed after a speculative Jacobian the host did not take
     // Per-frame solve mode in one launch (mmba_batch.hip), valid when every
     // parameter is a camera-frame parameter (no static parameter chains the
     // frames); frames [0, batch_nf) are solvable, batch_nfmax = most

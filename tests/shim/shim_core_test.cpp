@@ -12,6 +12,10 @@
 //      classic lens on camera.inLens (distortion solved) layered over a
 //      static radial lens, and a rolling
 //      shutter: keyed attributes, lens slots, rows of several frames
+//   3  scene 2 without the rolling shutter, its input radial lens animated
+//      (degree-2 / degree-4 distortion keyed per frame) and the current time
+//      at solve frame 2: the input layer holds its frame-2 values for the
+//      whole solve (maya_lens_model_utils.cpp:433-446)
 //
 // Built twice (tests/shim/Makefile): as an executable (main: every scene
 // through mmba_shim::solve; without a gfx950 device the core must report the
@@ -147,11 +151,13 @@ std::unique_ptr<Scene> make_scene(int which) {
         in.paramToAttrList = {{0, -1}, {1, -1}};
         return sc;
     }
-    // scene 2: 4 frames, per-frame camera rotate solved, classic lens, rolling shutter
+    // scenes 2 / 3: 4 frames, per-frame camera rotate solved, classic lens
+    // over a radial one (scene 2: static, rolling shutter; scene 3: animated
+    // input layer, current time at frame 2)
     const int F = 4;
     rd.F = F;
     in.num_frames = F;
-    in.current_frame = 0;
+    in.current_frame = which == 3 ? 2 : 0;
     std::vector<double> tx(F), tz(F), rx(F), ry(F), rz(F);
     for (int f = 0; f < F; ++f) {
         tx[f] = 0.1 * f;
@@ -178,12 +184,17 @@ std::unique_ptr<Scene> make_scene(int which) {
     LensRead lens0;
     lens0.connected = true;
     lens0.node = "lens0";
-    lens0.model = 3;  // 3DE radial std deg 4, static
+    lens0.model = 3;  // 3DE radial std deg 4
     rd.nodes["lens0"] = lens0;
-    rd.stat("lens0.tdeRadialStdDeg4_degree2_distortion", 0.03);
+    if (which == 3) {
+        rd.anim("lens0.tdeRadialStdDeg4_degree2_distortion", {0.01, 0.02, 0.03, 0.05});
+        rd.anim("lens0.tdeRadialStdDeg4_degree4_distortion", {0.0, 0.004, 0.012, 0.02});
+    } else {
+        rd.stat("lens0.tdeRadialStdDeg4_degree2_distortion", 0.03);
+        rd.stat("lens0.tdeRadialStdDeg4_degree4_distortion", 0.008);
+    }
     rd.stat("lens0.tdeRadialStdDeg4_degree2_u", 0.002);
     rd.stat("lens0.tdeRadialStdDeg4_degree2_v", -0.001);
-    rd.stat("lens0.tdeRadialStdDeg4_degree4_distortion", 0.008);
     rd.stat("lens0.tdeRadialStdDeg4_degree4_u", 0.0);
     rd.stat("lens0.tdeRadialStdDeg4_degree4_v", 0.0);
     rd.stat("lens0.tdeRadialStdDeg4_cylindricDirection", 15.0);
@@ -217,15 +228,16 @@ std::unique_ptr<Scene> make_scene(int which) {
         }
     in.paramToAttrList.push_back({3, -1});
     sc->x0.push_back(0.02);
-    in.rolling_shutter = {0.5};
+    if (which == 2) in.rolling_shutter = {0.5};
     sc->so.iterMax = 100;
     return sc;
 }
 
-std::unique_ptr<Scene> g_scene[3];
+constexpr int kScenes = 4;
+std::unique_ptr<Scene> g_scene[kScenes];
 
 Scene *scene(int which) {
-    if (which < 0 || which > 2) return nullptr;
+    if (which < 0 || which >= kScenes) return nullptr;
     if (!g_scene[which]) {
         g_scene[which] = make_scene(which);
         Scene *sc = g_scene[which].get();
@@ -299,7 +311,7 @@ int shim_demo_cached_plans() { return (int)shim().cached_plans(); }
 int main() {
     int failures = 0;
     const bool device = mmba_device_count() > 0;
-    for (int which = 0; which < 3; ++which) {
+    for (int which = 0; which < kScenes; ++which) {
         Scene *sc = scene(which);
         if (!sc->flat.why.empty()) {
             std::printf("scene %d: not mapped: %s\n", which, sc->flat.why.c_str());
@@ -339,7 +351,7 @@ int main() {
     }
     if (device) {
         // a second solve of every scene re-uses the cached plans
-        for (int which = 0; which < 3; ++which) {
+        for (int which = 0; which < kScenes; ++which) {
             Scene *sc = scene(which);
             std::vector<double> x(sc->x0.size()), f(2 * sc->flat.obs_marker.size());
             int reason = 0, fe = 0;
@@ -348,7 +360,8 @@ int main() {
                 ++failures;
         }
         std::printf("cached plans: %d\n", shim_demo_cached_plans());
-        if (shim_demo_cached_plans() != 3) ++failures;
+        // the shim caches at most 4 plans (Shim::kMaxPlans)
+        if (shim_demo_cached_plans() != kScenes) ++failures;
     }
     shim().release();
     std::printf("%s\n", failures ? "FAILED" : "PASSED");

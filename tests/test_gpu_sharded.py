@@ -14,15 +14,19 @@ from mayamatchmovesolver_amd.solver import Comm, Context, Solver
 pytestmark = pytest.mark.gpu
 
 
-def run_sharded(prob, opt, n):
+def run_sharded(prob, opt, n, replicated=None):
+    """Solve on n in-process shards.  replicated (list): receives each shard's
+    shards_replicated statistic (1: the problem did not shard and every shard
+    solved all of it, mmba_plan_create_sharded)."""
     comms = Comm.local_group(n)
     ctxs = [Context(0) for _ in range(n)]
-    outs, errs = [None] * n, [None] * n
+    outs, errs, reps = [None] * n, [None] * n, [None] * n
 
     def work(r):
         try:
             s = Solver(prob, opt, context=ctxs[r], comm=comms[r])
             try:
+                reps[r] = s.kernel_stats()["shards_replicated"]
                 outs[r] = s.solve()
             finally:
                 s.close()
@@ -40,6 +44,8 @@ def run_sharded(prob, opt, n):
     for c in ctxs:
         c.close()
     assert errs == [None] * n, errs
+    if replicated is not None:
+        replicated[:] = reps
     return outs
 
 
@@ -243,3 +249,26 @@ def test_local_group_allreduce(n, order, monkeypatch):
     for s, m in outs:
         np.testing.assert_array_equal(s, ref)
         np.testing.assert_array_equal(m, np.max(np.stack(vals), axis=0))
+
+
+def test_unshardable_problem_replicated(gpu_ctx):
+    """A problem the frame partition cannot take (rolling shutter: the blend
+    couples every camera-frame with its neighbours across a shard boundary)
+    is solved whole on every shard, without collectives: the same bits as
+    the unsharded plan, on every shard (mmba_plan_create_sharded)."""
+    prob = S.make_config(4, frames=12, scale=0.05, rolling_shutter=0.5)
+    opt = S.config_options(prob, iterations=6)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        assert s.kernel_stats()["shards_replicated"] == 0
+        ref = s.solve()
+    finally:
+        s.close()
+    reps = []
+    outs = run_sharded(prob, opt, 2, replicated=reps)
+    assert reps == [1, 1]
+    for o in outs:
+        np.testing.assert_array_equal(o.x, ref.x)
+        np.testing.assert_array_equal(o.fvec, ref.fvec)
+        np.testing.assert_array_equal(o.fnorm_trace, ref.fnorm_trace)
+        assert o.result["iterations"] == ref.result["iterations"]

@@ -69,17 +69,30 @@ def test_wide_arrow_block_diagonal(kw, mode, oracle, gpu_ctx):
     check(prob, opt, oracle, gpu_ctx)
 
 
-@pytest.mark.parametrize("kw,n", [(dict(n_witness=5, n_focal=5), 2),
-                                  (dict(frames=5, n_witness=5, n_focal=5), 3)])
-def test_wide_arrow_sharded(kw, n, oracle):
+@pytest.mark.parametrize("kw,n,rep", [
+    # 12 frames, no solved bundle: half bandwidth 5, four or six camera-frames
+    # per shard -- the frames really shard (partitioned band + the 32-wide
+    # arrow all-reduced); the oracle's 1-ulp x envelope is 3.5e-9
+    (dict(frames=12, solve_bundles=False, n_witness=5, n_focal=5), 2, 0),
+    (dict(frames=12, solve_bundles=False, n_witness=5, n_focal=5), 3, 0),
+    # every frame coupled through the solved bundles (half bandwidth 35 / 29)
+    # over 6 / 5 frames: fewer than 2 w + 8 camera-frame rows per shard, so
+    # the problem does not shard and every shard solves all of it
+    (dict(n_witness=5, n_focal=5), 2, 1),
+    (dict(frames=5, n_witness=5, n_focal=5), 3, 1)])
+def test_wide_arrow_sharded(kw, n, rep, oracle):
     """Frame shards (in-process communicators): the global rows are
-    all-reduced like the narrow arrow's."""
+    all-reduced like the narrow arrow's; a problem too small to shard is
+    solved redundantly on every shard (mmba_plan_create_sharded), not refused."""
     prob = S.witness_scene(**kw)
     opt = make_options()
-    outs = run_sharded(prob, opt, n)
+    reps = []
+    outs = run_sharded(prob, opt, n, replicated=reps)
+    assert reps == [rep] * n
     check_shards_agree(outs)
     xr, _f, _eu, _ed, rr, trr = oracle.solve(prob, opt)
     o = outs[0]
+    assert o.result["reason_number"] == rr.reason_number
     assert o.result["iterations"] == rr.iterations
     np.testing.assert_allclose(o.fnorm_trace, trr, rtol=1e-6, atol=1e-9 * trr[0])
     xs = np.maximum(np.abs(xr), 1e-3)

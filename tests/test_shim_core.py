@@ -60,8 +60,12 @@ def python_scene(which):
     tfm, tids = b.transform(t=[0.1 * f, 1.0, -0.05 * f],
                             r=[1.0 + 0.5 * f, -2.0 + 0.3 * f, 0.2 * f])
     lens, lids = b.lens_3de_classic(distortion=0.02)
-    lens0, _ = b.lens_3de_radial_std_deg4(0.03, 0.002, -0.001, 0.008, 0.0, 0.0, 15.0, 0.02)
-    b.lens_input(lens, lens0)  # the classic lens layered over a static radial one
+    if which == 3:  # animated input layer, read at the current time (frame 2)
+        d2, d4 = np.array([0.01, 0.02, 0.03, 0.05]), np.array([0.0, 0.004, 0.012, 0.02])
+        lens0, _ = b.lens_3de_radial_std_deg4(d2, 0.002, -0.001, d4, 0.0, 0.0, 15.0, 0.02)
+    else:
+        lens0, _ = b.lens_3de_radial_std_deg4(0.03, 0.002, -0.001, 0.008, 0.0, 0.0, 15.0, 0.02)
+    b.lens_input(lens, lens0)  # the classic lens layered over a radial one
     cam, _ = b.camera(tfm, lens=lens)
     for k in range(5):
         bt, _ = b.transform(t=(-4.0 + 2.0 * k, 1.0 + 0.5 * k, -20.0 - 3.0 * k))
@@ -71,7 +75,12 @@ def python_scene(which):
         b.solve(a)
     b.solve(lids[0])
     prob = b.build()
-    prob.cam_rs_value = np.array([0.5])
+    if which == 2:
+        prob.cam_rs_value = np.array([0.5])
+    else:
+        liv = np.zeros((len(prob.lens_type), abi.LENS_NUM_ATTRS))
+        liv[lens0, :8] = [d2[2], 0.002, -0.001, d4[2], 0.0, 0.0, 15.0, 0.02]
+        prob.lens_input_values = liv.reshape(-1)
     return prob
 
 
@@ -95,7 +104,7 @@ def oracle_run(oracle, pstruct, opt, x0, m, M):
     return f, x, fv, tb[:tr.count].copy(), res
 
 
-@pytest.mark.parametrize("which", [0, 1, 2])
+@pytest.mark.parametrize("which", [0, 1, 2, 3])
 def test_shim_problem_equals_python_scene(which, shim, oracle):
     p, x0, opt = shim_problem(shim, which)
     q = python_scene(which)
@@ -106,6 +115,10 @@ def test_shim_problem_equals_python_scene(which, shim, oracle):
     qs, keep = q.to_ctypes()
     a = oracle_run(oracle, p, opt, x0, m, M)
     b = oracle_run(oracle, qs, opt, q.x0, m, M)
+    if which == 3:  # the input layer at frame 2, not at frame 0
+        r0 = q.lens_input_values.reshape(-1, abi.LENS_NUM_ATTRS)
+        lay = [l for l in range(len(q.lens_type)) if l in set(q.lens_input.tolist())]
+        assert len(lay) == 1 and r0[lay[0], 0] == 0.03
     np.testing.assert_array_equal(a[0], b[0])   # residuals at x0
     np.testing.assert_array_equal(a[1], b[1])   # solved x
     np.testing.assert_array_equal(a[3], b[3])   # ||f|| trace
@@ -132,7 +145,7 @@ def test_shim_executable(shim):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("which", [0, 1, 2])
+@pytest.mark.parametrize("which", [0, 1, 2, 3])
 def test_gpu_shim(which, shim, oracle):
     """mmba_shim::solve on the device, through the plan cache: x and ||f||
     against the oracle at 1e-6 (the north star's bar)."""
