@@ -47,6 +47,32 @@ def shim_problem(L, which):
     return p, x0, opt
 
 
+# markers of scenes 2 / 3 (marker-major, frame-minor): the forward model at a
+# true pose and lens (tests/shim/gen_scene2_markers.py)
+SCENE2_MARKERS = np.array([
+    (-0.23873034935799486, -0.050894781155829634),
+    (-0.23181865466579299, -0.06415868658293411),
+    (-0.22496889641796142, -0.048549320201375472),
+    (-0.21805635698669693, -0.026341277304751515),
+    (-0.12918474157362708, -0.021228432336373618),
+    (-0.12170790356735069, -0.033055281860840904),
+    (-0.11422490874317545, -0.018575519493559296),
+    (-0.10638882977015819, -8.9621906492073043e-05),
+    (-0.044956863564452644, 0.0016716474101909832),
+    (-0.03722012829822597, -0.0093059329867673009),
+    (-0.029069090752251482, 0.0046899590908291615),
+    (-0.020263446930858117, 0.020251735335200423),
+    (0.021639233221250404, 0.019727113220638085),
+    (0.029532659655347186, 0.0096641178880656296),
+    (0.038486605759479368, 0.023090849868926223),
+    (0.047876170004553104, 0.0363256114043954),
+    (0.075032417674294347, 0.034178340970243096),
+    (0.083717764827209482, 0.024882861684639553),
+    (0.092810152575285257, 0.038010888700753316),
+    (0.10297730975261896, 0.049418792306458313),
+])
+
+
 def python_scene(which):
     """The same scenes built by the Python SceneBuilder (attribute ids in its
     own order)."""
@@ -70,7 +96,7 @@ def python_scene(which):
     for k in range(5):
         bt, _ = b.transform(t=(-4.0 + 2.0 * k, 1.0 + 0.5 * k, -20.0 - 3.0 * k))
         b.bundle(bt)
-        b.marker(cam, k, np.stack([-0.3 + 0.15 * k + 0.01 * f, 0.2 - 0.1 * k + 0.005 * f], 1))
+        b.marker(cam, k, SCENE2_MARKERS[k * F:(k + 1) * F])
     for a in tids[3:6]:
         b.solve(a)
     b.solve(lids[0])
