@@ -70,7 +70,22 @@ def parse():
                     help="skip the larger CPU window once this much CPU time is spent")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC passes that fill roofline.traffic")
+    ap.add_argument("--path", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B diagnostics: pin a plan-builder choice through the "
+                         "mmba_debug_set_path test hook (e.g. pcr=0); the line records it")
     return ap.parse_args()
+
+
+def apply_paths(args):
+    """--path NAME=VALUE -> mmba_debug_set_path(abi.PATH_NAME, VALUE)."""
+    from mayamatchmovesolver_amd import abi
+    from mayamatchmovesolver_amd.solver import set_path
+    pinned = {}
+    for item in args.path:
+        name, val = item.split("=")
+        set_path(getattr(abi, "PATH_" + name.upper()), int(val))
+        pinned[name.lower()] = int(val)
+    return pinned
 
 
 def dist_setup():
@@ -134,6 +149,8 @@ def pmc_traffic(args):
         base += ["--frames", str(args.frames)]
     if args.config == 4:
         base += ["--lens-model", args.lens_model, "--rolling-shutter", str(args.rolling_shutter)]
+    for item in args.path:
+        base += ["--path", item]
     env = dict(os.environ, TMPDIR="/tmp")
     per = {}
     tmp = tempfile.mkdtemp(prefix="mmba_pmc_", dir="/tmp")
@@ -334,6 +351,7 @@ def main():
         traffic, traffic_detail = pmc_traffic(args)
     from mayamatchmovesolver_amd import synthetic as S
     from mayamatchmovesolver_amd.solver import Comm, Context, Solver, comm_unique_id
+    pinned = apply_paths(args)
 
     frames = args.frames
     scale = args.scale
@@ -474,7 +492,8 @@ def main():
                        "parameters": prob.num_params, "residuals": prob.num_residuals,
                        "parallelism": "frame-sharded x%d (RCCL)" % world if world > 1
                        else "single",
-                       "solver": "lmder fwd-FD delta=1e-4 tau=1 tol=1e-6"},
+                       "solver": "lmder fwd-FD delta=1e-4 tau=1 tol=1e-6",
+                       **({"pinned_paths": pinned} if pinned else {})},
             "lm_iterations_per_s": lm_rate,
             "final_rms_px": r["error_rms"],
             "d2h_bytes_per_step": 8.0 * (2 * prob.num_residuals + prob.num_obs),

@@ -536,6 +536,24 @@ typedef struct mmba_kernel_stats {
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);
 
+/* Test hook (not part of the solver seam): pin a choice the plan builder
+ * otherwise makes itself, for the plans (and in-process communicators)
+ * this process creates afterwards; value -1 restores the builder's choice.
+ * The seam's caller never needs it: the GPU tests use it to run every
+ * solver path (it replaces the MMBA_* environment switches of ABI <= 5).
+ * Returns MMBA_ERR_INVALID for an unknown key. */
+#define MMBA_PATH_PCR 1            /* 0: block cyclic reduction instead of parallel cyclic
+                                      reduction for band systems without an arrow */
+#define MMBA_PATH_SHARD_BCR 2      /* 0: sharded plans factor with the partitioned band chain */
+#define MMBA_PATH_BCR_DATAFLOW 3   /* 0: block cyclic reduction in per-level launches */
+#define MMBA_PATH_BCR_GRID 4       /* n: the dataflow launches on at most n workgroups */
+#define MMBA_PATH_DENSE 5          /* 1: dense reduced solve, 0: tiled sparse Cholesky */
+#define MMBA_PATH_PERFRAME_BATCH 6 /* 0: per-frame mode with one plan per frame */
+#define MMBA_PATH_LOCAL_RING 7     /* 1: in-process communicators sum in ring order */
+#define MMBA_PATH_PROBE 8          /* 1: band / BCR phase probe, printed when the plan is destroyed */
+#define MMBA_PATH_NUM 9
+int mmba_debug_set_path(int key, int value);
+
 /* Test hook (not part of the solver seam): solve S x = r with the device
  * band + arrow Cholesky for a dense symmetric positive-definite S of order
  * nb + nG whose leading nb x nb block has half bandwidth w and whose last nG

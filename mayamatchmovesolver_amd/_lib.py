@@ -90,6 +90,8 @@ def lib():
                                  C.POINTER(abi.MmbaOptions), dp, dp, dp, dp,
                                  C.POINTER(abi.MmbaResult), C.POINTER(abi.MmbaCallbacks),
                                  C.POINTER(abi.MmbaTrace)]
+        L.mmba_debug_set_path.restype = C.c_int
+        L.mmba_debug_set_path.argtypes = [C.c_int, C.c_int]
         L.mmba_debug_band_solve.restype = C.c_int
         L.mmba_debug_band_solve.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, dp, dp,
                                             dp, dp, C.POINTER(C.c_int)]

@@ -24,6 +24,17 @@ ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
 ABI_VERSION = 6
 
+# mmba_debug_set_path keys (test hook: pin a plan-builder choice)
+PATH_PCR = 1
+PATH_SHARD_BCR = 2
+PATH_BCR_DATAFLOW = 3
+PATH_BCR_GRID = 4
+PATH_DENSE = 5
+PATH_PERFRAME_BATCH = 6
+PATH_LOCAL_RING = 7
+PATH_PROBE = 8
+PATH_NUM = 9
+
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
 FILM_FIT_VERTICAL = 2
@@ -240,6 +251,7 @@ EXPORTED_SYMBOLS = [
     "mmba_plan_outputs",
     "mmba_solve",
     "mmba_plan_kernel_stats",
+    "mmba_debug_set_path",
     "mmba_debug_band_solve",
     "mmba_debug_comm_allreduce",
     "mmba_debug_dgemm",

@@ -4,6 +4,7 @@
 // failure with a message retrievable through mmba_last_error(); the MINPACK
 // info code goes to mmba_result::reason_number exactly as cminpack returns it
 // (adjust_cminpack_base.h:51-83).
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -16,6 +17,12 @@
 namespace mmba {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
+
+static_assert(MMBA_PATH_NUM == 9, "one initialiser per path key");
+static std::atomic<int> g_path[MMBA_PATH_NUM] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+int path_choice(int key) {
+    return (key > 0 && key < MMBA_PATH_NUM) ? g_path[key].load() : -1;
+}
 }  // namespace mmba
 
 using namespace mmba;
@@ -41,6 +48,12 @@ using namespace mmba;
 extern "C" {
 
 int mmba_abi_version(void) { return MMBA_ABI_VERSION; }
+
+int mmba_debug_set_path(int key, int value) {
+    if (key <= 0 || key >= MMBA_PATH_NUM) return MMBA_ERR_INVALID;
+    g_path[key].store(value < 0 ? -1 : value);
+    return MMBA_OK;
+}
 
 int mmba_shard_layout(int32_t num_frames, int32_t num_obs, const int32_t *obs_frame,
                       const int32_t *obs_bundle, int32_t num_bundles, int32_t nranks,
@@ -459,24 +472,38 @@ int mmba_debug_band_solve(mmba_context *ctx, int nb, int w, int nG, int P, const
         int *dfail = p.dalloc<int>(1);
         MMBA_HIP(hipMemsetAsync(dfail, 0, sizeof(int), p.s));
         MMBA_HIP(hipMemcpyAsync(dr, r, (size_t)n * 8, hipMemcpyHostToDevice, p.s));
-        // x through the fused factor + forward path; ||L^-1 r||^2 through the
-        // standalone forward solve (the lmpar Newton-term path)
-        band_factor_forward(p.s, p.bs, dfail, nullptr, dr, dy);
-        band_backward(p.s, p.bs, dy, dx);
-        double *dy2 = p.dalloc<double>(n);
-        band_forward(p.s, p.bs, dr, dy2);
         std::vector<double> hy(n);
         int fail = 0;
+        if (p.bs.use_pcr) {
+            // parallel cyclic reduction: x in one launch; r^T S^-1 r through
+            // the right-hand-side pass (the lmpar Newton-term path)
+            pcr_solve(p.s, p.bs.pcr, dr, dx, nullptr, dfail);
+            const int *ones = p.upload(std::vector<int>(std::max(n, 1), 1));
+            pcr_rhs_dot(p.s, p.bs.pcr, dr, ones, dfail);
+            hy.assign(p.bs.pcr.nblk, 0.);
+            MMBA_HIP(hipMemcpyAsync(hy.data(), p.bs.pcr.part, sizeof(double) * hy.size(),
+                                    hipMemcpyDeviceToHost, p.s));
+        } else {
+            // x through the fused factor + forward path; ||L^-1 r||^2 through
+            // the standalone forward solve (the lmpar Newton-term path)
+            band_factor_forward(p.s, p.bs, dfail, nullptr, dr, dy);
+            band_backward(p.s, p.bs, dy, dx);
+            double *dy2 = p.dalloc<double>(n);
+            band_forward(p.s, p.bs, dr, dy2);
+            MMBA_HIP(hipMemcpyAsync(hy.data(), dy2, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
+        }
         MMBA_HIP(hipMemcpyAsync(x, dx, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
-        MMBA_HIP(hipMemcpyAsync(hy.data(), dy2, (size_t)n * 8, hipMemcpyDeviceToHost, p.s));
         MMBA_HIP(hipMemcpyAsync(&fail, dfail, sizeof(int), hipMemcpyDeviceToHost, p.s));
         MMBA_HIP(hipStreamSynchronize(p.s));
         if (ynorm2) {
             double acc = 0.;
-            for (double v : hy) acc += v * v;
+            if (p.bs.use_pcr)
+                for (double v : hy) acc += v;
+            else
+                for (double v : hy) acc += v * v;
             *ynorm2 = acc;
         }
-        if (parts_used) *parts_used = p.bs.P;
+        if (parts_used) *parts_used = p.bs.use_pcr ? -2 : p.bs.P;
         if (fail) {
             set_error("band factorisation: non-positive pivot");
             return MMBA_ERR_INVALID;

@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256)
     __shared__ double sPG[NAMAX][NB + 1];
     __shared__ double sZ[NAMAX * (NAMAX + 1) / 2];
     __shared__ int bad;
-    // probe (diagnostic, MMBA_PROBE=1): thread 0 of workgroup 0 accumulates
+    // probe (diagnostic, MMBA_PATH_PROBE = 1): thread 0 of workgroup 0 accumulates
     // s_memtime cycles per phase; never read by the solver.
     const bool prb = probe && blockIdx.x == 0 && threadIdx.x == 0;
     long long pt[4] = {0, 0, 0, 0}, tprev = prb ? (long long)clock64() : 0;
@@ -610,11 +610,7 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
 
 void band_factor_forward(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
                          const double *r, double *y) {
-    static const bool fused = [] {
-        const char *e = std::getenv("MMBA_BCR_FUSED");
-        return !(e && std::atoi(e) == 0);
-    }();
-    if (B.use_bcr && fused) {
+    if (B.use_bcr) {
         bcr_factor(s, B, fail, probe, r, y);
         return;
     }

@@ -5,8 +5,8 @@
 //   LocalComm  N shards driven by N host threads in one process (tests on a
 //              one-GPU box run the sharded code path against the unsharded
 //              one): every shard sums all shards' buffers in rank order, so
-//              all shards get bitwise identical results; MMBA_LOCAL_RING=1 at
-//              creation sums in ring order instead -- the order of a ring
+//              all shards get bitwise identical results; MMBA_PATH_LOCAL_RING
+//              = 1 at creation (mmba_debug_set_path) sums in ring order instead -- the order of a ring
 //              reduce-scatter (RCCL's ring all-reduce): the buffer is cut into
 //              N chunks and chunk c is accumulated starting at rank c + 1 and
 //              ending at rank c (mod N), so the sharded tests also see a
@@ -156,7 +156,7 @@ int mmba_comm_create_local(int nranks, mmba_comm **out) {
     if (!out || nranks < 1 || nranks > LOCAL_MAX) return MMBA_ERR_INVALID;
     auto g = std::make_shared<LocalGroup>();
     g->n = nranks;
-    if (const char *e = std::getenv("MMBA_LOCAL_RING")) g->ring = std::atoi(e) != 0;
+    g->ring = path_choice(MMBA_PATH_LOCAL_RING) > 0;
     for (int r = 0; r < nranks; ++r) {
         auto *c = new LocalComm();
         c->rank = r;

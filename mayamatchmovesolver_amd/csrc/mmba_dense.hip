@@ -12,8 +12,8 @@
 //             in-block trailing columns                 k_dgemm_nt<TRI> / k_dgemm_nt
 //   block:    A_22 -= L_21 L_21^T (rank 512)            k_dgemm_nt<TRI> (fp64 MFMA)
 //
-// k_dgemm_nt is the hand-written fp64 MFMA GEMM/SYRK of mmba_gemm.hip;
-// MMBA_DENSE_HAND=0 runs the same steps through rocBLAS (A/B).
+// k_dgemm_nt is the hand-written fp64 MFMA GEMM/SYRK of mmba_gemm.hip (it
+// replaced rocBLAS dgemm / dsyrk, which ran the same steps up to round 3).
 //
 // The right-hand side rides along as row n of A (A[n, j] = r_j): the panel
 // GEMMs and trailing updates that produce L also produce row n of the
@@ -24,7 +24,6 @@
 // stored Linv_kk, computed by every workgroup, then the workgroup's slice of
 // the update of the rest).  The flops are those of a dense Cholesky, n^3/3,
 // in fp64 MFMA GEMMs; the panel factorisation is the latency-bound part.
-#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -189,36 +188,11 @@ __global__ void __launch_bounds__(256) k_dense_bwd_step(const double *__restrict
     }
 }
 
-#define MMBA_RB(call)                                                                    \
-    do {                                                                                 \
-        rocblas_status st_ = (call);                                                     \
-        if (st_ != rocblas_status_success) {                                             \
-            ::mmba::set_error(std::string(#call) + ": " + rocblas_status_to_string(st_)); \
-            throw ::mmba::DeviceError();                                                 \
-        }                                                                                \
-    } while (0)
-
-DenseSolver::~DenseSolver() {
-    if (handle) (void)rocblas_destroy_handle((rocblas_handle)handle);
-}
-
-void DenseSolver::init(hipStream_t s) {
-    if (!handle) {
-        rocblas_handle h = nullptr;
-        MMBA_RB(rocblas_create_handle(&h));
-        handle = h;
-    }
-    MMBA_RB(rocblas_set_stream((rocblas_handle)handle, s));
-    MMBA_RB(rocblas_set_pointer_mode((rocblas_handle)handle, rocblas_pointer_mode_host));
-    const char *e = std::getenv("MMBA_DENSE_HAND");
-    hand = !(e && std::atoi(e) == 0);
-}
+void DenseSolver::init(hipStream_t) {}
 
 // Panels of the block of columns [k0, k0 + nb); rows below the diagonal run
 // to `end` (exclusive; includes the right-hand-side row).
 void DenseSolver::block(hipStream_t s, double *A, int ld, int k0, int nb, int end, int *fail) {
-    rocblas_handle h = (rocblas_handle)handle;
-    const double one = 1.0, mone = -1.0, zero = 0.0;
     for (int p = k0; p < k0 + nb; p += 64) {
         double *App = A + (size_t)p * ld + p;
         double *Li = Linv + (size_t)(p / 64) * 64 * 64;
@@ -226,33 +200,17 @@ void DenseSolver::block(hipStream_t s, double *A, int ld, int k0, int nb, int en
         const int m = end - (p + 64);
         if (m <= 0) continue;
         double *Aip = App + 64;
-        // L_ip = A_ip Linv^T.  k_dgemm_nt works in place (each workgroup
-        // reads its own 128 rows of A_ip in full before it writes them, and
-        // no other workgroup reads them); rocBLAS goes out of place
-        if (hand) {
-            launch_dgemm_nt(s, false, m, 64, 64, Aip, ld, Li, 64, Aip, ld, 1., 0.);
-        } else {
-            MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose, m, 64,
-                                  64, &one, Aip, ld, Li, 64, &zero, ws, m));
-            MMBA_HIP(hipMemcpy2DAsync(Aip, sizeof(double) * ld, ws, sizeof(double) * m,
-                                      sizeof(double) * m, 64, hipMemcpyDeviceToDevice, s));
-        }
+        // L_ip = A_ip Linv^T, in place (each workgroup of k_dgemm_nt reads its
+        // own 128 rows of A_ip in full before it writes them, and no other
+        // workgroup reads them)
+        launch_dgemm_nt(s, false, m, 64, 64, Aip, ld, Li, 64, Aip, ld, 1., 0.);
         // the rest of this block's columns [p + 64, k0 + nb)
         const int mb = k0 + nb - (p + 64);
         if (mb > 0) {
             double *Aqq = A + (size_t)(p + 64) * ld + (p + 64);
             const int mr = end - (k0 + nb);
-            if (hand) {
-                launch_dgemm_nt(s, true, mb, mb, 64, Aip, ld, Aip, ld, Aqq, ld, -1., 1.);
-                launch_dgemm_nt(s, false, mr, mb, 64, Aip + mb, ld, Aip, ld, Aqq + mb, ld, -1., 1.);
-            } else {
-                MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, mb, 64,
-                                      &mone, Aip, ld, &one, Aqq, ld));
-                if (mr > 0)
-                    MMBA_RB(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_transpose,
-                                          mr, mb, 64, &mone, Aip + mb, ld, Aip, ld, &one,
-                                          Aqq + mb, ld));
-            }
+            launch_dgemm_nt(s, true, mb, mb, 64, Aip, ld, Aip, ld, Aqq, ld, -1., 1.);
+            launch_dgemm_nt(s, false, mr, mb, 64, Aip + mb, ld, Aip, ld, Aqq + mb, ld, -1., 1.);
         }
     }
 }
@@ -266,17 +224,13 @@ void DenseSolver::setup(Plan &pl, int n) {
 }
 
 void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int *fail) {
-    init(s);
-    rocblas_handle h = (rocblas_handle)handle;
-    const double one = 1.0, mone = -1.0;
     k_dense_row_put<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, r);
     const int end = n + 1;  // rows 0..n-1 and the right-hand-side row n
-    // block width of the trailing updates (MMBA_DENSE_NB, a multiple of 64):
-    // 512 measured 229.6 ms per C3 factorisation with k_dgemm_nt (39.3 TF/s,
-    // 50 % of the fp64 MFMA peak) against 251.6 ms at 256 -- half as many
-    // read-modify-write passes over the trailing matrix
-    int NB = 512;
-    if (const char *e = std::getenv("MMBA_DENSE_NB")) NB = std::max(64, std::atoi(e) / 64 * 64);
+    // block width of the trailing updates: 512 measured 229.6 ms per C3
+    // factorisation with k_dgemm_nt (39.3 TF/s, 50 % of the fp64 MFMA peak)
+    // against 251.6 ms at 256 -- half as many read-modify-write passes over
+    // the trailing matrix
+    constexpr int NB = 512;
     for (int k0 = 0; k0 < n; k0 += NB) {
         const int nb = std::min(NB, n - k0);
         block(s, A, ld, k0, nb, end, fail);
@@ -286,11 +240,7 @@ void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int 
         // updates the unused A[n][n])
         double *L21 = A + (size_t)k0 * ld + k0 + nb;
         double *S22 = A + (size_t)(k0 + nb) * ld + (k0 + nb);
-        if (hand)
-            launch_dgemm_nt(s, true, m, m, nb, L21, ld, L21, ld, S22, ld, -1., 1.);
-        else
-            MMBA_RB(rocblas_dsyrk(h, rocblas_fill_lower, rocblas_operation_none, m, nb, &mone,
-                                  L21, ld, &one, S22, ld));
+        launch_dgemm_nt(s, true, m, m, nb, L21, ld, L21, ld, S22, ld, -1., 1.);
     }
     k_dense_row_get<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, y);
 }

@@ -24,8 +24,7 @@
 // A and C may be the same array when every workgroup's rows of A are its own
 // rows of C (the in-place panel solve, N <= 128).  Used by mmba_dense.hip for
 // the panel solves, the in-block updates and the
-// rank-256 trailing updates of the dense blocked Cholesky (MMBA_DENSE_HAND=0
-// falls back to rocBLAS for A/B measurements).
+// rank-512 trailing updates of the dense blocked Cholesky.
 #include "mmba_kernels.h"
 #include "mmba_plan.h"
 

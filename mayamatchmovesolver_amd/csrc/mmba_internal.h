@@ -72,7 +72,7 @@ struct BcrDev {
     // step, 2 blocked (8-column panels); a v_readlane-per-entry chain measured
     // 13 % slower than 0 and was dropped
     int regchol = 2;
-    int mfma_upd = 1;  // even-block updates as fp64 MFMA (MMBA_BCR_MFMA=0: VALU)
+    int mfma_upd = 1;  // even-block updates as fp64 MFMA (always; the VALU form is the K > 32 fallback)
     const double *Bd = nullptr, *Ga = nullptr, *Gd = nullptr;  // input (band layout)
     double *Dk = nullptr, *Lk0 = nullptr, *Lk1 = nullptr, *Gk = nullptr;
     double *FC = nullptr, *FU = nullptr, *FV = nullptr, *FY = nullptr, *Zc = nullptr;
@@ -82,7 +82,7 @@ struct BcrDev {
     int *flags = nullptr;
     const int *ord = nullptr;
     // dataflow factorisation (k_bcr_factor_df): one flag per level item and
-    // the root (nullptr: per-level launches, MMBA_BCR_DF=0)
+    // the root (nullptr: per-level launches, MMBA_PATH_BCR_DATAFLOW = 0)
     int *fflags = nullptr;
     int *fail = nullptr;
     // item tickets of the two dataflow launches ([0] factorisation, [1]
@@ -94,6 +94,20 @@ struct BcrDev {
     // (xs[row_param[R]] = x_R, k_scatter_xR's job)
     const int *row_param = nullptr;
     double *xs = nullptr;
+};
+
+// Parallel cyclic reduction of the band system without an arrow
+// (mmba_pcr.hip): K x K blocks (K <= 24), one persistent workgroup per block.
+// pub[(lvl * nblk + j) * (3 K^2 + K)]: C^-1, C^-1 L, C^-1 U (column-major) and
+// C^-1 r of block j's factor at level lvl (its final level: C^-1 and rho);
+// wlog: the update products W1, W2 of every (level, block) (Newton pass).
+struct PcrDev {
+    int K = 0, nb = 0, w = 0, nblk = 0, nlev = 0;
+    const double *Bd = nullptr;  // band input [nb][w+1]
+    double *pub = nullptr, *wlog = nullptr, *rpub = nullptr, *part = nullptr;
+    int *fflag = nullptr, *rflag = nullptr;  // [nlev][nblk] epochs
+    int *flev = nullptr;                     // final level of every block
+    const int *row_param = nullptr;          // reduced row -> parameter (scatter of x)
 };
 
 // Block-diagonal + arrow reduced system (mmba_bdiag.hip): no solved bundle,
@@ -159,6 +173,10 @@ struct BandSolver {
     BdDev bd;
     bool use_bcr = false;                    // w <= 32: block cyclic reduction
     BcrDev bcr;
+    // no arrow, w <= 23, every block's workgroup resident: parallel cyclic
+    // reduction (the BCR buffers stay as the fallback after a timed-out wait)
+    bool use_pcr = false;
+    PcrDev pcr;
     // host copies of the ticket counters (every launch draws a known count)
     // and the switch to the per-level launches after a timed-out dataflow wait
     mutable unsigned tick_f = 0, tick_b = 0;

@@ -286,6 +286,13 @@ void bcr_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe,
                 const double *r = nullptr, double *y = nullptr);
 void bcr_forward(hipStream_t s, const BandSolver &B, const double *r, double *y);
 void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x);
+// Parallel cyclic reduction (mmba_pcr.hip): x = S^-1 r in one launch (x also
+// scattered to parameter order into xs when non-null); the Newton pass
+// part[j] = sum over block j's rows (mask) of w (S^-1 w) with the factors of
+// the last pcr_solve; workgroups of the solve kernel resident at once.
+void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, double *xs, int *fail);
+void pcr_rhs_dot(hipStream_t s, const PcrDev &P, const double *w, const int *mask, int *fail);
+int pcr_max_resident(int K);
 // Block-diagonal + arrow solver (mmba_bdiag.hip): factor S, y = L^-1 r and,
 // with x, the solution (scattered to parameter order into xs when non-null).
 void bd_direct(hipStream_t s, const DevProblem &P, const BdDev &D, const double *Acc,

@@ -2980,19 +2980,6 @@ void launch_records(hipStream_t s, const DevProblem &P, const int *var_cf,
                     double *brec, int base_only) {
     const int ncb = (nblk(base_only ? P.ncf : nvar, 64) + 7) / 8 * 8;  // see k_records
     const int nbb = nblk(P.nB, 64);
-    static const bool split = [] {
-        const char *e = std::getenv("MMBA_REC_SPLIT");
-        return e && std::atoi(e) != 0;
-    }();
-    if (split) {  // diagnostic: camera and bundle records as separate launches
-        if (ncb > 0)
-            k_records<<<ncb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
-                                         ncb);
-        if (nbb > 0)
-            k_records<<<nbb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
-                                         0);
-        return;
-    }
     if (ncb + nbb > 0)
         k_records<<<ncb + nbb, 64, 0, s>>>(P, var_cf, ext_pert, step, recs, nvar, brec, base_only,
                                            ncb);
@@ -3043,11 +3030,8 @@ bool trial_cf_fusable(const DevProblem &P) {
     return jac_ne_fusable(P, P.pc_uniform) && P.all_bnd_fast && P.no_lens && P.jcol_implicit &&
            !trial_cf_off();
 }
-bool &trial_cf_off() {  // MMBA_TRIAL_CF=0: the per-256-observation kernel (A/B)
-    static bool off = [] {
-        const char *e = std::getenv("MMBA_TRIAL_CF");
-        return e && std::atoi(e) == 0;
-    }();
+bool &trial_cf_off() {  // the per-256-observation kernel instead (tests set it)
+    static bool off = false;
     return off;
 }
 int trial_blocks(const DevProblem &P) { return trial_cf_fusable(P) ? P.ncf : residual_blocks(P); }
@@ -3207,11 +3191,8 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
         launch_jacobian_rs(s, P, ext_pert, step, solver_type, J, jcol, nloc, stale_param, eu, ed);
         return;
     }
-    // MMBA_JAC_UNI=0: per-lane record loads only (A/B of the wave-uniform path)
-    static const bool uni = [] {
-        const char *e = std::getenv("MMBA_JAC_UNI");
-        return !(e && std::atoi(e) == 0);
-    }();
+    // wave-uniform record loads (per-lane loads only: measured slower)
+    constexpr bool uni = true;
 #define MMBA_JAC_U(NCV, GEN)                                                                \
     do {                                                                                    \
         if (uni)                                                                            \
@@ -3250,7 +3231,6 @@ void launch_jac_ne(hipStream_t s, const DevProblem &P, const double *recs, const
     // segment: 2 waves 41.7 us, 4 waves 34.6 us, 8 waves 45.7 us)
     const long long per = (P.M + P.ncf - 1) / P.ncf;
     int nw = per > 1024 ? 8 : (per > 256 ? 4 : 2);
-    if (const char *e = std::getenv("MMBA_K2_WAVES")) nw = std::atoi(e);
 #define MMBA_JN(PC, NW, GEN)                                                                  \
     k_jac_ne_u<PC, NW, GEN><<<P.ncf, 64 * NW, 0, s>>>(P, recs, step, solver_type, J, jcol, nloc, \
                                                         stale_param, eu, ed, Acc, g, E)
@@ -3720,12 +3700,9 @@ void launch_backsub_bundle(hipStream_t s, const DevProblem &P, const double *W, 
     if (P.nB == 0) return;
     // two passes (coalesced per-observation u_i, then the bundle gather)
     // measured faster than one per-bundle pass gathering W rows (21.6 vs
-    // 25.4 us on C4); MMBA_BACKSUB_WTX=0 selects the fused form
-    static const bool two_pass = [] {
-        const char *e = std::getenv("MMBA_BACKSUB_WTX");
-        return !(e && std::atoi(e) == 0);
-    }();
-    if (two_pass) {  // A/B: per-observation u_i pass, then the bundle gather
+    // 25.4 us on C4)
+    constexpr bool two_pass = true;
+    if (two_pass) {  // per-observation u_i pass, then the bundle gather
         k_obs_wtx<<<nblk(P.M, 64), 64, sizeof(double) * 64 * P.wst, s>>>(P, W, xR, U);
         k_backsub_bundle<<<nblk(P.nB, 64), 64, 0, s>>>(P, nullptr, U, Wg, tb, Lb, xR, x);
     } else {

@@ -309,7 +309,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     }
     // unsharded plans with fast bundles: the bundle pass forms the lam = 0
     // bundle factor the undamped solve reads next (no k_bundle_factor
-    // launch); with MMBA_TAIL_REDUCE=1 its last workgroup also reduces the
+    // launch); with tail_reduce its last workgroup also reduces the
     // epilogue rows
     const bool fold = fuse && nranks == 1 && P.nbs > 0 && P.JB != nullptr && fold_ok;
     const bool tail = fold && tail_reduce;
@@ -443,7 +443,7 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     // unsharded: the LM decision after this trial reads slots [0, SL_LAST],
     // which the reduction's last block mirrors to the host itself
     const bool mirror = host_mirror && nranks == 1;
-    // MMBA_TAIL_REDUCE=1 (unsharded): the residual pass's last workgroup
+    // tail_reduce (unsharded, compiled out): the residual pass's last workgroup
     // runs the reduction launch's work itself (RedTail: same rows, flag and
     // mirror) -- off by default, see Plan::tail_reduce
     RedTail T;
@@ -593,7 +593,10 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             bd_factor_solve(s, bs.bd, d_fail, d_rhs, d_yR, d_xR, d_xs);
         } else if (band) {
             if (bs.red) allreduce(bs.red, bs.red_count);
-            band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
+            if (bs.use_pcr && !bs.df_off)  // the whole solve: x, scattered when unsharded
+                pcr_solve(s, bs.pcr, d_rhs, d_xR, bs.pcr.row_param ? d_xs : nullptr, d_fail);
+            else
+                band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
         } else if (dense) {
             ds.factor_forward(s, d_rhs, d_yR, d_fail);  // y = L^-1 rhs rides along
         } else {
@@ -607,6 +610,8 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         span_end(SPAN_CHOL);
         if (band && bs.use_bd) {
             // solved and scattered to parameter order above
+        } else if (band && bs.use_pcr && !bs.df_off) {
+            // solved by pcr_solve
         } else if (band) {
             band_backward(s, bs, d_yR, d_xR);
             if (nranks > 1 && !bs.use_bcr) {  // every shard needs its halo camera-frame rows
@@ -629,7 +634,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             }
         }
         // else done by the BCR backward solve / the block-diagonal back substitution
-        if (!(band && ((bs.use_bcr && bs.bcr.xs) || bs.use_bd)))
+        const bool pcr_now = band && bs.use_pcr && !bs.df_off;
+        if (!(band && ((bs.use_bcr && !pcr_now && bs.bcr.xs) || (pcr_now && bs.pcr.row_param) ||
+                       bs.use_bd)))
             launch_scatter_xR(s, P, d_xR, d_xs);
     }
     trial_folded = false;
@@ -710,7 +717,12 @@ void Plan::newton_enqueue(double dxnorm) {
         launch_reduce_sum(s, d_usq, nB, d_scalar + SL_NEWT_B);
     }
     if (nR > 0) {
-        if (band && bs.use_bd) {
+        if (band && bs.use_pcr && !bs.df_off) {
+            // w^T S^-1 w (= ||L^-1 w||^2 of any Cholesky of S) from the last
+            // solve's factors: per-block partials, summed in block order
+            pcr_rhs_dot(s, bs.pcr, d_wR, d_ymask, d_fail);
+            launch_reduce_sum(s, bs.pcr.part, bs.pcr.nblk, d_scalar + SL_NEWT_R);
+        } else if (band && bs.use_bd) {
             bd_forward(s, bs.bd, d_wR, d_yR);
         } else if (band) {
             band_forward(s, bs, d_wR, d_yR);
@@ -724,8 +736,9 @@ void Plan::newton_enqueue(double dxnorm) {
                 launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
             }
         }
-        launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R, d_ymask,
-                     d_ticket);
+        if (!(band && bs.use_pcr && !bs.df_off))
+            launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R,
+                         d_ymask, d_ticket);
     }
     // B15: v^T (M + U B U^T)^-1 v = v^T M^-1 v - w^T K^-1 w (the factor and
     // z_u, z_c of the last damped solve)

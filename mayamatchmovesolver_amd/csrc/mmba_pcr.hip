@@ -1,0 +1,494 @@
+// mmba_pcr.hip -- parallel cyclic reduction (PCR) of the band reduced camera
+// system, fp64, for CDNA4 (gfx950): the damped solve (S + lam D^2) x = r of
+// lmpar's qrsolv in ONE persistent launch, no backward pass.
+//
+// The band system (half bandwidth w <= 23, no arrow) is block tridiagonal in
+// K x K blocks (K = 8 / 16 / 24 >= w).  PCR eliminates, at level l (stride
+// s = 2^l), the couplings of EVERY block j to its neighbours p = j - s and
+// q = j + s:
+//
+//   D_j <- D_j - A_jp D_p^-1 A_pj - A_jq D_q^-1 A_qj
+//   A_j,p-s <- -A_jp D_p^-1 A_p,p-s,   A_j,q+s <- -A_jq D_q^-1 A_q,q+s
+//   r_j <- r_j - A_jp D_p^-1 r_p - A_jq D_q^-1 r_q
+//
+// (block Gaussian elimination of an SPD matrix: every D stays SPD).  After
+// ceil(log2 nblk) levels every block is uncoupled and x_j = D_j^-1 r_j: the
+// solution comes out of the last level, where block cyclic reduction
+// (mmba_bcr.hip) needs a root and a backward pass of as many dependent hops
+// again.  The critical path per level is one 24-step pivot chain, two fp64
+// MFMA products and one hand-off.
+//
+// Layout: workgroup j owns block j for the whole solve (its D_j, couplings
+// L_j = A_j,j-s, U_j = A_j,j+s and r_j stay in LDS).  Right after its update
+// a block factors its new D_j = C_j C_j^T ONCE, by augmented pivot chains
+// (mmba_bcr_dev.h) whose right-hand-side lanes carry the identity, L_j, U_j
+// and r_j (P_j = C_j^-1 L_j, Q_j = C_j^-1 U_j, rho_j = C_j^-1 r_j), and
+// because A_(j-s),j = L_j^T and A_(j+s),j = U_j^T it can form everything its
+// two consumers subtract itself (fp64 MFMA), before it publishes:
+//
+//   left consumer j - s:   P_j^T P_j, P_j^T rho_j, -(Q_j^T P_j)^T (its new U)
+//   right consumer j + s:  Q_j^T Q_j, Q_j^T rho_j, -Q_j^T P_j     (its new L)
+//
+// so a consumer's update is loads and subtractions only:
+//
+//   D_j -= Q_p^T Q_p + P_q^T P_q,  L_j <- -Q_p^T P_p,  U_j <- -(Q_q^T P_q)^T,
+//   r_j -= Q_p^T rho_p + P_q^T rho_q.
+//
+// Hand-off per MI355X guide G16 R1 (as k_bcr_factor_df): publications stored
+// write-through (sc1), every storing wave drained, the barrier, one flag per
+// (level, block) = epoch; the consumer's wave 0 polls the producers' flags
+// (sc1, bounded: a timeout sets bit 1 of *fail and the plan falls back to
+// block cyclic reduction), the barrier, sc1 loads.  Every block's workgroup
+// must be resident at once: the plan uses PCR only when the occupancy
+// calculator admits nblk workgroups on the device.
+//
+// lmpar's Newton term v^T (S + lam D^2)^-1 v (the BCR path's ||L^-1 v||^2)
+// reruns the elimination on a right-hand side only (k_pcr_rhs): C_j^-1, P_j
+// and Q_j of every level are logged (plain stores, issued after the level's
+// flag so their drain is off the critical path).
+#include <atomic>
+#include <mutex>
+
+#include "mmba_bcr_dev.h"
+#include "mmba_kernels.h"
+#include "mmba_plan.h"
+
+namespace mmba {
+
+typedef double pcr_d4 __attribute__((ext_vector_type(4)));
+
+// doubles of one (level, block) publication: X1 = P^T [P | rho], X2 =
+// Q^T [Q | rho] (K x (K + 1), row-major) and X3 = Q^T P (K x K)
+template <int K>
+__host__ __device__ constexpr int pcr_pub_size() {
+    return 2 * K * (K + 1) + K * K;
+}
+// ... and of one (level, block) log: C^-1, P, Q (row-major K x K)
+template <int K>
+__host__ __device__ constexpr int pcr_log_size() {
+    return 3 * K * K;
+}
+
+// flags[a] (and flags[b], b >= 0) == epoch, polled by one wave; false after
+// the bound
+__device__ __forceinline__ bool pcr_wait(const int *flags, int a, int b, unsigned epoch) {
+    for (unsigned spins = 0;; ++spins) {
+        unsigned fa = a >= 0 ? __hip_atomic_load((bcr_gu32 *)(flags + a), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : epoch;
+        unsigned fb = b >= 0 ? __hip_atomic_load((bcr_gu32 *)(flags + b), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : epoch;
+        fa = __builtin_amdgcn_readfirstlane(fa);
+        fb = __builtin_amdgcn_readfirstlane(fb);
+        if (fa == epoch && fb == epoch) break;
+        if (spins > (1u << 22)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    // every published value is stored and loaded sc1: no agent-scope
+    // acquire; the fence keeps the compiler from hoisting those loads
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// The damped solve.  blockIdx.x = block j.  r_in / x_out: reduced-order
+// vectors (nb rows); x is also scattered to parameter order (xs[row_param]).
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__restrict__ r_in,
+                                                   double *__restrict__ x_out, double *xs,
+                                                   unsigned epoch, int *fail,
+                                                   long long *probe = nullptr) {
+    constexpr int KS = K + 1;  // LDS row stride (odd: a lane-per-row read is conflict-free)
+    constexpr int K1 = K + 1;  // row stride of X1 / X2 (the rho column)
+    constexpr int PW = MMBA_BCR_PW;
+    constexpr int PS = pcr_pub_size<K>(), LS = pcr_log_size<K>();
+    constexpr int NT = K / 4;  // MFMA k-steps
+    constexpr int NE = (K * K + 255) / 256;  // update entries per thread
+    __shared__ double sD[K * KS], sL[K * KS], sU[K * KS];  // own block (row-major)
+    // factor images (row-major): C^-1, P, Q, and rho
+    __shared__ double sCi[K * KS], sP[K * KS], sQ[K * KS];
+    __shared__ double sr[K], srho[K];
+    __shared__ double sI[K * KS];   // the identity (right-hand sides of the C^-1 chain)
+    __shared__ double sZ[2 * K];    // a zero row, then scratch for lanes without an operand
+    __shared__ double pl[3][64 * PW];  // pivot-chain panel images, waves 0..2
+    __shared__ int bad_s, ok_s;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int j = blockIdx.x, nblk = P.nblk, nb = P.nb, W1 = P.w + 1;
+    if (tid == 0) bad_s = 0;
+    // probe (tools/ubench/pcr_probe.hip): thread 0 of block nblk / 2 stores
+    // the wall clock (100 MHz) at the phase ends of every level
+    long long *pr = (probe && j == nblk / 2 && tid == 0) ? probe : nullptr;
+    auto stamp = [&](int lvl, int ph) {
+        if (pr) pr[lvl * 8 + ph] = (long long)wall_clock64();
+    };
+    // ---- level-0 state from the band layout: D_j (lower), L_j = S[j, j-1],
+    // U_j = S[j, j+1] = S[j+1, j]^T, r_j; padding rows: identity, uncoupled
+    for (int q = tid; q < K * K; q += 256) {
+        const int i = q / K, c = q % K, R = j * K + i;
+        double dv = 0., lv = 0., uv = 0.;
+        if (R < nb) {
+            const int C = j * K + c;
+            if (c <= i && R - C <= P.w) dv = P.Bd[(size_t)R * W1 + (C - R + P.w)];
+            const int Cl = (j - 1) * K + c;
+            if (j > 0 && R - Cl <= P.w) lv = P.Bd[(size_t)R * W1 + (Cl - R + P.w)];
+            const int R2 = (j + 1) * K + c;  // U_j[i][c] = S[R2, R]
+            if (R2 < nb && R2 - R <= P.w) uv = P.Bd[(size_t)R2 * W1 + (R - R2 + P.w)];
+        } else if (i == c) {
+            dv = 1.;
+        }
+        sD[i * KS + c] = dv;
+        sL[i * KS + c] = lv;
+        sU[i * KS + c] = uv;
+    }
+    if (tid < K) sr[tid] = (j * K + tid < nb) ? r_in[j * K + tid] : 0.;
+    for (int q = tid; q < K * KS; q += 256) sI[q] = (q / KS == q % KS) ? 1. : 0.;
+    if (tid < K) sZ[tid] = 0.;
+    __syncthreads();
+    int s = 1;
+    for (int lvl = 0;; ++lvl, s *= 2) {
+        const bool hp = j - s >= 0, hq = j + s < nblk;
+        stamp(lvl, 0);
+        // ---- factor D_j once: C^-1 with rho (wave 0), P = C^-1 L (wave 1),
+        // Q = C^-1 U (wave 2): the three chains are the same bits; their
+        // right-hand-side lanes write the column images
+        int bad = 0;
+        if (wv < 3 && (wv == 0 || (wv == 1 && hp) || (wv == 2 && hq))) {
+            // one LDS source / destination per lane (no divergent paths):
+            // rows of D (its upper part is zero), columns of the identity / L
+            // / U, r; the other lanes read a zero row and write scratch
+            const double *src = sZ;
+            int st = 0;
+            double *dst = sZ + K;
+            int dt = 0;
+            if (lane < K) {
+                src = sD + lane * KS;
+                st = 1;
+            } else if (lane < 2 * K) {
+                const int c = lane - K;
+                src = (wv == 0 ? sI : (wv == 1 ? sL : sU)) + c;
+                st = KS;
+                dst = (wv == 0 ? sCi : (wv == 1 ? sP : sQ)) + c;
+                dt = KS;
+            } else if (wv == 0 && lane == 2 * K) {
+                src = sr;
+                st = 1;
+                dst = srho;
+                dt = 1;
+            }
+            double a[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) a[c] = src[c * st];
+            bcr_chol_aug_blk<K, PW>(a, nullptr, pl[wv], bad);
+#pragma unroll
+            for (int i = 0; i < K; ++i) dst[i * dt] = a[i];
+        }
+        if (bad) atomicOr(&bad_s, 1);
+        __syncthreads();
+        stamp(lvl, 1);
+        double *log = P.wlog + ((size_t)lvl * nblk + j) * LS;
+        if (!hp && !hq) {
+            // uncoupled: x_j = C^-T rho; C^-1 logged for the Newton pass
+            if (tid < K) {
+                double acc = 0.;
+#pragma unroll
+                for (int i = 0; i < K; ++i) acc = fma(sCi[i * KS + tid], srho[i], acc);
+                const int R = j * K + tid;
+                if (R < nb) {
+                    x_out[R] = acc;
+                    if (xs && P.row_param[R] >= 0) xs[P.row_param[R]] = acc;
+                }
+            }
+            for (int q = tid; q < K * K; q += 256) log[q] = sCi[(q / K) * KS + q % K];
+            if (tid == 0) {
+                P.flev[j] = lvl;
+                if (bad_s) atomicOr(fail, 1);
+            }
+            return;
+        }
+        // ---- what the consumers subtract: X1 = P^T [P | rho] (left, hp),
+        // X2 = Q^T [Q | rho] (right, hq), X3 = Q^T P (both): 32 x 32 padded
+        // products, 12 tiles over the 4 waves (tile t: product t / 4, 16 x 16
+        // tile t % 4), stored write-through from the accumulators
+        double *pub = P.pub + ((size_t)lvl * nblk + j) * PS;
+        {
+            // the wave's three tiles interleaved (independent accumulators);
+            // a product nobody reads runs on zero operands and is not stored
+            const int i16 = lane & 15, k4 = lane >> 4;
+            pcr_d4 acc[3];
+            // per lane and tile one LDS operand base and stride each: A(i, u)
+            // = Y(u, i) (Y = P or Q), B(u, c) = Z(u, c) with column K = rho
+            // (X1, X2); padding rows / columns and unneeded products read the
+            // zero row
+            const double *pa[3], *pb[3];
+            int sa[3], sb[3], bc[3], cmax[3];
+            bool need[3];
+#pragma unroll
+            for (int tt = 0; tt < 3; ++tt) {
+                const int t = wv + 4 * tt, prod = t >> 2, ti = (t >> 1) & 1, tc = t & 1;
+                need[tt] = prod == 0 ? hp : (prod == 1 ? hq : (hp && hq));
+                cmax[tt] = prod == 2 ? K : K + 1;
+                const int ai = ti * 16 + i16;
+                bc[tt] = tc * 16 + i16;
+                const double *ia = prod == 0 ? sP : sQ, *ib = prod == 1 ? sQ : sP;
+                const bool av = need[tt] && ai < K;
+                pa[tt] = av ? ia + ai : sZ;
+                sa[tt] = av ? KS : 0;
+                const bool bv = need[tt] && bc[tt] < cmax[tt];
+                pb[tt] = !bv ? sZ : (bc[tt] < K ? ib + bc[tt] : srho);
+                sb[tt] = !bv ? 0 : (bc[tt] < K ? KS : 1);
+                acc[tt] = pcr_d4{0., 0., 0., 0.};
+            }
+#pragma unroll
+            for (int st = 0; st < NT; ++st) {
+                const int u = 4 * st + k4;
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt)
+                    acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[tt][u * sa[tt]], pb[tt][u * sb[tt]],
+                                                                   acc[tt], 0, 0, 0);
+            }
+#pragma unroll
+            for (int tt = 0; tt < 3; ++tt) {
+                if (!need[tt]) continue;
+                const int t = wv + 4 * tt, prod = t >> 2, ti = (t >> 1) & 1;
+                double *dst = pub + (prod == 0 ? 0 : (prod == 1 ? K * K1 : 2 * K * K1));
+                const int ld = prod == 2 ? K : K1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = ti * 16 + k4 + 4 * r;
+                    if (row < K && bc[tt] < cmax[tt]) bcr_st(dst + row * ld + bc[tt], acc[tt][r]);
+                }
+            }
+        }
+        stamp(lvl, 2);
+        // ---- publish level lvl
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store((bcr_gu32 *)(P.fflag + (size_t)lvl * nblk + j), epoch,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- the Newton pass's log (later launches read it: plain stores,
+        // draining while this block waits)
+        for (int q = tid; q < K * K; q += 256) {
+            const int x = (q / K) * KS + q % K;
+            log[q] = sCi[x];
+            log[K * K + q] = sP[x];
+            log[2 * K * K + q] = sQ[x];
+        }
+        // ---- wait for the neighbours' publications of this level
+        if (wv == 0) {
+            const bool ok = pcr_wait(P.fflag + (size_t)lvl * nblk, hp ? j - s : -1,
+                                     hq ? j + s : -1, epoch);
+            if (lane == 0) ok_s = ok;
+        }
+        __syncthreads();
+        stamp(lvl, 3);
+        if (!ok_s) {
+            if (tid == 0) atomicOr(fail, 2);
+            return;  // the blocks waiting on this one time out as well
+        }
+        // ---- the update: loads and subtractions only
+        //   D_j -= X2_p + X1_q (lower), L_j = -X3_p, U_j = -X3_q^T,
+        //   r_j -= X2_p(:, K) + X1_q(:, K)
+        {
+            const bool hpp = hp && j - 2 * s >= 0, hqq = hq && j + 2 * s < nblk;
+            // absent neighbours: an empty view (its loads read 0)
+            const auto vp = sc1_view(P.pub + ((size_t)lvl * nblk + (hp ? j - s : j)) * PS,
+                                     hp ? PS * 8u : 0u);
+            const auto vq = sc1_view(P.pub + ((size_t)lvl * nblk + (hq ? j + s : j)) * PS,
+                                     hq ? PS * 8u : 0u);
+            double dsub[NE], lnew[NE], unew[NE], rsub = 0.;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int q = tid + 256 * e, i = q / K, c = q % K;
+                double d = 0., l = 0., u = 0.;
+                if (q < K * K) {
+                    if (c <= i)
+                        d = sc1_load(vp, K * K1 + i * K1 + c) + sc1_load(vq, i * K1 + c);
+                    l = -sc1_load(vp, 2 * K * K1 + q);
+                    u = -sc1_load(vq, 2 * K * K1 + q);  // X3_q(i, c) -> U_j(c, i)
+                }
+                dsub[e] = d;
+                lnew[e] = hpp ? l : 0.;
+                unew[e] = hqq ? u : 0.;
+            }
+            if (tid < K) rsub = sc1_load(vp, K * K1 + tid * K1 + K) + sc1_load(vq, tid * K1 + K);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+                const int q = tid + 256 * e, i = q / K, c = q % K;
+                if (q < K * K) {
+                    if (c <= i) sD[i * KS + c] -= dsub[e];
+                    sL[i * KS + c] = lnew[e];
+                    sU[c * KS + i] = unew[e];
+                }
+            }
+            if (tid < K) sr[tid] -= rsub;
+        }
+        __syncthreads();
+        stamp(lvl, 4);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Right-hand side only (lmpar's Newton term): z = (S + lam D^2)^-1 w with the
+// factors of the last k_pcr_solve, then part[j] = sum over this block's rows
+// (mask) of w z.  One 64-lane workgroup per block.  Per level: rho = C^-1 r,
+// publish Q^T rho (right consumer) and P^T rho (left consumer), subtract the
+// neighbours'.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restrict__ w,
+                                                const int *__restrict__ mask, double *part,
+                                                unsigned epoch, int *fail) {
+    constexpr int LS = pcr_log_size<K>();
+    __shared__ double sr[K], srho[K];
+    const int lane = threadIdx.x, j = blockIdx.x, nblk = P.nblk, nb = P.nb;
+    const int R = j * K + lane;
+    const double w0 = (lane < K && R < nb) ? w[R] : 0.;
+    double r = w0;
+    const int L = P.flev[j];
+    int s = 1;
+    for (int lvl = 0; lvl < L; ++lvl, s *= 2) {
+        const bool hp = j - s >= 0, hq = j + s < nblk;
+        const double *lg = P.wlog + ((size_t)lvl * nblk + j) * LS;
+        if (lane < K) sr[lane] = r;
+        __syncthreads();
+        if (lane < K) {  // rho_i = sum_c C^-1(i, c) r_c
+            double rho = 0.;
+#pragma unroll
+            for (int c = 0; c < K; ++c) rho = fma(lg[lane * K + c], sr[c], rho);
+            srho[lane] = rho;
+        }
+        __syncthreads();
+        double *rp = P.rpub + ((size_t)lvl * nblk + j) * 2 * K;
+        if (lane < K) {  // (Q^T rho)_c, (P^T rho)_c
+            double a = 0., b = 0.;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                a = fma(lg[2 * K * K + i * K + lane], srho[i], a);
+                b = fma(lg[K * K + i * K + lane], srho[i], b);
+            }
+            if (hq) bcr_st(rp + lane, a);
+            if (hp) bcr_st(rp + K + lane, b);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0)
+            __hip_atomic_store((bcr_gu32 *)(P.rflag + (size_t)lvl * nblk + j), epoch,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool ok = pcr_wait(P.rflag + (size_t)lvl * nblk, hp ? j - s : -1, hq ? j + s : -1,
+                                 epoch);
+        if (!ok) {
+            if (lane == 0) atomicOr(fail, 2);
+            return;
+        }
+        if (lane < K) {  // r -= Q_p^T rho_p + P_q^T rho_q
+            double sub = 0.;
+            if (hp) sub += bcr_ld(P.rpub + ((size_t)lvl * nblk + j - s) * 2 * K + lane);
+            if (hq) sub += bcr_ld(P.rpub + ((size_t)lvl * nblk + j + s) * 2 * K + K + lane);
+            r -= sub;
+        }
+        __syncthreads();
+    }
+    // z = C^-T C^-1 r with the final level's factor
+    const double *lg = P.wlog + ((size_t)L * nblk + j) * LS;
+    if (lane < K) sr[lane] = r;
+    __syncthreads();
+    if (lane < K) {
+        double rho = 0.;
+#pragma unroll
+        for (int c = 0; c < K; ++c) rho = fma(lg[lane * K + c], sr[c], rho);
+        srho[lane] = rho;
+    }
+    __syncthreads();
+    double z = 0.;
+    if (lane < K) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) z = fma(lg[i * K + lane], srho[i], z);
+    }
+    double v = (lane < K && R < nb && mask[R]) ? w0 * z : 0.;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) part[j] = v;
+}
+
+static std::atomic<unsigned> g_pcr_epoch{0};
+
+static unsigned pcr_next_epoch() {
+    unsigned ep = ++g_pcr_epoch;
+    if (ep == 0) ep = ++g_pcr_epoch;  // flags start at 0: never use epoch 0
+    return ep;
+}
+
+// Two PCR launches running at once on one device can deadlock each other:
+// each may hold part of its workgroups resident, spinning, while the rest wait
+// for CU slots the other holds (until the bounded waits time out and the
+// plans fall back).  So the PCR launches of one process on one device are
+// ordered across streams: every launch waits, device-side, for the previous
+// PCR launch when that one was issued on another stream (an event recorded
+// after each launch).  Plans of one stream are ordered by the stream already;
+// other processes sharing the device are not covered (their launches time out
+// and fall back to block cyclic reduction).
+namespace {
+struct PcrOrder {
+    std::mutex mu;
+    hipStream_t last = nullptr;
+    hipEvent_t ev = nullptr;
+};
+PcrOrder g_pcr_order[64];
+}  // namespace
+
+template <class Launch>
+static void pcr_ordered(hipStream_t s, Launch &&launch) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    PcrOrder &o = g_pcr_order[dev & 63];
+    std::lock_guard<std::mutex> g(o.mu);
+    if (!o.ev) hipEventCreateWithFlags(&o.ev, hipEventDisableTiming);
+    if (o.last && o.last != s) hipStreamWaitEvent(s, o.ev, 0);
+    launch();
+    hipEventRecord(o.ev, s);
+    o.last = s;
+}
+
+void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, double *xs, int *fail) {
+    pcr_ordered(s, [&] {
+        const unsigned ep = pcr_next_epoch();
+        switch (P.K) {
+            case 8: k_pcr_solve<8><<<P.nblk, 256, 0, s>>>(P, r, x, xs, ep, fail); break;
+            case 16: k_pcr_solve<16><<<P.nblk, 256, 0, s>>>(P, r, x, xs, ep, fail); break;
+            default: k_pcr_solve<24><<<P.nblk, 256, 0, s>>>(P, r, x, xs, ep, fail); break;
+        }
+    });
+}
+
+void pcr_rhs_dot(hipStream_t s, const PcrDev &P, const double *w, const int *mask, int *fail) {
+    pcr_ordered(s, [&] {
+        const unsigned ep = pcr_next_epoch();
+        switch (P.K) {
+            case 8: k_pcr_rhs<8><<<P.nblk, 64, 0, s>>>(P, w, mask, P.part, ep, fail); break;
+            case 16: k_pcr_rhs<16><<<P.nblk, 64, 0, s>>>(P, w, mask, P.part, ep, fail); break;
+            default: k_pcr_rhs<24><<<P.nblk, 64, 0, s>>>(P, w, mask, P.part, ep, fail); break;
+        }
+    });
+}
+
+// Workgroups of k_pcr_solve<K> the device keeps resident at once (every
+// block's workgroup must be: the plan takes PCR only when nblk fits).
+int pcr_max_resident(int K) {
+    int dev = 0, per_cu = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    hipError_t e;
+    switch (K) {
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8>, 256, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16>, 256, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24>, 256, 0); break;
+    }
+    if (e != hipSuccess) return 0;
+    return per_cu * cus;
+}
+
+}  // namespace mmba

@@ -231,9 +231,8 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
         }
         if (!chained) {
             // one launch for every frame when the plan's structure allows it
-            // (MMBA_PERFRAME_BATCH=0: the per-frame plans below)
-            const char *e = std::getenv("MMBA_PERFRAME_BATCH");
-            if (!e || std::atoi(e) != 0) {
+            // (MMBA_PATH_PERFRAME_BATCH = 0: the per-frame plans below)
+            if (mmba::path_choice(MMBA_PATH_PERFRAME_BATCH) != 0) {
                 mmba_plan *plan = nullptr;
                 if (mmba_plan_create(ctx, prob, opt, &plan) == MMBA_OK) {
                     int rc = MMBA_ERR_UNSUPPORTED;

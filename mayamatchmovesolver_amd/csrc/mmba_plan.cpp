@@ -941,12 +941,10 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_p4 = upload(bnd_p4);
     {
         // per-camera-frame attribute-value indices for the camera records
-        // (cameras whose transform has no parent; MMBA_CAM_TABLE=0 disables)
+        // (cameras whose transform has no parent)
         bool ok = true;
         for (int c = 0; c < nC && ok; ++c)
             if (pr->tfm_parent[pr->cam_tfm[c]] >= 0) ok = false;
-        if (const char *e = std::getenv("MMBA_CAM_TABLE"))
-            if (std::atoi(e) == 0 && !rs_on) ok = false;
         D.cf_aidx = nullptr;
         if (ok && ncf > 0) {
             static const int cam_k[7] = {MMBA_CAM_FILM_BACK_W_INCH, MMBA_CAM_FILM_BACK_H_INCH,
@@ -1002,11 +1000,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         // the generic kernels
         if (central || opt.robust_loss || rs_on) fast = false;
         jac_ncv = fast ? pc_uniform : 0;
-        if (const char *e = std::getenv("MMBA_JAC_GENERIC"))
-            if (std::atoi(e)) jac_ncv = 0;
         D.jcol_implicit = jac_ncv > 0 ? 1 : 0;
-        if (const char *e = std::getenv("MMBA_JCOL"))
-            if (std::atoi(e)) D.jcol_implicit = 0;
     }
     d_brec = dalloc<double>((size_t)nB * BREC);
     D.brec = d_brec;
@@ -1048,10 +1042,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_pcomp = nullptr;
     {
         // fast parentless bundles: value indices of the translate and the
-        // component each parameter sets (MMBA_BND_TABLE=0 keeps the walk)
+        // component each parameter sets
         bool ok = nB > 0;
-        const char *e = std::getenv("MMBA_BND_TABLE");
-        if (e && std::atoi(e) == 0) ok = false;
         std::vector<int4> vx(std::max(nB, 1), make_int4(-1, -1, -1, 0));
         std::vector<int> pcomp(std::max(nB, 1), 0);
         for (int b = 0; b < nB && ok; ++b) {
@@ -1184,11 +1176,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     }
     {
         // dense reduced system: at least 30 % of the lower tiles non-zero
-        // after fill (MMBA_DENSE=0 keeps the tiled path, =1 forces dense)
+        // after fill (MMBA_PATH_DENSE pins it: 0 tiled, 1 dense)
         const long long full = (long long)NT * (NT + 1) / 2;
         dense = !band && nranks == 1 && NT >= 8 && (long long)nslots * 10 >= full * 3;
-        if (const char *e = std::getenv("MMBA_DENSE"))
-            dense = !band && nranks == 1 && NT > 0 && std::atoi(e) != 0;
+        if (path_choice(MMBA_PATH_DENSE) >= 0)
+            dense = !band && nranks == 1 && NT > 0 && path_choice(MMBA_PATH_DENSE) != 0;
     }
     if (dense) {
         ds.setup(*this, nRpad);
@@ -1209,7 +1201,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             cfblk_cf.push_back(cf);
         }
     if (band) setup_band();
-    if (band && std::getenv("MMBA_PROBE")) {
+    if (band && path_choice(MMBA_PATH_PROBE) > 0) {
         const size_t np = 8 + 4 * ((size_t)std::max(nR, 1) + 64);  // + the dataflow trace
         d_probe = dalloc<long long>(np);
         MMBA_HIP(hipMemsetAsync(d_probe, 0, np * sizeof(long long), s));
@@ -1310,14 +1302,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             if (p_class[p] != PC_B && p_pos[p] >= 0 && p_pos[p] < nR) row_param[p_pos[p]] = p;
         bs.bd.row_param = upload(row_param);
     }
-    if (bs.use_bcr && bs.bcr.flags) {
+    if (bs.use_bcr && (bs.bcr.flags || bs.use_pcr)) {
         bs.bcr.fail = d_fail;
         if (nranks == 1) {
             std::vector<int> row_param(std::max(nR, 1), -1);
             for (int p = 0; p < n; ++p)
                 if (p_class[p] != PC_B && p_pos[p] >= 0 && p_pos[p] < nR) row_param[p_pos[p]] = p;
             bs.bcr.row_param = upload(row_param);
-            bs.bcr.xs = d_xs;
+            bs.pcr.row_param = bs.bcr.row_param;
+            bs.bcr.xs = bs.bcr.flags ? d_xs : nullptr;
         }
     }
     // ---- batched per-frame solve (mmba_batch.hip): frames share nothing
@@ -1393,12 +1386,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
     MMBA_HIP(hipHostMalloc(&h_seq, sizeof(unsigned)));
     *h_seq = 0;
-    if (const char *e = std::getenv("MMBA_SEQ_POLL")) seq_poll = std::atoi(e) != 0;
-    if (const char *e = std::getenv("MMBA_PRE_JAC")) pre_jac = std::atoi(e) != 0;
     trial_fold_ok = nranks == 1 && nB_solved > 0;
-    if (const char *e = std::getenv("MMBA_TRIAL_FOLD")) trial_fold_ok = trial_fold_ok && std::atoi(e) != 0;
-    if (const char *e = std::getenv("MMBA_BACKSUB_WTX"))  // the fused form needs the two-pass u_i
-        trial_fold_ok = trial_fold_ok && std::atoi(e) != 0;
     d_gate = dalloc<int>(1);
     MMBA_HIP(hipMemsetAsync(d_gate, 0, sizeof(int), s));
     d_mticket = dalloc<unsigned>(1);
@@ -1407,18 +1395,12 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     for (int j = 0; j < n; ++j)
         if (param_weight[j] <= 0.) pweight_ok = false;
     MMBA_HIP(hipMemsetAsync(d_mticket, 0, sizeof(unsigned), s));
-    if (const char *e = std::getenv("MMBA_HOST_MIRROR")) host_mirror = std::atoi(e) != 0;
     if (b15) {  // the rank-one term corrects ||J p|| after the trial's reduction
         host_mirror = false;
         trial_fold_ok = false;
     }
     fold_init = dest_diag_all && use_dest && nranks == 1 && nG == 0 && !rs_on && nRpad == nR &&
                 (pc_uniform == 6 || pc_uniform == 7);
-    if (const char *e = std::getenv("MMBA_FOLD_SCHUR_INIT")) fold_init = fold_init && std::atoi(e) != 0;
-    if (const char *e = std::getenv("MMBA_SPIN_WAIT")) spin_wait = std::atoi(e) != 0;
-    if (const char *e = std::getenv("MMBA_K2_FUSED")) k2_split = std::atoi(e) == 0;
-    if (const char *e = std::getenv("MMBA_NE_FOLD")) fold_ok = std::atoi(e) != 0;
-    if (const char *e = std::getenv("MMBA_TAIL_REDUCE")) tail_reduce = std::atoi(e) != 0;
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
     MMBA_HIP(hipHostMalloc(&h_xstage, sizeof(double) * std::max(n, 1)));
     MMBA_HIP(hipStreamSynchronize(s));
@@ -1429,12 +1411,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
 void Plan::setup_band(int Pforce) {
     const int nb = nR - nG, w = bw;
     // No solved bundle (C2, C5, per-frame solves): the camera-frame blocks are
-    // uncoupled, so S is block diagonal + arrow (mmba_bdiag.hip);
-    // MMBA_BDIAG=0 keeps the band solvers (A/B)
+    // uncoupled, so S is block diagonal + arrow (mmba_bdiag.hip)
     {
-        const char *e = std::getenv("MMBA_BDIAG");
-        const bool off = e && std::atoi(e) == 0;
-        if (!off && nB_solved == 0 && nranks == 1 && !cfblk_pc.empty() && Pforce == 0 && !rs_on) {
+        if (nB_solved == 0 && nranks == 1 && !cfblk_pc.empty() && Pforce == 0 && !rs_on) {
             bs.use_bd = true;
             bs.P = 1;
             bs.w = w;
@@ -1472,19 +1451,16 @@ void Plan::setup_band(int Pforce) {
             return;
         }
     }
-    // Unsharded and w <= 32: block cyclic reduction (mmba_bcr.hip).  Pforce < 0
-    // forces it, Pforce > 0 forces the partitioned chain; MMBA_BAND_BCR=0
-    // disables it (A/B measurements).
+    // w <= 32: the log-depth solvers, block cyclic reduction (mmba_bcr.hip) or
+    // parallel cyclic reduction (mmba_pcr.hip).  Pforce < 0 forces them,
+    // Pforce > 0 the partitioned chain.
     {
-        const char *e = std::getenv("MMBA_BAND_BCR");
-        const bool env_off = e && std::atoi(e) == 0;
         // Sharded: the partitioned chain's separator system grows with the
         // shard count (one workgroup, (P-1) w rows at bandwidth 2w-1), so the
-        // shards all-reduce S instead and each runs the log-depth BCR on it;
-        // MMBA_SHARD_BCR=0 keeps the partitioned chain (A/B).
-        const char *es = std::getenv("MMBA_SHARD_BCR");
-        const bool shard_ok = nranks == 1 || !(es && std::atoi(es) == 0);
-        if (shard_ok && w <= 32 && (Pforce < 0 || (Pforce == 0 && !env_off))) {
+        // shards all-reduce S instead and each runs the log-depth solve on
+        // it; MMBA_PATH_SHARD_BCR = 0 keeps the partitioned chain (tests)
+        const bool shard_ok = nranks == 1 || path_choice(MMBA_PATH_SHARD_BCR) != 0;
+        if (shard_ok && w <= 32 && Pforce <= 0) {
             bs.use_bcr = true;
             bs.P = 1;
             bs.comm = nranks > 1 ? comm : nullptr;
@@ -1515,8 +1491,6 @@ void Plan::setup_band(int Pforce) {
             B.w = w;
             B.nblk = std::max(1, (nb + B.K - 1) / B.K);
             B.NR = B.K + (nG + 7) / 8 * 8;
-            if (const char *e3 = std::getenv("MMBA_BCR_CHOL")) B.regchol = std::atoi(e3) == 0 ? 0 : 2;
-            if (const char *e4 = std::getenv("MMBA_BCR_MFMA")) B.mfma_upd = std::atoi(e4) != 0;
             B.Bd = bs.Bd;
             B.Ga = bs.Ga;
             B.Gd = bs.Gd;
@@ -1534,22 +1508,19 @@ void Plan::setup_band(int Pforce) {
             B.gpart = dalloc<double>((size_t)B.nblk * nG);
             B.rw = dalloc<double>((size_t)nb + nG);
             {
-                const char *e5 = std::getenv("MMBA_BCR_DF");
-                if (!(e5 && std::atoi(e5) == 0)) {
+                if (path_choice(MMBA_PATH_BCR_DATAFLOW) != 0) {
                     B.fflags = dalloc<int>((size_t)B.nblk + 64);  // items < nblk + levels
                     MMBA_HIP(hipMemsetAsync(B.fflags, 0, sizeof(int) * ((size_t)B.nblk + 64), s));
                 }
                 B.tick = dalloc<unsigned>(2);
                 MMBA_HIP(hipMemsetAsync(B.tick, 0, sizeof(unsigned) * 2, s));
-                if (const char *e6 = std::getenv("MMBA_BCR_DF_GRID"))
-                    bs.df_grid = std::max(1, std::min(256, std::atoi(e6)));
+                if (path_choice(MMBA_PATH_BCR_GRID) > 0)
+                    bs.df_grid = std::max(1, std::min(256, path_choice(MMBA_PATH_BCR_GRID)));
             }
             {
                 // dataflow backward solve: blocks in dependency order (root,
-                // then levels coarse to fine); MMBA_BCR_BWD_LEVELS=1 keeps the
-                // per-level launches (A/B)
-                const char *e2 = std::getenv("MMBA_BCR_BWD_LEVELS");
-                if (!(e2 && std::atoi(e2) != 0)) {
+                // then levels coarse to fine)
+                {
                     std::vector<int> ord{0};
                     int L = 0;
                     while ((1 << L) < B.nblk) ++L;
@@ -1563,6 +1534,36 @@ void Plan::setup_band(int Pforce) {
             }
             // every shard holds the whole y = L^-1 v: rank 0 counts it
             d_ymask = upload(std::vector<int>(std::max(nR, 1), rank == 0 ? 1 : 0));
+            // no arrow and K <= 24: parallel cyclic reduction (mmba_pcr.hip)
+            // when every block's workgroup fits on the device at once
+            {
+                // Pforce == -2 (mmba_debug_band_solve): block cyclic reduction only
+                const bool pcr_off = path_choice(MMBA_PATH_PCR) == 0 || Pforce == -2;
+                if (!pcr_off && nG == 0 && B.K <= 24 && B.nblk <= pcr_max_resident(B.K)) {
+                    PcrDev &Q = bs.pcr;
+                    Q.K = B.K;
+                    Q.nb = nb;
+                    Q.w = w;
+                    Q.nblk = B.nblk;
+                    int L = 0;
+                    while ((1 << L) < B.nblk) ++L;  // block 0 is coupled until 2^L >= nblk
+                    Q.nlev = L;
+                    Q.Bd = bs.Bd;
+                    // publications (levels 0..L-1): P^T [P rho], Q^T [Q rho], Q^T P;
+                    // logs (levels 0..L): C^-1, P, Q; right-hand-side pass: 2 K
+                    const size_t ps = (size_t)2 * Q.K * (Q.K + 1) + (size_t)Q.K * Q.K;
+                    Q.pub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * ps));
+                    Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
+                    Q.rpub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * 2 * Q.K));
+                    Q.part = dalloc<double>(Q.nblk);
+                    Q.fflag = dalloc<int>(std::max<size_t>(1, (size_t)L * Q.nblk));
+                    Q.rflag = dalloc<int>(std::max<size_t>(1, (size_t)L * Q.nblk));
+                    MMBA_HIP(hipMemsetAsync(Q.fflag, 0, sizeof(int) * std::max<size_t>(1, (size_t)L * Q.nblk), s));
+                    MMBA_HIP(hipMemsetAsync(Q.rflag, 0, sizeof(int) * std::max<size_t>(1, (size_t)L * Q.nblk), s));
+                    Q.flev = dalloc<int>(Q.nblk);
+                    bs.use_pcr = true;
+                }
+            }
             return;
         }
     }
@@ -1580,7 +1581,6 @@ void Plan::setup_band(int Pforce) {
             // chain ((P-1) w rows at bandwidth 2w-1); measured on C4 (nb 2994,
             // w 23): P = 1/4/8/12/16/24 -> 1.20/0.70/0.44/0.40/0.41/0.48 ms
             P = (int)std::lround(std::sqrt((double)len / w));
-            if (const char *e = std::getenv("MMBA_BAND_PARTS")) P = std::atoi(e);
             P = std::max(1, std::min(P, len / (2 * w + 8)));
         }
         return P;

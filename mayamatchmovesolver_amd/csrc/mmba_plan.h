@@ -19,6 +19,8 @@ struct mmba_context {
 namespace mmba {
 
 void set_error(const std::string &msg);
+// mmba_debug_set_path's choice for MMBA_PATH_<key> (-1: the builder's own)
+int path_choice(int key);
 
 #define MMBA_HIP(call)                                                             \
     do {                                                                           \
@@ -42,15 +44,13 @@ void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd
                   int nranks, int32_t *bounds, int32_t *bnd_owner);
 
 // Dense reduced system (mmba_dense.hip): blocked right-looking Cholesky,
-// one-wave panel kernel + rocBLAS GEMM/SYRK trailing updates, right-hand
-// side carried as an extra row (fused forward solve), GEMV block solves.
+// two-wave panel kernel + fp64 MFMA GEMM/SYRK trailing updates (k_dgemm_nt),
+// right-hand side carried as an extra row (fused forward solve), block
+// triangular solves.
 struct Plan;
 struct DenseSolver {
-    void *handle = nullptr;  // rocblas_handle
     int n = 0, ld = 0;       // columns (nRpad), leading dimension (n + 64)
-    bool hand = true;        // k_dgemm_nt (MMBA_DENSE_HAND=0: rocBLAS)
     double *A = nullptr, *Linv = nullptr, *ws = nullptr;
-    ~DenseSolver();
     void setup(Plan &pl, int n);
     void init(hipStream_t s);
     void block(hipStream_t s, double *A, int ld, int k0, int nb, int end, int *fail);
@@ -97,20 +97,23 @@ struct Plan {
     bool use_dest = false;
     int ndest = 0;
     int jac_ncv = 0;     // uniform fast Jacobian kernel (k_jacobian_u<jac_ncv>), 0: generic
-    bool k2_split = false;  // MMBA_K2_FUSED=0: separate Jacobian and normal-equation passes
-    bool fold_ok = true;    // MMBA_NE_FOLD=0: lam = 0 bundle factor launched (k_bundle_factor)
-    // MMBA_TAIL_REDUCE=1: reductions folded into their producers' last
-    // workgroup (one ticket counter) instead of a k_reduce_multi launch.
-    // Measured slower on C4 (k_residual<JP> 16.7 -> 30.5 us, k_ne_bnd_jb
-    // +7 us): 782 / 196 arrivals on one device-scope counter cost more than
-    // the launch they save (MI355X guide "fanin", ~12 ns per atomic)
-    bool tail_reduce = false;
+    // fixed choices of earlier A/B measurements (the alternatives stay in
+    // the source, compiled out): the fused Jacobian + normal-equation pass,
+    // the lam = 0 bundle factor formed in the bundle pass
+    static constexpr bool k2_split = false;
+    static constexpr bool fold_ok = true;
+    // reductions folded into their producers' last workgroup (one ticket
+    // counter) instead of a k_reduce_multi launch: measured slower on C4
+    // (k_residual<JP> 16.7 -> 30.5 us, k_ne_bnd_jb +7 us): 782 / 196 arrivals
+    // on one device-scope counter cost more than the launch they save (MI355X
+    // guide "fanin", ~12 ns per atomic)
+    static constexpr bool tail_reduce = false;
     // page-locked sequence word of the mirrored reductions (read_slots
-    // polls it, MMBA_SEQ_POLL=0: stream events)
+    // polls it)
     unsigned *h_seq = nullptr;
     unsigned seq_next = 0;
     bool seq_pending = false;  // the next mirrored read_slots polls h_seq
-    bool seq_poll = true;  // MMBA_SEQ_POLL=0: stream events
+    static constexpr bool seq_poll = true;  // (stream events: measured slower)
     int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
@@ -138,7 +141,7 @@ struct Plan {
     bool dense = false;
     int dld = 0;
     DenseSolver ds;
-    long long *d_probe = nullptr;  // MMBA_PROBE=1: band-kernel phase cycles
+    long long *d_probe = nullptr;  // MMBA_PATH_PROBE = 1: band-kernel phase cycles
     bool nloc_set = false;         // d_nloc stored by a fused Jacobian pass
     // single-workgroup triangular solves for narrow (banded) structures
     bool narrow = false;
@@ -204,7 +207,7 @@ struct Plan {
     int *d_fail = nullptr;
     unsigned int *d_ticket = nullptr;  // single-launch reduction ticket (zero between uses)
     double *h_scalar = nullptr;  // pinned
-    // MMBA_HOST_MIRROR=1: trial reductions write slots [0, SL_LAST] straight
+    // host mirror: trial reductions write slots [0, SL_LAST] straight
     // into h_scalar (the last k_reduce_multi block) and read_slots skips its
     // copy launch.  With a stream-event wait it measured 3 % slower per C4
     // solve (round 2); with the page-locked sequence word the LM thread polls
@@ -318,7 +321,7 @@ struct Plan {
         NSLOT = 28
     };
     void read_slots(int lo, int hi);
-    bool spin_wait = true;  // MMBA_SPIN_WAIT=0: blocking synchronisation
+    static constexpr bool spin_wait = true;  // (blocking synchronisation: slower)
     hipEvent_t ev_sync = nullptr;  // [lo, hi] inclusive, one D2H copy + sync
     double read_scalar(int slot = 0);
     void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
@@ -368,10 +371,10 @@ struct Plan {
     // enqueued behind a trial whose reduction restates the host's decision
     // (LmDec): it runs only when that decision takes the trial and goes on,
     // so the GPU starts the next iteration while the host reads the trial.
-    // MMBA_PRE_JAC=0: off.
+    // (cleared for the replay of a SpecMismatch solve)
     // the trial point's parameter pass fused into the bundle back
     // substitution of the damped solve (launch_backsub_trial);
-    // MMBA_TRIAL_FOLD=0: k_trial_prep
+    // otherwise k_trial_prep
     bool trial_fold_ok = false, trial_folded = false;
     int *d_trial_other = nullptr;
     int n_trial_other = 0;

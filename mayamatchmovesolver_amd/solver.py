@@ -391,6 +391,13 @@ def device_count() -> int:
     return int(lib().mmba_device_count())
 
 
+def set_path(key: int, value: int = -1) -> None:
+    """Test hook (``mmba_debug_set_path``): pin a plan-builder choice
+    (``abi.PATH_*``) for the plans and in-process communicators created
+    afterwards; -1 restores the builder's own choice."""
+    check(lib().mmba_debug_set_path(int(key), int(value)))
+
+
 def debug_band_solve(ctx: "Context", S: np.ndarray, nb: int, w: int, nG: int, parts: int = 0):
     """Test hook: solve S x = r-style systems with the device band + arrow
     Cholesky (``mmba_debug_band_solve``).  Returns a function r -> (x, ||L^-1 r||^2, P)."""

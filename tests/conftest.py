@@ -19,6 +19,17 @@ def oracle():
     return refcpu
 
 
+@pytest.fixture
+def paths():
+    """Pin plan-builder choices for one test (mmba_debug_set_path);
+    everything is restored afterwards.  paths(abi.PATH_X, value)."""
+    from mayamatchmovesolver_amd import abi
+    from mayamatchmovesolver_amd.solver import set_path
+    yield set_path
+    for k in range(1, abi.PATH_NUM):
+        set_path(k, -1)
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     from mayamatchmovesolver_amd import solver

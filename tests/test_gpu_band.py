@@ -37,7 +37,12 @@ CASES = [
     (500, 23, 0, 1), (2994, 23, 0, 0), (2994, 23, 0, 11), (2994, 23, 0, 24),
     (1000, 23, 5, 6), (1000, 40, 16, 4), (640, 60, 3, 1), (777, 80, 1, 1),
     (10, 2, 16, 1), (0, 0, 4, 1), (90, 5, 0, 9),
-    # P = -1: block cyclic reduction (csrc/mmba_bcr.hip), K = 8/16/24/32
+    # P = -1: the log-depth solvers -- parallel cyclic reduction
+    # (csrc/mmba_pcr.hip) without an arrow and K <= 24, block cyclic reduction
+    # (csrc/mmba_bcr.hip) otherwise, K = 8/16/24/32; P = -2: block cyclic
+    # reduction only
+    (2994, 23, 0, -2), (84, 6, 0, -2), (4096, 24, 0, -2), (90, 5, 0, -2), (7, 3, 0, -2),
+    (840, 6, 0, -2), (24 * 257, 24, 0, -1), (24 * 256 + 5, 23, 0, -1), (24, 23, 0, -1),
     (84, 6, 0, -1), (300, 6, 2, -1), (2994, 23, 0, -1), (1000, 23, 5, -1),
     (1000, 32, 16, -1), (10, 2, 16, -1), (0, 0, 4, -1), (90, 5, 0, -1),
     (7, 3, 0, -1), (777, 31, 1, -1), (1000, 16, 3, -1), (17, 8, 2, -1),
@@ -105,9 +110,10 @@ def test_dgemm_nt_in_place_panel(M, gpu_ctx):
     assert np.all(np.abs(got - A @ Li.T) <= 1e-13 * scale)
 
 
+@pytest.mark.parametrize("parts", [-1, -2])
 @pytest.mark.parametrize("nb,w,nG", [(2994, 23, 0), (500, 23, 3), (1000, 15, 0)])
 @pytest.mark.parametrize("where", ["odd_block", "even_block", "root", "arrow", "nan"])
-def test_bcr_indefinite_is_reported(nb, w, nG, where, gpu_ctx):
+def test_bcr_indefinite_is_reported(nb, w, nG, where, parts, gpu_ctx):
     """A non-positive (or NaN) pivot anywhere in the block cyclic reduction --
     a block eliminated at level 0, a block eliminated at a later level, the
     root block, the arrow corner -- is reported as a failed factorisation (the
@@ -123,6 +129,6 @@ def test_bcr_indefinite_is_reported(nb, w, nG, where, gpu_ctx):
     row = {"odd_block": K + 3, "even_block": 2 * K + 5, "root": 2, "arrow": nb + nG - 1,
            "nan": 4 * K + 1}[where]
     S[row, row] = np.nan if where == "nan" else -10.0 * abs(S[row, row])
-    solve = debug_band_solve(gpu_ctx, S, nb, w, nG, parts=-1)
+    solve = debug_band_solve(gpu_ctx, S, nb, w, nG, parts=parts)
     with pytest.raises(MmbaError, match="non-positive pivot"):
         solve(np.ones(nb + nG))

@@ -1,16 +1,27 @@
-"""The block-cyclic-reduction factorisation's code paths give the same solve
-bit for bit: the one-launch dataflow factor (default), the per-level
-launches (MMBA_BCR_DF=0) and the unblocked pivot chain (MMBA_BCR_CHOL=0) all
-perform the same floating-point operations in the same order, so x, fvec and
-the whole ||f|| trace must be identical (the VALU updates, MMBA_BCR_MFMA=0,
-sum in another order and are checked against numpy in test_gpu_band.py).  A hand-off race in the dataflow factor (a stale block read across
-workgroups) shows up here as a mismatch.  Scenes: the C4 structure (nG = 0,
-K = 8 and 24) through the whole solver; band + arrow systems (nG = 2..16,
-root of order K + 8 / K + 16, K = 16 / 24 / 32) through the band-solve hook."""
+"""The log-depth band solvers through the whole solver.
+
+Block cyclic reduction (csrc/mmba_bcr.hip; MMBA_PATH_PCR = 0 selects it for
+band systems without an arrow): its code paths give the same solve bit for
+bit -- the one-launch dataflow factor (default), the per-level launches
+(MMBA_PATH_BCR_DATAFLOW = 0) and the dataflow launches on 1 / 3 workgroups
+(MMBA_PATH_BCR_GRID: most items drawn by workgroups that already ran others,
+the forward-progress path) all perform the same floating-point operations in
+the same order, so x, fvec and the whole ||f|| trace must be identical.  A
+hand-off race in the dataflow factor (a stale block read across workgroups)
+shows up here as a mismatch.
+
+Parallel cyclic reduction (csrc/mmba_pcr.hip, the default without an
+arrow): repeatable bit for bit through one plan, against block cyclic
+reduction on the same scenes at 1e-9 (a different elimination order: a few
+ulps of the reduced step), and under eight concurrent solves.
+
+Scenes: the C4 structure (nG = 0, K = 8 and 24) through the whole solver;
+band + arrow systems (nG = 2..16, root of order K + 8 / K + 16, K = 16 / 24 /
+32) through the band-solve hook."""
 import numpy as np
 import pytest
 
-from mayamatchmovesolver_amd import synthetic as S
+from mayamatchmovesolver_amd import abi, synthetic as S
 from mayamatchmovesolver_amd.solver import Solver, debug_band_solve
 from tests.test_gpu_band import band_arrow_spd
 
@@ -21,22 +32,21 @@ SCENES = {
     "c4_wide": (3, dict(frames=64, scale=0.01, window=6, depth=(4.0, 10.0))),
 }
 VARIANTS = {
-    "levels": {"MMBA_BCR_DF": "0"},
-    "chain": {"MMBA_BCR_CHOL": "0"},
+    "levels": {abi.PATH_BCR_DATAFLOW: 0},
     # dataflow launches on 1 / 3 workgroups: most items are drawn (item
     # tickets) by workgroups that already ran others -- the forward-progress
     # path when few workgroups are resident
-    "grid1": {"MMBA_BCR_DF_GRID": "1"},
-    "grid3": {"MMBA_BCR_DF_GRID": "3"},
+    "grid1": {abi.PATH_BCR_GRID: 1},
+    "grid3": {abi.PATH_BCR_GRID: 3},
 }
-ENV_KEYS = ("MMBA_BCR_DF", "MMBA_BCR_MFMA", "MMBA_BCR_CHOL", "MMBA_BCR_DF_GRID")
 
 
-def run(prob, opt, ctx, monkeypatch, env):
-    for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def run(prob, opt, ctx, paths, choice, pcr=0):
+    for k in (abi.PATH_BCR_DATAFLOW, abi.PATH_BCR_GRID):
+        paths(k, -1)
+    paths(abi.PATH_PCR, pcr)
+    for k, v in choice.items():
+        paths(k, v)
     s = Solver(prob, opt, context=ctx)
     try:
         return s.solve()
@@ -45,27 +55,42 @@ def run(prob, opt, ctx, monkeypatch, env):
 
 
 @pytest.mark.parametrize("scene", list(SCENES))
-def test_bcr_variants_bitwise(scene, gpu_ctx, monkeypatch):
+def test_bcr_variants_bitwise(scene, gpu_ctx, paths):
     idx, kw = SCENES[scene]
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
-    ref = run(prob, opt, gpu_ctx, monkeypatch, {})
+    ref = run(prob, opt, gpu_ctx, paths, {})
     assert ref.result["success"], ref.result
-    for name, env in VARIANTS.items():
-        out = run(prob, opt, gpu_ctx, monkeypatch, env)
+    for name, choice in VARIANTS.items():
+        out = run(prob, opt, gpu_ctx, paths, choice)
         np.testing.assert_array_equal(out.fnorm_trace, ref.fnorm_trace, err_msg=name)
         np.testing.assert_array_equal(out.x, ref.x, err_msg=name)
         np.testing.assert_array_equal(out.fvec, ref.fvec, err_msg=name)
 
 
-def test_bcr_dataflow_repeatable(gpu_ctx, monkeypatch):
-    """Ten solves through one plan (the dataflow factor reuses its flags with
-    a new epoch per launch): identical results every time."""
+@pytest.mark.parametrize("scene", list(SCENES))
+def test_pcr_against_bcr(scene, gpu_ctx, paths):
+    """Parallel against block cyclic reduction: the same LM path (reason,
+    counts) and the same solution up to the reduced step's roundoff."""
+    idx, kw = SCENES[scene]
+    prob = S.make_config(idx, **kw)
+    opt = S.config_options(prob)
+    bcr = run(prob, opt, gpu_ctx, paths, {}, pcr=0)
+    pcr = run(prob, opt, gpu_ctx, paths, {}, pcr=-1)
+    for k in ("reason_number", "iterations", "outer_iterations", "function_evals"):
+        assert pcr.result[k] == bcr.result[k], k
+    np.testing.assert_allclose(pcr.fnorm_trace, bcr.fnorm_trace, rtol=1e-9)
+    assert np.max(np.abs(pcr.x - bcr.x) / np.maximum(np.abs(bcr.x), 1e-3)) <= 1e-7
+
+
+@pytest.mark.parametrize("pcr", [0, -1])
+def test_dataflow_repeatable(pcr, gpu_ctx, paths):
+    """Ten solves through one plan (the dataflow launches reuse their flags
+    with a new epoch per launch): identical results every time."""
     idx, kw = SCENES["c4"]
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
-    for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+    paths(abi.PATH_PCR, pcr)
     s = Solver(prob, opt, context=gpu_ctx)
     try:
         ref = s.solve()
@@ -79,15 +104,13 @@ def test_bcr_dataflow_repeatable(gpu_ctx, monkeypatch):
 
 @pytest.mark.parametrize("nb,w,nG", [(1000, 23, 5), (1000, 32, 16), (2880, 11, 2),
                                      (1000, 16, 3), (24 * 65, 24, 1)])
-def test_bcr_band_arrow_dataflow_bitwise(nb, w, nG, gpu_ctx, monkeypatch):
+def test_bcr_band_arrow_dataflow_bitwise(nb, w, nG, gpu_ctx, paths):
     S_ = band_arrow_spd(nb, w, nG, seed=nb + w + nG)
     r = np.random.default_rng(nG).standard_normal(nb + nG)
     outs = []
-    for env in ({}, {"MMBA_BCR_DF": "0"}):
-        monkeypatch.delenv("MMBA_BCR_DF", raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        x, yn, _used = debug_band_solve(gpu_ctx, S_, nb, w, nG, -1)(r)
+    for df in (-1, 0):
+        paths(abi.PATH_BCR_DATAFLOW, df)
+        x, yn, _used = debug_band_solve(gpu_ctx, S_, nb, w, nG, -2)(r)
         outs.append((x, yn))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
@@ -113,18 +136,20 @@ def _threads(n, fn):
     return outs
 
 
-def test_bcr_dataflow_concurrent_full_c4(gpu_ctx, monkeypatch):
-    """Eight full-size C4 solves (125 band blocks: 63 workgroups of 256
-    threads per dataflow factorisation, 125 per backward solve) at once, one
-    host thread and one stream each: about 500 workgroups that each fill a CU
-    compete for 256 CUs, so the dataflow launches cannot all be resident.
-    With item tickets every wait still ends: each solve must equal the solo
-    solve bit for bit (a timed-out wait would fail the solve or switch the
-    plan to the per-level launches, whose bits are the same -- so the flag is
-    checked too)."""
+@pytest.mark.parametrize("pcr", [0, -1])
+def test_dataflow_concurrent_full_c4(pcr, gpu_ctx, paths):
+    """Eight full-size C4 solves (125 band blocks) at once, one host thread
+    and one stream each.  Block cyclic reduction: 63 workgroups of 256
+    threads per dataflow factorisation, 125 per backward solve, about 500
+    workgroups that each fill a CU compete for 256 CUs, so the dataflow
+    launches cannot all be resident; with item tickets every wait still ends.
+    Parallel cyclic reduction (125 resident workgroups per launch): the
+    launches of the eight streams are ordered device-side (mmba_pcr.hip).
+    Each solve must equal the solo solve bit for bit (a timed-out wait would
+    fail the solve or switch the plan to the per-level launches, whose bits
+    differ or whose flag is checked)."""
     from mayamatchmovesolver_amd.solver import Context
-    for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+    paths(abi.PATH_PCR, pcr)
     prob = S.make_config(3)
     opt = S.config_options(prob)
     s = Solver(prob, opt, context=gpu_ctx)

@@ -129,13 +129,13 @@ def test_config_parity(idx, kw, oracle, gpu_ctx):
     check_solve(prob, opt, oracle, gpu_ctx)
 
 
-@pytest.mark.parametrize("dense", ["0", "1"])
-def test_reduced_system_dense_and_tiled(dense, oracle, gpu_ctx, monkeypatch):
+@pytest.mark.parametrize("dense", [0, 1])
+def test_reduced_system_dense_and_tiled(dense, oracle, gpu_ctx, paths):
     """The C3 structure (bundles tracked by several cameras across the whole
     shot: an almost dense reduced system) through both reduced-system solvers:
-    the tiled Cholesky and the dense blocked Cholesky (rocBLAS trsm/syrk
-    trailing updates, one-wave panel kernel), each against the oracle."""
-    monkeypatch.setenv("MMBA_DENSE", dense)
+    the tiled Cholesky and the dense blocked Cholesky (fp64 MFMA GEMM / SYRK
+    trailing updates, two-wave panel kernel), each against the oracle."""
+    paths(abi.PATH_DENSE, dense)
     prob = S.make_config(2, frames=8, scale=0.002)
     opt = S.config_options(prob)
     check_solve(prob, opt, oracle, gpu_ctx)

@@ -8,7 +8,7 @@ Bar: per frame the same reason code and evaluation counts, final x within
 import numpy as np
 import pytest
 
-from mayamatchmovesolver_amd import synthetic as S
+from mayamatchmovesolver_amd import abi, synthetic as S
 from mayamatchmovesolver_amd.problem import Problem
 from mayamatchmovesolver_amd.solver import solve_per_frame
 
@@ -95,9 +95,9 @@ def test_per_frame_matches_oracle(idx, kw, conc, oracle):
 
 
 @pytest.fixture(params=["batched", "per-frame plans"])
-def path(request, monkeypatch):
+def path(request, paths):
     if request.param != "batched":
-        monkeypatch.setenv("MMBA_PERFRAME_BATCH", "0")
+        paths(abi.PATH_PERFRAME_BATCH, 0)
     return request.param
 
 

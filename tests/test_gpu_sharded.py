@@ -8,7 +8,7 @@ import threading
 import numpy as np
 import pytest
 
-from mayamatchmovesolver_amd import synthetic as S
+from mayamatchmovesolver_amd import abi, synthetic as S
 from mayamatchmovesolver_amd.solver import Comm, Context, Solver
 
 pytestmark = pytest.mark.gpu
@@ -72,21 +72,21 @@ def check_shards_agree(outs):
 
 # reduced-system solve of a sharded plan: S all-reduced and factored by block
 # cyclic reduction on every shard (default), or the partitioned band chain
-# with an all-reduced separator system (MMBA_SHARD_BCR=0)
-SOLVES = {"bcr": "1", "partitioned": "0"}
+# with an all-reduced separator system (MMBA_PATH_SHARD_BCR = 0)
+SOLVES = {"bcr": -1, "partitioned": 0}
 
 
 # summation order of the in-process all-reduce: rank order, or the ring
 # reduce-scatter order RCCL's ring all-reduce uses (mmba_comm.cpp)
-ORDERS = {"rank": "0", "ring": "1"}
+ORDERS = {"rank": 0, "ring": 1}
 
 
 @pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("solve", list(SOLVES))
 @pytest.mark.parametrize("idx,kw,nshards", CASES)
-def test_sharded_matches_oracle(idx, kw, nshards, solve, order, oracle, monkeypatch):
-    monkeypatch.setenv("MMBA_SHARD_BCR", SOLVES[solve])
-    monkeypatch.setenv("MMBA_LOCAL_RING", ORDERS[order])
+def test_sharded_matches_oracle(idx, kw, nshards, solve, order, oracle, paths):
+    paths(abi.PATH_SHARD_BCR, SOLVES[solve])
+    paths(abi.PATH_LOCAL_RING, ORDERS[order])
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
     xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt)
@@ -105,13 +105,13 @@ def test_sharded_matches_oracle(idx, kw, nshards, solve, order, oracle, monkeypa
 
 
 @pytest.mark.parametrize("solve", list(SOLVES))
-def test_sharded_ba_three_shards_structure(solve, gpu_ctx, monkeypatch):
+def test_sharded_ba_three_shards_structure(solve, gpu_ctx, paths):
     """3 shards (one with separators on both sides) on a bundle-Schur scene,
     against the unsharded GPU solve.  This scene is not conditioned well
     enough for a 1e-6 comparison (a rejected trial point moves by 1.4e-6), so
     the check is structural: same reason and counts, trace within 1e-5, x
     within 1e-4 (decomposition errors show up at 1e-2)."""
-    monkeypatch.setenv("MMBA_SHARD_BCR", SOLVES[solve])
+    paths(abi.PATH_SHARD_BCR, SOLVES[solve])
     prob = S.make_config(3, frames=54, scale=0.006, **WC)
     opt = S.config_options(prob)
     s = Solver(prob, opt, context=gpu_ctx)
@@ -159,7 +159,7 @@ def test_sharded_ba_many_shards(nshards, gpu_ctx):
 @pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("nshards", [2, 4, 8])
 @pytest.mark.parametrize("scene", ["c4", "wc"])
-def test_sharded_ba_x_before_the_valley(scene, nshards, order, gpu_ctx, monkeypatch):
+def test_sharded_ba_x_before_the_valley(scene, nshards, order, gpu_ctx, paths):
     """x itself, on the headline C4 structure (4-frame tracks at depth
     20-200) and on the 6-frame variant, sharded against unsharded, with the
     evaluation budget capped at 2 (x0 and one full LM step): past that the
@@ -168,7 +168,7 @@ def test_sharded_ba_x_before_the_valley(scene, nshards, order, gpu_ctx, monkeypa
     Schur / reduced solve across every shard boundary, so a wrong block, a
     missing halo term or a wrong separator shows up in x at 1e-3..1e-2; the
     bar here is 1e-6 relative on every component."""
-    monkeypatch.setenv("MMBA_LOCAL_RING", ORDERS[order])
+    paths(abi.PATH_LOCAL_RING, ORDERS[order])
     kw = WC if scene == "wc" else {}
     prob = S.make_config(3, frames=20 * nshards, scale=0.002 * nshards, **kw)
     opt = S.config_options(prob, iterations=2)
@@ -209,11 +209,11 @@ def test_rccl_communicator_one_rank(gpu_ctx):
 
 @pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("n", [2, 3, 8])
-def test_local_group_allreduce(n, order, monkeypatch):
+def test_local_group_allreduce(n, order, paths):
     """The in-process group's all-reduce (sum in rank or ring order, max) on
     n host threads, each with its own stream: every rank gets the same bits,
     equal to the numpy sum in that order."""
-    monkeypatch.setenv("MMBA_LOCAL_RING", ORDERS[order])
+    paths(abi.PATH_LOCAL_RING, ORDERS[order])
     comms = Comm.local_group(n)
     ctxs = [Context(0) for _ in range(n)]
     rng = np.random.default_rng(7)

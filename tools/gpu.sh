@@ -5,6 +5,7 @@
 #   smoke             __graft_entry__.smoke()
 #   bench             the default bench line (C4, CPU baseline, PMC traffic)
 #   benchcfg:I        bench line of configs[I] (no CPU baseline)
+#   benchpath:N=V     default-config bench line with a pinned path (--path N=V)
 #   prof              rocprofv3 --kernel-trace --stats of the default bench
 #   pmc               FETCH_SIZE / WRITE_SIZE passes of the default bench
 #   iter              kernel traces + one-iteration timelines of C2 / C4 / C5
@@ -33,6 +34,10 @@ for step in "$@"; do
       c=${step#benchcfg:}
       timeout -k 10 400 python -u bench.py --config "$c" --steps 8 --warmup 3 --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
       cat "$OUT/bench_$c.json" ;;
+    benchpath:*)
+      pv=${step#benchpath:}
+      timeout -k 10 400 python -u bench.py --path "$pv" --steps 8 --warmup 3 --no-cpu-baseline --no-traffic > "$OUT/bench_$pv.json" 2> "$OUT/bench_$pv.err" || { tail "$OUT/bench_$pv.err"; exit 1; }
+      cat "$OUT/bench_$pv.json" ;;
     prof)
       cd /tmp && cd "$ROOT"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c4 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" || { tail "$OUT/prof_bench.err"; exit 1; }

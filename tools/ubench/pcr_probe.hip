@@ -1,0 +1,122 @@
+// Microbenchmark: k_pcr_solve<24> (mmba_pcr.hip) on a C4-sized band system
+// (nb = 2994, w = 23: 125 blocks, 7 levels), warm, with the phase probe of
+// block nblk / 2: per level, the 100 MHz wall-clock time of the pivot chain,
+// the publication, the wait for the neighbours, staging, the W products and
+// the update; plus HIP-event time per launch.  Build (from this directory):
+//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -I../../mayamatchmovesolver_amd/csrc \
+//     pcr_probe.hip -o pcr_probe
+#include "mmba_pcr.hip"
+
+#include <cstdio>
+#include <vector>
+
+using namespace mmba;
+
+int main(int argc, char **argv) {
+    const int nb = argc > 1 ? std::atoi(argv[1]) : 2994, w = 23, K = 24;
+    const int W1 = w + 1;
+    std::vector<double> Bd((size_t)nb * W1, 0.);
+    for (int i = 0; i < nb; ++i)
+        for (int k = 0; k < W1; ++k) {
+            const int c = i - w + k;
+            if (c < 0) continue;
+            Bd[(size_t)i * W1 + k] = (c == i) ? 3.0 * w : 0.5 * std::sin(0.37 * i + 1.3 * c);
+        }
+    PcrDev P;
+    P.K = K;
+    P.nb = nb;
+    P.w = w;
+    P.nblk = (nb + K - 1) / K;
+    int L = 0;
+    while ((1 << L) < P.nblk) ++L;
+    P.nlev = L;
+    double *dBd, *r, *x;
+    hipMalloc(&dBd, Bd.size() * 8);
+    hipMemcpy(dBd, Bd.data(), Bd.size() * 8, hipMemcpyHostToDevice);
+    P.Bd = dBd;
+    const size_t ps = (size_t)2 * K * (K + 1) + K * K;
+    hipMalloc(&P.pub, (size_t)L * P.nblk * ps * 8);
+    hipMalloc(&P.wlog, (size_t)(L + 1) * P.nblk * 3 * K * K * 8);
+    hipMalloc(&P.rpub, (size_t)L * P.nblk * 2 * K * 8);
+    hipMalloc(&P.part, P.nblk * 8);
+    hipMalloc(&P.fflag, (size_t)L * P.nblk * 4);
+    hipMalloc(&P.rflag, (size_t)L * P.nblk * 4);
+    hipMemset(P.fflag, 0, (size_t)L * P.nblk * 4);
+    hipMemset(P.rflag, 0, (size_t)L * P.nblk * 4);
+    hipMalloc(&P.flev, P.nblk * 4);
+    hipMalloc(&r, nb * 8);
+    hipMalloc(&x, nb * 8);
+    std::vector<double> hr(nb, 1.0);
+    hipMemcpy(r, hr.data(), nb * 8, hipMemcpyHostToDevice);
+    int *fail;
+    hipMalloc(&fail, 4);
+    hipMemset(fail, 0, 4);
+    long long *probe;
+    hipMalloc(&probe, 8 * 64 * 8);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int reps = 20;
+    float best = 1e30f, sum = 0.f;
+    for (int it = 0; it < reps; ++it) {
+        hipMemset(probe, 0, 8 * 64 * 8);
+        hipEventRecord(a);
+        k_pcr_solve<24><<<P.nblk, 256>>>(P, r, x, nullptr, 1000u + it, fail, probe);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, a, b);
+        if (it >= 2) {
+            best = std::min(best, ms);
+            sum += ms;
+        }
+    }
+    int hf = 0;
+    hipMemcpy(&hf, fail, 4, hipMemcpyDeviceToHost);
+    {  // residual of the solve: max |S x - r| / max |r| (S symmetric, band lower)
+        std::vector<double> hx(nb), res(nb, 0.);
+        hipMemcpy(hx.data(), x, nb * 8, hipMemcpyDeviceToHost);
+        for (int i = 0; i < nb; ++i)
+            for (int k = 0; k < W1; ++k) {
+                const int c = i - w + k;
+                if (c < 0) continue;
+                const double v = Bd[(size_t)i * W1 + k];
+                res[i] += v * hx[c];
+                if (c != i) res[c] += v * hx[i];
+            }
+        double mr = 0.;
+        for (int i = 0; i < nb; ++i) mr = std::max(mr, std::fabs(res[i] - hr[i]));
+        std::printf("max |S x - r| = %.3e\n", mr);
+    }
+    std::printf("nb %d nblk %d levels %d: k_pcr_solve<24> best %.1f us, mean %.1f us (fail %d)\n",
+                nb, P.nblk, L, best * 1e3, sum / (reps - 2) * 1e3, hf);
+    std::vector<long long> t(8 * 64);
+    hipMemcpy(t.data(), probe, t.size() * 8, hipMemcpyDeviceToHost);
+    const long long t00 = t[0];
+    std::printf("block %d, us from its level-0 start (chain | products | publish+log+wait | update):\n",
+                P.nblk / 2);
+    for (int l = 0; l <= L; ++l) {
+        const long long *q = &t[l * 8];
+        if (!q[0]) break;
+        std::printf("  level %d start %6.2f:", l, (q[0] - t00) / 100.);
+        for (int ph = 1; ph <= 4 && q[ph]; ++ph) std::printf(" %5.2f", (q[ph] - q[ph - 1]) / 100.);
+        std::printf("\n");
+    }
+    // the right-hand-side pass
+    float rbest = 1e30f;
+    int *mask;
+    hipMalloc(&mask, nb * 4);
+    std::vector<int> ones(nb, 1);
+    hipMemcpy(mask, ones.data(), nb * 4, hipMemcpyHostToDevice);
+    for (int it = 0; it < 10; ++it) {
+        hipEventRecord(a);
+        k_pcr_rhs<24><<<P.nblk, 64>>>(P, r, mask, P.part, 5000u + it, fail);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, a, b);
+        if (it >= 2) rbest = std::min(rbest, ms);
+    }
+    std::printf("k_pcr_rhs<24> best %.1f us\n", rbest * 1e3);
+    return 0;
+}
