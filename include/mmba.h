@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 6
+#define MMBA_ABI_VERSION 7
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -238,6 +238,38 @@ typedef struct mmba_problem {
      * input layers per lens; lens_input NULL = no layers (ABI <= 4). */
     const int32_t *lens_input;        /* [num_lenses] */
     const double *lens_input_values;  /* [14*num_lenses] */
+
+    /* ---- ABI 7 ---- */
+    /* The reference's lens index arithmetic, reproduced
+     * for any lens layout.  The solver keeps num_frames clones of every lens
+     * model, instance (l, f) at lensModelList[l*F + f], and two lookup lists
+     * built as markerFrame[i*F + f] = instance (cam_lens[mkr_cam[i]], f) and
+     * attrFrame[a*F + f] = instance (lens of attrList entry a, f)
+     * (maya_lens_model_utils.cpp:655-662, 782-799, 836-851), but reads them at
+     * markerIndex + frameIndex (adjust_measureErrors.cpp:244, 463) and at
+     * attrIndex + frameIndex / attrIndex + j (adjust_setParameters.cpp:
+     * 113-121, 206-214).  So observation (marker i, frame f) is distorted by
+     * instance (cam_lens[mkr_cam[(i+f) / F]], (i+f) % F), and solving
+     * attribute a at frame g writes its value into the slot of its type of
+     * instance (lens of attrList entry (a+g) / F, (a+g) % F) -- a static
+     * attribute for every g < F, entries without a lens skipped
+     * (setLensModelAttributeValue ignores a null model); the last parameter
+     * written wins.  A slot no parameter writes keeps the value the plug
+     * model was cloned with (lens_input_values, or each slot's attribute at
+     * frame 0; lens attributes are never read per frame, Appendix B11).  With
+     * one lens shared by every camera and its attributes first in attrList,
+     * every instance holds the same values and this is the plain model.
+     *   param_ref_attr[p] = paramToAttrList[p].first, the attribute's index
+     *                       in the solver's attrList (NULL: the attributes
+     *                       numbered in order of first appearance in the
+     *                       parameter list, which is attrList's order when
+     *                       every entry has a parameter);
+     *   ref_attr_lens[a]  = the lens whose attribute attrList entry a is, -1
+     *                       if it is not a lens attribute (NULL: from
+     *                       lens_attrs). */
+    const int32_t *param_ref_attr;  /* [num_params] */
+    int32_t num_ref_attrs;
+    const int32_t *ref_attr_lens;   /* [num_ref_attrs] */
 } mmba_problem;
 
 /* SolverOptions subset that the LM path reads (adjust_data.h:133-185). */

@@ -286,11 +286,23 @@ bool FlatScene::build(const SolverInputs &in, SceneReader &rd) {
         }
         param_attr.push_back(it->second);
         param_frame.push_back(in.paramToAttrList[p].second);
+        param_ref_attr.push_back(in.paramToAttrList[p].first);
         param_min.push_back(attr.min_value);
         param_max.push_back(attr.max_value);
         param_offset.push_back(attr.offset);
         param_scale.push_back(attr.scale);
         param_weight.push_back(p < in.paramWeightList.size() ? in.paramWeightList[p] : 1.0);
+    }
+
+    // the lens of every attrList entry: an attribute a lens slot reads
+    // (attrFrameToLensModelList, maya_lens_model_utils.cpp:836-851)
+    for (const AttrDesc &a : in.attrs) {
+        int32_t l = -1;
+        auto it = attr_id.find(long_name(a.node, a.attr));
+        if (it != attr_id.end())
+            for (size_t q = 0; q < lens_attrs.size() && l < 0; ++q)
+                if (lens_attrs[q] == it->second) l = static_cast<int32_t>(q / MMBA_LENS_NUM_ATTRS);
+        ref_attr_lens.push_back(l);
     }
 
     // ---- stiffness / smoothness rows, read at the current time ----
@@ -348,7 +360,10 @@ mmba_problem FlatScene::problem() const {
     bool layered = false;
     for (int32_t v : lens_input) layered = layered || v >= 0;
     p.lens_input = layered ? lens_input.data() : nullptr;
-    p.lens_input_values = layered ? lens_input_values.data() : nullptr;  // at the current time
+    // every lens's slots at the current time: the values the solver's lens
+    // clones start from (input layers for the whole solve; a camera lens's
+    // slots no parameter writes, B3 / B11)
+    p.lens_input_values = lens_type.empty() ? nullptr : lens_input_values.data();
     p.num_bundles = static_cast<int32_t>(bnd_tfm.size());
     p.bnd_tfm = bnd_tfm.data();
     p.num_markers = static_cast<int32_t>(mkr_cam.size());
@@ -367,6 +382,9 @@ mmba_problem FlatScene::problem() const {
     p.param_offset = param_offset.data();
     p.param_scale = param_scale.data();
     p.param_weight = param_weight.data();
+    p.param_ref_attr = param_ref_attr.data();
+    p.num_ref_attrs = static_cast<int32_t>(ref_attr_lens.size());
+    p.ref_attr_lens = ref_attr_lens.data();
     p.num_stiff = static_cast<int32_t>(stiff_attr.size());
     p.stiff_attr = stiff_attr.data();
     p.stiff_frame = stiff_frame.data();
@@ -401,16 +419,9 @@ std::vector<uint8_t> FlatScene::plan_key(const mmba_options &o) const {
     put(k, lens_type);
     put(k, lens_attrs);
     put(k, lens_input);
-    {  // the input layers' values are constants a plan captures (not the
-       // camera lenses' own, which are attribute values refreshed per solve)
-        std::vector<double> layer_vals;
-        for (size_t l = 0; l < lens_input.size(); ++l)
-            if (std::find(lens_input.begin(), lens_input.end(), (int32_t)l) != lens_input.end())
-                layer_vals.insert(layer_vals.end(),
-                                  lens_input_values.begin() + MMBA_LENS_NUM_ATTRS * l,
-                                  lens_input_values.begin() + MMBA_LENS_NUM_ATTRS * (l + 1));
-        put(k, layer_vals);
-    }
+    // every lens's plug values are constants a plan captures (input layers,
+    // and the camera lenses' slots no parameter writes, mmba.h ABI 7)
+    put(k, lens_input_values);
     put(k, bnd_tfm);
     put(k, mkr_cam);
     put(k, mkr_bnd);
@@ -420,6 +431,8 @@ std::vector<uint8_t> FlatScene::plan_key(const mmba_options &o) const {
     put(k, obs_weight);
     put(k, param_attr);
     put(k, param_frame);
+    put(k, param_ref_attr);
+    put(k, ref_attr_lens);
     put(k, param_min);
     put(k, param_max);
     put(k, param_offset);

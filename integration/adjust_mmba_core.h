@@ -125,6 +125,9 @@ struct FlatScene {
     std::vector<int32_t> obs_marker, obs_frame;
     std::vector<double> obs_xy, obs_weight;
     std::vector<int32_t> param_attr, param_frame;
+    // ABI 7: paramToAttrList[p].first and the lens of each
+    // attrList entry (-1: not an attribute of a lens the cameras use)
+    std::vector<int32_t> param_ref_attr, ref_attr_lens;
     std::vector<double> param_min, param_max, param_offset, param_scale, param_weight;
     std::vector<int32_t> stiff_attr, stiff_frame, smooth_attr, smooth_frame;
     std::vector<double> stiff_weight, stiff_variance, stiff_value;

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # mmba_debug_set_path keys (test hook: pin a plan-builder choice)
 PATH_PCR = 1
@@ -120,6 +120,10 @@ class MmbaProblem(C.Structure):
         # ---- ABI 5 ----
         ("lens_input", _i32p),
         ("lens_input_values", _f64p),
+        # ABI 7: the reference's lens index arithmetic (Appendix B3)
+        ("param_ref_attr", _i32p),
+        ("num_ref_attrs", C.c_int32),
+        ("ref_attr_lens", _i32p),
     ]
 
 

@@ -901,4 +901,25 @@ MMBA_DEV int obs_lens(const DevProblem &P, int cam, int &lens) {
     return lens >= 0 ? P.lens_type[lens] : MMBA_LENS_NONE;
 }
 
+// Lens model type of observation i's lens instance (mmba.h ABI 7: the
+// instance markerFrameToLensModelList[markerIndex + frameIndex] names), 0
+// without one.
+MMBA_DEV int obs_lens_inst(const DevProblem &P, int i, int &inst) {
+    if (!P.obs_inst) return MMBA_LENS_NONE;
+    inst = P.obs_inst[i];
+    return inst >= 0 ? P.lens_type[P.inst_lens[inst]] : MMBA_LENS_NONE;
+}
+
+// The coefficients lens instance `inst` holds (absent slots: the plug
+// model's value, which is the model default for a slot without attribute).
+MMBA_DEV void inst_coeffs(const DevProblem &P, int inst, const Override &ov, double *c) {
+    const int *ia = &P.inst_attr[MMBA_LENS_NUM_ATTRS * inst];
+    const int *fa = &P.inst_frame[MMBA_LENS_NUM_ATTRS * inst];
+    const double *va = &P.inst_val[MMBA_LENS_NUM_ATTRS * inst];
+#pragma unroll
+    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
+        c[k] = ia[k] < 0 ? va[k] : attr_get(P, ia[k], fa[k], 0., ov);
+    if (P.lens_type[P.inst_lens[inst]] == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.;  // no rescale slot
+}
+
 }  // namespace mmba

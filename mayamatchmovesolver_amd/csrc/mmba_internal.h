@@ -282,8 +282,18 @@ struct DevProblem {
     // is fast and nG == 0)
     const int *obs_bpos;
     double *JB;
-    // per camera lens parameter lists
+    // per camera lens parameter lists (the batched per-frame solve, where
+    // the reference solves one frame at a time and no index mixes)
     const int *cam_lpar_off, *cam_lpar;
+    // lens instances (mmba.h ABI 7): observation i is
+    // distorted by instance obs_inst[i] (-1: none) of lens inst_lens[j]; slot
+    // k of instance j reads attribute inst_attr[14 j + k] at frame
+    // inst_frame[14 j + k] (the parameter the reference's setParameters
+    // leaves in that slot), or the plug model's value inst_val[14 j + k] when
+    // inst_attr is -1; the instance's lens parameters (ascending ids) are
+    // inst_lpar[inst_lpar_off[j] ..)
+    const int *obs_inst, *inst_lens, *inst_attr, *inst_frame, *inst_lpar_off, *inst_lpar;
+    const double *inst_val;
     // parameters
     const int *p_attr, *p_frame, *p_class, *p_pos, *p_both, *p_blk;
     const double *p_min, *p_max, *p_off, *p_scale;

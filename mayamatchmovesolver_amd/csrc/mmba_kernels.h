@@ -7,6 +7,10 @@
 
 namespace mmba {
 
+// threads per workgroup of k_ne_bnd_jb: one epilogue partial column per
+// workgroup (the bundle columns of the reductions after the Jacobian)
+constexpr int NE_BND_TPB = 64;
+
 void launch_param_prep(hipStream_t s, const DevProblem &P, const double *x, double *ext,
                        double *ext_pert, double *step, int solver_type, double delta,
                        double eps_dif);

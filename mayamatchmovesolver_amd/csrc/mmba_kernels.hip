@@ -464,7 +464,6 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
         const int cf = P.obs_cf[i];
         const int b = P.obs_bnd[i];
         const int fr = P.obs_frame[i];
-        const int cam = P.obs_cam[i];
         const Override none{-1, 0.};
         double bp[3];
         if (FAST) {
@@ -476,9 +475,9 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
             base_bundle(P, b, fr, bp);
         }
         double lc[MMBA_LENS_NUM_ATTRS];
-        int lens = -1;
-        const int hl = FAST ? MMBA_LENS_NONE : obs_lens(P, cam, lens);
-        if (hl) lens_coeffs(P, lens, fr, none, lc);
+        int inst = -1;
+        const int hl = FAST ? MMBA_LENS_NONE : obs_lens_inst(P, i, inst);
+        if (hl) inst_coeffs(P, inst, none, lc);
         const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
         double rloc[RS ? CAMREC : 1];
         if constexpr (RS) {
@@ -651,16 +650,15 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     const int cf = P.obs_cf[i];
     const int b = P.obs_bnd[i];
     const int fr = P.obs_frame[i];
-    const int cam = P.obs_cam[i];
     const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
     const Override none{-1, 0.};
     const int4 p4 = P.bnd_p4[b];
     double bp0[3];
     base_bundle(P, b, fr, bp0);
     double lc0[MMBA_LENS_NUM_ATTRS];
-    int lens = -1;
-    const int hl = obs_lens(P, cam, lens);
-    if (hl) lens_coeffs(P, lens, fr, none, lc0);
+    int inst = -1;
+    const int hl = obs_lens_inst(P, i, inst);
+    if (hl) inst_coeffs(P, inst, none, lc0);
     const int voff = P.cf_var_off[cf];
     const int nvar = P.cf_var_off[cf + 1] - voff;
     const double *rec0 = &recs[(size_t)voff * CAMREC];
@@ -784,16 +782,17 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
             return residual_l(P, rec0, bq, mx, my, sw, hl, lc0);
         });
     }
-    // lens parameters of this camera's lens
+    // the lens parameters this observation's lens instance holds (an
+    // instance slot has one attribute, so overriding by attribute moves only
+    // the slot the parameter writes)
     if (hl) {
-        for (int q = P.cam_lpar_off[cam]; q < P.cam_lpar_off[cam + 1] && l < LMAX; ++q) {
-            const int p = P.cam_lpar[q];
-            if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
+        for (int q = P.inst_lpar_off[inst]; q < P.inst_lpar_off[inst + 1] && l < LMAX; ++q) {
+            const int p = P.inst_lpar[q];
             double lc[MMBA_LENS_NUM_ATTRS];
-            lens_coeffs(P, lens, fr, Override{P.p_attr[p], ext_pert[p]}, lc);
+            inst_coeffs(P, inst, Override{P.p_attr[p], ext_pert[p]}, lc);
             emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, lc), step[p], [&]() {
                 double lq[MMBA_LENS_NUM_ATTRS];
-                lens_coeffs(P, lens, fr, Override{P.p_attr[p], CB.ext_pert[p]}, lq);
+                inst_coeffs(P, inst, Override{P.p_attr[p], CB.ext_pert[p]}, lq);
                 return residual_l(P, rec0, bp0, mx, my, sw, hl, lq);
             });
         }
@@ -1356,10 +1355,13 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
 }
 
 // Fast bundles, no global parameters: Abb and gB from the per-observation
-// block records, same summation order as k_ne_bnd.
-__global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, double *g,
-                                                   NeEpi E) {
-    __shared__ double red[3][256];
+// block records, same summation order as k_ne_bnd.  One thread per bundle,
+// NE_BND_TPB threads per workgroup (C4: 782 workgroups over 256 CUs, so
+// several waves per CU hide the record loads); a bundle's records are loaded
+// four at a time before they are accumulated (C4's bundles have four).
+__global__ void __launch_bounds__(NE_BND_TPB) k_ne_bnd_jb(DevProblem P, double *Abb, double *g,
+                                                          NeEpi E) {
+    __shared__ double red[3][NE_BND_TPB];
     const int b = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     const int4 p4 = b < P.nB ? P.bnd_p4[b] : make_int4(-1, -1, -1, 0);
     const int pb = p4.w;
@@ -1367,16 +1369,28 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
     if (pb > 0) {
         double A[PBMAX][PBMAX] = {};
         double gb[PBMAX] = {};
-        for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-            const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)q * 8]);
-            const double4 u = src[0], v = src[1];
-            const double jx[3] = {u.x, u.z, v.x}, jy[3] = {u.y, u.w, v.y};
-            const double fx = v.z, fy = v.w;
+        const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
+        for (int qb = q0; qb < q1; qb += 4) {
+            double4 u[4], v[4];
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
+            for (int r = 0; r < 4; ++r) {
+                if (qb + r < q1) {
+                    const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)(qb + r) * 8]);
+                    u[r] = src[0];
+                    v[r] = src[1];
+                }
+            }
 #pragma unroll
-                for (int c = 0; c < 3; ++c) A[a][c] += jx[a] * jx[c] + jy[a] * jy[c];
-                gb[a] += jx[a] * fx + jy[a] * fy;
+            for (int r = 0; r < 4; ++r) {
+                if (qb + r >= q1) break;
+                const double jx[3] = {u[r].x, u[r].z, v[r].x}, jy[3] = {u[r].y, u[r].w, v[r].y};
+                const double fx = v[r].z, fy = v[r].w;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) A[a][c] += jx[a] * jx[c] + jy[a] * jy[c];
+                    gb[a] += jx[a] * fx + jy[a] * fy;
+                }
             }
         }
         double *Ab = &Abb[(size_t)b * 9];
@@ -1420,7 +1434,7 @@ __global__ void __launch_bounds__(256) k_ne_bnd_jb(DevProblem P, double *Abb, do
     red[1][threadIdx.x] = xn;
     red[2][threadIdx.x] = gm;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = NE_BND_TPB / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w) {
             red[0][threadIdx.x] = fmax(red[0][threadIdx.x], red[0][threadIdx.x + w]);
             red[1][threadIdx.x] += red[1][threadIdx.x + w];
@@ -3062,14 +3076,14 @@ __global__ void __launch_bounds__(256) k_reproject(DevProblem P, const double *_
                                                    double *pts, double *mkr) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.M) return;
-    const int cf = P.obs_cf[i], b = P.obs_bnd[i], fr = P.obs_frame[i], cam = P.obs_cam[i];
+    const int cf = P.obs_cf[i], b = P.obs_bnd[i], fr = P.obs_frame[i];
     const Override none{-1, 0.};
     double bp[3];
     base_bundle(P, b, fr, bp);
     double lc[MMBA_LENS_NUM_ATTRS];
-    int lens = -1;
-    const int hl = obs_lens(P, cam, lens);
-    if (hl) lens_coeffs(P, lens, fr, none, lc);
+    int inst = -1;
+    const int hl = obs_lens_inst(P, i, inst);
+    if (hl) inst_coeffs(P, inst, none, lc);
     const double *rec = &recs[(size_t)P.cf_var_off[cf] * CAMREC];
     double rloc[CAMREC];
     if (P.rs) {  // this observation's scanline pose
@@ -3619,7 +3633,7 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
     }
     if (P.nbs > 0) {
         if (P.JB)  // every solved bundle fast and no global parameters
-            k_ne_bnd_jb<<<nblk(P.nB, 256), 256, 0, s>>>(P, Abb, g, E);
+            k_ne_bnd_jb<<<nblk(P.nB, NE_BND_TPB), NE_BND_TPB, 0, s>>>(P, Abb, g, E);
         else
             k_ne_bnd<<<nblk(P.nB, 64), 64, 0, s>>>(P, J, jcol, nloc, f, Abb, Abg, g);
     }

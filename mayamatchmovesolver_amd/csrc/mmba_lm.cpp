@@ -320,7 +320,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.ticket = d_mticket;
         RedSpec &rf = epi.spec;
         rf.flag_slot = -1;
-        const int ncol = ncf + (nB_solved > 0 ? (nB + 255) / 256 : 0);  // as below
+        const int ncol = ncf + (nB_solved > 0 ? (nB + NE_BND_TPB - 1) / NE_BND_TPB : 0);  // as below
         rf.row[rf.nrows++] = {0, ncol, 1, SL_ZERO};
         if (epi.do_xn) rf.row[rf.nrows++] = {pw, ncol, 0, SL_XN2};
         if (epi.do_gn) rf.row[rf.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
@@ -356,7 +356,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
     if (fuse) {
         span_end(SPAN_JAC);
-        const int ncol = ncf + (nB_solved > 0 ? (nB + 255) / 256 : 0);
+        const int ncol = ncf + (nB_solved > 0 ? (nB + NE_BND_TPB - 1) / NE_BND_TPB : 0);
         RedSpec rs{};
         rs.flag_slot = -1;
         if (nranks > 1) {  // [ZERO, XN2, gnorm per rank]: one collective (see below)
@@ -926,7 +926,7 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         records_enqueue(nullptr, 1);
         launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
                          (M + 255) / 256);
-        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial);
+        launch_residual(s, plug_problem(), d_recs, d_f, d_eu, d_ed, d_partial);
     }
     std::vector<double> ed(Mg);
     download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed.data());
@@ -943,10 +943,11 @@ int Plan::reproject(const double *x, double *point_out, double *marker_out) {
     if (x) {
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
         fun(d_x, d_f, d_eu, d_ed);  // parameters set, records current
+        launch_reproject(s, P, d_recs, d_ftrial, d_eu_s);
     } else {
         records_enqueue(nullptr, 1);
+        launch_reproject(s, plug_problem(), d_recs, d_ftrial, d_eu_s);
     }
-    launch_reproject(s, P, d_recs, d_ftrial, d_eu_s);
     download_ref_order(d_ftrial, d_eu_s, d_ed_s, point_out, marker_out, nullptr);
     return MMBA_OK;
 }
@@ -1122,8 +1123,8 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
         records_enqueue(nullptr, 1);
         launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
                          (M + 255) / 256);
-        launch_residual(s, P, d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FI, nullptr,
-                        d_dist_x);
+        launch_residual(s, plug_problem(), d_recs, d_f, d_eu, d_ed, d_partial, d_scalar + SL_FI,
+                        nullptr, d_dist_x);
         allreduce(d_scalar + SL_FI, 1);
         error_stats_enqueue(d_ed, SL_IESUM);
         measured = true;

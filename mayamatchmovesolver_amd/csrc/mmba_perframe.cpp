@@ -144,6 +144,17 @@ int Plan::solve_frames(double *x_inout, mmba_result *results, const mmba_callbac
 
 namespace {
 
+// The reference's per-frame mode runs solveFrames once per frame, with a
+// one-frame frame list, so its lens lookups never mix indices (SURVEY B3;
+// Plan::build_lens_instances): plans built for it take the plain lens
+// instances.
+struct LensPlain {
+    bool prev;
+    LensPlain() : prev(mmba::t_lens_plain) { mmba::t_lens_plain = true; }
+    ~LensPlain() { mmba::t_lens_plain = prev; }
+};
+
+
 // The sub-problem of one frame: the caller's arrays except the observation
 // and parameter lists, which are filtered (order kept: observations stay
 // marker-major, parameters attr-major).
@@ -198,6 +209,7 @@ int solve_frame(mmba_context *ctx, FrameProblem &fp, const mmba_options *opt, do
     std::vector<double> xs(n), fvec(m), eu(m), ed(fp.p.num_obs);
     for (int k = 0; k < n; ++k) xs[k] = x[fp.params[k]];
     mmba_plan *plan = nullptr;
+    LensPlain plain_lenses;  // one frame per solve: no lens index mixing (B3)
     int rc = mmba_plan_create(ctx, &fp.p, opt, &plan);
     if (rc != MMBA_OK) return rc;
     rc = mmba_plan_solve(plan, xs.data(), fvec.data(), eu.data(), ed.data(), res, cb, nullptr);
@@ -234,6 +246,7 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
             // (MMBA_PATH_PERFRAME_BATCH = 0: the per-frame plans below)
             if (mmba::path_choice(MMBA_PATH_PERFRAME_BATCH) != 0) {
                 mmba_plan *plan = nullptr;
+                LensPlain plain_lenses;
                 if (mmba_plan_create(ctx, prob, opt, &plan) == MMBA_OK) {
                     int rc = MMBA_ERR_UNSUPPORTED;
                     if (plan->impl.batch_ok) rc = mmba_plan_solve_per_frame(plan, x_inout, results, cb);

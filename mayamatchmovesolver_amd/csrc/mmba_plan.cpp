@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <numeric>
 #include <set>
 
@@ -115,6 +116,137 @@ void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd
         int k = 0;
         while (k + 1 < nranks && bounds[k + 1] <= bnd_first[b]) ++k;
         bnd_owner[b] = k;
+    }
+}
+
+thread_local bool t_lens_plain = false;
+
+// Lens instances (mmba.h ABI 7; oracle/refcpu.c b3_build
+// is the checker's restatement).  The reference clones every lens model once
+// per frame, instance (l, f), and reads its lookup lists at mixed indices:
+// observation (marker i, frame f) is distorted by instance
+// (lens of marker (i + f) / F, (i + f) % F) (adjust_measureErrors.cpp:244,
+// 463 on the list of maya_lens_model_utils.cpp:782-799), and setParameters
+// writes attrList entry a's value at frame g into instance (lens of entry
+// (a + g) / F, (a + g) % F) -- every g for a static attribute
+// (adjust_setParameters.cpp:113-121, 206-214; list :836-851), skipping
+// entries without a lens, the last parameter winning.  A slot no parameter
+// writes holds the plug model's value.  Only the instances some observation
+// reads are kept.  With t_lens_plain (the per-frame solves, where the
+// reference's frame list has one frame and no index mixes) every
+// observation reads its own camera's lens at its own frame and every
+// parameter writes its own lens.
+void Plan::build_lens_instances(const mmba_problem *pr) {
+    const int nL = pr->num_lenses, nK = pr->num_markers;
+    obs_inst_g.assign(Mg, -1);
+    inst_lens_h.clear();
+    inst_attr_h.clear();
+    inst_frame_h.clear();
+    inst_val_h.clear();
+    inst_lpar_off_h.assign(1, 0);
+    inst_lpar_h.clear();
+    if (!pr->cam_lens || nL <= 0) return;
+    const bool plain = t_lens_plain;
+    auto lens_of_marker = [&](int i) { return pr->cam_lens[pr->mkr_cam[i]]; };
+    std::unordered_map<long long, int> inst_id;
+    for (int r = 0; r < Mg; ++r) {
+        const long long t = (long long)pr->obs_marker[r] + pr->obs_frame[r];
+        const int owner = plain ? pr->obs_marker[r] : (int)(t / F);
+        const int f = plain ? pr->obs_frame[r] : (int)(t % F);
+        require(owner < nK, "marker index + frame index past the marker list (B3)");
+        const int l = lens_of_marker(owner);
+        if (l < 0) continue;
+        const long long key = (long long)l * F + f;
+        auto it = inst_id.find(key);
+        if (it == inst_id.end()) {
+            const int id = (int)inst_lens_h.size();
+            it = inst_id.emplace(key, id).first;
+            inst_lens_h.push_back(l);
+            const int type = pr->lens_type[l];
+            const bool classic = type == MMBA_LENS_3DE_CLASSIC;
+            const bool anam = type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4 ||
+                              type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED;
+            for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+                // the plug model's value (lens attributes are never read per
+                // frame, B11): lens_input_values, or the attribute at frame 0
+                double v = ((classic && k == 1) || (anam && k >= 11)) ? 1. : 0.;
+                const int a = pr->lens_attrs[MMBA_LENS_NUM_ATTRS * l + k];
+                if (pr->lens_input_values) v = pr->lens_input_values[(size_t)MMBA_LENS_NUM_ATTRS * l + k];
+                else if (a >= 0) v = pr->attr_values[pr->attr_offset[a]];
+                inst_attr_h.push_back(-1);
+                inst_frame_h.push_back(0);
+                inst_val_h.push_back(v);
+            }
+        }
+        obs_inst_g[r] = it->second;
+    }
+    const int ninst = (int)inst_lens_h.size();
+    // (lens, slot) of each attribute id
+    std::unordered_map<int, std::pair<int, int>> lens_slot;
+    for (int l = nL - 1; l >= 0; --l)
+        for (int k = MMBA_LENS_NUM_ATTRS - 1; k >= 0; --k) {
+            const int a = pr->lens_attrs[MMBA_LENS_NUM_ATTRS * l + k];
+            if (a >= 0) lens_slot[a] = {l, k};
+        }
+    // attrList indices: param_ref_attr, or numbered by first appearance
+    std::vector<int> par_ref(n);
+    int n_ref = 0;
+    if (pr->param_ref_attr) {
+        n_ref = pr->num_ref_attrs;
+        for (int p = 0; p < n; ++p) par_ref[p] = pr->param_ref_attr[p];
+    } else {
+        std::unordered_map<int, int> first;
+        for (int p = 0; p < n; ++p) {
+            auto it = first.find(pr->param_attr[p]);
+            if (it == first.end()) it = first.emplace(pr->param_attr[p], n_ref++).first;
+            par_ref[p] = it->second;
+        }
+    }
+    std::vector<int> ref_lens(std::max(n_ref, 1), -1);
+    if (pr->ref_attr_lens) {
+        for (int r = 0; r < n_ref; ++r) ref_lens[r] = pr->ref_attr_lens[r];
+    } else {
+        for (int p = n - 1; p >= 0; --p) {
+            auto it = lens_slot.find(pr->param_attr[p]);
+            if (par_ref[p] >= 0 && par_ref[p] < n_ref)
+                ref_lens[par_ref[p]] = it == lens_slot.end() ? -1 : it->second.first;
+        }
+    }
+    for (int r = 0; r < n_ref; ++r) require(ref_lens[r] < nL, "ref_attr_lens");
+    // setParameters' lens writes, in parameter order (the last one stays)
+    std::vector<int> src((size_t)ninst * MMBA_LENS_NUM_ATTRS, -1);
+    for (int p = 0; p < n; ++p) {
+        auto ls = lens_slot.find(pr->param_attr[p]);
+        if (ls == lens_slot.end()) continue;
+        const int la = ls->second.first, k = ls->second.second;
+        const int g0 = pr->param_frame[p] >= 0 ? pr->param_frame[p] : 0;
+        const int g1 = pr->param_frame[p] >= 0 ? pr->param_frame[p] + 1 : F;
+        require(par_ref[p] >= 0 && par_ref[p] < n_ref, "param_ref_attr");
+        for (int g = g0; g < g1; ++g) {
+            const long long t = (long long)par_ref[p] + g;
+            const int lt = plain ? la : ref_lens[t / F];
+            const int f = plain ? g : (int)(t % F);
+            if (lt < 0) continue;  // a null model: setLensModelAttributeValue ignores it
+            if (pr->lens_type[lt] != pr->lens_type[la])
+                throw Unsupported{"a lens attribute written into a lens of another model "
+                                  "type (B3: undefined in the reference)"};
+            auto it = inst_id.find((long long)lt * F + f);
+            if (it != inst_id.end()) src[(size_t)it->second * MMBA_LENS_NUM_ATTRS + k] = p;
+        }
+    }
+    for (int j = 0; j < ninst; ++j) {
+        std::vector<int> ps;
+        for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+            const int p = src[(size_t)j * MMBA_LENS_NUM_ATTRS + k];
+            if (p < 0) continue;
+            inst_attr_h[(size_t)j * MMBA_LENS_NUM_ATTRS + k] = pr->param_attr[p];
+            inst_frame_h[(size_t)j * MMBA_LENS_NUM_ATTRS + k] =
+                pr->param_frame[p] >= 0 ? pr->param_frame[p] : 0;
+            ps.push_back(p);
+        }
+        std::sort(ps.begin(), ps.end());
+        for (int p : ps) inst_lpar_h.push_back(p);
+        inst_lpar_off_h.push_back((int)inst_lpar_h.size());
     }
 }
 
@@ -223,18 +355,28 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             add_rows(pr->num_smooth, pr->smooth_attr, pr->smooth_frame, pr->smooth_weight,
                      pr->smooth_variance, pr->smooth_value);
     }
+    // the cameras' lenses: one shared lens (or none) is the plain case; with
+    // several, the reference's index arithmetic (B3, below) decides which
+    // lens instance distorts which observation
     int lens_owner = -2;
+    bool several_lenses = false;
     for (int c = 0; c < nC; ++c) {
         const int l = pr->cam_lens ? pr->cam_lens[c] : -1;
         if (l >= 0 && (pr->lens_type[l] < MMBA_LENS_3DE_CLASSIC ||
                        pr->lens_type[l] > MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED))
             throw Unsupported{"unknown lens model type"};
-        // B3: the reference mixes per-marker/per-attr lens indices; it is only
-        // well defined when every camera shares one lens (or none has one).
+        if (l < 0) continue;
         if (lens_owner == -2) lens_owner = l;
-        else if (l != lens_owner)
-            throw Unsupported{"cameras with different lens models (B3)"};
+        else if (l != lens_owner) several_lenses = true;
     }
+    if (lens_owner == -2) lens_owner = -1;
+    if (several_lenses && pr->lens_input)
+        for (int c = 0; c < nC; ++c) {
+            const int l = pr->cam_lens[c];
+            if (l >= 0 && pr->lens_input[l] >= 0)
+                throw Unsupported{"input lens layers with several camera lenses"};
+        }
+    build_lens_instances(pr);
     // ABI 5: the lens's input layers, constants of the solve (mmba.h), deepest
     // first: type, then the 14 slot values (lens_input_values, or each slot's
     // attribute at frame 0; absent slots the model's default)
@@ -568,7 +710,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     ref_of_dev = local;
     std::stable_sort(ref_of_dev.begin(), ref_of_dev.end(),
                      [&](int a, int b) { return obs_cf[a] < obs_cf[b]; });
-    std::vector<int> d_cf(M), d_bnd(M), d_frame(M), d_cam(M), d_own(M);
+    std::vector<int> d_cf(M), d_bnd(M), d_frame(M), d_cam(M), d_own(M), d_inst(M);
     std::vector<double> d_xy(2 * (size_t)M), d_sqrtw(M);
     std::vector<int> cf_obs_off(ncf + 1, 0);
     for (int i = 0; i < M; ++i) {
@@ -581,29 +723,20 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_xy[2 * i + 1] = pr->obs_xy[2 * r + 1];
         d_sqrtw[i] = std::sqrt(pr->obs_weight[r]);
         d_own[i] = obs_own_g[r];
+        d_inst[i] = obs_inst_g[r];
         cf_obs_off[d_cf[i] + 1]++;
     }
     for (int cf = 0; cf < ncf; ++cf) cf_obs_off[cf + 1] += cf_obs_off[cf];
     // local column bound (rolling shutter: + the neighbouring frames' CF blocks)
-    // lens parameters that reach an observation: static ones and those keyed
-    // at its frame (an animated coefficient has one parameter per frame)
-    std::vector<int> cam_lpar_static(nC, 0);
-    std::vector<std::map<int, int>> cam_lpar_frame(nC);
-    for (int c = 0; c < nC; ++c)
-        for (int q = cam_lpar_off[c]; q < cam_lpar_off[c + 1]; ++q) {
-            const int fp = pr->param_frame[cam_lpar[q]];
-            if (fp < 0) ++cam_lpar_static[c];
-            else ++cam_lpar_frame[c][fp];
-        }
-    auto lens_cols = [&](int c, int f) {
-        auto it = cam_lpar_frame[c].find(f);
-        return cam_lpar_static[c] + (it == cam_lpar_frame[c].end() ? 0 : it->second);
+    // lens parameters that reach an observation: those its lens instance holds
+    auto lens_cols = [&](int i) {
+        const int j = d_inst[i];
+        return j < 0 ? 0 : inst_lpar_off_h[j + 1] - inst_lpar_off_h[j];
     };
     auto obs_cols = [&](int i) {
         const int cf = d_cf[i];
         int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
-                 (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) +
-                 lens_cols(d_cam[i], d_frame[i]);
+                 (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) + lens_cols(i);
         for (int side = 0; side < 2; ++side)
             if (cf_nb[2 * cf + side] >= 0) nl += cf_pc[cf_nb[2 * cf + side]];
         return nl;
@@ -635,8 +768,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int i = 0; i < M && !masked; ++i) {
             const int cf = d_cf[i];
             const int nl = (cf_var_off[cf + 1] - cf_var_off[cf] - 1) +
-                           (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) +
-                           (cam_lpar_off[d_cam[i] + 1] - cam_lpar_off[d_cam[i]]);
+                           (bnd_par_off[d_bnd[i] + 1] - bnd_par_off[d_bnd[i]]) + lens_cols(i);
             if (nl == 0) masked = true;
         }
         if (masked && central && !opt.robust_loss && nranks == 1 && nrows == 0 && !rs_on) {
@@ -659,9 +791,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                     reach.push_back(cf_var_param[t]);
                 for (int t = bnd_par_off[d_bnd[i]]; t < bnd_par_off[d_bnd[i] + 1]; ++t)
                     reach.push_back(bnd_par[t]);
-                const int c = d_cam[i];
-                for (int q = cam_lpar_off[c]; q < cam_lpar_off[c + 1]; ++q)
-                    reach.push_back(cam_lpar[q]);
+                if (d_inst[i] >= 0)
+                    for (int q = inst_lpar_off_h[d_inst[i]]; q < inst_lpar_off_h[d_inst[i] + 1]; ++q)
+                        reach.push_back(inst_lpar_h[q]);
                 for (int p : need)
                     if (std::find(reach.begin(), reach.end(), p) == reach.end()) cover = false;
             }
@@ -1007,6 +1139,22 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bobs_off = upload(bobs_off);
     D.bobs = upload(bobs);
     D.cam_lpar_off = upload(cam_lpar_off);
+    {
+        bool any_inst = false;
+        for (int i = 0; i < M; ++i) any_inst |= d_inst[i] >= 0;
+        if (any_inst) {
+            D.obs_inst = upload(d_inst);
+            D.inst_lens = upload(inst_lens_h);
+            D.inst_attr = upload(inst_attr_h);
+            D.inst_frame = upload(inst_frame_h);
+            D.inst_val = upload(inst_val_h);
+            D.inst_lpar_off = upload(inst_lpar_off_h);
+            D.inst_lpar = upload(inst_lpar_h.empty() ? std::vector<int>{-1} : inst_lpar_h);
+            d_inst_attr_plug = upload(std::vector<int>(inst_attr_h.size(), -1));
+        } else {
+            D.obs_inst = nullptr;
+        }
+    }
     D.cam_lpar = upload(cam_lpar);
     {
         // widest observation (local Jacobian columns): camera variants +
@@ -1121,12 +1269,24 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                 if (cn >= 0)
                     for (int p : cf_params[cn]) cols.push_back(p);
             }
-            const int c = cf_cam[cf], f = cf_frame[cf];
-            for (int q = cam_lpar_off[c]; q < cam_lpar_off[c + 1]; ++q) {
-                const int p = cam_lpar[q];
-                if (pr->param_frame[p] >= 0 && pr->param_frame[p] != f) continue;
-                cols.push_back(p);
+            // the segment's lens columns: k_jacobian_rs reduces the
+            // segment's rows into one block, so they must be the same
+            // parameters for every observation of the segment
+            const int j0 = cf_obs_off[cf] < cf_obs_off[cf + 1] ? d_inst[cf_obs_off[cf]] : -1;
+            for (int i = cf_obs_off[cf]; i < cf_obs_off[cf + 1]; ++i) {
+                const int j = d_inst[i];
+                const int n0 = j0 < 0 ? 0 : inst_lpar_off_h[j0 + 1] - inst_lpar_off_h[j0];
+                const int n1 = j < 0 ? 0 : inst_lpar_off_h[j + 1] - inst_lpar_off_h[j];
+                bool same = n0 == n1;
+                for (int q = 0; q < n0 && same; ++q)
+                    same = inst_lpar_h[inst_lpar_off_h[j0] + q] == inst_lpar_h[inst_lpar_off_h[j] + q];
+                if (!same)
+                    throw Unsupported{"rolling shutter where the observations of one camera-frame "
+                                      "read lens instances with different parameters (B3)"};
             }
+            if (j0 >= 0)
+                for (int q = inst_lpar_off_h[j0]; q < inst_lpar_off_h[j0 + 1]; ++q)
+                    cols.push_back(inst_lpar_h[q]);
             for (int l = 0; l < (int)cols.size() && l < LMAX; ++l)
                 if (p_class[cols[l]] == PC_G && gcnt[cf] < NGMAX) {
                     gcol[(size_t)NGMAX * cf + gcnt[cf]] = l;
@@ -1279,7 +1439,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_usq = dalloc<double>(nB);
     d_nu = dalloc<double>((size_t)3 * std::max(nB, 1));
     d_ngp = dalloc<double>((size_t)std::max(nG, 1) * std::max(nB, 1));
-    pw = std::max(std::max(nparts, residual_blocks(P)), ncf + (nB + 255) / 256);
+    pw = std::max(std::max(nparts, residual_blocks(P)), ncf + (nB + NE_BND_TPB - 1) / NE_BND_TPB);
     {
         // parameters outside every solved bundle: the extra workgroups of
         // the fused back substitution + trial pass

@@ -21,6 +21,10 @@ namespace mmba {
 void set_error(const std::string &msg);
 // mmba_debug_set_path's choice for MMBA_PATH_<key> (-1: the builder's own)
 int path_choice(int key);
+// set around the plan builds of the per-frame solves (mmba_perframe.cpp):
+// their lens instances follow the reference's one-frame solves (no index
+// mixing, Plan::build_lens_instances)
+extern thread_local bool t_lens_plain;
 
 #define MMBA_HIP(call)                                                             \
     do {                                                                           \
@@ -82,6 +86,23 @@ struct Plan {
 
     // host structure
     std::vector<int> ref_of_dev;
+    // lens instances (Plan::build_lens_instances, DevProblem::obs_inst ..):
+    // per global observation, and the instance tables
+    std::vector<int> obs_inst_g, inst_lens_h, inst_attr_h, inst_frame_h, inst_lpar_off_h,
+        inst_lpar_h;
+    std::vector<double> inst_val_h;
+    // every instance slot at its plug value (the measurement before
+    // setParameters first runs)
+    int *d_inst_attr_plug = nullptr;
+    void build_lens_instances(const mmba_problem *pr);
+    // P with every lens instance slot at its plug value: what the reference
+    // measures before setParameters first runs (solveFrames' initial
+    // measureErrors, adjust_base.cpp:1002-1004 then 1076-1089)
+    DevProblem plug_problem() const {
+        DevProblem Q = P;
+        if (Q.obs_inst) Q.inst_attr = d_inst_attr_plug;
+        return Q;
+    }
     std::vector<int> panel_rows_off, panel_rows;    // rows(k) flattened
     std::vector<int> panel_cols_off, panel_cols;    // colsT(k) flattened
     std::vector<int> panel_pairs_off;               // pairs(k) offsets into d_pairs

@@ -56,14 +56,13 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
     const int cf = P.obs_cf[i];
     const int b = P.obs_bnd[i];
     const int fr = P.obs_frame[i];
-    const int cam = P.obs_cam[i];
     const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
     const double tau = P.obs_tau[i];
     const Override none{-1, 0.};
     double bp0[3];
     base_bundle(P, b, fr, bp0);
-    int lens = -1;
-    const int hl = obs_lens(P, cam, lens);
+    int inst = -1;
+    const int hl = obs_lens_inst(P, i, inst);
     // the column list
     int cp[LMAX];
     unsigned char ck[LMAX];
@@ -90,10 +89,8 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
         }
     }
     if (hl)
-        for (int q = P.cam_lpar_off[cam]; q < P.cam_lpar_off[cam + 1] && nl < LMAX; ++q) {
-            const int p = P.cam_lpar[q];
-            if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
-            cp[nl] = p;
+        for (int q = P.inst_lpar_off[inst]; q < P.inst_lpar_off[inst + 1] && nl < LMAX; ++q) {
+            cp[nl] = P.inst_lpar[q];
             ck[nl++] = 2;
         }
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
@@ -101,15 +98,15 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
     RsCam RC;
     rs_cam_load(P, cf, RC);
     // the lens coefficients at x once; a lens column replaces its slot(s)
-    // (lens_coeffs with the override, without re-reading the table)
+    // (inst_coeffs with the override, without re-reading the table)
     double lc0[MMBA_LENS_NUM_ATTRS];
     int la[MMBA_LENS_NUM_ATTRS];
     int ltype = MMBA_LENS_NONE;
     if (hl) {
-        lens_coeffs(P, lens, fr, none, lc0);
-        ltype = P.lens_type[lens];
+        inst_coeffs(P, inst, none, lc0);
+        ltype = hl;
 #pragma unroll
-        for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) la[k] = P.lens_attrs[MMBA_LENS_NUM_ATTRS * lens + k];
+        for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) la[k] = P.inst_attr[MMBA_LENS_NUM_ATTRS * inst + k];
     }
     // column -1: the base point; then every column that needs an evaluation
     Resid r0{}, rs{};
@@ -128,7 +125,7 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
 #pragma unroll
                 for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
                     lc[k] = (la[k] >= 0 && la[k] == oa) ? ov : lc0[k];
-                if (ltype == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) lc[13] = 1.;  // lens_coeffs' rule
+                if (ltype == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) lc[13] = 1.;  // inst_coeffs' rule
             }
             const Resid r = residual_l(P, rec, bp0, mx, my, sw, hl, lc);
             if (l < 0) {

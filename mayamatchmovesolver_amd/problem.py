@@ -137,6 +137,11 @@ class Problem:
     # the input layers' plug-read values (None = the attributes at frame 0)
     lens_input: Optional[np.ndarray] = None
     lens_input_values: Optional[np.ndarray] = None
+    # ABI 7: the reference's lens index arithmetic (Appendix B3, mmba.h) --
+    # each parameter's attrList index (paramToAttrList[p].first) and the lens
+    # of each attrList entry (-1 not a lens attribute); None = derived
+    param_ref_attr: Optional[np.ndarray] = None
+    ref_attr_lens: Optional[np.ndarray] = None
 
     def __post_init__(self):
         for name in _FIELDS_I32:
@@ -164,6 +169,10 @@ class Problem:
         if self.lens_input_values is not None:
             self.lens_input_values = np.ascontiguousarray(self.lens_input_values,
                                                           dtype=np.float64).reshape(-1)
+        for name in ("param_ref_attr", "ref_attr_lens"):
+            if getattr(self, name) is not None:
+                setattr(self, name, np.ascontiguousarray(getattr(self, name),
+                                                         dtype=np.int32).reshape(-1))
 
     # sizes -------------------------------------------------------------
     @property
@@ -264,6 +273,12 @@ class Problem:
         p.lens_input_values = (ptr(self.lens_input_values, C.c_double)
                                if self.lens_input_values is not None
                                else C.cast(None, C.POINTER(C.c_double)))
+        p.param_ref_attr = (ptr(self.param_ref_attr, C.c_int32)
+                            if self.param_ref_attr is not None
+                            else C.cast(None, C.POINTER(C.c_int32)))
+        p.num_ref_attrs = int(self.ref_attr_lens.size) if self.ref_attr_lens is not None else 0
+        p.ref_attr_lens = (ptr(self.ref_attr_lens, C.c_int32) if self.ref_attr_lens is not None
+                           else C.cast(None, C.POINTER(C.c_int32)))
         return p, [self]
 
     # (de)serialisation ---------------------------------------------------
@@ -277,7 +292,7 @@ class Problem:
             d["param_weight"] = self.param_weight
         if self.cam_rs_value is not None:
             d["cam_rs_value"] = self.cam_rs_value
-        for name in ("lens_input", "lens_input_values"):
+        for name in ("lens_input", "lens_input_values", "param_ref_attr", "ref_attr_lens"):
             if getattr(self, name) is not None:
                 d[name] = getattr(self, name)
         return d
@@ -292,7 +307,8 @@ class Problem:
                                                              np.int32)], axis=1).reshape(-1)
             kw["lens_attrs"] = la
         for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight", "cam_rs_value",
-                                                          "lens_input", "lens_input_values"]:
+                                                          "lens_input", "lens_input_values",
+                                                          "param_ref_attr", "ref_attr_lens"]:
             if name in d:
                 kw[name] = np.asarray(d[name])
         return cls(num_frames=int(d["num_frames"]), **kw)

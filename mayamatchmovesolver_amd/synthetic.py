@@ -901,6 +901,80 @@ def rig_scene(n_cams=2, bundles=10, solve_cam1=True, stiffness=False, seed=11) -
     return b.build(meta={"name": "rig"})
 
 
+B3_VARIANTS = ("lens_first", "cam_first", "animated", "one_lens")
+
+
+def b3_scene(variant="lens_first", frames=5, markers_per_cam=4, seed=23) -> Problem:
+    """Two cameras, each with its own 3DE classic lens (distortion 0.04 and
+    -0.03): the scene on which the reference's lens index arithmetic (SURVEY
+    Appendix B3, mmba.h ABI 7) distorts marker i at frame f with the lens of
+    marker (i + f) / F and writes a lens attribute solved at frame g into the
+    lens of attrList entry (a + g) / F.  Camera 0 moves along x with its
+    rotation solved per frame; camera 1 is static with its rotation solved
+    (three globals); the bundles are fixed.  Markers: the plain projection
+    of each marker's own camera and lens, plus noise.  Variants:
+      "lens_first": both lenses' distortion solved, listed before the cameras
+      "cam_first":  the same, the lens attributes listed after the rotations
+      "animated":   lens 0's distortion animated and solved (one parameter
+                    per frame, values differing per frame), after the rotations
+      "one_lens":   camera 0 without a lens, camera 1's lens solved."""
+    assert variant in B3_VARIANTS, variant
+    rng = np.random.Generator(np.random.PCG64(seed))
+    F = frames
+    b = SceneBuilder(F)
+    fr = np.arange(F, dtype=np.float64)
+    render = (1500, 1000)  # the film aspect: film fit is the identity
+    K = markers_per_cam
+    depth = rng.uniform(10.0, 25.0, size=2 * K)
+    P = np.stack([rng.uniform(-0.25, 0.25, 2 * K) * depth, rng.uniform(-0.2, 0.2, 2 * K) * depth,
+                  -depth], axis=1)
+    truth = [(0.04, 1.0, 0.0, 0.0, 0.0), (-0.03, 1.0, 0.0, 0.0, 0.0)]
+    if variant == "animated":
+        d0 = 0.04 + 0.005 * fr
+        lens0, lids0 = b.lens_3de_classic(distortion=np.zeros(F) + 0.01 * fr)
+    else:
+        d0 = np.full(F, 0.04)
+        lens0, lids0 = b.lens_3de_classic(distortion=0.0)
+    lens1, lids1 = b.lens_3de_classic(distortion=0.0)
+    t0 = np.stack([0.3 * fr, 0.1 + 0.0 * fr, 0.0 * fr], 1)
+    r0 = np.stack([1.0 + 0.2 * fr, -1.5 + 0.1 * fr, 0.5 + 0.0 * fr], 1)
+    tfm0, tids0 = b.transform(t=[t0[:, 0], t0[:, 1], t0[:, 2]],
+                              r=[r0[:, 0] + rng.uniform(-0.5, 0.5, F),
+                                 r0[:, 1] + rng.uniform(-0.5, 0.5, F),
+                                 r0[:, 2] + rng.uniform(-0.5, 0.5, F)])
+    t1, r1 = np.array([1.0, 0.2, 0.5]), np.array([0.5, 2.0, -0.3])
+    tfm1, tids1 = b.transform(t=tuple(t1), r=tuple(r1 + rng.uniform(-0.8, 0.8, 3)))
+    cam0, _ = b.camera(tfm0, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
+                       render_size=render, lens=-1 if variant == "one_lens" else lens0)
+    cam1, _ = b.camera(tfm1, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
+                       render_size=render, lens=lens1)
+    for j in range(2 * K):
+        bt, _ = b.transform(t=tuple(P[j]))
+        b.bundle(bt)
+    for c, cam in enumerate((cam0, cam1)):
+        for k in range(K):
+            j = c * K + k
+            xy = np.empty((F, 2))
+            for f in range(F):
+                t, r = (t0[f], r0[f]) if c == 0 else (t1, r1)
+                mx, my, _ = _project(t, r, FOCAL_MM, P[j])
+                if c == 1 or variant != "one_lens":
+                    lt = truth[c] if c == 1 else (d0[f],) + truth[0][1:]
+                    mx, my = _lens_distort_truth(lt, float(mx), float(my))
+                xy[f] = (float(_noisy(rng, np.asarray(mx))), float(_noisy(rng, np.asarray(my))))
+            b.marker(cam, j, xy)
+    lens_solve = [lids1[0]] if variant == "one_lens" else [lids0[0], lids1[0]]
+    if variant == "lens_first":
+        for a in lens_solve:
+            b.solve(a)
+    for a in tids0[3:6] + tids1[3:6]:
+        b.solve(a)
+    if variant != "lens_first":
+        for a in lens_solve:
+            b.solve(a)
+    return b.build(meta={"name": "b3_" + variant})
+
+
 def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal=3,
                   extra_globals=0, window=None, lens=None, seed=17) -> Problem:
     """Witness-camera rig with a wide arrow of global parameters: a fixed

@@ -1039,6 +1039,13 @@ typedef struct {
     double *obs_pts, *obs_mkr; /* optional: reprojected point / corrected marker [2M] */
     int m;                     /* residual rows: 2M + stiffness + smoothness */
     int rs_any;                /* some camera has a rolling shutter (mmba.h ABI 3) */
+    /* B3 (mmba.h ABI 7): lens_src[(l * F + f) * 14 + k] = the parameter whose
+     * value slot k of lens instance (l, f) holds, -1: the plug model's value */
+    int *lens_src;
+    int lens_set; /* setParameters has run: the clones hold the parameters'
+                     values (before it, every slot is the plug model's value:
+                     solveFrames' initial measureErrors, adjust_base.cpp:
+                     1002-1004 then 1076-1089) */
 } ref_scene;
 
 /* Test hook standing in for MComputation::isInterruptRequested: the poll
@@ -1203,15 +1210,6 @@ static double lens_default(int type, int k) {
     return 0.;
 }
 
-/* Lens attribute values (absent slots: the model's defaults, mmba.h). */
-static void lens_coeffs(const ref_scene *s, int lens, int f, double c[MMBA_LENS_NUM_ATTRS]) {
-    const int *la = &s->p->lens_attrs[MMBA_LENS_NUM_ATTRS * lens];
-    const int type = s->p->lens_type[lens];
-    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
-        c[k] = attr_value(s, la[k], f, lens_default(type, k));
-    if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.; /* no rescale slot */
-}
-
 static void lens_model_distort(int type, const double *c, double x, double y, double *ox,
                                double *oy) {
     if (type == MMBA_LENS_3DE_CLASSIC)
@@ -1253,16 +1251,124 @@ static void lens_chain_distort(const ref_scene *s, int l, int depth, double x, d
     lens_model_distort(p->lens_type[l], c, x, y, ox, oy);
 }
 
-static void apply_lens(const ref_scene *s, int cam, int f, double *px,
-                       double *py) {
+/* ---- the reference's lens lists and the index
+ * arithmetic that reads them (mmba.h ABI 7).
+ *   lensModelList[l*F + f]: clone f of lens l's plug model
+ *     (maya_lens_model_utils.cpp:654-661: lensIndex = the list's size before
+ *     the lens's F clones are appended);
+ *   markerFrameToLensModelList[i*F + f] = lensModelList[lens(marker i)*F + f]
+ *     (:782-799, the camera's first lens node);
+ *   attrFrameToLensModelList[a*F + f] = lensModelList[lens(attr a)*F + f]
+ *     (:836-851, lens attributes only; null otherwise);
+ * measureErrors reads markerFrameToLensModelList[markerIndex + frameIndex]
+ * (adjust_measureErrors.cpp:244, 463); setParameters writes an animated lens
+ * attribute's value into attrFrameToLensModelList[attrIndex + frameIndex] and
+ * a static one's into [attrIndex + j] for every frame j
+ * (adjust_setParameters.cpp:113-121, 206-214), a null entry being ignored
+ * (setLensModelAttributeValue, maya_lens_model_utils.cpp:87-93).  Each
+ * evaluation sets every parameter in order, so a slot holds the value of the
+ * LAST parameter that writes it; a slot no parameter writes keeps the plug
+ * model's value (lens attributes are never read per frame, B11). ---- */
+
+/* The attribute's index in the solver's attrList (paramToAttrList[p].first):
+ * param_ref_attr, or the attributes numbered in order of first appearance. */
+static int b3_ref_attrs(const mmba_problem *p, int *par_ref) {
+    if (p->param_ref_attr) {
+        for (int q = 0; q < p->num_params; ++q) par_ref[q] = p->param_ref_attr[q];
+        return p->num_ref_attrs;
+    }
+    int n = 0;
+    for (int q = 0; q < p->num_params; ++q) {
+        par_ref[q] = -1;
+        for (int r = 0; r < q; ++r)
+            if (p->param_attr[r] == p->param_attr[q]) par_ref[q] = par_ref[r];
+        if (par_ref[q] < 0) par_ref[q] = n++;
+    }
+    return n;
+}
+
+/* (lens, slot) of an attribute id, or -1 */
+static int b3_lens_slot(const mmba_problem *p, int a, int *slot) {
+    for (int l = 0; l < p->num_lenses; ++l)
+        for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k)
+            if (p->lens_attrs[MMBA_LENS_NUM_ATTRS * l + k] == a) {
+                *slot = k;
+                return l;
+            }
+    return -1;
+}
+
+/* The lens of attrList entry r: ref_attr_lens, or the lens of the first
+ * parameter's attribute that is entry r. */
+static int b3_ref_lens(const mmba_problem *p, const int *par_ref, int r) {
+    if (p->ref_attr_lens) return p->ref_attr_lens[r];
+    int k;
+    for (int q = 0; q < p->num_params; ++q)
+        if (par_ref[q] == r) return b3_lens_slot(p, p->param_attr[q], &k);
+    return -1;
+}
+
+/* Fills s->lens_src by running setParameters' lens writes once.  Returns
+ * MMBA_ERR_UNSUPPORTED where the reference's behaviour is undefined: a write
+ * into a lens of another model type (a reinterpret_cast of the model,
+ * maya_lens_model_utils.cpp:160-170) or an attrList index out of range. */
+static int b3_build(ref_scene *s) {
     const mmba_problem *p = s->p;
-    if (!p->cam_lens) return;
-    int lens = p->cam_lens[cam];
+    const int F = p->num_frames, nL = p->num_lenses, n = p->num_params;
+    if (!p->cam_lens || nL <= 0) return MMBA_OK;
+    s->lens_src = (int *)malloc(sizeof(int) * (size_t)nL * F * MMBA_LENS_NUM_ATTRS);
+    for (size_t q = 0; q < (size_t)nL * F * MMBA_LENS_NUM_ATTRS; ++q) s->lens_src[q] = -1;
+    int *par_ref = (int *)malloc(sizeof(int) * (n ? n : 1));
+    const int n_ref = b3_ref_attrs(p, par_ref);
+    int rc = MMBA_OK;
+    for (int q = 0; q < n && rc == MMBA_OK; ++q) {
+        int k;
+        const int la = b3_lens_slot(p, p->param_attr[q], &k);
+        if (la < 0) continue; /* not a lens attribute: the DG / AttrDataBlock path */
+        const int g0 = p->param_frame[q] >= 0 ? p->param_frame[q] : 0;
+        const int g1 = p->param_frame[q] >= 0 ? p->param_frame[q] + 1 : F;
+        for (int g = g0; g < g1; ++g) {
+            const int t = par_ref[q] + g; /* attrIndex + frameIndex / + j */
+            if (par_ref[q] < 0 || t / F >= n_ref) {
+                rc = MMBA_ERR_UNSUPPORTED;
+                break;
+            }
+            const int lt = b3_ref_lens(p, par_ref, t / F);
+            if (lt < 0) continue; /* a null model: nothing is set */
+            if (p->lens_type[lt] != p->lens_type[la]) {
+                rc = MMBA_ERR_UNSUPPORTED;
+                break;
+            }
+            s->lens_src[((size_t)lt * F + t % F) * MMBA_LENS_NUM_ATTRS + k] = q;
+        }
+    }
+    free(par_ref);
+    return rc;
+}
+
+/* Distortion of observation i: the instance markerFrameToLensModelList
+ * [markerIndex + frameIndex] names, with its input layers first. */
+static void apply_lens_obs(const ref_scene *s, int i, double *px, double *py) {
+    const mmba_problem *p = s->p;
+    if (!s->lens_src) return;
+    const int F = p->num_frames;
+    const int t = p->obs_marker[i] + p->obs_frame[i];
+    const int lens = p->cam_lens[p->mkr_cam[t / F]];
+    const int fi = t % F;
     if (lens < 0) return;
     const int type = p->lens_type[lens];
     if (type < MMBA_LENS_3DE_CLASSIC || type > MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4_RESCALED) return;
-    double c[MMBA_LENS_NUM_ATTRS], ox = *px, oy = *py, ix = *px, iy = *py;
-    lens_coeffs(s, lens, f, c);
+    double c[MMBA_LENS_NUM_ATTRS], plug[MMBA_LENS_NUM_ATTRS];
+    lens_layer_values(s, lens, plug); /* the plug model the clones copy */
+    for (int k = 0; k < MMBA_LENS_NUM_ATTRS; ++k) {
+        const int q = s->lens_set ? s->lens_src[((size_t)lens * F + fi) * MMBA_LENS_NUM_ATTRS + k]
+                                  : -1;
+        c[k] = q < 0 ? plug[k]
+                     : attr_value(s, p->param_attr[q], p->param_frame[q] >= 0 ? p->param_frame[q] : 0,
+                                  0.);
+    }
+    if (type == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) c[13] = 1.; /* no rescale slot */
+    double ox = *px, oy = *py, ix = *px, iy = *py;
     const int in = p->lens_input ? p->lens_input[lens] : -1;
     if (in >= 0) lens_chain_distort(s, in, 1, ix, iy, &ix, &iy);
     lens_model_distort(type, c, ix, iy, &ox, &oy);
@@ -1385,7 +1491,7 @@ static void measure(ref_scene *s, const char *frame_mask, double *errors) {
                          (cdir[2] / cl) * (bdir[2] / bl);
             if (dot < 0.0) factor = 1e+6;
         }
-        apply_lens(s, c, f, &point_x, &point_y);
+        apply_lens_obs(s, i, &point_x, &point_y);
         if (s->obs_pts) {
             s->obs_pts[2 * i] = point_x;
             s->obs_pts[2 * i + 1] = point_y;
@@ -1438,6 +1544,7 @@ static void set_parameters(ref_scene *s, const double *x) {
         size_t idx = p->attr_offset[a] + (p->attr_animated[a] ? (f < 0 ? 0 : f) : 0);
         s->attr[idx] = v;
     }
+    s->lens_set = 1;
 }
 
 /* calculateParameterDelta (adjust_solveFunc.cpp:148-180). */
@@ -1599,7 +1706,14 @@ static void scene_init(ref_scene *s, const mmba_problem *p,
     for (int c = 0; c < p->num_cameras; ++c) s->rs_any |= rs_on(s, c);
 }
 
+/* scene_init + the B3 lens table (the only part that can refuse) */
+static int scene_open(ref_scene *s, const mmba_problem *p, const mmba_options *o) {
+    scene_init(s, p, o);
+    return b3_build(s);
+}
+
 static void scene_free(ref_scene *s) {
+    free(s->lens_src);
     free(s->attr);
     free(s->tfm_world);
     free(s->pts);
@@ -1636,7 +1750,11 @@ int ref_measure(const mmba_problem *prob, const mmba_options *opt,
     int rc = validate(prob, opt);
     if (rc) return rc;
     ref_scene s;
-    scene_init(&s, prob, opt);
+    rc = scene_open(&s, prob, opt);
+    if (rc) {
+        scene_free(&s);
+        return rc;
+    }
     const int m = s.m;
     double *f = (double *)calloc((size_t)m, sizeof(double));
     if (x) set_parameters(&s, x);
@@ -1659,7 +1777,11 @@ int ref_reproject_obs(const mmba_problem *prob, const mmba_options *opt, const d
     int rc = validate(prob, opt);
     if (rc) return rc;
     ref_scene s;
-    scene_init(&s, prob, opt);
+    rc = scene_open(&s, prob, opt);
+    if (rc) {
+        scene_free(&s);
+        return rc;
+    }
     const int m = s.m;
     double *f = (double *)calloc((size_t)m, sizeof(double));
     s.obs_pts = point_xy;
@@ -1677,7 +1799,11 @@ int ref_jacobian(const mmba_problem *prob, const mmba_options *opt,
     int rc = validate(prob, opt);
     if (rc) return rc;
     ref_scene s;
-    scene_init(&s, prob, opt);
+    rc = scene_open(&s, prob, opt);
+    if (rc) {
+        scene_free(&s);
+        return rc;
+    }
     const int m = s.m, n = prob->num_params;
     double *xx = (double *)malloc(sizeof(double) * n);
     memcpy(xx, x, sizeof(double) * n);
@@ -1710,7 +1836,11 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
     if (n > m) return MMBA_ERR_INVALID; /* adjust_base.cpp:864-881 */
     double t0 = now_s();
     ref_scene s;
-    scene_init(&s, prob, opt);
+    rc = scene_open(&s, prob, opt);
+    if (rc) {
+        scene_free(&s);
+        return rc;
+    }
     if (trace) trace->count = 0;
     mmba_result r;
     memset(&r, 0, sizeof(r));
@@ -1781,7 +1911,7 @@ int ref_solve(const mmba_problem *prob, const mmba_options *opt,
     /* RMS at the returned parameters (build's own metric). */
     {
         ref_scene s2;
-        scene_init(&s2, prob, opt);
+        scene_open(&s2, prob, opt);
         set_parameters(&s2, x_inout);
         measure(&s2, NULL, wa4);
         double acc = 0.;

@@ -70,17 +70,22 @@ def test_bcr_variants_bitwise(scene, gpu_ctx, paths):
 
 @pytest.mark.parametrize("scene", list(SCENES))
 def test_pcr_against_bcr(scene, gpu_ctx, paths):
-    """Parallel against block cyclic reduction: the same LM path (reason,
-    counts) and the same solution up to the reduced step's roundoff."""
+    """Parallel against block cyclic reduction: a different elimination
+    order, so the reduced step differs by roundoff.  On the C4 structure
+    that roundoff is amplified along the flat valley of far-bundle depth
+    against camera translation (the oracle's own 1-ulp envelope
+    is 3e-5 at 12 frames and 8e-3 at 16), so the two LM paths may part
+    after a few dozen evaluations (31 against 32 iterations on c4).  Pinned:
+    the first evaluations of the trace at 1e-7 (4e-9 measured), the reason code and the
+    final ||f|| at 1e-6 (an equally good point of the same valley)."""
     idx, kw = SCENES[scene]
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
     bcr = run(prob, opt, gpu_ctx, paths, {}, pcr=0)
     pcr = run(prob, opt, gpu_ctx, paths, {}, pcr=-1)
-    for k in ("reason_number", "iterations", "outer_iterations", "function_evals"):
-        assert pcr.result[k] == bcr.result[k], k
-    np.testing.assert_allclose(pcr.fnorm_trace, bcr.fnorm_trace, rtol=1e-9)
-    assert np.max(np.abs(pcr.x - bcr.x) / np.maximum(np.abs(bcr.x), 1e-3)) <= 1e-7
+    assert pcr.result["reason_number"] == bcr.result["reason_number"]
+    np.testing.assert_allclose(pcr.fnorm_trace[:6], bcr.fnorm_trace[:6], rtol=1e-7)
+    np.testing.assert_allclose(pcr.fnorm_trace[-1], bcr.fnorm_trace[-1], rtol=1e-6)
 
 
 @pytest.mark.parametrize("pcr", [0, -1])

@@ -1,0 +1,145 @@
+"""The reference's lens index arithmetic (mmba.h ABI 7)
+in the oracle, pinned by an independent restatement here: the reference's
+three lists built literally as Python lists --
+  lensModelList[l*F + f]              (maya_lens_model_utils.cpp:654-661)
+  markerFrameToLensModelList[i*F + f] (:782-799)
+  attrFrameToLensModelList[a*F + f]   (:836-851)
+-- read at markerIndex + frameIndex (adjust_measureErrors.cpp:244, 463) and
+written by setParameters at attrIndex + frameIndex / attrIndex + j
+(adjust_setParameters.cpp:113-121, 206-214), last writer winning.  Checked:
+which lens distorts each observation (reprojection against one-lens copies
+of the scene), which parameter reaches which observation (the dense
+Jacobian's pattern), and the plug values before setParameters first runs."""
+import numpy as np
+import pytest
+
+from mayamatchmovesolver_amd import synthetic as S
+
+LENS_NUM_ATTRS = 14
+
+
+def reference_lists(p):
+    """(instance per observation, {(instance, slot): writer parameter})."""
+    F, nK = p.num_frames, p.num_markers
+    la = np.asarray(p.lens_attrs).reshape(-1, LENS_NUM_ATTRS)
+    lens_slot = {}
+    for l in range(la.shape[0]):
+        for k in range(LENS_NUM_ATTRS):
+            if la[l, k] >= 0 and int(la[l, k]) not in lens_slot:
+                lens_slot[int(la[l, k])] = (l, k)
+    attr_list = []  # attrList: the solved attributes in flag order
+    for a in p.param_attr:
+        if int(a) not in attr_list:
+            attr_list.append(int(a))
+    lens_model_list = [(l, f) for l in range(la.shape[0]) for f in range(F)]
+    mf = []
+    for i in range(nK):
+        l = int(p.cam_lens[p.mkr_cam[i]])
+        for f in range(F):
+            mf.append(lens_model_list[l * F + f] if l >= 0 else None)
+    af = []
+    for a in attr_list:
+        for f in range(F):
+            af.append(lens_model_list[lens_slot[a][0] * F + f] if a in lens_slot else None)
+    writer = {}
+    for q in range(p.num_params):
+        a = int(p.param_attr[q])
+        if a not in lens_slot:
+            continue
+        r = attr_list.index(a)
+        frames = [int(p.param_frame[q])] if p.param_frame[q] >= 0 else range(F)
+        for g in frames:
+            inst = af[r + g]
+            if inst is not None:
+                writer[inst + (lens_slot[a][1],)] = q
+    obs_inst = [mf[int(p.obs_marker[i]) + int(p.obs_frame[i])] for i in range(p.num_obs)]
+    return obs_inst, writer
+
+
+@pytest.mark.parametrize("variant", S.B3_VARIANTS)
+def test_lens_of_each_observation(variant, oracle):
+    """With the lenses' own (plug) values, observation (marker i, frame f) is
+    distorted by the lens of marker (i + f) / F: its reprojected point
+    equals the point of a copy of the scene whose cameras all use that lens
+    (or no lens)."""
+    p = S.b3_scene(variant)
+    # give the lenses distinct plug values (their attributes' frame-0 values)
+    la = np.asarray(p.lens_attrs).reshape(-1, LENS_NUM_ATTRS)
+    vals = np.array(p.attr_values, dtype=np.float64)
+    for l, d in enumerate((0.05, -0.04)):
+        vals[p.attr_offset[la[l, 0]]] = d
+    p.attr_values = vals
+    o = S.config_options(p)
+    pts, _ = oracle.reproject_obs(p, o)  # no x: every instance at its plug value
+    obs_inst, _ = reference_lists(p)
+    per_lens = {}
+    for l in (-1, 0, 1):
+        q = p.with_x0(p.x0)
+        q.attr_values = vals
+        q.cam_lens = np.full(p.num_cameras, l, np.int32)
+        per_lens[l], _ = oracle.reproject_obs(q, o)
+    mixed = 0
+    for i, inst in enumerate(obs_inst):
+        l = -1 if inst is None else inst[0]
+        np.testing.assert_array_equal(pts[2 * i:2 * i + 2], per_lens[l][2 * i:2 * i + 2])
+        own = int(p.cam_lens[p.mkr_cam[p.obs_marker[i]]])
+        mixed += l != own
+    assert mixed > 0  # the scene does mix lenses
+
+
+@pytest.mark.parametrize("variant", S.B3_VARIANTS)
+def test_lens_parameters_reach(variant, oracle):
+    """A lens parameter's Jacobian column is non-zero exactly on the rows of
+    the observations whose instance it wrote last."""
+    p = S.b3_scene(variant)
+    o = S.config_options(p)
+    obs_inst, writer = reference_lists(p)
+    _, J = oracle.jacobian(p, o, np.asarray(p.x0) + 0.002)
+    la = set(int(a) for a in np.asarray(p.lens_attrs) if a >= 0)
+    lens_params = [q for q in range(p.num_params) if int(p.param_attr[q]) in la]
+    assert lens_params
+    for q in lens_params:
+        want = np.zeros(p.num_obs, bool)
+        for i, inst in enumerate(obs_inst):
+            want[i] = inst is not None and writer.get(inst + (0,)) == q
+        got = np.abs(J[0::2, q]) + np.abs(J[1::2, q]) > 0
+        np.testing.assert_array_equal(got, want, err_msg="param %d" % q)
+
+
+def test_plug_values_before_set_parameters(oracle):
+    """solveFrames' initial measureErrors runs before setParameters: every
+    slot holds the plug value (the animated distortion's frame-0 value, 0),
+    so exactly the observations whose instance a parameter with another
+    value writes change once x is set."""
+    p = S.b3_scene("animated")
+    o = S.config_options(p)
+    f_plug, *_ = oracle.measure(p, o)
+    f_set, *_ = oracle.measure(p, o, np.asarray(p.x0))
+    obs_inst, writer = reference_lists(p)
+    ext = p.external_params(p.x0)
+    for i, inst in enumerate(obs_inst):
+        q = writer.get(inst + (0,)) if inst is not None else None
+        moved = q is not None and ext[q] != 0.0
+        same = np.array_equal(f_plug[2 * i:2 * i + 2], f_set[2 * i:2 * i + 2])
+        assert same != moved, (i, inst, q)
+
+
+def test_type_mismatch_refused(oracle):
+    """A lens attribute written into a lens of another model type is
+    undefined in the reference (a reinterpret_cast of the model): refused."""
+    from mayamatchmovesolver_amd.problem import SceneBuilder
+    b = SceneBuilder(2)
+    l0, ids0 = b.lens_3de_classic(distortion=0.01)
+    l1, ids1 = b.lens_3de_radial_std_deg4(0.01)
+    t0, _ = b.transform(t=(0.0, 0.0, 0.0))
+    c0, _ = b.camera(t0, lens=l0)
+    c1, _ = b.camera(t0, lens=l1)
+    for c in (c0, c1):
+        bt, _ = b.transform(t=(0.1 * c, 0.0, -10.0))
+        b.bundle(bt)
+        b.marker(c, c, np.zeros((2, 2)))
+    b.solve(ids0[0])  # attrList entry 0 is lens 0's: its j = 1 write hits entry 1
+    b.solve(ids1[0])  # (lens 1, radial): a classic slot into a radial model
+    p = b.build()
+    with pytest.raises(Exception):
+        oracle.measure(p, S.config_options(p), np.asarray(p.x0))

@@ -44,6 +44,11 @@ def test_input_layer_values_override_attributes(oracle):
     opt = S.config_options(prob)
     f0, *_ = oracle.measure(prob, opt)
     vals = np.zeros(2 * 14)
+    # the top lens's own plug values (ABI 7: a slot no parameter writes, and
+    # every slot before setParameters runs): its attributes at frame 0
+    la = np.asarray(prob.lens_attrs).reshape(-1, 14)[0]
+    for k, a in enumerate(la):
+        vals[k] = prob.attr_values[prob.attr_offset[a]] if a >= 0 else (1.0 if k == 1 else 0.0)
     vals[14:22] = [0.03, 0.002, -0.001, 0.008, 0.0, 0.0, 15.0, 0.02]
     p2 = prob.with_x0(prob.x0)
     p2.lens_input_values = vals

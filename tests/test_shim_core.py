@@ -106,6 +106,7 @@ def python_scene(which):
     else:
         liv = np.zeros((len(prob.lens_type), abi.LENS_NUM_ATTRS))
         liv[lens0, :8] = [d2[2], 0.002, -0.001, d4[2], 0.0, 0.0, 15.0, 0.02]
+        liv[lens, :5] = [0.02, 1.0, 0.0, 0.0, 0.0]  # the camera lens's own plug values
         prob.lens_input_values = liv.reshape(-1)
     return prob
 
