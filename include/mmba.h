@@ -563,7 +563,13 @@ typedef struct mmba_kernel_stats {
                                host's lmder decision was not the one the
                                host took (expected 0; the replay enqueues
                                every Jacobian after the decision)          */
-    int32_t pad_ks0;
+    int32_t band_solver;    /* ABI 7: the band reduced system's solver --
+                               0 none (not a band plan), 1 partitioned band
+                               Cholesky chains, 2 block cyclic reduction,
+                               3 parallel cyclic reduction, 4 separator form
+                               (sharded: interiors by parallel cyclic
+                               reduction, separator system all-reduced),
+                               5 block diagonal + arrow                    */
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);
@@ -583,7 +589,9 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
 #define MMBA_PATH_PERFRAME_BATCH 6 /* 0: per-frame mode with one plan per frame */
 #define MMBA_PATH_LOCAL_RING 7     /* 1: in-process communicators sum in ring order */
 #define MMBA_PATH_PROBE 8          /* 1: band / BCR phase probe, printed when the plan is destroyed */
-#define MMBA_PATH_NUM 9
+#define MMBA_PATH_SHARD_SEP 9      /* 0: sharded plans without an arrow all-reduce the whole
+                                      reduced system instead of its separator form */
+#define MMBA_PATH_NUM 10
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

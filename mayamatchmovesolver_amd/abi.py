@@ -33,7 +33,8 @@ PATH_DENSE = 5
 PATH_PERFRAME_BATCH = 6
 PATH_LOCAL_RING = 7
 PATH_PROBE = 8
-PATH_NUM = 9
+PATH_SHARD_SEP = 9
+PATH_NUM = 10
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -216,7 +217,7 @@ class MmbaKernelStats(C.Structure):
         ("dataflow_fallback", C.c_int32),
         ("shards_replicated", C.c_int32),
         ("spec_replays", C.c_int32),
-        ("pad_ks0", C.c_int32),
+        ("band_solver", C.c_int32),
     ]
 
     def as_dict(self):

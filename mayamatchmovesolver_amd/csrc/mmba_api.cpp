@@ -18,8 +18,8 @@ namespace mmba {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 
-static_assert(MMBA_PATH_NUM == 9, "one initialiser per path key");
-static std::atomic<int> g_path[MMBA_PATH_NUM] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(MMBA_PATH_NUM == 10, "one initialiser per path key");
+static std::atomic<int> g_path[MMBA_PATH_NUM] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int path_choice(int key) {
     return (key > 0 && key < MMBA_PATH_NUM) ? g_path[key].load() : -1;
 }
@@ -361,6 +361,15 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         out->dataflow_fallback = p.bs.df_off ? 1 : 0;
         out->shards_replicated = p.replicated ? 1 : 0;
         out->spec_replays = p.spec_replays;
+        {
+            const BandSolver &b = p.bs;
+            out->band_solver = !p.band ? 0
+                               : b.use_bd ? 5
+                               : b.pcr_int ? 4
+                               : (b.use_pcr && !b.df_off) ? 3
+                               : b.use_bcr ? 2
+                               : 1;
+        }
         // Algorithmic bytes: B_J = 48 + 8 p_c p_b per observation
         // for the Jacobian + normal-equation pass, B_f = 48 per observation for
         // the residual pass.

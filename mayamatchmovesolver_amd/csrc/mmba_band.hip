@@ -570,6 +570,74 @@ __global__ void k_band_tscatter(const double *__restrict__ vT, int w, int nb, in
 }
 
 // ---------------------------------------------------------------------------
+// Separator form of the sharded solve (BandSolver::pcr_int): the shard's one
+// partition has its interior eliminated by parallel cyclic reduction, XA =
+// S_II^-1 A^T (column-major, ast rows) and yI = S_II^-1 r_I come from
+// pcr_rhs_mc.  A (apool, row-major na x ast) is non-zero only on the first
+// and last w interior columns, so every product below runs over those.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int sep_col(int t, int ast, int w) {
+    // t-th column of A's non-zero range: [0, min(w, ast)) then [max(w, ast - w), ast)
+    const int n0 = min(w, ast);
+    return t < n0 ? t : max(w, ast - w) + (t - n0);
+}
+__device__ __forceinline__ int sep_ncols(int ast, int w) {
+    return min(w, ast) + (ast - max(w, ast - w));
+}
+
+// zpool: -Z_p = -(A XA) (packed lower), the partition's Schur update of T
+__global__ void k_sep_z(const BandPart *__restrict__ part, int w, const double *__restrict__ apool,
+                        const double *__restrict__ XA, double *zpool) {
+    const BandPart pd = *part;
+    const int na = pd.na, ast = pd.r1 - pd.r0, nc = sep_ncols(ast, w);
+    const double *A = apool + pd.aoff;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= na * (na + 1) / 2) return;
+    int a = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    while ((a + 1) * (a + 2) / 2 <= e) ++a;
+    while (a * (a + 1) / 2 > e) --a;
+    const int b = e - a * (a + 1) / 2;
+    double acc = 0.;
+    for (int t = 0; t < nc; ++t) {
+        const int c = sep_col(t, ast, w);
+        acc = fma(A[(size_t)a * ast + c], XA[(size_t)b * ast + c], acc);
+    }
+    zpool[pd.zoff + e] = -acc;
+}
+
+// cpool: c_p = A yI (what the partition takes from the separators' rhs)
+__global__ void k_sep_c(const BandPart *__restrict__ part, int w, const double *__restrict__ apool,
+                        const double *__restrict__ y, double *cpool) {
+    const BandPart pd = *part;
+    const int na = pd.na, ast = pd.r1 - pd.r0, nc = sep_ncols(ast, w);
+    const double *A = apool + pd.aoff;
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= na) return;
+    double acc = 0.;
+    for (int t = 0; t < nc; ++t) {
+        const int c = sep_col(t, ast, w);
+        acc = fma(A[(size_t)a * ast + c], y[pd.r0 + c], acc);
+    }
+    cpool[pd.coff + a] = acc;
+}
+
+// x_I = yI - XA x_A, x_A = x at the partition's separator rows (solved first)
+__global__ void k_sep_back(const BandPart *__restrict__ part, const double *__restrict__ XA,
+                           const double *__restrict__ y, double *x) {
+    __shared__ double xA[2 * WBAND_PART];
+    const BandPart pd = *part;
+    const int na = pd.na, ast = pd.r1 - pd.r0;
+    for (int a = threadIdx.x; a < na; a += blockDim.x)
+        xA[a] = x[a < pd.nprev ? pd.sprev + a : pd.snext + (a - pd.nprev)];
+    __syncthreads();
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= ast) return;
+    double acc = y[pd.r0 + r];
+    for (int a = 0; a < na; ++a) acc = fma(-XA[(size_t)a * ast + r], xA[a], acc);
+    x[pd.r0 + r] = acc;
+}
+
+// ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
 static inline int nblk_(long n, int bs) { return (int)((n + bs - 1) / bs); }
@@ -595,8 +663,18 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
         k_band_extract<<<grid, 256, 0, s>>>(B.Bd, B.w, B.Ga, B.nb, B.d_parts + B.p_lo, nloc,
                                             B.apool);
     }
-    k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGMAX, false><<<nloc, 256, 0, s>>>(
-        B.Bd, B.w, B.d_parts + B.p_lo, B.apool, B.zpool, B.Dinv, nullptr, nullptr, fail, probe);
+    if (B.pcr_int) {
+        // the interior's reduction (its logs), then XA = S_II^-1 A^T and -A XA
+        const BandPart &hp = B.hpart;
+        const int ast = hp.r1 - hp.r0;
+        pcr_solve(s, B.ipcr, B.izero, B.ix, nullptr, fail);
+        pcr_rhs_mc(s, B.ipcr, B.apool + hp.aoff, ast, hp.na, B.XA, ast, fail);
+        k_sep_z<<<nblk_((long)hp.na * (hp.na + 1) / 2, 256), 256, 0, s>>>(
+            B.d_parts + B.p_lo, B.w, B.apool, B.XA, B.zpool);
+    } else {
+        k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGMAX, false><<<nloc, 256, 0, s>>>(
+            B.Bd, B.w, B.d_parts + B.p_lo, B.apool, B.zpool, B.Dinv, nullptr, nullptr, fail, probe);
+    }
     {
         const int n = nbT * (2 * B.w) + B.nG * nbT + NGMAX * NGMAX;
         k_band_tassemble<<<nblk_(n, 256), 256, 0, s>>>(B.Bd, B.w, B.Ga, B.Gd, B.nb, B.nG,
@@ -634,8 +712,15 @@ void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y
     }
     const int nbT = (B.P - 1) * B.w;
     const int nloc = B.p_hi - B.p_lo;
-    k_band_fwd<8, 64, false><<<nloc, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts + B.p_lo, B.apool,
-                                                   B.Dinv, nullptr, B.cpool, r, y);
+    if (B.pcr_int) {  // y_I = S_II^-1 r_I, c = A y_I
+        const BandPart &hp = B.hpart;
+        const int ast = hp.r1 - hp.r0;
+        pcr_rhs_mc(s, B.ipcr, r + hp.r0, ast, 1, y + hp.r0, ast, B.fail);
+        k_sep_c<<<1, 64, 0, s>>>(B.d_parts + B.p_lo, B.w, B.apool, y, B.cpool);
+    } else {
+        k_band_fwd<8, 64, false><<<nloc, 256, 0, s>>>(B.Bd, B.w, B.nb, B.d_parts + B.p_lo,
+                                                       B.apool, B.Dinv, nullptr, B.cpool, r, y);
+    }
     k_band_trhs<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(r, B.w, B.nb, B.nG, B.d_parts, B.P,
                                                        B.p_lo, B.p_hi, B.cpool, B.rT);
     if (B.comm) B.comm->allreduce(B.rT, nbT + B.nG, ReduceOp::Sum, s);
@@ -666,6 +751,11 @@ void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *
                                                 B.TDinv, B.TGdinv, B.yT, B.xT);
     k_band_tscatter<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(B.xT, B.w, B.nb, B.nG, B.d_parts,
                                                            B.P, x);
+    if (B.pcr_int) {
+        const int ast = B.hpart.r1 - B.hpart.r0;
+        k_sep_back<<<nblk_(ast, 256), 256, 0, s>>>(B.d_parts + B.p_lo, B.XA, y, x);
+        return;
+    }
     k_band_bwd<8, 64, false><<<B.p_hi - B.p_lo, 256, 0, s>>>(
         B.Bd, B.w, B.nb, B.d_parts + B.p_lo, B.apool, B.Dinv, nullptr, y, x);
 }

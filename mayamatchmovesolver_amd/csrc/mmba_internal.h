@@ -101,6 +101,9 @@ struct BcrDev {
 // pub[(lvl * nblk + j) * (3 K^2 + K)]: C^-1, C^-1 L, C^-1 U (column-major) and
 // C^-1 r of block j's factor at level lvl (its final level: C^-1 and rho);
 // wlog: the update products W1, W2 of every (level, block) (Newton pass).
+// right-hand sides of one k_pcr_rhs_mc launch, at most
+constexpr int PCR_NCMAX = 48;
+
 struct PcrDev {
     int K = 0, nb = 0, w = 0, nblk = 0, nlev = 0;
     const double *Bd = nullptr;  // band input [nb][w+1]
@@ -108,6 +111,10 @@ struct PcrDev {
     int *fflag = nullptr, *rflag = nullptr;  // [nlev][nblk] epochs
     int *flev = nullptr;                     // final level of every block
     const int *row_param = nullptr;          // reduced row -> parameter (scatter of x)
+    // several right-hand sides (k_pcr_rhs_mc): publications [nlev][nblk][2 K
+    // PCR_NCMAX] and their epochs
+    double *mpub = nullptr;
+    int *mflag = nullptr;
 };
 
 // Block-diagonal + arrow reduced system (mmba_bdiag.hip): no solved bundle,
@@ -201,6 +208,17 @@ struct BandSolver {
     size_t tcount = 0;                       // TBd | TGa | TGd are contiguous
     BandPart *d_tpart = nullptr;
     double *rT = nullptr, *yT = nullptr, *xT = nullptr;
+    // separator form of the sharded solve (one partition per shard, no
+    // arrow): the shard's interior is eliminated by parallel cyclic
+    // reduction (ipcr, on the interior rows of Bd) instead of a band
+    // Cholesky chain; XA = S_II^-1 A_p^T (column-major, interior rows x na)
+    // gives the partition's Schur term A_p XA and the back substitution,
+    // y's interior rows hold S_II^-1 r (not L^-1 r)
+    bool pcr_int = false;
+    PcrDev ipcr;
+    BandPart hpart{};                        // the shard's partition (host copy)
+    double *XA = nullptr, *izero = nullptr, *ix = nullptr;
+    int *fail = nullptr;                     // the plan's failure flag
 };
 
 // Where entry (R, C), R >= C, of the reduced system lives.

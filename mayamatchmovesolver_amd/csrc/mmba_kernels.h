@@ -296,6 +296,10 @@ void bcr_backward(hipStream_t s, const BandSolver &B, const double *y, double *x
 // the last pcr_solve; workgroups of the solve kernel resident at once.
 void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, double *xs, int *fail);
 void pcr_rhs_dot(hipStream_t s, const PcrDev &P, const double *w, const int *mask, int *fail);
+// Z = S^-1 R for nc <= PCR_NCMAX column-major right-hand sides, with the
+// factors of the last pcr_solve on P (mmba_pcr.hip)
+void pcr_rhs_mc(hipStream_t s, const PcrDev &P, const double *R, int ldr, int nc, double *Z,
+                int ldz, int *fail);
 int pcr_max_resident(int K);
 // Block-diagonal + arrow solver (mmba_bdiag.hip): factor S, y = L^-1 r and,
 // with x, the solution (scattered to parameter order into xs when non-null).
@@ -313,6 +317,10 @@ void launch_sumsq(hipStream_t s, const double *a, const double *d, int n, double
 void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, double *partial,
                       int nparts, double *out, const int *mask = nullptr,
                       unsigned int *ticket = nullptr);
+// sum of y^2 over mask-1 rows and y v over mask-2 rows (separator form's
+// Newton term)
+void launch_sumsq_mix(hipStream_t s, const double *y, const double *v, int n, double *partial,
+                      int nparts, double *out, const int *mask);
 void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out);
 void launch_gnorm(hipStream_t s, const double *g, const double *acnorm, int n, double fnorm,
                   double *partial, int nparts, double *out, const int *mask = nullptr,

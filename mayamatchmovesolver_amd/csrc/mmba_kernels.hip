@@ -2777,6 +2777,28 @@ __global__ void __launch_bounds__(256) k_sumsq(const double *__restrict__ a,
     finish_blocks<false>(red[0], partial, out, ticket);
 }
 
+// Newton term of the separator form (BandSolver::pcr_int): mask 1 rows add
+// y^2 (||L_T^-1 ..||^2 of the separator system), mask 2 rows y v (the
+// interior's v^T S_II^-1 v, y = S_II^-1 v there).
+__global__ void __launch_bounds__(256) k_sumsq_mix(const double *__restrict__ y,
+                                                   const double *__restrict__ v, int n,
+                                                   const int *__restrict__ mask, double *partial) {
+    __shared__ double red[256];
+    double s = 0.;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int m = mask[i];
+        if (m == 1) s += y[i] * y[i];
+        else if (m == 2) s += y[i] * v[i];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
 __global__ void __launch_bounds__(256) k_sumsq_div(const double *__restrict__ a,
                                                    const double *__restrict__ d, int n,
                                                    const int *__restrict__ mask, double *partial,
@@ -3747,6 +3769,11 @@ void launch_sumsq_div(hipStream_t s, const double *a, const double *d, int n, do
                       int nparts, double *out, const int *mask, unsigned int *ticket) {
     k_sumsq_div<<<nparts, 256, 0, s>>>(a, d, n, mask, partial, out, ticket);
     if (!ticket) k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
+}
+void launch_sumsq_mix(hipStream_t s, const double *y, const double *v, int n, double *partial,
+                      int nparts, double *out, const int *mask) {
+    k_sumsq_mix<<<nparts, 256, 0, s>>>(y, v, n, mask, partial);
+    k_reduce_sum<<<1, 256, 0, s>>>(partial, nparts, out);
 }
 void launch_reduce_sum(hipStream_t s, const double *partial, int n, double *out) {
     k_reduce_sum<<<1, 256, 0, s>>>(partial, n, out);

@@ -413,6 +413,99 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
     if (lane == 0) part[j] = v;
 }
 
+// ---------------------------------------------------------------------------
+// Several right-hand sides at once: Z = (S)^-1 R with the factors (logs) of
+// the last k_pcr_solve, R and Z column-major (element (row r, column c) at
+// R[c * ldr + r], nc <= PCR_NCMAX columns).  The separator form of the
+// sharded solve (mmba_band.hip, Plan::setup_band) applies a shard interior's
+// inverse to its boundary couplings and to its right-hand side this way.  One
+// 256-thread workgroup per block; per level: rho = C^-1 R, publish Q^T rho
+// (right consumer) and P^T rho (left consumer), subtract the neighbours'; at
+// the block's last level Z = C^-T C^-1 R.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__restrict__ R,
+                                                    int ldr, int nc, double *Z, int ldz,
+                                                    double *mpub, int *mflag, unsigned epoch,
+                                                    int *fail) {
+    constexpr int LS = pcr_log_size<K>();
+    constexpr int NS = PCR_NCMAX + 1;  // LDS row stride
+    __shared__ double sr[K * NS], srho[K * NS], sl[3 * K * K];
+    __shared__ int ok_s;
+    const int tid = threadIdx.x, j = blockIdx.x, nblk = P.nblk, nb = P.nb;
+    const int ne = K * nc;  // entries (row i, column c) of the block's right-hand sides
+    for (int q = tid; q < ne; q += 256) {
+        const int i = q / nc, c = q % nc, row = j * K + i;
+        sr[i * NS + c] = row < nb ? R[(size_t)c * ldr + row] : 0.;
+    }
+    const int L = P.flev[j];
+    const size_t pst = (size_t)2 * K * PCR_NCMAX;  // doubles of one (level, block) publication
+    int s = 1;
+    for (int lvl = 0;; ++lvl, s *= 2) {
+        const double *lg = P.wlog + ((size_t)lvl * nblk + j) * LS;
+        for (int q = tid; q < (lvl < L ? 3 : 1) * K * K; q += 256) sl[q] = lg[q];
+        __syncthreads();
+        // rho = C^-1 R
+        for (int q = tid; q < ne; q += 256) {
+            const int i = q / nc, c = q % nc;
+            double a = 0.;
+#pragma unroll 8
+            for (int k = 0; k < K; ++k) a = fma(sl[i * K + k], sr[k * NS + c], a);
+            srho[i * NS + c] = a;
+        }
+        __syncthreads();
+        if (lvl == L) {  // uncoupled: Z = C^-T rho
+            for (int q = tid; q < ne; q += 256) {
+                const int i = q / nc, c = q % nc, row = j * K + i;
+                double a = 0.;
+#pragma unroll 8
+                for (int k = 0; k < K; ++k) a = fma(sl[k * K + i], srho[k * NS + c], a);
+                if (row < nb) Z[(size_t)c * ldz + row] = a;
+            }
+            return;
+        }
+        const bool hp = j - s >= 0, hq = j + s < nblk;
+        double *mp = mpub + ((size_t)lvl * nblk + j) * pst;
+        // (Q^T rho) for the right consumer, (P^T rho) for the left one
+        for (int q = tid; q < ne; q += 256) {
+            const int i = q / nc, c = q % nc;
+            double a = 0., b = 0.;
+#pragma unroll 8
+            for (int k = 0; k < K; ++k) {
+                a = fma(sl[2 * K * K + k * K + i], srho[k * NS + c], a);
+                b = fma(sl[K * K + k * K + i], srho[k * NS + c], b);
+            }
+            if (hq) bcr_st(mp + q, a);
+            if (hp) bcr_st(mp + K * PCR_NCMAX + q, b);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store((bcr_gu32 *)(mflag + (size_t)lvl * nblk + j), epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tid < 64) {
+            const bool ok = pcr_wait(mflag + (size_t)lvl * nblk, hp ? j - s : -1, hq ? j + s : -1,
+                                     epoch);
+            if (tid == 0) ok_s = ok;
+        }
+        __syncthreads();
+        if (!ok_s) {
+            if (tid == 0) atomicOr(fail, 2);
+            return;
+        }
+        // R -= Q_p^T rho_p + P_q^T rho_q
+        const double *pp = mpub + ((size_t)lvl * nblk + (hp ? j - s : j)) * pst;
+        const double *pq = mpub + ((size_t)lvl * nblk + (hq ? j + s : j)) * pst + K * PCR_NCMAX;
+        for (int q = tid; q < ne; q += 256) {
+            double sub = 0.;
+            if (hp) sub += bcr_ld(pp + q);
+            if (hq) sub += bcr_ld(pq + q);
+            sr[(q / nc) * NS + q % nc] -= sub;
+        }
+        __syncthreads();
+    }
+}
+
 static std::atomic<unsigned> g_pcr_epoch{0};
 
 static unsigned pcr_next_epoch() {
@@ -470,6 +563,19 @@ void pcr_rhs_dot(hipStream_t s, const PcrDev &P, const double *w, const int *mas
             case 8: k_pcr_rhs<8><<<P.nblk, 64, 0, s>>>(P, w, mask, P.part, ep, fail); break;
             case 16: k_pcr_rhs<16><<<P.nblk, 64, 0, s>>>(P, w, mask, P.part, ep, fail); break;
             default: k_pcr_rhs<24><<<P.nblk, 64, 0, s>>>(P, w, mask, P.part, ep, fail); break;
+        }
+    });
+}
+
+void pcr_rhs_mc(hipStream_t s, const PcrDev &P, const double *R, int ldr, int nc, double *Z,
+                int ldz, int *fail) {
+    if (nc <= 0 || nc > PCR_NCMAX) throw Invalid{"pcr_rhs_mc: 1..48 right-hand sides"};
+    pcr_ordered(s, [&] {
+        const unsigned ep = pcr_next_epoch();
+        switch (P.K) {
+            case 8: k_pcr_rhs_mc<8><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, P.mflag, ep, fail); break;
+            case 16: k_pcr_rhs_mc<16><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, P.mflag, ep, fail); break;
+            default: k_pcr_rhs_mc<24><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, P.mflag, ep, fail); break;
         }
     });
 }

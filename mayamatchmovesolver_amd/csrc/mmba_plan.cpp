@@ -1456,6 +1456,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_partial = dalloc<double>((size_t)8 * pw);  // rows 0..7 (launch_dist_stats: 0..2)
     d_scalar = dalloc<double>(NSLOT);
     d_fail = dalloc<int>(1);
+    bs.fail = d_fail;  // the separator form's right-hand-side passes report into it
     if (bs.use_bd) {
         std::vector<int> row_param(std::max(nR, 1), -1);
         for (int p = 0; p < n; ++p)
@@ -1620,7 +1621,7 @@ void Plan::setup_band(int Pforce) {
         // shards all-reduce S instead and each runs the log-depth solve on
         // it; MMBA_PATH_SHARD_BCR = 0 keeps the partitioned chain (tests)
         const bool shard_ok = nranks == 1 || path_choice(MMBA_PATH_SHARD_BCR) != 0;
-        if (shard_ok && w <= 32 && Pforce <= 0) {
+        if (shard_ok && w <= 32 && Pforce <= 0 && !sep_form(w)) {
             bs.use_bcr = true;
             bs.P = 1;
             bs.comm = nranks > 1 ? comm : nullptr;
@@ -1732,9 +1733,12 @@ void Plan::setup_band(int Pforce) {
         Rb_all.assign(1, nb);
     }
     // partitions per shard range [Ra_all[k], Rb_all[k]) (one range unsharded)
+    const bool sepf = sep_form(w);
     auto count_parts = [&](int len) {
         int P = 1;
-        if (Pforce > 0 && w <= WBAND_PART) {
+        if (sepf) {
+            // separator form: the shard's range is one partition
+        } else if (Pforce > 0 && w <= WBAND_PART) {
             P = std::max(1, std::min(Pforce, len / (w + 1)));
         } else if (w > 0 && w <= WBAND_PART) {
             // balance the interior chains (len/P rows) against the separator
@@ -1781,11 +1785,12 @@ void Plan::setup_band(int Pforce) {
         coff += q.na;
     }
     // ||L^-1 v||^2 terms counted by this shard: its interior rows; the
-    // separator and global rows (replicated) on the root shard
+    // separator and global rows (replicated) on the root shard.  Separator
+    // form: the interior's share is v^T S_II^-1 v = v . y (mask 2)
     {
         std::vector<int> ym(nR, 0);
         for (int p = bs.p_lo; p < bs.p_hi; ++p)
-            for (int r = parts[p].r0; r < parts[p].r1; ++r) ym[r] = 1;
+            for (int r = parts[p].r0; r < parts[p].r1; ++r) ym[r] = sepf ? 2 : 1;
         if (rank == 0) {
             for (int p = 0; p < P - 1; ++p)
                 for (int u = 0; u < w; ++u) ym[parts[p].snext + u] = 1;
@@ -1825,6 +1830,62 @@ void Plan::setup_band(int Pforce) {
         bs.yT = dalloc<double>(nbT + nG);
         bs.xT = dalloc<double>(nbT + nG);
     }
+    if (sepf) {
+        // the shard's interior by parallel cyclic reduction (mmba_pcr.hip) on
+        // its rows of Bd: the band layout is row-relative, so an offset view
+        // is the interior system with its couplings to the separators dropped
+        const BandPart &hp = parts[bs.p_lo];
+        const int ast = hp.r1 - hp.r0;
+        bs.pcr_int = true;
+        bs.hpart = hp;
+        bs.fail = d_fail;
+        PcrDev &Q = bs.ipcr;
+        Q.K = std::max(8, (w + 7) / 8 * 8);
+        Q.nb = ast;
+        Q.w = w;
+        Q.nblk = (ast + Q.K - 1) / Q.K;
+        int L = 0;
+        while ((1 << L) < Q.nblk) ++L;
+        Q.nlev = L;
+        Q.Bd = bs.Bd + (size_t)hp.r0 * (w + 1);
+        const size_t ps = (size_t)2 * Q.K * (Q.K + 1) + (size_t)Q.K * Q.K;
+        const size_t nl = std::max<size_t>(1, (size_t)L * Q.nblk);
+        Q.pub = dalloc<double>(nl * ps);
+        Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
+        Q.rpub = dalloc<double>(nl * 2 * Q.K);
+        Q.mpub = dalloc<double>(nl * 2 * Q.K * PCR_NCMAX);
+        Q.part = dalloc<double>(Q.nblk);
+        Q.fflag = dalloc<int>(nl);
+        Q.rflag = dalloc<int>(nl);
+        Q.mflag = dalloc<int>(nl);
+        MMBA_HIP(hipMemsetAsync(Q.fflag, 0, sizeof(int) * nl, s));
+        MMBA_HIP(hipMemsetAsync(Q.rflag, 0, sizeof(int) * nl, s));
+        MMBA_HIP(hipMemsetAsync(Q.mflag, 0, sizeof(int) * nl, s));
+        Q.flev = dalloc<int>(Q.nblk);
+        bs.XA = dalloc<double>((size_t)std::max(hp.na, 1) * ast);
+        bs.izero = dalloc<double>(ast);
+        bs.ix = dalloc<double>(ast);
+        MMBA_HIP(hipMemsetAsync(bs.izero, 0, sizeof(double) * ast, s));
+    }
+}
+
+// Separator form of the sharded reduced solve: every
+// shard eliminates the interior of its row range by parallel cyclic
+// reduction, only the separator system (the last w rows of every shard but
+// the last, with the shards' Schur terms) is all-reduced and solved on every
+// shard.  Needs no arrow, w <= 23 and every shard's interior resident on the
+// device; every shard decides the same from the shared partition.
+bool Plan::sep_form(int w) const {
+    if (nranks <= 1 || nG != 0 || w > 23 || w <= 0) return false;
+    if (path_choice(MMBA_PATH_SHARD_SEP) == 0 || path_choice(MMBA_PATH_SHARD_BCR) == 0) return false;
+    const int K = std::max(8, (w + 7) / 8 * 8);
+    int most = 0;
+    for (size_t k = 0; k < Ra_all.size(); ++k) {
+        const int len = Rb_all[k] - Ra_all[k] - ((int)k + 1 < (int)Ra_all.size() ? w : 0);
+        if (len < K) return false;
+        most = std::max(most, (len + K - 1) / K);
+    }
+    return most <= pcr_max_resident(K);
 }
 
 }  // namespace mmba

@@ -95,6 +95,7 @@ struct Plan {
     // setParameters first runs)
     int *d_inst_attr_plug = nullptr;
     void build_lens_instances(const mmba_problem *pr);
+    bool sep_form(int w) const;
     // P with every lens instance slot at its plug value: what the reference
     // measures before setParameters first runs (solveFrames' initial
     // measureErrors, adjust_base.cpp:1002-1004 then 1076-1089)

@@ -14,19 +14,22 @@ from mayamatchmovesolver_amd.solver import Comm, Context, Solver
 pytestmark = pytest.mark.gpu
 
 
-def run_sharded(prob, opt, n, replicated=None):
+def run_sharded(prob, opt, n, replicated=None, band_solver=None):
     """Solve on n in-process shards.  replicated (list): receives each shard's
     shards_replicated statistic (1: the problem did not shard and every shard
-    solved all of it, mmba_plan_create_sharded)."""
+    solved all of it, mmba_plan_create_sharded); band_solver (list): each
+    shard's band_solver statistic (4: the separator form)."""
     comms = Comm.local_group(n)
     ctxs = [Context(0) for _ in range(n)]
-    outs, errs, reps = [None] * n, [None] * n, [None] * n
+    outs, errs, reps, bsol = [None] * n, [None] * n, [None] * n, [None] * n
 
     def work(r):
         try:
             s = Solver(prob, opt, context=ctxs[r], comm=comms[r])
             try:
-                reps[r] = s.kernel_stats()["shards_replicated"]
+                st = s.kernel_stats()
+                reps[r] = st["shards_replicated"]
+                bsol[r] = st["band_solver"]
                 outs[r] = s.solve()
             finally:
                 s.close()
@@ -46,6 +49,8 @@ def run_sharded(prob, opt, n, replicated=None):
     assert errs == [None] * n, errs
     if replicated is not None:
         replicated[:] = reps
+    if band_solver is not None:
+        band_solver[:] = bsol
     return outs
 
 
@@ -70,10 +75,19 @@ def check_shards_agree(outs):
         assert o.result["iterations"] == outs[0].result["iterations"]
 
 
-# reduced-system solve of a sharded plan: S all-reduced and factored by block
-# cyclic reduction on every shard (default), or the partitioned band chain
-# with an all-reduced separator system (MMBA_PATH_SHARD_BCR = 0)
-SOLVES = {"bcr": -1, "partitioned": 0}
+# reduced-system solve of a sharded plan: the separator form (default where
+# it applies: no arrow; each shard's interior by parallel cyclic reduction,
+# the separator system all-reduced), S all-reduced whole and solved by the
+# log-depth solvers on every shard (MMBA_PATH_SHARD_SEP = 0), or the
+# partitioned band chains with an all-reduced separator system
+# (MMBA_PATH_SHARD_BCR = 0)
+SOLVES = {"separator": {}, "whole": {abi.PATH_SHARD_SEP: 0},
+          "partitioned": {abi.PATH_SHARD_BCR: 0}}
+
+
+def pin_solve(paths, solve):
+    for k, v in SOLVES[solve].items():
+        paths(k, v)
 
 
 # summation order of the in-process all-reduce: rank order, or the ring
@@ -85,13 +99,16 @@ ORDERS = {"rank": 0, "ring": 1}
 @pytest.mark.parametrize("solve", list(SOLVES))
 @pytest.mark.parametrize("idx,kw,nshards", CASES)
 def test_sharded_matches_oracle(idx, kw, nshards, solve, order, oracle, paths):
-    paths(abi.PATH_SHARD_BCR, SOLVES[solve])
+    pin_solve(paths, solve)
     paths(abi.PATH_LOCAL_RING, ORDERS[order])
     prob = S.make_config(idx, **kw)
     opt = S.config_options(prob)
     xr, fr, eur, edr, rr, trr = oracle.solve(prob, opt)
-    outs = run_sharded(prob, opt, nshards)
+    bsol = []
+    outs = run_sharded(prob, opt, nshards, band_solver=bsol)
     check_shards_agree(outs)
+    if solve == "separator" and idx == 3:  # bundle Schur, no arrow: the separator form
+        assert bsol == [4] * nshards, bsol
     g = outs[0]
     assert g.result["reason_number"] == rr.reason_number, (g.result, rr.as_dict())
     assert g.result["outer_iterations"] == rr.outer_iterations
@@ -111,7 +128,7 @@ def test_sharded_ba_three_shards_structure(solve, gpu_ctx, paths):
     enough for a 1e-6 comparison (a rejected trial point moves by 1.4e-6), so
     the check is structural: same reason and counts, trace within 1e-5, x
     within 1e-4 (decomposition errors show up at 1e-2)."""
-    paths(abi.PATH_SHARD_BCR, SOLVES[solve])
+    pin_solve(paths, solve)
     prob = S.make_config(3, frames=54, scale=0.006, **WC)
     opt = S.config_options(prob)
     s = Solver(prob, opt, context=gpu_ctx)
@@ -156,10 +173,11 @@ def test_sharded_ba_many_shards(nshards, gpu_ctx):
         1e-3 * ref.result["error_final"]
 
 
+@pytest.mark.parametrize("solve", ["separator", "whole"])
 @pytest.mark.parametrize("order", list(ORDERS))
 @pytest.mark.parametrize("nshards", [2, 4, 8])
 @pytest.mark.parametrize("scene", ["c4", "wc"])
-def test_sharded_ba_x_before_the_valley(scene, nshards, order, gpu_ctx, paths):
+def test_sharded_ba_x_before_the_valley(scene, nshards, order, solve, gpu_ctx, paths):
     """x itself, on the headline C4 structure (4-frame tracks at depth
     20-200) and on the 6-frame variant, sharded against unsharded, with the
     evaluation budget capped at 2 (x0 and one full LM step): past that the
@@ -177,8 +195,14 @@ def test_sharded_ba_x_before_the_valley(scene, nshards, order, gpu_ctx, paths):
         ref = s.solve()
     finally:
         s.close()
-    outs = run_sharded(prob, opt, nshards)
+    pin_solve(paths, solve)
+    bsol = []
+    outs = run_sharded(prob, opt, nshards, band_solver=bsol)
     check_shards_agree(outs)
+    # the separator form where it applies (no arrow, half bandwidth <= 23:
+    # the C4 spec's 4-frame tracks; the 6-frame variant's band is wider)
+    if solve == "separator" and scene == "c4":
+        assert bsol == [4] * nshards, bsol
     g = outs[0]
     for k in ("reason_number", "iterations", "function_evals"):
         assert g.result[k] == ref.result[k], k
