@@ -462,8 +462,8 @@ def main():
                 roofline = {"bound": "mfma", "achieved": tf, "peak": FP64_MFMA_PEAK_TF,
                             "unit": "TFLOP/s", "frac": tf / FP64_MFMA_PEAK_TF, "traffic": None,
                             "kernel": "dense reduced-system Cholesky (n_r^3/3 flop per "
-                                      "factorisation; k_dense_potf64 + rocBLAS fp64 MFMA "
-                                      "GEMM/SYRK)",
+                                      "factorisation; k_dense_potf64 + the hand-written "
+                                      "fp64 MFMA GEMM/SYRK k_dgemm_nt)",
                             "avg_ms": stats["chol_ms_avg"], "flops_per_launch":
                             stats["chol_flops"], "launches": stats["chol_launches"],
                             "k2_hbm": roofline}

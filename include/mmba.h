@@ -500,7 +500,8 @@ int mmba_plan_outputs(mmba_plan *plan, double *fvec_out, double *err_user_out,
  *     cb->interrupt is polled on the calling thread while the launch runs;
  *     once it returns non-zero every frame stops at its next evaluation or
  *     Jacobian poll (reason_number -1).  max_concurrency is not used.
- *     MMBA_PERFRAME_BATCH=0 in the environment selects the path below.
+ *     mmba_debug_set_path(MMBA_PATH_PERFRAME_BATCH, 0) selects the path
+ *     below (a test hook).
  *   - Otherwise one plan per frame: frames without a static parameter run
  *     max_concurrency at a time (0 = all) on host worker threads, each with
  *     its own stream; with a static parameter they are chained in order, as

@@ -365,7 +365,7 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
             const BandSolver &b = p.bs;
             out->band_solver = !p.band ? 0
                                : b.use_bd ? 5
-                               : b.pcr_int ? 4
+                               : (b.pcr_int && !b.df_off) ? 4
                                : (b.use_pcr && !b.df_off) ? 3
                                : b.use_bcr ? 2
                                : 1;

@@ -663,7 +663,7 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
         k_band_extract<<<grid, 256, 0, s>>>(B.Bd, B.w, B.Ga, B.nb, B.d_parts + B.p_lo, nloc,
                                             B.apool);
     }
-    if (B.pcr_int) {
+    if (B.pcr_int && !B.df_off) {  // (a timed-out wait: the band chains)
         // the interior's reduction (its logs), then XA = S_II^-1 A^T and -A XA
         const BandPart &hp = B.hpart;
         const int ast = hp.r1 - hp.r0;
@@ -712,7 +712,7 @@ void band_forward(hipStream_t s, const BandSolver &B, const double *r, double *y
     }
     const int nbT = (B.P - 1) * B.w;
     const int nloc = B.p_hi - B.p_lo;
-    if (B.pcr_int) {  // y_I = S_II^-1 r_I, c = A y_I
+    if (B.pcr_int && !B.df_off) {  // y_I = S_II^-1 r_I, c = A y_I
         const BandPart &hp = B.hpart;
         const int ast = hp.r1 - hp.r0;
         pcr_rhs_mc(s, B.ipcr, r + hp.r0, ast, 1, y + hp.r0, ast, B.fail);
@@ -751,7 +751,7 @@ void band_backward(hipStream_t s, const BandSolver &B, const double *y, double *
                                                 B.TDinv, B.TGdinv, B.yT, B.xT);
     k_band_tscatter<<<nblk_(nbT + B.nG, 256), 256, 0, s>>>(B.xT, B.w, B.nb, B.nG, B.d_parts,
                                                            B.P, x);
-    if (B.pcr_int) {
+    if (B.pcr_int && !B.df_off) {  // (a timed-out wait: the band chains)
         const int ast = B.hpart.r1 - B.hpart.r0;
         k_sep_back<<<nblk_(ast, 256), 256, 0, s>>>(B.d_parts + B.p_lo, B.XA, y, x);
         return;

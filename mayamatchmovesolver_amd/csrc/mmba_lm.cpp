@@ -736,7 +736,7 @@ void Plan::newton_enqueue(double dxnorm) {
                 launch_trsv_fwd(s, d_S, d_slot, NT, k, d_rows + r0, nr, d_Linv, d_wR, d_yR);
             }
         }
-        if (band && bs.pcr_int)
+        if (band && bs.pcr_int && !bs.df_off)
             launch_sumsq_mix(s, d_yR, d_wR, nR, d_partial, nparts, d_scalar + SL_NEWT_R, d_ymask);
         else if (!(band && bs.use_pcr && !bs.df_off))
             launch_sumsq(s, d_yR, nullptr, nRpad, d_partial, nparts, d_scalar + SL_NEWT_R,
