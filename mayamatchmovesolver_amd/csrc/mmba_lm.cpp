@@ -965,8 +965,8 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
     P.jcol_implicit = 0;  // this host-side reassembly reads jcol
     jac(d_x);
     P.jcol_implicit = implicit;
-    std::vector<double> J((size_t)2 * LMAX * M), Jr(nrows);
-    std::vector<int> jc((size_t)LMAX * M), nl(M), rp(nrows);
+    std::vector<double> J((size_t)2 * P.lmax * M), Jr(nrows);
+    std::vector<int> jc((size_t)std::max(P.lmax, 1) * M), nl(M), rp(nrows);
     if (nrows > 0) {
         MMBA_HIP(hipMemcpyAsync(Jr.data(), d_Jrow, sizeof(double) * nrows, hipMemcpyDeviceToHost,
                                 s));

@@ -1415,8 +1415,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_b15k = dalloc<double>(8);
         MMBA_HIP(hipMemsetAsync(d_b15k, 0, sizeof(double) * 8, s));
     }
-    d_J = dalloc<double>(std::max((size_t)2 * LMAX * M, (size_t)m + M));
-    d_jcol = dalloc<int>((size_t)LMAX * M);
+    // J / jcol: the widest observation's columns (D.lmax <= LMAX), not LMAX
+    d_J = dalloc<double>(std::max((size_t)2 * D.lmax * M, (size_t)m + M));
+    d_jcol = dalloc<int>((size_t)std::max(D.lmax, 1) * M);
     d_nloc = dalloc<int>(M);
     d_Acc = dalloc<double>((size_t)ncf * PCMAX * PCMAX);
     d_Acg = dalloc<double>((size_t)ncf * PCMAX * NGMAX);

@@ -9,6 +9,7 @@
 #   prof              rocprofv3 --kernel-trace --stats of the default bench
 #   pmc               FETCH_SIZE / WRITE_SIZE passes of the default bench
 #   iter              kernel traces + one-iteration timelines of C2 / C4 / C5
+#   ubench            tools/ubench dgemm_probe (C3 update shapes) and pcr_probe (C4 system)
 set -o pipefail
 OUT=${1:?out dir}
 shift
@@ -46,6 +47,10 @@ for step in "$@"; do
       for ctr in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$OUT/pmc_$ctr" -o c4 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/pmc_$ctr.json" 2> "$OUT/pmc_$ctr.err" || exit 1
       done ;;
+    ubench)
+      timeout -k 10 120 tools/ubench/dgemm_probe > "$OUT/dgemm_probe.txt" 2>&1 || { cat "$OUT/dgemm_probe.txt"; exit 1; }
+      timeout -k 10 120 tools/ubench/pcr_probe > "$OUT/pcr_probe.txt" 2>&1 || { cat "$OUT/pcr_probe.txt"; exit 1; }
+      cat "$OUT/dgemm_probe.txt" "$OUT/pcr_probe.txt" ;;
     iter)
       bash tools/gpu_iter.sh "$OUT/iter" || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
