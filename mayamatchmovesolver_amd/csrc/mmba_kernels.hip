@@ -788,6 +788,10 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     if (hl) {
         for (int q = P.inst_lpar_off[inst]; q < P.inst_lpar_off[inst + 1] && l < LMAX; ++q) {
             const int p = P.inst_lpar[q];
+            // an animated parameter's column re-measures its own frame only
+            // (adjust_solveFunc.cpp frameIndexEnable): the observations of
+            // other frames that read the instance it writes keep f - f = 0
+            if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
             double lc[MMBA_LENS_NUM_ATTRS];
             inst_coeffs(P, inst, Override{P.p_attr[p], ext_pert[p]}, lc);
             emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, lc), step[p], [&]() {

@@ -1271,7 +1271,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             }
             // the segment's lens columns: k_jacobian_rs reduces the
             // segment's rows into one block, so they must be the same
-            // parameters for every observation of the segment
+            // parameters for every observation of the segment, and (the
+            // blend re-measures the neighbouring frames too) each one static
+            // or keyed at the segment's own frame
             const int j0 = cf_obs_off[cf] < cf_obs_off[cf + 1] ? d_inst[cf_obs_off[cf]] : -1;
             for (int i = cf_obs_off[cf]; i < cf_obs_off[cf + 1]; ++i) {
                 const int j = d_inst[i];
@@ -1285,8 +1287,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
                                       "read lens instances with different parameters (B3)"};
             }
             if (j0 >= 0)
-                for (int q = inst_lpar_off_h[j0]; q < inst_lpar_off_h[j0 + 1]; ++q)
-                    cols.push_back(inst_lpar_h[q]);
+                for (int q = inst_lpar_off_h[j0]; q < inst_lpar_off_h[j0 + 1]; ++q) {
+                    const int p = inst_lpar_h[q];
+                    if (pr->param_frame[p] >= 0 && pr->param_frame[p] != cf_frame[cf])
+                        throw Unsupported{"rolling shutter where a camera-frame's lens instance "
+                                          "holds another frame's animated lens parameter (B3)"};
+                    cols.push_back(p);
+                }
             for (int l = 0; l < (int)cols.size() && l < LMAX; ++l)
                 if (p_class[cols[l]] == PC_G && gcnt[cf] < NGMAX) {
                     gcol[(size_t)NGMAX * cf + gcnt[cf]] = l;

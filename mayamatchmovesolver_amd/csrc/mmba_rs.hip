@@ -90,7 +90,9 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
     }
     if (hl)
         for (int q = P.inst_lpar_off[inst]; q < P.inst_lpar_off[inst + 1] && nl < LMAX; ++q) {
-            cp[nl] = P.inst_lpar[q];
+            const int p = P.inst_lpar[q];
+            if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;  // (plain instances: none)
+            cp[nl] = p;
             ck[nl++] = 2;
         }
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;

@@ -901,7 +901,7 @@ def rig_scene(n_cams=2, bundles=10, solve_cam1=True, stiffness=False, seed=11) -
     return b.build(meta={"name": "rig"})
 
 
-B3_VARIANTS = ("lens_first", "cam_first", "animated", "one_lens")
+B3_VARIANTS = ("lens_first", "cam_first", "animated", "animated_late", "one_lens")
 
 
 def b3_scene(variant="lens_first", frames=5, markers_per_cam=4, seed=23) -> Problem:
@@ -916,7 +916,12 @@ def b3_scene(variant="lens_first", frames=5, markers_per_cam=4, seed=23) -> Prob
       "lens_first": both lenses' distortion solved, listed before the cameras
       "cam_first":  the same, the lens attributes listed after the rotations
       "animated":   lens 0's distortion animated and solved (one parameter
-                    per frame, values differing per frame), after the rotations
+                    per frame, values differing per frame), lens attributes
+                    first: lens 1's static distortion then overwrites lens 0's
+                    clones at frames 1.. (attrList entry 1 + j lands in entry
+                    0's range), and marker i at frame f reads frame (i+f) % F
+      "animated_late": the same, the lens attributes after the rotations
+                    (their writes land on attrList entries of no lens)
       "one_lens":   camera 0 without a lens, camera 1's lens solved."""
     assert variant in B3_VARIANTS, variant
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -929,7 +934,7 @@ def b3_scene(variant="lens_first", frames=5, markers_per_cam=4, seed=23) -> Prob
     P = np.stack([rng.uniform(-0.25, 0.25, 2 * K) * depth, rng.uniform(-0.2, 0.2, 2 * K) * depth,
                   -depth], axis=1)
     truth = [(0.04, 1.0, 0.0, 0.0, 0.0), (-0.03, 1.0, 0.0, 0.0, 0.0)]
-    if variant == "animated":
+    if variant in ("animated", "animated_late"):
         d0 = 0.04 + 0.005 * fr
         lens0, lids0 = b.lens_3de_classic(distortion=np.zeros(F) + 0.01 * fr)
     else:
@@ -964,12 +969,13 @@ def b3_scene(variant="lens_first", frames=5, markers_per_cam=4, seed=23) -> Prob
                 xy[f] = (float(_noisy(rng, np.asarray(mx))), float(_noisy(rng, np.asarray(my))))
             b.marker(cam, j, xy)
     lens_solve = [lids1[0]] if variant == "one_lens" else [lids0[0], lids1[0]]
-    if variant == "lens_first":
+    first = variant in ("lens_first", "animated")
+    if first:
         for a in lens_solve:
             b.solve(a)
     for a in tids0[3:6] + tids1[3:6]:
         b.solve(a)
-    if variant != "lens_first":
+    if not first:
         for a in lens_solve:
             b.solve(a)
     return b.build(meta={"name": "b3_" + variant})
