@@ -195,6 +195,23 @@ def test_layered_lens_measure_jacobian_and_input_attr(oracle, gpu_ctx):
         d[name] = np.append(d[name], val)
     p2 = type(prob).from_npz_dict(d)
     p2.meta = dict(prob.meta)
+    # attrList (ABI 7): the solved attributes in flag order, then
+    # unsolved entries, the input layer's attribute at index 16 -- its static
+    # writes (attrIndex + j, j < 8) land on entry 2, a camera attribute, whose
+    # lens list entries are null.  (Appended right after the others, index 14,
+    # they would land on the classic lens's entry 1 and write a radial slot
+    # into a classic model: undefined in the reference, refused.)
+    order = []
+    for q in range(p2.num_params - 1):
+        if int(p2.param_attr[q]) not in order:
+            order.append(int(p2.param_attr[q]))
+    la = np.asarray(p2.lens_attrs).reshape(-1, 14)
+    lens_of = {int(la[l, k]): l for l in range(la.shape[0]) for k in range(14) if la[l, k] >= 0}
+    p2.param_ref_attr = np.array([order.index(int(p2.param_attr[q]))
+                                  for q in range(p2.num_params - 1)] + [16], np.int32)
+    ref_lens = [lens_of.get(a, -1) for a in order] + [-1] * (24 - len(order))
+    ref_lens[16] = lens_of[a]
+    p2.ref_attr_lens = np.array(ref_lens, np.int32)
     _, J2 = oracle.jacobian(p2, opt, p2.x0)
     assert not np.any(J2[:, -1])
     check_solve(p2, opt, oracle, gpu_ctx)

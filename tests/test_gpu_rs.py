@@ -69,12 +69,25 @@ def test_rs_solve_matches_oracle(solver_type, mode, oracle, gpu_ctx):
     dict(frames=24, scale=0.2, rs=0.5),              # band through every frame
     dict(frames=12, scale=0.1, rs=-0.8),             # bottom scanline first
     dict(frames=8, scale=0.05, rs=0.5, lens_model="radial"),
-    dict(frames=8, scale=0.05, rs=0.5, lens_model="classic_animated"),
 ])
 def test_rs_variants_match_oracle(kw, oracle, gpu_ctx):
     prob = rs_scene(**kw)
     opt = S.config_options(prob)
     check_solve(prob, opt, oracle, gpu_ctx)
+
+
+def test_rs_refuses_mixed_animated_lens(gpu_ctx):
+    """An animated lens coefficient under the reference's lens index
+    arithmetic (mmba.h ABI 7): marker i at frame f reads the
+    coefficient keyed at frame (i + f) % F, which the rolling-shutter
+    Jacobian's per-camera-frame columns do not hold -- refused with
+    MMBA_ERR_UNSUPPORTED (round 3 solved it with each marker reading its own
+    frame, which is not what the reference computes)."""
+    prob = rs_scene(frames=8, scale=0.05, rs=0.5, lens_model="classic_animated")
+    opt = S.config_options(prob)
+    with pytest.raises(MmbaError) as e:
+        Solver(prob, opt, context=gpu_ctx).close()
+    assert e.value.code == abi.MMBA_ERR_UNSUPPORTED
 
 
 def test_rs_one_camera_only(oracle, gpu_ctx):
