@@ -2,6 +2,7 @@
 #   gpurun --timeout 1200 -- 'bash tools/gpu.sh OUT STEP [STEP ...]'
 # Steps (each under its own time limit; the first failure ends the call):
 #   tests[:PYTEST_K]  the -m gpu suite (optionally only tests matching -k)
+#   testsall          the -m gpu suite without -x (every failure in one call)
 #   smoke             __graft_entry__.smoke()
 #   bench             the default bench line (C4, CPU baseline, PMC traffic)
 #   benchcfg:I        bench line of configs[I] (no CPU baseline)
@@ -18,6 +19,11 @@ ROOT=$(pwd)
 export TMPDIR=/tmp
 for step in "$@"; do
   case "$step" in
+    testsall)
+      # every failure in one call; the steps after it still run unless the
+      # run faulted or timed out (pytest: 1 = failed tests, 2+ = other)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > "$OUT/tests.log" 2>&1
+      rc=$?; tail -40 "$OUT/tests.log"; [ $rc -le 1 ] || exit $rc ;;
     tests*)
       K=${step#tests}; K=${K#:}
       if [ -n "$K" ]; then
