@@ -47,6 +47,18 @@ FP64_MFMA_PEAK_TF = 78.6  # MI355X dense FP64 matrix rate (spec)
 BASE_FRAMES = {1: 120, 2: 500, 3: 500, 4: 240}
 
 
+_last_note = [time.perf_counter()]
+
+
+def progress(msg, every=20.0):
+    """A line on stderr at most every `every` seconds (long configurations,
+    e.g. C3 at ~11 s per solve, would otherwise run silent for minutes)."""
+    now = time.perf_counter()
+    if now - _last_note[0] >= every:
+        _last_note[0] = now
+        print("[bench] %s" % msg, file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -364,6 +376,7 @@ def main():
     prob = S.make_config(args.config, frames=frames, scale=scale, **kw)
     opt = S.config_options(prob)
     gen_s = time.perf_counter() - t0
+    progress("scene built (%.1f s)" % gen_s, every=0.0)
     # MMBA_BENCH_DEVICE: every rank on one device (RCCL path rehearsal on a
     # one-GPU box; the driver's multi-GPU runs leave it unset)
     ctx = Context(int(os.environ.get("MMBA_BENCH_DEVICE", local)))
@@ -374,6 +387,7 @@ def main():
     t0 = time.perf_counter()
     solver = Solver(prob, opt, context=ctx, comm=comm)
     upload_s = time.perf_counter() - t0
+    progress("plan built (%.1f s)" % upload_s, every=0.0)
 
     # the caller's output buffers (errorList, ud->errorList,
     # errorDistanceList) are allocated once, in page-locked host memory
@@ -381,8 +395,9 @@ def main():
     from mayamatchmovesolver_amd.solver import host_array
     outs = (host_array(prob.num_residuals), host_array(prob.num_residuals),
             host_array(prob.num_obs))
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         solver.solve(out=outs)
+        progress("warmup %d/%d" % (w + 1, args.warmup))
 
     # value: inputs resident in HBM before the timed region; every solve hands
     # errorList / ud->errorList / errorDistanceList (plus x, the result
@@ -394,8 +409,9 @@ def main():
     t0 = time.perf_counter()
     iters = nfev = njev = 0
     last = None
-    for _ in range(args.steps):
+    for st in range(args.steps):
         last = solver.solve(out=outs)
+        progress("step %d/%d" % (st + 1, args.steps))
         iters += last.result["outer_iterations"]
         nfev += last.result["function_evals"]
         njev += last.result["outer_iterations"]
@@ -409,8 +425,9 @@ def main():
     barrier(dist)
     ctx.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for st in range(args.steps):
         solver.solve(fetch=False)
+        progress("device-resident step %d/%d" % (st + 1, args.steps))
     ctx.synchronize()
     barrier(dist)
     dt_dev = allreduce(dist, time.perf_counter() - t0, "max")

@@ -134,6 +134,7 @@ int mmba_context_create(int device, mmba_context **out) {
         c->device = device;
         MMBA_HIP(hipSetDevice(device));
         MMBA_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        pcr_note_context(device, +1);
         *out = c;
         return MMBA_OK;
     })
@@ -164,6 +165,7 @@ int mmba_context_synchronize(mmba_context *ctx) {
 void mmba_context_destroy(mmba_context *ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    pcr_note_context(ctx->device, -1);
     delete ctx;
 }
 

@@ -300,6 +300,9 @@ void pcr_rhs_dot(hipStream_t s, const PcrDev &P, const double *w, const int *mas
 // factors of the last pcr_solve on P (mmba_pcr.hip)
 void pcr_rhs_mc(hipStream_t s, const PcrDev &P, const double *R, int ldr, int nc, double *Z,
                 int ldz, int *fail);
+// contexts open on a device (mmba_context_create / _destroy): PCR launches
+// are ordered across streams while there is more than one
+void pcr_note_context(int dev, int delta);
 int pcr_max_resident(int K);
 // Block-diagonal + arrow solver (mmba_bdiag.hip): factor S, y = L^-1 r and,
 // with x, the solution (scattered to parameter order into xs when non-null).

@@ -520,17 +520,35 @@ static unsigned pcr_next_epoch() {
 // plans fall back).  So the PCR launches of one process on one device are
 // ordered across streams: every launch waits, device-side, for the previous
 // PCR launch when that one was issued on another stream (an event recorded
-// after each launch).  Plans of one stream are ordered by the stream already;
-// other processes sharing the device are not covered (their launches time out
-// and fall back to block cyclic reduction).
+// after each launch).  Plans of one stream are ordered by the stream already,
+// and an event record costs several microseconds of stream time, so events
+// are used only while more than one context (stream) is open on the device;
+// the context that makes it two drains the device first, so every launch
+// before the switch has finished.  Other processes sharing the device are
+// not covered (their launches time out and fall back to block cyclic
+// reduction).
 namespace {
 struct PcrOrder {
     std::mutex mu;
     hipStream_t last = nullptr;
     hipEvent_t ev = nullptr;
+    bool recorded = false;  // ev marks `last`'s latest PCR launch
+    int contexts = 0;
 };
 PcrOrder g_pcr_order[64];
 }  // namespace
+
+void pcr_note_context(int dev, int delta) {
+    PcrOrder &o = g_pcr_order[dev & 63];
+    std::lock_guard<std::mutex> g(o.mu);
+    const int before = o.contexts;
+    o.contexts += delta;
+    if (delta > 0 && before == 1) {
+        // one -> two streams: drain what the first one launched unordered
+        (void)hipDeviceSynchronize();
+        o.recorded = false;
+    }
+}
 
 template <class Launch>
 static void pcr_ordered(hipStream_t s, Launch &&launch) {
@@ -538,11 +556,18 @@ static void pcr_ordered(hipStream_t s, Launch &&launch) {
     hipGetDevice(&dev);
     PcrOrder &o = g_pcr_order[dev & 63];
     std::lock_guard<std::mutex> g(o.mu);
+    if (o.contexts <= 1) {
+        launch();
+        o.last = s;
+        o.recorded = false;
+        return;
+    }
     if (!o.ev) hipEventCreateWithFlags(&o.ev, hipEventDisableTiming);
-    if (o.last && o.last != s) hipStreamWaitEvent(s, o.ev, 0);
+    if (o.recorded && o.last != s) hipStreamWaitEvent(s, o.ev, 0);
     launch();
     hipEventRecord(o.ev, s);
     o.last = s;
+    o.recorded = true;
 }
 
 void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, double *xs, int *fail) {

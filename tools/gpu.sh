@@ -39,7 +39,9 @@ for step in "$@"; do
       cat "$OUT/bench.json" ;;
     benchcfg:*)
       c=${step#benchcfg:}
-      timeout -k 10 400 python -u bench.py --config "$c" --steps 8 --warmup 3 --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
+      st=8; wu=3
+      if [ "$c" = 2 ]; then st=3; wu=1; fi  # C3: ~11 s per solve
+      timeout -k 10 600 python -u bench.py --config "$c" --steps $st --warmup $wu --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
       cat "$OUT/bench_$c.json" ;;
     benchpath:*)
       pv=${step#benchpath:}
