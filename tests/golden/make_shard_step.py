@@ -6,7 +6,7 @@ unsharded GPU solve.  Run from the repo root:
 
     python tests/golden/make_shard_step.py
 
-Writes tests/golden/full/c4_shard_step.npz: for n in (4, 8), x_n (the
+Writes tests/golden/shard/c4_shard_step.npz: for n in (4, 8), x_n (the
 oracle's x), trace_n, and cond_n (the condition number of J^T J at x0, which
 bounds how closely any fp64 solve pins the step: about cond * 1e-16)."""
 import os
@@ -32,7 +32,7 @@ def main():
         out["trace_%d" % n] = tr
         out["cond_%d" % n] = np.float64(w[-1] / w[0])
         print(n, rr.reason_number, rr.iterations, "cond %.3e" % out["cond_%d" % n], flush=True)
-    path = os.path.join(ROOT, "tests", "golden", "full", "c4_shard_step.npz")
+    path = os.path.join(ROOT, "tests", "golden", "shard", "c4_shard_step.npz")
     np.savez_compressed(path, **out)
     print("wrote", path)
 

@@ -62,7 +62,7 @@ def run_sharded(prob, opt, n, replicated=None, band_solver=None):
 # to 5e-7 on the first case, so the sharded run is compared at the same 1e-6.
 WC = dict(window=6, depth=(4.0, 10.0))
 # oracle x after the first step of the valley test's C4 scenes at 4 / 8 shards
-SHARD_STEP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full",
+SHARD_STEP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shard",
                           "c4_shard_step.npz")
 CASES = [
     (3, dict(frames=40, scale=0.004, **WC), 2),   # bundle-Schur BA, 2 shards
