@@ -221,17 +221,6 @@ void DenseSolver::setup(Plan &pl, int n) {
     A = pl.dalloc<double>((size_t)ld * (n + 1));  // column n: the unused A[n][n]
     Linv = pl.dalloc<double>((size_t)n * 64);
     ws = pl.dalloc<double>((size_t)(n + 64) * 64);
-    MMBA_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    MMBA_HIP(hipEventCreateWithFlags(&ev_upd, hipEventDisableTiming));
-    MMBA_HIP(hipEventCreateWithFlags(&ev_blk, hipEventDisableTiming));
-}
-
-void DenseSolver::release() {
-    if (ev_upd) (void)hipEventDestroy(ev_upd);
-    if (ev_blk) (void)hipEventDestroy(ev_blk);
-    if (side) (void)hipStreamDestroy(side);
-    ev_upd = ev_blk = nullptr;
-    side = nullptr;
 }
 
 void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int *fail) {
@@ -242,43 +231,21 @@ void DenseSolver::factor_forward(hipStream_t s, const double *r, double *y, int 
     // against 251.6 ms at 256 -- half as many read-modify-write passes over
     // the trailing matrix
     constexpr int NB = 512;
-    // Look-ahead (right-looking with a depth-1 look-ahead): after block k is
-    // factored, its update of block k+1's columns runs first; block k+1's
-    // panels (a chain of small, latency-bound launches) are then factored on
-    // the side stream while the trailing update of the columns after it --
-    // the big SYRK, disjoint from block k+1's columns -- runs on s.  Same
-    // operations on the same operands as without look-ahead: the trailing
-    // update of block k+1's columns and of the rest is the same SYRK split
-    // at a column boundary (k_dgemm_nt sums each entry over k in the same
-    // order), so the bits do not change.
-    block(s, A, ld, 0, std::min(NB, n), end, fail);
     for (int k0 = 0; k0 < n; k0 += NB) {
         const int nb = std::min(NB, n - k0);
+        block(s, A, ld, k0, nb, end, fail);
+        const int m = end - (k0 + nb);
         if (k0 + nb >= n) break;
-        const int m = end - (k0 + nb);          // rows (and columns) after block k
-        const int nb1 = std::min(NB, n - (k0 + nb));  // block k+1's width
+        // trailing update with the whole block, rhs row included (it also
+        // updates the unused A[n][n])
         double *L21 = A + (size_t)k0 * ld + k0 + nb;
         double *S22 = A + (size_t)(k0 + nb) * ld + (k0 + nb);
-        // block k+1's columns: its diagonal tile (SYRK) and the rows below
-        launch_dgemm_nt(s, true, nb1, nb1, nb, L21, ld, L21, ld, S22, ld, -1., 1.);
-        if (m > nb1)
-            launch_dgemm_nt(s, false, m - nb1, nb1, nb, L21 + nb1, ld, L21, ld, S22 + nb1, ld, -1.,
-                            1.);
-        MMBA_HIP(hipEventRecord(ev_upd, s));
-        MMBA_HIP(hipStreamWaitEvent(side, ev_upd, 0));
-        block(side, A, ld, k0 + nb, nb1, end, fail);
-        MMBA_HIP(hipEventRecord(ev_blk, side));
-        // the rest of the trailing matrix (rhs row included)
-        if (m > nb1) {
-            double *L21r = L21 + nb1;
-            double *S33 = S22 + (size_t)nb1 * ld + nb1;
-            launch_dgemm_nt(s, true, m - nb1, m - nb1, nb, L21r, ld, L21r, ld, S33, ld, -1., 1.);
-        }
-        MMBA_HIP(hipStreamWaitEvent(s, ev_blk, 0));
+        launch_dgemm_nt(s, true, m, m, nb, L21, ld, L21, ld, S22, ld, -1., 1.);
     }
     k_dense_row_get<<<(n + 255) / 256, 256, 0, s>>>(A, ld, n, y);
 }
 
+// y = L^-1 r: per 64-row block, y_k = Linv_kk t_k, then t_(k+1..) -= L_(k+1..),k y_k.
 void DenseSolver::forward(hipStream_t s, const double *r, double *y) {
     double *t = ws;
     MMBA_HIP(hipMemcpyAsync(t, r, sizeof(double) * n, hipMemcpyDeviceToDevice, s));

@@ -76,7 +76,6 @@ Plan::~Plan() {
                          "update %lld tail %lld (nb=%d w=%d nG=%d P=%d)\n",
                          h[0], h[1], h[2], h[3], nR - nG, bw, nG, bs.P);
     }
-    ds.release();
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (ev_sync) (void)hipEventDestroy(ev_sync);
     for (void *p : allocs) (void)hipFree(p);

@@ -55,12 +55,7 @@ struct Plan;
 struct DenseSolver {
     int n = 0, ld = 0;       // columns (nRpad), leading dimension (n + 64)
     double *A = nullptr, *Linv = nullptr, *ws = nullptr;
-    // look-ahead: the next block's panels are factored on `side` while the
-    // trailing update of the rest runs on the plan's stream
-    hipStream_t side = nullptr;
-    hipEvent_t ev_upd = nullptr, ev_blk = nullptr;
     void setup(Plan &pl, int n);
-    void release();
     void init(hipStream_t s);
     void block(hipStream_t s, double *A, int ld, int k0, int nb, int end, int *fail);
     void factor_forward(hipStream_t s, const double *r, double *y, int *fail);
