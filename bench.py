@@ -455,18 +455,24 @@ def main():
                     "avg_ms": jac_ms, "bytes_per_launch": jac_bytes,
                     "launches": stats["jac_launches"], "traffic_pmc": traffic_detail}
         kind = stats.get("reduced_kind", 0)
+        band_names = {1: "band: partitioned Cholesky chains", 2: "band: block cyclic reduction",
+                      3: "band: parallel cyclic reduction (k_pcr_solve, one launch, x out)",
+                      4: "band: separator form (shard interiors by parallel cyclic reduction)",
+                      5: "block diagonal + arrow (per camera-frame Cholesky)"}
         chol = {"avg_ms": stats["chol_ms_avg"], "launches": stats["chol_launches"],
                 "reduced_dim": stats["reduced_dim"],
-                "solver": ["band (block cyclic reduction)", "tiled sparse Cholesky",
-                           "dense blocked Cholesky (MFMA GEMM trailing updates)",
-                           "block diagonal + arrow (per camera-frame Cholesky)"][kind],
-                "note": "time per factorisation (+ fused forward solve), HIP events"}
+                "solver": band_names.get(stats.get("band_solver", 0), "band") if kind in (0, 3)
+                else ["", "tiled sparse Cholesky",
+                      "dense blocked Cholesky (MFMA GEMM trailing updates)"][kind],
+                "note": "time per damped solve's factorisation (+ fused solve), HIP events"}
         if kind in (0, 3) and stats["chol_ms_avg"] > 0:
             # latency-bound (a dependent pivot chain per elimination level):
             # the fp64 MFMA fraction is reported as measured, not as a target
             tf = stats["chol_flops"] / (stats["chol_ms_avg"] * 1e-3) / 1e12
-            chol.update({"bound": "latency (dependent 24-step pivot chains, one per level)"
+            chol.update({"bound": "latency (a dependent 24-step pivot chain and a neighbour "
+                                  "hand-off per level)"
                          if kind == 0 else "latency (one wave per camera-frame block)",
+                         "dominant": stats["chol_ms_avg"] > jac_ms,
                          "achieved_tflops": tf, "peak_tflops": FP64_MFMA_PEAK_TF,
                          "frac": tf / FP64_MFMA_PEAK_TF, "flops": stats["chol_flops"]})
         if kind == 2 and stats["chol_ms_avg"] > 0:

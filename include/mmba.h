@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 7
+#define MMBA_ABI_VERSION 8
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -270,6 +270,22 @@ typedef struct mmba_problem {
     const int32_t *param_ref_attr;  /* [num_params] */
     int32_t num_ref_attrs;
     const int32_t *ref_attr_lens;   /* [num_ref_attrs] */
+
+    /* ---- ABI 8 ---- */
+    /* MM Scene Graph point indexing.  FlatScene emits its
+     * point and marker lists camera -> marker -> frame (flat.rs:271-356: the
+     * markers of camera 0 in marker order, then camera 1's ...), but
+     * measureErrors_mmSceneGraph reads both at markerIndex * F + frameIndex
+     * (adjust_measureErrors.cpp:454-459).  So with markers not grouped by
+     * ascending camera, observation (marker i, frame f) compares the point
+     * and marker position of flat marker k = (i-th marker in camera order) --
+     * its camera, bundle, film fit and x,y at frame f -- while its weight,
+     * frame enable and lens (B3) stay those of marker i.  mkr_frame_xy gives
+     * every marker's x,y at every frame, as obs_xy (the flat marker list
+     * before film fit); NULL: a remapped observation takes the x,y of the
+     * observation (k, f), and MMBA_ERR_UNSUPPORTED when marker k has none at
+     * frame f.  Unused in Maya-DAG mode and when markers are grouped. */
+    const double *mkr_frame_xy; /* [2*num_markers*num_frames] */
 } mmba_problem;
 
 /* SolverOptions subset that the LM path reads (adjust_data.h:133-185). */

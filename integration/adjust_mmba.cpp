@@ -224,6 +224,19 @@ bool inputs_of(SolverData &ud, const std::vector<double> &weights, SolverInputs 
     in.paramToAttrList = ud.paramToAttrList;
     in.errorToMarkerList = ud.errorToMarkerList;
     for (const MPoint &p : ud.markerPosList) in.markerPosList.push_back({p.x, p.y});
+    // MM Scene Graph with markers not grouped by camera: the flat
+    // marker list the reference reads holds every marker at every frame
+    bool grouped = true;
+    for (size_t k = 1; k < in.markers.size(); ++k)
+        grouped = grouped && in.markers[k].first >= in.markers[k - 1].first;
+    if (!grouped && ud.solverOptions->sceneGraphMode == SceneGraphMode::kMMSceneGraph) {
+        for (MarkerPtr &mkr : ud.markerList)
+            for (uint32_t f = 0; f < ud.frameList.length(); ++f) {
+                double px = 0.0, py = 0.0;
+                mkr->getPosXY(px, py, ud.frameList[f], ud.solverOptions->timeEvalMode, true);
+                in.markerFramePos.push_back({px, py});
+            }
+    }
     in.markerWeightList = ud.markerWeightList;
     in.paramWeightList = weights;
     auto rows = [&](auto &list, int count, std::vector<AttrRowDesc> &out) {

@@ -274,6 +274,16 @@ bool FlatScene::build(const SolverInputs &in, SceneReader &rd) {
         obs_xy.push_back(in.markerPosList[k][1]);
         obs_weight.push_back(in.markerWeightList[k]);
     }
+    if (!in.markerFramePos.empty()) {
+        if (in.markerFramePos.size() != in.markers.size() * static_cast<size_t>(num_frames)) {
+            why = "markerFramePos size";
+            return false;
+        }
+        for (const auto &xy : in.markerFramePos) {
+            mkr_frame_xy.push_back(xy[0]);
+            mkr_frame_xy.push_back(xy[1]);
+        }
+    }
 
     // ---- parameters: paramToAttrList ----
     for (size_t p = 0; p < in.paramToAttrList.size(); ++p) {
@@ -398,6 +408,7 @@ mmba_problem FlatScene::problem() const {
     p.smooth_variance = smooth_variance.data();
     p.smooth_value = smooth_value.data();
     p.cam_rs_value = cam_rs.empty() ? nullptr : cam_rs.data();
+    p.mkr_frame_xy = mkr_frame_xy.empty() ? nullptr : mkr_frame_xy.data();
     return p;
 }
 
@@ -429,6 +440,7 @@ std::vector<uint8_t> FlatScene::plan_key(const mmba_options &o) const {
     put(k, obs_frame);
     put(k, obs_xy);
     put(k, obs_weight);
+    put(k, mkr_frame_xy);
     put(k, param_attr);
     put(k, param_frame);
     put(k, param_ref_attr);

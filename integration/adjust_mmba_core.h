@@ -104,6 +104,10 @@ struct SolverInputs {
     std::vector<double> paramWeightList;       // diag of mode 2 (empty = 1.0)
     std::vector<AttrRowDesc> stiff, smooth;
     std::vector<double> rolling_shutter;       // per camera, frames (ABI 3; empty = none)
+    // ABI 8: every marker's x,y at every frame, marker-major
+    // [markers * num_frames], overscan applied like markerPosList -- what
+    // FlatScene's marker list holds; empty = taken from the observations
+    std::vector<std::array<double, 2>> markerFramePos;
 };
 
 // ---------------------------------------------------------------------------
@@ -124,6 +128,7 @@ struct FlatScene {
     std::vector<int32_t> bnd_tfm, mkr_cam, mkr_bnd;
     std::vector<int32_t> obs_marker, obs_frame;
     std::vector<double> obs_xy, obs_weight;
+    std::vector<double> mkr_frame_xy;  // ABI 8 (empty: NULL)
     std::vector<int32_t> param_attr, param_frame;
     // ABI 7: paramToAttrList[p].first and the lens of each
     // attrList entry (-1: not an attribute of a lens the cameras use)

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # mmba_debug_set_path keys (test hook: pin a plan-builder choice)
 PATH_PCR = 1
@@ -125,6 +125,8 @@ class MmbaProblem(C.Structure):
         ("param_ref_attr", _i32p),
         ("num_ref_attrs", C.c_int32),
         ("ref_attr_lens", _i32p),
+        # ABI 8: MMSG flat marker positions (Appendix B4)
+        ("mkr_frame_xy", _f64p),
     ]
 
 

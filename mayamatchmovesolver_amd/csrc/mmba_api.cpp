@@ -385,7 +385,15 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         out->jac_bytes = bj * p.M;
         out->resid_bytes = 48.0 * p.M;
         // reduced-system flops per factorisation as each solver performs them
-        if (p.band && p.bs.use_bcr) {
+        if (p.band && p.bs.use_pcr && !p.bs.df_off) {
+            // parallel cyclic reduction: per block and level the factor of D
+            // (K^3/3), the right-hand sides of the three pivot chains (C^-1
+            // with r, P, Q: K^2 (3K + 1)), the products X1, X2 (2 K^2 (K + 1)
+            // each) and X3 (2 K^3), the update (4 K^2); x = C^-T rho at the end
+            const double K = p.bs.pcr.K;
+            out->chol_flops = (double)p.bs.pcr.nblk *
+                              (p.bs.pcr.nlev * (28.0 / 3.0 * K * K * K + 9.0 * K * K) + 2.0 * K * K);
+        } else if (p.band && p.bs.use_bcr) {
             // block cyclic reduction: per eliminated K x K block its Cholesky
             // (K^3/3), U / V / Y / y solves (2K^3 + nG K^2 + K^2), the two
             // symmetric Schur updates (2 x K^3), the coupling (2K^3), the arrow

@@ -553,7 +553,7 @@ void pcr_note_context(int dev, int delta) {
 template <class Launch>
 static void pcr_ordered(hipStream_t s, Launch &&launch) {
     int dev = 0;
-    hipGetDevice(&dev);
+    MMBA_HIP(hipGetDevice(&dev));
     PcrOrder &o = g_pcr_order[dev & 63];
     std::lock_guard<std::mutex> g(o.mu);
     if (o.contexts <= 1) {
@@ -562,10 +562,10 @@ static void pcr_ordered(hipStream_t s, Launch &&launch) {
         o.recorded = false;
         return;
     }
-    if (!o.ev) hipEventCreateWithFlags(&o.ev, hipEventDisableTiming);
-    if (o.recorded && o.last != s) hipStreamWaitEvent(s, o.ev, 0);
+    if (!o.ev) MMBA_HIP(hipEventCreateWithFlags(&o.ev, hipEventDisableTiming));
+    if (o.recorded && o.last != s) MMBA_HIP(hipStreamWaitEvent(s, o.ev, 0));
     launch();
-    hipEventRecord(o.ev, s);
+    MMBA_HIP(hipEventRecord(o.ev, s));
     o.last = s;
     o.recorded = true;
 }

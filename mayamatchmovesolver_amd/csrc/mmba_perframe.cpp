@@ -159,7 +159,7 @@ struct LensPlain {
 // and parameter lists, which are filtered (order kept: observations stay
 // marker-major, parameters attr-major).
 struct FrameProblem {
-    std::vector<int32_t> obs_marker, obs_frame, param_attr, param_frame;
+    std::vector<int32_t> obs_marker, obs_frame, param_attr, param_frame, param_ref;
     std::vector<double> obs_xy, obs_weight, pmin, pmax, poff, pscale;
     std::vector<int> params;  // indices into the full parameter vector
     mmba_problem p{};
@@ -179,6 +179,7 @@ struct FrameProblem {
             params.push_back(j);
             param_attr.push_back(full.param_attr[j]);
             param_frame.push_back(full.param_frame[j]);
+            if (full.param_ref_attr) param_ref.push_back(full.param_ref_attr[j]);
             pmin.push_back(full.param_min[j]);
             pmax.push_back(full.param_max[j]);
             poff.push_back(full.param_offset[j]);
@@ -192,6 +193,7 @@ struct FrameProblem {
         p.num_params = (int32_t)params.size();
         p.param_attr = param_attr.data();
         p.param_frame = param_frame.data();
+        if (full.param_ref_attr) p.param_ref_attr = param_ref.data();
         p.param_min = pmin.data();
         p.param_max = pmax.data();
         p.param_offset = poff.data();

@@ -306,14 +306,51 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         require(pr->mkr_cam[k] >= 0 && pr->mkr_cam[k] < nC, "mkr_cam");
         require(pr->mkr_bnd[k] >= 0 && pr->mkr_bnd[k] < nB, "mkr_bnd");
     }
-    if (opt.scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH)
-        for (int k = 1; k < nK; ++k)
-            if (pr->mkr_cam[k] < pr->mkr_cam[k - 1])
-                throw Unsupported{"MMSG needs markers grouped by ascending camera (B4)"};
     for (int i = 0; i < M; ++i) {
         require(pr->obs_marker[i] >= 0 && pr->obs_marker[i] < nK, "obs_marker");
         require(pr->obs_frame[i] >= 0 && pr->obs_frame[i] < F, "obs_frame");
         require(pr->obs_weight[i] > 0.0, "obs_weight must be > 0");
+    }
+    // B4 (mmba.h ABI 8): in MMSG mode observation (marker i, frame f) reads the
+    // flat lists at i * F + f, which hold the i-th marker in camera order
+    // (flat.rs:271-356, adjust_measureErrors.cpp:454-459).  obs_geo = the
+    // marker whose camera, bundle and x,y the observation compares; its weight
+    // and lens instance (B3, from obs_marker) are its own.
+    std::vector<int> obs_geo(pr->obs_marker, pr->obs_marker + M);
+    std::vector<double> obs_xy_geo;  // empty: obs_xy
+    if (opt.scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
+        std::vector<int> flat;
+        flat.reserve(nK);
+        for (int c = 0; c < nC; ++c)
+            for (int k = 0; k < nK; ++k)
+                if (pr->mkr_cam[k] == c) flat.push_back(k);
+        bool moved = false;
+        for (int k = 0; k < nK; ++k) moved |= flat[k] != k;
+        if (moved) {
+            if (rs_on) throw Unsupported{"rolling shutter with MMSG markers not grouped by camera (B4)"};
+            std::map<std::pair<int, int>, int> obs_at;
+            if (!pr->mkr_frame_xy)
+                for (int i = 0; i < M; ++i) obs_at[{pr->obs_marker[i], pr->obs_frame[i]}] = i;
+            obs_xy_geo.assign(pr->obs_xy, pr->obs_xy + 2 * (size_t)M);
+            for (int i = 0; i < M; ++i) {
+                const int k = flat[pr->obs_marker[i]], f = pr->obs_frame[i];
+                obs_geo[i] = k;
+                if (k == pr->obs_marker[i]) continue;
+                const double *xy;
+                if (pr->mkr_frame_xy) {
+                    xy = &pr->mkr_frame_xy[2 * ((size_t)k * F + f)];
+                } else {
+                    auto it = obs_at.find({k, f});
+                    if (it == obs_at.end())
+                        throw Unsupported{"MMSG markers not grouped by camera (B4): a flat marker "
+                                          "without an observation at the frame read, and no "
+                                          "mkr_frame_xy"};
+                    xy = &pr->obs_xy[2 * (size_t)it->second];
+                }
+                obs_xy_geo[2 * i] = xy[0];
+                obs_xy_geo[2 * i + 1] = xy[1];
+            }
+        }
     }
     for (int p = 0; p < n; ++p) {
         const int a = pr->param_attr[p];
@@ -452,7 +489,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     // over a window of frames then couples a contiguous band of the reduced
     // system, for any number of cameras ----
     std::vector<int> obs_cam(M);
-    for (int i = 0; i < M; ++i) obs_cam[i] = pr->mkr_cam[pr->obs_marker[i]];
+    for (int i = 0; i < M; ++i) obs_cam[i] = pr->mkr_cam[obs_geo[i]];
     std::map<std::pair<int, int>, int> cf_id;
     for (int i = 0; i < M; ++i) cf_id[{pr->obs_frame[i], obs_cam[i]}] = 0;
 
@@ -607,7 +644,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     std::vector<int> obs_cf(Mg);
     for (int i = 0; i < Mg; ++i) obs_cf[i] = cf_id[{pr->obs_frame[i], obs_cam[i]}];
     std::vector<int> obs_bnd_g(Mg);
-    for (int i = 0; i < Mg; ++i) obs_bnd_g[i] = pr->mkr_bnd[pr->obs_marker[i]];
+    for (int i = 0; i < Mg; ++i) obs_bnd_g[i] = pr->mkr_bnd[obs_geo[i]];
     // rolling shutter: the camera-frames of the same camera at f - 1 / f + 1
     // (cameras with rs != 0), whose translate / rotate values the blend reads
     std::vector<int> cf_nb(2 * (size_t)std::max(ncf, 1), -1);
@@ -716,11 +753,12 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     for (int i = 0; i < M; ++i) {
         const int r = ref_of_dev[i];
         d_cf[i] = obs_cf[r];
-        d_bnd[i] = pr->mkr_bnd[pr->obs_marker[r]];
+        d_bnd[i] = obs_bnd_g[r];
         d_frame[i] = pr->obs_frame[r];
         d_cam[i] = obs_cam[r];
-        d_xy[2 * i] = pr->obs_xy[2 * r];
-        d_xy[2 * i + 1] = pr->obs_xy[2 * r + 1];
+        const double *xy = obs_xy_geo.empty() ? pr->obs_xy : obs_xy_geo.data();
+        d_xy[2 * i] = xy[2 * r];
+        d_xy[2 * i + 1] = xy[2 * r + 1];
         d_sqrtw[i] = std::sqrt(pr->obs_weight[r]);
         d_own[i] = obs_own_g[r];
         d_inst[i] = obs_inst_g[r];

@@ -142,6 +142,10 @@ class Problem:
     # of each attrList entry (-1 not a lens attribute); None = derived
     param_ref_attr: Optional[np.ndarray] = None
     ref_attr_lens: Optional[np.ndarray] = None
+    # ABI 8: every marker's x,y at every frame, [num_markers, num_frames, 2]
+    # flattened (the MMSG flat marker list, Appendix B4; None = taken from the
+    # observations)
+    mkr_frame_xy: Optional[np.ndarray] = None
 
     def __post_init__(self):
         for name in _FIELDS_I32:
@@ -173,6 +177,9 @@ class Problem:
             if getattr(self, name) is not None:
                 setattr(self, name, np.ascontiguousarray(getattr(self, name),
                                                          dtype=np.int32).reshape(-1))
+        if self.mkr_frame_xy is not None:
+            self.mkr_frame_xy = np.ascontiguousarray(self.mkr_frame_xy,
+                                                     dtype=np.float64).reshape(-1)
 
     # sizes -------------------------------------------------------------
     @property
@@ -279,6 +286,8 @@ class Problem:
         p.num_ref_attrs = int(self.ref_attr_lens.size) if self.ref_attr_lens is not None else 0
         p.ref_attr_lens = (ptr(self.ref_attr_lens, C.c_int32) if self.ref_attr_lens is not None
                            else C.cast(None, C.POINTER(C.c_int32)))
+        p.mkr_frame_xy = (ptr(self.mkr_frame_xy, C.c_double) if self.mkr_frame_xy is not None
+                          else C.cast(None, C.POINTER(C.c_double)))
         return p, [self]
 
     # (de)serialisation ---------------------------------------------------
@@ -292,7 +301,8 @@ class Problem:
             d["param_weight"] = self.param_weight
         if self.cam_rs_value is not None:
             d["cam_rs_value"] = self.cam_rs_value
-        for name in ("lens_input", "lens_input_values", "param_ref_attr", "ref_attr_lens"):
+        for name in ("lens_input", "lens_input_values", "param_ref_attr", "ref_attr_lens",
+                     "mkr_frame_xy"):
             if getattr(self, name) is not None:
                 d[name] = getattr(self, name)
         return d
@@ -308,7 +318,8 @@ class Problem:
             kw["lens_attrs"] = la
         for name in _FIELDS_OPT_I32 + _FIELDS_OPT_F64 + ["param_weight", "cam_rs_value",
                                                           "lens_input", "lens_input_values",
-                                                          "param_ref_attr", "ref_attr_lens"]:
+                                                          "param_ref_attr", "ref_attr_lens",
+                                                          "mkr_frame_xy"]:
             if name in d:
                 kw[name] = np.asarray(d[name])
         return cls(num_frames=int(d["num_frames"]), **kw)

@@ -981,6 +981,92 @@ def b3_scene(variant="lens_first", frames=5, markers_per_cam=4, seed=23) -> Prob
     return b.build(meta={"name": "b3_" + variant})
 
 
+def b4_scene(frames=4, bundles=6, partial=False, frame_xy=False, seed=29) -> Problem:
+    """Two cameras seeing every bundle, the markers listed bundle by bundle
+    (camera 1's, then camera 0's): not grouped by camera, so in MM Scene
+    Graph mode observation (marker i, frame f) reads the flat point and marker
+    lists at i * F + f, which hold the i-th marker in camera order (SURVEY
+    Appendix B4, mmba.h ABI 8).  Camera 0 moves along x with its rotation
+    solved per frame, camera 1 is static with its rotation solved (three
+    globals), the bundles' translates are solved.  Marker weights differ per
+    marker.  ``partial``: some markers disabled on some frames, so a remapped
+    observation can read a flat marker with no observation there;
+    ``frame_xy``: mkr_frame_xy filled with every marker's x,y at every frame."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    F, B = frames, bundles
+    b = SceneBuilder(F)
+    fr = np.arange(F, dtype=np.float64)
+    render = (1500, 1000)
+    depth = rng.uniform(10.0, 25.0, size=B)
+    P = np.stack([rng.uniform(-0.25, 0.25, B) * depth, rng.uniform(-0.2, 0.2, B) * depth,
+                  -depth], axis=1)
+    t0 = np.stack([0.3 * fr, 0.1 + 0.0 * fr, 0.0 * fr], 1)
+    r0 = np.stack([1.0 + 0.2 * fr, -1.5 + 0.1 * fr, 0.5 + 0.0 * fr], 1)
+    tfm0, tids0 = b.transform(t=[t0[:, 0], t0[:, 1], t0[:, 2]],
+                              r=[r0[:, 0] + rng.uniform(-0.5, 0.5, F),
+                                 r0[:, 1] + rng.uniform(-0.5, 0.5, F),
+                                 r0[:, 2] + rng.uniform(-0.5, 0.5, F)])
+    t1, r1 = np.array([1.0, 0.2, 0.5]), np.array([0.5, 2.0, -0.3])
+    tfm1, tids1 = b.transform(t=tuple(t1), r=tuple(r1 + rng.uniform(-0.8, 0.8, 3)))
+    cam0, _ = b.camera(tfm0, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN), render_size=render)
+    cam1, _ = b.camera(tfm1, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN), render_size=render)
+    P0 = P * (1.0 + rng.uniform(-0.03, 0.03, size=(B, 1)))
+    bids = []
+    for j in range(B):
+        bt, ids = b.transform(t=tuple(P0[j]))
+        b.bundle(bt)
+        bids.append(ids)
+    all_xy = []
+    for j in range(B):
+        for c, cam in ((1, cam1), (0, cam0)):
+            xy = np.empty((F, 2))
+            for f in range(F):
+                t, r = (t0[f], r0[f]) if c == 0 else (t1, r1)
+                mx, my, _ = _project(t, r, FOCAL_MM, P[j])
+                xy[f] = (float(_noisy(rng, np.asarray(mx))), float(_noisy(rng, np.asarray(my))))
+            en = None
+            if partial and (j + c) % 3 == 1:  # a gap of one frame
+                en = np.ones(F, bool)
+                en[(j + 2 * c) % F] = False
+            b.marker(cam, j, xy, enable=en, weight=1.0 + 0.25 * ((2 * j + c) % 3))
+            all_xy.append(xy)
+    for a in tids0[3:6] + tids1[3:6]:
+        b.solve(a)
+    for j in range(B):
+        for a in bids[j][:3]:
+            b.solve(a)
+    prob = b.build(meta={"name": "b4" + ("_partial" if partial else "")})
+    if frame_xy:
+        prob.mkr_frame_xy = np.ascontiguousarray(np.stack(all_xy), dtype=np.float64).reshape(-1)
+    return prob
+
+
+def b4_grouped_twin(prob: Problem) -> Problem:
+    """The grouped scene a B4 problem is equivalent to in MM Scene Graph mode
+    (tests): the markers renumbered into the flat (camera-major) order and
+    each observation's x,y replaced by that of the flat marker it reads --
+    its own weight, frame and marker number kept."""
+    K, F = prob.num_markers, int(prob.num_frames)
+    flat = np.concatenate([np.flatnonzero(prob.mkr_cam == c) for c in range(prob.num_cameras)])
+    g = flat[prob.obs_marker]
+    if prob.mkr_frame_xy is not None:
+        fxy = prob.mkr_frame_xy.reshape(K, F, 2)
+    else:
+        fxy = np.full((K, F, 2), np.nan)
+        fxy[prob.obs_marker, prob.obs_frame] = prob.obs_xy.reshape(-1, 2)
+    xy = prob.obs_xy.reshape(-1, 2).copy()
+    moved = g != prob.obs_marker
+    xy[moved] = fxy[g[moved], prob.obs_frame[moved]]
+    d = prob.to_npz_dict()
+    d["mkr_cam"] = prob.mkr_cam[flat]
+    d["mkr_bnd"] = prob.mkr_bnd[flat]
+    d["obs_xy"] = xy.reshape(-1)
+    d.pop("mkr_frame_xy", None)
+    twin = Problem.from_npz_dict(d)
+    twin.meta = dict(prob.meta)
+    return twin
+
+
 def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal=3,
                   extra_globals=0, window=None, lens=None, seed=17) -> Problem:
     """Witness-camera rig with a wide arrow of global parameters: a fixed

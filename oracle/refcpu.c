@@ -1046,6 +1046,10 @@ typedef struct {
                      values (before it, every slot is the plug model's value:
                      solveFrames' initial measureErrors, adjust_base.cpp:
                      1002-1004 then 1076-1089) */
+    /* B4 (mmba.h ABI 8): the marker whose flat entry observation i reads in
+     * MMSG mode, and that entry's x,y (before film fit) */
+    int *geo_mkr;      /* [M] */
+    double *geo_xy;    /* [2M] */
 } ref_scene;
 
 /* Test hook standing in for MComputation::isInterruptRequested: the poll
@@ -1450,14 +1454,15 @@ static void measure(ref_scene *s, const char *frame_mask, double *errors) {
         const int k = p->obs_marker[i];
         const int f = p->obs_frame[i];
         if (frame_mask && !frame_mask[f]) continue;
-        const int c = p->mkr_cam[k];
-        double mkr_x = p->obs_xy[2 * i], mkr_y = p->obs_xy[2 * i + 1];
+        const int g = s->geo_mkr[i]; /* B4: the flat entry's marker */
+        const int c = p->mkr_cam[g];
+        double mkr_x = s->geo_xy[2 * i], mkr_y = s->geo_xy[2 * i + 1];
         double point_x, point_y, factor = 1.0;
         double P[16], fa, ra;
         camera_projection(s, c, f, P, &fa, &ra);
         film_fit_marker(p->cam_film_fit[c], fa, ra, &mkr_x, &mkr_y);
         const int ct = p->cam_tfm[c];
-        const int bt = p->bnd_tfm[p->mkr_bnd[k]];
+        const int bt = p->bnd_tfm[p->mkr_bnd[g]];
         const double *cw = &s->tfm_world[((size_t)ct * F + f) * 16];
         const double *bw = &s->tfm_world[((size_t)bt * F + f) * 16];
         double bp[3] = {bw[3], bw[7], bw[11]};
@@ -1665,12 +1670,6 @@ static int scene_jac_dif(void *c, int m, int n, double *x, double *fvec,
 static int validate(const mmba_problem *p, const mmba_options *o) {
     if (!p || !o) return MMBA_ERR_INVALID;
     if (p->num_frames <= 0 || p->num_obs <= 0 || p->num_params <= 0) return MMBA_ERR_INVALID;
-    if (o->scene_graph_mode == MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) {
-        /* B4: MMSG indexes points marker-major; markers must be grouped by
-         * ascending camera for that to be correct. */
-        for (int k = 1; k < p->num_markers; ++k)
-            if (p->mkr_cam[k] < p->mkr_cam[k - 1]) return MMBA_ERR_UNSUPPORTED;
-    }
     for (int i = 0; i < p->num_params; ++i) {
         int a = p->param_attr[i];
         if (a < 0 || a >= p->num_attrs) return MMBA_ERR_INVALID;
@@ -1706,14 +1705,63 @@ static void scene_init(ref_scene *s, const mmba_problem *p,
     for (int c = 0; c < p->num_cameras; ++c) s->rs_any |= rs_on(s, c);
 }
 
-/* scene_init + the B3 lens table (the only part that can refuse) */
+/* B4: FlatScene::evaluate lists markers camera by camera, each camera's in
+ * marker order (flat.rs:271-356), and measureErrors_mmSceneGraph reads the
+ * point and marker lists at markerIndex * F + frameIndex
+ * (adjust_measureErrors.cpp:454-459): observation (marker i, frame f) sees
+ * the i-th marker of that listing at f.  Its x,y there: mkr_frame_xy, else the
+ * observation of that marker at f (none: refused). */
+static int b4_build(ref_scene *s) {
+    const mmba_problem *p = s->p;
+    const int K = p->num_markers, F = p->num_frames, M = p->num_obs;
+    s->geo_mkr = (int *)malloc(sizeof(int) * (size_t)(M > 0 ? M : 1));
+    s->geo_xy = (double *)malloc(sizeof(double) * 2 * (size_t)(M > 0 ? M : 1));
+    for (int i = 0; i < M; ++i) {
+        s->geo_mkr[i] = p->obs_marker[i];
+        s->geo_xy[2 * i] = p->obs_xy[2 * i];
+        s->geo_xy[2 * i + 1] = p->obs_xy[2 * i + 1];
+    }
+    if (s->o->scene_graph_mode != MMBA_SCENE_GRAPH_MM_SCENE_GRAPH) return MMBA_OK;
+    int *flat = (int *)malloc(sizeof(int) * (size_t)(K > 0 ? K : 1));
+    int n = 0, moved = 0;
+    for (int c = 0; c < p->num_cameras; ++c)
+        for (int k = 0; k < K; ++k)
+            if (p->mkr_cam[k] == c) flat[n++] = k;
+    for (int k = 0; k < K; ++k) moved |= flat[k] != k;
+    int rc = MMBA_OK;
+    if (moved && s->rs_any) rc = MMBA_ERR_UNSUPPORTED;
+    for (int i = 0; moved && rc == MMBA_OK && i < M; ++i) {
+        const int k = flat[p->obs_marker[i]], f = p->obs_frame[i];
+        s->geo_mkr[i] = k;
+        if (k == p->obs_marker[i]) continue;
+        const double *xy = NULL;
+        if (p->mkr_frame_xy) {
+            xy = &p->mkr_frame_xy[2 * ((size_t)k * F + f)];
+        } else {
+            for (int j = 0; j < M && !xy; ++j)
+                if (p->obs_marker[j] == k && p->obs_frame[j] == f) xy = &p->obs_xy[2 * j];
+            if (!xy) rc = MMBA_ERR_UNSUPPORTED;
+        }
+        if (xy) {
+            s->geo_xy[2 * i] = xy[0];
+            s->geo_xy[2 * i + 1] = xy[1];
+        }
+    }
+    free(flat);
+    return rc;
+}
+
+/* scene_init + the B3 lens table and the B4 listing (the parts that can refuse) */
 static int scene_open(ref_scene *s, const mmba_problem *p, const mmba_options *o) {
     scene_init(s, p, o);
-    return b3_build(s);
+    const int rc = b3_build(s);
+    return rc != MMBA_OK ? rc : b4_build(s);
 }
 
 static void scene_free(ref_scene *s) {
     free(s->lens_src);
+    free(s->geo_mkr);
+    free(s->geo_xy);
     free(s->attr);
     free(s->tfm_world);
     free(s->pts);
