@@ -7,8 +7,10 @@
 #   bench             the default bench line (C4, CPU baseline, PMC traffic)
 #   benchcfg:I        bench line of configs[I] (no CPU baseline)
 #   benchpath:N=V     default-config bench line with a pinned path (--path N=V)
+#   benchlib:FILE     default-config bench line (C4, 8 steps) through another build of libmmba.so (MMBA_LIB)
 #   prof              rocprofv3 --kernel-trace --stats of the default bench
 #   pmc               FETCH_SIZE / WRITE_SIZE passes of the default bench
+#   sqpmc             one pass of 8 SQ counters (wave cycles, waits, VALU) on the default bench
 #   iter              kernel traces + one-iteration timelines of C2 / C4 / C5
 #   ubench            tools/ubench dgemm_probe (C3 update shapes) and pcr_probe (C4 system)
 set -o pipefail
@@ -47,6 +49,10 @@ for step in "$@"; do
       pv=${step#benchpath:}
       timeout -k 10 400 python -u bench.py --path "$pv" --steps 8 --warmup 3 --no-cpu-baseline --no-traffic > "$OUT/bench_$pv.json" 2> "$OUT/bench_$pv.err" || { tail "$OUT/bench_$pv.err"; exit 1; }
       cat "$OUT/bench_$pv.json" ;;
+    benchlib:*)
+      lib=${step#benchlib:}; tag=$(basename "$lib" .so)
+      MMBA_LIB="$ROOT/$lib" timeout -k 10 400 python -u bench.py --steps 8 --warmup 3 --no-cpu-baseline --no-traffic > "$OUT/bench_$tag.json" 2> "$OUT/bench_$tag.err" || { tail "$OUT/bench_$tag.err"; exit 1; }
+      cat "$OUT/bench_$tag.json" ;;
     prof)
       cd /tmp && cd "$ROOT"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c4 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" || { tail "$OUT/prof_bench.err"; exit 1; }
@@ -55,6 +61,9 @@ for step in "$@"; do
       for ctr in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$OUT/pmc_$ctr" -o c4 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/pmc_$ctr.json" 2> "$OUT/pmc_$ctr.err" || exit 1
       done ;;
+    sqpmc)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/sqpmc" -o c4 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/sqpmc.json" 2> "$OUT/sqpmc.err" || { tail "$OUT/sqpmc.err"; exit 1; }
+      python3 tools/pmc_summary.py "$OUT/sqpmc" > "$OUT/sqpmc_summary.txt" && cat "$OUT/sqpmc_summary.txt" ;;
     ubench)
       timeout -k 10 120 tools/ubench/dgemm_probe > "$OUT/dgemm_probe.txt" 2>&1 || { cat "$OUT/dgemm_probe.txt"; exit 1; }
       timeout -k 10 120 tools/ubench/pcr_probe > "$OUT/pcr_probe.txt" 2>&1 || { cat "$OUT/pcr_probe.txt"; exit 1; }
