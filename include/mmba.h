@@ -216,9 +216,11 @@ typedef struct mmba_problem {
      *   v(f + tau) = v(f) + tau b + tau^2 c,
      * with the exporter's end extrapolation v(-1) = v(0) + (v(0) - v(1)),
      * v(F) = v(F-1) + (v(F-1) - v(F-2)) (:311-314).  The FD column of an
-     * animated parameter then re-measures frames f-1..f+1.  Supported on
-     * camera transforms without a parent, without solved bundles, unsharded
-     * (MMBA_ERR_UNSUPPORTED otherwise). */
+     * animated parameter then re-measures frames f-1..f+1.  A camera under a
+     * parent blends its own translate / rotate values; its world pose is the
+     * parent's world matrix at frame f times the blended local matrix.
+     * Supported without solved bundles, unsharded (MMBA_ERR_UNSUPPORTED
+     * otherwise). */
     const double *cam_rs_value;   /* [num_cameras] */
 
     /* ---- ABI 5 ---- */

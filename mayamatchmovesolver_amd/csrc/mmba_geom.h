@@ -372,7 +372,7 @@ MMBA_DEV void camera_record(const DevProblem &P, int c, int f, const Override &o
 // -1 = default): one dependent load level instead of the attribute-table walk.
 // ov_idx is the perturbed attribute's value index (-1: none).
 MMBA_DEV void camera_record_fast(const DevProblem &P, int cf, long long ov_idx, double ov_val,
-                                 double *rec) {
+                                 double *rec, int ov_attr = -1) {
     const int *ix = &P.cf_aidx[(size_t)CF_AIDX * cf];
     const double dflt[CF_AIDX] = {36.0 / 25.4, 24.0 / 25.4, 0., 0., 35.0, 10000.0, 1.0,
                                   0., 0., 0., 0., 0., 0., 1., 1., 1.};
@@ -386,6 +386,15 @@ MMBA_DEV void camera_record_fast(const DevProblem &P, int cf, long long ov_idx, 
     double W[16];
     trs_matrix(v[7], v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15],
                P.tfm_roo[P.cam_tfm[c]], W);
+    // a parented camera (the table exists for them in rolling-shutter plans):
+    // world = parent world x local, world_matrix's order (ov_attr: the
+    // overridden attribute, for a parent attribute's column)
+    const int pt = P.tfm_parent[P.cam_tfm[c]];
+    if (pt >= 0) {
+        double Wp[16];
+        world_matrix(P, pt, P.cf_frame[cf], Override{ov_attr, ov_val}, Wp);
+        mat4_mul(Wp, W, W);
+    }
     camera_record_tail(P, c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], W, rec);
 }
 
@@ -407,6 +416,7 @@ MMBA_DEV void camera_record_fast(const DevProblem &P, int cf, long long ov_idx, 
 // the oracle to ~1e-15 relative, not bit for bit.
 struct RsCam {
     int c, roo;
+    int ptf, f;             // parent transform (-1: none) and the camera-frame's frame
     int ix[7];              // value indices of the 7 camera attributes (-1: default)
     int tx[6], px[6], nx[6];  // translate / rotate value indices at f, f - 1, f + 1
     double cam[7];          // camera attribute values
@@ -464,6 +474,8 @@ MMBA_DEV void rs_cam_load(const DevProblem &P, int cf, RsCam &R) {
                                   0., 0., 0., 0., 0., 0., 1., 1., 1.};
     R.c = P.cf_cam[cf];
     R.roo = P.tfm_roo[P.cam_tfm[R.c]];
+    R.ptf = P.tfm_parent[P.cam_tfm[R.c]];
+    R.f = P.cf_frame[cf];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
         R.ix[k] = ix[k];
@@ -484,7 +496,7 @@ MMBA_DEV void rs_cam_load(const DevProblem &P, int cf, RsCam &R) {
 }
 
 MMBA_DEV void rs_record(const DevProblem &P, const RsCam &R, double tau, long long ov_idx,
-                        double ov_val, double *rec) {
+                        double ov_val, double *rec, int ov_attr = -1) {
     // projection part: recomputed only when a camera attribute is the override
     double p00 = R.p00, p02 = R.p02, p11 = R.p11, p12 = R.p12, p32 = R.p32, sx = R.sx, sy = R.sy;
     bool cam_ov = false;
@@ -511,13 +523,24 @@ MMBA_DEV void rs_record(const DevProblem &P, const RsCam &R, double tau, long lo
     }
     double W[16];
     trs_matrix(b6[0], b6[1], b6[2], b6[3], b6[4], b6[5], R.s[0], R.s[1], R.s[2], R.roo, W);
-    // C^-1 of W = T R S: rows k = (R S)^-1 = S^-1 R^T, column 3 = -S^-1 R^T t
-    double Ci[12];
+    double Ci[16];
+    if (R.ptf >= 0) {
+        // a parented camera: the blend moves the camera's own translate /
+        // rotate only; world = parent world at the frame (unblended; the
+        // override reaches a parent attribute's column) x blended local, as
+        // oracle/refcpu.c rs_camera_world, and the general inverse
+        double Wp[16];
+        world_matrix(P, R.ptf, R.f, Override{ov_attr, ov_val}, Wp);
+        mat4_mul(Wp, W, W);
+        mat4_inverse(W, Ci);
+    } else {
+        // C^-1 of W = T R S: rows k = (R S)^-1 = S^-1 R^T, column 3 = -S^-1 R^T t
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 3; ++k) {
 #pragma unroll
-        for (int r = 0; r < 3; ++r) Ci[k * 4 + r] = (W[r * 4 + k] / R.s[k]) / R.s[k];
-        Ci[k * 4 + 3] = -(Ci[k * 4 + 0] * W[3] + Ci[k * 4 + 1] * W[7] + Ci[k * 4 + 2] * W[11]);
+            for (int r = 0; r < 3; ++r) Ci[k * 4 + r] = (W[r * 4 + k] / R.s[k]) / R.s[k];
+            Ci[k * 4 + 3] = -(Ci[k * 4 + 0] * W[3] + Ci[k * 4 + 1] * W[7] + Ci[k * 4 + 2] * W[11]);
+        }
     }
     // rows 0, 1, 3 of P C^-1 (P: p00 / p02 in row 0, p11 / p12 in row 1, p32
     // in row 3; row 3 of C^-1 is 0 0 0 1)

@@ -359,7 +359,7 @@ __device__ __forceinline__ void cam_record_thread(const DevProblem &P, int t,
     if (P.cf_aidx) {
         long long ov_idx = -1;
         if (p >= 0) ov_idx = P.p_vidx[p];  // the variant's parameter (at this frame)
-        camera_record_fast(P, cf, ov_idx, ov.value, &recs[(size_t)idx * CAMREC]);
+        camera_record_fast(P, cf, ov_idx, ov.value, &recs[(size_t)idx * CAMREC], ov.attr);
         return;
     }
     camera_record(P, P.cf_cam[cf], P.cf_frame[cf], ov, &recs[(size_t)idx * CAMREC]);
@@ -1567,15 +1567,14 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
         if (lane == 0) wsum[wave][e] = v;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
-        const bool mat = t < NGMAX * NGMAX;
-        const int a = mat ? t / NGMAX : t - NGMAX * NGMAX, b = mat ? t % NGMAX : 0;
-        double v = 0.;
-        if (a < NG && b < NG) {
-            const int e = mat ? a * NG + b : NG * NG + a;
-            v = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
-        }
-        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = v;
+    // the block's row of [Agg | gG] in the compact layout of the plan's nG
+    // (nG^2 + nG entries, k_ne_glob_reduce)
+    const int NA_ = nG * nG + nG;
+    for (int t = threadIdx.x; t < NA_; t += blockDim.x) {
+        const bool mat = t < nG * nG;
+        const int a = mat ? t / nG : t - nG * nG, b = mat ? t % nG : 0;
+        const int e = mat ? a * NG + b : NG * NG + a;
+        partial[(size_t)blockIdx.x * NA_ + t] = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
     }
 }
 
@@ -1632,21 +1631,11 @@ __global__ void __launch_bounds__(256) k_ne_glob_wide(DevProblem P, const double
             acc[k] = v;
         }
     }
-    // compact [Agg | gG] through LDS, then the NGMAX-layout row (zeros beyond nG)
-    double *cmp = &sg[0][0];
-    __syncthreads();
+    // the block's row of [Agg | gG], compact (nG^2 + nG entries, as k_ne_glob)
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
         const int e = threadIdx.x + 256 * k;
-        if (e < NA) cmp[e] = acc[k];
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < NGMAX * NGMAX + NGMAX; t += blockDim.x) {
-        const bool mat = t < NGMAX * NGMAX;
-        const int a = mat ? t / NGMAX : t - NGMAX * NGMAX, c = mat ? t % NGMAX : 0;
-        double v = 0.;
-        if (a < nG && c < nG) v = cmp[mat ? a * nG + c : nG * nG + a];
-        partial[(size_t)blockIdx.x * (NGMAX * NGMAX + NGMAX) + t] = v;
+        if (e < NA) partial[(size_t)blockIdx.x * NA + e] = acc[k];
     }
 }
 
@@ -1655,20 +1644,19 @@ __global__ void __launch_bounds__(256) k_ne_glob_wide(DevProblem P, const double
 __global__ void __launch_bounds__(256) k_ne_glob_reduce(DevProblem P,
                                                         const double *__restrict__ partial,
                                                         int nblk, double *Agg, double *gG) {
-    const int nG = P.nG;
+    const int nG = P.nG, NA = nG * nG + nG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int t = wave; t < NGMAX * NGMAX + NGMAX; t += 4) {
-        const bool mat = t < NGMAX * NGMAX;
-        if (mat ? ((t / NGMAX) >= nG || (t % NGMAX) >= nG) : (t - NGMAX * NGMAX) >= nG) continue;
+    for (int t = wave; t < NA; t += 4) {
+        const bool mat = t < nG * nG;
         double s = 0.;
-        for (int k = lane; k < nblk; k += 64) s += partial[(size_t)k * (NGMAX * NGMAX + NGMAX) + t];
+        for (int k = lane; k < nblk; k += 64) s += partial[(size_t)k * NA + t];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
         if (lane == 0) {
             if (mat)
-                Agg[t] = s;
+                Agg[(t / nG) * NGMAX + t % nG] = s;
             else
-                gG[t - NGMAX * NGMAX] = s;
+                gG[t - nG * nG] = s;
         }
     }
 }

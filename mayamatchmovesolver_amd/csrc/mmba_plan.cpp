@@ -653,9 +653,6 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         if (central) throw Unsupported{"rolling shutter with central differences"};
         if (nB_solved > 0) throw Unsupported{"rolling shutter with solved bundles"};
         if (!bnd_par.empty()) throw Unsupported{"rolling shutter with bundle-side parameters"};
-        for (int c = 0; c < nC; ++c)
-            if (pr->tfm_parent[pr->cam_tfm[c]] >= 0)
-                throw Unsupported{"rolling shutter on a camera transform with a parent"};
         for (int v : cf_var_flags)
             if (v != 0) throw Unsupported{"rolling shutter with a camera / bundle shared attribute"};
         for (int cf = 0; cf < ncf; ++cf) {
@@ -1111,9 +1108,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.bnd_p4 = upload(bnd_p4);
     {
         // per-camera-frame attribute-value indices for the camera records
-        // (cameras whose transform has no parent)
+        // (cameras whose transform has no parent; in rolling-shutter plans
+        // every camera: the records then multiply by the parent's world
+        // matrix, camera_record_fast / rs_record)
         bool ok = true;
-        for (int c = 0; c < nC && ok; ++c)
+        for (int c = 0; c < nC && ok && !rs_on; ++c)
             if (pr->tfm_parent[pr->cam_tfm[c]] >= 0) ok = false;
         D.cf_aidx = nullptr;
         if (ok && ncf > 0) {

@@ -14,7 +14,8 @@
 // equations couple each camera-frame with the next two of the same camera:
 // the reduced system is a band (+ arrow) factored by the band solvers
 // (block cyclic reduction for C5's 2 cameras x 6 parameters: half bandwidth
-// 29).  Restricted to camera transforms without a parent, no solved bundle,
+// 29).  A parented camera blends its own translate / rotate under the
+// parent's world matrix at the frame.  Restricted to no solved bundle,
 // forward differences, one shard (Plan::build refuses the rest).
 #include <hip/hip_runtime.h>
 
@@ -119,7 +120,7 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
         if (kind != 1) {
             double rec[CAMREC];
             rs_record(P, RC, tau, kind == 0 && p >= 0 ? param_vidx(P, p) : -1,
-                      p >= 0 ? ext_pert[p] : 0., rec);
+                      p >= 0 ? ext_pert[p] : 0., rec, kind == 0 && p >= 0 ? P.p_attr[p] : -1);
             double lc[MMBA_LENS_NUM_ATTRS];
             if (hl) {
                 const int oa = kind == 2 ? P.p_attr[p] : -2;

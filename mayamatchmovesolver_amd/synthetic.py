@@ -766,7 +766,8 @@ EDGE_RENDERS = {"wide": (2048, 858), "narrow": (2048, 1556)}  # aspect above / b
 def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0.0, 0.0),
                camera_scale=1.0, rotate_order=abi.ROO_XYZ, parented=False, frames=6,
                bundles=24, seed=9, stiffness=False, static_focal=False,
-               offset_shifts=True, gauge=True) -> Problem:
+               offset_shifts=True, gauge=True, solve_bundles=True,
+               solve_parent=False) -> Problem:
     """Small bundle-adjustment scene over the camera settings the synthetic
     configs keep benign: any film fit, a render aspect above or
     below the film aspect, film offsets (inches, Appendix B5/B6), a camera
@@ -780,7 +781,11 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
     translates and a smoothness row on one camera rotate
     (adjust_measureErrors.cpp:311-387).  ``static_focal``: the camera focal
     is solved too, as one static (global) parameter.  ``gauge=False``: nothing
-    locked (with one frame: a bundle-only solve against a fixed camera)."""
+    locked (with one frame: a bundle-only solve against a fixed camera).
+    ``solve_bundles=False``: the bundles stay at their true positions, unsolved
+    (the rolling-shutter plans' restriction).  ``solve_parent`` (with
+    ``parented``): the parent group's rotation is solved too -- three static
+    (global) parameters starting 0.5-1 degree off."""
     rng = np.random.Generator(np.random.PCG64(seed))
     F, B = frames, bundles
     b = SceneBuilder(F)
@@ -794,9 +799,11 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
     r0 = r_true + rng.uniform(-1.0, 1.0, size=r_true.shape)
     t0[0], r0[0] = t_true[0], r_true[0]
     parent = None
+    pids = None
     if parented:
-        parent, _ = b.transform(t=(0.3, -0.2, 0.5), r=(1.5, -2.0, 3.0), s=(1.0, 1.0, 1.0),
-                                rotate_order=rotate_order)
+        pr0 = (2.0, -2.8, 3.6) if solve_parent else (1.5, -2.0, 3.0)
+        parent, pids = b.transform(t=(0.3, -0.2, 0.5), r=pr0, s=(1.0, 1.0, 1.0),
+                                   rotate_order=rotate_order)
     ctfm, tids = b.transform(t=[t0[:, 0], t0[:, 1], t0[:, 2]], r=[r0[:, 0], r0[:, 1], r0[:, 2]],
                              parent=parent, rotate_order=rotate_order)
     cam, cids = b.camera(ctfm, focal=FOCAL_MM * (1.03 if static_focal else 1.0),
@@ -804,8 +811,10 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
                          film_fit=film_fit, render_size=EDGE_RENDERS[render],
                          camera_scale=camera_scale)
     P0 = P * (1.0 + rng.uniform(-0.03, 0.03, size=(B, 1)))
-    if gauge:
+    if gauge or not solve_bundles:
         P0[0] = P[0]
+    if not solve_bundles:
+        P0 = P.copy()
     bids = []
     for j in range(B):
         bt, ids = b.transform(t=tuple(P0[j]))
@@ -833,7 +842,10 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
         b.solve(cids[abi.CAM_FOCAL_MM])
     for a in tids[:6]:
         b.solve(a)
-    for j in range(1 if gauge else 0, B):
+    if solve_parent and pids is not None:
+        for a in pids[3:6]:
+            b.solve(a)
+    for j in range(1 if gauge else 0, B if solve_bundles else 0):
         for a in bids[j][:3]:
             b.solve(a)
     if stiffness:

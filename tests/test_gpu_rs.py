@@ -123,3 +123,34 @@ def test_rs_refuses_solved_bundles(gpu_ctx):
     with pytest.raises(MmbaError) as e:
         Solver(prob, opt, context=gpu_ctx)
     assert e.value.code == abi.MMBA_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("solve_parent", [False, True])
+@pytest.mark.parametrize("mode", MODES)
+def test_rs_parented_camera(solve_parent, mode, oracle, gpu_ctx):
+    """A camera under a rotated, translated group (tests/test_oracle_rs.py
+    pins the model: the group's world matrix at the frame times the blended
+    local pose): measurement, reprojection and the FD Jacobian at 1e-12 /
+    1e-7, then the whole solve against the oracle; with the group's rotation
+    solved its three static columns move every observation through the
+    parent's world matrix (rs_record's attribute override)."""
+    prob = S.edge_scene(parented=True, solve_bundles=False, solve_parent=solve_parent)
+    prob.cam_rs_value = np.array([0.6])
+    opt = S.config_options(prob, scene_graph_mode=mode)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        for x in (None, prob.x0 + 0.01):
+            f, eu, ed, _ = s.measure(x)
+            fr, eur, edr, _ = oracle.measure(prob, opt, x)
+            np.testing.assert_allclose(f, fr, rtol=1e-12, atol=1e-12)
+            pts, _ = s.reproject(x)
+            pr, _ = oracle.reproject_obs(prob, opt, x)
+            np.testing.assert_allclose(pts, pr, rtol=1e-12, atol=1e-14)
+        x1 = prob.x0 + 0.01
+        J = s.jacobian(x1)
+        _, Jr = oracle.jacobian(prob, opt, x1)
+        scale = np.max(np.abs(Jr))
+        assert np.max(np.abs(J - Jr)) <= 1e-7 * scale
+    finally:
+        s.close()
+    check_solve(prob, opt, oracle, gpu_ctx)

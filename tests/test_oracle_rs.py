@@ -253,3 +253,49 @@ def test_rs_forward_model_inverts_the_exporter(rs, oracle):
     # negative control: blending forward (the opposite sign convention)
     # doubles the shift instead of removing it
     assert wrong[0] > 1.5 * shifts[0], (wrong, shifts)
+
+
+def test_rs_parented_reprojection_matches_numpy(oracle):
+    """A camera under a (static, rotated and translated) group: the blend
+    moves the camera's own translate / rotate values and the world pose is the
+    group's world matrix times the blended local one (oracle
+    rs_camera_world) -- the oracle's reprojected points against that numpy
+    model, 1e-10 in film units."""
+    p = S.edge_scene(parented=True, solve_bundles=False)
+    p.cam_rs_value = np.array([0.6])
+    o = S.config_options(p)
+    pts, _ = oracle.reproject_obs(p, o)
+    F = p.num_frames
+    ta = p.tfm_attrs.reshape(-1, 9)
+    t = p.cam_tfm[0]
+    par = p.tfm_parent[t]
+    assert par >= 0
+
+    def vals(tf, k):
+        a = ta[tf, k]
+        off = p.attr_offset[a]
+        return p.attr_values[off:off + F] if p.attr_animated[a] else np.full(F, p.attr_values[off])
+
+    tr = np.stack([vals(t, k) for k in range(3)], 1)
+    rr = np.stack([vals(t, k) for k in range(3, 6)], 1)
+    tp = np.array([vals(par, k)[0] for k in range(3)])
+    Rp = S._euler_xyz(*[vals(par, k)[0] for k in range(3, 6)])
+    fs = p.obs_frame
+    tau = p.cam_rs_value[0] * (0.5 - p.obs_xy[1::2])
+    tb = np.stack([S._blend_at(tr[:, k], fs, tau) for k in range(3)], 1)
+    rb = np.stack([S._blend_at(rr[:, k], fs, tau) for k in range(3)], 1)
+    Rw = Rp[None] @ S._euler_xyz(rb[:, 0], rb[:, 1], rb[:, 2])
+    tw = tb @ Rp.T + tp
+    bpos = np.array([[p.attr_values[p.attr_offset[ta[p.bnd_tfm[p.mkr_bnd[k]], j]]] for j in range(3)]
+                     for k in p.obs_marker])
+    pc = np.einsum("nji,nj->ni", Rw, bpos - tw)
+    mx = S.FOCAL_MM * pc[:, 0] / (S.FILM_W_MM * -pc[:, 2])
+    my = S.FOCAL_MM * pc[:, 1] / (S.FILM_H_MM * -pc[:, 2])
+    ra = S.EDGE_RENDERS["narrow"][0] / S.EDGE_RENDERS["narrow"][1]
+    fa = S.FILM_W_MM / S.FILM_H_MM
+    np.testing.assert_allclose(pts[0::2], mx, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(pts[1::2], my * (ra / fa), rtol=0, atol=1e-10)
+    # and the blend matters
+    p.cam_rs_value = np.array([0.0])
+    pts0, _ = oracle.reproject_obs(p, o)
+    assert np.max(np.abs(pts0 - pts)) > 1e-6
