@@ -48,10 +48,12 @@ def test_wide_arrow_band(kw, ng, mode, oracle, gpu_ctx):
 def test_wide_arrow_bcr(kw, oracle, gpu_ctx):
     """Four / five frames of the animated camera: half bandwidth 23 / 29, so
     the reduced system is factored by block cyclic reduction (K = 24 / 32)
-    with the 24 / 32-wide arrow (roots of order 48 / 64).  (Windowed
-    visibility of the animated camera over more frames leaves these rigs
-    without a parity bar: the oracle's own x moves by O(1) under a 1-ulp
-    change of x0.)"""
+    with the 24 / 32-wide arrow (roots of order 48 / 64).  The oracle's own
+    1-ulp x envelope on these rigs is 4.2e-7 / 2.7e-8, inside the 1e-6 bar.
+    (Windowed visibility of the animated camera over 8-12 frames leaves a rig
+    without a parity bar: there the envelope is 8e1 to 3e6 and even the
+    oracle's reason code and evaluation count change under a 1-ulp change of
+    x0 -- tools/wide_arrow_envelope.py, profiles/r4_parity/.)"""
     prob = S.witness_scene(**kw)
     opt = make_options()
     assert reduced_kind(prob, opt, gpu_ctx) == BAND
