@@ -148,7 +148,8 @@ def test_sharded_ba_three_shards_structure(solve, gpu_ctx, paths):
 
 @pytest.mark.parametrize("nshards", [4, 8])
 def test_sharded_ba_many_shards(nshards, gpu_ctx):
-    """The shard counts the 1/2/4/8-GPU bench runs (default BCR reduced solve)
+    """The shard counts the 1/2/4/8-GPU bench runs (default reduced solve: the
+    separator form)
     on the 2-shard oracle case's scene density (20 frames per shard), against
     the unsharded GPU solve.  Every shard agrees bit for bit; same reason;
     the first five ||f|| (where a decomposition error shows: a wrong Schur
