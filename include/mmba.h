@@ -219,8 +219,8 @@ typedef struct mmba_problem {
      * animated parameter then re-measures frames f-1..f+1.  A camera under a
      * parent blends its own translate / rotate values; its world pose is the
      * parent's world matrix at frame f times the blended local matrix.
-     * Supported without solved bundles, unsharded (MMBA_ERR_UNSUPPORTED
-     * otherwise). */
+     * Supported with forward differences, unsharded, without bundle-side
+     * global parameters (MMBA_ERR_UNSUPPORTED otherwise). */
     const double *cam_rs_value;   /* [num_cameras] */
 
     /* ---- ABI 5 ---- */

@@ -206,6 +206,11 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
                           double *Lb, double *tb, double *Wg, int *fail);
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
                       double *W);
+// rolling shutter with solved bundles: W rows of the virtual observations
+// (Plan::build, PV)
+void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,
+                         const int *vobs, const int *vcoff, const double *J, const double *Lb,
+                         double *W);
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
                        const SView &V, int npad, double *rhs);

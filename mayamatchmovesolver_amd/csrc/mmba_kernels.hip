@@ -1476,7 +1476,9 @@ __global__ void k_ne_bnd(DevProblem P, const double *__restrict__ J,
     for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
         const int i = P.bobs[q];
         const int cf = P.obs_cf[i];
-        const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
+        // the bundle's columns follow the camera-frame's variants, or come
+        // last in a rolling-shutter row (k_jacobian_rs)
+        const int s = P.rs ? nloc[i] - pb : P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
         double jx[PBMAX], jy[PBMAX];
         for (int a = 0; a < pb; ++a) {
             jx[a] = J[(size_t)(2 * (s + a)) * M + i];
@@ -2062,6 +2064,53 @@ __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__
     }
 }
 
+// Rolling shutter with solved bundles: the W row of virtual observation v
+// (real observation i = vobs[v], camera-frame block PV.obs_cf[v] whose
+// columns start at vcoff[v] in i's row, the bundle's columns last:
+// k_jacobian_rs) -- k_schur_obs's arithmetic, one thread per virtual
+// observation.  J is indexed by the real observation count Mr.
+__global__ void __launch_bounds__(64) k_schur_obs_rs(DevProblem PV, int Mr,
+                                                     const int *__restrict__ nloc,
+                                                     const int *__restrict__ vobs,
+                                                     const int *__restrict__ vcoff,
+                                                     const double *__restrict__ J,
+                                                     const double *__restrict__ Lb, double *W) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= PV.M) return;
+    const int wst = PV.wst;
+    double *row = &W[(size_t)v * wst];
+    for (int k = 0; k < wst; ++k) row[k] = 0.;
+    const int b = PV.obs_bnd[v];
+    const int pb = PV.bnd_pb[b];
+    if (pb <= 0) return;
+    const int i = vobs[v], cf = PV.obs_cf[v];
+    const int pc = min(PV.cf_pc[cf], wst / 3);
+    const int c0 = vcoff[v], s = nloc[i] - pb;
+    double bx[3], by[3], L[3][3], il[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        bx[a] = a < pb ? J[(size_t)(2 * (s + a)) * Mr + i] : 0.;
+        by[a] = a < pb ? J[(size_t)(2 * (s + a) + 1) * Mr + i] : 0.;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) L[a][c] = Lb[(size_t)b * 9 + a * 3 + c];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) il[a] = a < pb ? 1.0 / L[a][a] : 0.;
+    for (int r = 0; r < pc; ++r) {
+        const double cx = J[(size_t)(2 * (c0 + r)) * Mr + i], cy = J[(size_t)(2 * (c0 + r) + 1) * Mr + i];
+        double w[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            double t = cx * bx[a] + cy * by[a];
+#pragma unroll
+            for (int k = 0; k < a; ++k) t -= L[a][k] * w[k];
+            w[a] = t * il[a];
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) row[r * 3 + a] = w[a];
+    }
+}
+
 // S = (Acc + lam D^2 | Acg | Agg + lam D^2), lower triangle, plus identity
 // on the padded tail; rhs = g_R.
 __global__ void __launch_bounds__(256) k_schur_init(
@@ -2349,7 +2398,11 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
             for (int c = 0; c < PC; ++c)
                 acc[a * PC + c] += wi[a * 3] * wj[c * 3] + wi[a * 3 + 1] * wj[c * 3 + 1] +
                                    wi[a * 3 + 2] * wj[c * 3 + 2];
-        if (diag) {
+        // rhs_R -= W_i t_b(i) once per observation: from its pair (i, i)
+        // only (a diagonal destination also holds pairs (i, j) of two
+        // observations of one bundle in one camera-frame, or of two
+        // rolling-shutter virtual observations)
+        if (diag && pr.x == pr.y) {
             const int b = P.obs_bnd[pr.x];
             const double t0 = tb[(size_t)b * 3], t1 = tb[(size_t)b * 3 + 1],
                          t2 = tb[(size_t)b * 3 + 2];
@@ -3680,6 +3733,12 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
                       double *W) {
     k_schur_obs<<<nblk(P.M, 64), 64, sizeof(double) * 64 * P.wst, s>>>(P, J, Lb, W);
+}
+void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,
+                         const int *vobs, const int *vcoff, const double *J, const double *Lb,
+                         double *W) {
+    if (PV.M > 0)
+        k_schur_obs_rs<<<nblk(PV.M, 64), 64, 0, s>>>(PV, Mr, nloc, vobs, vcoff, J, Lb, W);
 }
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,

@@ -546,8 +546,12 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         if (!(lam == 0. && lb0_valid))  // else formed by the Jacobian's bundle pass
             launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
         lb0_valid = false;
-        launch_schur_obs(s, P, d_J, d_Lb, d_W);
+        if (rs_bnd)  // W rows of the virtual observations
+            launch_schur_obs_rs(s, PV, M, d_nloc, d_vobs, d_vcoff, d_J, d_Lb, d_W);
+        else
+            launch_schur_obs(s, P, d_J, d_Lb, d_W);
     }
+    const DevProblem &PS = schur_problem();
     if (nR > 0) {
         const SView V = sview();
         // unsharded, every rhs row is written by k_schur_init
@@ -558,7 +562,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         // zeroed once at plan build; the partitioned path factors in place
         if (band && bs.red) {  // d_rhs is the tail of the block, zeroed above
             MMBA_HIP(hipMemsetAsync(bs.red, 0, sizeof(double) * (bs.red_count - nRpad), s));
-        } else if (band && !bs.use_bcr && !bs.use_bd) {
+        } else if (band && ((!bs.use_bcr && !bs.use_bd) || rs_bnd)) {
+            // (rolling shutter with solved bundles: k_rs_offdiag writes the
+            // coupling blocks, so k_schur_dest subtracts instead of assigning)
             const int nb = nR - nG;
             MMBA_HIP(hipMemsetAsync(bs.Bd, 0, sizeof(double) * (size_t)nb * (bw + 1), s));
             if (nG > 0) MMBA_HIP(hipMemsetAsync(bs.Ga, 0, sizeof(double) * (size_t)nG * nb, s));
@@ -579,13 +585,13 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
                 SchurInitFold fi{};
                 if (fold) fi = SchurInitFold{1, d_Acc, d_g, d_diag, lam};
                 const bool rhs_done =
-                    launch_schur_dest(s, P, d_W, d_dest, d_dest_off, ndest, d_dpairs, V,
-                                      pc_uniform, band && bs.use_bcr, d_tb,
+                    launch_schur_dest(s, PS, d_W, d_dest, d_dest_off, ndest, d_dpairs, V,
+                                      pc_uniform, band && bs.use_bcr && !rs_bnd, d_tb,
                                       nranks > 1 ? nullptr : d_rhs, fi);
-                if (!rhs_done) launch_schur_rhs(s, P, d_W, d_tb, d_row_cf, d_rhs);
-                launch_schur_glob(s, P, d_W, d_Wg, d_tb, V, d_rhs);
+                if (!rhs_done) launch_schur_rhs(s, PS, d_W, d_tb, d_row_cf, d_rhs);
+                launch_schur_glob(s, PS, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
-                launch_schur_pairs(s, P, d_W, d_Wg, d_tb, V, d_rhs);
+                launch_schur_pairs(s, PS, d_W, d_Wg, d_tb, V, d_rhs);
             }
         }
         span_begin(SPAN_CHOL);
@@ -644,7 +650,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         if (trial_fold_ok) {
             // the trial point's parameter pass rides in the back substitution
             // (the last damped solve before a trial is the one it keeps)
-            launch_obs_wtx(s, P, d_W, d_xR, d_U);
+            launch_obs_wtx(s, PS, d_W, d_xR, d_U);
             TrialFold T;
             T.x = d_x;
             T.diag = d_diag;
@@ -661,12 +667,12 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             T.nother = n_trial_other;
             T.partial = d_partial + 3 * (size_t)pw;
             T.rstride = pw;
-            launch_backsub_trial(s, P, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
+            launch_backsub_trial(s, PS, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
             trial_folded = true;
             params_at = nullptr;  // the attribute block now holds the trial point
             recs_full_at = nullptr;
         } else {
-            launch_backsub_bundle(s, P, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
+            launch_backsub_bundle(s, PS, d_W, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs);
         }
     }
     if (dnorm_by_trial) {
@@ -713,7 +719,7 @@ void Plan::newton_enqueue(double dxnorm) {
     MMBA_HIP(hipMemsetAsync(d_scalar + SL_NEWT_B, 0, 2 * sizeof(double), s));
     if (nR > 0) launch_gather_R(s, P, d_v, d_wR, nRpad);
     if (nB_solved > 0) {
-        launch_newton_bundle(s, P, d_W, d_Wg, d_Lb, d_v, d_wR, d_usq, d_nu, d_ngp);
+        launch_newton_bundle(s, schur_problem(), d_W, d_Wg, d_Lb, d_v, d_wR, d_usq, d_nu, d_ngp);
         launch_reduce_sum(s, d_usq, nB, d_scalar + SL_NEWT_B);
     }
     if (nR > 0) {

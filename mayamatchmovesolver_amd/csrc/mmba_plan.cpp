@@ -651,8 +651,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     if (rs_on) {
         if (nranks > 1) throw Unsupported{"rolling shutter: sharded solve"};
         if (central) throw Unsupported{"rolling shutter with central differences"};
-        if (nB_solved > 0) throw Unsupported{"rolling shutter with solved bundles"};
-        if (!bnd_par.empty()) throw Unsupported{"rolling shutter with bundle-side parameters"};
+        for (int b = 0; b < nB; ++b)
+            if (!bglob[b].empty()) throw Unsupported{"rolling shutter with bundle-side global parameters"};
         for (int v : cf_var_flags)
             if (v != 0) throw Unsupported{"rolling shutter with a camera / bundle shared attribute"};
         for (int cf = 0; cf < ncf; ++cf) {
@@ -680,10 +680,16 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     {
         std::vector<int> blo(nB, nCF), bhi(nB, -1);
         for (int i = 0; i < Mg; ++i) {
-            const int b = obs_bnd_g[i], cf = obs_cf[i];
-            if (bnd_pb[b] == 0 || cf_pc[cf] == 0) continue;
-            blo[b] = std::min(blo[b], cf_roff[cf]);
-            bhi[b] = std::max(bhi[b], cf_roff[cf] + cf_pc[cf] - 1);
+            const int b = obs_bnd_g[i];
+            if (bnd_pb[b] == 0) continue;
+            // a rolling-shutter row also reaches the neighbouring frames' blocks
+            const int cfs[3] = {obs_cf[i], rs_on ? cf_nb[2 * obs_cf[i]] : -1,
+                                rs_on ? cf_nb[2 * obs_cf[i] + 1] : -1};
+            for (int cf : cfs) {
+                if (cf < 0 || cf_pc[cf] == 0) continue;
+                blo[b] = std::min(blo[b], cf_roff[cf]);
+                bhi[b] = std::max(bhi[b], cf_roff[cf] + cf_pc[cf] - 1);
+            }
         }
         for (int b = 0; b < nB; ++b)
             if (bhi[b] >= 0) bw = std::max(bw, bhi[b] - blo[b]);
@@ -852,6 +858,42 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         std::vector<int> fill(bobs_off.begin(), bobs_off.end() - 1);
         for (int i = 0; i < M; ++i) bobs[fill[d_bnd[i]]++] = i;
     }
+    // rolling shutter with solved bundles: a row reaches the camera-frame
+    // blocks of f - 1, f, f + 1, so the Schur complement runs over virtual
+    // observations -- one per (observation, block it reaches) with its own W
+    // row (k_schur_obs_rs), grouped by camera-frame and by bundle like the
+    // real ones; the Schur kernels take that view (PV) unchanged
+    rs_bnd = rs_on && nB_solved > 0;
+    std::vector<int> v_obs, v_cf, v_bnd, v_coff, vcf_off(ncf + 1, 0), vbobs, vbobs_off(nB + 1, 0);
+    if (rs_bnd) {
+        struct VObs {
+            int cf, i, coff;
+        };
+        std::vector<VObs> vs;
+        for (int i = 0; i < M; ++i) {
+            if (bnd_pb[d_bnd[i]] == 0) continue;
+            const int cf = d_cf[i], pp = cf_nb[2 * cf], nn = cf_nb[2 * cf + 1];
+            const int nvs = cf_var_off[cf + 1] - cf_var_off[cf] - 1;  // k_jacobian_rs's order
+            if (cf_pc[cf] > 0) vs.push_back({cf, i, 0});
+            if (pp >= 0 && cf_pc[pp] > 0) vs.push_back({pp, i, nvs});
+            if (nn >= 0 && cf_pc[nn] > 0) vs.push_back({nn, i, nvs + (pp >= 0 ? cf_pc[pp] : 0)});
+        }
+        std::stable_sort(vs.begin(), vs.end(), [](const VObs &a, const VObs &b) { return a.cf < b.cf; });
+        Mv = (int)vs.size();
+        for (const VObs &v : vs) {
+            v_obs.push_back(v.i);
+            v_cf.push_back(v.cf);
+            v_bnd.push_back(d_bnd[v.i]);
+            v_coff.push_back(v.coff);
+            vcf_off[v.cf + 1]++;
+            vbobs_off[d_bnd[v.i] + 1]++;
+        }
+        for (int cf = 0; cf < ncf; ++cf) vcf_off[cf + 1] += vcf_off[cf];
+        for (int b = 0; b < nB; ++b) vbobs_off[b + 1] += vbobs_off[b];
+        vbobs.assign(std::max(Mv, 1), 0);
+        std::vector<int> fill(vbobs_off.begin(), vbobs_off.end() - 1);
+        for (int v = 0; v < Mv; ++v) vbobs[fill[v_bnd[v]]++] = v;
+    }
     // stale errorDistanceList source per frame (B13): last parameter whose
     // frame mask includes the frame; lmdif re-measures everything per column.
     std::vector<int> stale(F, -1);
@@ -966,7 +1008,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         long long npairs = 0;
         for (int b = 0; b < nB; ++b)
             if (bnd_pb[b] > 0) {
-                const long long kb = bobs_off[b + 1] - bobs_off[b];
+                const long long kb = rs_bnd ? vbobs_off[b + 1] - vbobs_off[b] : bobs_off[b + 1] - bobs_off[b];
                 npairs += kb * kb;
             }
         use_dest = nB_solved > 0 && nR > 0 && npairs <= (1ll << 30);
@@ -980,14 +1022,18 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             // bucket by (cfj, i, j): O(pairs) grouping instead of one global
             // sort (C3: ~50M pairs)
             std::vector<long long> cnt(ncf + 1, 0);
+            // (rolling shutter with solved bundles: the virtual observations)
+            const std::vector<int> &sbo = rs_bnd ? vbobs_off : bobs_off;
+            const std::vector<int> &sb = rs_bnd ? vbobs : bobs;
+            const std::vector<int> &scf = rs_bnd ? v_cf : d_cf;
             auto for_pairs = [&](auto &&fn) {
                 for (int b = 0; b < nB; ++b) {
                     if (bnd_pb[b] == 0) continue;
-                    for (int qi = bobs_off[b]; qi < bobs_off[b + 1]; ++qi) {
-                        const int i = bobs[qi], cfi = d_cf[i];
+                    for (int qi = sbo[b]; qi < sbo[b + 1]; ++qi) {
+                        const int i = sb[qi], cfi = scf[i];
                         if (cf_pc[cfi] == 0 || !cf_own[cfi]) continue;
-                        for (int qj = bobs_off[b]; qj < bobs_off[b + 1]; ++qj) {
-                            const int j = bobs[qj], cfj = d_cf[j];
+                        for (int qj = sbo[b]; qj < sbo[b + 1]; ++qj) {
+                            const int j = sb[qj], cfj = scf[j];
                             // destination rows must be this shard's camera-frames
                             if (cf_pc[cfj] == 0 || cfi < cfj) continue;
                             fn(cfi, cfj, i, j);
@@ -1150,7 +1196,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         std::vector<int> bpos(M);
         for (int q = 0; q < M; ++q) bpos[bobs[q]] = q;
         D.obs_bpos = upload(bpos);
-        bool all_fast = nG == 0 && nB_solved > 0;
+        // (the rolling-shutter Jacobian writes no bundle block records: its
+        // bundle normal equations come from the J rows, k_ne_bnd)
+        bool all_fast = nG == 0 && nB_solved > 0 && !rs_on;
         for (int b = 0; b < nB && all_fast; ++b)
             if (bnd_pb[b] > 0 && bnd_p4[b].w < 0) all_fast = false;
         D.JB = all_fast ? dalloc<double>((size_t)8 * M) : nullptr;
@@ -1362,6 +1410,17 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_p_own = upload(p_own);
     }
     P = D;
+    if (rs_bnd) {
+        PV = P;
+        PV.M = Mv;
+        PV.obs_cf = upload(v_cf);
+        PV.obs_bnd = upload(v_bnd);
+        PV.cf_obs_off = upload(vcf_off);
+        PV.bobs_off = upload(vbobs_off);
+        PV.bobs = upload(vbobs);
+        d_vobs = upload(v_obs);
+        d_vcoff = upload(v_coff);
+    }
 
     d_var_cf = upload(var_cf);
     d_stale = upload(stale);
@@ -1475,8 +1534,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_Lb = dalloc<double>((size_t)nB * 9);
     d_tb = dalloc<double>((size_t)nB * 3);
     d_Wg = dalloc<double>((size_t)nB * NGMAX * 3);
-    d_W = dalloc<double>((size_t)P.wst * (nB_solved > 0 ? M : 1));
-    d_U = dalloc<double>((size_t)4 * (nB_solved > 0 ? M : 1));
+    const int Mw = rs_bnd ? std::max(Mv, 1) : M;  // W rows: (virtual) observations
+    d_W = dalloc<double>((size_t)P.wst * (nB_solved > 0 ? Mw : 1));
+    d_U = dalloc<double>((size_t)4 * (nB_solved > 0 ? Mw : 1));
     d_rhs = bs.red_rhs ? bs.red_rhs : dalloc<double>(nRpad);
     d_yR = dalloc<double>(nRpad);
     d_xR = dalloc<double>(nRpad);

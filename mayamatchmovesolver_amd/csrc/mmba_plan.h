@@ -99,6 +99,15 @@ struct Plan {
     // P with every lens instance slot at its plug value: what the reference
     // measures before setParameters first runs (solveFrames' initial
     // measureErrors, adjust_base.cpp:1002-1004 then 1076-1089)
+    // rolling shutter with solved bundles: the Schur complement's view of
+    // the problem, over virtual observations (one per observation and
+    // camera-frame block its row reaches, grouped by camera-frame):
+    // obs_cf / obs_bnd / cf_obs_off / bobs / M are theirs (Plan::build)
+    bool rs_bnd = false;
+    int Mv = 0;
+    DevProblem PV{};
+    const int *d_vobs = nullptr, *d_vcoff = nullptr;
+    const DevProblem &schur_problem() const { return rs_bnd ? PV : P; }
     DevProblem plug_problem() const {
         DevProblem Q = P;
         if (Q.obs_inst) Q.inst_attr = d_inst_attr_plug;

@@ -15,8 +15,10 @@
 // the reduced system is a band (+ arrow) factored by the band solvers
 // (block cyclic reduction for C5's 2 cameras x 6 parameters: half bandwidth
 // 29).  A parented camera blends its own translate / rotate under the
-// parent's world matrix at the frame.  Restricted to no solved bundle,
-// forward differences, one shard (Plan::build refuses the rest).
+// parent's world matrix at the frame.  Solved bundles: the Schur
+// complement runs over virtual observations, one per (observation,
+// camera-frame block it reaches) (Plan::build, k_schur_obs_rs).  Restricted
+// to forward differences, one shard (Plan::build refuses the rest).
 #include <hip/hip_runtime.h>
 
 #include "mmba_geom.h"
@@ -43,7 +45,8 @@ __device__ __forceinline__ long long param_vidx(const DevProblem &P, int p) { re
 // The columns are listed first (parameter, kind), then evaluated by one code
 // site: kind 0 = a camera-side value (this frame or a blended neighbour),
 // 1 = a neighbouring frame's parameter the blend does not read (entry 0,
-// no evaluation), 2 = a lens coefficient.  One evaluation site keeps the
+// no evaluation), 2 = a lens coefficient, 3 = a parameter of the
+// observation's bundle (the bundle moved, the base record).  One evaluation site keeps the
 // inlined record + lens code (the register-heavy part) once.
 template <int TPB>
 __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P, const double *__restrict__ ext_pert,
@@ -96,6 +99,12 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
             cp[nl] = p;
             ck[nl++] = 2;
         }
+    // the observation's bundle parameters last (k_ne_bnd / k_schur_obs_rs
+    // find them at nloc - pb): the base record with the bundle moved
+    for (int q = P.bnd_par_off[b]; q < P.bnd_par_off[b] + P.bnd_pb[b] && nl < LMAX; ++q) {
+        cp[nl] = P.bnd_par[q];
+        ck[nl++] = 3;
+    }
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     const int pstale = stale_param[fr];
     RsCam RC;
@@ -121,6 +130,8 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
             double rec[CAMREC];
             rs_record(P, RC, tau, kind == 0 && p >= 0 ? param_vidx(P, p) : -1,
                       p >= 0 ? ext_pert[p] : 0., rec, kind == 0 && p >= 0 ? P.p_attr[p] : -1);
+            double bq[3] = {bp0[0], bp0[1], bp0[2]};
+            if (kind == 3) bundle_position(P, b, fr, Override{P.p_attr[p], ext_pert[p]}, bq);
             double lc[MMBA_LENS_NUM_ATTRS];
             if (hl) {
                 const int oa = kind == 2 ? P.p_attr[p] : -2;
@@ -130,7 +141,7 @@ __global__ void __launch_bounds__(TPB, MMBA_RS_WAVES) k_jacobian_rs(DevProblem P
                     lc[k] = (la[k] >= 0 && la[k] == oa) ? ov : lc0[k];
                 if (ltype == MMBA_LENS_3DE_ANAMORPHIC_STD_DEG4) lc[13] = 1.;  // inst_coeffs' rule
             }
-            const Resid r = residual_l(P, rec, bp0, mx, my, sw, hl, lc);
+            const Resid r = residual_l(P, rec, bq, mx, my, sw, hl, lc);
             if (l < 0) {
                 r0 = r;
                 rs = r;

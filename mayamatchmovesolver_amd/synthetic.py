@@ -767,7 +767,7 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
                camera_scale=1.0, rotate_order=abi.ROO_XYZ, parented=False, frames=6,
                bundles=24, seed=9, stiffness=False, static_focal=False,
                offset_shifts=True, gauge=True, solve_bundles=True,
-               solve_parent=False) -> Problem:
+               solve_parent=False, duplicate_markers=0) -> Problem:
     """Small bundle-adjustment scene over the camera settings the synthetic
     configs keep benign: any film fit, a render aspect above or
     below the film aspect, film offsets (inches, Appendix B5/B6), a camera
@@ -785,7 +785,9 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
     ``solve_bundles=False``: the bundles stay at their true positions, unsolved
     (the rolling-shutter plans' restriction).  ``solve_parent`` (with
     ``parented``): the parent group's rotation is solved too -- three static
-    (global) parameters starting 0.5-1 degree off."""
+    (global) parameters starting 0.5-1 degree off.  ``duplicate_markers`` = k:
+    bundles 1..k get a second marker of the same camera (a bundle seen twice
+    in one camera-frame), its positions offset by 0.002."""
     rng = np.random.Generator(np.random.PCG64(seed))
     F, B = frames, bundles
     b = SceneBuilder(F)
@@ -838,6 +840,8 @@ def edge_scene(film_fit=abi.FILM_FIT_HORIZONTAL, render="narrow", film_offset=(0
     mx, my = _noisy(rng, mx).reshape(B, F), _noisy(rng, my).reshape(B, F)
     for j in range(B):
         b.marker(cam, j, np.stack([mx[j], my[j]], axis=1))
+    for j in range(1, 1 + duplicate_markers):
+        b.marker(cam, j, np.stack([mx[j] + 0.002, my[j] - 0.002], axis=1))
     if static_focal:
         b.solve(cids[abi.CAM_FOCAL_MM])
     for a in tids[:6]:

@@ -246,3 +246,15 @@ def test_initial_error_given(oracle, gpu_ctx):
             assert (out.accepted_x is out.x) == better
     finally:
         s.close()
+
+
+@pytest.mark.parametrize("mode", [DAG, MMSG])
+def test_bundle_seen_twice_in_a_camera_frame(mode, oracle, gpu_ctx):
+    """Two markers of one camera on one bundle: the Schur complement's
+    diagonal destination then holds pairs (i, j) of two observations of the
+    bundle in one camera-frame, and its right-hand side must take W_i t_b
+    once per observation (from the pair (i, i) only)."""
+    prob = S.edge_scene(duplicate_markers=3)
+    opt = make_options(scene_graph_mode=mode, iterations=100)
+    check_measure_jacobian(prob, opt, oracle, gpu_ctx)
+    check(prob, opt, oracle, gpu_ctx)

@@ -114,15 +114,40 @@ def test_rs_zero_equals_global_shutter(gpu_ctx):
     np.testing.assert_array_equal(outs[0].fnorm_trace, outs[1].fnorm_trace)
 
 
-def test_rs_refuses_solved_bundles(gpu_ctx):
-    """Outside the supported scope (solved bundles) the plan is refused with
-    MMBA_ERR_UNSUPPORTED, never silently solved without the blend."""
-    prob = S.make_config(3, frames=8, scale=0.001)
-    prob.cam_rs_value = np.full(prob.num_cameras, 0.5)
-    opt = S.config_options(prob)
+def test_rs_refuses_central_differences(gpu_ctx):
+    """Outside the supported scope (central differences) the plan is refused
+    with MMBA_ERR_UNSUPPORTED, never silently solved without the blend."""
+    prob = rs_scene()
+    opt = S.config_options(prob, auto_diff_type=abi.AUTO_DIFF_TYPE_CENTRAL)
     with pytest.raises(MmbaError) as e:
         Solver(prob, opt, context=gpu_ctx)
     assert e.value.code == abi.MMBA_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("parented", [False, True])
+@pytest.mark.parametrize("mode", MODES)
+def test_rs_solved_bundles(parented, mode, oracle, gpu_ctx):
+    """Solved bundles under a rolling shutter: a row reaches the camera-frame
+    blocks of f - 1, f, f + 1 and its bundle, so the Schur complement runs
+    over virtual observations (one per block a row reaches; Plan::build,
+    k_schur_obs_rs).  Measurement, the FD Jacobian (the bundle columns last
+    in each row) and the whole solve against the oracle."""
+    prob = S.edge_scene(parented=parented, solve_bundles=True)
+    prob.cam_rs_value = np.array([0.6])
+    opt = S.config_options(prob, scene_graph_mode=mode)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        x1 = prob.x0 + 0.01
+        f, _, _, _ = s.measure(x1)
+        fr, _, _, _ = oracle.measure(prob, opt, x1)
+        np.testing.assert_allclose(f, fr, rtol=1e-12, atol=1e-12)
+        J = s.jacobian(x1)
+        _, Jr = oracle.jacobian(prob, opt, x1)
+        scale = np.max(np.abs(Jr))
+        assert np.max(np.abs(J - Jr)) <= 1e-7 * scale
+    finally:
+        s.close()
+    check_solve(prob, opt, oracle, gpu_ctx)
 
 
 @pytest.mark.parametrize("solve_parent", [False, True])
