@@ -131,10 +131,14 @@ def test_rs_solved_bundles(parented, mode, oracle, gpu_ctx):
     blocks of f - 1, f, f + 1 and its bundle, so the Schur complement runs
     over virtual observations (one per block a row reaches; Plan::build,
     k_schur_obs_rs).  Measurement, the FD Jacobian (the bundle columns last
-    in each row) and the whole solve against the oracle."""
+    in each row) and the solve against the oracle -- whole for the plain
+    camera; for the parented one the first four evaluations: after them the
+    cost crawls along a valley (16.99 -> 16.98 over 200 evaluations) where
+    the oracle's own 1-ulp x envelope is 7e-2 and its evaluation count moves
+    from 92 to 279."""
     prob = S.edge_scene(parented=parented, solve_bundles=True)
     prob.cam_rs_value = np.array([0.6])
-    opt = S.config_options(prob, scene_graph_mode=mode)
+    opt = S.config_options(prob, scene_graph_mode=mode, **({"iterations": 4} if parented else {}))
     s = Solver(prob, opt, context=gpu_ctx)
     try:
         x1 = prob.x0 + 0.01
