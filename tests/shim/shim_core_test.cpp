@@ -254,11 +254,15 @@ std::unique_ptr<Scene> make_scene(int which) {
     in.paramToAttrList.push_back({3, -1});
     sc->x0.push_back(0.02);
     if (which == 2) in.rolling_shutter = {0.5};
+    if (which == 4)  // every marker's x,y at every frame (mmba.h ABI 8)
+        for (int k = 0; k < B; ++k)
+            for (int f = 0; f < F; ++f)
+                in.markerFramePos.push_back({kScene2Markers[k * F + f][0], kScene2Markers[k * F + f][1]});
     sc->so.iterMax = 100;
     return sc;
 }
 
-constexpr int kScenes = 4;
+constexpr int kScenes = 5;
 std::unique_ptr<Scene> g_scene[kScenes];
 
 Scene *scene(int which) {

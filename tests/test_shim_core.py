@@ -192,3 +192,17 @@ def test_gpu_shim(which, shim, oracle):
     # exact-fit scenes (test3) stop at ||f|| ~ 1e-7, roundoff of the initial
     # ||f||: an absolute floor of 1e-9 ||f0|| as in test_gpu_parity.check_solve
     assert abs(np.linalg.norm(fv) - rr.error_final) <= 1e-6 * rr.error_final + 1e-9 * trr[0]
+
+
+def test_shim_passes_marker_frame_positions(shim):
+    """Scene 4 = scene 2's layout without the rolling shutter, with SolverInputs::markerFramePos filled
+    (every marker at every frame, mmba.h ABI 8): the flat problem carries it
+    as mkr_frame_xy, marker-major, frame-minor; the scenes without it pass
+    NULL."""
+    p, _, _ = shim_problem(shim, 4)
+    assert bool(p.mkr_frame_xy)
+    K, F = p.num_markers, p.num_frames
+    got = np.array([p.mkr_frame_xy[k] for k in range(2 * K * F)]).reshape(K, F, 2)
+    np.testing.assert_array_equal(got.reshape(-1, 2), SCENE2_MARKERS)
+    q, _, _ = shim_problem(shim, 3)
+    assert not bool(q.mkr_frame_xy)
