@@ -66,3 +66,11 @@ def test_b4_unknown_flat_xy_refused(gpu_ctx):
     assert e.value.code == abi.MMBA_ERR_UNSUPPORTED
     dag = S.config_options(prob, scene_graph_mode=abi.SCENE_GRAPH_MODE_MAYA_DAG)
     Solver(prob, dag, context=gpu_ctx).close()  # Maya-DAG mode has no B4
+
+
+def test_b4_rolling_shutter_refused(gpu_ctx):
+    prob = S.b4_scene()
+    prob.cam_rs_value = np.full(prob.num_cameras, 0.5)
+    with pytest.raises(MmbaError) as e:
+        Solver(prob, S.config_options(prob), context=gpu_ctx).close()
+    assert e.value.code == abi.MMBA_ERR_UNSUPPORTED

@@ -125,3 +125,15 @@ def test_mkr_frame_xy_matches_observations(oracle):
     x = np.asarray(p.x0) + 0.002
     np.testing.assert_array_equal(oracle.measure(p, mmsg(p), x)[0],
                                   oracle.measure(q, mmsg(q), x)[0])
+
+
+def test_rolling_shutter_with_remap_refused(oracle):
+    """The rolling shutter's scanline time comes from the observation's own
+    marker y while B4 compares another marker's: the combination is refused
+    (mmba.h ABI 8); in Maya-DAG mode (no remap) it is measured."""
+    p = S.b4_scene()
+    p.cam_rs_value = np.full(p.num_cameras, 0.5)
+    with pytest.raises(RuntimeError):
+        oracle.measure(p, mmsg(p), np.asarray(p.x0))
+    f, *_ = oracle.measure(p, dag(p), np.asarray(p.x0))
+    assert np.all(np.isfinite(f))
