@@ -16,11 +16,18 @@ leaving those outputs in HBM (mmba_plan_outputs) are timed beside it
 Jacobian evaluations) per second (SURVEY 8(d) metric definitions); LM
 iterations/s is reported beside it.
 
-Multi-GPU (torch.distributed.run, one process per GPU): weak scaling, the
-per-GPU shard is the C4 scene -- N GPUs solve ONE N x 500-frame scene
-(N x 50k bundles, N x 200k observations) frame-sharded over the GPUs, the
-library all-reducing over RCCL (xGMI); torch.distributed (gloo) only
-broadcasts the RCCL id and brackets the timed region.
+Multi-GPU: weak scaling, the per-GPU shard is the C4 scene -- N GPUs solve
+ONE N x 500-frame scene (N x 50k bundles, N x 200k observations)
+frame-sharded over the GPUs, the library exchanging over RCCL (xGMI).
+  - under torch.distributed.run (WORLD_SIZE = N): one process per GPU, each
+    rank a shard (mmba_comm_create_rccl); torch.distributed (gloo) only
+    broadcasts the RCCL id and brackets the timed region;
+  - run plainly with --gpus N: one process, the seam's single caller, over
+    mmba_context_create_multi(devices 0..N-1) (mmba.h ABI 9) -- the library
+    drives the N devices from its own threads (ncclCommInitAll).  With fewer
+    than N visible devices the N shards run on device 0 (the in-process
+    transport), labelled in `config.devices` and `parallelism`: a rehearsal
+    of the sharded path, not a multi-GPU measurement.
 
 The CPU baseline (rank 0, N = 1) is the oracle (oracle/refcpu.c, a
 cost-faithful restatement of the reference MM-Scene-Graph + cminpack path)
@@ -44,6 +51,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_MFMA_PEAK_TF = 78.6  # MI355X dense FP64 matrix rate (spec)
+FP64_VALU_PEAK_TF = 78.6  # MI355X FP64 vector rate (spec)
 BASE_FRAMES = {1: 120, 2: 500, 3: 500, 4: 240}
 
 
@@ -138,6 +146,8 @@ def broadcast_bytes(dist, data: bytes | None, n: int) -> bytes:
 # Kernels inside the K2 span (Plan::jac: span_begin .. span_end), i.e. the
 # launches whose HIP-event time is roofline.avg_ms.
 K2_REGEX = "k_jacobian|k_jac_ne|k_ne_|k_colnorms|k_jac_epilogue"
+VALU_F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+            "SQ_INSTS_VALU_TRANS_F64")
 
 
 def pmc_traffic(args):
@@ -166,10 +176,13 @@ def pmc_traffic(args):
     env = dict(os.environ, TMPDIR="/tmp")
     per = {}
     tmp = tempfile.mkdtemp(prefix="mmba_pmc_", dir="/tmp")
+    # one pass per counter group: FETCH_SIZE and WRITE_SIZE do not fit one
+    # pass; the four fp64 VALU instruction counters (SQ) fit one
+    passes = (("FETCH_SIZE",), ("WRITE_SIZE",), VALU_F64)
     try:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            out = os.path.join(tmp, ctr)
-            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr,
+        for group in passes:
+            out = os.path.join(tmp, group[0])
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", *group,
                    "--kernel-include-regex", K2_REGEX, "-d", out, "-o", "k2",
                    "--output-format", "csv", "--"] + base
             r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
@@ -177,18 +190,36 @@ def pmc_traffic(args):
             files = [os.path.join(dp, f) for dp, _, fs in os.walk(out) for f in fs
                      if f.endswith("counter_collection.csv")]
             if r.returncode != 0 or not files:
-                return None, "rocprofv3 --pmc %s pass failed (rc=%d)" % (ctr, r.returncode)
+                if group is VALU_F64:  # optional: the traffic stands without it
+                    per["valu_error"] = "rocprofv3 --pmc pass failed (rc=%d)" % r.returncode
+                    continue
+                return None, "rocprofv3 --pmc %s pass failed (rc=%d)" % (group[0], r.returncode)
             acc = {}
             for row in csv.DictReader(open(files[0])):
                 k = row["Kernel_Name"].split("(")[0]
-                acc.setdefault(k, []).append(float(row["Counter_Value"]))
-            per[ctr] = {k: sum(v) / len(v) for k, v in acc.items()}
+                c = row.get("Counter_Name", group[0])
+                acc.setdefault(c, {}).setdefault(k, []).append(float(row["Counter_Value"]))
+            for c, kv in acc.items():
+                per[c] = {k: sum(v) / len(v) for k, v in kv.items()}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     fetch = sum(per["FETCH_SIZE"].values()) * 1024.0
     write = sum(per["WRITE_SIZE"].values()) * 1024.0
+    valu = None
+    if all(c in per for c in VALU_F64):
+        # fp64 flops per K2 pass from the instruction counts (per wave, 64
+        # lanes): 2 per FMA, 1 per add / mul / transcendental
+        n = {c: sum(per[c].values()) for c in VALU_F64}
+        flops = 64.0 * (2.0 * n["SQ_INSTS_VALU_FMA_F64"] + n["SQ_INSTS_VALU_ADD_F64"] +
+                        n["SQ_INSTS_VALU_MUL_F64"] + n["SQ_INSTS_VALU_TRANS_F64"])
+        valu = {"flops_per_launch": flops, "instructions_per_launch": n,
+                "per_kernel": {c: per[c] for c in VALU_F64},
+                "note": "64 x (2 FMA + ADD + MUL + TRANS) fp64 VALU instructions, rocprofv3 "
+                        "--pmc, averaged per launch, summed over the K2 kernels"}
     detail = {"fetch_size_bytes_raw": fetch, "write_size_bytes": write,
-              "per_kernel_kib": per,
+              "valu_f64": valu, "valu_error": per.get("valu_error"),
+              "per_kernel_kib": {"FETCH_SIZE": per["FETCH_SIZE"],
+                                 "WRITE_SIZE": per["WRITE_SIZE"]},
               "correction": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE "
                             "halving, MI355X_MICROARCH.md HBM section), averaged per launch "
                             "over one solve, summed over the K2 kernels (%s)" % K2_REGEX}
@@ -351,15 +382,31 @@ def per_frame_line(args):
         sv.close()
 
 
+def parallelism(world, group, devices):
+    if world > 1:
+        return "frame-sharded x%d, one process per GPU (RCCL)" % world
+    if group and len(set(devices)) == len(devices):
+        return "frame-sharded x%d, one caller over %d GPUs (mmba_context_create_multi, " \
+               "RCCL)" % (len(devices), len(devices))
+    if group:
+        return ("frame-sharded x%d in-process on device %d (one-GPU rehearsal of the sharded "
+                "path through mmba_context_create_multi; not a multi-GPU measurement)"
+                % (len(devices), devices[0]))
+    return "single"
+
+
 def main():
     args = parse()
     if args.per_frame:
         return per_frame_line(args)
     world, rank, local, dist = dist_setup()
+    # one process over --gpus N devices (mmba_context_create_multi)
+    group = world == 1 and args.gpus > 1
+    nshards = args.gpus if group else world
     # PMC passes first, as child processes, before this process initialises
     # the GPU (rank 0 of a 1-GPU run only)
     traffic, traffic_detail = None, None
-    if world == 1 and not args.no_traffic:
+    if nshards == 1 and not args.no_traffic:
         traffic, traffic_detail = pmc_traffic(args)
     from mayamatchmovesolver_amd import synthetic as S
     from mayamatchmovesolver_amd.solver import Comm, Context, Solver, comm_unique_id
@@ -367,9 +414,9 @@ def main():
 
     frames = args.frames
     scale = args.scale
-    if world > 1:  # weak scaling: the per-GPU shard is the single-GPU scene
-        frames = (frames or BASE_FRAMES.get(args.config, 500)) * world
-        scale = scale * world
+    if nshards > 1:  # weak scaling: the per-GPU shard is the single-GPU scene
+        frames = (frames or BASE_FRAMES.get(args.config, 500)) * nshards
+        scale = scale * nshards
     t0 = time.perf_counter()
     kw = ({"lens_model": args.lens_model, "rolling_shutter": args.rolling_shutter}
           if args.config == 4 else {})
@@ -379,7 +426,15 @@ def main():
     progress("scene built (%.1f s)" % gen_s, every=0.0)
     # MMBA_BENCH_DEVICE: every rank on one device (RCCL path rehearsal on a
     # one-GPU box; the driver's multi-GPU runs leave it unset)
-    ctx = Context(int(os.environ.get("MMBA_BENCH_DEVICE", local)))
+    devices = [int(os.environ.get("MMBA_BENCH_DEVICE", local))]
+    if group:
+        from mayamatchmovesolver_amd.solver import device_count
+        visible = device_count()
+        devices = list(range(nshards)) if visible >= nshards else [0] * nshards
+        ctx = Context.multi(devices)
+        progress("%d shards on devices %s" % (nshards, devices), every=0.0)
+    else:
+        ctx = Context(devices[0])
     comm = None
     if world > 1:
         uid = broadcast_bytes(dist, comm_unique_id() if rank == 0 else None, 128)
@@ -387,6 +442,8 @@ def main():
     t0 = time.perf_counter()
     solver = Solver(prob, opt, context=ctx, comm=comm)
     upload_s = time.perf_counter() - t0
+    if group and solver.num_shards != nshards:
+        raise SystemExit("bench: the scene did not shard over %d devices" % nshards)
     progress("plan built (%.1f s)" % upload_s, every=0.0)
 
     # the caller's output buffers (errorList, ud->errorList,
@@ -454,6 +511,14 @@ def main():
                     "kernel": "k_jacobian+k_ne_* (FD Jacobian blocks + normal equations)",
                     "avg_ms": jac_ms, "bytes_per_launch": jac_bytes,
                     "launches": stats["jac_launches"], "traffic_pmc": traffic_detail}
+        valu = (traffic_detail or {}).get("valu_f64")
+        if valu and jac_ms > 0:
+            # the same K2 pass against the fp64 VALU peak: the FD Jacobian's
+            # re-projections are arithmetic (C5: the LDPK fixed-point inverse)
+            vt = valu["flops_per_launch"] / (jac_ms * 1e-3) / 1e12
+            roofline["valu_fp64"] = {"achieved_tflops": vt, "peak_tflops": FP64_VALU_PEAK_TF,
+                                     "frac": vt / FP64_VALU_PEAK_TF,
+                                     "flops_per_launch": valu["flops_per_launch"]}
         kind = stats.get("reduced_kind", 0)
         band_names = {1: "band: partitioned Cholesky chains", 2: "band: block cyclic reduction",
                       3: "band: parallel cyclic reduction (k_pcr_solve, one launch, x out)",
@@ -467,14 +532,32 @@ def main():
                 "note": "time per damped solve's factorisation (+ fused solve), HIP events"}
         if kind in (0, 3) and stats["chol_ms_avg"] > 0:
             # latency-bound (a dependent pivot chain per elimination level):
-            # the fp64 MFMA fraction is reported as measured, not as a target
-            tf = stats["chol_flops"] / (stats["chol_ms_avg"] * 1e-3) / 1e12
+            # the fp64 fraction is reported on the ALGORITHMIC flops of the
+            # band system (n_b w^2 + 4 n_b w, + the arrow), as measured, not
+            # as a target; what the solver executes is beside it
+            t_s = stats["chol_ms_avg"] * 1e-3
+            tf = stats["chol_flops_alg"] / t_s / 1e12
             chol.update({"bound": "latency (a dependent 24-step pivot chain and a neighbour "
                                   "hand-off per level)"
                          if kind == 0 else "latency (one wave per camera-frame block)",
                          "dominant": stats["chol_ms_avg"] > jac_ms,
                          "achieved_tflops": tf, "peak_tflops": FP64_MFMA_PEAK_TF,
-                         "frac": tf / FP64_MFMA_PEAK_TF, "flops": stats["chol_flops"]})
+                         "frac": tf / FP64_MFMA_PEAK_TF, "flops": stats["chol_flops_alg"],
+                         "flops_note": "algorithmic: n_b w^2 + 4 n_b w (+ arrow) for the band "
+                                       "system, per damped solve",
+                         "executed_flops": stats["chol_flops"],
+                         "executed_tflops": stats["chol_flops"] / t_s / 1e12})
+            if stats.get("band_levels", 0) > 0:
+                lv = stats["band_levels"]
+                # latency model: one launch whose levels run back to back --
+                # per level one K-step pivot chain, the products and one
+                # neighbour hand-off; the time per level is what a faster
+                # chain or hand-off would cut
+                chol["latency_model"] = {
+                    "levels": lv, "block": stats["band_block"],
+                    "us_per_level": 1e3 * stats["chol_ms_avg"] / (lv + 1),
+                    "model": "t = (levels + 1) x (K-step pivot chain + products + neighbour "
+                             "hand-off); the last term is the uncoupled block's solve"}
         if kind == 2 and stats["chol_ms_avg"] > 0:
             tf = stats["chol_flops"] / (stats["chol_ms_avg"] * 1e-3) / 1e12
             chol.update({"achieved_tflops": tf, "peak_tflops": FP64_MFMA_PEAK_TF,
@@ -491,7 +574,7 @@ def main():
                             stats["chol_flops"], "launches": stats["chol_launches"],
                             "k2_hbm": roofline}
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and nshards == 1:
             cpu = cpu_baseline(args.config, args.cpu_budget_s, ctx)
         r = last.result
         line = {
@@ -499,7 +582,7 @@ def main():
                       "final RMS reproj error",
             "value": value,
             "unit": "residuals/s",
-            "n_gpus": world,
+            "n_gpus": nshards,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * dt_max / args.steps,
@@ -513,8 +596,8 @@ def main():
                        "cameras": prob.num_cameras, "bundles": prob.num_bundles,
                        "markers": prob.num_markers, "observations": prob.num_obs,
                        "parameters": prob.num_params, "residuals": prob.num_residuals,
-                       "parallelism": "frame-sharded x%d (RCCL)" % world if world > 1
-                       else "single",
+                       "parallelism": parallelism(world, group, devices),
+                       **({"devices": devices} if group else {}),
                        "solver": "lmder fwd-FD delta=1e-4 tau=1 tol=1e-6",
                        **({"pinned_paths": pinned} if pinned else {})},
             "lm_iterations_per_s": lm_rate,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 8
+#define MMBA_ABI_VERSION 9
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -394,6 +394,25 @@ double mmba_param_internal_to_external(double value, double xmin, double xmax,
                                        double offset, double scale);
 
 int mmba_context_create(int device, mmba_context **out);
+/* ABI 9: one caller, several devices.  The reference calls solveFrames once,
+ * on Maya's main thread (adjust_base.cpp:1174-1183), so the multi-GPU
+ * fan-out stays inside the library (SURVEY 8(b) "Threading"): a context over
+ * `ndevices` devices (<= 8) -- one stream per device and the group's
+ * communicators, RCCL (ncclCommInitAll, in this process) when the devices are
+ * distinct, the in-process transport when one device is named ndevices times
+ * (a one-GPU box runs the sharded path this way; mixing is MMBA_ERR_INVALID).
+ * mmba_plan_create on it builds the frame-sharded plan of
+ * mmba_plan_create_sharded over every device, and the plan's entry points
+ * (solve, measure, reproject, outputs, set_attr_values, kernel_stats) run all
+ * shards from the calling thread: the library's own threads drive devices
+ * 1..N-1, the interrupt callback is polled on the calling thread only (its
+ * answer reaches every shard), and every shard writes its own parameters and
+ * observations straight into the caller's buffers.  A problem that does not
+ * shard is solved by the first device alone.  Destroy every plan before the
+ * context. */
+int mmba_context_create_multi(const int *devices, int ndevices, mmba_context **out);
+/* Devices of a context (1 for mmba_context_create). */
+int mmba_context_num_devices(const mmba_context *ctx);
 void mmba_context_destroy(mmba_context *ctx);
 /* Wait for all work on the context's device (bench timing brackets). */
 int mmba_context_synchronize(mmba_context *ctx);
@@ -435,13 +454,19 @@ int mmba_comm_create_rccl(mmba_context *ctx, int rank, int nranks,
 int mmba_comm_create_local(int nranks, mmba_comm **out);
 void mmba_comm_destroy(mmba_comm *comm);
 /* Like mmba_plan_create, for the shard `comm` stands for.  Collective: every
- * shard calls it (and then every solve / measure) together. */
+ * shard calls it (and then every solve / measure / outputs call) together,
+ * with the same pattern of NULL / non-NULL output pointers.  Each shard's
+ * results reach the others by one all-gather of its own rows (parameters,
+ * observations), not by an all-reduce of full vectors. */
 int mmba_plan_create_sharded(mmba_context *ctx, const mmba_problem *prob,
                              const mmba_options *opt, mmba_comm *comm, mmba_plan **out);
 /* The frame partition a sharded plan uses (host only, no device needed):
  * shard k owns frames [bounds[k], bounds[k+1]) (balanced by observation
  * count) and the bundles whose earliest observation lies in them
  * (bundle_owner, nullable).  obs_bundle[i] = bundle of observation i. */
+/* Shards a plan solves on: 1 unsharded (or replicated), N for a sharded
+ * plan or a plan over an N-device context (ABI 9). */
+int mmba_plan_num_shards(const mmba_plan *plan);
 int mmba_shard_layout(int32_t num_frames, int32_t num_obs, const int32_t *obs_frame,
                       const int32_t *obs_bundle, int32_t num_bundles, int32_t nranks,
                       int32_t *bounds_out /* nranks + 1 */, int32_t *bundle_owner_out);
@@ -589,6 +614,15 @@ typedef struct mmba_kernel_stats {
                                (sharded: interiors by parallel cyclic
                                reduction, separator system all-reduced),
                                5 block diagonal + arrow                    */
+    /* ---- ABI 9 ---- */
+    int32_t band_levels;    /* parallel / block cyclic reduction: elimination
+                               levels of one factorisation (0 otherwise)   */
+    int32_t band_block;     /* ... and their block edge K                  */
+    double chol_flops_alg;  /* algorithmic flops of one damped solve of the
+                               reduced system: band n_b w^2 + 4 n_b w (+ the
+                               arrow's n_b nG (2w + nG) + nG^3/3); block
+                               diagonal sum pc^3/3 + 4 pc; dense n^3/3 + 4n^2
+                               -- chol_flops is what the solver executes   */
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);

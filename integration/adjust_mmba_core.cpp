@@ -518,7 +518,13 @@ bool Shim::ready() {
         no_device_ = true;
         return false;
     }
-    if (mmba_context_create(0, &ctx_) != MMBA_OK) {
+    // every visible GPU (<= 8) behind this one caller: the library shards a
+    // solve over them itself (mmba_context_create_multi, ABI 9), Maya's main
+    // thread stays the only caller (adjust_base.cpp:1174-1183)
+    int devs[8];
+    const int nd = std::min(mmba_device_count(), 8);
+    for (int d = 0; d < nd; ++d) devs[d] = d;
+    if (mmba_context_create_multi(devs, nd, &ctx_) != MMBA_OK) {
         why_ = std::string("no gfx950 device: ") + mmba_last_error();
         no_device_ = true;
         ctx_ = nullptr;

@@ -53,6 +53,13 @@ def lib():
             f.argtypes = [C.c_double] * 5
         L.mmba_context_create.restype = C.c_int
         L.mmba_context_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.mmba_context_create_multi.restype = C.c_int
+        L.mmba_context_create_multi.argtypes = [C.POINTER(C.c_int), C.c_int,
+                                                C.POINTER(C.c_void_p)]
+        L.mmba_context_num_devices.restype = C.c_int
+        L.mmba_context_num_devices.argtypes = [C.c_void_p]
+        L.mmba_plan_num_shards.restype = C.c_int
+        L.mmba_plan_num_shards.argtypes = [C.c_void_p]
         L.mmba_context_synchronize.restype = C.c_int
         L.mmba_context_synchronize.argtypes = [C.c_void_p]
         L.mmba_host_alloc.restype = C.c_int

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # mmba_debug_set_path keys (test hook: pin a plan-builder choice)
 PATH_PCR = 1
@@ -220,6 +220,9 @@ class MmbaKernelStats(C.Structure):
         ("shards_replicated", C.c_int32),
         ("spec_replays", C.c_int32),
         ("band_solver", C.c_int32),
+        ("band_levels", C.c_int32),
+        ("band_block", C.c_int32),
+        ("chol_flops_alg", C.c_double),
     ]
 
     def as_dict(self):
@@ -236,6 +239,9 @@ EXPORTED_SYMBOLS = [
     "mmba_param_external_to_internal",
     "mmba_param_internal_to_external",
     "mmba_context_create",
+    "mmba_context_create_multi",
+    "mmba_context_num_devices",
+    "mmba_plan_num_shards",
     "mmba_context_destroy",
     "mmba_context_synchronize",
     "mmba_host_alloc",

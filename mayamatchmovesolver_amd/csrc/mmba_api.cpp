@@ -158,12 +158,25 @@ void mmba_host_free(void *p) {
 
 int mmba_context_synchronize(mmba_context *ctx) {
     if (!ctx) return MMBA_ERR_INVALID;
+    if (!ctx->shards.empty()) {
+        for (mmba_context *c : ctx->shards) {
+            const int rc = mmba_context_synchronize(c);
+            if (rc != MMBA_OK) return rc;
+        }
+        return MMBA_OK;
+    }
     if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;
     return hipDeviceSynchronize() == hipSuccess ? MMBA_OK : MMBA_ERR_DEVICE;
 }
 
 void mmba_context_destroy(mmba_context *ctx) {
     if (!ctx) return;
+    if (!ctx->shards.empty() || !ctx->comms.empty()) {  // multi-device (mmba_group.cpp)
+        for (Comm *c : ctx->comms) delete c;
+        for (mmba_context *c : ctx->shards) mmba_context_destroy(c);
+        delete ctx;
+        return;
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     pcr_note_context(ctx->device, -1);
     delete ctx;
@@ -205,6 +218,15 @@ int mmba_plan_create_sharded(mmba_context *ctx, const mmba_problem *prob,
                              const mmba_options *opt, mmba_comm *comm, mmba_plan **out) {
     if (!ctx || !prob || !opt || !out) return MMBA_ERR_INVALID;
     *out = nullptr;
+    if (!ctx->shards.empty()) {  // one caller, several devices (ABI 9)
+        if (comm) {
+            set_error("a multi-device context brings its own communicators");
+            return MMBA_ERR_INVALID;
+        }
+        if (ctx->shards.size() == 1) return mmba_plan_create_sharded(ctx->shards[0], prob, opt,
+                                                                     nullptr, out);
+        MMBA_GUARD({ return group_plan_create(ctx, prob, opt, out); })
+    }
     Comm *c = reinterpret_cast<Comm *>(comm);
     auto make = [&](bool replicate, mmba_plan **pp) -> int {
         mmba_plan *p = new mmba_plan();
@@ -258,6 +280,8 @@ void mmba_plan_destroy(mmba_plan *plan) { delete plan; }
 int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out, double *err_user_out,
                       double *err_dist_out, double *avg_min_max_out) {
     if (!plan) return MMBA_ERR_INVALID;
+    if (plan->group)
+        return group_plan_measure(plan, x, fvec_out, err_user_out, err_dist_out, avg_min_max_out);
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
         plan->impl.outputs_ready = false;
@@ -271,6 +295,7 @@ int mmba_plan_measure(mmba_plan *plan, const double *x, double *fvec_out, double
 int mmba_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
                         double *marker_xy_out) {
     if (!plan) return MMBA_ERR_INVALID;
+    if (plan->group) return group_plan_reproject(plan, x, point_xy_out, marker_xy_out);
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
         plan->impl.outputs_ready = false;
@@ -280,6 +305,7 @@ int mmba_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
 
 int mmba_plan_jacobian(mmba_plan *plan, const double *x, double *fjac) {
     if (!plan || !x || !fjac) return MMBA_ERR_INVALID;
+    if (plan->group) return group_plan_jacobian(plan, x, fjac);
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
         plan->impl.outputs_ready = false;
@@ -291,6 +317,9 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *
                     double *err_dist_out, mmba_result *res, const mmba_callbacks *cb,
                     mmba_trace *trace) {
     if (!plan || !x_inout) return MMBA_ERR_INVALID;
+    if (plan->group)
+        return group_plan_solve(plan, x_inout, fvec_out, err_user_out, err_dist_out, res, cb,
+                                trace);
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
         plan->impl.outputs_ready = false;
@@ -303,6 +332,7 @@ int mmba_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *
 
 int mmba_plan_outputs(mmba_plan *plan, double *fvec_out, double *err_user_out,
                       double *err_dist_out) {
+    if (plan && plan->group) return group_plan_outputs(plan, fvec_out, err_user_out, err_dist_out);
     if (!plan || !plan->impl.outputs_ready) return MMBA_ERR_INVALID;
     MMBA_GUARD({
         Plan &p = plan->impl;
@@ -315,6 +345,7 @@ int mmba_plan_outputs(mmba_plan *plan, double *fvec_out, double *err_user_out,
 
 int mmba_plan_set_attr_values(mmba_plan *plan, const double *attr_values) {
     if (!plan || !attr_values) return MMBA_ERR_INVALID;
+    if (plan->group) return group_plan_set_attr_values(plan, attr_values);
     MMBA_GUARD({
         Plan &p = plan->impl;
         MMBA_HIP(hipSetDevice(p.ctx->device));
@@ -329,6 +360,7 @@ int mmba_plan_set_attr_values(mmba_plan *plan, const double *attr_values) {
 int mmba_plan_solve_per_frame(mmba_plan *plan, double *x_inout, mmba_result *results,
                               const mmba_callbacks *cb) {
     if (!plan || !x_inout || !results) return MMBA_ERR_INVALID;
+    if (plan->group) return group_plan_solve_per_frame(plan, x_inout, results, cb);
     MMBA_GUARD({
         MMBA_HIP(hipSetDevice(plan->impl.ctx->device));
         plan->impl.outputs_ready = false;
@@ -349,6 +381,7 @@ int mmba_solve(mmba_context *ctx, const mmba_problem *prob, const mmba_options *
 
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats *out) {
     if (!plan) return MMBA_ERR_INVALID;
+    if (plan->group) return group_plan_kernel_stats(plan, enable_timing, out);
     Plan &p = plan->impl;
     if (out) {
         std::memset(out, 0, sizeof(*out));
@@ -409,6 +442,30 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
             out->chol_flops = (double)(p.nR - p.nG) * p.bw * p.bw;  // band Cholesky
         } else {
             out->chol_flops = (double)p.nRpad * p.nRpad * p.nRpad / 3.0;
+        }
+        // algorithmic flops of one damped solve (factor + both triangular
+        // solves) of the structure itself, whatever the solver does
+        {
+            const double G = p.nG, nb = p.nR - p.nG;
+            const double arrow = nb * G * (2.0 * p.bw + G) + G * G * G / 3.0 + 4.0 * G * G;
+            if (p.band && p.bs.use_bd) {
+                const double pc = p.ncf ? (double)p.nCF / p.ncf : 0.;
+                out->chol_flops_alg = (double)p.ncf * (pc * pc * pc / 3.0 + 4.0 * pc * pc) +
+                                      nb * G * (2.0 * pc + G) + G * G * G / 3.0 + 4.0 * G * G;
+            } else if (p.band) {
+                out->chol_flops_alg = nb * p.bw * p.bw + 4.0 * nb * p.bw + arrow;
+            } else {
+                const double N = p.nR;
+                out->chol_flops_alg = N * N * N / 3.0 + 4.0 * N * N;
+            }
+            if (p.band && p.bs.use_pcr && !p.bs.df_off) {
+                out->band_levels = p.bs.pcr.nlev;
+                out->band_block = p.bs.pcr.K;
+            } else if (p.band && p.bs.use_bcr) {
+                out->band_levels = 0;
+                for (int a = p.bs.bcr.nblk; a > 1; a = (a + 1) / 2) ++out->band_levels;
+                out->band_block = p.bs.bcr.K;
+            }
         }
     }
     p.timing = enable_timing != 0;

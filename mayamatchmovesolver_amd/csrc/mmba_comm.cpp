@@ -27,19 +27,41 @@ namespace mmba {
 // ---- RCCL ----
 struct RcclComm : Comm {
     ncclComm_t c = nullptr;
+    bool aborted = false;
     ~RcclComm() override {
-        if (c) (void)ncclCommDestroy(c);
+        if (c && !aborted) (void)ncclCommDestroy(c);
     }
-    void allreduce(double *buf, size_t count, ReduceOp op, hipStream_t s) override {
-        if (count == 0) return;
-        const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclDouble,
-                                             op == ReduceOp::Max ? ncclMax : ncclSum, c, s);
+    void abort() override {
+        if (c && !aborted) (void)ncclCommAbort(c);
+        aborted = true;
+    }
+    void check(ncclResult_t r, const char *what) {
         if (r != ncclSuccess) {
-            set_error(std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+            set_error(std::string(what) + ": " + ncclGetErrorString(r));
             throw CommError();
         }
     }
+    void allgather(const double *send, double *recv, size_t count, hipStream_t s) override {
+        if (count == 0) return;
+        if (aborted) throw CommError();
+        check(ncclAllGather(send, recv, count, ncclDouble, c, s), "ncclAllGather");
+    }
+    void allreduce(double *buf, size_t count, ReduceOp op, hipStream_t s) override {
+        if (count == 0) return;
+        if (aborted) throw CommError();
+        check(ncclAllReduce(buf, buf, count, ncclDouble, op == ReduceOp::Max ? ncclMax : ncclSum,
+                            c, s),
+              "ncclAllReduce");
+    }
 };
+
+Comm *make_rccl_comm(ncclComm_t c, int rank, int nranks) {
+    auto *r = new RcclComm();
+    r->c = c;
+    r->rank = rank;
+    r->nranks = nranks;
+    return r;
+}
 
 // ---- in-process group ----
 constexpr int LOCAL_MAX = 8;
@@ -51,17 +73,29 @@ struct LocalGroup {
     int arrived = 0;
     long gen = 0;
     bool ring = false;
+    bool aborted = false;
     double *bufs[LOCAL_MAX] = {};
+    const double *sends[LOCAL_MAX] = {};
     void barrier() {
         std::unique_lock<std::mutex> lk(m);
+        if (aborted) throw CommError();
         const long g = gen;
         if (++arrived == n) {
             arrived = 0;
             ++gen;
             cv.notify_all();
         } else {
-            cv.wait(lk, [&] { return gen != g; });
+            cv.wait(lk, [&] { return gen != g || aborted; });
+            if (gen == g) {
+                set_error("in-process shard group aborted (another shard failed)");
+                throw CommError();
+            }
         }
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
     }
 };
 
@@ -109,6 +143,18 @@ struct LocalComm : Comm {
         g->barrier();  // nobody reads a shard's buffer any more
         MMBA_HIP(hipMemcpyAsync(buf, tmp, count * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
+    void allgather(const double *send, double *recv, size_t count, hipStream_t s) override {
+        if (count == 0) return;
+        MMBA_HIP(hipStreamSynchronize(s));
+        g->sends[rank] = send;
+        g->barrier();  // every shard's send buffer is final
+        for (int k = 0; k < g->n; ++k)
+            MMBA_HIP(hipMemcpyAsync(recv + (size_t)k * count, g->sends[k], count * sizeof(double),
+                                    hipMemcpyDeviceToDevice, s));
+        MMBA_HIP(hipStreamSynchronize(s));
+        g->barrier();  // nobody reads a shard's send buffer any more
+    }
+    void abort() override { g->abort(); }
 };
 
 }  // namespace mmba
@@ -135,6 +181,10 @@ int mmba_comm_create_rccl(mmba_context *ctx, int rank, int nranks,
     if (!ctx || !unique_id || !out || nranks < 1 || rank < 0 || rank >= nranks)
         return MMBA_ERR_INVALID;
     *out = nullptr;
+    if (!ctx->shards.empty()) {
+        set_error("a multi-device context brings its own communicators");
+        return MMBA_ERR_INVALID;
+    }
     if (hipSetDevice(ctx->device) != hipSuccess) return MMBA_ERR_DEVICE;
     auto *c = new RcclComm();
     c->rank = rank;

@@ -43,6 +43,12 @@ struct Comm {
     int rank = 0, nranks = 1;
     virtual ~Comm() {}
     virtual void allreduce(double *buf, size_t count, ReduceOp op, hipStream_t s) = 0;
+    // recv[k * count .. (k + 1) * count) = rank k's send[0 .. count) on every
+    // rank (send and recv distinct device buffers)
+    virtual void allgather(const double *send, double *recv, size_t count, hipStream_t s) = 0;
+    // a shard failed outside a collective: the others' pending and future
+    // collectives fail (CommError) instead of waiting forever
+    virtual void abort() {}
 };
 
 // Band + arrow layout of the reduced system (narrow structures): rows of

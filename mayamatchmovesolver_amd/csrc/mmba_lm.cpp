@@ -159,6 +159,14 @@ void Plan::read_slots(int lo, int hi) {
     }
 }
 
+// Everything enqueued so far done: poll an event (a blocking stream
+// synchronisation's wake-up costs tens of microseconds).
+void Plan::stream_wait() {
+    if (!ev_sync) MMBA_HIP(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
+    MMBA_HIP(hipEventRecord(ev_sync, s));
+    wait_event();
+}
+
 double Plan::read_scalar(int slot) {
     read_slots(slot, slot);
     return h_scalar[slot];
@@ -333,6 +341,9 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     }
     const bool k2_fused = !central && jac_ne_fusable(P, jac_ncv) && !k2_split;
     const bool pre_done = pre_jac_pending && pre_jac_x == dx && k2_fused && fuse;
+    // sharded: g holds only this shard's terms -- zeroed BEFORE the fused
+    // pass, which writes the camera-frame part of g itself
+    if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     pre_jac_pending = false;
     if (pre_done) {
         // k_jac_ne_u ran ahead at this x (its gate was open: the device took
@@ -349,7 +360,6 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
                     central ? d_stepB : nullptr, lmder ? 1 : 0, d_Jrow, d_eu + 2 * (size_t)M,
                     n - 1);
-    if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
               d_glob_partial, glob_chunk, epi, k2_fused);
     launch_rows_ne(s, P, d_Jrow, d_f + 2 * (size_t)M, d_p_own, d_Acc, d_Abb, d_Agg, d_g);
@@ -620,10 +630,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             // solved by pcr_solve
         } else if (band) {
             band_backward(s, bs, d_yR, d_xR);
-            if (nranks > 1 && !bs.use_bcr) {  // every shard needs its halo camera-frame rows
-                launch_keep_rows(s, d_xR, Ra, Rb, nR - nG, nR, rank == 0);
-                allreduce(d_xR, nR);
-            }
+            // every shard needs its halo camera-frame rows: each shard's own
+            // rows [Ra, Rb) (and shard 0's arrow rows) all-gathered
+            if (nranks > 1 && !bs.use_bcr) gather_step_rows();
         } else if (dense) {
             ds.backward(s, d_yR, d_xR);
         } else if (narrow) {
@@ -766,10 +775,23 @@ static void lmpar_first_enqueue(Plan &pl, bool defer = false, bool by_trial = fa
     pl.solve_damped_enqueue(0.0, Plan::SL_DNORM, defer, by_trial);
 }
 
+// A timed-out wait in a parallel-cyclic-reduction right-hand-side pass (the
+// Newton term's k_pcr_rhs / k_pcr_rhs_mc) leaves NaN partials instead of
+// stale ones: the plan switches to the band chains for good (the flag bit
+// is cleared) and lmpar starts over from its first, undamped solve.
+struct PcrRestart {};
+static void check_newton(Plan &pl) {
+    if (std::isfinite(pl.h_scalar[Plan::SL_NEWT_R])) return;
+    if (!(pl.band && (pl.bs.use_pcr || pl.bs.pcr_int)) || pl.bs.df_off) return;
+    pl.bs.df_off = true;
+    launch_flag_to_scalar(pl.s, pl.d_fail, pl.d_scalar + Plan::SL_FAIL);
+    throw PcrRestart{};
+}
+
 // A timed-out dataflow wait in the undamped solve (flag bit 2) switches the
 // plan to the per-level launches and solves again; `pre` is cleared then, so
 // the caller does not take the speculative trial built on the failed solve.
-static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *undamped) {
+static double lmpar_ne_once(Plan &pl, double delta, double *par, bool &pre, bool *undamped) {
     const double p1 = .1, p001 = .001;
     const double dwarf = DBL_MIN;
     double *h = pl.h_scalar;
@@ -800,6 +822,7 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *und
                      pl.d_scalar + Plan::SL_GDIV, pl.d_p_own, pl.d_ticket);
     pl.allreduce(pl.d_scalar + Plan::SL_GDIV, 1);
     pl.read_slots(Plan::SL_NEWT_B, Plan::SL_GDIV);
+    if (newton0) check_newton(pl);
     if (newton0) {
         const double temp = std::sqrt(h[Plan::SL_NEWT_B] + h[Plan::SL_NEWT_R]);
         parl = fp / delta / temp / temp;
@@ -846,6 +869,7 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *und
             break;
         pl.newton_enqueue(dxnorm);
         pl.read_slots(Plan::SL_NEWT_B, Plan::SL_NEWT_R);
+        check_newton(pl);
         temp = std::sqrt(h[Plan::SL_NEWT_B] + h[Plan::SL_NEWT_R]);
         const double parc = fp / delta / temp / temp;
         if (fp > 0.) parl = std::max(parl, *par);
@@ -856,11 +880,27 @@ static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *und
     return dxnorm;
 }
 
+static double lmpar_ne(Plan &pl, double delta, double *par, bool &pre, bool *undamped) {
+    const double par0 = *par;
+    for (;;) {
+        try {
+            return lmpar_ne_once(pl, delta, par, pre, undamped);
+        } catch (const PcrRestart &) {
+            *par = par0;
+            pre = false;
+        }
+    }
+}
+
 // Device order -> reference (errorToMarkerList) order on the host.  Sharded:
 // every shard scatters the observations it owns and the shards' buffers are
 // summed, so every shard returns the full vectors.
 void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
-                              double *f_out, double *eu_out, double *ed_out) {
+                              double *f_out, double *eu_out, double *ed_out, bool sync) {
+    if (nranks > 1) {  // each shard's own observations (mmba_group.cpp)
+        handback_sharded(nullptr, nullptr, f_out, eu_out, ed_out, d_f2, d_eu2, d_ed1);
+        return;
+    }
     double *tf = d_gather, *te = d_gather + mg, *td = d_gather + 2 * (size_t)mg;
     const size_t total = 2 * (size_t)mg + Mg;
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_gather, 0, sizeof(double) * total, s));
@@ -880,16 +920,14 @@ void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const dou
         MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
     if (ed_out)
         MMBA_HIP(hipMemcpyAsync(ed_out, td, sizeof(double) * Mg, hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    if (sync) stream_wait();
 }
 
 // Parameter vector of the solve on the host (sharded: owners' entries summed).
 void Plan::download_params(const double *dx, double *x_out) {
-    if (nranks > 1) {
-        double *tx = d_gather + 2 * (size_t)mg + Mg;
-        launch_keep_mask(s, dx, d_p_own, n, tx);
-        allreduce(tx, n);
-        dx = tx;
+    if (nranks > 1) {  // each shard's own parameters (mmba_group.cpp)
+        handback_sharded(dx, x_out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+        return;
     }
     MMBA_HIP(hipMemcpyAsync(x_out, dx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipStreamSynchronize(s));
@@ -935,6 +973,17 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
         launch_rows_eval(s, P, d_f + 2 * (size_t)M, d_eu + 2 * (size_t)M, d_partial,
                          (M + 255) / 256);
         launch_residual(s, plug_problem(), d_recs, d_f, d_eu, d_ed, d_partial);
+    }
+    if (nranks > 1) {
+        // sharded: the statistics all-reduced, the outputs handed back by
+        // each shard's own observations
+        double st[3];
+        error_stats_device(d_ed, &st[0], &st[1], &st[2]);
+        if (stats) std::memcpy(stats, st, sizeof(st));
+        if (fvec_out || eu_out || ed_out)
+            download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out);
+        collect_spans();
+        return MMBA_OK;
     }
     std::vector<double> ed(Mg);
     download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed.data());
@@ -1175,7 +1224,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
     // (adjust_solveFunc.cpp:551-571)
     nfev = 1;
     func_evals = 1;
-    if (polls && poll_interrupt()) {
+    if (polls && poll_agree()) {
         interrupted = true;
         info = -1;
         goto TERMINATE;
@@ -1195,12 +1244,15 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                 // the Jacobian request: lmder polls at solveFunc entry and before
                 // every FD column (adjust_solveFunc.cpp:321-325); every fdjac2
                 // column of lmdif is a solveFunc call (counted, then polled)
+                // (a group shard takes shard 0's answer: poll_agree_index)
                 int k = -1;
-                if (!lmdif && poll_interrupt()) k = 0;
-                for (int j = 0; j < n && k < 0; ++j) {
-                    if (lmdif) ++jac_evals;
-                    if (poll_interrupt()) k = j;
+                if (!pshare || rank == 0) {
+                    if (!lmdif && poll_interrupt()) k = 0;
+                    for (int j = 0; j < n && k < 0; ++j)
+                        if (poll_interrupt()) k = j;
                 }
+                k = poll_agree_index(k);
+                if (lmdif) jac_evals += k >= 0 ? k + 1 : n;
                 if (k >= 0) {
                     interrupted = true;
                     info = -1;
@@ -1302,7 +1354,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                 // the trial point's solveFunc call: counted, then polled
                 ++nfev;
                 ++func_evals;
-                if (polls && poll_interrupt()) {
+                if (polls && poll_agree()) {
                     interrupted = true;
                     info = -1;
                     goto TERMINATE;
@@ -1423,8 +1475,13 @@ TERMINATE:
                      d_scalar + SL_RMS, P.obs_own);
         allreduce(d_scalar + SL_RMS, 1);
         const bool staged = nranks == 1 && n > 0;
-        if (staged)
+        const bool outs = fvec_out || eu_out || ed_out;
+        if (staged) {
+            // x, the reordered outputs and the slots: every copy enqueued, then
+            // one wait (read_slots' event follows them on the stream)
             MMBA_HIP(hipMemcpyAsync(h_xstage, d_x, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+            if (outs) download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out, false);
+        }
         read_slots(SL_RMS, SL_IEMAX);  // also x0's ||f|| and the initial measurement's
         if (f0_pending) {  // stopped between x0's evaluation and the first decision
             fnorm = std::sqrt(h_scalar[SL_F0]);
@@ -1441,12 +1498,18 @@ TERMINATE:
         r.error_max = h_scalar[SL_EMAX];
         r.error_is_better = opt.accept_only_better ? (avg <= init_avg) : 1;
         r.error_rms = std::sqrt(h_scalar[SL_RMS] / Mg);
-        if (staged)
+        if (staged) {
             std::memcpy(x_inout, h_xstage, sizeof(double) * n);
-        else
+        } else if (nranks > 1) {
+            // x and the outputs in one hand-back (a group shard writes its own
+            // parameters into the caller's x, group_x_out)
+            handback_sharded(d_x, host_gather ? group_x_out : x_inout, fvec_out, eu_out, ed_out,
+                             d_f, d_eu, d_ed);
+        } else {
             download_params(d_x, x_inout);
-        if (fvec_out || eu_out || ed_out)
-            download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out);
+            if (fvec_out || eu_out || ed_out)
+                download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out);
+        }
     }
     collect_spans();
     r.num_trace = trace ? trace->count : 0;

@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
     const int R = j * K + lane;
     const double w0 = (lane < K && R < nb) ? w[R] : 0.;
     double r = w0;
-    const int L = P.flev[j];
+    const int L = min(max(P.flev[j], 0), P.nlev);  // (flev is zeroed at plan build)
     int s = 1;
     for (int lvl = 0; lvl < L; ++lvl, s *= 2) {
         const bool hp = j - s >= 0, hq = j + s < nblk;
@@ -380,7 +380,12 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
         const bool ok = pcr_wait(P.rflag + (size_t)lvl * nblk, hp ? j - s : -1, hq ? j + s : -1,
                                  epoch);
         if (!ok) {
-            if (lane == 0) atomicOr(fail, 2);
+            // a timed-out wait: the partial is NaN, so the Newton term that
+            // sums it cannot pass for a number (lmpar_ne restarts on it)
+            if (lane == 0) {
+                atomicOr(fail, 2);
+                part[j] = __builtin_nan("");
+            }
             return;
         }
         if (lane < K) {  // r -= Q_p^T rho_p + P_q^T rho_q
@@ -438,7 +443,7 @@ __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__re
         const int i = q / nc, c = q % nc, row = j * K + i;
         sr[i * NS + c] = row < nb ? R[(size_t)c * ldr + row] : 0.;
     }
-    const int L = P.flev[j];
+    const int L = min(max(P.flev[j], 0), P.nlev);
     const size_t pst = (size_t)2 * K * PCR_NCMAX;  // doubles of one (level, block) publication
     int s = 1;
     for (int lvl = 0;; ++lvl, s *= 2) {
@@ -490,7 +495,12 @@ __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__re
         }
         __syncthreads();
         if (!ok_s) {
+            // timed out: this block's rows of Z are NaN (never a stale number)
             if (tid == 0) atomicOr(fail, 2);
+            for (int q = tid; q < ne; q += 256) {
+                const int i = q / nc, c = q % nc, row = j * K + i;
+                if (row < nb) Z[(size_t)c * ldz + row] = __builtin_nan("");
+            }
             return;
         }
         // R -= Q_p^T rho_p + P_q^T rho_q

@@ -230,6 +230,7 @@ extern "C" int mmba_solve_per_frame(mmba_context *ctx, const mmba_problem *prob,
                                     const mmba_callbacks *cb) {
     if (!ctx || !prob || !opt || !x_inout || !results || prob->num_frames <= 0)
         return MMBA_ERR_INVALID;
+    if (!ctx->shards.empty()) ctx = ctx->shards[0];  // a multi-device context: its first device
     try {
         const int F = prob->num_frames;
         std::vector<FrameProblem> fr(F);

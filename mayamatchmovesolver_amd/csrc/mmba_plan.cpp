@@ -84,6 +84,7 @@ Plan::~Plan() {
     if (h_bflag) (void)hipHostFree(h_bflag);
     if (h_xstage) (void)hipHostFree(h_xstage);
     if (h_seq) (void)hipHostFree(h_seq);
+    if (h_pack) (void)hipHostFree(h_pack);
 }
 
 static void require(bool c, const char *what) {
@@ -707,6 +708,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     Rb_all.assign(1, nCF);
     std::vector<int> local;  // global observation indices on this shard
     std::vector<int> cf_own(ncf, 1);
+    // sharded: every global observation's and camera-frame's owning shard
+    // (the hand-back lists, setup_handback)
+    std::vector<int> obs_rank_g, cf_rank;
     if (nranks > 1) {
         if (!band || bw > WBAND_PART)
             throw Unsupported{"sharded solve needs a narrow camera-frame band (w <= 40)"};
@@ -733,6 +737,13 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             const int f = pr->obs_frame[i];
             obs_own_g[i] = (f >= fa && f < fb) ? 1 : 0;
         }
+        std::vector<int> frame_rank(F, nranks - 1);
+        for (int k = 0; k < nranks; ++k)
+            for (int f = bf[k]; f < bf[k + 1]; ++f) frame_rank[f] = k;
+        obs_rank_g.resize((size_t)Mg + n);
+        for (int i = 0; i < Mg; ++i) obs_rank_g[i] = frame_rank[pr->obs_frame[i]];
+        cf_rank.resize(ncf);
+        for (int cf = 0; cf < ncf; ++cf) cf_rank[cf] = frame_rank[cf_frame[cf]];
         bnd_owner = bnd_owner_all;
         std::vector<char> bnd_here(nB, 0);
         for (int i = 0; i < Mg; ++i)
@@ -1404,6 +1415,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             else if (p_class[q] == PC_B) p_own[q] = bown[p_blk[q]];
             else p_own[q] = rank == 0 ? 1 : 0;
         }
+        // every parameter's owner, the same rule for every rank
+        for (int q = 0; q < n; ++q)
+            obs_rank_g[(size_t)Mg + q] = p_class[q] == PC_CF  ? cf_rank[p_blk[q]]
+                                         : p_class[q] == PC_B ? bnd_owner[p_blk[q]]
+                                                              : 0;
         D.obs_own = upload(d_own);
         D.cf_own = upload(cf_own);
         D.bnd_own = upload(bown);
@@ -1530,6 +1546,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     // gnorm of rank 0 .. nranks-1] all-reduced together (Plan::jac)
     d_Agg = dalloc<double>(NGMAX * NGMAX + NGMAX + 2 + std::max(nranks, 1));
     d_gather = dalloc<double>((size_t)2 * mg + Mg + n);
+    if (nranks > 1) setup_handback(obs_rank_g);
     d_glob_partial = dalloc<double>((size_t)((M + glob_chunk - 1) / glob_chunk) * (NGMAX * NGMAX + NGMAX));
     d_Lb = dalloc<double>((size_t)nB * 9);
     d_tb = dalloc<double>((size_t)nB * 3);
@@ -1827,6 +1844,7 @@ void Plan::setup_band(int Pforce) {
                     MMBA_HIP(hipMemsetAsync(Q.fflag, 0, sizeof(int) * std::max<size_t>(1, (size_t)L * Q.nblk), s));
                     MMBA_HIP(hipMemsetAsync(Q.rflag, 0, sizeof(int) * std::max<size_t>(1, (size_t)L * Q.nblk), s));
                     Q.flev = dalloc<int>(Q.nblk);
+                    MMBA_HIP(hipMemsetAsync(Q.flev, 0, sizeof(int) * Q.nblk, s));
                     bs.use_pcr = true;
                 }
             }
@@ -1967,6 +1985,7 @@ void Plan::setup_band(int Pforce) {
         MMBA_HIP(hipMemsetAsync(Q.rflag, 0, sizeof(int) * nl, s));
         MMBA_HIP(hipMemsetAsync(Q.mflag, 0, sizeof(int) * nl, s));
         Q.flev = dalloc<int>(Q.nblk);
+                    MMBA_HIP(hipMemsetAsync(Q.flev, 0, sizeof(int) * Q.nblk, s));
         bs.XA = dalloc<double>((size_t)std::max(hp.na, 1) * ast);
         bs.izero = dalloc<double>(ast);
         bs.ix = dalloc<double>(ast);
@@ -1979,8 +1998,11 @@ void Plan::setup_band(int Pforce) {
 // reduction, only the separator system (the last w rows of every shard but
 // the last, with the shards' Schur terms) is all-reduced and solved on every
 // shard.  Needs no arrow, w <= 23 and every shard's interior resident on the
-// device; every shard decides the same from the shared partition.
-bool Plan::sep_form(int w) const {
+// device; every shard decides the same from the shared partition and the
+// smallest residency bound of the shards' devices (all-reduced once: a
+// shard on a device with fewer CUs must not take another path than the
+// rest, whose collectives would then differ).
+bool Plan::sep_form(int w) {
     if (nranks <= 1 || nG != 0 || w > 23 || w <= 0) return false;
     if (path_choice(MMBA_PATH_SHARD_SEP) == 0 || path_choice(MMBA_PATH_SHARD_BCR) == 0) return false;
     const int K = std::max(8, (w + 7) / 8 * 8);
@@ -1990,7 +2012,16 @@ bool Plan::sep_form(int w) const {
         if (len < K) return false;
         most = std::max(most, (len + K - 1) / K);
     }
-    return most <= pcr_max_resident(K);
+    if (sep_resident_K != K) {
+        double v = -(double)pcr_max_resident(K), *d = dalloc<double>(1);
+        MMBA_HIP(hipMemcpyAsync(d, &v, sizeof(double), hipMemcpyHostToDevice, s));
+        allreduce(d, 1, ReduceOp::Max);
+        MMBA_HIP(hipMemcpyAsync(&v, d, sizeof(double), hipMemcpyDeviceToHost, s));
+        MMBA_HIP(hipStreamSynchronize(s));
+        sep_resident = (int)-v;
+        sep_resident_K = K;
+    }
+    return most <= sep_resident;
 }
 
 }  // namespace mmba

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -14,6 +15,11 @@
 struct mmba_context {
     int device = 0;
     hipStream_t stream = nullptr;
+    // ABI 9, mmba_context_create_multi: one context per shard (each with its
+    // own stream) and the group's communicators; device / stream above are
+    // shard 0's.  Empty for a one-device context.
+    std::vector<mmba_context *> shards;
+    std::vector<mmba::Comm *> comms;
 };
 
 namespace mmba {
@@ -52,6 +58,14 @@ void shard_layout(int F, int M, const int32_t *obs_frame, const int32_t *obs_bnd
 // right-hand side carried as an extra row (fused forward solve), block
 // triangular solves.
 struct Plan;
+// Interrupt polls of a shard group (mmba_group.cpp): shard 0 polls the
+// caller's callback, every shard takes its answer, so the shards' LM control
+// flows stay identical.
+struct PollShare {
+    virtual ~PollShare() {}
+    // leader: publishes v and returns it; others: return the leader's v
+    virtual int agree(int rank, int v) = 0;
+};
 struct DenseSolver {
     int n = 0, ld = 0;       // columns (nRpad), leading dimension (n + 64)
     double *A = nullptr, *Linv = nullptr, *ws = nullptr;
@@ -95,7 +109,8 @@ struct Plan {
     // setParameters first runs)
     int *d_inst_attr_plug = nullptr;
     void build_lens_instances(const mmba_problem *pr);
-    bool sep_form(int w) const;
+    bool sep_form(int w);
+    int sep_resident = 0, sep_resident_K = 0;  // min over shards of pcr_max_resident(K)
     // P with every lens instance slot at its plug value: what the reference
     // measures before setParameters first runs (solveFrames' initial
     // measureErrors, adjust_base.cpp:1002-1004 then 1076-1089)
@@ -276,6 +291,34 @@ struct Plan {
 
     // multi-GPU
     Comm *comm = nullptr;
+    // shard of a group plan (one caller, several devices, mmba_group.cpp):
+    // interrupt answers come from shard 0; outputs go straight to the
+    // caller's host buffers (each shard its own observations and
+    // parameters), no collective
+    PollShare *pshare = nullptr;
+    bool host_gather = false;
+    // sharded hand-back: this shard's own observations in reference order
+    // (device index, reference index), its own parameters
+    int M_own = 0, own_pad = 0, n_own = 0, npar_pad = 0;
+    std::vector<int> own_ref_h, own_par_h;
+    int *d_own_dev = nullptr, *d_own_par = nullptr;
+    // every shard's lists, padded (-1), for the all-gather of the
+    // one-process-per-GPU path
+    int *d_own_ref_all = nullptr, *d_own_par_all = nullptr;
+    double *d_pack = nullptr, *d_pack_all = nullptr, *h_pack = nullptr;
+    // the step's rows after a sharded band solve: each shard's rows
+    // [Ra_all[k], Rb_all[k]) (+ the arrow rows, shard 0's) all-gathered
+    int rows_pad = 0;
+    int *d_Ra_all = nullptr, *d_Rb_all = nullptr;
+    double *d_rows_send = nullptr, *d_rows_all = nullptr;
+    double *group_x_out = nullptr;  // group solve: the caller's x (own parameters written)
+    void gather_step_rows();
+    void handback_sharded(const double *dx, double *x_out, double *f_out, double *eu_out,
+                          double *ed_out, const double *f2, const double *eu2, const double *ed1);
+    // [rank of each global observation (Mg) | rank of each parameter (n)]
+    void setup_handback(const std::vector<int> &own_rank_obs_par);
+    bool poll_agree();
+    int poll_agree_index(int k);
     // a sharded plan whose problem does not shard (mmba_plan_create_sharded):
     // every shard solves the whole problem, no collectives
     bool replicated = false;
@@ -355,6 +398,7 @@ struct Plan {
     static constexpr bool spin_wait = true;  // (blocking synchronisation: slower)
     hipEvent_t ev_sync = nullptr;  // [lo, hi] inclusive, one D2H copy + sync
     double read_scalar(int slot = 0);
+    void stream_wait();
     void allreduce(double *d, size_t count, ReduceOp op = ReduceOp::Sum);
     double reduce_read(int slot, ReduceOp op = ReduceOp::Sum);
     void fun_enqueue(const double *dx, double *df, double *eu, double *ed,
@@ -482,12 +526,46 @@ struct Plan {
     int measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
                 double *stats);
     void download_params(const double *dx, double *x_out);
+    // sync = false (unsharded): the copies are only enqueued, the caller's
+    // next wait covers them
     void download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
-                            double *f_out, double *eu_out, double *ed_out);
+                            double *f_out, double *eu_out, double *ed_out, bool sync = true);
 };
 
 }  // namespace mmba
 
+namespace mmba {
+struct ShardGroup;  // mmba_group.cpp
+void destroy_group(ShardGroup *g);
+struct GroupDeleter {
+    void operator()(ShardGroup *g) const { destroy_group(g); }
+};
+}  // namespace mmba
+
+namespace mmba {
+// group forms of the plan entry points (mmba_group.cpp; mmba_api.cpp routes
+// a plan whose group is set, or a multi-device context, here)
+int group_plan_create(mmba_context *ctx, const mmba_problem *prob, const mmba_options *opt,
+                      mmba_plan **out);
+int group_plan_solve(mmba_plan *plan, double *x_inout, double *fvec_out, double *err_user_out,
+                     double *err_dist_out, mmba_result *res, const mmba_callbacks *cb,
+                     mmba_trace *trace);
+int group_plan_measure(mmba_plan *plan, const double *x, double *fvec_out, double *err_user_out,
+                       double *err_dist_out, double *avg_min_max_out);
+int group_plan_reproject(mmba_plan *plan, const double *x, double *point_xy_out,
+                         double *marker_xy_out);
+int group_plan_jacobian(mmba_plan *plan, const double *x, double *fjac);
+int group_plan_outputs(mmba_plan *plan, double *fvec_out, double *err_user_out,
+                       double *err_dist_out);
+int group_plan_set_attr_values(mmba_plan *plan, const double *attr_values);
+int group_plan_solve_per_frame(mmba_plan *plan, double *x_inout, mmba_result *results,
+                               const mmba_callbacks *cb);
+int group_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats *out);
+}  // namespace mmba
+
 struct mmba_plan {
     mmba::Plan impl;
+    // ABI 9: a plan over a multi-device context -- one sharded plan per
+    // device, driven by the library's own threads (impl unused)
+    std::unique_ptr<mmba::ShardGroup, mmba::GroupDeleter> group;
 };

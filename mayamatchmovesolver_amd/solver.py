@@ -72,9 +72,30 @@ class SolveResult:
 
 
 class Context:
-    def __init__(self, device: int = 0):
+    """A device context (``mmba_context``).  ``Context.multi(devices)``: one
+    context over several devices (ABI 9) -- a ``Solver`` on it is frame-sharded
+    over every device and driven from this thread (the library runs the other
+    devices' shards on its own threads); naming one device N times runs the N
+    shards there (the in-process transport)."""
+
+    def __init__(self, device: int = 0, _handle=None):
         self._h = C.c_void_p()
-        check(lib().mmba_context_create(int(device), C.byref(self._h)))
+        if _handle is not None:
+            self._h = _handle
+        else:
+            check(lib().mmba_context_create(int(device), C.byref(self._h)))
+
+    @classmethod
+    def multi(cls, devices) -> "Context":
+        devs = [int(d) for d in devices]
+        arr = (C.c_int * len(devs))(*devs)
+        h = C.c_void_p()
+        check(lib().mmba_context_create_multi(arr, len(devs), C.byref(h)))
+        return cls(_handle=h)
+
+    @property
+    def num_devices(self) -> int:
+        return int(lib().mmba_context_num_devices(self._h))
 
     @property
     def handle(self):
@@ -221,6 +242,11 @@ class Solver:
             self.close()
         except Exception:
             pass
+
+    @property
+    def num_shards(self) -> int:
+        """Shards this plan solves on (``mmba_plan_num_shards``)."""
+        return int(lib().mmba_plan_num_shards(self._h))
 
     def set_timing(self, enable=True):
         st = abi.MmbaKernelStats()

@@ -69,7 +69,7 @@ def test_struct_layouts_match_header():
 
 
 def test_host_helpers(L, oracle):
-    assert L.mmba_abi_version() == abi.ABI_VERSION == 8
+    assert L.mmba_abi_version() == abi.ABI_VERSION == 9
     o = abi.MmbaOptions()
     L.mmba_options_default(C.byref(o), abi.SOLVER_TYPE_CMINPACK_LMDER)
     assert (o.iter_max, o.tau, o.eps1, o.delta, o.auto_param_scale, o.image_width) == \
@@ -91,6 +91,8 @@ def test_no_device_fails_loudly(L):
     rc = L.mmba_context_create(0, C.byref(h))
     assert rc == abi.MMBA_ERR_NO_DEVICE
     assert b"gfx950" in L.mmba_last_error()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.mmba_context_create_multi(devs, 2, C.byref(h)) == abi.MMBA_ERR_NO_DEVICE
 
 
 def test_bound_transforms_keep_nan(L, oracle):
