@@ -320,8 +320,24 @@ def cpu_baseline(cfg_index, budget_s, ctx):
                 "F'=%d n=%d m=%d: CPU %.2f s, GPU %.2f ms" % (
                     q["frames"], q["params"], q["residuals"], q["cpu_s"], 1e3 * q["gpu_s"])
                 for q in samples)))
+    full_run = None
+    fx = {1: "c2_full_it1", 4: "c5_full_it1"}.get(cfg_index)
+    if fx:
+        # the oracle on the WHOLE configuration, one LM iteration (lmder
+        # iterMax 2): measured once when the full-size parity fixture was
+        # made (tests/golden/make_full_golden.py, one thread, this repo's
+        # build container) -- a measurement on another host, labelled so
+        path = os.path.join(ROOT, "tests", "golden", "full", fx + ".npz")
+        if os.path.exists(path):
+            d = np.load(path, allow_pickle=False)
+            it = max(1, int(d["res_outer_iterations"]))
+            full_run = {"fixture": os.path.relpath(path, ROOT),
+                        "seconds": float(d["oracle_seconds"]), "lm_iterations": it,
+                        "lm_iterations_per_s": it / float(d["oracle_seconds"]),
+                        "host": "build container (one thread), not the GPU box",
+                        "params": int(d["exp_x"].size)}
     return {"value": big["cpu_lm_iterations_per_s"], "unit": "LM iterations/s", "cores": 1,
-            "kind": "port", "sample": desc, "windows": samples,
+            "kind": "port", "sample": desc, "windows": samples, "full_config_run": full_run,
             "speedup_measured_same_window": big["speedup_measured"],
             "extrapolated_full_scene": {
                 "label": "EXTRAPOLATION, not a measurement: largest window's per-iteration time "

@@ -672,6 +672,14 @@ int mmba_debug_dgemm(mmba_context *ctx, int tri, int in_place, int M, int N, int
                      const double *A, int lda, const double *B, int ldb, double *C, int ldc,
                      double alpha, double beta);
 
+/* Test hook (not part of the solver seam; ABI 9): on a plan whose reduced
+ * system takes the dense solver (C3-class scenes), evaluate at internal x,
+ * form the Jacobian's damped reduced system (S + lam D^2) and its right-hand
+ * side r, keep them aside, solve with the plan's factorisation and return
+ * ||S xR - r|| / ||r|| -- the full-size dense solve's own accuracy.
+ * MMBA_ERR_UNSUPPORTED for other plans. */
+int mmba_debug_reduced_residual(mmba_plan *plan, const double *x, double lam, double *relres);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,6 +56,8 @@ def lib():
         L.mmba_context_create_multi.restype = C.c_int
         L.mmba_context_create_multi.argtypes = [C.POINTER(C.c_int), C.c_int,
                                                 C.POINTER(C.c_void_p)]
+        L.mmba_debug_reduced_residual.restype = C.c_int
+        L.mmba_debug_reduced_residual.argtypes = [C.c_void_p, dp, C.c_double, dp]
         L.mmba_context_num_devices.restype = C.c_int
         L.mmba_context_num_devices.argtypes = [C.c_void_p]
         L.mmba_plan_num_shards.restype = C.c_int

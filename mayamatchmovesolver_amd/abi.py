@@ -242,6 +242,7 @@ EXPORTED_SYMBOLS = [
     "mmba_context_create_multi",
     "mmba_context_num_devices",
     "mmba_plan_num_shards",
+    "mmba_debug_reduced_residual",
     "mmba_context_destroy",
     "mmba_context_synchronize",
     "mmba_host_alloc",

@@ -477,6 +477,20 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
     return MMBA_OK;
 }
 
+int mmba_debug_reduced_residual(mmba_plan *plan, const double *x, double lam, double *relres) {
+    if (!plan || !x || !relres || lam < 0.) return MMBA_ERR_INVALID;
+    if (plan->group) {
+        set_error("unsupported: reduced residual hook on a multi-device plan");
+        return MMBA_ERR_UNSUPPORTED;
+    }
+    MMBA_GUARD({
+        Plan &p = plan->impl;
+        MMBA_HIP(hipSetDevice(p.ctx->device));
+        p.outputs_ready = false;
+        return p.reduced_residual(x, lam, relres);
+    })
+}
+
 int mmba_debug_dgemm(mmba_context *ctx, int tri, int in_place, int M, int N, int K,
                      const double *A, int lda, const double *B, int ldb, double *C, int ldc,
                      double alpha, double beta) {

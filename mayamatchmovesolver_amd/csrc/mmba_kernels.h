@@ -185,6 +185,10 @@ struct NeEpi {
     // gate != nullptr: the launch runs only when *gate != 0 (a Jacobian
     // enqueued ahead of the host's decision, LmDec)
     const int *gate = nullptr;
+    // MMBA_PATH_PROBE = 2: k_jac_ne_u stores, per workgroup (logical
+    // camera-frame), the wall clock at entry, after staging, after its
+    // observations and at exit, and its XCC id
+    long long *probe = nullptr;
 };
 // Fused K2 (k_jac_ne_u): FD Jacobian + camera-frame normal equations in one
 // pass for uniform fast plans without global parameters (ncv = jac_ncv).

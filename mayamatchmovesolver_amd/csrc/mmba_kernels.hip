@@ -1259,6 +1259,8 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
     if (E.gate && __hip_atomic_load(E.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         return;
     const int cf = xcd_remap(blockIdx.x, gridDim.x);
+    long long *pr = (E.probe && threadIdx.x == 0) ? E.probe + 5 * (size_t)cf : nullptr;
+    if (pr) pr[0] = (long long)wall_clock64();
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
@@ -1281,6 +1283,7 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
         }
     }
     __syncthreads();
+    if (pr) pr[1] = (long long)wall_clock64();
     JacCf<PC> C;
     C.rcf = sRec;
 #pragma unroll
@@ -1311,8 +1314,10 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
 #pragma unroll
         for (int a = 0; a < PC; ++a) acc[NCC + a] += jx[a] * fx + jy[a] * fy;
     }
+    if (pr) pr[2] = (long long)wall_clock64();
     if (!solved) {  // no camera parameter on this camera-frame: J only
         if (E.on && tid == 0) epi_store(E, E.cf_base + cf, 0., 0., 0.);
+        if (pr) pr[3] = pr[2];
         return;
     }
 #pragma unroll
@@ -1355,6 +1360,12 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
             epi_param(E, P.cf_var_param[v0 + a], d, gp, zf, xn, gm);
         }
         epi_store(E, E.cf_base + cf, zf, xn, gm);
+    }
+    if (pr) {
+        pr[3] = (long long)wall_clock64();
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        pr[4] = (long long)(xcc & 0xf);
     }
 }
 

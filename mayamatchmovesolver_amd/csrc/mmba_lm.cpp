@@ -255,6 +255,7 @@ void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
     epi.cf_base = 0;
     epi.bnd_base = ncf;
     epi.gate = d_gate;
+    epi.probe = d_k2probe;
     launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, nloc_set ? nullptr : d_nloc,
                   d_stale, eu, ed, d_Acc, d_g, epi);
     nloc_set = true;
@@ -315,6 +316,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.cf_base = 0;
         epi.bnd_base = ncf;
     }
+    epi.probe = d_k2probe;
     // unsharded plans with fast bundles: the bundle pass forms the lam = 0
     // bundle factor the undamped solve reads next (no k_bundle_factor
     // launch); with tail_reduce its last workgroup also reduces the
@@ -603,6 +605,12 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             } else {
                 launch_schur_pairs(s, PS, d_W, d_Wg, d_tb, V, d_rhs);
             }
+        }
+        if (dbg_keep_S && dense) {  // mmba_debug_reduced_residual: S and r before the factor
+            MMBA_HIP(hipMemcpyAsync(d_Skeep, ds.A, sizeof(double) * (size_t)ds.ld * (ds.n + 1),
+                                    hipMemcpyDeviceToDevice, s));
+            MMBA_HIP(hipMemcpyAsync(d_rkeep, d_rhs, sizeof(double) * nRpad, hipMemcpyDeviceToDevice,
+                                    s));
         }
         span_begin(SPAN_CHOL);
         if (band && bs.use_bd) {  // factor, forward and backward
@@ -1058,6 +1066,56 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
             }
         }
     }
+    return MMBA_OK;
+}
+
+// ||S x - r||^2 and ||r||^2 of a dense symmetric S (lower triangle,
+// column-major, ld): one thread per row, the lower part read down its row
+// (coalesced across threads), the upper part from its own column.
+__global__ void k_dense_symv_res(const double *__restrict__ A, int ld, int n,
+                                 const double *__restrict__ x, const double *__restrict__ r,
+                                 double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0.;
+    if (i < n) {
+        for (int j = 0; j <= i; ++j) acc = fma(A[(size_t)j * ld + i], x[j], acc);
+        for (int j = i + 1; j < n; ++j) acc = fma(A[(size_t)i * ld + j], x[j], acc);
+        const double d = acc - r[i];
+        atomicAdd(&out[0], d * d);
+        atomicAdd(&out[1], r[i] * r[i]);
+    }
+}
+
+int Plan::reduced_residual(const double *x, double lam, double *relres) {
+    if (!dense) throw Unsupported{"reduced residual hook: dense reduced plans only"};
+    if (!d_Skeep) {
+        d_Skeep = dalloc<double>((size_t)ds.ld * (ds.n + 1));
+        d_rkeep = dalloc<double>(nRpad);
+    }
+    attrs_reset();
+    MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    MMBA_HIP(hipMemsetAsync(d_diag, 0, sizeof(double) * n, s));
+    fun(d_x, d_f, d_eu, d_ed);
+    const JacLM lm{1, 1, 1.0, nullptr};
+    jac(d_x, &lm);
+    dbg_keep_S = true;
+    try {
+        solve_damped_enqueue(lam, SL_DNORM);
+    } catch (...) {
+        dbg_keep_S = false;
+        throw;
+    }
+    dbg_keep_S = false;
+    double *acc = dalloc<double>(2);
+    MMBA_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(double), s));
+    k_dense_symv_res<<<(nR + 255) / 256, 256, 0, s>>>(d_Skeep, ds.ld, nR, d_xR, d_rkeep, acc);
+    double h[2];
+    MMBA_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
+    MMBA_HIP(hipStreamSynchronize(s));
+    read_slots(SL_DNORM, SL_FAIL);
+    if (h_scalar[SL_FAIL] != 0.) throw Invalid{"reduced residual hook: the factorisation failed"};
+    *relres = std::sqrt(h[0] / h[1]);
+    collect_spans();
     return MMBA_OK;
 }
 

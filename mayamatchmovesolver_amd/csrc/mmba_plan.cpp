@@ -11,6 +11,7 @@
 //   G   anything else (static camera attrs, lens coefficients, group
 //       transforms shared by several bundles/cameras) -> dense arrow rows
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -26,6 +27,46 @@
 namespace mmba {
 
 Plan::~Plan() {
+    if (d_k2probe) {
+        // the last k_jac_ne_u launch: per workgroup entry / staged / observations
+        // done / exit (10-ns ticks), summarised in microseconds
+        std::vector<long long> t(5 * (size_t)ncf);
+        if (hipMemcpy(t.data(), d_k2probe, sizeof(long long) * t.size(), hipMemcpyDeviceToHost) ==
+            hipSuccess) {
+            long long t0 = LLONG_MAX, tend = 0;
+            for (int c = 0; c < ncf; ++c)
+                if (t[5 * c]) {
+                    t0 = std::min(t0, t[5 * c]);
+                    tend = std::max(tend, t[5 * c + 3]);
+                }
+            std::vector<double> st, stg, obs, tail, tot;
+            int per_xcc[16] = {};
+            for (int c = 0; c < ncf; ++c) {
+                const long long *q = &t[5 * c];
+                if (!q[0]) continue;
+                st.push_back((q[0] - t0) / 100.);
+                stg.push_back((q[1] - q[0]) / 100.);
+                obs.push_back((q[2] - q[1]) / 100.);
+                tail.push_back((q[3] - q[2]) / 100.);
+                tot.push_back((q[3] - q[0]) / 100.);
+                per_xcc[q[4] & 15]++;
+            }
+            auto pct = [](std::vector<double> v, double p) {
+                if (v.empty()) return 0.;
+                std::sort(v.begin(), v.end());
+                return v[std::min(v.size() - 1, (size_t)(p * (v.size() - 1) + 0.5))];
+            };
+            std::fprintf(stderr, "[mmba probe] k_jac_ne_u %zu workgroups, span %.2f us; p0/p50/p100 "
+                                 "(us): start %.2f/%.2f/%.2f staging %.2f/%.2f/%.2f observations "
+                                 "%.2f/%.2f/%.2f tail %.2f/%.2f/%.2f total %.2f/%.2f/%.2f; per XCC",
+                         st.size(), (tend - t0) / 100., pct(st, 0), pct(st, .5), pct(st, 1),
+                         pct(stg, 0), pct(stg, .5), pct(stg, 1), pct(obs, 0), pct(obs, .5),
+                         pct(obs, 1), pct(tail, 0), pct(tail, .5), pct(tail, 1), pct(tot, 0),
+                         pct(tot, .5), pct(tot, 1));
+            for (int x = 0; x < 8; ++x) std::fprintf(stderr, " %d", per_xcc[x]);
+            std::fprintf(stderr, "\n");
+        }
+    }
     if (d_probe && bs.use_bcr && bs.bcr.fflags && bs.bcr.nblk >= 2) {
         // dataflow factor trace of the last factorisation: per level, the
         // mean wait, item and publish times and the level's span (us)
@@ -1480,7 +1521,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             cfblk_cf.push_back(cf);
         }
     if (band) setup_band();
-    if (band && path_choice(MMBA_PATH_PROBE) > 0) {
+    if (path_choice(MMBA_PATH_PROBE) == 2) {  // k_jac_ne_u workgroup timeline
+        d_k2probe = dalloc<long long>(5 * (size_t)std::max(ncf, 1));
+        MMBA_HIP(hipMemsetAsync(d_k2probe, 0, 5 * (size_t)std::max(ncf, 1) * sizeof(long long), s));
+    }
+    if (band && path_choice(MMBA_PATH_PROBE) == 1) {
         const size_t np = 8 + 4 * ((size_t)std::max(nR, 1) + 64);  // + the dataflow trace
         d_probe = dalloc<long long>(np);
         MMBA_HIP(hipMemsetAsync(d_probe, 0, np * sizeof(long long), s));

@@ -188,6 +188,7 @@ struct Plan {
     int dld = 0;
     DenseSolver ds;
     long long *d_probe = nullptr;  // MMBA_PATH_PROBE = 1: band-kernel phase cycles
+    long long *d_k2probe = nullptr;  // MMBA_PATH_PROBE = 2: k_jac_ne_u workgroup timeline
     bool nloc_set = false;         // d_nloc stored by a fused Jacobian pass
     // single-workgroup triangular solves for narrow (banded) structures
     bool narrow = false;
@@ -522,6 +523,12 @@ struct Plan {
     int *h_bflag = nullptr, *d_bflag = nullptr;  // host-mapped interrupt flag
     int solve_frames(double *x_inout, mmba_result *results, const mmba_callbacks *cb);
     int dense_jacobian(const double *x, double *fjac);
+    // test hook (mmba_debug_reduced_residual): the damped reduced system at
+    // x and lam, kept aside before the factorisation; its solve's relative
+    // residual ||S x - r|| / ||r|| (dense plans)
+    bool dbg_keep_S = false;
+    double *d_Skeep = nullptr, *d_rkeep = nullptr;
+    int reduced_residual(const double *x, double lam, double *relres);
     int reproject(const double *x, double *point_out, double *marker_out);
     int measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
                 double *stats);

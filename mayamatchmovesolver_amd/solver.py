@@ -248,6 +248,14 @@ class Solver:
         """Shards this plan solves on (``mmba_plan_num_shards``)."""
         return int(lib().mmba_plan_num_shards(self._h))
 
+    def reduced_residual(self, x=None, lam: float = 0.0) -> float:
+        """||S x - r|| / ||r|| of the damped reduced system the plan forms at x
+        (test hook ``mmba_debug_reduced_residual``; dense reduced plans)."""
+        xx = np.ascontiguousarray(self.problem.x0 if x is None else x, dtype=np.float64)
+        out = np.zeros(1)
+        check(lib().mmba_debug_reduced_residual(self._h, _dp(xx), float(lam), _dp(out)))
+        return float(out[0])
+
     def set_timing(self, enable=True):
         st = abi.MmbaKernelStats()
         self._timing = bool(enable)

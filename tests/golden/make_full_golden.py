@@ -59,12 +59,17 @@ CASES = {
     "c5_full_it1": (4, None, 1.0, 2, True),
     "c4_w24_it1": (3, 24, 24 / 500.0, 2, True),
     "c4_w10_full": (3, 10, 10 / 500.0, 1000, True),
+    # configs[4] with its rolling shutter (rs 0.5, the bench's C5-RS line), one
+    # LM step at the full 2 cameras x 240 frames (VERDICT r4 "next" 9)
+    "c5rs_full_it1": (4, None, 1.0, 2, True),
 }
+# extra generator arguments of a case
+CASE_KW = {"c5rs_full_it1": {"rolling_shutter": 0.5}}
 
 
 def make_problem(name):
     idx, frames, scale, _it, _f = CASES[name]
-    return S.make_config(idx, frames=frames, scale=scale)
+    return S.make_config(idx, frames=frames, scale=scale, **CASE_KW.get(name, {}))
 
 
 def make_options(name, prob):
@@ -141,7 +146,7 @@ def load(name):
     d = dict(np.load(os.path.join(FULL, name + ".npz"), allow_pickle=False))
     frames = int(d["gen_frames"])
     prob = S.make_config(int(d["gen_config"]), frames=None if frames < 0 else frames,
-                         scale=float(d["gen_scale"]))
+                         scale=float(d["gen_scale"]), **CASE_KW.get(name, {}))
     dg = problem_digest(prob)
     if dg != str(d["digest"]):
         raise RuntimeError("%s: regenerated scene differs from the fixture's (%s != %s)" % (

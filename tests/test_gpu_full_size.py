@@ -42,3 +42,33 @@ def test_gpu_full_size_matches_oracle(name, gpu_ctx):
         assert np.linalg.norm(out.fvec - d["exp_fvec"]) <= REL * float(tr[0])
     assert abs(g["error_final"] - float(d["res_error_final"])) <= \
         REL * float(d["res_error_final"])
+
+
+def test_c3_full_dense_reduced_solve(gpu_ctx):
+    """BASELINE configs[2] at its full size (10 cameras x 500 frames, 10k
+    bundles, 50k markers: n_r = 29,994 reduced rows after the bundles are
+    eliminated; VERDICT r4 "next" 9).  The dense reduced system takes the
+    hand-written fp64 MFMA Cholesky; its solve at x0, undamped and damped
+    (mmba_debug_reduced_residual: S and r kept aside before the
+    factorisation), has ||S x - r|| / ||r|| <= 1e-10; then the whole LM run
+    converges (MINPACK info 1-3) to the 0.5 px marker noise of the scene.
+    The oracle cannot run this size (its dense Jacobian is 1M x 60k), so the
+    structure is pinned against it on c3_f8 (test_gpu_golden.py)."""
+    from mayamatchmovesolver_amd import synthetic as S
+    prob = S.make_config(2)
+    opt = S.config_options(prob)
+    s = Solver(prob, opt, context=gpu_ctx)
+    try:
+        st = s.kernel_stats()
+        assert st["reduced_kind"] == 2, st  # dense blocked Cholesky
+        assert st["reduced_dim"] >= 29_000
+        for lam in (0.0, 1e-2):
+            rr = s.reduced_residual(prob.x0, lam)
+            assert rr <= 1e-10, (lam, rr)
+        out = s.solve()
+    finally:
+        s.close()
+    g = out.result
+    assert g["reason_number"] in (1, 2, 3), g
+    assert 0.3 <= g["error_rms"] <= 0.8, g
+    assert out.fnorm_trace[-1] < 1e-2 * out.fnorm_trace[0]

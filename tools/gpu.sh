@@ -43,7 +43,9 @@ for step in "$@"; do
       c=${step#benchcfg:}
       st=8; wu=3
       if [ "$c" = 2 ]; then st=3; wu=1; fi  # C3: ~11 s per solve
-      timeout -k 10 600 python -u bench.py --config "$c" --steps $st --warmup $wu --no-cpu-baseline --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
+      cb=--no-cpu-baseline
+      if [ "$c" = 1 ] || [ "$c" = 4 ]; then cb=; fi  # C2 / C5: the CPU windows + the full-config oracle run
+      timeout -k 10 600 python -u bench.py --config "$c" --steps $st --warmup $wu $cb --no-traffic > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail "$OUT/bench_$c.err"; exit 1; }
       cat "$OUT/bench_$c.json" ;;
     benchpath:*)
       pv=${step#benchpath:}

@@ -10,6 +10,10 @@
 #include <cstdio>
 #include <vector>
 
+namespace mmba {
+void set_error(const std::string &) {}  // (the library's; unused here)
+}  // namespace mmba
+
 using namespace mmba;
 
 int main(int argc, char **argv) {
