@@ -622,6 +622,10 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             else
                 band_factor_forward(s, bs, d_fail, d_probe, d_rhs, d_yR);
         } else if (dense) {
+            if (nranks > 1) {  // each shard's rows of S and r, summed (shard_dense)
+                allreduce(d_S, (size_t)ds.ld * (ds.n + 1));
+                allreduce(d_rhs, nRpad);
+            }
             ds.factor_forward(s, d_rhs, d_yR, d_fail);  // y = L^-1 rhs rides along
         } else {
             for (int k = 0; k < NT; ++k) {

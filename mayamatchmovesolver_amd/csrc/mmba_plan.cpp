@@ -753,8 +753,16 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     // (the hand-back lists, setup_handback)
     std::vector<int> obs_rank_g, cf_rank;
     if (nranks > 1) {
-        if (!band || bw > WBAND_PART)
-            throw Unsupported{"sharded solve needs a narrow camera-frame band (w <= 40)"};
+        // a camera-frame band wider than the partitioned solvers take (C3:
+        // bundles tracked across the whole shot): each shard still assembles
+        // the reduced rows of its own camera-frames, the shards' dense S are
+        // all-reduced and every shard factors it with the dense solver
+        // (Plan::shard_dense)
+        shard_dense = !band || bw > WBAND_PART;
+        if (shard_dense) {
+            band = false;
+            if (nR > 65536) throw Unsupported{"sharded dense reduced system above 65,536 rows"};
+        }
         std::vector<int> bf(nranks + 1, F), bnd_owner_all(nB, 0);
         shard_layout(F, Mg, pr->obs_frame, obs_bnd_g.data(), nB, nranks, bf.data(),
                      bnd_owner_all.data());
@@ -767,7 +775,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         for (int k = 0; k < nranks; ++k) {
             Ra_all[k] = first_row[bf[k]];
             Rb_all[k] = first_row[bf[k + 1]];
-            if (Rb_all[k] - Ra_all[k] < 2 * bw + 8)
+            if (Rb_all[k] - Ra_all[k] < (shard_dense ? 1 : 2 * bw + 8))
                 throw Unsupported{"too few camera-frame rows per shard"};
         }
         Ra = Ra_all[rank];
@@ -1501,12 +1509,16 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         dense = !band && nranks == 1 && NT >= 8 && (long long)nslots * 10 >= full * 3;
         if (path_choice(MMBA_PATH_DENSE) >= 0)
             dense = !band && nranks == 1 && NT > 0 && path_choice(MMBA_PATH_DENSE) != 0;
+        if (shard_dense) dense = true;  // sharded, not a band: the dense solver (above)
     }
     if (dense) {
         ds.setup(*this, nRpad);
         d_S = ds.A;
         dld = ds.ld;
         d_Linv = nullptr;
+        // sharded: every shard factors the same all-reduced S, so the rows
+        // of lmpar's L^-1 w are counted on shard 0 only
+        if (nranks > 1) d_ymask = upload(std::vector<int>(std::max(nR, 1), rank == 0 ? 1 : 0));
     } else {
         d_S = dalloc<double>((size_t)nslots * TILE * TILE);
         d_Linv = dalloc<double>((size_t)NT * TILE * TILE);

@@ -185,6 +185,7 @@ struct Plan {
     }
     // dense reduced system (most tiles structurally non-zero)
     bool dense = false;
+    bool shard_dense = false;  // sharded plan without a narrow band: dense S all-reduced
     int dld = 0;
     DenseSolver ds;
     long long *d_probe = nullptr;  // MMBA_PATH_PROBE = 1: band-kernel phase cycles

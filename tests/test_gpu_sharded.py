@@ -262,6 +262,40 @@ def test_separator_form_well_conditioned(nshards, gpu_ctx):
     assert dx <= 1e-6, dx
 
 
+@pytest.mark.parametrize("nshards", [2, 4])
+def test_sharded_dense_c3_structure(nshards, gpu_ctx, paths):
+    """A reduced system that is no narrow band (the C3 structure: ten cameras,
+    bundles tracked across the shot) shards too (VERDICT r4 "next" 8): each
+    shard assembles the rows of its own camera-frames, the dense S and its
+    right-hand side are all-reduced and every shard factors it with the fp64
+    MFMA dense solver.  Against the unsharded dense
+    solve: the first full step's x at 1e-6 and its ||f|| at 1e-9, then the
+    whole run's reason, counts and trace at 1e-6 (the committed oracle
+    fixture c3_f8 pins the unsharded run, test_gpu_golden.py)."""
+    prob = S.make_config(2, frames=8, scale=0.002)
+    for it in (2, 1000):
+        opt = S.config_options(prob, iterations=it)
+        s = Solver(prob, opt, context=gpu_ctx)
+        try:
+            assert s.kernel_stats()["reduced_kind"] == 2
+            ref = s.solve()
+        finally:
+            s.close()
+        reps = []
+        outs = run_sharded(prob, opt, nshards, replicated=reps)
+        assert reps == [0] * nshards, reps  # really sharded, not replicated
+        check_shards_agree(outs)
+        g = outs[0]
+        for k in ("reason_number", "iterations", "function_evals"):
+            assert g.result[k] == ref.result[k], k
+        if it == 2:
+            np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-9)
+            dx = np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3))
+            assert dx <= 1e-6, dx
+        else:
+            np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-6)
+
+
 def test_rccl_communicator_one_rank(gpu_ctx):
     """A real RCCL communicator on the box's GPU (ncclGetUniqueId,
     ncclCommInitRank, ncclAllReduce in place on the plan's stream -- the calls
