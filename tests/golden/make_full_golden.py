@@ -140,6 +140,22 @@ def combine(name):
         float(main["seconds"]), os.path.getsize(path) / 1024))
 
 
+def subspace(name):
+    """One-step fixtures (iteration cap 2): the step's undetermined directions
+    (tests/golden/make_steps.py: right singular vectors of the scaled oracle J
+    at x0 with sigma < RATIO sigma_max, float32) stored in the fixture, so the
+    GPU test holds x at 1e-6 once they are projected out."""
+    from tests.golden import make_steps as ST
+    prob, opt, d = load(name)
+    assert int(d["gen_iterations"]) == 2, "one-step fixtures only"
+    scale = np.maximum(np.abs(d["exp_x"]), 1e-3)
+    Vu, sv = ST.undetermined_basis(prob, opt, prob.x0, scale)
+    d["undet_basis"], d["sigma"], d["ratio"] = Vu, sv, np.array(ST.RATIO)
+    np.savez_compressed(os.path.join(FULL, name + ".npz"), **d)
+    print("%s: %d undetermined directions of %d (cond %.1e)" % (name, Vu.shape[1], sv.size,
+                                                               sv[0] / sv[-1]))
+
+
 def load(name):
     """(problem, options, fixture dict); raises if the regenerated scene's
     digest differs from the one the oracle ran on."""
@@ -166,8 +182,11 @@ if __name__ == "__main__":
     ap.add_argument("--case", required=True, choices=sorted(CASES))
     ap.add_argument("--seed", type=int, default=-1)
     ap.add_argument("--combine", action="store_true")
+    ap.add_argument("--subspace", action="store_true")
     a = ap.parse_args()
-    if a.combine:
+    if a.subspace:
+        subspace(a.case)
+    elif a.combine:
         combine(a.case)
     else:
         run(a.case, a.seed)
