@@ -642,8 +642,10 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
 #define MMBA_PATH_PERFRAME_BATCH 6 /* 0: per-frame mode with one plan per frame */
 #define MMBA_PATH_LOCAL_RING 7     /* 1: in-process communicators sum in ring order */
 #define MMBA_PATH_PROBE 8          /* 1: band / BCR phase probe, printed when the plan is destroyed */
-#define MMBA_PATH_SHARD_SEP 9      /* 0: sharded plans without an arrow all-reduce the whole
-                                      reduced system instead of its separator form */
+#define MMBA_PATH_SHARD_SEP 9      /* 1: sharded plans without an arrow solve the reduced
+                                      system in its separator form (each shard's interior
+                                      eliminated, the separator system all-reduced) instead
+                                      of all-reducing it whole (the default since ABI 9) */
 #define MMBA_PATH_NUM 10
 int mmba_debug_set_path(int key, int value);
 

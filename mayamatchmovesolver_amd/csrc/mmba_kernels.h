@@ -269,6 +269,8 @@ struct TrialFold {
     int nother = 0;
     double *partial = nullptr;
     int rstride = 0;
+    // sharded: the parameters this shard counts in ||D p||^2, ||D x_new||^2
+    const int *own = nullptr;
 };
 int trial_fold_parts(const DevProblem &P, int nother);
 void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,

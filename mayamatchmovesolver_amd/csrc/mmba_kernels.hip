@@ -2654,16 +2654,18 @@ __device__ __forceinline__ void trial_one(const DevProblem &P, const TrialFold &
     T.wa3[j] = w3;
     param_prep_one(P, j, xj, T.ext, T.ext_pert, T.step, T.solver_type, T.delta, T.eps_dif);
     set_attr_one(P, j, T.ext[j]);
-    pn += w3 * w3;
-    const double v = dj * xj;
-    xn += v * v;
+    if (own_mask(T.own, j)) {  // sharded: each parameter counted by its owner
+        pn += w3 * w3;
+        const double v = dj * xj;
+        xn += v * v;
+    }
 }
 
 // k_backsub_bundle (two-pass form: u_i from k_obs_wtx) + the trial point's
 // parameter pass: workgroups [0, nbb) back-substitute their bundles and
 // prepare those parameters from the step just formed; workgroups [nbb, ..)
 // prepare the other parameters from xs (the reduced solve's scatter).
-// Unsharded plans only (every parameter owned).
+// Sharded plans count only their own parameters in the sums (TrialFold::own).
 __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double *__restrict__ U,
                                                       const double *__restrict__ Wg,
                                                       const double *__restrict__ tb,

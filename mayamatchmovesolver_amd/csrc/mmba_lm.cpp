@@ -321,8 +321,10 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     // bundle factor the undamped solve reads next (no k_bundle_factor
     // launch); with tail_reduce its last workgroup also reduces the
     // epilogue rows
-    const bool fold = fuse && nranks == 1 && P.nbs > 0 && P.JB != nullptr && fold_ok;
-    const bool tail = fold && tail_reduce;
+    // (sharded too: every bundle a shard touches has all its observations
+    // there; the others have Abb = 0 and factor as the identity)
+    const bool fold = fuse && P.nbs > 0 && P.JB != nullptr && fold_ok;
+    const bool tail = fold && tail_reduce && nranks == 1;
     lb0_valid = false;
     if (tail) {
         epi.fold = 1;
@@ -598,8 +600,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
                 if (fold) fi = SchurInitFold{1, d_Acc, d_g, d_diag, lam};
                 const bool rhs_done =
                     launch_schur_dest(s, PS, d_W, d_dest, d_dest_off, ndest, d_dpairs, V,
-                                      pc_uniform, band && bs.use_bcr && !rs_bnd, d_tb,
-                                      nranks > 1 ? nullptr : d_rhs, fi);
+                                      pc_uniform, band && bs.use_bcr && !rs_bnd, d_tb, d_rhs, fi);
                 if (!rhs_done) launch_schur_rhs(s, PS, d_W, d_tb, d_row_cf, d_rhs);
                 launch_schur_glob(s, PS, d_W, d_Wg, d_tb, V, d_rhs);
             } else {
@@ -688,6 +689,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             T.nother = n_trial_other;
             T.partial = d_partial + 3 * (size_t)pw;
             T.rstride = pw;
+            T.own = d_p_own;
             launch_backsub_trial(s, PS, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
             trial_folded = true;
             params_at = nullptr;  // the attribute block now holds the trial point

@@ -1131,8 +1131,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
             for (const int2 &d : dest_h)
                 if (d.x == d.y) hasd[d.x] = 1;
             dest_diag_all = true;
-            for (int cf = 0; cf < ncf; ++cf)
-                if (cf_pc[cf] > 0 && !hasd[cf]) dest_diag_all = false;
+            for (int cf = 0; cf < ncf; ++cf)  // (sharded: this shard's camera-frames)
+                if (cf_pc[cf] > 0 && cf_own[cf] && !hasd[cf]) dest_diag_all = false;
             dest_diag_ii = true;
             for (size_t d = 0; d < dest_h.size() && dest_diag_ii; ++d)
                 if (dest_h[d].x == dest_h[d].y)
@@ -1726,7 +1726,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     MMBA_HIP(hipHostMalloc(&h_scalar, NSLOT * sizeof(double)));
     MMBA_HIP(hipHostMalloc(&h_seq, sizeof(unsigned)));
     *h_seq = 0;
-    trial_fold_ok = nranks == 1 && nB_solved > 0;
+    trial_fold_ok = nB_solved > 0;
     d_gate = dalloc<int>(1);
     MMBA_HIP(hipMemsetAsync(d_gate, 0, sizeof(int), s));
     d_mticket = dalloc<unsigned>(1);
@@ -1739,7 +1739,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         host_mirror = false;
         trial_fold_ok = false;
     }
-    fold_init = dest_diag_all && use_dest && nranks == 1 && nG == 0 && !rs_on && nRpad == nR &&
+    fold_init = dest_diag_all && use_dest && nG == 0 && !rs_on && nRpad == nR &&
                 (pc_uniform == 6 || pc_uniform == 7);
     MMBA_HIP(hipHostMalloc(&h_fail, sizeof(int)));
     MMBA_HIP(hipHostMalloc(&h_xstage, sizeof(double) * std::max(n, 1)));
@@ -2061,7 +2061,12 @@ void Plan::setup_band(int Pforce) {
 // rest, whose collectives would then differ).
 bool Plan::sep_form(int w) {
     if (nranks <= 1 || nG != 0 || w > 23 || w <= 0) return false;
-    if (path_choice(MMBA_PATH_SHARD_SEP) == 0 || path_choice(MMBA_PATH_SHARD_BCR) == 0) return false;
+    // round 5: measured slower than the whole-S form at 2, 4 and 8 shards
+    // (profiles/r5_sep: its interior reduction, two multi-column right-hand
+    // side passes and the one-workgroup separator chain cost more per damped
+    // solve than the all-reduce of S plus one reduction of the whole system),
+    // so it is taken only when pinned (MMBA_PATH_SHARD_SEP = 1)
+    if (path_choice(MMBA_PATH_SHARD_SEP) != 1 || path_choice(MMBA_PATH_SHARD_BCR) == 0) return false;
     const int K = std::max(8, (w + 7) / 8 * 8);
     int most = 0;
     for (size_t k = 0; k < Ra_all.size(); ++k) {

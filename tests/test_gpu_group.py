@@ -90,15 +90,12 @@ def test_group_fused_jacobian_shards(nshards, wc, gpu_ctx):
     """Shards of >= 256 camera-frames take the fused Jacobian + camera-frame
     normal-equation pass (k_jac_ne_u, the bench scene's path; the smaller
     sharded scenes take the split passes): 256 frames per shard at a fifth of
-    the C4 bundle density.  First full step against the unsharded solve:
-    every ||f|| at 1e-7 and x at 1e-6 -- on the C4 spec at 2 shards and on
-    the 6-frame variant (the partitioned band form) at 4; on the C4 spec at
-    4 shards the separator form eliminates in another order than the
-    unsharded parallel cyclic reduction and x parts by cond(J^T J) eps (the
-    bar of test_gpu_sharded.test_sharded_ba_x_before_the_valley), so there the
-    whole run is checked: the first five ||f|| at 1e-6 and the final cost at
-    1e-3 (a wrong block or a missing gradient term diverges at the first
-    step: 1.2e9 against 476)."""
+    the C4 bundle density, and the 6-frame variant (the partitioned band
+    form).  First full step against the unsharded solve: every ||f|| at 1e-7
+    and x at 1e-6 (the default whole-S form runs the unsharded solver on the
+    all-reduced S); then the whole run's first five ||f|| at 1e-6 and the
+    final cost at 1e-3 (a wrong block or a missing gradient term diverges at
+    the first step: 1.2e9 against 476)."""
     kw = dict(window=6, depth=(4.0, 10.0)) if wc else {}
     prob = S.make_config(3, frames=256 * nshards, scale=0.1 * nshards, **kw)
     for it in (2, 60):
@@ -108,8 +105,7 @@ def test_group_fused_jacobian_shards(nshards, wc, gpu_ctx):
         assert shards == nshards
         if it == 2:
             np.testing.assert_allclose(g.fnorm_trace, ref.fnorm_trace, rtol=1e-7)
-            if nshards == 2 or wc:
-                assert np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3)) <= 1e-6
+            assert np.max(np.abs(g.x - ref.x) / np.maximum(np.abs(ref.x), 1e-3)) <= 1e-6
         else:
             np.testing.assert_allclose(g.fnorm_trace[:5], ref.fnorm_trace[:5], rtol=1e-6)
             assert abs(g.result["error_final"] - ref.result["error_final"]) <= \

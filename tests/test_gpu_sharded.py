@@ -85,7 +85,7 @@ def check_shards_agree(outs):
 # log-depth solvers on every shard (MMBA_PATH_SHARD_SEP = 0), or the
 # partitioned band chains with an all-reduced separator system
 # (MMBA_PATH_SHARD_BCR = 0)
-SOLVES = {"separator": {}, "whole": {abi.PATH_SHARD_SEP: 0},
+SOLVES = {"separator": {abi.PATH_SHARD_SEP: 1}, "whole": {},
           "partitioned": {abi.PATH_SHARD_BCR: 0}}
 
 
@@ -236,7 +236,7 @@ def test_sharded_ba_x_before_the_valley(scene, nshards, order, solve, gpu_ctx, p
 
 
 @pytest.mark.parametrize("nshards", [4, 8])
-def test_separator_form_well_conditioned(nshards, gpu_ctx):
+def test_separator_form_well_conditioned(nshards, gpu_ctx, paths):
     """The separator form at 4 and 8 shards held to the 1e-6 x bar itself
     (ADVICE r4): the C4 spec's 4-frame tracks (half bandwidth 23, so the
     separator form applies) with the bundles near the camera (depth 4-10
@@ -251,6 +251,7 @@ def test_separator_form_well_conditioned(nshards, gpu_ctx):
     finally:
         s.close()
     bsol = []
+    pin_solve(paths, "separator")
     outs = run_sharded(prob, opt, nshards, band_solver=bsol)
     check_shards_agree(outs)
     assert bsol == [4] * nshards, bsol

@@ -18,8 +18,8 @@ cap = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 frames = int(sys.argv[3]) if len(sys.argv) > 3 else 500 * n
 prob = S.make_config(3, frames=frames, scale=frames / 500.0)
 opt = S.config_options(prob, iterations=cap)
-runs = [("unsharded", None, {}), ("separator", n, {}),
-        ("whole", n, {abi.PATH_SHARD_SEP: 0}), ("partitioned", n, {abi.PATH_SHARD_BCR: 0})]
+runs = [("unsharded", None, {}), ("whole (default)", n, {}),
+        ("separator", n, {abi.PATH_SHARD_SEP: 1}), ("partitioned", n, {abi.PATH_SHARD_BCR: 0})]
 ref = None
 for name, shards, pins in runs:
     for k, v in pins.items():
