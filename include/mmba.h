@@ -646,7 +646,9 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       system in its separator form (each shard's interior
                                       eliminated, the separator system all-reduced) instead
                                       of all-reducing it whole (the default since ABI 9) */
-#define MMBA_PATH_NUM 10
+#define MMBA_PATH_TRIAL_RECORDS 10 /* 0: the trial point's records in their own launch instead
+                                      of inside the trial's back substitution */
+#define MMBA_PATH_NUM 11
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -34,7 +34,8 @@ PATH_PERFRAME_BATCH = 6
 PATH_LOCAL_RING = 7
 PATH_PROBE = 8
 PATH_SHARD_SEP = 9
-PATH_NUM = 10
+PATH_TRIAL_RECORDS = 10
+PATH_NUM = 11
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1

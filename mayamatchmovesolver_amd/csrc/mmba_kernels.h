@@ -271,8 +271,18 @@ struct TrialFold {
     int rstride = 0;
     // sharded: the parameters this shard counts in ||D p||^2, ||D x_new||^2
     const int *own = nullptr;
+    // rec (trial_records_ok): the trial point's record set is built here too
+    // -- bundle records by the bundle's thread, camera-frame records by the
+    // camera-frame's workgroup after its parameters -- and k_records is not
+    // launched; the other parameters are then exactly the camera-frames'
+    int rec = 0;
+    double *recs = nullptr, *brec = nullptr;
 };
-int trial_fold_parts(const DevProblem &P, int nother);
+// Whether the trial's records can be built inside the back substitution: no
+// global parameter (every non-bundle parameter belongs to one camera-frame),
+// camera records from the per-camera-frame table, no rolling shutter.
+bool trial_records_ok(const DevProblem &P);
+int trial_fold_parts(const DevProblem &P, int nother, bool rec = false);
 void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,
                     double *U);
 void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,

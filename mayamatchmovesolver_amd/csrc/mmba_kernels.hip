@@ -2713,6 +2713,33 @@ __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double
                     trial_one(P, T, j, xb[a], pn, xn);
                 }
         }
+        // the bundle's record at the trial point (k_records' arithmetic; this
+        // thread just set its parameters)
+        if (T.rec && b < P.nB) bnd_record_thread(P, b, T.ext_pert, T.step, T.brec, 0);
+    } else if (T.rec) {
+        // four camera-frames per workgroup, 16 threads each: the trial values
+        // of the camera-frame's parameters, then (after the barrier) its base
+        // and variant records, as k_records builds them (measured: these
+        // workgroups first in the grid, 18.4-19.1 us against 17.4-17.9 us)
+        const int cf = ((int)blockIdx.x - nbb) * 4 + (int)(threadIdx.x >> 4);
+        const int v = threadIdx.x & 15;
+        int off = 0, nv = -1;
+        if (cf < P.ncf) {
+            off = P.cf_var_off[cf];
+            nv = P.cf_var_off[cf + 1] - off - 1;
+        }
+        if (v < nv) {
+            const int j = P.cf_var_param[off + 1 + v];
+            trial_one(P, T, j, x[j], pn, xn);
+        }
+        __syncthreads();
+        if (v <= nv) {
+            const int p = P.cf_var_param[off + v];  // -1: the base record
+            const long long ov_idx = p >= 0 ? P.p_vidx[p] : -1;
+            const double ov_val = p >= 0 ? T.ext_pert[p] : 0.;
+            camera_record_fast(P, cf, ov_idx, ov_val, &T.recs[(size_t)(off + v) * CAMREC],
+                               p >= 0 ? P.p_attr[p] : -1);
+        }
     } else {
         const int k = (blockIdx.x - nbb) * blockDim.x + threadIdx.x;
         if (k < T.nother) {
@@ -3044,15 +3071,19 @@ __global__ void k_unpermute(int M, const int *__restrict__ ref_of_dev,
 namespace mmba {
 
 static inline int nblk(long n, int bs) { return (int)((n + bs - 1) / bs); }
-int trial_fold_parts(const DevProblem &P, int nother) {
-    return nblk(P.nB, 64) + nblk(nother, 64);
+bool trial_records_ok(const DevProblem &P) {
+    return P.nG == 0 && P.cf_aidx != nullptr && !P.rs && P.ncf > 0;
+}
+
+int trial_fold_parts(const DevProblem &P, int nother, bool rec) {
+    return nblk(P.nB, 64) + (rec ? (P.ncf + 3) / 4 : nblk(nother, 64));
 }
 
 void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,
                           const double *Lb, const double *xR, const double *U, double *x,
                           const TrialFold &T) {
     const int nbb = nblk(P.nB, 64);
-    const int g = nbb + nblk(T.nother, 64);
+    const int g = trial_fold_parts(P, T.nother, T.rec != 0);
     if (g > 0) k_backsub_trial<<<g, 64, 0, s>>>(P, U, Wg, tb, Lb, xR, x, nbb, T);
 }
 

@@ -434,13 +434,16 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     // the parameter pass ran in the damped solve's back substitution, or here
-    const int tparts = trial_folded ? trial_fold_parts(P, n_trial_other) : nparts;
+    const int tparts = trial_folded ? trial_fold_parts(P, n_trial_other, trial_rec) : nparts;
     if (!trial_folded)
         launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
                           opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
     if (b15) launch_b15_rot(s, P, d_q15, d_wa1, d_p15);  // p in the rotated basis of J
     params_at = d_wa2;  // x <- wa2 on acceptance: the next Jacobian skips k_param_set
-    records_enqueue(d_wa2, 0);  // ... and k_records
+    if (trial_folded && trial_rec)
+        recs_full_at = d_wa2;  // built by the back substitution
+    else
+        records_enqueue(d_wa2, 0);  // ... and k_records
     span_begin(SPAN_RESID);
     launch_rows_eval(s, P, d_ftrial + 2 * (size_t)M, eu + 2 * (size_t)M, pr + 2 * (size_t)pw,
                      (M + 255) / 256, d_Jrow, d_wa1, pr + 3 * (size_t)pw);
@@ -690,6 +693,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             T.partial = d_partial + 3 * (size_t)pw;
             T.rstride = pw;
             T.own = d_p_own;
+            T.rec = trial_rec ? 1 : 0;
+            T.recs = d_recs;
+            T.brec = d_brec;
             launch_backsub_trial(s, PS, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
             trial_folded = true;
             params_at = nullptr;  // the attribute block now holds the trial point

@@ -1631,6 +1631,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         n_trial_other = (int)other.size();
         d_trial_other = upload(other.empty() ? std::vector<int>(1, 0) : other);
         pw = std::max(pw, trial_fold_parts(P, n_trial_other));
+        pw = std::max(pw, trial_fold_parts(P, n_trial_other, true));
     }
     d_partial = dalloc<double>((size_t)8 * pw);  // rows 0..7 (launch_dist_stats: 0..2)
     d_scalar = dalloc<double>(NSLOT);
@@ -1738,6 +1739,19 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     if (b15) {  // the rank-one term corrects ||J p|| after the trial's reduction
         host_mirror = false;
         trial_fold_ok = false;
+    }
+    {
+        // the trial's records inside its back substitution: every non-bundle
+        // parameter is one camera-frame's (its workgroup sets it, then builds
+        // that camera-frame's records), at most 15 per camera-frame (16 lanes)
+        int maxpc = 0, sumpc = 0;
+        for (int cf = 0; cf < ncf; ++cf) {
+            maxpc = std::max(maxpc, cf_pc[cf]);
+            sumpc += cf_pc[cf];
+        }
+        trial_rec = trial_fold_ok && nranks == 1 && trial_records_ok(P) && maxpc <= 15 &&
+                    sumpc == n_trial_other && nvar == ncf + sumpc &&
+                    path_choice(MMBA_PATH_TRIAL_RECORDS) != 0;
     }
     fold_init = dest_diag_all && use_dest && nG == 0 && !rs_on && nRpad == nR &&
                 (pc_uniform == 6 || pc_uniform == 7);

@@ -453,6 +453,9 @@ struct Plan {
     // substitution of the damped solve (launch_backsub_trial);
     // otherwise k_trial_prep
     bool trial_fold_ok = false, trial_folded = false;
+    // the folded trial pass also builds the trial point's records (no
+    // k_records launch; TrialFold::rec)
+    bool trial_rec = false;
     int *d_trial_other = nullptr;
     int n_trial_other = 0;
     bool pre_jac = true;

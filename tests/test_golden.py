@@ -71,7 +71,11 @@ def test_full_fixture_scene_digest(name):
         assert abs(np.linalg.norm(d["exp_fvec"]) - float(d["res_error_final"])) <= \
             1e-12 * float(d["res_error_final"])
     assert d["exp_trace"].size == int(d["res_function_evals"])
-    assert int(d["envelope_runs"]) >= 1
+    # an envelope, where the fixture has one, is the registered one; a fixture
+    # without one (envelope_runs 0) is held at the flat 1e-6 bar on the GPU
+    if int(d["envelope_runs"]) > 0 and "envelope_seeds" in d:
+        from tests.golden.envelopes import SEEDS
+        assert tuple(d["envelope_seeds"]) == SEEDS and int(d["envelope_runs"]) == len(SEEDS)
 
 
 # ---- waypoint one-step fixtures (tests/golden/make_steps.py): the scene

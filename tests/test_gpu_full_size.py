@@ -3,7 +3,9 @@ HIP solve through the C ABI against the CPU oracle's committed outputs
 (tests/golden/full, make_full_golden.py) on the FULL configurations --
 C2 (1 camera x 120 frames, 840 parameters, 397,530 residuals) and C5 (2
 cameras x 240 frames + a 3DE classic lens, 2,882 parameters, 241,146
-residuals), one LM step each (the reference's call with iterMax 2) -- and on
+residuals), one LM step each (the reference's call with iterMax 2), C5 with
+its rolling shutter at rs 0.5 (the bench's C5-RS line; c5rs_full_it1, the
+oracle's one step took 62 min) -- and on
 full-density C4 frame windows (F' = 24: 7,335 parameters, one step; F' = 10:
 the whole run).  Bar (north star): same reason code and evaluation counts,
 every ||f|| of the trace within 1e-6 relative, x within 1e-6 relative (or
