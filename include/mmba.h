@@ -648,7 +648,10 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       of all-reducing it whole (the default since ABI 9) */
 #define MMBA_PATH_TRIAL_RECORDS 10 /* 0: the trial point's records in their own launch instead
                                       of inside the trial's back substitution */
-#define MMBA_PATH_NUM 11
+#define MMBA_PATH_LENS_CF 11       /* 0: every lens coefficient a global parameter (an
+                                      animated one read by one camera-frame's rows joins
+                                      that camera-frame's block otherwise) */
+#define MMBA_PATH_NUM 12
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -35,7 +35,8 @@ PATH_LOCAL_RING = 7
 PATH_PROBE = 8
 PATH_SHARD_SEP = 9
 PATH_TRIAL_RECORDS = 10
-PATH_NUM = 11
+PATH_LENS_CF = 11
+PATH_NUM = 12
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1

@@ -246,7 +246,10 @@ struct SView {
 enum ParamClass : int { PC_CF = 0, PC_B = 1, PC_G = 2 };
 
 // Flags on camera-variant entries.
-enum VarFlags : int { VF_BUNDLE_SIDE = 1 };
+// VF_LENS: the variant is a lens coefficient of the camera-frame (an
+// animated coefficient only its own camera-frame's rows read, Plan::build):
+// its camera record is the base one and its column perturbs the lens
+enum VarFlags : int { VF_BUNDLE_SIDE = 1, VF_LENS = 2 };
 
 // Device view of the problem + derived structure (all device pointers).
 struct DevProblem {

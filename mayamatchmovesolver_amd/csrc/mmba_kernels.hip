@@ -700,6 +700,24 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
         const int t = voff + v;
         const int p = P.cf_var_param[t];
         const bool bside = (P.cf_var_flags[t] & VF_BUNDLE_SIDE) != 0;
+        if (P.cf_var_flags[t] & VF_LENS) {
+            // a lens coefficient in the camera-frame block: the lens loop's
+            // column (below), at its place in the block -- where this
+            // observation's lens instance holds the coefficient (B3 may give
+            // it an instance another frame's parameter wrote: then f - f = 0)
+            bool holds = false;
+            if (hl)
+                for (int q = P.inst_lpar_off[inst]; q < P.inst_lpar_off[inst + 1]; ++q)
+                    holds |= P.inst_lpar[q] == p;
+            double lc[MMBA_LENS_NUM_ATTRS];
+            if (holds) inst_coeffs(P, inst, Override{P.p_attr[p], ext_pert[p]}, lc);
+            emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, holds ? lc : lc0), step[p], [&]() {
+                double lq[MMBA_LENS_NUM_ATTRS];
+                if (holds) inst_coeffs(P, inst, Override{P.p_attr[p], CB.ext_pert[p]}, lq);
+                return residual_l(P, rec0, bp0, mx, my, sw, hl, holds ? lq : lc0);
+            });
+            continue;
+        }
         double bp[3] = {bp0[0], bp0[1], bp0[2]};
         if (bside) bundle_position(P, b, fr, Override{P.p_attr[p], ext_pert[p]}, bp);
         emit_s(p, residual_l(P, &recs[(size_t)t * CAMREC], bp, mx, my, sw, hl, lc0), step[p],
@@ -792,6 +810,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
             // (adjust_solveFunc.cpp frameIndexEnable): the observations of
             // other frames that read the instance it writes keep f - f = 0
             if (P.p_frame[p] >= 0 && P.p_frame[p] != fr) continue;
+            if (P.p_class[p] == PC_CF) continue;  // a camera-frame block column (VF_LENS)
             double lc[MMBA_LENS_NUM_ATTRS];
             inst_coeffs(P, inst, Override{P.p_attr[p], ext_pert[p]}, lc);
             emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, lc), step[p], [&]() {

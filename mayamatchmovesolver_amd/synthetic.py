@@ -320,7 +320,7 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                 scene_graph_mode=abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH, window: int = 4,
                 depth=(20.0, 200.0), lens_model: str = "classic",
                 init_noise: float = 1.0, obs_noise: float = 1.0,
-                rolling_shutter: float = 0.0) -> Problem:
+                rolling_shutter: float = 0.0, cameras: int = 2) -> Problem:
     """Concrete synthetic input for BASELINE.json ``configs[index]``.
 
     ``frames`` / ``scale`` shrink a configuration (frame-window subsets and
@@ -345,6 +345,9 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
     SURVEY 8(f) row 2.
     ``rolling_shutter`` (configs[4] only): rs in frames (time shift x fps),
     the configs[4] "rolling-shutter per-scanline pose" (mmba.h ABI 3; 0 = off).
+    ``cameras`` (configs[4] only): cameras sharing the lens (the spec's 2; 1
+    gives the one-camera shot whose animated lens coefficients each reach one
+    camera-frame).
     """
     rng = np.random.Generator(np.random.PCG64(20241008 + index))
     if index == 0:
@@ -360,7 +363,7 @@ def make_config(index: int, frames: int | None = None, scale: float = 1.0,
                           K=int(50000 * scale), window=window, per_cam_markers=False,
                           depth=depth, init_noise=init_noise, obs_noise=obs_noise)
     if index == 4:
-        return _config_c5(rng, frames or 240, scale, lens_model, rolling_shutter)
+        return _config_c5(rng, frames or 240, scale, lens_model, rolling_shutter, cameras)
     raise KeyError(index)
 
 
@@ -677,16 +680,16 @@ def _config_ba(rng, index, n_cams, F, B, K, window, per_cam_markers, depth=(20.0
                          meta={"name": CONFIG_NAMES[index]})
 
 
-def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0):
+def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0, n_cams=2):
     """2 cams, 1k locked bundles, 2k markers (1k per cam), windows mean 60,
     one shared 3DE-classic lens with distortion + quartic solved (lens attrs first).
     ``rolling_shutter`` = rs (frames, time shift x fps) != 0: both cameras
     have that rolling shutter (mmba.h ABI 3) and the markers are synthesised
     through the same per-scanline pose blend."""
     B, K = max(1, int(1000 * scale)), max(2, int(2000 * scale))
-    ts, rs = zip(*[_camera_path(rng, F, c) for c in range(2)])
+    ts, rs = zip(*[_camera_path(rng, F, c) for c in range(n_cams)])
     P = _bundles_in_front(rng, B)
-    mkr_cam = np.repeat(np.arange(2), K // 2)
+    mkr_cam = np.repeat(np.arange(n_cams), K // n_cams)
     K = mkr_cam.size
     mkr_bnd = np.arange(K) % B
     start, length = _windows(rng, K, F, 60)
@@ -725,7 +728,7 @@ def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0):
     def proj(ks, fs):
         mx = np.empty(ks.size)
         my = np.empty(ks.size)
-        for c in range(2):
+        for c in range(n_cams):
             sel = mkr_cam[ks] == c
             mx[sel], my[sel] = _pose_project(ts[c], rs[c], FOCAL_MM, P[mkr_bnd[ks[sel]]], fs[sel])
             if rolling_shutter:
@@ -749,11 +752,12 @@ def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0):
     ks, fs, xy = _obs_from_windows(rng, start, length, proj)
     t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
     r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
-    prob = _bulk_problem(F, t0, r0, [FOCAL_MM, FOCAL_MM], lambda tids, cids: list(tids[:6]),
+    prob = _bulk_problem(F, t0, r0, [FOCAL_MM] * n_cams, lambda tids, cids: list(tids[:6]),
                          P, np.zeros(B, bool), mkr_cam, mkr_bnd, ks, fs, xy, lens=lens,
                          lens_first=True,
                          meta={"name": CONFIG_NAMES[4] + ("" if lens_model == "classic"
                                                           else "_" + lens_model) +
+                               ("" if n_cams == 2 else "_%dcam" % n_cams) +
                                ("_rs" if rolling_shutter else "")})
     if rolling_shutter:
         prob.cam_rs_value = np.full(prob.num_cameras, float(rolling_shutter))
