@@ -229,7 +229,9 @@ def pmc_traffic(args):
 # Full-density frame windows of the workload timed on the CPU: the same
 # scene generator with the window's share of bundles (C4: 100 new bundles per
 # frame, each tracked over 4 frames), i.e. the full C4 density on F' frames.
-CPU_WINDOWS = {3: (5, 10), 2: (2, 3), 1: (2, 3), 4: (2, 3), 0: (10,)}
+# Sized so the largest window's oracle iteration takes ~10-30 s (cost ~ F'^3:
+# the full C2 iteration is ~980 s on 120 frames, the full C5 ~3,860 s on 240).
+CPU_WINDOWS = {3: (5, 10), 2: (2, 3), 1: (12, 32), 4: (16, 40), 0: (10,)}
 
 
 def _pinned_core():
