@@ -1933,7 +1933,10 @@ void Plan::setup_band(int Pforce) {
                     // publications (levels 0..L-1): P^T [P rho], Q^T [Q rho], Q^T P;
                     // logs (levels 0..L): C^-1, P, Q; right-hand-side pass: 2 K
                     const size_t ps = (size_t)2 * Q.K * (Q.K + 1) + (size_t)Q.K * Q.K;
-                    Q.pub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * ps));
+                    // 16-B granules, one per published double; zeroed (no
+                    // stale tag can match: epochs start at 1)
+                    Q.pub = dalloc<double>(std::max<size_t>(1, (size_t)2 * L * Q.nblk * ps));
+                    MMBA_HIP(hipMemsetAsync(Q.pub, 0, sizeof(double) * std::max<size_t>(1, (size_t)2 * L * Q.nblk * ps), s));
                     Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
                     Q.rpub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * 2 * Q.K));
                     Q.part = dalloc<double>(Q.nblk);
@@ -2071,7 +2074,8 @@ void Plan::setup_band(int Pforce) {
         Q.Bd = bs.Bd + (size_t)hp.r0 * (w + 1);
         const size_t ps = (size_t)2 * Q.K * (Q.K + 1) + (size_t)Q.K * Q.K;
         const size_t nl = std::max<size_t>(1, (size_t)L * Q.nblk);
-        Q.pub = dalloc<double>(nl * ps);
+        Q.pub = dalloc<double>(2 * nl * ps);  // 16-B granules (k_pcr_solve), zeroed
+        MMBA_HIP(hipMemsetAsync(Q.pub, 0, sizeof(double) * 2 * nl * ps, s));
         Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
         Q.rpub = dalloc<double>(nl * 2 * Q.K);
         Q.mpub = dalloc<double>(nl * 2 * Q.K * PCR_NCMAX);

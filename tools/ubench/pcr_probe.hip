@@ -39,7 +39,8 @@ int main(int argc, char **argv) {
     hipMemcpy(dBd, Bd.data(), Bd.size() * 8, hipMemcpyHostToDevice);
     P.Bd = dBd;
     const size_t ps = (size_t)2 * K * (K + 1) + K * K;
-    hipMalloc(&P.pub, (size_t)L * P.nblk * ps * 8);
+    hipMalloc(&P.pub, (size_t)2 * L * P.nblk * ps * 8);  // 16-B granules
+    hipMemset(P.pub, 0, (size_t)2 * L * P.nblk * ps * 8);
     hipMalloc(&P.wlog, (size_t)(L + 1) * P.nblk * 3 * K * K * 8);
     hipMalloc(&P.rpub, (size_t)L * P.nblk * 2 * K * 8);
     hipMalloc(&P.part, P.nblk * 8);
