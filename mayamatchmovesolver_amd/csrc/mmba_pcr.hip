@@ -388,7 +388,9 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
                                                 unsigned epoch, int *fail) {
     constexpr int LS = pcr_log_size<K>();
     __shared__ double sr[K], srho[K];
+    __shared__ int late_s;
     const int lane = threadIdx.x, j = blockIdx.x, nblk = P.nblk, nb = P.nb;
+    if (lane == 0) late_s = 0;
     const int R = j * K + lane;
     const double w0 = (lane < K && R < nb) ? w[R] : 0.;
     double r = w0;
@@ -406,25 +408,46 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
             srho[lane] = rho;
         }
         __syncthreads();
-        double *rp = P.rpub + ((size_t)lvl * nblk + j) * 2 * K;
-        if (lane < K) {  // (Q^T rho)_c, (P^T rho)_c
+        // publications: 2 K granules per (level, block) (k_pcr_solve's
+        // data-tagged hand-off): (Q^T rho)_c for the right consumer, (P^T
+        // rho)_c for the left one
+        const auto gpub = sc1_view(P.rpub + ((size_t)lvl * nblk + j) * 4 * K, 2 * K * 16u);
+        if (lane < K) {
             double a = 0., b = 0.;
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 a = fma(lg[2 * K * K + i * K + lane], srho[i], a);
                 b = fma(lg[K * K + i * K + lane], srho[i], b);
             }
-            if (hq) bcr_st(rp + lane, a);
-            if (hp) bcr_st(rp + K + lane, b);
+            if (hq) gran_st(gpub, lane, a, epoch);
+            if (hp) gran_st(gpub, K + lane, b, epoch);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane < K) {  // r -= Q_p^T rho_p + P_q^T rho_q, from the neighbours' granules
+            const auto vp = sc1_view(P.rpub + ((size_t)lvl * nblk + (hp ? j - s : j)) * 4 * K,
+                                     hp ? 2 * K * 16u : 0u);
+            const auto vq = sc1_view(P.rpub + ((size_t)lvl * nblk + (hq ? j + s : j)) * 4 * K,
+                                     hq ? 2 * K * 16u : 0u);
+            pcr_u4 gp{}, gq{};
+            if (hp) gp = gran_ld(vp, lane);
+            if (hq) gq = gran_ld(vq, K + lane);
+            for (unsigned spins = 0;; ++spins) {
+                const bool okp = !hp || gran_ok(gp, epoch), okq = !hq || gran_ok(gq, epoch);
+                if (okp && okq) break;
+                if (spins > (1u << 20)) {
+                    late_s = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                if (!okp) gp = gran_ld(vp, lane);
+                if (!okq) gq = gran_ld(vq, K + lane);
+            }
+            double sub = 0.;
+            if (hp) sub += gran_val(gp);
+            if (hq) sub += gran_val(gq);
+            r -= sub;
+        }
         __syncthreads();
-        if (lane == 0)
-            __hip_atomic_store((bcr_gu32 *)(P.rflag + (size_t)lvl * nblk + j), epoch,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool ok = pcr_wait(P.rflag + (size_t)lvl * nblk, hp ? j - s : -1, hq ? j + s : -1,
-                                 epoch);
-        if (!ok) {
+        if (late_s) {
             // a timed-out wait: the partial is NaN, so the Newton term that
             // sums it cannot pass for a number (lmpar_ne restarts on it)
             if (lane == 0) {
@@ -433,13 +456,6 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
             }
             return;
         }
-        if (lane < K) {  // r -= Q_p^T rho_p + P_q^T rho_q
-            double sub = 0.;
-            if (hp) sub += bcr_ld(P.rpub + ((size_t)lvl * nblk + j - s) * 2 * K + lane);
-            if (hq) sub += bcr_ld(P.rpub + ((size_t)lvl * nblk + j + s) * 2 * K + K + lane);
-            r -= sub;
-        }
-        __syncthreads();
     }
     // z = C^-T C^-1 r with the final level's factor
     const double *lg = P.wlog + ((size_t)L * nblk + j) * LS;

@@ -1938,7 +1938,8 @@ void Plan::setup_band(int Pforce) {
                     Q.pub = dalloc<double>(std::max<size_t>(1, (size_t)2 * L * Q.nblk * ps));
                     MMBA_HIP(hipMemsetAsync(Q.pub, 0, sizeof(double) * std::max<size_t>(1, (size_t)2 * L * Q.nblk * ps), s));
                     Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
-                    Q.rpub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * 2 * Q.K));
+                    Q.rpub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * 4 * Q.K));  // granules
+                    MMBA_HIP(hipMemsetAsync(Q.rpub, 0, sizeof(double) * std::max<size_t>(1, (size_t)L * Q.nblk * 4 * Q.K), s));
                     Q.part = dalloc<double>(Q.nblk);
                     Q.fflag = dalloc<int>(std::max<size_t>(1, (size_t)L * Q.nblk));
                     Q.rflag = dalloc<int>(std::max<size_t>(1, (size_t)L * Q.nblk));
@@ -2077,7 +2078,8 @@ void Plan::setup_band(int Pforce) {
         Q.pub = dalloc<double>(2 * nl * ps);  // 16-B granules (k_pcr_solve), zeroed
         MMBA_HIP(hipMemsetAsync(Q.pub, 0, sizeof(double) * 2 * nl * ps, s));
         Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
-        Q.rpub = dalloc<double>(nl * 2 * Q.K);
+        Q.rpub = dalloc<double>(nl * 4 * Q.K);  // granules (k_pcr_rhs), zeroed
+        MMBA_HIP(hipMemsetAsync(Q.rpub, 0, sizeof(double) * nl * 4 * Q.K, s));
         Q.mpub = dalloc<double>(nl * 2 * Q.K * PCR_NCMAX);
         Q.part = dalloc<double>(Q.nblk);
         Q.fflag = dalloc<int>(nl);

@@ -1,5 +1,5 @@
 set -o pipefail
-OUT=gpurun_out/r5_gran
+OUT=${1:-gpurun_out/r5_gran}
 mkdir -p $OUT
 (cd tools/ubench && timeout -k 10 60 ./pcr_probe 2994 > ../../$OUT/probe.txt 2>&1) || { cat $OUT/probe.txt; exit 1; }
 cat $OUT/probe.txt

@@ -42,7 +42,8 @@ int main(int argc, char **argv) {
     hipMalloc(&P.pub, (size_t)2 * L * P.nblk * ps * 8);  // 16-B granules
     hipMemset(P.pub, 0, (size_t)2 * L * P.nblk * ps * 8);
     hipMalloc(&P.wlog, (size_t)(L + 1) * P.nblk * 3 * K * K * 8);
-    hipMalloc(&P.rpub, (size_t)L * P.nblk * 2 * K * 8);
+    hipMalloc(&P.rpub, (size_t)L * P.nblk * 4 * K * 8);  // 16-B granules
+    hipMemset(P.rpub, 0, (size_t)L * P.nblk * 4 * K * 8);
     hipMalloc(&P.part, P.nblk * 8);
     hipMalloc(&P.fflag, (size_t)L * P.nblk * 4);
     hipMalloc(&P.rflag, (size_t)L * P.nblk * 4);
