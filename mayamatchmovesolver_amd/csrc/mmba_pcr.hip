@@ -496,16 +496,20 @@ __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__re
                                                     int *fail) {
     constexpr int LS = pcr_log_size<K>();
     constexpr int NS = PCR_NCMAX + 1;  // LDS row stride
+    constexpr int QN = (K * PCR_NCMAX + 255) / 256;  // entries per thread
     __shared__ double sr[K * NS], srho[K * NS], sl[3 * K * K];
     __shared__ int ok_s;
     const int tid = threadIdx.x, j = blockIdx.x, nblk = P.nblk, nb = P.nb;
+    if (tid == 0) ok_s = 1;
     const int ne = K * nc;  // entries (row i, column c) of the block's right-hand sides
     for (int q = tid; q < ne; q += 256) {
         const int i = q / nc, c = q % nc, row = j * K + i;
         sr[i * NS + c] = row < nb ? R[(size_t)c * ldr + row] : 0.;
     }
     const int L = min(max(P.flev[j], 0), P.nlev);
-    const size_t pst = (size_t)2 * K * PCR_NCMAX;  // doubles of one (level, block) publication
+    // one (level, block) publication: 2 K PCR_NCMAX granules (k_pcr_solve's
+    // data-tagged hand-off), 4 K PCR_NCMAX doubles
+    const size_t pst = (size_t)4 * K * PCR_NCMAX;
     int s = 1;
     for (int lvl = 0;; ++lvl, s *= 2) {
         const double *lg = P.wlog + ((size_t)lvl * nblk + j) * LS;
@@ -531,7 +535,7 @@ __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__re
             return;
         }
         const bool hp = j - s >= 0, hq = j + s < nblk;
-        double *mp = mpub + ((size_t)lvl * nblk + j) * pst;
+        const auto gmp = sc1_view(mpub + ((size_t)lvl * nblk + j) * pst, 2 * K * PCR_NCMAX * 16u);
         // (Q^T rho) for the right consumer, (P^T rho) for the left one
         for (int q = tid; q < ne; q += 256) {
             const int i = q / nc, c = q % nc;
@@ -541,18 +545,52 @@ __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__re
                 a = fma(sl[2 * K * K + k * K + i], srho[k * NS + c], a);
                 b = fma(sl[K * K + k * K + i], srho[k * NS + c], b);
             }
-            if (hq) bcr_st(mp + q, a);
-            if (hp) bcr_st(mp + K * PCR_NCMAX + q, b);
+            if (hq) gran_st(gmp, q, a, epoch);
+            if (hp) gran_st(gmp, K * PCR_NCMAX + q, b, epoch);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0)
-            __hip_atomic_store((bcr_gu32 *)(mflag + (size_t)lvl * nblk + j), epoch, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (tid < 64) {
-            const bool ok = pcr_wait(mflag + (size_t)lvl * nblk, hp ? j - s : -1, hq ? j + s : -1,
-                                     epoch);
-            if (tid == 0) ok_s = ok;
+        // R -= Q_p^T rho_p + P_q^T rho_q, from the neighbours' granules
+        const auto vp = sc1_view(mpub + ((size_t)lvl * nblk + (hp ? j - s : j)) * pst,
+                                 hp ? 2 * K * PCR_NCMAX * 16u : 0u);
+        const auto vq = sc1_view(mpub + ((size_t)lvl * nblk + (hq ? j + s : j)) * pst,
+                                 hq ? 2 * K * PCR_NCMAX * 16u : 0u);
+        {
+            pcr_u4 gp[QN], gq[QN];
+#pragma unroll
+            for (int e = 0; e < QN; ++e) {
+                const int q = tid + 256 * e;
+                if (q < ne && hp) gp[e] = gran_ld(vp, q);
+                if (q < ne && hq) gq[e] = gran_ld(vq, K * PCR_NCMAX + q);
+            }
+            for (unsigned spins = 0;; ++spins) {
+                bool all = true;
+#pragma unroll
+                for (int e = 0; e < QN; ++e) {
+                    const int q = tid + 256 * e;
+                    if (q < ne && ((hp && !gran_ok(gp[e], epoch)) || (hq && !gran_ok(gq[e], epoch))))
+                        all = false;
+                }
+                if (all) break;
+                if (spins > (1u << 20)) {
+                    ok_s = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int e = 0; e < QN; ++e) {
+                    const int q = tid + 256 * e;
+                    if (q < ne && hp && !gran_ok(gp[e], epoch)) gp[e] = gran_ld(vp, q);
+                    if (q < ne && hq && !gran_ok(gq[e], epoch)) gq[e] = gran_ld(vq, K * PCR_NCMAX + q);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < QN; ++e) {
+                const int q = tid + 256 * e;
+                if (q >= ne) continue;
+                double sub = 0.;
+                if (hp) sub += gran_val(gp[e]);
+                if (hq) sub += gran_val(gq[e]);
+                sr[(q / nc) * NS + q % nc] -= sub;
+            }
         }
         __syncthreads();
         if (!ok_s) {
@@ -564,16 +602,6 @@ __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__re
             }
             return;
         }
-        // R -= Q_p^T rho_p + P_q^T rho_q
-        const double *pp = mpub + ((size_t)lvl * nblk + (hp ? j - s : j)) * pst;
-        const double *pq = mpub + ((size_t)lvl * nblk + (hq ? j + s : j)) * pst + K * PCR_NCMAX;
-        for (int q = tid; q < ne; q += 256) {
-            double sub = 0.;
-            if (hp) sub += bcr_ld(pp + q);
-            if (hq) sub += bcr_ld(pq + q);
-            sr[(q / nc) * NS + q % nc] -= sub;
-        }
-        __syncthreads();
     }
 }
 

@@ -2080,7 +2080,8 @@ void Plan::setup_band(int Pforce) {
         Q.wlog = dalloc<double>((size_t)(L + 1) * Q.nblk * 3 * Q.K * Q.K);
         Q.rpub = dalloc<double>(nl * 4 * Q.K);  // granules (k_pcr_rhs), zeroed
         MMBA_HIP(hipMemsetAsync(Q.rpub, 0, sizeof(double) * nl * 4 * Q.K, s));
-        Q.mpub = dalloc<double>(nl * 2 * Q.K * PCR_NCMAX);
+        Q.mpub = dalloc<double>(nl * 4 * Q.K * PCR_NCMAX);  // granules (k_pcr_rhs_mc), zeroed
+        MMBA_HIP(hipMemsetAsync(Q.mpub, 0, sizeof(double) * nl * 4 * Q.K * PCR_NCMAX, s));
         Q.part = dalloc<double>(Q.nblk);
         Q.fflag = dalloc<int>(nl);
         Q.rflag = dalloc<int>(nl);
