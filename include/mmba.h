@@ -642,10 +642,11 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
 #define MMBA_PATH_PERFRAME_BATCH 6 /* 0: per-frame mode with one plan per frame */
 #define MMBA_PATH_LOCAL_RING 7     /* 1: in-process communicators sum in ring order */
 #define MMBA_PATH_PROBE 8          /* 1: band / BCR phase probe, printed when the plan is destroyed */
-#define MMBA_PATH_SHARD_SEP 9      /* 1: sharded plans without an arrow solve the reduced
+#define MMBA_PATH_SHARD_SEP 9      /* 1 / 0: sharded plans without an arrow solve the reduced
                                       system in its separator form (each shard's interior
-                                      eliminated, the separator system all-reduced) instead
-                                      of all-reducing it whole (the default since ABI 9) */
+                                      eliminated, the separator system all-reduced) / by
+                                      all-reducing it whole; default: whole while the whole
+                                      band system fits one resident PCR grid */
 #define MMBA_PATH_TRIAL_RECORDS 10 /* 0: the trial point's records in their own launch instead
                                       of inside the trial's back substitution */
 #define MMBA_PATH_LENS_CF 11       /* 0: every lens coefficient a global parameter (an

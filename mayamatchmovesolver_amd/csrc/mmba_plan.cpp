@@ -2109,12 +2109,16 @@ void Plan::setup_band(int Pforce) {
 // rest, whose collectives would then differ).
 bool Plan::sep_form(int w) {
     if (nranks <= 1 || nG != 0 || w > 23 || w <= 0) return false;
-    // round 5: measured slower than the whole-S form at 2, 4 and 8 shards
-    // (profiles/r5_sep: its interior reduction, two multi-column right-hand
-    // side passes and the one-workgroup separator chain cost more per damped
-    // solve than the all-reduce of S plus one reduction of the whole system),
-    // so it is taken only when pinned (MMBA_PATH_SHARD_SEP = 1)
-    if (path_choice(MMBA_PATH_SHARD_SEP) != 1 || path_choice(MMBA_PATH_SHARD_BCR) == 0) return false;
+    // Default (round 5): the whole-S form while the WHOLE band system fits one
+    // resident PCR grid (C4 shards: N <= 4), the separator form beyond -- the
+    // whole system then falls back to block cyclic reduction (142 us at
+    // 998 blocks against PCR's 62 us on one shard's interior; profiles/r5_occ,
+    // r5_gran).  The one-device rehearsal of 2/4/8 shards measured the
+    // separator form slower (profiles/r5_sep), but there the shards' PCR
+    // launches queue behind each other on the one device.  Pinned either way
+    // by MMBA_PATH_SHARD_SEP (0 / 1).
+    const int pin = path_choice(MMBA_PATH_SHARD_SEP);
+    if (pin == 0 || path_choice(MMBA_PATH_SHARD_BCR) == 0) return false;
     const int K = std::max(8, (w + 7) / 8 * 8);
     int most = 0;
     for (size_t k = 0; k < Ra_all.size(); ++k) {
@@ -2131,7 +2135,9 @@ bool Plan::sep_form(int w) {
         sep_resident = (int)-v;
         sep_resident_K = K;
     }
-    return most <= sep_resident;
+    if (most > sep_resident) return false;
+    if (pin == 1) return true;
+    return (nR + K - 1) / K > sep_resident;  // the whole system would not be resident
 }
 
 }  // namespace mmba

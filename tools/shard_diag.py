@@ -18,7 +18,7 @@ cap = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 frames = int(sys.argv[3]) if len(sys.argv) > 3 else 500 * n
 prob = S.make_config(3, frames=frames, scale=frames / 500.0)
 opt = S.config_options(prob, iterations=cap)
-runs = [("unsharded", None, {}), ("whole (default)", n, {}),
+runs = [("unsharded", None, {}), ("default", n, {}), ("whole", n, {abi.PATH_SHARD_SEP: 0}),
         ("separator", n, {abi.PATH_SHARD_SEP: 1}), ("partitioned", n, {abi.PATH_SHARD_BCR: 0})]
 ref = None
 for name, shards, pins in runs:
