@@ -203,20 +203,48 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
                                                 double *x, double *xs, int factor, int *fail) {
     __shared__ double zs[NGMAX * NGMAX], gs[NGMAX];
     const int lane = threadIdx.x, nG = B.nG, nb = B.nb;
-    // sums over blocks: lanes stride, fixed xor tree
-    for (int e = 0; e < nG * NGMAX + NGMAX; ++e) {
-        const bool mat = e < nG * NGMAX;
-        if (mat && e % NGMAX >= nG) continue;
-        if (!mat && e - nG * NGMAX >= nG) continue;
-        if (mat && !factor) continue;
-        double v = 0.;
-        for (int b = lane; b < B.nblk; b += 64)
-            v += mat ? B.Zc[(size_t)b * NGMAX * NGMAX + e] : B.gpart[(size_t)b * NGMAX + (e - nG * NGMAX)];
+    // sums over blocks: lane l adds blocks l, l + 64, ... in that order, then
+    // a fixed xor tree.  Entries are taken RB at a time and each lane's loads
+    // of a round (BK blocks per entry) are issued before its adds: one memory
+    // round trip per round instead of one per block (the additions and their
+    // order are unchanged, so are the bits)
+    constexpr int RB = 4, BK = 8;
+    const int nmat = factor ? nG * nG : 0, ntot = nmat + nG;
+    for (int e0 = 0; e0 < ntot; e0 += RB) {
+        double v[RB];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) {
-            if (mat) zs[e] = v;
-            else gs[e - nG * NGMAX] = v;
+        for (int k = 0; k < RB; ++k) v[k] = 0.;
+        for (int b0 = 0; b0 < B.nblk; b0 += 64 * BK) {
+            double q[RB][BK];
+#pragma unroll
+            for (int k = 0; k < RB; ++k) {
+                const int e = e0 + k;
+                const double *src = e >= ntot ? nullptr
+                                  : e < nmat ? B.Zc + (e / nG) * NGMAX + e % nG
+                                             : B.gpart + (e - nmat);
+                const size_t st = e < nmat ? (size_t)NGMAX * NGMAX : (size_t)NGMAX;
+#pragma unroll
+                for (int t = 0; t < BK; ++t) {
+                    const int b = b0 + lane + 64 * t;
+                    q[k][t] = (src && b < B.nblk) ? src[(size_t)b * st] : 0.;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < RB; ++k)
+#pragma unroll
+                for (int t = 0; t < BK; ++t)
+                    if (b0 + lane + 64 * t < B.nblk) v[k] += q[k][t];
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int e = e0 + k;
+            double w = v[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off);
+            if (lane == 0 && e < ntot) {
+                if (e < nmat) zs[(e / nG) * NGMAX + e % nG] = w;
+                else gs[e - nmat] = w;
+            }
         }
     }
     __syncthreads();
@@ -231,21 +259,25 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
             else if (lane < NGMAX && lane >= nG && c == lane) v = 1.;
             a[c] = v;
         }
-        double rsl = 0.;
+        // rows / columns >= nG are identity padding: their pivots change
+        // nothing, so the chain stops at nG (their 1 / C_jj is 1)
+        double rsl = lane >= nG ? 1. : 0.;
         bool bad = false;
 #pragma unroll
         for (int j = 0; j < NGMAX; ++j) {
-            double d = wave_rdlane(a[j], j);
-            if (!(d > 0.) || !isfinite(d)) {
-                bad = true;
-                d = 1.;
-            }
-            const double rs = wave_rsq(d);
-            const double l = (lane > j) ? a[j] * rs : 0.;
-            a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
-            if (lane == j) rsl = rs;
+            if (j < nG) {  // (wave-uniform)
+                double d = wave_rdlane(a[j], j);
+                if (!(d > 0.) || !isfinite(d)) {
+                    bad = true;
+                    d = 1.;
+                }
+                const double rs = wave_rsq(d);
+                const double l = (lane > j) ? a[j] * rs : 0.;
+                a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
+                if (lane == j) rsl = rs;
 #pragma unroll
-            for (int c = j + 1; c < NGMAX; ++c) a[c] = fma(-l, wave_rdlane(l, c), a[c]);
+                for (int c = j + 1; c < NGMAX; ++c) a[c] = fma(-l, wave_rdlane(l, c), a[c]);
+            }
         }
         if (bad && lane == 0) atomicOr(fail, 1);
         if (lane < NGMAX)
