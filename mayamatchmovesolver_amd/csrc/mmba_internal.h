@@ -113,14 +113,14 @@ constexpr int PCR_NCMAX = 48;
 struct PcrDev {
     int K = 0, nb = 0, w = 0, nblk = 0, nlev = 0;
     const double *Bd = nullptr;  // band input [nb][w+1]
+    // publications of k_pcr_solve / k_pcr_rhs: 16-B granules {value, epoch,
+    // epoch} (zeroed at build; epochs start at 1), per [nlev][nblk]
     double *pub = nullptr, *wlog = nullptr, *rpub = nullptr, *part = nullptr;
-    int *fflag = nullptr, *rflag = nullptr;  // [nlev][nblk] epochs
     int *flev = nullptr;                     // final level of every block
     const int *row_param = nullptr;          // reduced row -> parameter (scatter of x)
-    // several right-hand sides (k_pcr_rhs_mc): publications [nlev][nblk][2 K
-    // PCR_NCMAX] and their epochs
+    // several right-hand sides (k_pcr_rhs_mc): granule publications
+    // [nlev][nblk][2 K PCR_NCMAX]
     double *mpub = nullptr;
-    int *mflag = nullptr;
 };
 
 // Block-diagonal + arrow reduced system (mmba_bdiag.hip): no solved bundle,

@@ -638,7 +638,12 @@ __global__ void __launch_bounds__(256) k_residual_jp_cf(
 // parameters that can change this observation (all other entries of the
 // reference column are exactly zero).
 // -------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__restrict__ recs,
+// CEN: central differences / B15 compiled in (CB.recs != nullptr).  The
+// forward-difference build drops the deltaB evaluations and is held to two
+// waves per SIMD (256 VGPRs, some spilled; one wave at 340 registers before):
+// C5 1.21 against 1.33 ms per solve (profiles/r5_jac/).
+template <bool CEN>
+__global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, const double *__restrict__ recs,
                                                   const double *__restrict__ ext_pert,
                                                   const double *__restrict__ step,
                                                   int solver_type, double *J, int *jcol,
@@ -672,7 +677,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
     // column (CB.step[p] != 0)
     auto emit_s = [&](int p, const Resid &r, double st, auto &&evalB) {
         double jx, jy;
-        const double sB = (lmder && CB.recs) ? CB.step[p] : 0.;
+        const double sB = (CEN && lmder && CB.recs) ? CB.step[p] : 0.;
         if (sB != 0.) {  // central: (f(x + dA) - f(x + dB)) * 0.5 / (|dA| + |dB|)
             const Resid rb = evalB();
             jx = (r.ex - rb.ex) * sB;
@@ -727,7 +732,7 @@ __global__ void __launch_bounds__(128) k_jacobian(DevProblem P, const double *__
                    return residual_l(P, &CB.recs[(size_t)t * CAMREC], bq, mx, my, sw, hl, lc0);
                });
     }
-    if (CB.q15) {
+    if (CEN && CB.q15) {
         // B15 (Plan::b15): the camera-frame block's columns (the first pc
         // emitted) in the basis Q_cf (Q c = kappa e_0): J_s Q = J Q - f kappa
         // e_0^T with J the central differences of the block's own frame.  The
@@ -3355,8 +3360,12 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
         return;
     }
 #undef MMBA_JAC_U
-    k_jacobian<<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J, jcol,
-                                                nloc, stale_param, eu, ed, CB);
+    if (CB.recs)
+        k_jacobian<true><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J,
+                                                      jcol, nloc, stale_param, eu, ed, CB);
+    else
+        k_jacobian<false><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J,
+                                                       jcol, nloc, stale_param, eu, ed, CB);
 }
 // One workgroup per camera-frame only fills the chip with enough
 // camera-frames (C4: 500 x 400 observations); a few long segments (C2: 120 x

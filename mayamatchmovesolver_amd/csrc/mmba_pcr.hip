@@ -93,28 +93,6 @@ __host__ __device__ constexpr int pcr_log_size() {
     return 3 * K * K;
 }
 
-// flags[a] (and flags[b], b >= 0) == epoch, polled by one wave; false after
-// the bound
-__device__ __forceinline__ bool pcr_wait(const int *flags, int a, int b, unsigned epoch) {
-    for (unsigned spins = 0;; ++spins) {
-        unsigned fa = a >= 0 ? __hip_atomic_load((bcr_gu32 *)(flags + a), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)
-                             : epoch;
-        unsigned fb = b >= 0 ? __hip_atomic_load((bcr_gu32 *)(flags + b), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)
-                             : epoch;
-        fa = __builtin_amdgcn_readfirstlane(fa);
-        fb = __builtin_amdgcn_readfirstlane(fb);
-        if (fa == epoch && fb == epoch) break;
-        if (spins > (1u << 22)) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    // every published value is stored and loaded sc1: no agent-scope
-    // acquire; the fence keeps the compiler from hoisting those loads
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    return true;
-}
-
 // ---------------------------------------------------------------------------
 // The damped solve.  blockIdx.x = block j.  r_in / x_out: reduced-order
 // vectors (nb rows); x is also scattered to parameter order (xs[row_param]).
@@ -290,7 +268,8 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
             }
         }
         stamp(lvl, 2);
-        // ---- the Newton pass's log (later launches read it: plain stores)
+        // ---- the Newton pass's log (later launches read it: plain stores;
+        // issued during the granule wait instead: 66.7 against 65.0 us)
         for (int q = tid; q < K * K; q += 256) {
             const int x = (q / K) * KS + q % K;
             log[q] = sCi[x];
@@ -492,7 +471,7 @@ __global__ void __launch_bounds__(64) k_pcr_rhs(PcrDev P, const double *__restri
 template <int K>
 __global__ void __launch_bounds__(256) k_pcr_rhs_mc(PcrDev P, const double *__restrict__ R,
                                                     int ldr, int nc, double *Z, int ldz,
-                                                    double *mpub, int *mflag, unsigned epoch,
+                                                    double *mpub, unsigned epoch,
                                                     int *fail) {
     constexpr int LS = pcr_log_size<K>();
     constexpr int NS = PCR_NCMAX + 1;  // LDS row stride
@@ -609,7 +588,7 @@ static std::atomic<unsigned> g_pcr_epoch{0};
 
 static unsigned pcr_next_epoch() {
     unsigned ep = ++g_pcr_epoch;
-    if (ep == 0) ep = ++g_pcr_epoch;  // flags start at 0: never use epoch 0
+    if (ep == 0) ep = ++g_pcr_epoch;  // zeroed granules: never use epoch 0
     return ep;
 }
 
@@ -697,9 +676,9 @@ void pcr_rhs_mc(hipStream_t s, const PcrDev &P, const double *R, int ldr, int nc
     pcr_ordered(s, [&] {
         const unsigned ep = pcr_next_epoch();
         switch (P.K) {
-            case 8: k_pcr_rhs_mc<8><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, P.mflag, ep, fail); break;
-            case 16: k_pcr_rhs_mc<16><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, P.mflag, ep, fail); break;
-            default: k_pcr_rhs_mc<24><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, P.mflag, ep, fail); break;
+            case 8: k_pcr_rhs_mc<8><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, ep, fail); break;
+            case 16: k_pcr_rhs_mc<16><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, ep, fail); break;
+            default: k_pcr_rhs_mc<24><<<P.nblk, 256, 0, s>>>(P, R, ldr, nc, Z, ldz, P.mpub, ep, fail); break;
         }
     });
 }

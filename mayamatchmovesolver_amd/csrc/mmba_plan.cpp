@@ -1941,10 +1941,6 @@ void Plan::setup_band(int Pforce) {
                     Q.rpub = dalloc<double>(std::max<size_t>(1, (size_t)L * Q.nblk * 4 * Q.K));  // granules
                     MMBA_HIP(hipMemsetAsync(Q.rpub, 0, sizeof(double) * std::max<size_t>(1, (size_t)L * Q.nblk * 4 * Q.K), s));
                     Q.part = dalloc<double>(Q.nblk);
-                    Q.fflag = dalloc<int>(std::max<size_t>(1, (size_t)L * Q.nblk));
-                    Q.rflag = dalloc<int>(std::max<size_t>(1, (size_t)L * Q.nblk));
-                    MMBA_HIP(hipMemsetAsync(Q.fflag, 0, sizeof(int) * std::max<size_t>(1, (size_t)L * Q.nblk), s));
-                    MMBA_HIP(hipMemsetAsync(Q.rflag, 0, sizeof(int) * std::max<size_t>(1, (size_t)L * Q.nblk), s));
                     Q.flev = dalloc<int>(Q.nblk);
                     MMBA_HIP(hipMemsetAsync(Q.flev, 0, sizeof(int) * Q.nblk, s));
                     bs.use_pcr = true;
@@ -2083,12 +2079,6 @@ void Plan::setup_band(int Pforce) {
         Q.mpub = dalloc<double>(nl * 4 * Q.K * PCR_NCMAX);  // granules (k_pcr_rhs_mc), zeroed
         MMBA_HIP(hipMemsetAsync(Q.mpub, 0, sizeof(double) * nl * 4 * Q.K * PCR_NCMAX, s));
         Q.part = dalloc<double>(Q.nblk);
-        Q.fflag = dalloc<int>(nl);
-        Q.rflag = dalloc<int>(nl);
-        Q.mflag = dalloc<int>(nl);
-        MMBA_HIP(hipMemsetAsync(Q.fflag, 0, sizeof(int) * nl, s));
-        MMBA_HIP(hipMemsetAsync(Q.rflag, 0, sizeof(int) * nl, s));
-        MMBA_HIP(hipMemsetAsync(Q.mflag, 0, sizeof(int) * nl, s));
         Q.flev = dalloc<int>(Q.nblk);
                     MMBA_HIP(hipMemsetAsync(Q.flev, 0, sizeof(int) * Q.nblk, s));
         bs.XA = dalloc<double>((size_t)std::max(hp.na, 1) * ast);

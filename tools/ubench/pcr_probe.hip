@@ -45,10 +45,6 @@ int main(int argc, char **argv) {
     hipMalloc(&P.rpub, (size_t)L * P.nblk * 4 * K * 8);  // 16-B granules
     hipMemset(P.rpub, 0, (size_t)L * P.nblk * 4 * K * 8);
     hipMalloc(&P.part, P.nblk * 8);
-    hipMalloc(&P.fflag, (size_t)L * P.nblk * 4);
-    hipMalloc(&P.rflag, (size_t)L * P.nblk * 4);
-    hipMemset(P.fflag, 0, (size_t)L * P.nblk * 4);
-    hipMemset(P.rflag, 0, (size_t)L * P.nblk * 4);
     hipMalloc(&P.flev, P.nblk * 4);
     hipMalloc(&r, nb * 8);
     hipMalloc(&x, nb * 8);
