@@ -3747,7 +3747,9 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
     if (P.rs) {  // coupled camera-frame blocks (mmba_rs.hip)
         launch_ne_rs(s, P, J, jcol, nloc, f, Acc, Acg, g);
     } else if (P.ncf > 0 && !cf_done) {
-        const bool wide = P.M > 1024 * P.ncf;  // long camera-frame segments (C2): 4 waves
+        // long camera-frame segments (C2), or segments of a few hundred
+        // observations on fewer camera-frames than SIMDs (C5): 4 waves each
+        const bool wide = P.M > 1024 * P.ncf || (P.M > 128 * P.ncf && P.ncf < 1024);
 #define MMBA_NE_U(PC, NW, NG)                                                              \
     k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E)
         const int pcu = P.pc_uniform;
