@@ -1550,6 +1550,7 @@ __global__ void k_ne_bnd(DevProblem P, const double *__restrict__ J,
 // array of NG = 16 spills 2 KB per lane to scratch; wider arrows take
 // k_ne_glob_wide).  Partial rows keep the
 // NGMAX layout.
+constexpr int NE_GLOB_L = 12;  // observations with at most this many columns: batched loads
 template <int NG>
 __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__restrict__ J,
                                                  const int *__restrict__ jcol,
@@ -1577,15 +1578,39 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
 #pragma unroll
         for (int q = 0; q < NG; ++q) gx[q] = gy[q] = 0.;
         const int nl = nloc[i];
-        for (int l = 0; l < nl; ++l) {
-            const int p = jcol[(size_t)l * M + i];
-            if (P.p_class[p] != PC_G) continue;
-            const int gi = P.p_pos[p] - nCF;
-            const double jx = J[(size_t)(2 * l) * M + i], jy = J[(size_t)(2 * l + 1) * M + i];
+        if (nl <= NE_GLOB_L) {
+            // the same assignments, with every column's loads issued level by
+            // level (parameter ids, then class and position, then the J
+            // entries): three memory round trips instead of three per column
+            int pl[NE_GLOB_L], gq[NE_GLOB_L];
 #pragma unroll
-            for (int q = 0; q < NG; ++q) {
-                gx[q] = (gi == q) ? jx : gx[q];
-                gy[q] = (gi == q) ? jy : gy[q];
+            for (int l = 0; l < NE_GLOB_L; ++l) pl[l] = l < nl ? jcol[(size_t)l * M + i] : -1;
+#pragma unroll
+            for (int l = 0; l < NE_GLOB_L; ++l) {
+                const int p = pl[l];
+                gq[l] = (p >= 0 && P.p_class[p] == PC_G) ? P.p_pos[p] - nCF : -1;
+            }
+#pragma unroll
+            for (int l = 0; l < NE_GLOB_L; ++l) {
+                if (gq[l] < 0) continue;
+                const double jx = J[(size_t)(2 * l) * M + i], jy = J[(size_t)(2 * l + 1) * M + i];
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    gx[q] = (gq[l] == q) ? jx : gx[q];
+                    gy[q] = (gq[l] == q) ? jy : gy[q];
+                }
+            }
+        } else {
+            for (int l = 0; l < nl; ++l) {
+                const int p = jcol[(size_t)l * M + i];
+                if (P.p_class[p] != PC_G) continue;
+                const int gi = P.p_pos[p] - nCF;
+                const double jx = J[(size_t)(2 * l) * M + i], jy = J[(size_t)(2 * l + 1) * M + i];
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    gx[q] = (gi == q) ? jx : gx[q];
+                    gy[q] = (gi == q) ? jy : gy[q];
+                }
             }
         }
         const double fx = f[2 * i], fy = f[2 * i + 1];
