@@ -283,6 +283,11 @@ struct TrialFold {
 // camera records from the per-camera-frame table, no rolling shutter.
 bool trial_records_ok(const DevProblem &P);
 int trial_fold_parts(const DevProblem &P, int nother, bool rec = false);
+// Plans without a solved bundle (Plan::trial_prep_rec): the trial's parameter
+// pass and its records in one launch (T.other: the parameters outside every
+// camera-frame block); partial rows of trial_prep_rec_parts entries.
+int trial_prep_rec_parts(const DevProblem &P, int nother);
+void launch_trial_prep_rec(hipStream_t s, const DevProblem &P, const double *xs, const TrialFold &T);
 void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,
                     double *U);
 void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,

@@ -2813,6 +2813,59 @@ __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double
     }
 }
 
+// The trial point's parameter pass with its records, for plans without a
+// solved bundle (C5): workgroups [0, ncfb) take four camera-frames each (16
+// lanes per camera-frame: its parameters' trial values, then after the
+// barrier its base and variant records, as k_records builds them);
+// workgroups [ncfb, ..) the other parameters, T.other (global parameters no
+// camera or bundle record reads).  k_trial_prep + k_records in one launch.
+__global__ void __launch_bounds__(64) k_trial_prep_rec(DevProblem P, const double *__restrict__ xs,
+                                                       int ncfb, TrialFold T) {
+    __shared__ double red[128];
+    double pn = 0., xn = 0.;
+    if ((int)blockIdx.x < ncfb) {
+        const int cf = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 4);
+        const int v = threadIdx.x & 15;
+        int off = 0, nv = -1;
+        if (cf < P.ncf) {
+            off = P.cf_var_off[cf];
+            nv = P.cf_var_off[cf + 1] - off - 1;
+        }
+        if (v < nv) {
+            const int j = P.cf_var_param[off + 1 + v];
+            trial_one(P, T, j, xs[j], pn, xn);
+        }
+        __syncthreads();
+        if (v <= nv) {
+            const int p = P.cf_var_param[off + v];  // -1: the base record
+            const long long ov_idx = p >= 0 ? P.p_vidx[p] : -1;
+            const double ov_val = p >= 0 ? T.ext_pert[p] : 0.;
+            camera_record_fast(P, cf, ov_idx, ov_val, &T.recs[(size_t)(off + v) * CAMREC],
+                               p >= 0 ? P.p_attr[p] : -1);
+        }
+    } else {
+        const int k = ((int)blockIdx.x - ncfb) * 64 + (int)threadIdx.x;
+        if (k < T.nother) {
+            const int j = T.other[k];
+            trial_one(P, T, j, xs[j], pn, xn);
+        }
+    }
+    red[threadIdx.x] = pn;
+    red[64 + threadIdx.x] = xn;
+    __syncthreads();
+    for (int w = 32; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            red[threadIdx.x] += red[threadIdx.x + w];
+            red[64 + threadIdx.x] += red[64 + threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        T.partial[blockIdx.x] = red[0];
+        T.partial[T.rstride + blockIdx.x] = red[64];
+    }
+}
+
 // Reduced-system solution (R order) -> parameter order.
 __global__ void k_scatter_xR(DevProblem P, const double *__restrict__ xR, double *x) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3124,6 +3177,12 @@ bool trial_records_ok(const DevProblem &P) {
     return P.nG == 0 && P.cf_aidx != nullptr && !P.rs && P.ncf > 0;
 }
 
+int trial_prep_rec_parts(const DevProblem &P, int nother) {
+    return (P.ncf + 3) / 4 + nblk(nother, 64);
+}
+void launch_trial_prep_rec(hipStream_t s, const DevProblem &P, const double *xs, const TrialFold &T) {
+    k_trial_prep_rec<<<trial_prep_rec_parts(P, T.nother), 64, 0, s>>>(P, xs, (P.ncf + 3) / 4, T);
+}
 int trial_fold_parts(const DevProblem &P, int nother, bool rec) {
     return nblk(P.nB, 64) + (rec ? (P.ncf + 3) / 4 : nblk(nother, 64));
 }

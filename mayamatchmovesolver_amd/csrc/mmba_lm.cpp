@@ -434,14 +434,39 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     // the parameter pass ran in the damped solve's back substitution, or here
-    const int tparts = trial_folded ? trial_fold_parts(P, n_trial_other, trial_rec) : nparts;
-    if (!trial_folded)
+    const int tparts = trial_folded     ? trial_fold_parts(P, n_trial_other, trial_rec)
+                       : trial_prep_rec ? trial_prep_rec_parts(P, n_prep_other)
+                                        : nparts;
+    if (!trial_folded && trial_prep_rec) {
+        TrialFold T;
+        T.x = d_x;
+        T.diag = d_diag;
+        T.wa1 = d_wa1;
+        T.wa2 = d_wa2;
+        T.wa3 = d_wa3;
+        T.ext = d_ext;
+        T.ext_pert = d_ext_pert;
+        T.step = d_step;
+        T.solver_type = opt.solver_type;
+        T.delta = opt.delta;
+        T.eps_dif = fd_eps();
+        T.other = d_prep_other;
+        T.nother = n_prep_other;
+        T.partial = pr;
+        T.rstride = pw;
+        T.own = d_p_own;
+        T.rec = 1;
+        T.recs = d_recs;
+        T.brec = d_brec;
+        launch_trial_prep_rec(s, P, d_xs, T);
+    } else if (!trial_folded) {
         launch_trial_prep(s, P, d_xs, d_x, d_diag, d_wa1, d_wa2, d_wa3, d_ext, d_ext_pert, d_step,
                           opt.solver_type, opt.delta, fd_eps(), d_p_own, pr, nparts, pw);
+    }
     if (b15) launch_b15_rot(s, P, d_q15, d_wa1, d_p15);  // p in the rotated basis of J
     params_at = d_wa2;  // x <- wa2 on acceptance: the next Jacobian skips k_param_set
-    if (trial_folded && trial_rec)
-        recs_full_at = d_wa2;  // built by the back substitution
+    if ((trial_folded && trial_rec) || (!trial_folded && trial_prep_rec))
+        recs_full_at = d_wa2;  // built by the back substitution / the trial pass
     else
         records_enqueue(d_wa2, 0);  // ... and k_records
     span_begin(SPAN_RESID);

@@ -1657,6 +1657,7 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_trial_other = upload(other.empty() ? std::vector<int>(1, 0) : other);
         pw = std::max(pw, trial_fold_parts(P, n_trial_other));
         pw = std::max(pw, trial_fold_parts(P, n_trial_other, true));
+        pw = std::max(pw, trial_prep_rec_parts(P, n));  // >= any n_prep_other
     }
     d_partial = dalloc<double>((size_t)8 * pw);  // rows 0..7 (launch_dist_stats: 0..2)
     d_scalar = dalloc<double>(NSLOT);
@@ -1779,6 +1780,29 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         trial_rec = trial_fold_ok && nranks == 1 && trial_records_ok(P) && maxpc <= 15 &&
                     sumpc == n_trial_other && nvar == ncf + sumpc &&
                     path_choice(MMBA_PATH_TRIAL_RECORDS) != 0;
+        // without a solved bundle (C5): the same in k_trial_prep's place, when
+        // every parameter outside the camera-frame blocks is a global that no
+        // camera or bundle record reads (lens coefficients)
+        bool ok = nB_solved == 0 && nranks == 1 && !rs_on && !b15 && P.cf_aidx != nullptr &&
+                  ncf > 0 && maxpc <= 15 && nvar == ncf + sumpc &&
+                  path_choice(MMBA_PATH_TRIAL_RECORDS) != 0;
+        for (int f : cf_var_flags)
+            if (f & VF_BUNDLE_SIDE) ok = false;
+        // (no parameter moves a bundle: the bundle records stay those of the
+        // first evaluation)
+        std::vector<int> other;
+        for (int p = 0; p < n && ok; ++p) {
+            const int a = pr->param_attr[p];
+            if (!attr_bnds[a].empty()) ok = false;
+            if (p_class[p] == PC_CF) continue;
+            if (p_class[p] != PC_G || !attr_cams[a].empty()) ok = false;
+            other.push_back(p);
+        }
+        trial_prep_rec = ok;
+        if (ok) {
+            n_prep_other = (int)other.size();
+            d_prep_other = upload(other.empty() ? std::vector<int>(1, 0) : other);
+        }
     }
     fold_init = dest_diag_all && use_dest && nG == 0 && !rs_on && nRpad == nR &&
                 (pc_uniform == 6 || pc_uniform == 7);

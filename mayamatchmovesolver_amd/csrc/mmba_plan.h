@@ -456,6 +456,12 @@ struct Plan {
     // the folded trial pass also builds the trial point's records (no
     // k_records launch; TrialFold::rec)
     bool trial_rec = false;
+    // plans without a solved bundle: k_trial_prep_rec sets the trial point
+    // and builds its records (no k_records launch); the parameters outside
+    // every camera-frame block (globals no record reads)
+    bool trial_prep_rec = false;
+    int *d_prep_other = nullptr;
+    int n_prep_other = 0;
     int *d_trial_other = nullptr;
     int n_trial_other = 0;
     bool pre_jac = true;
