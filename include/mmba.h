@@ -648,11 +648,15 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       all-reducing it whole; default: whole while the whole
                                       band system fits one resident PCR grid */
 #define MMBA_PATH_TRIAL_RECORDS 10 /* 0: the trial point's records in their own launch instead
-                                      of inside the trial's back substitution */
+                                      of inside the trial's back substitution (or, without a
+                                      solved bundle, its parameter pass) */
 #define MMBA_PATH_LENS_CF 11       /* 0: every lens coefficient a global parameter (an
                                       animated one read by one camera-frame's rows joins
                                       that camera-frame's block otherwise) */
-#define MMBA_PATH_NUM 12
+#define MMBA_PATH_DEST_LANE 12     /* 0 / 1: small off-diagonal Schur destinations never /
+                                      always by a lane each (default: where they are most
+                                      of at least 16,384) */
+#define MMBA_PATH_NUM 13
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

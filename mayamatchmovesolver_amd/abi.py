@@ -36,7 +36,8 @@ PATH_PROBE = 8
 PATH_SHARD_SEP = 9
 PATH_TRIAL_RECORDS = 10
 PATH_LENS_CF = 11
-PATH_NUM = 12
+PATH_DEST_LANE = 12
+PATH_NUM = 13
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1

@@ -247,7 +247,9 @@ struct SchurInitFold {
 bool launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
                        int pc_uniform, int assign_off, const double *tb = nullptr,
-                       double *rhs = nullptr, SchurInitFold fold = SchurInitFold{});
+                       double *rhs = nullptr, SchurInitFold fold = SchurInitFold{},
+                       const int *wave_list = nullptr, int n_wave = 0,
+                       const int *lane_list = nullptr, int n_lane = 0);
 void launch_schur_rhs(hipStream_t s, const DevProblem &P, const double *W, const double *tb,
                       const int *row_cf, double *rhs);
 void launch_schur_glob(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,

@@ -2378,7 +2378,8 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
                                                      const int2 *__restrict__ pairs,
                                                      const SView V, int assign_off, int ndest,
                                                      const double *__restrict__ tb, double *rhs,
-                                                     const SchurInitFold fold) {
+                                                     const SchurInitFold fold,
+                                                     const int *__restrict__ list) {
     // diagonal destinations (cf, cf) hold exactly the pairs (i, i) of the
     // camera-frame's observations with a bundle block, so they also form
     // rhs_R -= sum_i W_i t_b(i) (k_schur_rhs) in the same loop
@@ -2388,8 +2389,9 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
     // grid in two rounds)
     __shared__ double red[PC * PC + PC][33];
     const int per = (ndest + 7) / 8;
-    const int d = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    int d = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (d >= ndest) return;
+    if (list) d = list[d];  // the destinations k_schur_dest_lane leaves
     const int2 cc = dest[d];
     const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
     const int q0 = dest_off[d], q1 = dest_off[d + 1];
@@ -2522,6 +2524,69 @@ __global__ void __launch_bounds__(64, 2) k_schur_dest_u(DevProblem P, const doub
             }
         }
     }
+}
+
+// Off-diagonal destinations of at most 32 pairs (C3: 9.3M destinations, 5.5
+// pairs on average, where a wave per destination idles 59 of its 64 lanes
+// and then reduces 36 sums through LDS): one lane per destination, its
+// pairs in order.  k_schur_dest_u's lane l holds pair l alone for such a
+// destination and its fixed-order lane sum adds them in pair order, so
+// every entry is the same sum, bit for bit.  list: the destinations (XCD-
+// contiguous runs of 256 per workgroup).
+template <int PC>
+__global__ void __launch_bounds__(256) k_schur_dest_lane(DevProblem P, const double *__restrict__ W,
+                                                         const int2 *__restrict__ dest,
+                                                         const int *__restrict__ dest_off,
+                                                         const int2 *__restrict__ pairs,
+                                                         const SView V, int assign_off,
+                                                         const int *__restrict__ list, int nlist) {
+    const int per = (int)(gridDim.x + 7) / 8;
+    const int wg = (int)(blockIdx.x % 8) * per + (int)blockIdx.x / 8;
+    const int k = wg * 256 + (int)threadIdx.x;
+    if (k >= nlist) return;
+    const int d = list[k];
+    const int2 cc = dest[d];
+    const int ri = P.cf_roff[cc.x], rj = P.cf_roff[cc.y];
+    const int q0 = dest_off[d], q1 = dest_off[d + 1];
+    double acc[PC * PC];
+#pragma unroll
+    for (int e = 0; e < PC * PC; ++e) acc[e] = 0.;
+    for (int q = q0; q < q1; ++q) {
+        const int2 pr = pairs[q];
+        double wi[3 * PC], wj[3 * PC];
+        if constexpr ((3 * PC) % 2 == 0) {
+            const double2 *pi = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.x)]);
+            const double2 *pj = reinterpret_cast<const double2 *>(&W[widx(P, 0, pr.y)]);
+#pragma unroll
+            for (int u = 0; u < 3 * PC / 2; ++u) {
+                const double2 a = pi[u], b = pj[u];
+                wi[2 * u] = a.x;
+                wi[2 * u + 1] = a.y;
+                wj[2 * u] = b.x;
+                wj[2 * u + 1] = b.y;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 3 * PC; ++u) {
+                wi[u] = W[widx(P, u, pr.x)];
+                wj[u] = W[widx(P, u, pr.y)];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < PC; ++a)
+#pragma unroll
+            for (int c = 0; c < PC; ++c)
+                acc[a * PC + c] += wi[a * 3] * wj[c * 3] + wi[a * 3 + 1] * wj[c * 3 + 1] +
+                                   wi[a * 3 + 2] * wj[c * 3 + 2];
+    }
+#pragma unroll
+    for (int a = 0; a < PC; ++a)
+#pragma unroll
+        for (int c = 0; c < PC; ++c)
+            if (ri + a >= rj + c) {
+                double *dd = s_at(V, ri + a, rj + c);
+                *dd = assign_off ? -acc[a * PC + c] : *dd - acc[a * PC + c];  // see k_schur_dest
+            }
 }
 
 // rhs_R -= sum_{i in cf} W_i t_b(i): one wave per camera-frame, lanes stride
@@ -3913,17 +3978,30 @@ void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, con
 bool launch_schur_dest(hipStream_t s, const DevProblem &P, const double *W, const int2 *dest,
                        const int *dest_off, int ndest, const int2 *pairs, const SView &V,
                        int pc_uniform, int assign_off, const double *tb, double *rhs,
-                       SchurInitFold fold) {
+                       SchurInitFold fold, const int *wave_list, int n_wave,
+                       const int *lane_list, int n_lane) {
     if (ndest <= 0) return false;
+    // split pass: the wave kernel over its list, the lane kernel over the rest
+    const int nw = lane_list ? n_wave : ndest;
+    const int *wl = lane_list ? wave_list : nullptr;
+    const int lg = 8 * ((nblk(n_lane, 256) + 7) / 8);
     // fold.on only comes with rhs and pc_uniform 6 / 7 (Plan::fold_init)
     if (pc_uniform == 6) {
-        k_schur_dest_u<6><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
-                                                                assign_off, ndest, tb, rhs, fold);
+        if (nw > 0)
+            k_schur_dest_u<6><<<8 * ((nw + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
+                                                                assign_off, nw, tb, rhs, fold, wl);
+        if (lane_list)
+            k_schur_dest_lane<6><<<lg, 256, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off,
+                                                    lane_list, n_lane);
         return rhs != nullptr;
     }
     if (pc_uniform == 7) {
-        k_schur_dest_u<7><<<8 * ((ndest + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
-                                                                assign_off, ndest, tb, rhs, fold);
+        if (nw > 0)
+            k_schur_dest_u<7><<<8 * ((nw + 7) / 8), 64, 0, s>>>(P, W, dest, dest_off, pairs, V,
+                                                                assign_off, nw, tb, rhs, fold, wl);
+        if (lane_list)
+            k_schur_dest_lane<7><<<lg, 256, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off,
+                                                    lane_list, n_lane);
         return rhs != nullptr;
     }
     k_schur_dest<<<ndest, 64, 0, s>>>(P, W, dest, dest_off, pairs, V, assign_off);

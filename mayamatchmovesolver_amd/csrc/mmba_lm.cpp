@@ -628,7 +628,8 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
                 if (fold) fi = SchurInitFold{1, d_Acc, d_g, d_diag, lam};
                 const bool rhs_done =
                     launch_schur_dest(s, PS, d_W, d_dest, d_dest_off, ndest, d_dpairs, V,
-                                      pc_uniform, band && bs.use_bcr && !rs_bnd, d_tb, d_rhs, fi);
+                                      pc_uniform, band && bs.use_bcr && !rs_bnd, d_tb, d_rhs, fi,
+                                      d_dest_wave, n_dest_wave, d_dest_lane, n_dest_lane);
                 if (!rhs_done) launch_schur_rhs(s, PS, d_W, d_tb, d_row_cf, d_rhs);
                 launch_schur_glob(s, PS, d_W, d_Wg, d_tb, V, d_rhs);
             } else {

@@ -1526,6 +1526,25 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
         d_dest = upload(dest_h);
         d_dest_off = upload(dest_off_h);
         d_dpairs = upload(dpairs_h);
+        // many small off-diagonal destinations (C3: 9.3M destinations of 5.5
+        // pairs on average): those of at most 32 pairs take one lane each
+        // (k_schur_dest_lane, the same sums in the same order), the others
+        // (diagonal ones among them) a wave each
+        if (pc_uniform == 6 || pc_uniform == 7) {
+            std::vector<int> wl, ll;
+            for (int d = 0; d < ndest; ++d) {
+                const bool lane = dest_h[d].x != dest_h[d].y && dest_off_h[d + 1] - dest_off_h[d] <= 32;
+                (lane ? ll : wl).push_back(d);
+            }
+            const int pin = path_choice(MMBA_PATH_DEST_LANE);  // 1: whenever there are any
+            if (!ll.empty() && pin != 0 &&
+                (pin == 1 || (ll.size() >= 16384 && 2 * ll.size() >= (size_t)ndest))) {
+                n_dest_wave = (int)wl.size();
+                n_dest_lane = (int)ll.size();
+                d_dest_wave = upload(wl.empty() ? std::vector<int>(1, 0) : wl);
+                d_dest_lane = upload(ll);
+            }
+        }
     }
     {
         // dense reduced system: at least 30 % of the lower tiles non-zero

@@ -162,6 +162,10 @@ struct Plan {
     static constexpr bool seq_poll = true;  // (stream events: measured slower)
     int pc_uniform = 0;  // common block size of the solved camera-frames (0: mixed)
     int2 *d_dest = nullptr, *d_dpairs = nullptr;
+    // destination lists of the split Schur pass (k_schur_dest_u over the
+    // wave list, k_schur_dest_lane over the lane list); null: one pass
+    int *d_dest_wave = nullptr, *d_dest_lane = nullptr;
+    int n_dest_wave = 0, n_dest_lane = 0;
     int *d_dest_off = nullptr, *d_row_cf = nullptr;
     // band + arrow layout of the reduced system (mmba_band.hip)
     bool band = false;

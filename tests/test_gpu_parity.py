@@ -141,6 +141,31 @@ def test_reduced_system_dense_and_tiled(dense, oracle, gpu_ctx, paths):
     check_solve(prob, opt, oracle, gpu_ctx)
 
 
+@pytest.mark.parametrize("idx,kw,dense", [(2, dict(frames=8, scale=0.002), 1),
+                                         (2, dict(frames=8, scale=0.002), 0),
+                                         (3, dict(frames=8, scale=0.001), -1)])
+def test_schur_dest_lane_bit_identical(idx, kw, dense, oracle, gpu_ctx, paths):
+    """The lane-per-destination Schur pass (k_schur_dest_lane: off-diagonal
+    destinations of at most 32 pairs, C3's common case) forms every entry of
+    S with the sums of the wave-per-destination pass in the same order: the
+    solve is bit-identical with the pass pinned on and off, and matches the
+    oracle.  (Full-size C3 takes it by default: 9.3M destinations.)"""
+    paths(abi.PATH_DENSE, dense)
+    prob = S.make_config(idx, **kw)
+    opt = S.config_options(prob)
+    runs = []
+    for lane in (0, 1):
+        paths(abi.PATH_DEST_LANE, lane)
+        s = Solver(prob, opt, context=gpu_ctx)
+        try:
+            runs.append(s.solve())
+        finally:
+            s.close()
+    np.testing.assert_array_equal(runs[1].x, runs[0].x)
+    np.testing.assert_array_equal(runs[1].fnorm_trace, runs[0].fnorm_trace)
+    check_solve(prob, opt, oracle, gpu_ctx)
+
+
 @pytest.mark.parametrize("mode", [abi.SCENE_GRAPH_MODE_MAYA_DAG,
                                   abi.SCENE_GRAPH_MODE_MM_SCENE_GRAPH])
 @pytest.mark.parametrize("idx,kw", [(3, dict(frames=8, scale=0.001)),
