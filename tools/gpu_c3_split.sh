@@ -1,3 +1,5 @@
+# (round 5 record: the dense_split path key was removed after this measurement --
+# profiles/r5_c3split/; the script no longer runs against the current library)
 # C3: the dense factorisation with its panel chain on a CU partition
 # (--path dense_split=V) against the single-stream form
 set -o pipefail
