@@ -1141,11 +1141,12 @@ __device__ __forceinline__ void epi_store(const NeEpi &E, int col, double zf, do
 
 
 template <int PC, int NW, int NG>
-__global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
-                                                     const int *__restrict__ jcol,
-                                                     const int *__restrict__ nloc,
-                                                     const double *__restrict__ f, double *Acc,
-                                                     double *Acg, double *g, NeEpi E) {
+__device__ __forceinline__ void ne_cf_u_body(const DevProblem &P, const double *__restrict__ J,
+                                             const int *__restrict__ jcol,
+                                             const int *__restrict__ nloc,
+                                             const double *__restrict__ f, double *Acc,
+                                             double *Acg, double *g, const NeEpi &E, int blk,
+                                             int nblk_cf) {
     // NW waves per camera-frame (long segments: C2 has ~1,700 observations
     // per camera-frame): thread t takes observations t, t + 64 NW, ...;
     // each wave folds its partial sums with a fixed xor-shuffle tree, the NW
@@ -1154,7 +1155,7 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
     // follow the camera block in each observation (found through jcol).
     constexpr int NCC = PC * (PC + 1) / 2, NE = NCC + PC, NT = NE + PC * NG;
     __shared__ double wsum[NW][NT];
-    const int cf = xcd_remap(blockIdx.x, gridDim.x);  // the XCD that wrote its J rows
+    const int cf = xcd_remap(blk, nblk_cf);  // the XCD that wrote its J rows
     if (!own_cf(P, cf) || P.cf_pc[cf] != PC) {
         if (E.on && threadIdx.x == 0) epi_store(E, E.cf_base + cf, 0., 0., 0.);
         return;
@@ -1250,6 +1251,14 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double 
         }
         epi_store(E, E.cf_base + cf, zf, xn, gm);
     }
+}
+template <int PC, int NW, int NG>
+__global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
+                                                     const int *__restrict__ jcol,
+                                                     const int *__restrict__ nloc,
+                                                     const double *__restrict__ f, double *Acc,
+                                                     double *Acg, double *g, NeEpi E) {
+    ne_cf_u_body<PC, NW, NG>(P, J, jcol, nloc, f, Acc, Acg, g, E, blockIdx.x, gridDim.x);
 }
 
 // Camera-frame -> XCD-contiguous order: workgroups are dispatched to the 8
@@ -1552,11 +1561,11 @@ __global__ void k_ne_bnd(DevProblem P, const double *__restrict__ J,
 // NGMAX layout.
 constexpr int NE_GLOB_L = 12;  // observations with at most this many columns: batched loads
 template <int NG>
-__global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__restrict__ J,
-                                                 const int *__restrict__ jcol,
-                                                 const int *__restrict__ nloc,
-                                                 const double *__restrict__ f,
-                                                 double *partial, int chunk) {
+__device__ __forceinline__ void ne_glob_body(const DevProblem &P, const double *__restrict__ J,
+                                             const int *__restrict__ jcol,
+                                             const int *__restrict__ nloc,
+                                             const double *__restrict__ f, double *partial,
+                                             int chunk, int blk) {
     // One observation per thread (grid-stride over the block's chunk); each
     // thread scatters its global-parameter Jacobian entries into a dense
     // register vector, products are reduced wave -> block in a fixed order
@@ -1570,7 +1579,7 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
     double accv[NA];
 #pragma unroll
     for (int e = 0; e < NA; ++e) accv[e] = 0.;
-    const int i0 = blockIdx.x * chunk;
+    const int i0 = blk * chunk;
     const int i1 = min(M, i0 + chunk);
     for (int i = i0 + (int)threadIdx.x; i < i1; i += blockDim.x) {
         if (!own_obs(P, i)) continue;
@@ -1636,8 +1645,34 @@ __global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__r
         const bool mat = t < nG * nG;
         const int a = mat ? t / nG : t - nG * nG, b = mat ? t % nG : 0;
         const int e = mat ? a * NG + b : NG * NG + a;
-        partial[(size_t)blockIdx.x * NA_ + t] = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
+        partial[(size_t)blk * NA_ + t] = (wsum[0][e] + wsum[1][e]) + (wsum[2][e] + wsum[3][e]);
     }
+}
+template <int NG>
+__global__ void __launch_bounds__(256) k_ne_glob(DevProblem P, const double *__restrict__ J,
+                                                 const int *__restrict__ jcol,
+                                                 const int *__restrict__ nloc,
+                                                 const double *__restrict__ f,
+                                                 double *partial, int chunk) {
+    ne_glob_body<NG>(P, J, jcol, nloc, f, partial, chunk, blockIdx.x);
+}
+
+// Both in one launch (C5: camera-frame blocks of four waves and at most two
+// global parameters): workgroups [0, ncf) are k_ne_cf_u<PC, 4, 2>'s, the rest
+// k_ne_glob<2>'s -- the same code on the same data, so the same sums, with
+// the global chunks running beside the camera-frame blocks instead of after
+// them (C5: 10.9 us of k_ne_glob per Jacobian).
+template <int PC>
+__global__ void __launch_bounds__(256) k_ne_cf_glob(DevProblem P, const double *__restrict__ J,
+                                                    const int *__restrict__ jcol,
+                                                    const int *__restrict__ nloc,
+                                                    const double *__restrict__ f, double *Acc,
+                                                    double *Acg, double *g, NeEpi E,
+                                                    double *partial, int chunk) {
+    if ((int)blockIdx.x < P.ncf)
+        ne_cf_u_body<PC, 4, 2>(P, J, jcol, nloc, f, Acc, Acg, g, E, blockIdx.x, P.ncf);
+    else
+        ne_glob_body<2>(P, J, jcol, nloc, f, partial, chunk, (int)blockIdx.x - P.ncf);
 }
 
 // Globals wider than 16 (NG^2 + NG accumulators no longer fit a thread's
@@ -3893,6 +3928,7 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
                const NeEpi &epi, bool cf_done) {
     const NeEpi E = ne_epilogue_fusable(P) ? epi : NeEpi();
     double *Agg = aggbuf, *gG = aggbuf + NGMAX * NGMAX;
+    bool glob_done = false;  // the global chunks ran in the camera-frame launch
     if (P.rs) {  // coupled camera-frame blocks (mmba_rs.hip)
         launch_ne_rs(s, P, J, jcol, nloc, f, Acc, Acg, g);
     } else if (P.ncf > 0 && !cf_done) {
@@ -3902,7 +3938,17 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
 #define MMBA_NE_U(PC, NW, NG)                                                              \
     k_ne_cf_u<PC, NW, NG><<<P.ncf, 64 * NW, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E)
         const int pcu = P.pc_uniform;
-        if ((pcu == 6 || pcu == 7) && (P.nG == 0 || P.nG <= 2)) {
+        if ((pcu == 6 || pcu == 7) && wide && P.nG > 0 && P.nG <= 2) {
+            // camera-frame blocks and global chunks in one launch
+            const int nbg = nblk(P.M, glob_chunk);
+            if (pcu == 6)
+                k_ne_cf_glob<6><<<P.ncf + nbg, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E,
+                                                           glob_partial, glob_chunk);
+            else
+                k_ne_cf_glob<7><<<P.ncf + nbg, 256, 0, s>>>(P, J, jcol, nloc, f, Acc, Acg, g, E,
+                                                           glob_partial, glob_chunk);
+            glob_done = true;
+        } else if ((pcu == 6 || pcu == 7) && (P.nG == 0 || P.nG <= 2)) {
             if (P.nG == 0) {
                 if (pcu == 6) {
                     if (wide) MMBA_NE_U(6, 4, 0); else MMBA_NE_U(6, 1, 0);
@@ -3929,7 +3975,9 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
     }
     if (P.nG > 0) {
         const int nb = nblk(P.M, glob_chunk);
-        if (P.nG <= 2)
+        if (glob_done)
+            ;
+        else if (P.nG <= 2)
             k_ne_glob<2><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
         else if (P.nG <= 4)
             k_ne_glob<4><<<nb, 256, 0, s>>>(P, J, jcol, nloc, f, glob_partial, glob_chunk);
