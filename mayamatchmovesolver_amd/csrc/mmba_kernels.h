@@ -209,15 +209,19 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
                           const double *Abg, const double *g, const double *diag, double lam,
                           double *Lb, double *tb, double *Wg, int *fail);
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
-                      double *W);
+                      double *W, const RedSpec *red = nullptr, const double *partial = nullptr,
+                      double *scalar = nullptr);
 // rolling shutter with solved bundles: W rows of the virtual observations
 // (Plan::build, PV)
 void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,
                          const int *vobs, const int *vcoff, const double *J, const double *Lb,
                          double *W);
+// red (optional): row reductions of k_reduce_multi's plain form (no flag,
+// mirror or decision) run by extra workgroups of the same launch
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
-                       const SView &V, int npad, double *rhs);
+                       const SView &V, int npad, double *rhs, const RedSpec *red = nullptr,
+                       const double *partial = nullptr, double *scalar = nullptr);
 void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                         const double *tb, const SView &V, double *rhs);
 void launch_chol_panel(hipStream_t s, double *S, const int *slot, int NT, int k, const int *rows,

@@ -169,6 +169,33 @@ __device__ __forceinline__ double reduce_row_block(const double *partial, const 
     return v;
 }
 
+// reduce_row_block by one wave (a 64-thread workgroup of another launch):
+// lane t holds the block's threads t, t + 64, t + 128 and t + 192 and combines
+// them, then the lanes, in that block's tree order -- the same value.
+__device__ __forceinline__ double reduce_row_w64(const double *partial, const RedRow &rw) {
+    const bool mx = rw.is_max != 0;
+    const int t = threadIdx.x & 63;
+    double s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double v = 0.;
+        for (int i = t + 64 * k; i < rw.n; i += 256) {
+            const double q = partial[rw.off + i];
+            v = mx ? fmax(v, q) : v + q;
+        }
+        s[k] = v;
+    }
+    const double a0 = mx ? fmax(s[0], s[2]) : s[0] + s[2];  // w = 128
+    const double a1 = mx ? fmax(s[1], s[3]) : s[1] + s[3];
+    double r = mx ? fmax(a0, a1) : a0 + a1;                 // w = 64
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) {
+        const double o = __shfl_down(r, w);
+        if (t < w) r = mx ? fmax(r, o) : r + o;
+    }
+    return r;  // lane 0
+}
+
 // Every row of spec at once (the last workgroup of a folded launch): each
 // thread issues its loads of all rows before any sum, then one fixed tree
 // per row, level by level for all rows -- per row the arithmetic of
@@ -2098,11 +2125,22 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
 // doubles).  One wave per 64 consecutive observations: the rows are built in
 // LDS and the wave's contiguous 64 wst-double chunk is stored coalesced
 // (zeros where a row has no bundle block / no camera block).
+// nob: the observation workgroups; workgroups nob + r reduce row r of red
+// (the Jacobian epilogue's rows, which no W row reads: one launch less)
 __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__restrict__ J,
-                                                  const double *__restrict__ Lb, double *W) {
+                                                  const double *__restrict__ Lb, double *W,
+                                                  int nob, const RedSpec red,
+                                                  const double *__restrict__ partial,
+                                                  double *scalar) {
     extern __shared__ double sw[];  // 64 x wst doubles (9 KB for pose-only BA)
     const int lane = threadIdx.x;
-    const int i0 = xcd_remap(blockIdx.x, gridDim.x) * 64;  // J rows from this XCD's L2
+    if ((int)blockIdx.x >= nob) {
+        const RedRow rw = red.row[blockIdx.x - nob];
+        const double v = reduce_row_w64(partial, rw);
+        if (lane == 0) scalar[rw.slot] = v;
+        return;
+    }
+    const int i0 = xcd_remap(blockIdx.x, nob) * 64;  // J rows from this XCD's L2
     const int i = i0 + lane;
     const int M = P.M, wst = P.wst;
     double *row = &sw[lane * wst];
@@ -2208,14 +2246,13 @@ __global__ void __launch_bounds__(64) k_schur_obs_rs(DevProblem PV, int Mr,
 
 // S = (Acc + lam D^2 | Acg | Agg + lam D^2), lower triangle, plus identity
 // on the padded tail; rhs = g_R.
-__global__ void __launch_bounds__(256) k_schur_init(
-    DevProblem P, const double *__restrict__ Acc, const double *__restrict__ Acg,
+__device__ __forceinline__ void schur_init_row(
+    const DevProblem &P, const double *__restrict__ Acc, const double *__restrict__ Acg,
     const double *__restrict__ Agg, const double *__restrict__ g,
-    const double *__restrict__ diag, double lam, const SView V, int npad,
-    double *__restrict__ rhs) {
+    const double *__restrict__ diag, double lam, const SView &V, int npad,
+    double *__restrict__ rhs, int t) {
     // one thread per reduced row: (camera-frame, row a) for t < ncf * PCMAX,
     // then the global rows, then the padding rows
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int nG = P.nG;
     const int nCF = P.nR - nG;
     const int ncr = P.ncf * PCMAX;
@@ -2268,6 +2305,34 @@ __global__ void __launch_bounds__(256) k_schur_init(
             rhs[r] = 0.;
         }
     }
+}
+__global__ void __launch_bounds__(256) k_schur_init(
+    DevProblem P, const double *__restrict__ Acc, const double *__restrict__ Acg,
+    const double *__restrict__ Agg, const double *__restrict__ g,
+    const double *__restrict__ diag, double lam, const SView V, int npad,
+    double *__restrict__ rhs) {
+    schur_init_row(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs,
+                   blockIdx.x * blockDim.x + threadIdx.x);
+}
+// ... with the Jacobian epilogue's row reductions beside it (C5: the
+// reduction that followed the epilogue was its own launch, and k_schur_init
+// does not read its slots): workgroups [0, nb) form the rows, workgroup nb + r
+// reduces row r exactly as k_reduce_multi's block r does.
+__global__ void __launch_bounds__(256) k_schur_init_red(
+    DevProblem P, const double *__restrict__ Acc, const double *__restrict__ Acg,
+    const double *__restrict__ Agg, const double *__restrict__ g,
+    const double *__restrict__ diag, double lam, const SView V, int npad,
+    double *__restrict__ rhs, int nb, const double *__restrict__ partial, RedSpec spec,
+    double *scalar) {
+    if ((int)blockIdx.x < nb) {
+        schur_init_row(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs,
+                       blockIdx.x * blockDim.x + threadIdx.x);
+        return;
+    }
+    __shared__ double red[256];
+    const RedRow rw = spec.row[blockIdx.x - nb];
+    const double v = reduce_row_block<false>(partial, rw, red);
+    if (threadIdx.x == 0) scalar[rw.slot] = v;
 }
 
 // Schur complement over bundles: S -= sum_b W_b W_b^T, rhs -= W_b tb.
@@ -4002,8 +4067,11 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
     k_bundle_factor<<<nblk(P.nB, 64), 64, 0, s>>>(P, Abb, Abg, g, diag, lam, Lb, tb, Wg, fail);
 }
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
-                      double *W) {
-    k_schur_obs<<<nblk(P.M, 64), 64, sizeof(double) * 64 * P.wst, s>>>(P, J, Lb, W);
+                      double *W, const RedSpec *red, const double *partial, double *scalar) {
+    const int nob = nblk(P.M, 64), nr = red ? red->nrows : 0;
+    if (nob + nr > 0)
+        k_schur_obs<<<nob + nr, 64, sizeof(double) * 64 * P.wst, s>>>(
+            P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar);
 }
 void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,
                          const int *vobs, const int *vcoff, const double *J, const double *Lb,
@@ -4013,9 +4081,14 @@ void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int 
 }
 void launch_schur_init(hipStream_t s, const DevProblem &P, const double *Acc, const double *Acg,
                        const double *Agg, const double *g, const double *diag, double lam,
-                       const SView &V, int npad, double *rhs) {
+                       const SView &V, int npad, double *rhs, const RedSpec *red,
+                       const double *partial, double *scalar) {
     const int n = P.ncf * PCMAX + P.nG + npad;
-    k_schur_init<<<nblk(n, 256), 256, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs);
+    if (red && red->nrows > 0)
+        k_schur_init_red<<<nblk(n, 256) + red->nrows, 256, 0, s>>>(
+            P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs, nblk(n, 256), partial, *red, scalar);
+    else
+        k_schur_init<<<nblk(n, 256), 256, 0, s>>>(P, Acc, Acg, Agg, g, diag, lam, V, npad, rhs);
     if (P.rs) launch_rs_offdiag(s, P, V);  // camera-frame coupling blocks
 }
 void launch_schur_pairs(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,

@@ -85,7 +85,25 @@ void Plan::collect_spans() {
 // The trial's slots on their way to the host before anything else is
 // enqueued behind them (the pre-enqueued Jacobian): the D2H copy (unless the
 // reduction mirrors them) and the event read_slots waits on.
+bool Plan::red_defer_ok() const {
+    // the next damped solve's k_schur_init launch takes them (no bundles:
+    // nothing is launched ahead of it -- no one-launch block-diagonal solve
+    // at nG == 0, no shard memsets); with solved bundles k_schur_obs does
+    // (the bundle factor ahead of it touches neither the partial rows nor
+    // the slots)
+    if (nranks != 1 || b15 || nR <= 0) return false;
+    if (nB_solved > 0) return !rs_bnd;
+    return band && bs.use_bd && nG > 0;
+}
+
+void Plan::flush_red() {
+    if (!pend_red) return;
+    pend_red = false;
+    launch_reduce_multi(s, d_partial, pend_rs, d_scalar);
+}
+
 void Plan::stage_slots() {
+    flush_red();
     const bool mirrored = mirror_pending;
     if (!mirrored)
         MMBA_HIP(hipMemcpyAsync(h_scalar, d_scalar, sizeof(double) * (SL_LAST + 1),
@@ -110,6 +128,7 @@ void Plan::wait_event() {
 }
 
 void Plan::read_slots(int lo, int hi) {
+    flush_red();
     const bool mirrored = mirror_pending && lo == 0 && hi == SL_LAST;
     mirror_pending = false;
     const bool by_seq = mirrored && seq_pending;
@@ -201,6 +220,7 @@ void Plan::records_enqueue(const double *xat, int base_only) {
 // iflag = 1: setParameters + measureErrors; ||f||^2 -> SL_FNORM.
 void Plan::fun_enqueue(const double *dx, double *df, double *eu, double *ed, double *dist,
                        int slot) {
+    flush_red();
     // ext_pert / step with the Jacobian's eps: a Jacobian at dx that follows
     // reuses this parameter pass (params_at)
     launch_param_set(s, P, dx, d_ext, d_ext_pert, d_step, opt.solver_type, opt.delta, fd_eps());
@@ -265,6 +285,7 @@ void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
 
 // iflag = 2: FD Jacobian blocks + normal equations + column norms at x.
 void Plan::jac(const double *dx, const JacLM *lm) {
+    flush_red();
     const double t0 = wall_now();
     const double eps_dif = fd_eps();
     const bool lmder = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER;
@@ -386,7 +407,12 @@ void Plan::jac(const double *dx, const JacLM *lm) {
             rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
             if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, SL_XN2};
             if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
-            launch_reduce_multi(s, d_partial, rs, d_scalar);
+            if (red_defer_ok() && !timing) {  // rides in the next k_schur_init launch
+                pend_rs = rs;
+                pend_red = true;
+            } else {
+                launch_reduce_multi(s, d_partial, rs, d_scalar);
+            }
         }
     } else if (!lm) {
         launch_colnorms(s, P, d_Acc, d_Abb, d_Agg, d_acnorm, d_g);
@@ -431,6 +457,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
 // setParameters), measureErrors, ||J p||, one reduction launch.
 void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnorm,
                          const LmDec *dec) {
+    flush_red();
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
     // the parameter pass ran in the damped solve's back substitution, or here
@@ -540,6 +567,7 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
 void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dnorm_by_trial) {
+    if (!red_defer_ok()) flush_red();
     if (b15 && !b15_inner) {
         // B15: (M + U B U^T) xs = u + s c from M z_u = u and M z_c = c, the
         // same damped factorisation formed twice (the right-hand side rides
@@ -590,8 +618,11 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         lb0_valid = false;
         if (rs_bnd)  // W rows of the virtual observations
             launch_schur_obs_rs(s, PV, M, d_nloc, d_vobs, d_vcoff, d_J, d_Lb, d_W);
-        else
-            launch_schur_obs(s, P, d_J, d_Lb, d_W);
+        else {
+            launch_schur_obs(s, P, d_J, d_Lb, d_W, pend_red ? &pend_rs : nullptr, d_partial,
+                             d_scalar);
+            pend_red = false;
+        }
     }
     const DevProblem &PS = schur_problem();
     if (nR > 0) {
@@ -617,8 +648,12 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             MMBA_HIP(hipMemsetAsync(d_S, 0, sizeof(double) * (size_t)nslots * TILE * TILE, s));
         }
         const bool fold = fold_init && nB_solved > 0;
-        if (!fold)
-            launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs);
+        if (!fold) {
+            launch_schur_init(s, P, d_Acc, d_Acg, d_Agg, d_g, d_diag, lam, V, nRpad - nR, d_rhs,
+                              pend_red ? &pend_rs : nullptr, d_partial, d_scalar);
+            pend_red = false;
+        }
+        flush_red();
         if (nB_solved > 0) {
             if (use_dest) {
                 // unsharded uniform plans fold the rhs update into the

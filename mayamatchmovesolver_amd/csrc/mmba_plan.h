@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "mmba_internal.h"
+#include "mmba_kernels.h"
 
 struct mmba_context {
     int device = 0;
@@ -478,6 +479,14 @@ struct Plan {
     // before the pre-enqueued Jacobian: read_slots(0, SL_LAST) only waits
     bool slots_staged = false;
     void stage_slots();
+    // the Jacobian epilogue's row reductions held back for the next damped
+    // solve's k_schur_init launch (block diagonal + arrow plans without a
+    // solved bundle, C5); flush_red launches them alone wherever anything
+    // else comes first
+    bool pend_red = false;
+    RedSpec pend_rs{};
+    bool red_defer_ok() const;
+    void flush_red();
     void wait_event();
     // speculative trial (lmpar's first, undamped, step taken before the
     // host has read it): its errorList / errorDistanceList land here and are
