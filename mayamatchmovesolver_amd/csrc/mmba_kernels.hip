@@ -176,14 +176,34 @@ __device__ __forceinline__ double reduce_row_w64(const double *partial, const Re
     const bool mx = rw.is_max != 0;
     const int t = threadIdx.x & 63;
     double s[4];
+    constexpr int JB = 6;  // rows of up to 1,536 entries (C4: 1,282): every load issued first
+    if (rw.n <= 256 * JB) {
+        double q[4][JB];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        double v = 0.;
-        for (int i = t + 64 * k; i < rw.n; i += 256) {
-            const double q = partial[rw.off + i];
-            v = mx ? fmax(v, q) : v + q;
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < JB; ++j) {
+                const int i = t + 64 * k + 256 * j;
+                q[k][j] = i < rw.n ? partial[rw.off + i] : 0.;
+            }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double v = 0.;
+#pragma unroll
+            for (int j = 0; j < JB; ++j)
+                if (t + 64 * k + 256 * j < rw.n) v = mx ? fmax(v, q[k][j]) : v + q[k][j];
+            s[k] = v;
         }
-        s[k] = v;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double v = 0.;
+            for (int i = t + 64 * k; i < rw.n; i += 256) {
+                const double q = partial[rw.off + i];
+                v = mx ? fmax(v, q) : v + q;
+            }
+            s[k] = v;
+        }
     }
     const double a0 = mx ? fmax(s[0], s[2]) : s[0] + s[2];  // w = 128
     const double a1 = mx ? fmax(s[1], s[3]) : s[1] + s[3];
