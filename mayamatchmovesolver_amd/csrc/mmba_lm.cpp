@@ -446,6 +446,9 @@ void Plan::jac(const double *dx, const JacLM *lm) {
             launch_reduce_multi(s, d_partial, rj, tail);
             allreduce(tail, 2 + nranks);
             launch_fold_ranks(s, tail, nranks, d_scalar + SL_ZERO, do_xn, do_gn);
+        } else if (red_defer_ok() && !timing) {  // rides in the next k_schur_init launch (C5)
+            pend_rs = rs;
+            pend_red = true;
         } else {
             launch_reduce_multi(s, d_partial, rs, d_scalar);
         }
