@@ -446,13 +446,19 @@ void mmba_plan_destroy(mmba_plan *plan);
 typedef struct mmba_comm mmba_comm;
 /* 128-byte RCCL unique id, made on one rank and broadcast by the caller. */
 int mmba_comm_unique_id(unsigned char out_id[128]);
-/* RCCL communicator on ctx's device (ncclCommInitRank). */
+/* RCCL communicator on ctx's device (ncclCommInitRankConfig, non-blocking:
+ * the initialisation and every collective wait at most the collective timeout
+ * -- MMBA_PATH_COMM_TIMEOUT_MS / MMBA_COMM_TIMEOUT_MS, 120 s by default --
+ * before the communicator is aborted and the call returns MMBA_ERR_COMM). */
 int mmba_comm_create_rccl(mmba_context *ctx, int rank, int nranks,
                           const unsigned char unique_id[128], mmba_comm **out);
 /* nranks in-process communicators (out[0..nranks-1], nranks <= 8), each used
  * by one host thread with its own context. */
 int mmba_comm_create_local(int nranks, mmba_comm **out);
 void mmba_comm_destroy(mmba_comm *comm);
+/* Ranks of the communicator as the transport reports them (ncclCommCount for
+ * RCCL, the group size in-process); negative on error. */
+int mmba_comm_count(const mmba_comm *comm);
 /* Like mmba_plan_create, for the shard `comm` stands for.  Collective: every
  * shard calls it (and then every solve / measure / outputs call) together,
  * with the same pattern of NULL / non-NULL output pointers.  Each shard's
@@ -656,7 +662,24 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
 #define MMBA_PATH_DEST_LANE 12     /* 0 / 1: small off-diagonal Schur destinations never /
                                       always by a lane each (default: where they are most
                                       of at least 16,384) */
-#define MMBA_PATH_NUM 13
+#define MMBA_PATH_FAULT_SHARD 13   /* n >= 1: the shard of rank n - 1 of a sharded plan fails
+                                      (MMBA_ERR_INVALID) at its first damped solve -- a test
+                                      hook for a shard failing while its peers are inside a
+                                      collective */
+#define MMBA_PATH_COMM_TIMEOUT_MS 14 /* n > 0: collectives (and the host waits behind them)
+                                        give up after n ms: the communicator is aborted and
+                                        the call returns MMBA_ERR_COMM (default: environment
+                                        MMBA_COMM_TIMEOUT_MS, else 120000) */
+#define MMBA_PATH_STALL_SHARD 15   /* n >= 1: the shard of rank n - 1 of a sharded plan sleeps
+                                      for twice the collective timeout before its first damped
+                                      solve (a test hook for a shard that never reaches a
+                                      collective) */
+#define MMBA_PATH_PCR_CHAIN 16    /* 1: parallel cyclic reduction factors its blocks with the
+                                      2 x 2-pivot chain without square roots (16 % faster
+                                      chain, but 4.5e-6 off the oracle's one-step ||f|| on the
+                                      160-frame C4-spec scene where the default one-pivot
+                                      Cholesky chain is 1.8e-8 off: measured, opt-in only) */
+#define MMBA_PATH_NUM 17
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -21,6 +21,7 @@
 #include "adjust_mmba_core.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace mmba_shim {
@@ -518,13 +519,22 @@ bool Shim::ready() {
         no_device_ = true;
         return false;
     }
-    // every visible GPU (<= 8) behind this one caller: the library shards a
-    // solve over them itself (mmba_context_create_multi, ABI 9), Maya's main
-    // thread stays the only caller (adjust_base.cpp:1174-1183)
+    // One device by default (device 0: the plain single-device context).
+    // Sharding a solve over every visible GPU (mmba_context_create_multi,
+    // ABI 9; Maya's main thread stays the only caller, adjust_base.cpp:
+    // 1174-1183) is opt-in with MMSOLVER_MMBA_DEVICES=all (or a count): the
+    // in-process RCCL group has no test on distinct devices yet,
+    // and on one-device rehearsals the sharded forms measured slower than
+    // the whole solve on one GPU.
     int devs[8];
-    const int nd = std::min(mmba_device_count(), 8);
+    int nd = 1;
+    if (const char *e = std::getenv("MMSOLVER_MMBA_DEVICES")) {
+        const int avail = std::min(mmba_device_count(), 8);
+        nd = std::string(e) == "all" ? avail : std::max(1, std::min(std::atoi(e), avail));
+    }
     for (int d = 0; d < nd; ++d) devs[d] = d;
-    if (mmba_context_create_multi(devs, nd, &ctx_) != MMBA_OK) {
+    const int rc = nd == 1 ? mmba_context_create(0, &ctx_) : mmba_context_create_multi(devs, nd, &ctx_);
+    if (rc != MMBA_OK) {
         why_ = std::string("no gfx950 device: ") + mmba_last_error();
         no_device_ = true;
         ctx_ = nullptr;

@@ -115,6 +115,8 @@ def lib():
         L.mmba_comm_create_local.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.mmba_comm_destroy.restype = None
         L.mmba_comm_destroy.argtypes = [C.c_void_p]
+        L.mmba_comm_count.restype = C.c_int
+        L.mmba_comm_count.argtypes = [C.c_void_p]
         L.mmba_debug_dgemm.restype = C.c_int
         L.mmba_debug_dgemm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                        dp, C.c_int, C.c_void_p, C.c_int, dp, C.c_int,

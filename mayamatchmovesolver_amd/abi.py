@@ -37,7 +37,11 @@ PATH_SHARD_SEP = 9
 PATH_TRIAL_RECORDS = 10
 PATH_LENS_CF = 11
 PATH_DEST_LANE = 12
-PATH_NUM = 13
+PATH_FAULT_SHARD = 13
+PATH_COMM_TIMEOUT_MS = 14
+PATH_STALL_SHARD = 15
+PATH_PCR_CHAIN = 16
+PATH_NUM = 17
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -257,6 +261,7 @@ EXPORTED_SYMBOLS = [
     "mmba_comm_create_rccl",
     "mmba_comm_create_local",
     "mmba_comm_destroy",
+    "mmba_comm_count",
     "mmba_plan_create_sharded",
     "mmba_plan_measure",
     "mmba_plan_reproject",

@@ -139,4 +139,227 @@ __device__ __forceinline__ void bcr_chol_aug_blk(double (&a)[K], double *rs_out,
     if (rs_out && lane0 < K) rs_out[lane0] = rsl;
 }
 
+// 1/d: v_rcp_f64 plus two Newton steps (full fp64 precision).
+__device__ __forceinline__ double bcr_rcp(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, y, 1.);
+    y = fma(y, e, y);
+    e = fma(-d, y, 1.);
+    return fma(y, e, y);
+}
+
+// The same augmented factorisation with 2 x 2 pivot blocks (round 6): D =
+// U B U^T, U unit block-lower, B = diag(B_0 .. B_{K/2-1}) of 2 x 2 SPD blocks,
+// eliminated without square roots; the right-hand-side lanes leave with
+// (C^-1 b)^T for the Cholesky factor C = U chol(B) -- the same quantity as
+// bcr_chol_aug_blk (other rounding).  Per PAIR of pivots the dependent chain is
+// one broadcast of the 2 x 2 block, its determinant, one reciprocal and the two
+// multipliers' updates of the next pair (~11 fp64 operations), where the
+// one-pivot chain spends ~9 and two broadcasts per PIVOT (rsq, the scaled
+// column, its broadcast).  The multipliers' numerators u B_k adj are formed
+// from the lane's own entries while the reciprocal is in flight, and the
+// columns the update reads are the unscaled entries a_cp (broadcast at the
+// step's start, off the chain).  Panels of PW columns (PW even) take the
+// panel's updates from an LDS image (a broadcast read per entry).
+//
+// MODE 0: after each panel, the trailing update of every later column, then
+// the next panel (bcr_chol_aug_blk's schedule).  MODE 2: only the NEXT
+// panel's columns are updated right away; the panel's updates of the columns
+// beyond are deferred into the next panel's pivot steps (a slice per pair
+// step, from a double-buffered image), so they fill the latency of its
+// dependent chain instead of standing in front of it.  No wave fence: a
+// wave's LDS accesses execute in issue order and the compiler keeps the image
+// stores and loads (possibly aliasing) in program order.
+//
+// pl: (MODE 2 ? 2 : 1) * 64 * PW doubles of this wave's LDS plus 3 * K / 2
+// after them (pair constants).  K even.  bad: set when a pivot block is not
+// positive definite.
+template <int K, int PW, int MODE = 2>
+__device__ __forceinline__ void bcr_ldl2_aug_blk(double (&a)[K], double *pl, int &bad) {
+    static_assert(K % 2 == 0 && PW % 2 == 0, "pairs of pivots");
+    constexpr int NB = MODE == 2 ? 2 : 1;  // image buffers
+    const int lane0 = threadIdx.x & 63;
+    double mm[PW];   // this lane's multipliers of the current panel
+    double mmp[PW];  // ... of the previous panel (MODE 2: its deferred updates)
+#pragma unroll
+    for (int k = 0; k < PW; ++k) mmp[k] = 0.;
+#pragma unroll
+    for (int j0 = 0; j0 < K; j0 += PW) {
+        const int pn = j0 / PW;
+        const double *img_prev = pl + ((pn + 1) % NB) * 64 * PW;  // previous panel's image (MODE 2)
+        // deferred columns of the previous panel: [j0 + PW, K), in PW / 2 slices
+        constexpr int NSL = PW / 2;
+        const int d0 = j0 + PW, dcnt = (pn >= 1 && MODE == 2) ? (K - d0 > 0 ? K - d0 : 0) : 0;
+        const int dsl = (dcnt + NSL - 1) / NSL;
+#pragma unroll
+        for (int p = j0; p < j0 + PW && p < K; p += 2) {
+            int lane = lane0;
+            asm volatile("" : "+v"(lane));
+            const double x11 = bcr_rdlane(a[p], p), x21 = bcr_rdlane(a[p], p + 1),
+                         x22 = bcr_rdlane(a[p + 1], p + 1);
+            // the panel columns' pivot-column entries, before anything moves
+            double v1[PW], v2[PW];
+#pragma unroll
+            for (int c = p + 2; c < j0 + PW && c < K; ++c) {
+                v1[c - j0] = bcr_rdlane(a[p], c);
+                v2[c - j0] = bcr_rdlane(a[p + 1], c);
+            }
+            const double det = fma(-x21, x21, x11 * x22);
+            const bool below = lane > p + 1;
+            const double u1 = a[p], u2 = a[p + 1];
+            const double t1 = below ? fma(-u2, x21, u1 * x22) : 0.;
+            const double t2 = below ? fma(-u1, x21, u2 * x11) : 0.;
+            const double id = bcr_rcp(det);
+            const double m1 = t1 * id, m2 = t2 * id;
+            mm[p - j0] = m1;
+            mm[p - j0 + 1] = m2;
+#pragma unroll
+            for (int c = p + 2; c < j0 + PW && c < K; ++c)
+                a[c] = fma(-m2, v2[c - j0], fma(-m1, v1[c - j0], a[c]));
+            if constexpr (MODE == 2) {
+                // a slice of the previous panel's deferred updates
+                const int sl = (p - j0) / 2;
+#pragma unroll
+                for (int c = d0 + sl * dsl; c < d0 + (sl + 1) * dsl && c < K; ++c) {
+#pragma unroll
+                    for (int k = 0; k < PW; k += 2)
+                        a[c] = fma(-mmp[k + 1], img_prev[c * PW + k + 1],
+                                   fma(-mmp[k], img_prev[c * PW + k], a[c]));
+                }
+            }
+        }
+        if (j0 + PW < K) {
+            double *img = pl + (pn % NB) * 64 * PW;
+            // panel image: the pivot-column entries a_cp of every lane (the
+            // rows c beyond the panel read theirs back as broadcasts)
+            if constexpr (MODE == 0) wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < PW; ++k) img[lane0 * PW + k] = a[j0 + k];
+            if constexpr (MODE == 0) wave_lds_sync();
+            // MODE 0: every later column now; MODE 2: the next panel's only
+            constexpr int CE = MODE == 2 ? 2 * PW : K;
+#pragma unroll
+            for (int c = j0 + PW; c < j0 + CE && c < K; ++c) {
+#pragma unroll
+                for (int k = 0; k < PW; k += 2)
+                    a[c] = fma(-mm[k + 1], img[c * PW + k + 1], fma(-mm[k], img[c * PW + k], a[c]));
+            }
+            if constexpr (MODE == 0) wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < PW; ++k) mmp[k] = mm[k];
+        }
+    }
+    // chol(B_k) = [c11 0; c21 c22]: lanes k < K/2 form r11 = 1/c11, c21 and
+    // r22 = 1/c22 of pair k from the pivot rows 2k, 2k+1; then every
+    // right-hand-side lane applies chol(B)^-1 to its pair entries
+    double *pc = pl + NB * 64 * PW;
+    double *pv = pl + (NB - 1) * 64 * PW;  // (the last image is no longer read)
+    if constexpr (MODE == 0) wave_lds_sync();
+    {
+        double s0 = 0., s1 = 0.;
+#pragma unroll
+        for (int k = 0; k < K / 2; ++k)
+            if ((lane0 >> 1) == k) {
+                s0 = a[2 * k];
+                s1 = a[2 * k + 1];
+            }
+        if (lane0 < K) {
+            pv[lane0 * 2] = s0;
+            pv[lane0 * 2 + 1] = s1;
+        }
+    }
+    wave_lds_sync();
+    bool anybad = false;
+    if (lane0 < K / 2) {
+        const double x11 = pv[4 * lane0], x21 = pv[4 * lane0 + 2], x22 = pv[4 * lane0 + 3];
+        const double r11 = bcr_rsq(x11), c21 = x21 * r11;
+        const double s22 = fma(-c21, c21, x22);
+        const double r22 = bcr_rsq(s22);
+        anybad = !(x11 > 0. && s22 > 0. && r11 < __builtin_inf() && r22 < __builtin_inf());
+        pc[3 * lane0] = r11;
+        pc[3 * lane0 + 1] = c21;
+        pc[3 * lane0 + 2] = r22;
+    }
+    if (__builtin_amdgcn_ballot_w64(anybad) != 0) bad = 1;
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < K / 2; ++k) {
+        const double z1 = a[2 * k] * pc[3 * k];
+        a[2 * k] = z1;
+        a[2 * k + 1] = fma(-pc[3 * k + 1], z1, a[2 * k + 1]) * pc[3 * k + 2];
+    }
+    wave_lds_sync();
+}
+
+// LDL^T with 1 x 1 pivots (round 6), no square root on the chain: D =
+// U diag(d) U^T; per pivot the dependent chain is the broadcast of d_p, its
+// reciprocal and the multiplier's update of the next column (the column
+// entries a_cp the update reads are broadcast before the reciprocal is
+// ready).  The right-hand-side lanes hold y = U^-1 b; C^-1 b = diag(d)^-1/2 y
+// is applied after the chain (one rsq per pivot, lane-parallel).  Elimination
+// without pivoting of an SPD matrix, numerically Cholesky's.  Deferred
+// trailing updates and double-buffered panel images as bcr_ldl2_aug_blk's
+// MODE 2.  pl: 2 * 64 * PW + K doubles of this wave's LDS.
+template <int K, int PW>
+__device__ __forceinline__ void bcr_ldl1_aug_blk(double (&a)[K], double *pl, int &bad) {
+    const int lane0 = threadIdx.x & 63;
+    double mm[PW], mmp[PW];
+#pragma unroll
+    for (int k = 0; k < PW; ++k) mmp[k] = 0.;
+#pragma unroll
+    for (int j0 = 0; j0 < K; j0 += PW) {
+        const int pn = j0 / PW;
+        const double *img_prev = pl + ((pn + 1) % 2) * 64 * PW;
+        const int d0 = j0 + PW, dcnt = pn >= 1 ? (K - d0 > 0 ? K - d0 : 0) : 0;
+        const int dsl = (dcnt + PW - 1) / PW;  // one slice per pivot step
+#pragma unroll
+        for (int p = j0; p < j0 + PW && p < K; ++p) {
+            int lane = lane0;
+            asm volatile("" : "+v"(lane));
+            const double d = bcr_rdlane(a[p], p);
+            double v[PW];
+#pragma unroll
+            for (int c = p + 1; c < j0 + PW && c < K; ++c) v[c - j0] = bcr_rdlane(a[p], c);
+            const double u = lane > p ? a[p] : 0.;
+            const double m = u * bcr_rcp(d);
+            mm[p - j0] = m;
+#pragma unroll
+            for (int c = p + 1; c < j0 + PW && c < K; ++c) a[c] = fma(-m, v[c - j0], a[c]);
+            const int sl = p - j0;
+#pragma unroll
+            for (int c = d0 + sl * dsl; c < d0 + (sl + 1) * dsl && c < K; ++c) {
+#pragma unroll
+                for (int k = 0; k < PW; ++k) a[c] = fma(-mmp[k], img_prev[c * PW + k], a[c]);
+            }
+        }
+        if (j0 + PW < K) {
+            double *img = pl + (pn % 2) * 64 * PW;
+#pragma unroll
+            for (int k = 0; k < PW; ++k) img[lane0 * PW + k] = a[j0 + k];
+#pragma unroll
+            for (int c = j0 + PW; c < j0 + 2 * PW && c < K; ++c) {
+#pragma unroll
+                for (int k = 0; k < PW; ++k) a[c] = fma(-mm[k], img[c * PW + k], a[c]);
+            }
+#pragma unroll
+            for (int k = 0; k < PW; ++k) mmp[k] = mm[k];
+        }
+    }
+    // C^-1 b = d^-1/2 y: lane i < K holds d_i = a[i] (its own pivot)
+    double *rs = pl + 2 * 64 * PW;
+    double di = 0.;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (lane0 == k) di = a[k];
+    const double ri = bcr_rsq(di);
+    const bool anybad = lane0 < K && !(di > 0. && ri < __builtin_inf());
+    if (__builtin_amdgcn_ballot_w64(anybad) != 0) bad = 1;
+    wave_lds_sync();
+    if (lane0 < K) rs[lane0] = ri;
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] *= rs[k];
+    wave_lds_sync();
+}
+
 }  // namespace mmba

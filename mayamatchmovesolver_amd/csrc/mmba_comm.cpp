@@ -18,13 +18,85 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <chrono>
 #include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
 
 #include "mmba_plan.h"
 
 namespace mmba {
 
+// ---- bounded waits ----
+int comm_timeout_ms() {
+    const int p = path_choice(MMBA_PATH_COMM_TIMEOUT_MS);
+    if (p > 0) return p;
+    if (const char *e = std::getenv("MMBA_COMM_TIMEOUT_MS")) {
+        const int v = std::atoi(e);
+        if (v > 0) return v;
+    }
+    return 120000;
+}
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+void comm_wait(Comm *c, hipStream_t s, hipEvent_t ev) {
+    if (!c || !c->bounded()) {
+        if (ev)
+            MMBA_HIP(hipEventSynchronize(ev));
+        else
+            MMBA_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    const double t_end = now_ms() + comm_timeout_ms();
+    for (unsigned spins = 0;; ++spins) {
+        const hipError_t e = ev ? hipEventQuery(ev) : hipStreamQuery(s);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) MMBA_HIP(e);
+        if ((spins & 255u) == 255u) {
+            c->poll_async();  // throws on a communicator error
+            if (now_ms() > t_end) {
+                c->abort();
+                set_error("collective timed out after " + std::to_string(comm_timeout_ms()) +
+                          " ms (communicator aborted; another rank never joined)");
+                throw CommError();
+            }
+            if (spins > 65536u) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+}
+
 // ---- RCCL ----
+// Communicators are created non-blocking (ncclConfig_t::blocking = 0): the
+// initialisation and every collective return at once (ncclInProgress while
+// the communicator works) and the library polls ncclCommGetAsyncError with
+// the same deadline as comm_wait, so a rank that never joins costs the others
+// MMBA_ERR_COMM after comm_timeout_ms(), never a hang.
+static void rccl_settle(ncclComm_t c, const char *what) {
+    const double t_end = now_ms() + comm_timeout_ms();
+    for (unsigned spins = 0;; ++spins) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(c, &st);
+        if (r != ncclSuccess) st = r;
+        if (st == ncclSuccess) return;
+        if (st != ncclInProgress) {
+            set_error(std::string(what) + ": " + ncclGetErrorString(st));
+            throw CommError();
+        }
+        if (now_ms() > t_end) {
+            set_error(std::string(what) + ": timed out after " +
+                      std::to_string(comm_timeout_ms()) + " ms");
+            throw CommError();
+        }
+        if (spins > 1024u) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
 struct RcclComm : Comm {
     ncclComm_t c = nullptr;
     bool aborted = false;
@@ -35,9 +107,35 @@ struct RcclComm : Comm {
         if (c && !aborted) (void)ncclCommAbort(c);
         aborted = true;
     }
+    bool bounded() const override { return true; }
+    void poll_async() override {
+        if (aborted) throw CommError();
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess ||
+            (st != ncclSuccess && st != ncclInProgress)) {
+            set_error(std::string("RCCL asynchronous error: ") + ncclGetErrorString(st));
+            abort();
+            throw CommError();
+        }
+    }
+    int count() const override {
+        int n = 0;
+        if (c && !aborted && ncclCommCount(c, &n) == ncclSuccess) return n;
+        return nranks;
+    }
     void check(ncclResult_t r, const char *what) {
+        if (r == ncclInProgress) {
+            try {
+                rccl_settle(c, what);
+            } catch (const CommError &) {
+                abort();
+                throw;
+            }
+            return;
+        }
         if (r != ncclSuccess) {
             set_error(std::string(what) + ": " + ncclGetErrorString(r));
+            abort();
             throw CommError();
         }
     }
@@ -54,6 +152,54 @@ struct RcclComm : Comm {
               "ncclAllReduce");
     }
 };
+
+Comm *make_rccl_comm(ncclComm_t c, int rank, int nranks);
+
+// One communicator per device of this process (the multi-device context):
+// ncclCommInitRankConfig per device inside one group, non-blocking, settled
+// with a deadline -- ncclCommInitAll's blocking form could hang the caller.
+int rccl_init_all(const int *devices, int n, std::vector<Comm *> &out) {
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        set_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+        return MMBA_ERR_COMM;
+    }
+    std::vector<ncclComm_t> nc(n, nullptr);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    r = ncclGroupStart();
+    for (int k = 0; k < n && (r == ncclSuccess || r == ncclInProgress); ++k) {
+        if (hipSetDevice(devices[k]) != hipSuccess) {
+            r = ncclUnhandledCudaError;
+            break;
+        }
+        r = ncclCommInitRankConfig(&nc[k], n, id, k, &cfg);
+    }
+    const ncclResult_t re = ncclGroupEnd();
+    (void)hipSetDevice(cur);
+    bool ok = (r == ncclSuccess || r == ncclInProgress) &&
+              (re == ncclSuccess || re == ncclInProgress);
+    if (!ok) set_error(std::string("RCCL communicator group init: ") +
+                       ncclGetErrorString(r != ncclSuccess && r != ncclInProgress ? r : re));
+    for (int k = 0; k < n && ok; ++k) {
+        try {
+            if (!nc[k]) throw CommError();
+            rccl_settle(nc[k], "RCCL communicator group init");
+        } catch (const CommError &) {
+            ok = false;
+        }
+    }
+    if (!ok) {
+        for (ncclComm_t c : nc)
+            if (c) (void)ncclCommAbort(c);
+        return MMBA_ERR_COMM;
+    }
+    for (int k = 0; k < n; ++k) out.push_back(make_rccl_comm(nc[k], k, n));
+    return MMBA_OK;
+}
 
 Comm *make_rccl_comm(ncclComm_t c, int rank, int nranks) {
     auto *r = new RcclComm();
@@ -76,6 +222,9 @@ struct LocalGroup {
     bool aborted = false;
     double *bufs[LOCAL_MAX] = {};
     const double *sends[LOCAL_MAX] = {};
+    // bounded like RCCL's waits: a shard that never arrives aborts the group
+    // after comm_timeout_ms() (every waiter, and the late shard when it
+    // arrives, gets CommError)
     void barrier() {
         std::unique_lock<std::mutex> lk(m);
         if (aborted) throw CommError();
@@ -85,7 +234,15 @@ struct LocalGroup {
             ++gen;
             cv.notify_all();
         } else {
-            cv.wait(lk, [&] { return gen != g || aborted; });
+            const bool done = cv.wait_for(lk, std::chrono::milliseconds(comm_timeout_ms()),
+                                          [&] { return gen != g || aborted; });
+            if (!done) {
+                aborted = true;
+                cv.notify_all();
+                set_error("in-process shard group: collective timed out after " +
+                          std::to_string(comm_timeout_ms()) + " ms (group aborted)");
+                throw CommError();
+            }
             if (gen == g) {
                 set_error("in-process shard group aborted (another shard failed)");
                 throw CommError();
@@ -191,9 +348,20 @@ int mmba_comm_create_rccl(mmba_context *ctx, int rank, int nranks,
     c->nranks = nranks;
     ncclUniqueId id;
     std::memcpy(&id, unique_id, 128);
-    const ncclResult_t r = ncclCommInitRank(&c->c, nranks, id, rank);
-    if (r != ncclSuccess) {
-        set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;  // bounded: rccl_settle polls with a deadline
+    const ncclResult_t r = ncclCommInitRankConfig(&c->c, nranks, id, rank, &cfg);
+    bool ok = r == ncclSuccess || r == ncclInProgress;
+    if (!ok) set_error(std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+    if (ok && c->c) {
+        try {
+            rccl_settle(c->c, "ncclCommInitRankConfig");
+        } catch (const CommError &) {
+            ok = false;
+        }
+    }
+    if (!ok) {
+        if (c->c) (void)ncclCommAbort(c->c);
         c->c = nullptr;
         delete c;
         return MMBA_ERR_COMM;
@@ -215,6 +383,11 @@ int mmba_comm_create_local(int nranks, mmba_comm **out) {
         out[r] = reinterpret_cast<mmba_comm *>(static_cast<Comm *>(c));
     }
     return MMBA_OK;
+}
+
+int mmba_comm_count(const mmba_comm *comm) {
+    if (!comm) return MMBA_ERR_INVALID;
+    return reinterpret_cast<const Comm *>(comm)->count();
 }
 
 void mmba_comm_destroy(mmba_comm *comm) {

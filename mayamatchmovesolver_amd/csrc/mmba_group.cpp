@@ -5,8 +5,9 @@
 // (src/mmSolver/adjust/adjust_base.cpp:1174-1183); SURVEY 8(b) "Threading":
 // multi-GPU fan-out stays inside the library.  mmba_context_create_multi
 // makes one context (own stream) per device plus the group's communicators:
-//   - distinct devices: RCCL, ncclCommInitAll -- one communicator per device
-//     in this process, each driven by its own host thread;
+//   - distinct devices: RCCL, one communicator per device in this process
+//     (non-blocking ncclCommInitRankConfig in one group, settled with a
+//     deadline: rccl_init_all), each driven by its own host thread;
 //   - one device named N times: the in-process transport (LocalComm), so a
 //     one-GPU box runs the N-shard path through the same entry.
 // mmba_plan_create over such a context builds one sharded plan per device
@@ -38,6 +39,7 @@
 namespace mmba {
 
 Comm *make_rccl_comm(ncclComm_t c, int rank, int nranks);  // mmba_comm.cpp
+int rccl_init_all(const int *devices, int n, std::vector<Comm *> &out);  // mmba_comm.cpp
 
 // ---------------------------------------------------------------------------
 // kernels of the hand-back and the step-row gather
@@ -204,7 +206,7 @@ void Plan::handback_sharded(const double *dx, double *x_out, double *f_out, doub
                 MMBA_HIP(hipMemcpyAsync(eu_out + 2 * (size_t)Mg, eu2 + 2 * (size_t)M,
                                         sizeof(double) * nrows, hipMemcpyDeviceToHost, s));
         }
-        MMBA_HIP(hipStreamSynchronize(s));
+        host_sync();
         if (x_out)
             for (int j = 0; j < n_own; ++j) x_out[own_par_h[j]] = h_pack[j];
         if (outs) {
@@ -241,7 +243,7 @@ void Plan::handback_sharded(const double *dx, double *x_out, double *f_out, doub
     if (f_out) MMBA_HIP(hipMemcpyAsync(f_out, tf, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
     if (eu_out) MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
     if (ed_out) MMBA_HIP(hipMemcpyAsync(ed_out, td, sizeof(double) * Mg, hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    host_sync();
 }
 
 bool Plan::poll_agree() {
@@ -325,9 +327,13 @@ struct ShardGroup {
         }
         rc[k] = r;
         err[k] = r == MMBA_OK ? std::string() : std::string(mmba_last_error());
-        // a device or communicator failure can leave the other shards in a
-        // collective: release them (the group is unusable afterwards)
-        if (r == MMBA_ERR_DEVICE || r == MMBA_ERR_COMM) abort_all();
+        // ANY failure of one shard can leave the others inside a collective
+        // (an Invalid / Unsupported / bad_alloc thrown mid-solve is as fatal
+        // to them as a device error): release them at once; the group is
+        // unusable afterwards (run() marks it broken).  The interrupt is
+        // agreed through the poll share, so every shard stops at the same
+        // point and nobody waits.
+        if (n > 1 && r != MMBA_OK && r != MMBA_ERR_INTERRUPTED) abort_all();
         return r;
     }
 
@@ -341,6 +347,9 @@ struct ShardGroup {
                 cv.wait(lk, [&] { return stop || gen != seen; });
                 if (stop) return;
                 seen = gen;
+                // a replicated problem runs shard 0 alone (n == 1): the
+                // other workers stay idle whatever wakes them
+                if (k >= n || !job) continue;
                 f = job;
             }
             run_one(*f, k);
@@ -375,13 +384,17 @@ struct ShardGroup {
             done_cv.wait(lk, [&] { return remaining == 0; });
             job = nullptr;
         }
-        int out = MMBA_OK;
+        // the first shard's failure, preferring a cause over the
+        // communicator errors of the shards it released
+        int out = MMBA_OK, first = -1;
         for (int k = 0; k < n; ++k) {
-            if (rc[k] == MMBA_ERR_DEVICE || rc[k] == MMBA_ERR_COMM) broken = true;
-            if (rc[k] != MMBA_OK && out == MMBA_OK) {
-                out = rc[k];
-                set_error(err[k]);
-            }
+            if (n > 1 && rc[k] != MMBA_OK && rc[k] != MMBA_ERR_INTERRUPTED) broken = true;
+            if (rc[k] == MMBA_OK) continue;
+            if (first < 0 || (rc[first] == MMBA_ERR_COMM && rc[k] != MMBA_ERR_COMM)) first = k;
+        }
+        if (first >= 0) {
+            out = rc[first];
+            set_error(err[first]);
         }
         return out;
     }
@@ -580,15 +593,7 @@ int mmba_context_create_multi(const int *devices, int ndevices, mmba_context **o
             if (rc == MMBA_OK)
                 for (mmba_comm *x : cs) c->comms.push_back(reinterpret_cast<Comm *>(x));
         } else {
-            std::vector<ncclComm_t> nc(ndevices, nullptr);
-            const ncclResult_t r = ncclCommInitAll(nc.data(), ndevices, devices);
-            if (r != ncclSuccess) {
-                set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
-                rc = MMBA_ERR_COMM;
-            } else {
-                for (int k = 0; k < ndevices; ++k)
-                    c->comms.push_back(make_rccl_comm(nc[k], k, ndevices));
-            }
+            rc = rccl_init_all(devices, ndevices, c->comms);
         }
     }
     if (rc != MMBA_OK) {

@@ -49,7 +49,24 @@ struct Comm {
     // a shard failed outside a collective: the others' pending and future
     // collectives fail (CommError) instead of waiting forever
     virtual void abort() {}
+    // RCCL: collectives complete on the device, so a host wait on a stream
+    // that carries one is bounded (comm_wait) and polls the communicator's
+    // asynchronous error; the in-process group waits in its own barrier
+    virtual bool bounded() const { return false; }
+    virtual void poll_async() {}
+    // ranks as the transport reports them (ncclCommCount)
+    virtual int count() const { return nranks; }
 };
+
+// Bounded wait for every collective: milliseconds before
+// a communicator is aborted and the call fails with MMBA_ERR_COMM instead of
+// hanging its caller (path MMBA_PATH_COMM_TIMEOUT_MS, else the environment's
+// MMBA_COMM_TIMEOUT_MS, else 120 s).
+int comm_timeout_ms();
+// Wait until the event (or, ev == NULL, the stream) completes; through a
+// bounded communicator the wait polls and, past comm_timeout_ms(), aborts the
+// communicator and throws CommError.
+void comm_wait(Comm *c, hipStream_t s, hipEvent_t ev);
 
 // Band + arrow layout of the reduced system (narrow structures): rows of
 // camera-frame parameters keep w+1 entries each (columns r-w .. r), the
@@ -112,6 +129,7 @@ constexpr int PCR_NCMAX = 48;
 
 struct PcrDev {
     int K = 0, nb = 0, w = 0, nblk = 0, nlev = 0;
+    int nth = 256;  // k_pcr_solve workgroup: 512 threads when that grid is resident (same bits)
     const double *Bd = nullptr;  // band input [nb][w+1]
     // publications of k_pcr_solve / k_pcr_rhs: 16-B granules {value, epoch,
     // epoch} (zeroed at build; epochs start at 1), per [nlev][nblk]

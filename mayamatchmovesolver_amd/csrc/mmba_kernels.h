@@ -336,6 +336,9 @@ void pcr_rhs_mc(hipStream_t s, const PcrDev &P, const double *R, int ldr, int nc
 // are ordered across streams while there is more than one
 void pcr_note_context(int dev, int delta);
 int pcr_max_resident(int K);
+int pcr_resident_wide(int K);  // the 512-thread form's bound
+// workgroups of one k_pcr_solve launch over nblk blocks (the XCD map)
+int pcr_grid(int nblk);
 // Block-diagonal + arrow solver (mmba_bdiag.hip): factor S, y = L^-1 r and,
 // with x, the solution (scattered to parameter order into xs when non-null).
 void bd_direct(hipStream_t s, const DevProblem &P, const BdDev &D, const double *Acc,

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -61,7 +62,7 @@ void Plan::span_end(int kind) {
 
 void Plan::collect_spans() {
     if (!spans.empty()) {
-        MMBA_HIP(hipStreamSynchronize(s));
+        host_sync();
         for (const Span &sp : spans) {
             float ms = 0.f;
             MMBA_HIP(hipEventElapsedTime(&ms, sp.a, sp.b));
@@ -115,7 +116,17 @@ void Plan::stage_slots() {
     slots_staged = true;
 }
 
+// A host wait on the plan's stream: bounded through an RCCL communicator
+// (the stream may carry a collective another rank never joins: comm_wait
+// aborts it after comm_timeout_ms() and throws CommError), a plain
+// synchronisation otherwise.
+void Plan::host_sync() { comm_wait(nranks > 1 ? comm : nullptr, s, nullptr); }
+
 void Plan::wait_event() {
+    if (nranks > 1 && comm && comm->bounded()) {
+        comm_wait(comm, s, ev_sync);
+        return;
+    }
     if (!spin_wait) {
         MMBA_HIP(hipEventSynchronize(ev_sync));
         return;
@@ -149,6 +160,12 @@ void Plan::read_slots(int lo, int hi) {
         for (unsigned spins = 1;; ++spins) {
             if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq_next) return;
             if ((spins & 4095u) == 0) {
+                if (nranks > 1 && comm && comm->bounded()) {
+                    // (mirrored reductions are taken unsharded only; kept
+                    // bounded should that change)
+                    host_sync();
+                    if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq_next) return;
+                }
                 const hipError_t e = hipStreamQuery(s);
                 if (e == hipSuccess) {
                     if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq_next) return;
@@ -162,8 +179,8 @@ void Plan::read_slots(int lo, int hi) {
     if (!mirrored)
         MMBA_HIP(hipMemcpyAsync(h_scalar + lo, d_scalar + lo, sizeof(double) * (hi - lo + 1),
                                 hipMemcpyDeviceToHost, s));
-    if (!spin_wait) {
-        MMBA_HIP(hipStreamSynchronize(s));
+    if (!spin_wait || (nranks > 1 && comm && comm->bounded())) {
+        host_sync();
         return;
     }
     // The LM control thread has nothing else to do: poll an event instead of
@@ -570,6 +587,14 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
 
 // d_xs = (A + lam D^2)^-1 g; failure flag -> SL_FAIL (max over shards).
 void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dnorm_by_trial) {
+    if (nranks > 1 && path_choice(MMBA_PATH_FAULT_SHARD) == rank + 1)
+        throw Invalid{"injected shard fault (MMBA_PATH_FAULT_SHARD)"};
+    if (nranks > 1 && path_choice(MMBA_PATH_STALL_SHARD) == rank + 1 && !stall_done) {
+        // test hook: this shard reaches its next collective only after its
+        // peers' bounded waits have expired
+        stall_done = true;
+        std::this_thread::sleep_for(std::chrono::milliseconds(2 * (long long)comm_timeout_ms()));
+    }
     if (!red_defer_ok()) flush_red();
     if (b15 && !b15_inner) {
         // B15: (M + U B U^T) xs = u + s c from M z_u = u and M z_c = c, the
@@ -1014,7 +1039,7 @@ void Plan::download_params(const double *dx, double *x_out) {
         return;
     }
     MMBA_HIP(hipMemcpyAsync(x_out, dx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    host_sync();
 }
 
 void Plan::error_stats_enqueue(const double *ed, int base) {
@@ -1116,7 +1141,7 @@ int Plan::dense_jacobian(const double *x, double *fjac) {
     MMBA_HIP(hipMemcpyAsync(J.data(), d_J, sizeof(double) * J.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(jc.data(), d_jcol, sizeof(int) * jc.size(), hipMemcpyDeviceToHost, s));
     MMBA_HIP(hipMemcpyAsync(nl.data(), d_nloc, sizeof(int) * M, hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    host_sync();
     collect_spans();
     std::memset(fjac, 0, sizeof(double) * (size_t)m * n);
     for (int i = 0; i < M; ++i) {
@@ -1187,7 +1212,7 @@ int Plan::reduced_residual(const double *x, double lam, double *relres) {
     k_dense_symv_res<<<(nR + 255) / 256, 256, 0, s>>>(d_Skeep, ds.ld, nR, d_xR, d_rkeep, acc);
     double h[2];
     MMBA_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, s));
-    MMBA_HIP(hipStreamSynchronize(s));
+    host_sync();
     read_slots(SL_DNORM, SL_FAIL);
     if (h_scalar[SL_FAIL] != 0.) throw Invalid{"reduced residual hook: the factorisation failed"};
     *relres = std::sqrt(h[0] / h[1]);
@@ -1250,7 +1275,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
     try {
         return solve_once(x_inout, fvec_out, eu_out, ed_out, res, cb, trace);
     } catch (const SpecMismatch &) {
-        MMBA_HIP(hipStreamSynchronize(s));
+        host_sync();
         ++spec_replays;
         pre_jac_pending = false;
         seq_pending = false;
@@ -1401,7 +1426,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                             std::vector<double> sb(n);
                             MMBA_HIP(hipMemcpyAsync(sb.data(), d_stepB, sizeof(double) * n,
                                                     hipMemcpyDeviceToHost, s));
-                            MMBA_HIP(hipStreamSynchronize(s));
+                            host_sync();
                             for (int j = 0; j < k; ++j) jac_evals += sb[j] != 0. ? 1 : 0;
                         }
                     }

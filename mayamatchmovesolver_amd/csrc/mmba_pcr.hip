@@ -59,6 +59,20 @@
 namespace mmba {
 
 typedef double pcr_d4 __attribute__((ext_vector_type(4)));
+
+// panel width of the 2 x 2-pivot chain (bcr_ldl2_aug_blk, deferred trailing
+// updates): one wave, 24 x 24 augmented factorisation 2.32 us at 4, 2.44 at
+// 6, 2.39 at 8 against the one-pivot chain's 2.75 (tools/ubench/chain2.hip,
+// profiles/r6_pcr/chain2.txt)
+#ifndef PCR_PW
+#define PCR_PW 4
+#endif
+// threads per k_pcr_solve workgroup: the pivot chains use three waves, the
+// products (12 MFMA tiles), the granule loads of the update and the log
+// spread over all of them
+#ifndef PCR_NTH
+#define PCR_NTH 256
+#endif
 typedef unsigned int pcr_u4 __attribute__((ext_vector_type(4)));
 
 // Data-tagged 16-B granules (MI355X guide: handoff-1to1, Guideline 16 R2):
@@ -97,40 +111,49 @@ __host__ __device__ constexpr int pcr_log_size() {
 // The damped solve.  blockIdx.x = block j.  r_in / x_out: reduced-order
 // vectors (nb rows); x is also scattered to parameter order (xs[row_param]).
 // ---------------------------------------------------------------------------
-template <int K>
-__global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__restrict__ r_in,
+template <int K, bool L2 = false, int NTH = PCR_NTH>
+__global__ void __launch_bounds__(NTH) k_pcr_solve(PcrDev P, const double *__restrict__ r_in,
                                                    double *__restrict__ x_out, double *xs,
                                                    unsigned epoch, int *fail,
                                                    long long *probe = nullptr) {
     constexpr int KS = K + 1;  // LDS row stride (odd: a lane-per-row read is conflict-free)
     constexpr int K1 = K + 1;  // row stride of X1 / X2 (the rho column)
-    constexpr int PW = MMBA_BCR_PW;
     constexpr int PS = pcr_pub_size<K>(), LS = pcr_log_size<K>();
     constexpr int NT = K / 4;  // MFMA k-steps
-    constexpr int NE = (K * K + 255) / 256;  // update entries per thread
+    constexpr int NE = (K * K + NTH - 1) / NTH;  // update entries per thread
+    constexpr int NW = NTH / 64;                // waves
     __shared__ double sD[K * KS], sL[K * KS], sU[K * KS];  // own block (row-major)
     // factor images (row-major): C^-1, P, Q, and rho
     __shared__ double sCi[K * KS], sP[K * KS], sQ[K * KS];
     __shared__ double sr[K], srho[K];
     __shared__ double sI[K * KS];   // the identity (right-hand sides of the C^-1 chain)
     __shared__ double sZ[2 * K];    // a zero row, then scratch for lanes without an operand
-    __shared__ double pl[3][64 * PW];  // pivot-chain panel images, waves 0..2
+    // pivot-chain panel images + pair constants, waves 0..2
+    __shared__ double pl[3][2 * 64 * PCR_PW + 64];
     __shared__ int bad_s, ok_s;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int j = blockIdx.x, nblk = P.nblk, nb = P.nb, W1 = P.w + 1;
+    // XCD-aware placement (round 6): workgroup b runs on XCD b % 8; block
+    // j = (b % 8) * per + b / 8 keeps the neighbours of the first four levels
+    // (strides 1..8) on one XCD; the grid is 8 * per workgroups (pcr_grid),
+    // the extra ones exit at once (60.8 against 62.3 us on the C4 system,
+    // profiles/r6_pcr/)
+    const int per = (P.nblk + 7) / 8;
+    const int j = (blockIdx.x % 8) * per + blockIdx.x / 8, nblk = P.nblk, nb = P.nb, W1 = P.w + 1;
+    if (j >= nblk) return;
     if (tid == 0) {
         bad_s = 0;
         ok_s = 1;
     }
-    // probe (tools/ubench/pcr_probe.hip): thread 0 of block nblk / 2 stores
-    // the wall clock (100 MHz) at the phase ends of every level
-    long long *pr = (probe && j == nblk / 2 && tid == 0) ? probe : nullptr;
+    // probe (tools/ubench/pcr_probe.hip): thread 0 of every block stores the
+    // wall clock (100 MHz) at the phase ends of every level (block j's slots
+    // at probe[64 j ..])
+    long long *pr = (probe && tid == 0) ? probe + (size_t)j * 64 : nullptr;
     auto stamp = [&](int lvl, int ph) {
         if (pr) pr[lvl * 8 + ph] = (long long)wall_clock64();
     };
     // ---- level-0 state from the band layout: D_j (lower), L_j = S[j, j-1],
     // U_j = S[j, j+1] = S[j+1, j]^T, r_j; padding rows: identity, uncoupled
-    for (int q = tid; q < K * K; q += 256) {
+    for (int q = tid; q < K * K; q += NTH) {
         const int i = q / K, c = q % K, R = j * K + i;
         double dv = 0., lv = 0., uv = 0.;
         if (R < nb) {
@@ -148,7 +171,7 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
         sU[i * KS + c] = uv;
     }
     if (tid < K) sr[tid] = (j * K + tid < nb) ? r_in[j * K + tid] : 0.;
-    for (int q = tid; q < K * KS; q += 256) sI[q] = (q / KS == q % KS) ? 1. : 0.;
+    for (int q = tid; q < K * KS; q += NTH) sI[q] = (q / KS == q % KS) ? 1. : 0.;
     if (tid < K) sZ[tid] = 0.;
     __syncthreads();
     int s = 1;
@@ -185,7 +208,12 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
             double a[K];
 #pragma unroll
             for (int c = 0; c < K; ++c) a[c] = src[c * st];
-            bcr_chol_aug_blk<K, PW>(a, nullptr, pl[wv], bad);
+            stamp(lvl, 5);
+            if constexpr (L2)
+                bcr_ldl2_aug_blk<K, PCR_PW, 2>(a, pl[wv], bad);
+            else
+                bcr_chol_aug_blk<K, MMBA_BCR_PW>(a, nullptr, pl[wv], bad);
+            stamp(lvl, 6);
 #pragma unroll
             for (int i = 0; i < K; ++i) dst[i * dt] = a[i];
         }
@@ -205,7 +233,7 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
                     if (xs && P.row_param[R] >= 0) xs[P.row_param[R]] = acc;
                 }
             }
-            for (int q = tid; q < K * K; q += 256) log[q] = sCi[(q / K) * KS + q % K];
+            for (int q = tid; q < K * K; q += NTH) log[q] = sCi[(q / K) * KS + q % K];
             if (tid == 0) {
                 P.flev[j] = lvl;
                 if (bad_s) atomicOr(fail, 1);
@@ -214,25 +242,26 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
         }
         // ---- what the consumers subtract: X1 = P^T [P | rho] (left, hp),
         // X2 = Q^T [Q | rho] (right, hq), X3 = Q^T P (both): 32 x 32 padded
-        // products, 12 tiles over the 4 waves (tile t: product t / 4, 16 x 16
+        // products, 12 tiles over the NW waves (tile t: product t / 4, 16 x 16
         // tile t % 4), stored write-through from the accumulators
         const auto gpub = sc1_view(P.pub + ((size_t)lvl * nblk + j) * PS * 2, PS * 16u);
         {
             // the wave's three tiles interleaved (independent accumulators);
             // a product nobody reads runs on zero operands and is not stored
             const int i16 = lane & 15, k4 = lane >> 4;
-            pcr_d4 acc[3];
+            constexpr int TT = (12 + NW - 1) / NW;  // tiles per wave
+            pcr_d4 acc[TT];
             // per lane and tile one LDS operand base and stride each: A(i, u)
             // = Y(u, i) (Y = P or Q), B(u, c) = Z(u, c) with column K = rho
             // (X1, X2); padding rows / columns and unneeded products read the
             // zero row
-            const double *pa[3], *pb[3];
-            int sa[3], sb[3], bc[3], cmax[3];
-            bool need[3];
+            const double *pa[TT], *pb[TT];
+            int sa[TT], sb[TT], bc[TT], cmax[TT];
+            bool need[TT];
 #pragma unroll
-            for (int tt = 0; tt < 3; ++tt) {
-                const int t = wv + 4 * tt, prod = t >> 2, ti = (t >> 1) & 1, tc = t & 1;
-                need[tt] = prod == 0 ? hp : (prod == 1 ? hq : (hp && hq));
+            for (int tt = 0; tt < TT; ++tt) {
+                const int t = wv + NW * tt, prod = t >> 2, ti = (t >> 1) & 1, tc = t & 1;
+                need[tt] = t < 12 && (prod == 0 ? hp : (prod == 1 ? hq : (hp && hq)));
                 cmax[tt] = prod == 2 ? K : K + 1;
                 const int ai = ti * 16 + i16;
                 bc[tt] = tc * 16 + i16;
@@ -249,14 +278,14 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
             for (int st = 0; st < NT; ++st) {
                 const int u = 4 * st + k4;
 #pragma unroll
-                for (int tt = 0; tt < 3; ++tt)
+                for (int tt = 0; tt < TT; ++tt)
                     acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[tt][u * sa[tt]], pb[tt][u * sb[tt]],
                                                                    acc[tt], 0, 0, 0);
             }
 #pragma unroll
-            for (int tt = 0; tt < 3; ++tt) {
+            for (int tt = 0; tt < TT; ++tt) {
                 if (!need[tt]) continue;
-                const int t = wv + 4 * tt, prod = t >> 2, ti = (t >> 1) & 1;
+                const int t = wv + NW * tt, prod = t >> 2, ti = (t >> 1) & 1;
                 const int g0 = prod == 0 ? 0 : (prod == 1 ? K * K1 : 2 * K * K1);
                 const int ld = prod == 2 ? K : K1;
 #pragma unroll
@@ -270,7 +299,7 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
         stamp(lvl, 2);
         // ---- the Newton pass's log (later launches read it: plain stores;
         // issued during the granule wait instead: 66.7 against 65.0 us)
-        for (int q = tid; q < K * K; q += 256) {
+        for (int q = tid; q < K * K; q += NTH) {
             const int x = (q / K) * KS + q % K;
             log[q] = sCi[x];
             log[K * K + q] = sP[x];
@@ -294,7 +323,7 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
             int gi[2][NG];
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
-                const int q = tid + 256 * e, i = q / K, c = q % K;
+                const int q = tid + NTH * e, i = q / K, c = q % K;
                 const bool in = q < K * K;
                 gi[0][2 * e] = (hp && in && c <= i) ? K * K1 + i * K1 + c : -1;
                 // X3 is published only by a block with neighbours on both
@@ -332,11 +361,12 @@ __global__ void __launch_bounds__(256) k_pcr_solve(PcrDev P, const double *__res
                         if (gi[h][k] >= 0 && !gran_ok(g[h][k], epoch))
                             g[h][k] = gran_ld(h ? vq : vp, gi[h][k]);
             }
+            stamp(lvl, 7);
             if (late) ok_s = 0;  // (ok_s = 1 was set before this level's chain)
             auto val = [&](int h, int k) { return gi[h][k] >= 0 ? gran_val(g[h][k]) : 0.; };
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
-                const int q = tid + 256 * e, i = q / K, c = q % K;
+                const int q = tid + NTH * e, i = q / K, c = q % K;
                 if (q < K * K) {
                     if (c <= i) sD[i * KS + c] -= val(0, 2 * e) + val(1, 2 * e);
                     sL[i * KS + c] = -val(0, 2 * e + 1);  // 0 without j - 2s
@@ -648,14 +678,33 @@ static void pcr_ordered(hipStream_t s, Launch &&launch) {
     o.recorded = true;
 }
 
+// k_pcr_solve's grid: 8 workgroups per block-row of the XCD map
+int pcr_grid(int nblk) { return 8 * ((nblk + 7) / 8); }
+
 void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, double *xs, int *fail) {
+    const int g = pcr_grid(P.nblk);
+    // the one-pivot Cholesky chain by default: the 2 x 2-pivot chain is
+    // faster (2.32 against 2.75 us per factorisation, tools/ubench/chain2.hip)
+    // but measured less accurate on an ill-conditioned C4-spec step
+    // (tools/pcr_chain_diag.py, profiles/r6_pcr/pcr_chain_diag.txt): opt-in
+    const bool l2 = path_choice(MMBA_PATH_PCR_CHAIN) > 0;
+    const bool wide = P.nth == 512;
     pcr_ordered(s, [&] {
         const unsigned ep = pcr_next_epoch();
-        switch (P.K) {
-            case 8: k_pcr_solve<8><<<P.nblk, 256, 0, s>>>(P, r, x, xs, ep, fail); break;
-            case 16: k_pcr_solve<16><<<P.nblk, 256, 0, s>>>(P, r, x, xs, ep, fail); break;
-            default: k_pcr_solve<24><<<P.nblk, 256, 0, s>>>(P, r, x, xs, ep, fail); break;
+#define MMBA_PCR_GO(KK, L2V, NT) k_pcr_solve<KK, L2V, NT><<<g, NT, 0, s>>>(P, r, x, xs, ep, fail)
+#define MMBA_PCR_K(L2V, NT)                          \
+    switch (P.K) {                                   \
+        case 8: MMBA_PCR_GO(8, L2V, NT); break;      \
+        case 16: MMBA_PCR_GO(16, L2V, NT); break;    \
+        default: MMBA_PCR_GO(24, L2V, NT); break;    \
+    }
+        if (l2) {
+            if (wide) { MMBA_PCR_K(true, 512) } else { MMBA_PCR_K(true, 256) }
+        } else {
+            if (wide) { MMBA_PCR_K(false, 512) } else { MMBA_PCR_K(false, 256) }
         }
+#undef MMBA_PCR_K
+#undef MMBA_PCR_GO
     });
 }
 
@@ -683,8 +732,28 @@ void pcr_rhs_mc(hipStream_t s, const PcrDev &P, const double *R, int ldr, int nc
     });
 }
 
-// Workgroups of k_pcr_solve<K> the device keeps resident at once (every
-// block's workgroup must be: the plan takes PCR only when nblk fits).
+// Workgroups of the 512-thread k_pcr_solve<K> the device keeps resident at
+// once: the plan takes that form (8 waves: the products and the update's
+// granule loads over twice the waves; 62.6 against 65.5 us on the C4 system,
+// profiles/r6_pcr/) when its whole grid fits, the 256-thread one otherwise.
+int pcr_resident_wide(int K) {
+    int dev = 0, per_cu = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    hipError_t e;
+    switch (K) {
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8, false, 512>, 512, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16, false, 512>, 512, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24, false, 512>, 512, 0); break;
+    }
+    if (e != hipSuccess) return 0;
+    return per_cu * cus;
+}
+
+// Workgroups of k_pcr_solve<K> (256 threads) the device keeps resident at
+// once (every block's workgroup must be: the plan takes PCR only when nblk
+// fits).
 int pcr_max_resident(int K) {
     int dev = 0, per_cu = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -692,9 +761,9 @@ int pcr_max_resident(int K) {
         return 0;
     hipError_t e;
     switch (K) {
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8>, 256, 0); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16>, 256, 0); break;
-        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24>, 256, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8, false, 256>, 256, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16, false, 256>, 256, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24, false, 256>, 256, 0); break;
     }
     if (e != hipSuccess) return 0;
     return per_cu * cus;

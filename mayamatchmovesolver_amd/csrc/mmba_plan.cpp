@@ -1963,9 +1963,17 @@ void Plan::setup_band(int Pforce) {
             {
                 // Pforce == -2 (mmba_debug_band_solve): block cyclic reduction only
                 const bool pcr_off = path_choice(MMBA_PATH_PCR) == 0 || Pforce == -2;
-                if (!pcr_off && nG == 0 && B.K <= 24 && B.nblk <= pcr_max_resident(B.K)) {
+                // shards take the agreed (smallest) bound: the same solver,
+                // hence the same bits, on every shard
+                const int kres = std::min(B.K / 8 - 1, 2);
+                const int resident = B.K > 24 ? 0
+                                     : (nranks > 1 && shard_resident[kres] >= 0)
+                                         ? shard_resident[kres]
+                                         : pcr_max_resident(B.K);
+                if (!pcr_off && nG == 0 && B.K <= 24 && pcr_grid(B.nblk) <= resident) {
                     PcrDev &Q = bs.pcr;
                     Q.K = B.K;
+                    Q.nth = pcr_grid(B.nblk) <= pcr_resident_wide(B.K) ? 512 : 256;
                     Q.nb = nb;
                     Q.w = w;
                     Q.nblk = B.nblk;
@@ -2105,6 +2113,8 @@ void Plan::setup_band(int Pforce) {
         bs.fail = d_fail;
         PcrDev &Q = bs.ipcr;
         Q.K = std::max(8, (w + 7) / 8 * 8);
+        // (one process's PCR launches on a device are ordered, pcr_ordered)
+        Q.nth = pcr_grid((hp.r1 - hp.r0 + Q.K - 1) / Q.K) <= pcr_resident_wide(Q.K) ? 512 : 256;
         Q.nb = ast;
         Q.w = w;
         Q.nblk = (ast + Q.K - 1) / Q.K;
@@ -2137,9 +2147,11 @@ void Plan::setup_band(int Pforce) {
 // the last, with the shards' Schur terms) is all-reduced and solved on every
 // shard.  Needs no arrow, w <= 23 and every shard's interior resident on the
 // device; every shard decides the same from the shared partition and the
-// smallest residency bound of the shards' devices (all-reduced once: a
-// shard on a device with fewer CUs must not take another path than the
-// rest, whose collectives would then differ).
+// smallest residency bound of the shards' devices (all-reduced by
+// mmba_plan_create_sharded before any shard builds, so that no build-time
+// failure can leave a shard in another collective than its peers: a shard on
+// a device with fewer CUs must not take another path than the rest, whose
+// collectives would then differ).  No collective here.
 bool Plan::sep_form(int w) {
     if (nranks <= 1 || nG != 0 || w > 23 || w <= 0) return false;
     // Default (round 5): the whole-S form while the WHOLE band system fits one
@@ -2159,18 +2171,11 @@ bool Plan::sep_form(int w) {
         if (len < K) return false;
         most = std::max(most, (len + K - 1) / K);
     }
-    if (sep_resident_K != K) {
-        double v = -(double)pcr_max_resident(K), *d = dalloc<double>(1);
-        MMBA_HIP(hipMemcpyAsync(d, &v, sizeof(double), hipMemcpyHostToDevice, s));
-        allreduce(d, 1, ReduceOp::Max);
-        MMBA_HIP(hipMemcpyAsync(&v, d, sizeof(double), hipMemcpyDeviceToHost, s));
-        MMBA_HIP(hipStreamSynchronize(s));
-        sep_resident = (int)-v;
-        sep_resident_K = K;
-    }
-    if (most > sep_resident) return false;
+    const int sep_resident = shard_resident[K / 8 - 1];
+    if (sep_resident < 0) return false;
+    if (pcr_grid(most) > sep_resident) return false;
     if (pin == 1) return true;
-    return (nR + K - 1) / K > sep_resident;  // the whole system would not be resident
+    return pcr_grid((nR + K - 1) / K) > sep_resident;  // the whole system would not be resident
 }
 
 }  // namespace mmba

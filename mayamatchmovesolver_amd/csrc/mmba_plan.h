@@ -111,7 +111,11 @@ struct Plan {
     int *d_inst_attr_plug = nullptr;
     void build_lens_instances(const mmba_problem *pr);
     bool sep_form(int w);
-    int sep_resident = 0, sep_resident_K = 0;  // min over shards of pcr_max_resident(K)
+    // min over shards of pcr_max_resident(K) for K = 8 / 16 / 24, agreed by
+    // mmba_plan_create_sharded BEFORE the build (a collective inside the
+    // build could pair with another shard's build-status collective); -1:
+    // not agreed (the separator form is then never taken)
+    int shard_resident[3] = {-1, -1, -1};
     // P with every lens instance slot at its plug value: what the reference
     // measures before setParameters first runs (solveFrames' initial
     // measureErrors, adjust_base.cpp:1002-1004 then 1076-1089)
@@ -487,6 +491,8 @@ struct Plan {
     RedSpec pend_rs{};
     bool red_defer_ok() const;
     void flush_red();
+    void host_sync();
+    bool stall_done = false;  // MMBA_PATH_STALL_SHARD fired
     void wait_event();
     // speculative trial (lmpar's first, undamped, step taken before the
     // host has read it): its errorList / errorDistanceList land here and are

@@ -144,6 +144,12 @@ class Comm:
     def handle(self):
         return self._h
 
+    def count(self) -> int:
+        """Ranks as the transport reports them (``ncclCommCount`` for RCCL)."""
+        n = lib().mmba_comm_count(self._h)
+        check(min(n, 0))
+        return n
+
     def debug_allreduce(self, ctx: "Context", values, op: str = "sum") -> np.ndarray:
         """The plan's in-place all-reduce on a copy of ``values`` (test hook,
         ``mmba_debug_comm_allreduce``); collective over the communicator."""

@@ -235,3 +235,59 @@ def test_group_refusals():
             s.close()
     finally:
         ctx.close()
+
+
+def _group_solver(prob, opt, n):
+    ctx = Context.multi([0] * n)
+    return ctx, Solver(prob, opt, context=ctx)
+
+
+def test_group_shard_failure_releases_peers(paths):
+    """a shard failing with an ordinary error (Invalid) in the
+    middle of a solve, while its peer waits in a collective, releases the
+    peer: the call returns the failing shard's code in bounded time and the
+    group is unusable afterwards (MMBA_ERR_COMM), never a hang."""
+    import time
+    prob = S.make_config(1, frames=24, scale=0.05)
+    opt = S.config_options(prob)
+    ctx, s = _group_solver(prob, opt, 2)
+    try:
+        assert s.num_shards == 2
+        paths(abi.PATH_FAULT_SHARD, 2)  # rank 1 fails at its first damped solve
+        t0 = time.perf_counter()
+        with pytest.raises(MmbaError) as e:
+            s.solve()
+        assert e.value.code == abi.MMBA_ERR_INVALID
+        assert "injected shard fault" in str(e.value)
+        assert time.perf_counter() - t0 < 30.0
+        paths(abi.PATH_FAULT_SHARD, -1)
+        with pytest.raises(MmbaError) as e:
+            s.solve()
+        assert e.value.code == abi.MMBA_ERR_COMM
+    finally:
+        s.close()
+        ctx.close()
+
+
+def test_group_stalled_shard_times_out(paths):
+    """a shard that never reaches a collective costs its
+    peers MMBA_ERR_COMM after the collective timeout (here 1.5 s), not a
+    hang; the whole call returns once the stalled shard wakes (2 x timeout)."""
+    import time
+    prob = S.make_config(1, frames=24, scale=0.05)
+    opt = S.config_options(prob)
+    ctx, s = _group_solver(prob, opt, 2)
+    try:
+        assert s.num_shards == 2
+        paths(abi.PATH_COMM_TIMEOUT_MS, 1500)
+        paths(abi.PATH_STALL_SHARD, 2)
+        t0 = time.perf_counter()
+        with pytest.raises(MmbaError) as e:
+            s.solve()
+        dt = time.perf_counter() - t0
+        assert e.value.code == abi.MMBA_ERR_COMM
+        assert "timed out" in str(e.value) or "aborted" in str(e.value)
+        assert 1.4 <= dt < 20.0
+    finally:
+        s.close()
+        ctx.close()

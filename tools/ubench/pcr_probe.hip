@@ -7,11 +7,13 @@
 //     pcr_probe.hip -o pcr_probe
 #include "mmba_pcr.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
 namespace mmba {
 void set_error(const std::string &) {}  // (the library's; unused here)
+int path_choice(int) { return -1; }       // (the library's; defaults here)
 }  // namespace mmba
 
 using namespace mmba;
@@ -54,16 +56,17 @@ int main(int argc, char **argv) {
     hipMalloc(&fail, 4);
     hipMemset(fail, 0, 4);
     long long *probe;
-    hipMalloc(&probe, 8 * 64 * 8);
+    const size_t probe_n = (size_t)64 * P.nblk;
+    hipMalloc(&probe, probe_n * 8);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     const int reps = 20;
     float best = 1e30f, sum = 0.f;
     for (int it = 0; it < reps; ++it) {
-        hipMemset(probe, 0, 8 * 64 * 8);
+        hipMemset(probe, 0, probe_n * 8);
         hipEventRecord(a);
-        k_pcr_solve<24><<<P.nblk, 256>>>(P, r, x, nullptr, 1000u + it, fail, probe);
+        k_pcr_solve<24><<<pcr_grid(P.nblk), PCR_NTH>>>(P, r, x, nullptr, 1000u + it, fail, probe);
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms = 0.f;
@@ -92,8 +95,9 @@ int main(int argc, char **argv) {
     }
     std::printf("nb %d nblk %d levels %d: k_pcr_solve<24> best %.1f us, mean %.1f us (fail %d)\n",
                 nb, P.nblk, L, best * 1e3, sum / (reps - 2) * 1e3, hf);
-    std::vector<long long> t(8 * 64);
-    hipMemcpy(t.data(), probe, t.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<long long> tall(probe_n);
+    hipMemcpy(tall.data(), probe, probe_n * 8, hipMemcpyDeviceToHost);
+    const long long *t = tall.data() + (size_t)64 * (P.nblk / 2);
     const long long t00 = t[0];
     std::printf("block %d, us from its level-0 start (chain | products | publish+log+wait | update):\n",
                 P.nblk / 2);
@@ -102,7 +106,50 @@ int main(int argc, char **argv) {
         if (!q[0]) break;
         std::printf("  level %d start %6.2f:", l, (q[0] - t00) / 100.);
         for (int ph = 1; ph <= 4 && q[ph]; ++ph) std::printf(" %5.2f", (q[ph] - q[ph - 1]) / 100.);
+        if (q[5] && q[6])  // inside the chain phase (wave 0): load | chain | stores + barrier
+            std::printf("   [load %4.2f chain %4.2f rest %4.2f]", (q[5] - q[0]) / 100.,
+                        (q[6] - q[5]) / 100., q[1] ? (q[1] - q[6]) / 100. : 0.);
+        if (q[7] && q[4])  // thread 0's granules all in -> update done
+            std::printf(" [arrived->ready %4.2f]", (q[4] - q[7]) / 100.);
         std::printf("\n");
+    }
+    // every block: level-start skew and the hand-off -- per level, the
+    // spread of level starts, and per coupled block the time from the LATER
+    // neighbour's publication (phase 2 end) to this block's update end
+    long long g0 = tall[0];
+    for (int j = 0; j < P.nblk; ++j)
+        if (tall[(size_t)64 * j] && tall[(size_t)64 * j] < g0) g0 = tall[(size_t)64 * j];
+    std::printf("all blocks (us from the first block's start): level | start min med max | "
+                "later neighbour's publish -> thread 0's granules in min med max | own publish -> later neighbour's publish med max\n");
+    for (int l = 0; l < L; ++l) {
+        std::vector<double> st, ho, lag;
+        const int s = 1 << l;
+        for (int j = 0; j < P.nblk; ++j) {
+            const long long *q = &tall[(size_t)64 * j + l * 8];
+            if (!q[0]) continue;
+            st.push_back((q[0] - g0) / 100.);
+            long long late = 0;
+            for (int nb = -1; nb <= 1; nb += 2) {
+                const int k = j + nb * s;
+                if (k < 0 || k >= P.nblk) continue;
+                const long long pk = tall[(size_t)64 * k + l * 8 + 2];
+                if (pk > late) late = pk;
+            }
+            if (late && q[4]) {
+                ho.push_back((q[7] ? q[7] - late : q[4] - late) / 100.);
+                if (q[2]) lag.push_back((late - q[2]) / 100.);
+            }
+        }
+        auto mmm = [](std::vector<double> v, double &a, double &m, double &b) {
+            if (v.empty()) { a = m = b = 0; return; }
+            std::sort(v.begin(), v.end());
+            a = v.front(); m = v[v.size() / 2]; b = v.back();
+        };
+        double a, m, b, c, d, e, f, g, h;
+        mmm(st, a, m, b);
+        mmm(ho, c, d, e);
+        mmm(lag, f, g, h);
+        std::printf("  %d | %6.2f %6.2f %6.2f | %5.2f %5.2f %5.2f | %5.2f %5.2f\n", l, a, m, b, c, d, e, g, h);
     }
     // the right-hand-side pass
     float rbest = 1e30f;
