@@ -674,11 +674,12 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       for twice the collective timeout before its first damped
                                       solve (a test hook for a shard that never reaches a
                                       collective) */
-#define MMBA_PATH_PCR_CHAIN 16    /* 1: parallel cyclic reduction factors its blocks with the
-                                      2 x 2-pivot chain without square roots (16 % faster
-                                      chain, but 4.5e-6 off the oracle's one-step ||f|| on the
-                                      160-frame C4-spec scene where the default one-pivot
-                                      Cholesky chain is 1.8e-8 off: measured, opt-in only) */
+#define MMBA_PATH_PCR_CHAIN 16    /* pivot chain of parallel cyclic reduction's block
+                                      factorisations: 0 one-pivot Cholesky (default); 1 the
+                                      2 x 2-pivot chain without square roots (16 % faster,
+                                      but 4.5e-6 off the oracle's one-step ||f|| on the
+                                      160-frame C4-spec scene where Cholesky is 1.8e-8 off);
+                                      2 LDL^T with 1 x 1 pivots */
 #define MMBA_PATH_NUM 17
 int mmba_debug_set_path(int key, int value);
 

@@ -111,7 +111,7 @@ __host__ __device__ constexpr int pcr_log_size() {
 // The damped solve.  blockIdx.x = block j.  r_in / x_out: reduced-order
 // vectors (nb rows); x is also scattered to parameter order (xs[row_param]).
 // ---------------------------------------------------------------------------
-template <int K, bool L2 = false, int NTH = PCR_NTH>
+template <int K, int CH = 0, int NTH = PCR_NTH>
 __global__ void __launch_bounds__(NTH) k_pcr_solve(PcrDev P, const double *__restrict__ r_in,
                                                    double *__restrict__ x_out, double *xs,
                                                    unsigned epoch, int *fail,
@@ -209,8 +209,10 @@ __global__ void __launch_bounds__(NTH) k_pcr_solve(PcrDev P, const double *__res
 #pragma unroll
             for (int c = 0; c < K; ++c) a[c] = src[c * st];
             stamp(lvl, 5);
-            if constexpr (L2)
+            if constexpr (CH == 1)
                 bcr_ldl2_aug_blk<K, PCR_PW, 2>(a, pl[wv], bad);
+            else if constexpr (CH == 2)
+                bcr_ldl1_aug_blk<K, PCR_PW>(a, pl[wv], bad);
             else
                 bcr_chol_aug_blk<K, MMBA_BCR_PW>(a, nullptr, pl[wv], bad);
             stamp(lvl, 6);
@@ -678,6 +680,14 @@ static void pcr_ordered(hipStream_t s, Launch &&launch) {
     o.recorded = true;
 }
 
+// The pivot chain of k_pcr_solve's block factorisations (MMBA_PATH_PCR_CHAIN):
+// 0 the one-pivot Cholesky chain (default), 1 the 2 x 2-pivot chain, 2 LDL^T
+// with 1 x 1 pivots (no square root on the chain).
+static int pcr_chain_choice() {
+    const int v = path_choice(MMBA_PATH_PCR_CHAIN);
+    return (v == 1 || v == 2) ? v : 0;
+}
+
 // k_pcr_solve's grid: 8 workgroups per block-row of the XCD map
 int pcr_grid(int nblk) { return 8 * ((nblk + 7) / 8); }
 
@@ -687,7 +697,7 @@ void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, doubl
     // faster (2.32 against 2.75 us per factorisation, tools/ubench/chain2.hip)
     // but measured less accurate on an ill-conditioned C4-spec step
     // (tools/pcr_chain_diag.py, profiles/r6_pcr/pcr_chain_diag.txt): opt-in
-    const bool l2 = path_choice(MMBA_PATH_PCR_CHAIN) > 0;
+    const int ch = pcr_chain_choice();
     const bool wide = P.nth == 512;
     pcr_ordered(s, [&] {
         const unsigned ep = pcr_next_epoch();
@@ -698,10 +708,12 @@ void pcr_solve(hipStream_t s, const PcrDev &P, const double *r, double *x, doubl
         case 16: MMBA_PCR_GO(16, L2V, NT); break;    \
         default: MMBA_PCR_GO(24, L2V, NT); break;    \
     }
-        if (l2) {
-            if (wide) { MMBA_PCR_K(true, 512) } else { MMBA_PCR_K(true, 256) }
+        if (ch == 1) {
+            if (wide) { MMBA_PCR_K(1, 512) } else { MMBA_PCR_K(1, 256) }
+        } else if (ch == 2) {
+            if (wide) { MMBA_PCR_K(2, 512) } else { MMBA_PCR_K(2, 256) }
         } else {
-            if (wide) { MMBA_PCR_K(false, 512) } else { MMBA_PCR_K(false, 256) }
+            if (wide) { MMBA_PCR_K(0, 512) } else { MMBA_PCR_K(0, 256) }
         }
 #undef MMBA_PCR_K
 #undef MMBA_PCR_GO
@@ -743,9 +755,9 @@ int pcr_resident_wide(int K) {
         return 0;
     hipError_t e;
     switch (K) {
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8, false, 512>, 512, 0); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16, false, 512>, 512, 0); break;
-        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24, false, 512>, 512, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8, 0, 512>, 512, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16, 0, 512>, 512, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24, 0, 512>, 512, 0); break;
     }
     if (e != hipSuccess) return 0;
     return per_cu * cus;
@@ -761,9 +773,9 @@ int pcr_max_resident(int K) {
         return 0;
     hipError_t e;
     switch (K) {
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8, false, 256>, 256, 0); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16, false, 256>, 256, 0); break;
-        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24, false, 256>, 256, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<8, 0, 256>, 256, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<16, 0, 256>, 256, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcr_solve<24, 0, 256>, 256, 0); break;
     }
     if (e != hipSuccess) return 0;
     return per_cu * cus;

@@ -21,6 +21,7 @@ for n in (4, 8):
     opt = S.config_options(prob, iterations=2)
     xo, tro = fx["x_%d" % n], fx["trace_%d" % n]
     for name, paths in (("chol", {abi.PATH_PCR_CHAIN: 0}), ("ldl2", {abi.PATH_PCR_CHAIN: 1}),
+                        ("ldl1", {abi.PATH_PCR_CHAIN: 2}),
                         ("bcr", {abi.PATH_PCR: 0})):
         for k in range(1, abi.PATH_NUM):
             set_path(k, -1)
