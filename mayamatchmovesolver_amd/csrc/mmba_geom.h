@@ -654,8 +654,14 @@ MMBA_DEV void fixed_point_inverse(EVAL f, double qx, double qy, double &px, doub
     }
 }
 
+// LT >= 0: the caller knows every lens it passes is of model LT (the plan's
+// lens_uniform), so only that model's code is compiled in -- the generic
+// form holds every model's inverse and their registers at once (C5's
+// k_jacobian spilled 288 B per lane with it, round 6).
+template <int LT = -1>
 MMBA_DEV void lens_distort(int type, const double *coeff, double x, double y, double &ox,
                            double &oy) {
+    if constexpr (LT >= 0) type = LT;
     const double w = 3.6, h = 2.4;  // LensModel defaults (lens_model.h:42)
     const double r = sqrt(w * w + h * h) / 2.0;
     double ux = x + 0.5, uy = y + 0.5;
@@ -728,6 +734,7 @@ MMBA_DEV void project_point(const double *rec, const double *bp, double &point_x
 // lens's constant input layers, deepest first (mmba.h ABI 5), applied before
 // the lens itself with no check between layers (each model's
 // applyModelDistort runs its input's first, lens_model_3de_classic.cpp:82-88).
+template <int LT = -1>
 MMBA_DEV void distort_point(int lens_type, const double *lens, double &point_x,
                             double &point_y, const double *chain = nullptr, int nchain = 0) {
     if (lens_type != MMBA_LENS_NONE) {
@@ -736,13 +743,14 @@ MMBA_DEV void distort_point(int lens_type, const double *lens, double &point_x,
             const double *ly = chain + (size_t)k * LENS_LAYER;
             lens_distort((int)ly[0], ly + 1, ix, iy, ix, iy);
         }
-        lens_distort(lens_type, lens, ix, iy, ox, oy);
+        lens_distort<LT>(lens_type, lens, ix, iy, ox, oy);
         if (isfinite(ox)) point_x = ox;
         if (isfinite(oy)) point_y = oy;
     }
 }
 
 // One observation's residual from a camera record and a bundle position.
+template <int LT = -1>
 MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, double mkr_y,
                         double sqrtw, int mode, double image_width, int lens_type,
                         const double *lens, const double *chain = nullptr, int nchain = 0) {
@@ -757,7 +765,7 @@ MMBA_DEV Resid residual(const double *rec, const double *bp, double mkr_x, doubl
         double dot = rec[15] * (bd0 / bl) + rec[16] * (bd1 / bl) + rec[17] * (bd2 / bl);
         if (dot < 0.0) factor = 1e+6;
     }
-    distort_point(lens_type, lens, point_x, point_y, chain, nchain);
+    distort_point<LT>(lens_type, lens, point_x, point_y, chain, nchain);
     double dx = fabs(mkr_x - point_x), dy = fabs(mkr_y - point_y);
     double dxp = dx * image_width, dyp = dy * image_width;
     Resid r;
@@ -817,10 +825,11 @@ MMBA_DEV double robust_loss(double f, int type, double scale) {
 
 // residual() with the robust loss applied to the weighted rows when the
 // solver applies one (fvec only: errorList / errorDistanceList are unscaled).
+template <int LT = -1>
 MMBA_DEV Resid residual_l(const DevProblem &P, const double *rec, const double *bp, double mkr_x,
                           double mkr_y, double sqrtw, int lens_type, const double *lens) {
-    Resid r = residual(rec, bp, mkr_x, mkr_y, sqrtw, P.mode, P.image_width, lens_type, lens,
-                       P.lens_chain, P.lens_chain_n);
+    Resid r = residual<LT>(rec, bp, mkr_x, mkr_y, sqrtw, P.mode, P.image_width, lens_type, lens,
+                           P.lens_chain, P.lens_chain_n);
     if (P.loss_on) {
         r.ex = robust_loss(r.ex, P.loss_type, P.loss_scale);
         r.ey = robust_loss(r.ey, P.loss_type, P.loss_scale);

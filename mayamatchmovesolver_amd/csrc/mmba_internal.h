@@ -284,6 +284,9 @@ struct DevProblem {
     // each: type, 14 slot values), constant for the solve (mmba.h ABI 5)
     const double *lens_chain;
     int lens_chain_n;
+    // the one lens model every lens instance of the plan uses (no input
+    // layers), -1 when mixed or chained: k_jacobian compiles that model only
+    int lens_uniform;
     const int *bnd_tfm;
     // observations (device order)
     const int *obs_cf, *obs_bnd, *obs_frame, *obs_cam;

@@ -689,7 +689,7 @@ __global__ void __launch_bounds__(256) k_residual_jp_cf(
 // forward-difference build drops the deltaB evaluations and is held to two
 // waves per SIMD (256 VGPRs, some spilled; one wave at 340 registers before):
 // C5 1.21 against 1.33 ms per solve (profiles/r5_jac/).
-template <bool CEN>
+template <bool CEN, int LT = -1>
 __global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, const double *__restrict__ recs,
                                                   const double *__restrict__ ext_pert,
                                                   const double *__restrict__ step,
@@ -714,7 +714,7 @@ __global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, con
     const int voff = P.cf_var_off[cf];
     const int nvar = P.cf_var_off[cf + 1] - voff;
     const double *rec0 = &recs[(size_t)voff * CAMREC];
-    const Resid r0 = residual_l(P, rec0, bp0, mx, my, sw, hl, lc0);
+    const Resid r0 = residual_l<LT>(P, rec0, bp0, mx, my, sw, hl, lc0);
     const bool lmder = solver_type == MMBA_SOLVER_CMINPACK_LMDER;
     const int pstale = stale_param[fr];
     Resid rs = r0;
@@ -763,20 +763,20 @@ __global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, con
                     holds |= P.inst_lpar[q] == p;
             double lc[MMBA_LENS_NUM_ATTRS];
             if (holds) inst_coeffs(P, inst, Override{P.p_attr[p], ext_pert[p]}, lc);
-            emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, holds ? lc : lc0), step[p], [&]() {
+            emit_s(p, residual_l<LT>(P, rec0, bp0, mx, my, sw, hl, holds ? lc : lc0), step[p], [&]() {
                 double lq[MMBA_LENS_NUM_ATTRS];
                 if (holds) inst_coeffs(P, inst, Override{P.p_attr[p], CB.ext_pert[p]}, lq);
-                return residual_l(P, rec0, bp0, mx, my, sw, hl, holds ? lq : lc0);
+                return residual_l<LT>(P, rec0, bp0, mx, my, sw, hl, holds ? lq : lc0);
             });
             continue;
         }
         double bp[3] = {bp0[0], bp0[1], bp0[2]};
         if (bside) bundle_position(P, b, fr, Override{P.p_attr[p], ext_pert[p]}, bp);
-        emit_s(p, residual_l(P, &recs[(size_t)t * CAMREC], bp, mx, my, sw, hl, lc0), step[p],
+        emit_s(p, residual_l<LT>(P, &recs[(size_t)t * CAMREC], bp, mx, my, sw, hl, lc0), step[p],
                [&]() {
                    double bq[3] = {bp0[0], bp0[1], bp0[2]};
                    if (bside) bundle_position(P, b, fr, Override{P.p_attr[p], CB.ext_pert[p]}, bq);
-                   return residual_l(P, &CB.recs[(size_t)t * CAMREC], bq, mx, my, sw, hl, lc0);
+                   return residual_l<LT>(P, &CB.recs[(size_t)t * CAMREC], bq, mx, my, sw, hl, lc0);
                });
     }
     if (CEN && CB.q15) {
@@ -818,10 +818,10 @@ __global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, con
         for (int a = 0; a < p4.w && l < LMAX; ++a) {
             const int p = a == 0 ? p4.x : (a == 1 ? p4.y : p4.z);
             const double bp[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
-            emit_s(p, residual_l(P, rec0, bp, mx, my, sw, hl, lc0), br[12 + a], [&]() {
+            emit_s(p, residual_l<LT>(P, rec0, bp, mx, my, sw, hl, lc0), br[12 + a], [&]() {
                 const double *bb = &CB.brec[(size_t)b * BREC];
                 const double bq[3] = {bb[3 + 3 * a], bb[4 + 3 * a], bb[5 + 3 * a]};
-                return residual_l(P, rec0, bq, mx, my, sw, hl, lc0);
+                return residual_l<LT>(P, rec0, bq, mx, my, sw, hl, lc0);
             });
             jb[2 * a] = ljx;
             jb[2 * a + 1] = ljy;
@@ -846,10 +846,10 @@ __global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, con
         }
         double bp[3];
         bundle_position(P, b, fr, Override{P.p_attr[p], ext_pert[p]}, bp);
-        emit_s(p, residual_l(P, rec0, bp, mx, my, sw, hl, lc0), step[p], [&]() {
+        emit_s(p, residual_l<LT>(P, rec0, bp, mx, my, sw, hl, lc0), step[p], [&]() {
             double bq[3];
             bundle_position(P, b, fr, Override{P.p_attr[p], CB.ext_pert[p]}, bq);
-            return residual_l(P, rec0, bq, mx, my, sw, hl, lc0);
+            return residual_l<LT>(P, rec0, bq, mx, my, sw, hl, lc0);
         });
     }
     // the lens parameters this observation's lens instance holds (an
@@ -865,10 +865,10 @@ __global__ void __launch_bounds__(128, CEN ? 1 : 2) k_jacobian(DevProblem P, con
             if (P.p_class[p] == PC_CF) continue;  // a camera-frame block column (VF_LENS)
             double lc[MMBA_LENS_NUM_ATTRS];
             inst_coeffs(P, inst, Override{P.p_attr[p], ext_pert[p]}, lc);
-            emit_s(p, residual_l(P, rec0, bp0, mx, my, sw, hl, lc), step[p], [&]() {
+            emit_s(p, residual_l<LT>(P, rec0, bp0, mx, my, sw, hl, lc), step[p], [&]() {
                 double lq[MMBA_LENS_NUM_ATTRS];
                 inst_coeffs(P, inst, Override{P.p_attr[p], CB.ext_pert[p]}, lq);
-                return residual_l(P, rec0, bp0, mx, my, sw, hl, lq);
+                return residual_l<LT>(P, rec0, bp0, mx, my, sw, hl, lq);
             });
         }
     }
@@ -3632,6 +3632,9 @@ void launch_jacobian(hipStream_t s, const DevProblem &P, const double *recs,
     if (CB.recs)
         k_jacobian<true><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J,
                                                       jcol, nloc, stale_param, eu, ed, CB);
+    else if (P.lens_uniform == MMBA_LENS_3DE_CLASSIC)  // C5: the classic model only
+        k_jacobian<false, MMBA_LENS_3DE_CLASSIC><<<nblk(P.M, 128), 128, 0, s>>>(
+            P, recs, ext_pert, step, solver_type, J, jcol, nloc, stale_param, eu, ed, CB);
     else
         k_jacobian<false><<<nblk(P.M, 128), 128, 0, s>>>(P, recs, ext_pert, step, solver_type, J,
                                                        jcol, nloc, stale_param, eu, ed, CB);

@@ -1215,6 +1215,15 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     D.lens_type = upload(pr->lens_type, nL);
     D.lens_chain = lens_chain_h.empty() ? nullptr : upload(lens_chain_h);
     D.lens_chain_n = (int)(lens_chain_h.size() / LENS_LAYER);
+    {
+        // the one lens model every instance uses (k_jacobian's fixed-model form)
+        int lt = -2;
+        for (int l : inst_lens_h) {
+            const int t = pr->lens_type[l];
+            lt = (lt == -2 || lt == t) ? t : -1;
+        }
+        D.lens_uniform = (D.lens_chain_n == 0 && lt >= 0) ? lt : -1;
+    }
     D.bnd_tfm = upload(pr->bnd_tfm, nB);
     D.obs_cf = upload(d_cf);
     D.obs_bnd = upload(d_bnd);
