@@ -134,6 +134,16 @@ def allreduce(dist, v, op="max"):
     return float(t.item())
 
 
+def allgather_float(dist, v):
+    """Every rank's v, in rank order (one value per rank)."""
+    if dist is None:
+        return [v]
+    import torch
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, torch.tensor([v], dtype=torch.float64))
+    return [float(t.item()) for t in out]
+
+
 def broadcast_bytes(dist, data: bytes | None, n: int) -> bytes:
     import torch
     t = torch.zeros(n, dtype=torch.uint8)
@@ -454,9 +464,13 @@ def main():
     else:
         ctx = Context(devices[0])
     comm = None
+    rccl_ranks = None
     if world > 1:
         uid = broadcast_bytes(dist, comm_unique_id() if rank == 0 else None, 128)
         comm = Comm.rccl(ctx, rank, world, uid)
+        rccl_ranks = comm.count()  # ncclCommCount: the ranks RCCL itself reports
+        progress("rank %d: RCCL communicator up, ncclCommCount = %d" % (rank, rccl_ranks),
+                 every=0.0)
     t0 = time.perf_counter()
     solver = Solver(prob, opt, context=ctx, comm=comm)
     upload_s = time.perf_counter() - t0
@@ -494,6 +508,7 @@ def main():
     barrier(dist)
     dt = time.perf_counter() - t0
     dt_max = allreduce(dist, dt, "max")
+    dt_ranks = allgather_float(dist, dt)  # per-shard times (the max is the value's clock)
     # device-resident rate (reported beside value, never as value): the same
     # solves leaving the per-residual outputs in HBM (mmba_plan_solve with
     # NULL output pointers; mmba_plan_outputs fetches them on demand)
@@ -619,6 +634,9 @@ def main():
                        "solver": "lmder fwd-FD delta=1e-4 tau=1 tol=1e-6",
                        **({"pinned_paths": pinned} if pinned else {})},
             "lm_iterations_per_s": lm_rate,
+            **({"shards": {"rccl_ranks": rccl_ranks, "num_shards": solver.num_shards,
+                           "per_rank_ms_per_step": [1e3 * t / args.steps for t in dt_ranks]}}
+               if nshards > 1 else {}),
             "final_rms_px": r["error_rms"],
             "d2h_bytes_per_step": 8.0 * (2 * prob.num_residuals + prob.num_obs),
             "device_resident": {

@@ -680,7 +680,9 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       but 4.5e-6 off the oracle's one-step ||f|| on the
                                       160-frame C4-spec scene where Cholesky is 1.8e-8 off);
                                       2 LDL^T with 1 x 1 pivots */
-#define MMBA_PATH_NUM 17
+#define MMBA_PATH_BACKSUB_ONEPASS 17 /* 1: the trial back substitution forms u_i = W_i^T x
+                                         itself (no k_obs_wtx launch; same sums) */
+#define MMBA_PATH_NUM 18
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -296,9 +296,9 @@ int trial_prep_rec_parts(const DevProblem &P, int nother);
 void launch_trial_prep_rec(hipStream_t s, const DevProblem &P, const double *xs, const TrialFold &T);
 void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,
                     double *U);
-void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,
-                          const double *Lb, const double *xR, const double *U, double *x,
-                          const TrialFold &T);
+void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                          const double *tb, const double *Lb, const double *xR, const double *U,
+                          double *x, const TrialFold &T);
 void launch_scatter_xR(hipStream_t s, const DevProblem &P, const double *xR, double *x);
 void launch_newton_bundle(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
                           const double *Lb, const double *v, double *wR, double *usq,

@@ -2901,6 +2901,7 @@ __device__ __forceinline__ void trial_one(const DevProblem &P, const TrialFold &
 // prepare the other parameters from xs (the reduced solve's scatter).
 // Sharded plans count only their own parameters in the sums (TrialFold::own).
 __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double *__restrict__ U,
+                                                      const double *__restrict__ W,
                                                       const double *__restrict__ Wg,
                                                       const double *__restrict__ tb,
                                                       const double *__restrict__ Lb,
@@ -2916,10 +2917,27 @@ __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double
             const int nCF = P.nR - nG;
             double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
             for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-                const double4 uu = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
-                s[0] -= uu.x;
-                s[1] -= uu.y;
-                s[2] -= uu.z;
+                double u[3];
+                if (W) {  // one pass (MMBA_PATH_BACKSUB_ONEPASS): k_obs_wtx's arithmetic here
+                    const int i = P.bobs[q];
+                    const int cf = P.obs_cf[i];
+                    const int pc = min(P.cf_pc[cf], P.wst / 3);
+                    const int r0 = P.cf_roff[cf];
+                    const double *row = &W[widx(P, 0, i)];
+                    u[0] = u[1] = u[2] = 0.;
+                    for (int a = 0; a < pc; ++a) {
+                        const double xv = xR[r0 + a];
+                        for (int c = 0; c < 3; ++c) u[c] += row[a * 3 + c] * xv;
+                    }
+                } else {
+                    const double4 uu = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
+                    u[0] = uu.x;
+                    u[1] = uu.y;
+                    u[2] = uu.z;
+                }
+                s[0] -= u[0];
+                s[1] -= u[1];
+                s[2] -= u[2];
             }
             for (int q = 0; q < nG; ++q) {
                 const double xv = xR[nCF + q];
@@ -3372,12 +3390,12 @@ int trial_fold_parts(const DevProblem &P, int nother, bool rec) {
     return nblk(P.nB, 64) + (rec ? (P.ncf + 3) / 4 : nblk(nother, 64));
 }
 
-void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *Wg, const double *tb,
-                          const double *Lb, const double *xR, const double *U, double *x,
-                          const TrialFold &T) {
+void launch_backsub_trial(hipStream_t s, const DevProblem &P, const double *W, const double *Wg,
+                          const double *tb, const double *Lb, const double *xR, const double *U,
+                          double *x, const TrialFold &T) {
     const int nbb = nblk(P.nB, 64);
     const int g = trial_fold_parts(P, T.nother, T.rec != 0);
-    if (g > 0) k_backsub_trial<<<g, 64, 0, s>>>(P, U, Wg, tb, Lb, xR, x, nbb, T);
+    if (g > 0) k_backsub_trial<<<g, 64, 0, s>>>(P, U, W, Wg, tb, Lb, xR, x, nbb, T);
 }
 
 void launch_obs_wtx(hipStream_t s, const DevProblem &P, const double *W, const double *xR,

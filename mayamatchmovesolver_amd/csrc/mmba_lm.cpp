@@ -764,7 +764,10 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         if (trial_fold_ok) {
             // the trial point's parameter pass rides in the back substitution
             // (the last damped solve before a trial is the one it keeps)
-            launch_obs_wtx(s, PS, d_W, d_xR, d_U);
+            // one pass (MMBA_PATH_BACKSUB_ONEPASS = 1): the bundle threads form
+            // u_i = W_i^T x_cf(i) themselves (the same sums), no k_obs_wtx
+            const bool onepass = path_choice(MMBA_PATH_BACKSUB_ONEPASS) == 1;
+            if (!onepass) launch_obs_wtx(s, PS, d_W, d_xR, d_U);
             TrialFold T;
             T.x = d_x;
             T.diag = d_diag;
@@ -785,7 +788,7 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             T.rec = trial_rec ? 1 : 0;
             T.recs = d_recs;
             T.brec = d_brec;
-            launch_backsub_trial(s, PS, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
+            launch_backsub_trial(s, PS, onepass ? d_W : nullptr, d_Wg, d_tb, d_Lb, d_xR, d_U, d_xs, T);
             trial_folded = true;
             params_at = nullptr;  // the attribute block now holds the trial point
             recs_full_at = nullptr;
