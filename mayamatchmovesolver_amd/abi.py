@@ -42,7 +42,8 @@ PATH_COMM_TIMEOUT_MS = 14
 PATH_STALL_SHARD = 15
 PATH_PCR_CHAIN = 16
 PATH_BACKSUB_ONEPASS = 17
-PATH_NUM = 18
+PATH_JB_RECOMPUTE = 18
+PATH_NUM = 19
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1

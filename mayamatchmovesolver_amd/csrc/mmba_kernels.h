@@ -178,6 +178,13 @@ struct NeEpi {
     RedSpec spec{};
     double *scalar = nullptr;
     unsigned *ticket = nullptr;
+    // jb_recs != nullptr (MMBA_PATH_JB_RECOMPUTE, the fused path only): the
+    // bundle pass re-evaluates each observation's three bundle columns and f
+    // from the base camera record (jb_recs) and the bundle record -- the
+    // arithmetic of jac_obs_u, so the same bits -- instead of reading the
+    // 64-B JB record k_jac_ne_u would have written
+    const double *jb_recs = nullptr;
+    int jb_lmder = 1;
     // Lb != nullptr: the bundle pass also factors Abb at lam = 0
     // (k_bundle_factor's arithmetic) for the undamped solve that follows
     double *Lb = nullptr, *tb = nullptr;

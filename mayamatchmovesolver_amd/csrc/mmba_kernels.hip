@@ -1465,14 +1465,42 @@ __global__ void __launch_bounds__(NE_BND_TPB) k_ne_bnd_jb(DevProblem P, double *
         double A[PBMAX][PBMAX] = {};
         double gb[PBMAX] = {};
         const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
+        const double *__restrict__ br = &P.brec[(size_t)b * BREC];
         for (int qb = q0; qb < q1; qb += 4) {
             double4 u[4], v[4];
+            if (E.jb_recs) {
+                // the records' values re-evaluated: jac_obs_u's base residual
+                // and bundle columns (residual_e is residual's ex / ey)
+                const double bp0[3] = {br[0], br[1], br[2]};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                if (qb + r < q1) {
-                    const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)(qb + r) * 8]);
-                    u[r] = src[0];
-                    v[r] = src[1];
+                for (int r = 0; r < 4; ++r) {
+                    if (qb + r >= q1) break;
+                    const int i = P.bobs[qb + r];
+                    const double *__restrict__ rec0 = &E.jb_recs[(size_t)P.cf_var_off[P.obs_cf[i]] * CAMREC];
+                    const double mx = P.obs_xy[2 * i], my = P.obs_xy[2 * i + 1], sw = P.obs_sqrtw[i];
+                    const double2 f0 = residual_e(rec0, bp0, mx, my, sw, P.mode, P.image_width);
+                    double jb[6] = {0., 0., 0., 0., 0., 0.};
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        if (a < pb) {
+                            const double bq[3] = {br[3 + 3 * a], br[4 + 3 * a], br[5 + 3 * a]};
+                            const double2 rr = residual_e(rec0, bq, mx, my, sw, P.mode, P.image_width);
+                            const double st = br[12 + a];
+                            jb[2 * a] = E.jb_lmder ? (rr.x - f0.x) * st : (rr.x - f0.x) / st;
+                            jb[2 * a + 1] = E.jb_lmder ? (rr.y - f0.y) * st : (rr.y - f0.y) / st;
+                        }
+                    }
+                    u[r] = make_double4(jb[0], jb[1], jb[2], jb[3]);
+                    v[r] = make_double4(jb[4], jb[5], f0.x, f0.y);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (qb + r < q1) {
+                        const double4 *src = reinterpret_cast<const double4 *>(&P.JB[(size_t)(qb + r) * 8]);
+                        u[r] = src[0];
+                        v[r] = src[1];
+                    }
                 }
             }
 #pragma unroll

@@ -293,11 +293,28 @@ void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
     epi.bnd_base = ncf;
     epi.gate = d_gate;
     epi.probe = d_k2probe;
-    launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, nloc_set ? nullptr : d_nloc,
-                  d_stale, eu, ed, d_Acc, d_g, epi);
+    launch_jac_ne(s, jb_recompute() ? P_nojb() : P, d_recs, d_step, opt.solver_type, d_J, d_jcol,
+                  nloc_set ? nullptr : d_nloc, d_stale, eu, ed, d_Acc, d_g, epi);
     nloc_set = true;
     pre_jac_pending = true;
     pre_jac_x = dx;
+}
+
+// The bundle records of the fused Jacobian pass re-evaluated by the bundle
+// pass instead of stored and re-fetched (the default since round 6; only
+// where k_jac_ne_u -- jac_obs_u's arithmetic -- is the Jacobian pass;
+// MMBA_PATH_JB_RECOMPUTE = 0 pins the record round trip).  Same bits
+// (test_k2_records_and_backsub_forms_bit_identical); C4 K2 52 against 69 us,
+// 4,761 against 4,406 LM it/s on the same box (profiles/r6_ab2/).
+bool Plan::jb_recompute() const {
+    return P.JB != nullptr && P.all_bnd_fast && path_choice(MMBA_PATH_JB_RECOMPUTE) != 0;
+}
+
+// The plan's problem without the JB records: k_jac_ne_u then stores none.
+DevProblem Plan::P_nojb() const {
+    DevProblem Q = P;
+    Q.JB = nullptr;
+    return Q;
 }
 
 // iflag = 2: FD Jacobian blocks + normal equations + column norms at x.
@@ -392,9 +409,14 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         // this trial point, as the host did)
     } else if (k2_fused) {
         // the local column counts are a property of the plan: stored once
-        launch_jac_ne(s, P, d_recs, d_step, opt.solver_type, d_J, d_jcol, nloc_set ? nullptr : d_nloc,
-                      d_stale, d_eu, d_ed, d_Acc, d_g, epi);
+        launch_jac_ne(s, jb_recompute() ? P_nojb() : P, d_recs, d_step, opt.solver_type, d_J,
+                      d_jcol, nloc_set ? nullptr : d_nloc, d_stale, d_eu, d_ed, d_Acc, d_g, epi);
         nloc_set = true;
+    }
+    if (k2_fused && jb_recompute()) {
+        // the bundle pass re-evaluates the records k_jac_ne_u did not store
+        epi.jb_recs = d_recs;
+        epi.jb_lmder = lmder ? 1 : 0;
     }
     else
         launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
@@ -765,7 +787,9 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
             // the trial point's parameter pass rides in the back substitution
             // (the last damped solve before a trial is the one it keeps)
             // one pass (MMBA_PATH_BACKSUB_ONEPASS = 1): the bundle threads form
-            // u_i = W_i^T x_cf(i) themselves (the same sums), no k_obs_wtx
+            // u_i = W_i^T x_cf(i) themselves (the same sums), no k_obs_wtx --
+            // measured slower on C4 (4,299 against 4,406 LM it/s, same box,
+            // profiles/r6_ab2/: the gathered 144-B W rows), so opt-in
             const bool onepass = path_choice(MMBA_PATH_BACKSUB_ONEPASS) == 1;
             if (!onepass) launch_obs_wtx(s, PS, d_W, d_xR, d_U);
             TrialFold T;

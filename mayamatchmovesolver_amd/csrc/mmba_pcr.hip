@@ -301,12 +301,14 @@ __global__ void __launch_bounds__(NTH) k_pcr_solve(PcrDev P, const double *__res
         stamp(lvl, 2);
         // ---- the Newton pass's log (later launches read it: plain stores;
         // issued during the granule wait instead: 66.7 against 65.0 us)
+#ifndef PCR_NOLOG
         for (int q = tid; q < K * K; q += NTH) {
             const int x = (q / K) * KS + q % K;
             log[q] = sCi[x];
             log[K * K + q] = sP[x];
             log[2 * K * K + q] = sQ[x];
         }
+#endif
         stamp(lvl, 3);
         // ---- the update from the neighbours' granules of this level: loads
         // and subtractions only

@@ -492,6 +492,8 @@ struct Plan {
     bool red_defer_ok() const;
     void flush_red();
     void host_sync();
+    bool jb_recompute() const;
+    DevProblem P_nojb() const;
     bool stall_done = false;  // MMBA_PATH_STALL_SHARD fired
     void wait_event();
     // speculative trial (lmpar's first, undamped, step taken before the

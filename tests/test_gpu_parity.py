@@ -240,3 +240,34 @@ def test_layered_lens_measure_jacobian_and_input_attr(oracle, gpu_ctx):
     _, J2 = oracle.jacobian(p2, opt, p2.x0)
     assert not np.any(J2[:, -1])
     check_solve(p2, opt, oracle, gpu_ctx)
+
+
+@pytest.mark.parametrize("solver_type", [abi.SOLVER_TYPE_CMINPACK_LMDER, abi.SOLVER_TYPE_CMINPACK_LMDIF])
+def test_k2_records_and_backsub_forms_bit_identical(solver_type, gpu_ctx, paths):
+    """Round 6 forms of the C4 iteration, pinned on and off: the bundle pass
+    re-evaluating each observation's bundle columns instead of reading the
+    records the fused Jacobian pass stores (MMBA_PATH_JB_RECOMPUTE, jac_obs_u's
+    arithmetic) and the trial back substitution forming W_i^T x itself
+    (MMBA_PATH_BACKSUB_ONEPASS, k_obs_wtx's sums) give the same bits: x, the
+    ||f|| trace and fvec identical in all four combinations.  300 frames: the
+    fused Jacobian + camera-frame pass (>= 256 camera-frames) is taken."""
+    prob = S.make_config(3, frames=300, scale=0.06)
+    # lmdif's maxfev counts the n FD evaluations of a Jacobian too
+    its = 12 if solver_type == abi.SOLVER_TYPE_CMINPACK_LMDER else 2 * prob.num_params + 6
+    opt = S.config_options(prob, solver_type=solver_type, iterations=its)
+    runs = {}
+    for jb in (0, 1):
+        for one in (0, 1):
+            paths(abi.PATH_JB_RECOMPUTE, jb)
+            paths(abi.PATH_BACKSUB_ONEPASS, one)
+            s = Solver(prob, opt, context=gpu_ctx)
+            try:
+                runs[(jb, one)] = s.solve()
+            finally:
+                s.close()
+    ref = runs[(0, 0)]
+    assert ref.result["iterations"] > 2
+    for k, r in runs.items():
+        np.testing.assert_array_equal(r.x, ref.x, err_msg=str(k))
+        np.testing.assert_array_equal(r.fnorm_trace, ref.fnorm_trace, err_msg=str(k))
+        np.testing.assert_array_equal(r.fvec, ref.fvec, err_msg=str(k))
