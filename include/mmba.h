@@ -682,9 +682,9 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       2 LDL^T with 1 x 1 pivots */
 #define MMBA_PATH_BACKSUB_ONEPASS 17 /* 1: the trial back substitution forms u_i = W_i^T x
                                          itself (no k_obs_wtx launch; same sums) */
-#define MMBA_PATH_JB_RECOMPUTE 18  /* 0: the fused Jacobian pass stores a 64-B bundle record
-                                      per observation for the bundle pass (round 5); default:
-                                      the bundle pass re-evaluates them (same bits) */
+#define MMBA_PATH_JB_RECOMPUTE 18  /* 1: the bundle pass re-evaluates each observation's bundle
+                                      columns instead of reading the 64-B records the fused
+                                      Jacobian pass stores (same bits; measured slower on C4) */
 #define MMBA_PATH_NUM 19
 int mmba_debug_set_path(int key, int value);
 

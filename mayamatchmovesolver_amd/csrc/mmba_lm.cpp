@@ -301,13 +301,15 @@ void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
 }
 
 // The bundle records of the fused Jacobian pass re-evaluated by the bundle
-// pass instead of stored and re-fetched (the default since round 6; only
-// where k_jac_ne_u -- jac_obs_u's arithmetic -- is the Jacobian pass;
-// MMBA_PATH_JB_RECOMPUTE = 0 pins the record round trip).  Same bits
-// (test_k2_records_and_backsub_forms_bit_identical); C4 K2 52 against 69 us,
-// 4,761 against 4,406 LM it/s on the same box (profiles/r6_ab2/).
+// pass instead of stored and re-fetched (MMBA_PATH_JB_RECOMPUTE = 1; only
+// where k_jac_ne_u -- jac_obs_u's arithmetic -- is the Jacobian pass).  Same
+// bits (test_k2_records_and_backsub_forms_bit_identical).  Measured on C4
+// (profiles/r6_b2/c4_iteration_trace.txt): k_jac_ne_u 31.5 -> 29.1 us (12.8
+// MB fewer stores) but k_ne_bnd_jb 12.0 -> 19.7 us (each bundle thread
+// gathers and re-projects its four observations in series) and the 5.8 us
+// gap before it unchanged -- a net loss, so opt-in.
 bool Plan::jb_recompute() const {
-    return P.JB != nullptr && P.all_bnd_fast && path_choice(MMBA_PATH_JB_RECOMPUTE) != 0;
+    return P.JB != nullptr && P.all_bnd_fast && path_choice(MMBA_PATH_JB_RECOMPUTE) == 1;
 }
 
 // The plan's problem without the JB records: k_jac_ne_u then stores none.
