@@ -414,15 +414,15 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         launch_jac_ne(s, jb_recompute() ? P_nojb() : P, d_recs, d_step, opt.solver_type, d_J,
                       d_jcol, nloc_set ? nullptr : d_nloc, d_stale, d_eu, d_ed, d_Acc, d_g, epi);
         nloc_set = true;
+    } else {
+        launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
+                        d_stale, d_eu, d_ed, jac_ncv, d_f, CB);
     }
     if (k2_fused && jb_recompute()) {
         // the bundle pass re-evaluates the records k_jac_ne_u did not store
         epi.jb_recs = d_recs;
         epi.jb_lmder = lmder ? 1 : 0;
     }
-    else
-        launch_jacobian(s, P, d_recs, d_ext_pert, d_step, opt.solver_type, d_J, d_jcol, d_nloc,
-                        d_stale, d_eu, d_ed, jac_ncv, d_f, CB);
     launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
                     central ? d_stepB : nullptr, lmder ? 1 : 0, d_Jrow, d_eu + 2 * (size_t)M,
                     n - 1);
