@@ -685,7 +685,9 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
 #define MMBA_PATH_JB_RECOMPUTE 18  /* 1: the bundle pass re-evaluates each observation's bundle
                                       columns instead of reading the 64-B records the fused
                                       Jacobian pass stores (same bits; measured slower on C4) */
-#define MMBA_PATH_NUM 19
+#define MMBA_PATH_NE_CF_SPLIT 19   /* 0: long camera-frame segments (C2) take one workgroup per
+                                      camera-frame in the normal equations instead of four */
+#define MMBA_PATH_NUM 20
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -43,7 +43,8 @@ PATH_STALL_SHARD = 15
 PATH_PCR_CHAIN = 16
 PATH_BACKSUB_ONEPASS = 17
 PATH_JB_RECOMPUTE = 18
-PATH_NUM = 19
+PATH_NE_CF_SPLIT = 19
+PATH_NUM = 20
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1

@@ -101,7 +101,23 @@ struct RcclComm : Comm {
     ncclComm_t c = nullptr;
     bool aborted = false;
     ~RcclComm() override {
-        if (c && !aborted) (void)ncclCommDestroy(c);
+        if (!c || aborted) return;
+        // non-blocking communicator: finalize (flushes issued operations,
+        // ncclInProgress until done), settled with the deadline, then free;
+        // a communicator that does not settle is aborted instead
+        const ncclResult_t r = ncclCommFinalize(c);
+        bool ok = r == ncclSuccess || r == ncclInProgress;
+        if (ok) {
+            try {
+                rccl_settle(c, "ncclCommFinalize");
+            } catch (const CommError &) {
+                ok = false;
+            }
+        }
+        if (ok)
+            (void)ncclCommDestroy(c);
+        else
+            (void)ncclCommAbort(c);
     }
     void abort() override {
         if (c && !aborted) (void)ncclCommAbort(c);

@@ -163,6 +163,8 @@ void launch_rows_ne(hipStream_t s, const DevProblem &P, const double *Jrow, cons
 // normal-equation kernels: each camera-frame / bundle block writes one
 // partial per quantity at column cf_base + cf / bnd_base + block of the rows
 // partial[0 | rstride | 2 rstride] (max, sum, max).
+constexpr int NE_CF_SPLIT = 4;  // workgroups per camera-frame of k_ne_cf_split
+constexpr int NE_CF_NT = 36;    // partial sums per workgroup (PC <= 7: 28 + 7)
 struct NeEpi {
     int on = 0;
     int first = 0, mode = 1, do_xn = 0, do_gn = 0;
@@ -185,6 +187,13 @@ struct NeEpi {
     // 64-B JB record k_jac_ne_u would have written
     const double *jb_recs = nullptr;
     int jb_lmder = 1;
+    // cf_part != nullptr (C2-like long segments, no global parameter): each
+    // camera-frame's observations are split over NE_CF_SPLIT workgroups,
+    // which store their partial sums write-through; the last of them (per
+    // camera-frame ticket, monotonic) adds them in part order and writes
+    // Acc / g and the epilogue (k_ne_cf_split)
+    double *cf_part = nullptr;
+    unsigned *cf_ticket = nullptr;
     // Lb != nullptr: the bundle pass also factors Abb at lam = 0
     // (k_bundle_factor's arithmetic) for the undamped solve that follows
     double *Lb = nullptr, *tb = nullptr;

@@ -1299,6 +1299,111 @@ __device__ __forceinline__ void ne_cf_u_body(const DevProblem &P, const double *
         epi_store(E, E.cf_base + cf, zf, xn, gm);
     }
 }
+// k_ne_cf_u for long camera-frame segments without global parameters (C2:
+// ~1,650 observations per camera-frame, 120 camera-frames -- 120 workgroups
+// left half the SIMDs idle and read J at ~1 TB/s): NS workgroups per
+// camera-frame (logical blocks cf * NS + part, consecutive on one XCD), part
+// p takes observations o0 + 64 NW p + t, o0 + 64 NW (NS + p) + t, ...; each
+// workgroup stores its NT partial sums write-through, the last to arrive
+// (per camera-frame ticket: monotonic, last when old % NS == NS - 1) loads
+// them sc1 and adds them in part order -- deterministic whichever arrives
+// last -- then writes Acc / g and the lmder epilogue as k_ne_cf_u does.
+template <int PC, int NW, int NS>
+__global__ void __launch_bounds__(64 * NW) k_ne_cf_split(DevProblem P, const double *__restrict__ J,
+                                                         const double *__restrict__ f, double *Acc,
+                                                         double *g, NeEpi E) {
+    constexpr int NCC = PC * (PC + 1) / 2, NT = NCC + PC;
+    static_assert(NT <= NE_CF_NT, "partial sums per workgroup");
+    __shared__ double wsum[NW][NT];
+    __shared__ double fin[NT];
+    __shared__ unsigned last_s;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int cf = L / NS, part = L % NS;
+    if (cf >= P.ncf) return;
+    if (!own_cf(P, cf) || P.cf_pc[cf] != PC) {
+        if (E.on && part == 0 && threadIdx.x == 0) epi_store(E, E.cf_base + cf, 0., 0., 0.);
+        return;
+    }
+    const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
+    const size_t M = P.M;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double acc[NT];
+#pragma unroll
+    for (int e = 0; e < NT; ++e) acc[e] = 0.;
+    for (int i = o0 + 64 * NW * part + tid; i < o1; i += 64 * NW * NS) {
+        double jx[PC], jy[PC];
+#pragma unroll
+        for (int a = 0; a < PC; ++a) {
+            jx[a] = J[(2 * a) * M + i];
+            jy[a] = J[(2 * a + 1) * M + i];
+        }
+        const double fx = f[2 * i], fy = f[2 * i + 1];
+        int e = 0;
+#pragma unroll
+        for (int a = 0; a < PC; ++a)
+#pragma unroll
+            for (int c = a; c < PC; ++c) acc[e++] += jx[a] * jx[c] + jy[a] * jy[c];
+#pragma unroll
+        for (int a = 0; a < PC; ++a) acc[NCC + a] += jx[a] * fx + jy[a] * fy;
+    }
+#pragma unroll
+    for (int e = 0; e < NT; ++e) {
+        double v = acc[e];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) wsum[wv][e] = v;
+    }
+    __syncthreads();
+    double *mine = E.cf_part + ((size_t)cf * NS + part) * NE_CF_NT;
+    for (int e = tid; e < NT; e += 64 * NW) {
+        double v = wsum[0][e];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v += wsum[w][e];
+        st_sc1(&mine[e], v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        last_s = (__hip_atomic_fetch_add(&E.cf_ticket[cf], 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) %
+                  NS) == NS - 1;
+    __syncthreads();
+    if (!last_s) return;
+    const double *all = E.cf_part + (size_t)cf * NS * NE_CF_NT;
+    for (int e = tid; e < NT; e += 64 * NW) {
+        double v = ld_sc1(&all[e]);
+#pragma unroll
+        for (int q = 1; q < NS; ++q) v += ld_sc1(&all[(size_t)q * NE_CF_NT + e]);
+        fin[e] = v;
+    }
+    __syncthreads();
+    double *A = &Acc[(size_t)cf * PCMAX * PCMAX];
+    for (int e = tid; e < NT; e += 64 * NW) {
+        const double v = fin[e];
+        if (e < NCC) {
+            int a = 0, rem = e;
+            while (rem >= PC - a) {
+                rem -= PC - a;
+                ++a;
+            }
+            const int c = a + rem;
+            A[a * PCMAX + c] = v;
+            A[c * PCMAX + a] = v;
+        } else {
+            g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
+        }
+    }
+    if (E.on && tid == 0) {
+        double zf = 0., xn = 0., gm = 0.;
+        const int v0 = P.cf_var_off[cf] + 1;
+        for (int a = 0; a < PC; ++a) {
+            const int ed = a * PC - a * (a - 1) / 2;  // upper-triangle index of (a, a)
+            epi_param(E, P.cf_var_param[v0 + a], fin[ed], fin[NCC + a], zf, xn, gm);
+        }
+        epi_store(E, E.cf_base + cf, zf, xn, gm);
+    }
+}
+
 template <int PC, int NW, int NG>
 __global__ void __launch_bounds__(64 * NW) k_ne_cf_u(DevProblem P, const double *__restrict__ J,
                                                      const int *__restrict__ jcol,
@@ -1457,6 +1562,10 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
 __global__ void __launch_bounds__(NE_BND_TPB) k_ne_bnd_jb(DevProblem P, double *Abb, double *g,
                                                           NeEpi E) {
     __shared__ double red[3][NE_BND_TPB];
+    // enqueued ahead of the host's decision with its Jacobian pass (round 6):
+    // runs only when the device's restatement of that decision let it
+    if (E.gate && __hip_atomic_load(E.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        return;
     const int b = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // XCD-contiguous
     const int4 p4 = b < P.nB ? P.bnd_p4[b] : make_int4(-1, -1, -1, 0);
     const int pb = p4.w;
@@ -4084,7 +4193,14 @@ void launch_ne(hipStream_t s, const DevProblem &P, const double *J, const int *j
             glob_done = true;
         } else if ((pcu == 6 || pcu == 7) && (P.nG == 0 || P.nG <= 2)) {
             if (P.nG == 0) {
-                if (pcu == 6) {
+                const bool split = wide && E.cf_part && E.cf_ticket && P.M > 1024 * P.ncf;
+                if (split) {  // long segments: NE_CF_SPLIT workgroups per camera-frame
+                    const int gs = P.ncf * NE_CF_SPLIT;
+                    if (pcu == 6)
+                        k_ne_cf_split<6, 4, NE_CF_SPLIT><<<gs, 256, 0, s>>>(P, J, f, Acc, g, E);
+                    else
+                        k_ne_cf_split<7, 4, NE_CF_SPLIT><<<gs, 256, 0, s>>>(P, J, f, Acc, g, E);
+                } else if (pcu == 6) {
                     if (wide) MMBA_NE_U(6, 4, 0); else MMBA_NE_U(6, 1, 0);
                 } else {
                     if (wide) MMBA_NE_U(7, 4, 0); else MMBA_NE_U(7, 1, 0);

@@ -297,6 +297,26 @@ void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
                   nloc_set ? nullptr : d_nloc, d_stale, eu, ed, d_Acc, d_g, epi);
     nloc_set = true;
     pre_jac_pending = true;
+    // the bundle pass right behind it, under the same gate (round 6): the
+    // GPU no longer idles between the two while the host takes its decision
+    // (the 5.8 us gap of profiles/r5_final6 / r6_k2).  jac() would launch
+    // it with this epilogue: the fused path's, at a later iteration (first
+    // = 0, gnorm from the device slot), with the lam = 0 bundle factor
+    pre_bnd_pending = false;
+    if (P.nbs > 0 && P.JB != nullptr && nG == 0) {
+        if (jb_recompute()) {
+            epi.jb_recs = d_recs;
+            epi.jb_lmder = opt.solver_type == MMBA_SOLVER_CMINPACK_LMDER ? 1 : 0;
+        }
+        if (fold_ok && nB_solved > 0) {
+            epi.Lb = d_Lb;
+            epi.tb = d_tb;
+            epi.fail = d_fail;
+        }
+        launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
+                  d_glob_partial, glob_chunk, epi, true);
+        pre_bnd_pending = true;
+    }
     pre_jac_x = dx;
 }
 
@@ -374,6 +394,12 @@ void Plan::jac(const double *dx, const JacLM *lm) {
         epi.bnd_base = ncf;
     }
     epi.probe = d_k2probe;
+    if (fuse && path_choice(MMBA_PATH_NE_CF_SPLIT) != 0) {
+        // long camera-frame segments: the camera-frame normal equations over
+        // NE_CF_SPLIT workgroups each (k_ne_cf_split; launch_ne decides)
+        epi.cf_part = d_cf_part;
+        epi.cf_ticket = d_cf_ticket;
+    }
     // unsharded plans with fast bundles: the bundle pass forms the lam = 0
     // bundle factor the undamped solve reads next (no k_bundle_factor
     // launch); with tail_reduce its last workgroup also reduces the
@@ -406,6 +432,8 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     // pass, which writes the camera-frame part of g itself
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_g, 0, sizeof(double) * n, s));
     pre_jac_pending = false;
+    const bool pre_bnd = pre_done && pre_bnd_pending;  // its bundle pass ran ahead too
+    pre_bnd_pending = false;
     if (pre_done) {
         // k_jac_ne_u ran ahead at this x (its gate was open: the device took
         // this trial point, as the host did)
@@ -426,8 +454,9 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     launch_rows_jac(s, P, d_ext, d_ext_pert, d_step, central ? d_ext_pertB : nullptr,
                     central ? d_stepB : nullptr, lmder ? 1 : 0, d_Jrow, d_eu + 2 * (size_t)M,
                     n - 1);
-    launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
-              d_glob_partial, glob_chunk, epi, k2_fused);
+    if (!pre_bnd)
+        launch_ne(s, P, d_J, d_jcol, d_nloc, d_f, d_Acc, d_Acg, d_Abb, d_Abg, d_Agg, d_g,
+                  d_glob_partial, glob_chunk, epi, k2_fused);
     launch_rows_ne(s, P, d_Jrow, d_f + 2 * (size_t)M, d_p_own, d_Acc, d_Abb, d_Agg, d_g);
     if (nG > 0) allreduce(d_Agg, NGMAX * NGMAX + NGMAX);  // global block: all shards
     if (fuse) {
@@ -1102,6 +1131,10 @@ static void error_stats(const double *dist, int M, double *avg, double *mn, doub
 
 int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_out,
                   double *stats) {
+    // an epilogue reduction a previous entry point deferred (pend_red) reads
+    // d_partial rows this call rewrites: dropped, its slots are not read
+    // outside the solve that deferred it
+    pend_red = false;
     attrs_reset();
     if (x) {
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
@@ -1134,6 +1167,10 @@ int Plan::measure(const double *x, double *fvec_out, double *eu_out, double *ed_
 // Per-observation reprojected point and corrected marker at x (caller's
 // observation order); the scratch trial buffers carry them (no solve runs).
 int Plan::reproject(const double *x, double *point_out, double *marker_out) {
+    // an epilogue reduction a previous entry point deferred (pend_red) reads
+    // d_partial rows this call rewrites: dropped, its slots are not read
+    // outside the solve that deferred it
+    pend_red = false;
     attrs_reset();
     if (x) {
         MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
@@ -1150,6 +1187,10 @@ int Plan::reproject(const double *x, double *point_out, double *marker_out) {
 // Dense reference-order Jacobian at x (column-major, ldfjac = m); for tests
 // and small problems only.
 int Plan::dense_jacobian(const double *x, double *fjac) {
+    // an epilogue reduction a previous entry point deferred (pend_red) reads
+    // d_partial rows this call rewrites: dropped, its slots are not read
+    // outside the solve that deferred it
+    pend_red = false;
     if (nranks > 1) throw Unsupported{"dense Jacobian of a sharded plan"};
     attrs_reset();
     MMBA_HIP(hipMemcpyAsync(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice, s));
@@ -1217,6 +1258,10 @@ __global__ void k_dense_symv_res(const double *__restrict__ A, int ld, int n,
 }
 
 int Plan::reduced_residual(const double *x, double lam, double *relres) {
+    // an epilogue reduction a previous entry point deferred (pend_red) reads
+    // d_partial rows this call rewrites: dropped, its slots are not read
+    // outside the solve that deferred it
+    pend_red = false;
     if (!dense) throw Unsupported{"reduced residual hook: dense reduced plans only"};
     if (!d_Skeep) {
         d_Skeep = dalloc<double>((size_t)ds.ld * (ds.n + 1));
@@ -1307,6 +1352,7 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         host_sync();
         ++spec_replays;
         pre_jac_pending = false;
+        pre_bnd_pending = false;
         seq_pending = false;
         mirror_pending = false;
         slots_staged = false;
@@ -1328,6 +1374,10 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
 
 int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *ed_out,
                      mmba_result *res, const mmba_callbacks *cb, mmba_trace *trace) {
+    // an epilogue reduction a previous entry point deferred (pend_red) reads
+    // d_partial rows this call rewrites: dropped, its slots are not read
+    // outside the solve that deferred it
+    pend_red = false;
     const double t_start = wall_now();
     t_func = t_jac = t_linear = 0.;
     cbk = cb;

@@ -1649,6 +1649,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_jcol = dalloc<int>((size_t)std::max(D.lmax, 1) * M);
     d_nloc = dalloc<int>(M);
     d_Acc = dalloc<double>((size_t)ncf * PCMAX * PCMAX);
+    // k_ne_cf_split's partial sums and per camera-frame tickets (monotonic:
+    // zeroed once)
+    d_cf_part = dalloc<double>((size_t)std::max(ncf, 1) * NE_CF_SPLIT * NE_CF_NT);
+    d_cf_ticket = dalloc<unsigned>((size_t)std::max(ncf, 1));
+    MMBA_HIP(hipMemsetAsync(d_cf_ticket, 0, sizeof(unsigned) * std::max(ncf, 1), s));
     d_Acg = dalloc<double>((size_t)ncf * PCMAX * NGMAX);
     d_Abb = dalloc<double>((size_t)nB * 9);
     d_Abg = dalloc<double>((size_t)nB * PBMAX * NGMAX);

@@ -495,6 +495,9 @@ struct Plan {
     bool jb_recompute() const;
     DevProblem P_nojb() const;
     bool stall_done = false;  // MMBA_PATH_STALL_SHARD fired
+    bool pre_bnd_pending = false;
+    double *d_cf_part = nullptr;      // k_ne_cf_split partial sums
+    unsigned *d_cf_ticket = nullptr;  // k_ne_cf_split tickets (monotonic)  // the bundle pass was enqueued with the pre-enqueued Jacobian
     void wait_event();
     // speculative trial (lmpar's first, undamped, step taken before the
     // host has read it): its errorList / errorDistanceList land here and are
