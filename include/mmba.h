@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MMBA_ABI_VERSION 9
+#define MMBA_ABI_VERSION 10
 
 /* Return codes. */
 #define MMBA_OK 0
@@ -629,6 +629,12 @@ typedef struct mmba_kernel_stats {
                                arrow's n_b nG (2w + nG) + nG^3/3); block
                                diagonal sum pc^3/3 + 4 pc; dense n^3/3 + 4n^2
                                -- chol_flops is what the solver executes   */
+    /* ---- ABI 10 ---- */
+    int32_t pre_handbacks;  /* solves of this plan whose page-locked output
+                               lists the speculative hand-back stored (one
+                               kernel behind the trial the device decided
+                               ends the solve)                            */
+    int32_t reserved10;
 } mmba_kernel_stats;
 int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                            mmba_kernel_stats *out);
@@ -687,7 +693,15 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       Jacobian pass stores (same bits; measured slower on C4) */
 #define MMBA_PATH_NE_CF_SPLIT 19   /* 0: long camera-frame segments (C2) take one workgroup per
                                       camera-frame in the normal equations instead of four */
-#define MMBA_PATH_NUM 20
+#define MMBA_PATH_RED_BD 20        /* 0: the Jacobian epilogue's scalar reduction runs as its own
+                                      launch on block-diagonal plans without globals (C2) instead
+                                      of riding in the one-launch damped solve */
+#define MMBA_PATH_HANDBACK_DMA 21  /* 1: page-locked output lists come back by DMA copies (one
+                                      per list, on their own streams) instead of one kernel
+                                      storing them through their host-mapped addresses */
+#define MMBA_PATH_PRE_HANDBACK 22  /* 0: no speculative hand-back behind each decided trial (the
+                                      page-locked lists leave after the host's last decision) */
+#define MMBA_PATH_NUM 23
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -22,7 +22,7 @@ AUTO_DIFF_TYPE_CENTRAL = 1
 ROBUST_LOSS_TYPE_TRIVIAL = 0
 ROBUST_LOSS_TYPE_SOFT_L_ONE = 1
 ROBUST_LOSS_TYPE_CAUCHY = 2
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # mmba_debug_set_path keys (test hook: pin a plan-builder choice)
 PATH_PCR = 1
@@ -44,7 +44,10 @@ PATH_PCR_CHAIN = 16
 PATH_BACKSUB_ONEPASS = 17
 PATH_JB_RECOMPUTE = 18
 PATH_NE_CF_SPLIT = 19
-PATH_NUM = 20
+PATH_RED_BD = 20
+PATH_HANDBACK_DMA = 21
+PATH_PRE_HANDBACK = 22
+PATH_NUM = 23
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1
@@ -233,6 +236,8 @@ class MmbaKernelStats(C.Structure):
         ("band_levels", C.c_int32),
         ("band_block", C.c_int32),
         ("chol_flops_alg", C.c_double),
+        ("pre_handbacks", C.c_int32),
+        ("reserved10", C.c_int32),
     ]
 
     def as_dict(self):

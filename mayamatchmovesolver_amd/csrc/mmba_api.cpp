@@ -18,9 +18,9 @@ namespace mmba {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 
-static_assert(MMBA_PATH_NUM == 20, "one initialiser per path key");
-static std::atomic<int> g_path[MMBA_PATH_NUM] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
-                                                 -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static_assert(MMBA_PATH_NUM == 23, "one initialiser per path key");
+static std::atomic<int> g_path[MMBA_PATH_NUM] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                                 -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int path_choice(int key) {
     return (key > 0 && key < MMBA_PATH_NUM) ? g_path[key].load() : -1;
 }
@@ -424,6 +424,7 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing, mmba_kernel_stats
         out->dataflow_fallback = p.bs.df_off ? 1 : 0;
         out->shards_replicated = p.replicated ? 1 : 0;
         out->spec_replays = p.spec_replays;
+        out->pre_handbacks = (int32_t)p.pre_handbacks;
         {
             const BandSolver &b = p.bs;
             out->band_solver = !p.band ? 0

@@ -96,7 +96,8 @@ __device__ __forceinline__ int potrf_inv(double (&a)[NB], double (&x)[NB]) {
 }
 
 // Corner factor of the arrow, one wave: Ld (lower) and Ld^-1 of the packed
-// lower nc x nc matrix sZ (na rows used, identity padding), NC a power of 2.
+// lower nc x nc matrix sZ (na rows used, identity padding), NC a power of 2
+// (64 for arrows wider than 32: NGMAX = 48 is not one).
 template <int NC>
 __device__ __forceinline__ int band_corner(const double *sZ, int na, double *Gd, double *Gdinv) {
     const int tid = threadIdx.x, r = tid & (NC - 1);
@@ -105,9 +106,10 @@ __device__ __forceinline__ int band_corner(const double *sZ, int na, double *Gd,
     for (int c = 0; c < NC; ++c) a[c] = (c <= r && r < na) ? sZ[r * (r + 1) / 2 + c] : 0.;
     if (r >= na) a[r] = 1.;
     const int badl = potrf_inv<NC>(a, x);
-    if (tid < NC) {
+    if (tid < NC && r < NGMAX) {  // (NC = 64 > NGMAX: the padding rows stay out)
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
+            if (c >= NGMAX) break;
             Gd[r * NGMAX + c] = (c <= r) ? a[c] : 0.;
             Gdinv[c * NGMAX + r] = x[c];
         }
@@ -285,8 +287,10 @@ __global__ void __launch_bounds__(256)
     if (CORNER) {
         // Ld Ld^T = D - Y Y^T (accumulated in sZ), na = nG <= NGMAX
         if (na > 0 && tid < 64) {
-            const int badl = na <= 16 ? band_corner<16>(sZ, na, Gd, Gdinv)
-                                      : band_corner<NGMAX>(sZ, na, Gd, Gdinv);
+            // (NC a power of two: lanes r = tid & (NC - 1))
+            const int badl = na <= 16   ? band_corner<16>(sZ, na, Gd, Gdinv)
+                             : na <= 32 ? band_corner<32>(sZ, na, Gd, Gdinv)
+                                        : band_corner<64>(sZ, na, Gd, Gdinv);
             if (tid == 0 && badl) bad = 1;
         }
     } else {
@@ -672,7 +676,7 @@ void band_factor(hipStream_t s, const BandSolver &B, int *fail, long long *probe
         k_sep_z<<<nblk_((long)hp.na * (hp.na + 1) / 2, 256), 256, 0, s>>>(
             B.d_parts + B.p_lo, B.w, B.apool, B.XA, B.zpool);
     } else {
-        k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGMAX, false><<<nloc, 256, 0, s>>>(
+        k_band_factor<8, 64, WBAND_PART, 2 * WBAND_PART + NGPART, false><<<nloc, 256, 0, s>>>(
             B.Bd, B.w, B.d_parts + B.p_lo, B.apool, B.zpool, B.Dinv, nullptr, nullptr, fail, probe);
     }
     {

@@ -14,17 +14,18 @@
 #include "mmba_geom.h"
 #include "mmba_kernels.h"
 #include "mmba_plan.h"
+#include "mmba_red_dev.h"
 
 namespace mmba {
 
 // Lane roles of one block's wave: rows 0..PC-1 of the block, then one
 // right-hand-side lane per arrow row (Y_b columns), then the rhs lane.
-constexpr int BD_G0 = 16;  // first arrow lane
+constexpr int BD_G0 = PCMAX;  // first arrow lane (12 + NGMAX 48 + rhs: 61 lanes)
 constexpr int BD_R = BD_G0 + NGMAX;  // right-hand-side lane (after the widest arrow)
 static_assert(BD_R < 64, "arrow and right-hand-side lanes exceed the wave");
 
 // Augmented Cholesky of one block by one wave (bcr_chol_aug_wave's scheme
-// with a register-only column broadcast: PC <= 10 is short enough for
+// with a register-only column broadcast: PC <= 12 is short enough for
 // v_readlane per entry): lane i < PC holds row i of [S_b], every
 // right-hand-side lane holds its column; afterwards rows hold C and the
 // right-hand-side lanes (C^-1 b)^T.  Rows >= pc are identity padding.
@@ -199,6 +200,10 @@ __global__ void __launch_bounds__(256) k_bd_fwd(BdDev B, const double *__restric
 // Arrow corner: T = S_GG - sum_b Y_b^T Y_b = Ct Ct^T (dense, one wave, lane =
 // row), y_G = Ct^-1 (r_G - sum_b Y_b^T y_b); with back: x_G = Ct^-T y_G (the
 // back kernel then needs it).  factor = false: forward with the stored Ct.
+// NGT: the arrow width this instantiation carries in registers (nG <= NGT;
+// the identity padding beyond nG changes no entry, so the bits do not depend
+// on NGT)
+template <int NGT>
 __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restrict__ r, double *y,
                                                 double *x, double *xs, int factor, int *fail) {
     __shared__ double zs[NGMAX * NGMAX], gs[NGMAX];
@@ -251,12 +256,12 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
     double *Ct = B.FT;  // NGMAX x NGMAX lower, diagonal 1/C_jj
     if (factor) {
         // row `lane` of T
-        double a[NGMAX];
+        double a[NGT];
 #pragma unroll
-        for (int c = 0; c < NGMAX; ++c) {
+        for (int c = 0; c < NGT; ++c) {
             double v = 0.;
             if (lane < nG && c <= lane) v = B.Gd[lane * NGMAX + c] - zs[lane * NGMAX + c];
-            else if (lane < NGMAX && lane >= nG && c == lane) v = 1.;
+            else if (lane < NGT && lane >= nG && c == lane) v = 1.;
             a[c] = v;
         }
         // rows / columns >= nG are identity padding: their pivots change
@@ -264,7 +269,7 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
         double rsl = lane >= nG ? 1. : 0.;
         bool bad = false;
 #pragma unroll
-        for (int j = 0; j < NGMAX; ++j) {
+        for (int j = 0; j < NGT; ++j) {
             if (j < nG) {  // (wave-uniform)
                 double d = wave_rdlane(a[j], j);
                 if (!(d > 0.) || !isfinite(d)) {
@@ -276,18 +281,18 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
                 a[j] = (lane == j) ? d * rs : (lane > j ? l : a[j]);
                 if (lane == j) rsl = rs;
 #pragma unroll
-                for (int c = j + 1; c < NGMAX; ++c) a[c] = fma(-l, wave_rdlane(l, c), a[c]);
+                for (int c = j + 1; c < NGT; ++c) a[c] = fma(-l, wave_rdlane(l, c), a[c]);
             }
         }
         if (bad && lane == 0) atomicOr(fail, 1);
-        if (lane < NGMAX)
+        if (lane < NGT)
 #pragma unroll
-            for (int c = 0; c < NGMAX; ++c) Ct[lane * NGMAX + c] = c == lane ? rsl : (c < lane ? a[c] : 0.);
+            for (int c = 0; c < NGT; ++c) Ct[lane * NGMAX + c] = c == lane ? rsl : (c < lane ? a[c] : 0.);
         __syncthreads();
     }
     // y_G = Ct^-1 (r_G - gs), x_G = Ct^-T y_G: serial in one lane (nG <= 16)
     if (lane == 0) {
-        double v[NGMAX];
+        double v[NGT];
         for (int q = 0; q < nG; ++q) {
             double s = r[nb + q] - gs[q];
             for (int c = 0; c < q; ++c) s = fma(-Ct[q * NGMAX + c], v[c], s);
@@ -313,17 +318,28 @@ __global__ void __launch_bounds__(64) k_bd_root(BdDev B, const double *__restric
 // register rows, scatter to parameter order, and ||D xs||^2 plus the fail
 // flag reduced by the last block into scalar[dn_slot] / scalar[fail_slot]
 // (the flag is cleared).  One launch replaces k_schur_init, k_bd_factor,
-// k_bd_back, k_sumsq and k_reduce_multi.
+// k_bd_back, k_sumsq and k_reduce_multi.  Workgroups [nb, nb + spec.nrows)
+// reduce the rows of the Jacobian epilogue's deferred reduction (Plan::
+// red_defer_ok; k_reduce_multi's arithmetic, reduce_row_block) -- the C2
+// iteration's separate k_reduce_multi launch.
 template <int PC>
 __global__ void __launch_bounds__(256) k_bd_direct(DevProblem P, BdDev B,
                                                    const double *__restrict__ Acc,
                                                    const double *__restrict__ g,
                                                    const double *__restrict__ diag, double lam,
                                                    double *xR, double *xs, int *fail,
-                                                   double *scalar, int dn_slot, int fail_slot) {
+                                                   double *scalar, int dn_slot, int fail_slot,
+                                                   int nb, const double *__restrict__ partial,
+                                                   const RedSpec spec) {
     __shared__ double wpart[4];
     __shared__ double red[256];
     __shared__ int last;
+    if ((int)blockIdx.x >= nb) {
+        const RedRow rw = spec.row[blockIdx.x - nb];
+        const double v = reduce_row_block<false>(partial, rw, red);
+        if (threadIdx.x == 0) scalar[rw.slot] = v;
+        return;
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.x * 4 + wv;
     double dn = 0.;
@@ -396,13 +412,13 @@ __global__ void __launch_bounds__(256) k_bd_direct(DevProblem P, BdDev B,
         const double v = (wpart[0] + wpart[1]) + (wpart[2] + wpart[3]);
         __hip_atomic_store(&B.part[blockIdx.x], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __threadfence();
-        last = atomicAdd(B.ticket, 1u) == gridDim.x - 1;
+        last = atomicAdd(B.ticket, 1u) == (unsigned)nb - 1;
     }
     __syncthreads();
     if (!last) return;
     __threadfence();
     double s = 0.;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+    for (int i = threadIdx.x; i < nb; i += blockDim.x)
         s += __hip_atomic_load(&B.part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     red[threadIdx.x] = s;
     __syncthreads();
@@ -420,14 +436,28 @@ __global__ void __launch_bounds__(256) k_bd_direct(DevProblem P, BdDev B,
 
 void bd_direct(hipStream_t s, const DevProblem &P, const BdDev &D, const double *Acc,
                const double *g, const double *diag, double lam, double *xR, double *xs,
-               int *fail, double *scalar, int dn_slot, int fail_slot) {
+               int *fail, double *scalar, int dn_slot, int fail_slot, const RedSpec *red,
+               const double *partial) {
     const int grid = (D.nblk + 3) / 4;
+    const RedSpec rs = red ? *red : RedSpec{};
+    const int nr = red ? red->nrows : 0;
     if (D.PC <= 8)
-        k_bd_direct<8><<<grid, 256, 0, s>>>(P, D, Acc, g, diag, lam, xR, xs, fail, scalar,
-                                            dn_slot, fail_slot);
+        k_bd_direct<8><<<grid + nr, 256, 0, s>>>(P, D, Acc, g, diag, lam, xR, xs, fail, scalar,
+                                                 dn_slot, fail_slot, grid, partial, rs);
     else
-        k_bd_direct<PCMAX><<<grid, 256, 0, s>>>(P, D, Acc, g, diag, lam, xR, xs, fail, scalar,
-                                                dn_slot, fail_slot);
+        k_bd_direct<PCMAX><<<grid + nr, 256, 0, s>>>(P, D, Acc, g, diag, lam, xR, xs, fail,
+                                                     scalar, dn_slot, fail_slot, grid, partial,
+                                                     rs);
+}
+
+static void bd_root(hipStream_t s, const BdDev &D, const double *r, double *y, double *x,
+                    double *xs, int factor, int *fail) {
+    if (D.nG <= 16)
+        k_bd_root<16><<<1, 64, 0, s>>>(D, r, y, x, xs, factor, fail);
+    else if (D.nG <= 32)
+        k_bd_root<32><<<1, 64, 0, s>>>(D, r, y, x, xs, factor, fail);
+    else
+        k_bd_root<NGMAX><<<1, 64, 0, s>>>(D, r, y, x, xs, factor, fail);
 }
 
 template <int PC>
@@ -441,7 +471,7 @@ static void bd_factor_k(hipStream_t s, const BdDev &D, int *fail, const double *
         return;
     }
     k_bd_factor<PC><<<g, 256, 0, s>>>(D, r, y, fail);
-    k_bd_root<<<1, 64, 0, s>>>(D, r, y, x, xs, 1, fail);
+    bd_root(s, D, r, y, x, xs, 1, fail);
     if (x) k_bd_back<PC><<<g, 256, 0, s>>>(D, y, x, xs);
 }
 
@@ -459,7 +489,7 @@ void bd_forward(hipStream_t s, const BdDev &D, const double *w, double *y) {
         k_bd_fwd<8><<<g, 256, 0, s>>>(D, w, y);
     else
         k_bd_fwd<PCMAX><<<g, 256, 0, s>>>(D, w, y);
-    if (D.nG > 0) k_bd_root<<<1, 64, 0, s>>>(D, w, y, nullptr, nullptr, 0, nullptr);
+    if (D.nG > 0) bd_root(s, D, w, y, nullptr, nullptr, 0, nullptr);
 }
 
 }  // namespace mmba

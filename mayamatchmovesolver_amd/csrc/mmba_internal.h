@@ -23,10 +23,11 @@
 
 namespace mmba {
 
-constexpr int PCMAX = 10;   // params per camera-frame block
+constexpr int PCMAX = 12;   // params per camera-frame block
 constexpr int PBMAX = 3;    // params per bundle block
-constexpr int NGMAX = 32;   // global parameters (the arrow of the reduced system)
+constexpr int NGMAX = 48;   // global parameters (the arrow of the reduced system)
 constexpr int NGLANE = 16;  // arrows up to this width ride in spare lanes of the BCR pivot chains
+constexpr int NGPART = 32;  // widest arrow the partitioned band chain's LDS window carries
 constexpr int LMAX = 32;    // local Jacobian columns per observation
 constexpr int CF_AIDX = 16;  // camera-frame attribute table: 7 camera + 9 TRS
 constexpr int TILE = 64;    // reduced-system tile edge

@@ -359,7 +359,8 @@ int pcr_grid(int nblk);
 // with x, the solution (scattered to parameter order into xs when non-null).
 void bd_direct(hipStream_t s, const DevProblem &P, const BdDev &D, const double *Acc,
                const double *g, const double *diag, double lam, double *xR, double *xs,
-               int *fail, double *scalar, int dn_slot, int fail_slot);
+               int *fail, double *scalar, int dn_slot, int fail_slot,
+               const RedSpec *red = nullptr, const double *partial = nullptr);
 void bd_factor_solve(hipStream_t s, const BdDev &D, int *fail, const double *r, double *y,
                      double *x, double *xs);
 // y = L^-1 w with the stored factor (lmpar's Newton term)
@@ -395,6 +396,11 @@ void launch_diag_init(hipStream_t s, int n, const double *acnorm, double *diag, 
                       int mode);
 void launch_newton_v(hipStream_t s, int n, const double *diag, const double *x, double dxnorm,
                      double *v);
+// unsharded hand-back into host-mapped page-locked lists (k_handback_host)
+void launch_handback_host(hipStream_t s, int Mg, int nrows, const int *dev_of_ref,
+                          const double *f2, const double *eu2, const double *ed, double *hf,
+                          double *heu, double *hed, const double *dec = nullptr,
+                          const double *f2_trial = nullptr);
 void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const int *obs_own,
                       const double *f2,
                       const double *eu2, const double *ed, double *f2o, double *eu2o,

@@ -11,6 +11,7 @@
 
 #include "mmba_geom.h"
 #include "mmba_kernels.h"
+#include "mmba_red_dev.h"
 
 namespace mmba {
 
@@ -69,16 +70,6 @@ __device__ __forceinline__ void finish_blocks(double v, double *partial, double 
         *out = red[0];
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-__device__ __forceinline__ void st_sc1(double *p, double v) {  // write-through store
-    __hip_atomic_store((gu64_t *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double *p) {  // L1-bypassing load
-    return __longlong_as_double((long long)__hip_atomic_load(
-        (gu64_t *)const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // 3 x 3 damped bundle factor of one bundle (k_bundle_factor's arithmetic):
@@ -143,30 +134,6 @@ __device__ __forceinline__ void bundle_chol3(double (&A)[3][3], double (&rhs)[3]
             for (int c = 0; c < 3; ++c) Lo[a][c] = L[a][c];
         }
     }
-}
-
-// One partial row reduced by one 256-thread workgroup: k_reduce_multi's
-// arithmetic (thread t sums entries t, t + 256, ..., then the fixed tree).
-template <bool SC1>
-__device__ __forceinline__ double reduce_row_block(const double *partial, const RedRow &rw,
-                                                   double *red) {
-    const bool mx = rw.is_max != 0;
-    double s = 0.;
-    for (int i = threadIdx.x; i < rw.n; i += blockDim.x) {
-        const double q = SC1 ? ld_sc1(&partial[rw.off + i]) : partial[rw.off + i];
-        s = mx ? fmax(s, q) : s + q;
-    }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            red[threadIdx.x] = mx ? fmax(red[threadIdx.x], red[threadIdx.x + w])
-                                  : red[threadIdx.x] + red[threadIdx.x + w];
-        __syncthreads();
-    }
-    const double v = red[0];
-    __syncthreads();
-    return v;
 }
 
 // reduce_row_block by one wave (a 64-thread workgroup of another launch):
@@ -1186,6 +1153,68 @@ __device__ __forceinline__ void epi_store(const NeEpi &E, int col, double zf, do
     E.partial[2 * E.rstride + col] = gm;
 }
 
+// A camera-frame's PC parameters' bookkeeping with one wave: lane a < PC
+// takes parameter a (epi_param; d / gp its diagonal and gradient sums), then
+// every lane folds the PC contributions in parameter order and lane 0 stores
+// them -- the serial loop's sums (xn: ((0 + t_0) + t_1) + ...; zf / gm are
+// order-free), without its chain of PC dependent index / diag loads (the
+// last step of k_ne_cf_u / k_ne_cf_split / k_jac_ne_u: ~10 us on C2 as one
+// thread).  Called by all 64 lanes of one wave.
+// The operands epi_param reads from memory, loaded by epi_preload before the
+// observation loop, so the epilogue after it issues no dependent loads.
+struct EpiPre {
+    int p;      // the parameter of lane a (camera-frame variant a)
+    double dg;  // diag[p] before this Jacobian
+    double xv;  // x[p] (do_xn)
+    double fn;  // ||f|| (do_gn)
+};
+template <int PC>
+__device__ __forceinline__ EpiPre epi_preload(const DevProblem &P, const NeEpi &E, int cf,
+                                              int lane) {
+    EpiPre q{-1, 0., 0., 0.};
+    if (!E.on || lane >= PC) return q;
+    q.p = P.cf_var_param[P.cf_var_off[cf] + 1 + lane];
+    q.dg = E.diag[q.p];
+    if (E.do_xn) q.xv = E.x[q.p];
+    if (E.do_gn) q.fn = E.fnorm_sq ? sqrt(*E.fnorm_sq) : E.fnorm;
+    return q;
+}
+// epi_param with its loads done (same operations, same bits)
+__device__ __forceinline__ void epi_param_pre(const NeEpi &E, const EpiPre &q, double d, double gp,
+                                              double &zf, double &xn, double &gm) {
+    const double an = sqrt(d);
+    E.acnorm[q.p] = an;
+    double dg = q.dg;
+    if (E.mode != 2) {
+        if (E.first) dg = an == 0. ? 1. : an;
+        dg = fmax(dg, an);
+        E.diag[q.p] = dg;
+    }
+    if (an == 0.) zf = 1.;
+    if (E.do_xn) {
+        const double v = dg * q.xv;
+        xn += v * v;
+    }
+    if (E.do_gn && an != 0.) {
+        if (q.fn != 0.) gm = fmax(gm, fabs((gp / q.fn) / an));
+    }
+}
+template <int PC>
+__device__ __forceinline__ void epi_params_wave(const DevProblem &P, const NeEpi &E, int cf,
+                                                int lane, double d, double gp, const EpiPre &q) {
+    double zf = 0., xn = 0., gm = 0.;
+    if (lane < PC) epi_param_pre(E, q, d, gp, zf, xn, gm);
+    double Z = 0., X = 0., G = 0.;
+#pragma unroll
+    for (int a = 0; a < PC; ++a) {
+        const double za = __shfl(zf, a), xa = __shfl(xn, a), ga = __shfl(gm, a);
+        if (za != 0.) Z = 1.;
+        X += xa;
+        G = fmax(G, ga);
+    }
+    if (lane == 0) epi_store(E, E.cf_base + cf, Z, X, G);
+}
+
 
 template <int PC, int NW, int NG>
 __device__ __forceinline__ void ne_cf_u_body(const DevProblem &P, const double *__restrict__ J,
@@ -1211,6 +1240,7 @@ __device__ __forceinline__ void ne_cf_u_body(const DevProblem &P, const double *
     const size_t M = P.M;
     const int nCF = P.nR - P.nG;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const EpiPre epq = epi_preload<PC>(P, E, cf, lane);
     double acc[NT];
 #pragma unroll
     for (int e = 0; e < NT; ++e) acc[e] = 0.;
@@ -1282,21 +1312,20 @@ __device__ __forceinline__ void ne_cf_u_body(const DevProblem &P, const double *
             if (q < P.nG) Acg[((size_t)cf * PCMAX + a) * NGMAX + q] = v;
         }
     }
-    if (E.on && tid == 0) {
+    if (E.on && wv == 0) {
         // the block's parameters (sums re-formed in the same order as above)
-        double zf = 0., xn = 0., gm = 0.;
-        const int v0 = P.cf_var_off[cf] + 1;
-        for (int a = 0; a < PC; ++a) {
-            const int ed = a * PC - a * (a - 1) / 2;  // upper-triangle index of (a, a)
-            double d = wsum[0][ed], gp = wsum[0][NCC + a];
+        double d = 0., gp = 0.;
+        if (lane < PC) {
+            const int ed = lane * PC - lane * (lane - 1) / 2;  // upper-triangle index of (a, a)
+            d = wsum[0][ed];
+            gp = wsum[0][NCC + lane];
 #pragma unroll
             for (int w = 1; w < NW; ++w) {
                 d += wsum[w][ed];
-                gp += wsum[w][NCC + a];
+                gp += wsum[w][NCC + lane];
             }
-            epi_param(E, P.cf_var_param[v0 + a], d, gp, zf, xn, gm);
         }
-        epi_store(E, E.cf_base + cf, zf, xn, gm);
+        epi_params_wave<PC>(P, E, cf, lane, d, gp, epq);
     }
 }
 // k_ne_cf_u for long camera-frame segments without global parameters (C2:
@@ -1327,6 +1356,7 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_split(DevProblem P, const dou
     const int o0 = P.cf_obs_off[cf], o1 = P.cf_obs_off[cf + 1];
     const size_t M = P.M;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const EpiPre epq = epi_preload<PC>(P, E, cf, lane);
     double acc[NT];
 #pragma unroll
     for (int e = 0; e < NT; ++e) acc[e] = 0.;
@@ -1371,9 +1401,12 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_split(DevProblem P, const dou
     if (!last_s) return;
     const double *all = E.cf_part + (size_t)cf * NS * NE_CF_NT;
     for (int e = tid; e < NT; e += 64 * NW) {
-        double v = ld_sc1(&all[e]);
+        double t[NS];  // every part's load issued before the sum
 #pragma unroll
-        for (int q = 1; q < NS; ++q) v += ld_sc1(&all[(size_t)q * NE_CF_NT + e]);
+        for (int q = 0; q < NS; ++q) t[q] = ld_sc1(&all[(size_t)q * NE_CF_NT + e]);
+        double v = t[0];
+#pragma unroll
+        for (int q = 1; q < NS; ++q) v += t[q];
         fin[e] = v;
     }
     __syncthreads();
@@ -1393,14 +1426,10 @@ __global__ void __launch_bounds__(64 * NW) k_ne_cf_split(DevProblem P, const dou
             g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
         }
     }
-    if (E.on && tid == 0) {
-        double zf = 0., xn = 0., gm = 0.;
-        const int v0 = P.cf_var_off[cf] + 1;
-        for (int a = 0; a < PC; ++a) {
-            const int ed = a * PC - a * (a - 1) / 2;  // upper-triangle index of (a, a)
-            epi_param(E, P.cf_var_param[v0 + a], fin[ed], fin[NCC + a], zf, xn, gm);
-        }
-        epi_store(E, E.cf_base + cf, zf, xn, gm);
+    if (E.on && wv == 0) {
+        const int ed = lane * PC - lane * (lane - 1) / 2;  // upper-triangle index of (a, a)
+        epi_params_wave<PC>(P, E, cf, lane, lane < PC ? fin[ed] : 0., lane < PC ? fin[NCC + lane] : 0.,
+                            epq);
     }
 }
 
@@ -1531,20 +1560,22 @@ __global__ void __launch_bounds__(64 * NW) k_jac_ne_u(
             g[P.cf_var_param[P.cf_var_off[cf] + 1 + (e - NCC)]] = v;
         }
     }
-    if (E.on && tid == 0) {
-        double zf = 0., xn = 0., gm = 0.;
-        const int v0 = P.cf_var_off[cf] + 1;
-        for (int a = 0; a < PC; ++a) {
-            const int ed2 = a * PC - a * (a - 1) / 2;
-            double d = wsum[0][ed2], gp = wsum[0][NCC + a];
+    if (E.on && (tid >> 6) == 0) {
+        const int ln = tid & 63;
+        double d = 0., gp = 0.;
+        if (ln < PC) {
+            const int ed2 = ln * PC - ln * (ln - 1) / 2;
+            d = wsum[0][ed2];
+            gp = wsum[0][NCC + ln];
 #pragma unroll
             for (int w = 1; w < NW; ++w) {
                 d += wsum[w][ed2];
-                gp += wsum[w][NCC + a];
+                gp += wsum[w][NCC + ln];
             }
-            epi_param(E, P.cf_var_param[v0 + a], d, gp, zf, xn, gm);
         }
-        epi_store(E, E.cf_base + cf, zf, xn, gm);
+        // (loaded here: preloaded before the loop they cost this 232-VGPR
+        // kernel its second wave per SIMD)
+        epi_params_wave<PC>(P, E, cf, ln, d, gp, epi_preload<PC>(P, E, cf, ln));
     }
     if (pr) {
         pr[3] = (long long)wall_clock64();
@@ -2284,6 +2315,9 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
 // (zeros where a row has no bundle block / no camera block).
 // nob: the observation workgroups; workgroups nob + r reduce row r of red
 // (the Jacobian epilogue's rows, which no W row reads: one launch less)
+// PCT: the widest camera-frame block the launch carries in registers (the
+// plan's pc_uniform-based bound: 8 for pose + focal plans, else PCMAX).
+template <int PCT>
 __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__restrict__ J,
                                                   const double *__restrict__ Lb, double *W,
                                                   int nob, const RedSpec red,
@@ -2306,7 +2340,7 @@ __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__
     const int pb = i < M ? P.bnd_pb[b] : 0;
     if (pb > 0) {
         const int cf = P.obs_cf[i];
-        const int pc = min(P.cf_pc[cf], wst / 3);
+        const int pc = min(min(P.cf_pc[cf], wst / 3), PCT);
         const int s = P.cf_var_off[cf + 1] - P.cf_var_off[cf] - 1;
         // every index static (no scratch): bundle columns a < pb, camera rows r < pc
         double bx[3], by[3], L[3][3], il[3];
@@ -2319,14 +2353,14 @@ __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__
         }
 #pragma unroll
         for (int a = 0; a < 3; ++a) il[a] = a < pb ? 1.0 / L[a][a] : 0.;
-        double cx[PCMAX], cy[PCMAX];
+        double cx[PCT], cy[PCT];
 #pragma unroll
-        for (int r = 0; r < PCMAX; ++r) {  // every load issued before the solves
+        for (int r = 0; r < PCT; ++r) {  // every load issued before the solves
             cx[r] = r < pc ? J[(size_t)(2 * r) * M + i] : 0.;
             cy[r] = r < pc ? J[(size_t)(2 * r + 1) * M + i] : 0.;
         }
 #pragma unroll
-        for (int r = 0; r < PCMAX; ++r) {
+        for (int r = 0; r < PCT; ++r) {
             if (r < pc) {
                 double w[3];
 #pragma unroll
@@ -3505,6 +3539,47 @@ __global__ void k_unpermute(int M, const int *__restrict__ ref_of_dev,
     if (ed) edo[r] = ed[i];
 }
 
+// Unsharded hand-back straight into the caller's page-locked lists (their
+// host-mapped addresses): thread r takes reference position r, gathers
+// device position dev_of_ref[r] and stores 16 + 16 + 8 B, so consecutive
+// threads write consecutive host bytes (full PCIe write requests); positions
+// [Mg, Mg + nrows) copy the stiffness / smoothness rows that follow the
+// observations in errorList / ud->errorList.  One launch replaces k_unpermute
+// and the three DMA copies (tools/ubench/d2h: 163 against 192 us for C2's
+// 8 MB).
+// dec (the speculative form, enqueued behind a trial on its own stream):
+// the device's LM decision on that trial (LmDec slots from SL_DGO: [1] the
+// ratio, [4] info when the trial was taken) -- the lists are stored only when
+// the solve ends on it (info > 0), errorList from the trial's f when lmder
+// accepts it (ratio >= 1e-4, lm_decide) and from the accepted f otherwise.
+__global__ void __launch_bounds__(256) k_handback_host(int Mg, int nrows,
+                                                       const int *__restrict__ dev_of_ref,
+                                                       const double *__restrict__ f2,
+                                                       const double *__restrict__ eu2,
+                                                       const double *__restrict__ ed,
+                                                       double *hf, double *heu, double *hed,
+                                                       const double *__restrict__ dec,
+                                                       const double *__restrict__ f2_trial) {
+    if (dec) {
+        if (!(dec[4] > 0.)) return;
+        if (dec[1] >= 1e-4) f2 = f2_trial;
+    }
+    const int stride = gridDim.x * blockDim.x;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < Mg + nrows; r += stride) {
+        if (r < Mg) {
+            const int d = dev_of_ref[r];
+            if (hf) reinterpret_cast<double2 *>(hf)[r] = reinterpret_cast<const double2 *>(f2)[d];
+            if (heu)
+                reinterpret_cast<double2 *>(heu)[r] = reinterpret_cast<const double2 *>(eu2)[d];
+            if (hed) hed[r] = ed[d];
+        } else {
+            const int k = r - Mg;  // rows: device and reference order agree
+            if (hf) hf[2 * (size_t)Mg + k] = f2[2 * (size_t)Mg + k];
+            if (heu) heu[2 * (size_t)Mg + k] = eu2[2 * (size_t)Mg + k];
+        }
+    }
+}
+
 }  // namespace mmba
 
 // =========================================================================
@@ -4255,8 +4330,14 @@ void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const
                       double *W, const RedSpec *red, const double *partial, double *scalar) {
     const int nob = nblk(P.M, 64), nr = red ? red->nrows : 0;
     if (nob + nr > 0)
-        k_schur_obs<<<nob + nr, 64, sizeof(double) * 64 * P.wst, s>>>(
-            P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar);
+    {
+        if (P.wst / 3 <= 8)
+            k_schur_obs<8><<<nob + nr, 64, sizeof(double) * 64 * P.wst, s>>>(
+                P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar);
+        else
+            k_schur_obs<PCMAX><<<nob + nr, 64, sizeof(double) * 64 * P.wst, s>>>(
+                P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar);
+    }
 }
 void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,
                          const int *vobs, const int *vcoff, const double *J, const double *Lb,
@@ -4421,6 +4502,17 @@ void launch_unpermute(hipStream_t s, int M, const int *ref_of_dev, const int *ob
                       double *edo) {
     k_unpermute<<<nblk(M, 256), 256, 0, s>>>(M, ref_of_dev, obs_own, f2, eu2, ed, f2o, eu2o,
                                              edo);
+}
+void launch_handback_host(hipStream_t s, int Mg, int nrows, const int *dev_of_ref,
+                          const double *f2, const double *eu2, const double *ed, double *hf,
+                          double *heu, double *hed, const double *dec, const double *f2_trial) {
+    const int n = Mg + nrows;
+    if (n <= 0) return;
+    // PCIe, not the grid, bounds it: 512 workgroups keep ~100 KB of stores
+    // in flight and leave most wave slots to the kernels running beside it
+    // (2,048 held the statistics kernels behind it for ~50 us)
+    k_handback_host<<<std::min(nblk(n, 256), 512), 256, 0, s>>>(Mg, nrows, dev_of_ref, f2, eu2,
+                                                                 ed, hf, heu, hed, dec, f2_trial);
 }
 
 }  // namespace mmba

@@ -94,7 +94,10 @@ bool Plan::red_defer_ok() const {
     // the slots)
     if (nranks != 1 || b15 || nR <= 0) return false;
     if (nB_solved > 0) return !rs_bnd;
-    return band && bs.use_bd && nG > 0;
+    // nG == 0: the one-launch block-diagonal solve carries them (k_bd_direct's
+    // extra workgroups); a damped solve without a norm slot takes the general
+    // path, whose k_schur_init does
+    return band && bs.use_bd && (nG > 0 || path_choice(MMBA_PATH_RED_BD) != 0);
 }
 
 void Plan::flush_red() {
@@ -529,7 +532,7 @@ void Plan::jac(const double *dx, const JacLM *lm) {
 // Trial point x + p, p = -xs (lmder): one parameter pass (step, norms,
 // setParameters), measureErrors, ||J p||, one reduction launch.
 void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnorm,
-                         const LmDec *dec) {
+                         const LmDec *dec, bool jac_ahead) {
     flush_red();
     const double t0 = wall_now();
     double *pr = d_partial + 3 * (size_t)pw;  // rows 3..6 (0..2: jac epilogue)
@@ -629,9 +632,19 @@ void Plan::trial_enqueue(double *eu, double *ed, bool with_dnorm, bool fill_dnor
     if (b15)  // ||J p||^2 of J = J_s + f c^T (no host mirror on these plans; rotated basis)
         launch_b15_jp(s, n, d_xs15r, d_g, d_c15r, d_b15k + 4, d_scalar + SL_JP);
     mirror_pending = mirror;
-    if (dec) {  // the next Jacobian's first launch, gated on the device's decision
+    pre_hb_enq = dec && pre_hb_on && !b15;
+    if (pre_hb_enq)  // (the previous trial's kernel precedes it on s_hb[0]: no wait)
+        MMBA_HIP(hipEventRecord(ev_hb[3], s));
+    if (dec && jac_ahead) {  // the next Jacobian's first launch, gated on the device's decision
         stage_slots();
         pre_jac_enqueue(d_wa2, eu, ed);
+    }
+    if (pre_hb_enq) {  // behind the decision, beside the gated Jacobian
+        MMBA_HIP(hipStreamWaitEvent(s_hb[0], ev_hb[3], 0));
+        launch_handback_host(s_hb[0], Mg, nrows, d_dev_of_ref, d_f, eu, ed, pre_hb_map[0],
+                             pre_hb_map[1], pre_hb_map[2], d_scalar + SL_DGO, d_ftrial);
+        hb_used[0] = true;
+        hb_pending = true;
     }
     // [PNORM, XN2T, FNORM, JP] (+ [DNORM, FAIL] of the undamped solve)
     allreduce(d_scalar + SL_PNORM, with_dnorm ? 6 : 4);
@@ -685,7 +698,8 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         // the whole damped solve, ||D xs||^2 and the flag in one launch
         span_begin(SPAN_CHOL);
         bd_direct(s, P, bs.bd, d_Acc, d_g, d_diag, lam, d_xR, d_xs, d_fail, d_scalar, dnorm_slot,
-                  SL_FAIL);
+                  SL_FAIL, pend_red ? &pend_rs : nullptr, d_partial);
+        pend_red = false;
         span_end(SPAN_CHOL);
         t_linear += wall_now() - t0;
         return;
@@ -1068,6 +1082,22 @@ void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const dou
         handback_sharded(nullptr, nullptr, f_out, eu_out, ed_out, d_f2, d_eu2, d_ed1);
         return;
     }
+    handback_wait();  // (a hand-back an exception left in flight still reads d_gather)
+    handback_streams();
+    // page-locked caller lists (hipHostMalloc / hipHostRegister, 16-B
+    // aligned): one kernel stores them in reference order through their
+    // host-mapped addresses, on its own stream beside whatever follows on s
+    double *hmap[3] = {nullptr, nullptr, nullptr};
+    if (map_outputs(f_out, eu_out, ed_out, hmap)) {
+        MMBA_HIP(hipEventRecord(ev_hb[3], s));
+        MMBA_HIP(hipStreamWaitEvent(s_hb[0], ev_hb[3], 0));
+        launch_handback_host(s_hb[0], Mg, nrows, d_dev_of_ref, d_f2, d_eu2, d_ed1, hmap[0],
+                             hmap[1], hmap[2]);
+        hb_used[0] = true;
+        hb_pending = true;
+        if (sync) handback_wait();
+        return;
+    }
     double *tf = d_gather, *te = d_gather + mg, *td = d_gather + 2 * (size_t)mg;
     const size_t total = 2 * (size_t)mg + Mg;
     if (nranks > 1) MMBA_HIP(hipMemsetAsync(d_gather, 0, sizeof(double) * total, s));
@@ -1082,12 +1112,61 @@ void Plan::download_ref_order(const double *d_f2, const double *d_eu2, const dou
             MMBA_HIP(hipMemcpyAsync(te + 2 * (size_t)Mg, d_eu2 + 2 * (size_t)M,
                                     sizeof(double) * nrows, hipMemcpyDeviceToDevice, s));
     }
-    if (f_out) MMBA_HIP(hipMemcpyAsync(f_out, tf, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
-    if (eu_out)
-        MMBA_HIP(hipMemcpyAsync(eu_out, te, sizeof(double) * mg, hipMemcpyDeviceToHost, s));
-    if (ed_out)
-        MMBA_HIP(hipMemcpyAsync(ed_out, td, sizeof(double) * Mg, hipMemcpyDeviceToHost, s));
-    if (sync) stream_wait();
+    // the three lists on three streams (measured on C2's 8 MB: one stream
+    // runs the copies back to back with ~9 us between them; tools/ubench/d2h)
+    MMBA_HIP(hipEventRecord(ev_hb[3], s));
+    double *dst[3] = {f_out, eu_out, ed_out};
+    const double *src[3] = {tf, te, td};
+    const size_t cnt[3] = {(size_t)mg, (size_t)mg, (size_t)Mg};
+    for (int k = 0; k < 3; ++k) {
+        if (!dst[k]) continue;
+        MMBA_HIP(hipStreamWaitEvent(s_hb[k], ev_hb[3], 0));
+        MMBA_HIP(hipMemcpyAsync(dst[k], src[k], sizeof(double) * cnt[k], hipMemcpyDeviceToHost,
+                                s_hb[k]));
+        hb_used[k] = true;
+    }
+    hb_pending = true;
+    if (sync) handback_wait();
+}
+
+void Plan::handback_streams() {
+    if (s_hb[0]) return;
+    for (hipStream_t &c : s_hb) MMBA_HIP(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    for (hipEvent_t &e : ev_hb) MMBA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+}
+
+bool Plan::map_outputs(double *f_out, double *eu_out, double *ed_out, double *hmap[3]) {
+    if (!d_dev_of_ref || path_choice(MMBA_PATH_HANDBACK_DMA) == 1) return false;
+    double *outs3[3] = {f_out, eu_out, ed_out};
+    for (int k = 0; k < 3; ++k) {
+        hmap[k] = nullptr;
+        if (!outs3[k]) continue;
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, outs3[k]) != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory: not an error of the solve
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost || !a.devicePointer ||
+            (k < 2 && ((uintptr_t)a.devicePointer & 15u)))
+            return false;
+        hmap[k] = static_cast<double *>(a.devicePointer);
+    }
+    return true;
+}
+
+// The hand-back's copies done (polled events: a blocking synchronisation's
+// wake-up costs tens of microseconds).
+void Plan::handback_wait() {
+    if (!hb_pending) return;
+    hb_pending = false;
+    for (int k = 0; k < 3; ++k)
+        if (hb_used[k]) MMBA_HIP(hipEventRecord(ev_hb[k], s_hb[k]));
+    for (int k = 0; k < 3; ++k)
+        for (; hb_used[k];) {
+            const hipError_t e = hipEventQuery(ev_hb[k]);
+            if (e == hipSuccess) hb_used[k] = false;
+            else if (e != hipErrorNotReady) MMBA_HIP(e);
+        }
 }
 
 // Parameter vector of the solve on the host (sharded: owners' entries summed).
@@ -1381,8 +1460,14 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
     const double t_start = wall_now();
     t_func = t_jac = t_linear = 0.;
     cbk = cb;
+    pre_hb_enq = false;
+    pre_hb_on = nranks == 1 && n > 0 && pre_jac && (fvec_out || eu_out || ed_out) &&
+                path_choice(MMBA_PATH_PRE_HANDBACK) != 0 &&
+                map_outputs(fvec_out, eu_out, ed_out, pre_hb_map);
+    if (pre_hb_on) handback_streams();
     mmba_result r;
     std::memset(&r, 0, sizeof(r));
+    bool post_trial_end = false;  // ended by the tests after a trial (lm_decide's info)
     if (trace) trace->count = 0;
     auto push_trace = [&](double fn) {
         if (trace) {
@@ -1542,8 +1627,11 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
             // the next Jacobian is enqueued behind the trial, gated on the
             // device's restatement of the decision the host takes below
             const bool pj = pre_jac_ok();
+            // the device's restatement of the decision: for the Jacobian
+            // enqueued ahead (pj) and for the speculative hand-back
+            const bool dv = pj || pre_hb_on;
             LmDec dec;
-            if (pj) {
+            if (dv) {
                 dec.spec = 1;
                 dec.first = iter == 1;
                 dec.f0 = f0_pending;
@@ -1559,7 +1647,8 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                 dec.xtol = xtol;
                 dec.gtol = gtol;
             }
-            if (spec) trial_enqueue(d_eu_s, d_ed_s, nranks > 1, by_trial, pj ? &dec : nullptr);
+            if (spec)
+                trial_enqueue(d_eu_s, d_ed_s, nranks > 1, by_trial, dv ? &dec : nullptr, pj);
             {
                 const double t0 = wall_now();
                 read_slots(0, SL_LAST);
@@ -1604,7 +1693,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                 } else {
                     settle_pre(false);  // a speculative trial lmpar did not take
                     LmDec dec2;
-                    if (pj) {
+                    if (dv) {
                         dec2.spec = 0;
                         dec2.first = iter == 1;
                         dec2.fnorm = fnorm;
@@ -1621,7 +1710,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                     }
                     // trial point: ||D p||, f(x + p), ||J p|| and the
                     // candidate ||D x_new|| -- one synchronisation
-                    trial_enqueue(d_eu, d_ed, false, false, pj ? &dec2 : nullptr);
+                    trial_enqueue(d_eu, d_ed, false, false, dv ? &dec2 : nullptr, pj);
                     const double t0 = wall_now();
                     read_slots(0, SL_LAST);
                     t_func += wall_now() - t0;
@@ -1669,6 +1758,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                     info = 3;
                 if (info != 0) {
                     settle_pre(false);
+                    post_trial_end = true;
                     goto TERMINATE;
                 }
                 if (nfev >= maxfev) info = 5;
@@ -1677,6 +1767,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
                 if (gnorm <= epsmch) info = 8;
                 if (info != 0) {
                     settle_pre(false);
+                    post_trial_end = true;
                     goto TERMINATE;
                 }
                 settle_pre(ratio >= p0001);
@@ -1707,20 +1798,25 @@ TERMINATE:
             fun(d_x, d_ftrial, d_J, d_J + m, d_dist_x);  // scratch user buffers
         }
         // compute_error_stats (B13: the last measured distances), the RMS
-        // and x: one synchronisation
+        // and x: one synchronisation.  Unsharded, the output lists' unpermute
+        // and copies go first: the copies (their own streams) run beside the
+        // statistics kernels
+        const bool staged = nranks == 1 && n > 0;
+        const bool outs = fvec_out || eu_out || ed_out;
+        // the speculative hand-back behind the last trial stored the lists
+        // (the device decided the solve ends there: its info slot, mirrored)
+        const bool dev_handed = post_trial_end && pre_hb_enq && h_scalar[SL_DGO + 4] > 0.;
+        if (dev_handed) ++pre_handbacks;
+        if (staged && outs && !dev_handed)
+            download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out, false);
         error_stats_enqueue(d_ed);
         launch_sumsq(s, d_dist_x, nullptr, M, d_partial + 3 * (size_t)pw, nparts,
                      d_scalar + SL_RMS, P.obs_own);
         allreduce(d_scalar + SL_RMS, 1);
-        const bool staged = nranks == 1 && n > 0;
-        const bool outs = fvec_out || eu_out || ed_out;
-        if (staged) {
-            // x, the reordered outputs and the slots: every copy enqueued, then
-            // one wait (read_slots' event follows them on the stream)
+        if (staged)  // x and the slots: one wait (read_slots' event follows the copy)
             MMBA_HIP(hipMemcpyAsync(h_xstage, d_x, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-            if (outs) download_ref_order(d_f, d_eu, d_ed, fvec_out, eu_out, ed_out, false);
-        }
         read_slots(SL_RMS, SL_IEMAX);  // also x0's ||f|| and the initial measurement's
+        handback_wait();
         if (f0_pending) {  // stopped between x0's evaluation and the first decision
             fnorm = std::sqrt(h_scalar[SL_F0]);
             push_trace(fnorm);

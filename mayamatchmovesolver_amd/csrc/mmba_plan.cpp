@@ -119,6 +119,13 @@ Plan::~Plan() {
     }
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (ev_sync) (void)hipEventDestroy(ev_sync);
+    if (hb_pending)
+        for (hipStream_t c : s_hb)
+            if (c) (void)hipStreamSynchronize(c);
+    for (hipEvent_t e : ev_hb)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t c : s_hb)
+        if (c) (void)hipStreamDestroy(c);
     for (void *p : allocs) (void)hipFree(p);
     if (h_scalar) (void)hipHostFree(h_scalar);
     if (h_fail) (void)hipHostFree(h_fail);
@@ -619,7 +626,9 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     nCF = 0;
     for (int cf = 0; cf < ncf; ++cf) {
         cf_pc[cf] = (int)cf_params[cf].size();
-        if (cf_pc[cf] > PCMAX) throw Unsupported{"more than 10 parameters on one camera-frame"};
+        if (cf_pc[cf] > PCMAX)
+            throw Unsupported{"more than " + std::to_string(PCMAX) +
+                              " parameters on one camera-frame"};
         cf_roff[cf] = nCF;
         for (int a = 0; a < cf_pc[cf]; ++a) p_pos[cf_params[cf][a]] = nCF + a;
         nCF += cf_pc[cf];
@@ -629,7 +638,8 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     for (int p = 0; p < n; ++p)
         if (p_class[p] == PC_G) g_param.push_back(p);
     nG = (int)g_param.size();
-    if (nG > NGMAX) throw Unsupported{"more than 32 global parameters"};
+    if (nG > NGMAX)
+        throw Unsupported{"more than " + std::to_string(NGMAX) + " global parameters"};
     for (int q = 0; q < nG; ++q) p_pos[g_param[q]] = nCF + q;
     nR = nCF + nG;
 
@@ -1524,6 +1534,11 @@ void Plan::build(const mmba_problem *pr, const mmba_options *o) {
     d_var_cf = upload(var_cf);
     d_stale = upload(stale);
     d_ref_of_dev = upload(ref_of_dev);
+    if (nranks == 1 && M > 0) {  // the host-mapped hand-back gathers in reference order
+        std::vector<int> dev_of_ref(M, 0);
+        for (int i = 0; i < M; ++i) dev_of_ref[ref_of_dev[i]] = i;
+        d_dev_of_ref = upload(dev_of_ref);
+    }
     d_slot = upload(slot);
     d_rows = upload(panel_rows);
     d_cols = upload(panel_cols);
@@ -1898,7 +1913,9 @@ void Plan::setup_band(int Pforce) {
         // shards all-reduce S instead and each runs the log-depth solve on
         // it; MMBA_PATH_SHARD_BCR = 0 keeps the partitioned chain (tests)
         const bool shard_ok = nranks == 1 || path_choice(MMBA_PATH_SHARD_BCR) != 0;
-        if (shard_ok && w <= 32 && Pforce <= 0 && !sep_form(w)) {
+        // the root (block 0 + the arrow corner) is one wave: K + nG <= 64
+        const bool root_fits = std::max(8, (w + 7) / 8 * 8) + (nG + 7) / 8 * 8 <= 64;
+        if (shard_ok && w <= 32 && Pforce <= 0 && !sep_form(w) && root_fits) {
             bs.use_bcr = true;
             bs.P = 1;
             bs.comm = nranks > 1 ? comm : nullptr;
@@ -2020,9 +2037,17 @@ void Plan::setup_band(int Pforce) {
     }
     // partitions per shard range [Ra_all[k], Rb_all[k]) (one range unsharded)
     const bool sepf = sep_form(w);
+    // the partitioned chain's windows carry arrows up to NGPART wide; a wider
+    // arrow factors the band as one partition (sharded: refused -- block
+    // cyclic reduction takes sharded arrows up to 64 - K)
+    const bool one_part = !sepf && nG > NGPART;
+    if (one_part && Ra_all.size() > 1)
+        throw Unsupported{"more than " + std::to_string(NGPART) +
+                          " global parameters on a sharded band plan"};
     auto count_parts = [&](int len) {
         int P = 1;
-        if (sepf) {
+        if (one_part) {
+        } else if (sepf) {
             // separator form: the shard's range is one partition
         } else if (Pforce > 0 && w <= WBAND_PART) {
             P = std::max(1, std::min(Pforce, len / (w + 1)));

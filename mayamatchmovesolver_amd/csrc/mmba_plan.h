@@ -204,6 +204,7 @@ struct Plan {
     bool narrow = false;
     int *d_rows_off = nullptr, *d_cols_off = nullptr;
     int *d_var_cf = nullptr, *d_stale = nullptr, *d_ref_of_dev = nullptr;
+    int *d_dev_of_ref = nullptr;  // unsharded: the inverse permutation
     double *d_attr0 = nullptr;
     size_t attr_bytes = 0;
 
@@ -452,7 +453,7 @@ struct Plan {
     // fill_dnorm: this trial's ||D p||^2 also fills SL_DNORM and the fail
     // flag SL_FAIL of the undamped solve enqueued with dnorm_by_trial
     void trial_enqueue(double *eu, double *ed, bool with_dnorm = false, bool fill_dnorm = false,
-                       const LmDec *dec = nullptr);
+                       const LmDec *dec = nullptr, bool jac_ahead = false);
     // The next Jacobian's first launch (k_jac_ne_u at the trial point),
     // enqueued behind a trial whose reduction restates the host's decision
     // (LmDec): it runs only when that decision takes the trial and goes on,
@@ -571,6 +572,27 @@ struct Plan {
     // next wait covers them
     void download_ref_order(const double *d_f2, const double *d_eu2, const double *d_ed1,
                             double *f_out, double *eu_out, double *ed_out, bool sync = true);
+    // unsharded hand-back: each output list's device-to-host copy on its own
+    // stream (its own DMA queue) behind the unpermute, so the three copies
+    // run together and beside the kernels enqueued after them on s;
+    // handback_wait() polls their events
+    hipStream_t s_hb[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_hb[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool hb_pending = false;
+    bool hb_used[3] = {false, false, false};
+    void handback_wait();
+    void handback_streams();
+    // host-mapped addresses of page-locked caller lists (all non-null lists
+    // mapped and 16-B aligned, else false)
+    bool map_outputs(double *f_out, double *eu_out, double *ed_out, double *hmap[3]);
+    // speculative hand-back (unsharded solves into page-locked lists): every
+    // trial enqueued with the device's decision also enqueues k_handback_host
+    // gated on it, so the lists leave as soon as the device has decided the
+    // solve ends there; the host skips its own hand-back when it ends on
+    // that trial and the device's slots say the kernel stored them
+    bool pre_hb_on = false, pre_hb_enq = false;
+    long long pre_handbacks = 0;  // solves whose lists the speculative hand-back stored
+    double *pre_hb_map[3] = {nullptr, nullptr, nullptr};
 };
 
 }  // namespace mmba

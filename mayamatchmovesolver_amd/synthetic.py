@@ -423,7 +423,7 @@ def _config_c1(rng, F):
 
 def _bulk_problem(F, cams_t, cams_r, cams_focal, cam_solve, bnd_init, bnd_solved, mkr_cam,
                   mkr_bnd, obs_m, obs_f, obs_xy, lens=None, gauge_cam0=False,
-                  lens_first=False, meta=None):
+                  lens_first=False, meta=None, cams_offset=None):
     """Vectorised problem assembly (same semantics as SceneBuilder.build)."""
     b = SceneBuilder(F)
     lens_ids = []
@@ -445,6 +445,7 @@ def _bulk_problem(F, cams_t, cams_r, cams_focal, cam_solve, bnd_init, bnd_solved
         tfm, tids = b.transform(t=[cams_t[c][:, 0], cams_t[c][:, 1], cams_t[c][:, 2]],
                                 r=[cams_r[c][:, 0], cams_r[c][:, 1], cams_r[c][:, 2]])
         _, cids = b.camera(tfm, focal=cams_focal[c], film_back=(FILM_W_IN, FILM_H_IN),
+                           film_offset=(0.0, 0.0) if cams_offset is None else cams_offset[c],
                            render_size=RENDER, lens=lens_idx)
         cam_attr_ids.append((tids, cids))
     bnd_attr_ids = []
@@ -724,6 +725,12 @@ def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0, n_cams=
         lens = {"init": (0.0, 1.0, 0.0, 0.0, 0.0), "solve_slots": (0, 4)}
         if lens_model == "classic_animated":  # distortion keyed per frame (F params)
             lens["init"] = (np.zeros(F),) + lens["init"][1:]
+        elif lens_model == "classic_wide":
+            # all five classic coefficients keyed per frame and solved, with the
+            # camera's focal length: 6 + 1 + 5 = 12 parameters on each
+            # camera-frame of a one-camera shot
+            lens["init"] = (np.zeros(F), np.ones(F), np.zeros(F), np.zeros(F), np.zeros(F))
+            lens["solve_slots"] = (0, 1, 2, 3, 4)
 
     def proj(ks, fs):
         mx = np.empty(ks.size)
@@ -752,9 +759,16 @@ def _config_c5(rng, F, scale, lens_model="classic", rolling_shutter=0.0, n_cams=
     ks, fs, xy = _obs_from_windows(rng, start, length, proj)
     t0 = [tc + rng.uniform(-0.05, 0.05, size=tc.shape) for tc in ts]
     r0 = [rc + rng.uniform(-2.0, 2.0, size=rc.shape) for rc in rs]
-    prob = _bulk_problem(F, t0, r0, [FOCAL_MM] * n_cams, lambda tids, cids: list(tids[:6]),
+    wide = lens_model == "classic_wide"
+    focal0 = [FOCAL_MM * (1.0 + rng.uniform(-0.01, 0.01, F)) if wide else FOCAL_MM
+              for _ in range(n_cams)]
+    offset0 = None
+
+    def cam_solve(tids, cids):
+        return list(tids[:6]) + ([cids[abi.CAM_FOCAL_MM]] if wide else [])
+    prob = _bulk_problem(F, t0, r0, focal0, cam_solve,
                          P, np.zeros(B, bool), mkr_cam, mkr_bnd, ks, fs, xy, lens=lens,
-                         lens_first=True,
+                         lens_first=True, cams_offset=offset0,
                          meta={"name": CONFIG_NAMES[4] + ("" if lens_model == "classic"
                                                           else "_" + lens_model) +
                                ("" if n_cams == 2 else "_%dcam" % n_cams) +
@@ -1088,7 +1102,8 @@ def b4_grouped_twin(prob: Problem) -> Problem:
 
 
 def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal=3,
-                  extra_globals=0, window=None, lens=None, seed=17) -> Problem:
+                  extra_globals=0, window=None, lens=None, wide_block=False,
+                  seed=17) -> Problem:
     """Witness-camera rig with a wide arrow of global parameters: a fixed
     static reference camera 0, ``n_witness`` static witness cameras whose
     poses are solved as static (global) parameters (witness 1: rotation
@@ -1103,7 +1118,12 @@ def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal
     reduced system instead of a dense one).  ``lens="anamorphic"``: every
     camera shares one 3DE anamorphic deg 4 lens whose ten polynomial
     coefficients are solved (created and solved first: B3), so a witness
-    observation reaches more than 20 parameters.  Markers camera-major (B4)."""
+    observation reaches more than 20 parameters.  ``wide_block``: the animated
+    camera also solves its focal length and film offsets per frame and has
+    its own 3DE classic lens whose distortion and x / y curvature are keyed
+    per frame -- 6 + 3 + 3 = 12 parameters on each of its camera-frames (the
+    lens coefficients join the block: one camera reads them, Plan::build).
+    Markers camera-major (B4)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     F = int(frames)
     b = SceneBuilder(F)
@@ -1152,8 +1172,20 @@ def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal
     ra0 = ra + rng.uniform(-1.0, 1.0, size=ra.shape)
     tfm, aids = b.transform(t=tuple(ta0[:, k] for k in range(3)),
                             r=tuple(ra0[:, k] for k in range(3)))
-    cam, _ = b.camera(tfm, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
-                      render_size=RENDER, lens=lens_idx)
+    block_ids = []
+    if wide_block:
+        wl, wlids = b.lens_3de_classic(distortion=np.full(F, 0.01), curvature_x=np.full(F, -0.01),
+                                       curvature_y=np.full(F, 0.01))
+        cam, acids = b.camera(tfm, focal=FOCAL_MM * (1.0 + rng.uniform(-0.02, 0.02, F)),
+                              film_back=(FILM_W_IN, FILM_H_IN),
+                              film_offset=(rng.uniform(-0.01, 0.01, F), rng.uniform(-0.01, 0.01, F)),
+                              render_size=RENDER, lens=wl)
+        block_ids = [acids[abi.CAM_FOCAL_MM], acids[abi.CAM_FILM_OFFSET_X_INCH],
+                     acids[abi.CAM_FILM_OFFSET_Y_INCH]]
+        lens_solve = [wlids[0], wlids[2], wlids[3]] + lens_solve  # lens first (B3)
+    else:
+        cam, _ = b.camera(tfm, focal=FOCAL_MM, film_back=(FILM_W_IN, FILM_H_IN),
+                          render_size=RENDER, lens=lens_idx)
     views.append((cam, ta, ra, FOCAL_MM))
     P0 = P * (1.0 + rng.uniform(-0.04, 0.04, size=(B, 1))) if solve_bundles else P
     bids = []
@@ -1177,7 +1209,7 @@ def witness_scene(n_witness=4, frames=6, bundles=24, solve_bundles=True, n_focal
             b.marker(cam, j, _noisy(rng, xy[j]), enable=en)
     for a in lens_solve + solve_ids:
         b.solve(a)
-    for a in aids[0:6]:
+    for a in list(aids[0:6]) + block_ids:
         b.solve(a)
     if solve_bundles:
         for j in range(B):

@@ -69,7 +69,7 @@ def test_struct_layouts_match_header():
 
 
 def test_host_helpers(L, oracle):
-    assert L.mmba_abi_version() == abi.ABI_VERSION == 9
+    assert L.mmba_abi_version() == abi.ABI_VERSION == 10
     o = abi.MmbaOptions()
     L.mmba_options_default(C.byref(o), abi.SOLVER_TYPE_CMINPACK_LMDER)
     assert (o.iter_max, o.tau, o.eps1, o.delta, o.auto_param_scale, o.image_width) == \

@@ -6,7 +6,7 @@ column (adjust_solveFunc.cpp frameIndexEnable) and clones the lens per frame
 an animated lens coefficient whose lens instances at its frame are read by
 one camera reaches the rows of ONE camera-frame: the plan puts it in that
 camera-frame's block (Plan::build, VF_LENS) instead of the global arrow,
-where more than NGMAX = 32 animated frames were refused.  Pinned here: the
+where more than NGMAX animated frames (32 then, 48 since round 6) were refused.  Pinned here: the
 residuals and the FD Jacobian against the oracle on a one-camera shot with
 its distortion animated over 36 frames, the refusal that remains with the
 classification pinned off, and (tests/test_gpu_golden.py,
@@ -48,12 +48,12 @@ def test_animated_lens_over_ngmax_residuals_and_jacobian(oracle, gpu_ctx):
 
 def test_animated_lens_as_globals_refused(gpu_ctx, paths):
     """With the classification pinned off every animated coefficient is a
-    global parameter: 36 + 1 > NGMAX, refused as before round 5."""
+    global parameter: 50 + 1 > NGMAX (48), refused as before round 5."""
     paths(abi.PATH_LENS_CF, 0)
-    prob = scene()
+    prob = scene(frames=50)
     with pytest.raises(MmbaError) as e:
         Solver(prob, S.config_options(prob), context=gpu_ctx).close()
-    assert "32 global" in str(e.value)
+    assert "48 global" in str(e.value)
 
 
 def test_shared_lens_stays_global(oracle, gpu_ctx):

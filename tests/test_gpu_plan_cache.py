@@ -49,25 +49,52 @@ def test_set_attr_values_equals_fresh_plan(cfg, kw):
     assert cached.result["error_initial_avg"] == fresh.result["error_initial_avg"]
 
 
-def test_solve_into_page_locked_buffers(gpu_ctx):
+@pytest.mark.parametrize("scene", ["c3", "c2", "rows"])
+@pytest.mark.parametrize("dma", [0, 1])
+def test_solve_into_page_locked_buffers(scene, dma, gpu_ctx, paths):
     """Output buffers in page-locked host memory (mmba_host_alloc, as bench.py
     and a caching caller keep them) receive the same bits as ordinary numpy
-    arrays, solve after solve."""
-    from mayamatchmovesolver_amd import synthetic as S
-    from mayamatchmovesolver_amd.solver import Solver, host_array
+    arrays, solve after solve: through k_handback_host's host-mapped stores
+    (default) and through the per-list DMA copies (PATH_HANDBACK_DMA=1);
+    "rows": stiffness / smoothness rows after the observations."""
+    from mayamatchmovesolver_amd import abi, make_options
+    from mayamatchmovesolver_amd.solver import host_array
 
-    prob = S.make_config(3, frames=12, scale=0.002)
-    opt = S.config_options(prob)
+    paths(abi.PATH_HANDBACK_DMA, dma)
+    if scene == "rows":
+        prob = S.edge_scene(stiffness=True)
+        opt = make_options(scene_graph_mode=abi.SCENE_GRAPH_MODE_MAYA_DAG, iterations=40)
+        assert prob.num_residuals > 2 * prob.num_obs
+    else:
+        prob = S.make_config(3 if scene == "c3" else 1, frames=12, scale=0.002)
+        opt = S.config_options(prob)
     s = Solver(prob, opt, context=gpu_ctx)
     try:
         m, M = prob.num_residuals, prob.num_obs
         ref = s.solve(out=(np.zeros(m), np.zeros(m), np.zeros(M)))
         pin = (host_array(m), host_array(m), host_array(M))
+        pre0 = s.kernel_stats()["pre_handbacks"]
         for _ in range(2):
+            for a in pin:
+                a[:] = np.nan  # every entry rewritten by the hand-back
             got = s.solve(out=pin)
             np.testing.assert_array_equal(got.x, ref.x)
             np.testing.assert_array_equal(pin[0], ref.fvec)
             np.testing.assert_array_equal(pin[1], ref.err_user)
             np.testing.assert_array_equal(pin[2], ref.err_dist)
+        pre = s.kernel_stats()["pre_handbacks"] - pre0
+        if dma:
+            assert pre == 0
+        elif ref.result["reason_number"] in (1, 2, 3, 5, 6, 7, 8):
+            # ended by the tests after a trial: the speculative hand-back
+            # behind it stored the lists
+            assert pre == 2
+        # the on-demand fetch of a solve(fetch=False) into the same buffers
+        s.solve(fetch=False)
+        for a in pin:
+            a[:] = np.nan
+        s.outputs(out=pin)
+        np.testing.assert_array_equal(pin[0], ref.fvec)
+        np.testing.assert_array_equal(pin[2], ref.err_dist)
     finally:
         s.close()

@@ -11,6 +11,7 @@
 #   prof              rocprofv3 --kernel-trace --stats of the default bench
 #   pmc               FETCH_SIZE / WRITE_SIZE passes of the default bench
 #   sqpmc             one pass of 8 SQ counters (wave cycles, waits, VALU) on the default bench
+#   cfgpmc:I          FETCH_SIZE / WRITE_SIZE / SQ passes of configs[I]
 #   iter              kernel traces + one-iteration timelines of C2 / C4 / C5
 #   ubench            tools/ubench dgemm_probe (C3 update shapes) and pcr_probe (C4 system)
 set -o pipefail
@@ -66,6 +67,14 @@ for step in "$@"; do
     sqpmc)
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/sqpmc" -o c4 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/sqpmc.json" 2> "$OUT/sqpmc.err" || { tail "$OUT/sqpmc.err"; exit 1; }
       python3 tools/pmc_summary.py "$OUT/sqpmc" > "$OUT/sqpmc_summary.txt" && cat "$OUT/sqpmc_summary.txt" ;;
+    cfgpmc:*)
+      # FETCH_SIZE, WRITE_SIZE and the SQ pass on configs[I] (one solve each)
+      c=${step#cfgpmc:}
+      for ctr in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"; do
+        tag=${ctr%% *}
+        timeout -s KILL 120 rocprofv3 --pmc $ctr -d "$OUT/c${c}_$tag" -o c$c --output-format csv -- python3 bench.py --config $c --steps 1 --warmup 0 --no-cpu-baseline --no-traffic > "$OUT/c${c}_$tag.json" 2> "$OUT/c${c}_$tag.err" || { tail "$OUT/c${c}_$tag.err"; exit 1; }
+        python3 tools/pmc_summary.py "$OUT/c${c}_$tag" > "$OUT/c${c}_${tag}_summary.txt" && head -14 "$OUT/c${c}_${tag}_summary.txt"
+      done ;;
     ubench)
       timeout -k 10 120 tools/ubench/dgemm_probe > "$OUT/dgemm_probe.txt" 2>&1 || { cat "$OUT/dgemm_probe.txt"; exit 1; }
       timeout -k 10 120 tools/ubench/pcr_probe > "$OUT/pcr_probe.txt" 2>&1 || { cat "$OUT/pcr_probe.txt"; exit 1; }

@@ -11,6 +11,12 @@ acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         acc[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+if not any("SQ_WAVES" in c for c in acc.values()):
+    # other counters (FETCH_SIZE / WRITE_SIZE, KB per launch): per-kernel means
+    for k, c in sorted(acc.items(), key=lambda kc: -sum(sum(v) for v in kc[1].values())):
+        print("%-42s " % k[:42] + "  ".join("%s=%.1f (n=%d)" % (n, sum(v) / len(v), len(v))
+                                              for n, v in sorted(c.items())))
+    sys.exit(0)
 rows = []
 for k, c in acc.items():
     m = {n: sum(v) / len(v) for n, v in c.items()}
