@@ -696,11 +696,11 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
 #define MMBA_PATH_RED_BD 20        /* 0: the Jacobian epilogue's scalar reduction runs as its own
                                       launch on block-diagonal plans without globals (C2) instead
                                       of riding in the one-launch damped solve */
-#define MMBA_PATH_HANDBACK_DMA 21  /* 1: page-locked output lists come back by DMA copies (one
-                                      per list, on their own streams) instead of one kernel
-                                      storing them through their host-mapped addresses */
-#define MMBA_PATH_PRE_HANDBACK 22  /* 0: no speculative hand-back behind each decided trial (the
-                                      page-locked lists leave after the host's last decision) */
+#define MMBA_PATH_HANDBACK_DMA 21  /* 0: page-locked output lists come back through one kernel
+                                      storing them at their host-mapped addresses instead of
+                                      the DMA copies (one per list, on their own streams) */
+#define MMBA_PATH_PRE_HANDBACK 22  /* with the kernel hand-back (21 = 0), 0: no speculative
+                                      launch of it behind each decided trial */
 #define MMBA_PATH_NUM 23
 int mmba_debug_set_path(int key, int value);
 

@@ -4508,10 +4508,11 @@ void launch_handback_host(hipStream_t s, int Mg, int nrows, const int *dev_of_re
                           double *heu, double *hed, const double *dec, const double *f2_trial) {
     const int n = Mg + nrows;
     if (n <= 0) return;
-    // PCIe, not the grid, bounds it: 512 workgroups keep ~100 KB of stores
-    // in flight and leave most wave slots to the kernels running beside it
-    // (2,048 held the statistics kernels behind it for ~50 us)
-    k_handback_host<<<std::min(nblk(n, 256), 512), 256, 0, s>>>(Mg, nrows, dev_of_ref, f2, eu2,
+    // PCIe, not the grid, bounds it: 128 workgroups (half the CUs, one each)
+    // keep ~1 MB of stores in flight and leave the other CUs' memory pipes to
+    // the statistics kernels running beside it (2,048 / 512 held them behind
+    // its PCIe-bound stores for ~50 us)
+    k_handback_host<<<std::min(nblk(n, 256), 128), 256, 0, s>>>(Mg, nrows, dev_of_ref, f2, eu2,
                                                                  ed, hf, heu, hed, dec, f2_trial);
 }
 

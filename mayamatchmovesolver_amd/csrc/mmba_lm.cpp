@@ -1136,7 +1136,12 @@ void Plan::handback_streams() {
 }
 
 bool Plan::map_outputs(double *f_out, double *eu_out, double *ed_out, double *hmap[3]) {
-    if (!d_dev_of_ref || path_choice(MMBA_PATH_HANDBACK_DMA) == 1) return false;
+    // opt-in (MMBA_PATH_HANDBACK_DMA = 0): on C2 the three DMA copies on their
+    // own streams measured 6,498 / 6,513 LM it/s against 6,266 / 6,275 for the
+    // host-mapped stores with the speculative launch and 6,338 / 6,688 without
+    // it, on one box (profiles/r6_c2hb/) -- the stores' PCIe-bound waves slow
+    // the kernels beside them
+    if (!d_dev_of_ref || path_choice(MMBA_PATH_HANDBACK_DMA) != 0) return false;
     double *outs3[3] = {f_out, eu_out, ed_out};
     for (int k = 0; k < 3; ++k) {
         hmap[k] = nullptr;

@@ -54,8 +54,10 @@ def test_set_attr_values_equals_fresh_plan(cfg, kw):
 def test_solve_into_page_locked_buffers(scene, dma, gpu_ctx, paths):
     """Output buffers in page-locked host memory (mmba_host_alloc, as bench.py
     and a caching caller keep them) receive the same bits as ordinary numpy
-    arrays, solve after solve: through k_handback_host's host-mapped stores
-    (default) and through the per-list DMA copies (PATH_HANDBACK_DMA=1);
+    arrays, solve after solve: through the per-list DMA copies (the default,
+    PATH_HANDBACK_DMA=1 pinned) and through k_handback_host's host-mapped
+    stores with its speculative launch behind every decided trial
+    (PATH_HANDBACK_DMA=0);
     "rows": stiffness / smoothness rows after the observations."""
     from mayamatchmovesolver_amd import abi, make_options
     from mayamatchmovesolver_amd.solver import host_array
