@@ -66,6 +66,44 @@ __global__ void __launch_bounds__(256) k_read(const double *__restrict__ J, cons
     out[(size_t)L * 256 + threadIdx.x] = s;
 }
 
+// the same loop with its operands behind a 1 KB by-value argument block (the
+// library's kernels take DevProblem, 792 B, and NeEpi, 312 B, by value)
+struct BigArg {
+    double pad[128];
+    const double *J, *f;
+    size_t stride;
+    int ncf, per, NS;
+    double *out;
+};
+__global__ void __launch_bounds__(256) k_read_big(const BigArg a) {
+    const int L = blockIdx.x;
+    const int cf = L / a.NS, part = L % a.NS;
+    const int o0 = cf * a.per, o1 = o0 + a.per;
+    double acc[NT];
+#pragma unroll
+    for (int e = 0; e < NT; ++e) acc[e] = 0.;
+    for (int i = o0 + 256 * part + threadIdx.x; i < o1; i += 256 * a.NS) {
+        double jx[PC], jy[PC];
+#pragma unroll
+        for (int q = 0; q < PC; ++q) {
+            jx[q] = a.J[(2 * q) * a.stride + i];
+            jy[q] = a.J[(2 * q + 1) * a.stride + i];
+        }
+        const double fx = a.f[2 * i], fy = a.f[2 * i + 1];
+        int e = 0;
+#pragma unroll
+        for (int q = 0; q < PC; ++q)
+#pragma unroll
+            for (int c = q; c < PC; ++c) acc[e++] += jx[q] * jx[c] + jy[q] * jy[c];
+#pragma unroll
+        for (int q = 0; q < PC; ++q) acc[NCC + q] += jx[q] * fx + jy[q] * fy;
+    }
+    double s = 0.;
+#pragma unroll
+    for (int e = 0; e < NT; ++e) s += acc[e] * (e + 1);
+    a.out[(size_t)L * 256 + threadIdx.x] = s;
+}
+
 __global__ void k_sum(const double2 *__restrict__ a, size_t n2, double *out) {
     double s = 0.;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x) {
@@ -124,6 +162,29 @@ int main() {
             if (r == reps + 1) printf("  (producer %.2f us)\n", 1e3 * mw);
         }
         printf("afterw col NS=%2d  %7.2f us  %6.2f TB/s\n", NS, 1e3 * tsum / reps, bytes / (1e3 * tsum / reps) / 1e6);
+    }
+    {  // by-value 1 KB argument block, warm, after the producer
+        BigArg ba{};
+        ba.J = J; ba.f = f; ba.stride = M; ba.ncf = ncf; ba.per = per; ba.NS = 4; ba.out = out;
+        double tsum = 0., tsmall = 0.;
+        const int reps = 20;
+        hipEvent_t em;
+        CK(hipEventCreate(&em));
+        for (int r = 0; r < reps + 2; ++r) {
+            k_writeJ<<<(M + 255) / 256, 256>>>(J, M, M, 16);
+            CK(hipEventRecord(e0));
+            k_read_big<<<ncf * 4, 256>>>(ba);
+            CK(hipEventRecord(em));
+            k_read<0><<<ncf * 4, 256>>>(J, f, M, ncf, per, 4, out);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float mb, ms;
+            CK(hipEventElapsedTime(&mb, e0, em));
+            CK(hipEventElapsedTime(&ms, em, e1));
+            if (r >= 2) { tsum += mb; tsmall += ms; }
+        }
+        printf("bigarg NS=4  %7.2f us (small-argument kernel right after it: %7.2f us)\n",
+               1e3 * tsum / reps, 1e3 * tsmall / reps);
     }
     for (int cold = 0; cold < 2; ++cold) {
         for (int lay = 0; lay < 4; ++lay) {
