@@ -701,7 +701,9 @@ int mmba_plan_kernel_stats(mmba_plan *plan, int enable_timing,
                                       the DMA copies (one per list, on their own streams) */
 #define MMBA_PATH_PRE_HANDBACK 22  /* with the kernel hand-back (21 = 0), 0: no speculative
                                       launch of it behind each decided trial */
-#define MMBA_PATH_NUM 23
+#define MMBA_PATH_PRE_SCHUR 23     /* 1: the next damped solve's k_schur_obs is enqueued with the
+                                      gated Jacobian ahead of the host's decision */
+#define MMBA_PATH_NUM 24
 int mmba_debug_set_path(int key, int value);
 
 /* Test hook (not part of the solver seam): solve S x = r with the device

@@ -47,7 +47,8 @@ PATH_NE_CF_SPLIT = 19
 PATH_RED_BD = 20
 PATH_HANDBACK_DMA = 21
 PATH_PRE_HANDBACK = 22
-PATH_NUM = 23
+PATH_PRE_SCHUR = 23
+PATH_NUM = 24
 
 FILM_FIT_FILL = 0
 FILM_FIT_HORIZONTAL = 1

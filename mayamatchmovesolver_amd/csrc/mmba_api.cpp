@@ -18,9 +18,9 @@ namespace mmba {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 
-static_assert(MMBA_PATH_NUM == 23, "one initialiser per path key");
+static_assert(MMBA_PATH_NUM == 24, "one initialiser per path key");
 static std::atomic<int> g_path[MMBA_PATH_NUM] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
-                                                 -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                                                 -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 int path_choice(int key) {
     return (key > 0 && key < MMBA_PATH_NUM) ? g_path[key].load() : -1;
 }

@@ -226,7 +226,7 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
                           double *Lb, double *tb, double *Wg, int *fail);
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
                       double *W, const RedSpec *red = nullptr, const double *partial = nullptr,
-                      double *scalar = nullptr);
+                      double *scalar = nullptr, const int *gate = nullptr);
 // rolling shutter with solved bundles: W rows of the virtual observations
 // (Plan::build, PV)
 void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,

@@ -2317,13 +2317,17 @@ __global__ void k_bundle_factor(DevProblem P, const double *__restrict__ Abb,
 // (the Jacobian epilogue's rows, which no W row reads: one launch less)
 // PCT: the widest camera-frame block the launch carries in registers (the
 // plan's pc_uniform-based bound: 8 for pose + focal plans, else PCMAX).
+// gate (enqueued behind the gated Jacobian, Plan::pre_jac_enqueue): runs
+// only when the device's restatement of the host's decision let the
+// Jacobian run.
 template <int PCT>
 __global__ void __launch_bounds__(64) k_schur_obs(DevProblem P, const double *__restrict__ J,
                                                   const double *__restrict__ Lb, double *W,
                                                   int nob, const RedSpec red,
                                                   const double *__restrict__ partial,
-                                                  double *scalar) {
+                                                  double *scalar, const int *gate) {
     extern __shared__ double sw[];  // 64 x wst doubles (9 KB for pose-only BA)
+    if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     const int lane = threadIdx.x;
     if ((int)blockIdx.x >= nob) {
         const RedRow rw = red.row[blockIdx.x - nob];
@@ -4327,16 +4331,16 @@ void launch_bundle_factor(hipStream_t s, const DevProblem &P, const double *Abb,
     k_bundle_factor<<<nblk(P.nB, 64), 64, 0, s>>>(P, Abb, Abg, g, diag, lam, Lb, tb, Wg, fail);
 }
 void launch_schur_obs(hipStream_t s, const DevProblem &P, const double *J, const double *Lb,
-                      double *W, const RedSpec *red, const double *partial, double *scalar) {
+                      double *W, const RedSpec *red, const double *partial, double *scalar,
+                      const int *gate) {
     const int nob = nblk(P.M, 64), nr = red ? red->nrows : 0;
-    if (nob + nr > 0)
-    {
+    if (nob + nr > 0) {
         if (P.wst / 3 <= 8)
             k_schur_obs<8><<<nob + nr, 64, sizeof(double) * 64 * P.wst, s>>>(
-                P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar);
+                P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar, gate);
         else
             k_schur_obs<PCMAX><<<nob + nr, 64, sizeof(double) * 64 * P.wst, s>>>(
-                P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar);
+                P, J, Lb, W, nob, red ? *red : RedSpec{}, partial, scalar, gate);
     }
 }
 void launch_schur_obs_rs(hipStream_t s, const DevProblem &PV, int Mr, const int *nloc,

@@ -320,6 +320,25 @@ void Plan::pre_jac_enqueue(const double *dx, double *eu, double *ed) {
                   d_glob_partial, glob_chunk, epi, true);
         pre_bnd_pending = true;
     }
+    // ... and (MMBA_PATH_PRE_SCHUR = 1) the next damped solve's first launch
+    // (the undamped solve of the next lmpar: lam = 0 with the bundle factor
+    // the pass just formed), which carries the epilogue's reduction -- the
+    // rows jac() defers at a later iteration (first = 0: no XN2; gnorm).
+    // Measured on C4 (profiles/r6_presch/): the 5.8 us idle gap moves from
+    // before k_schur_obs to before k_schur_dest_u -- the host's launches of
+    // the trial and the gated passes are what it waits for -- and the rate is
+    // unchanged, so opt-in
+    pre_sobs_pending = false;
+    if (pre_bnd_pending && fold_ok && nB_solved > 0 && !rs_bnd && red_defer_ok() &&
+        path_choice(MMBA_PATH_PRE_SCHUR) == 1) {
+        const int ncol = ncf + (nB + NE_BND_TPB - 1) / NE_BND_TPB;
+        RedSpec rs{};
+        rs.flag_slot = -1;
+        rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
+        rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
+        launch_schur_obs(s, P, d_J, d_Lb, d_W, &rs, d_partial, d_scalar, d_gate);
+        pre_sobs_pending = true;
+    }
     pre_jac_x = dx;
 }
 
@@ -437,6 +456,8 @@ void Plan::jac(const double *dx, const JacLM *lm) {
     pre_jac_pending = false;
     const bool pre_bnd = pre_done && pre_bnd_pending;  // its bundle pass ran ahead too
     pre_bnd_pending = false;
+    sobs_ahead = pre_done && pre_sobs_pending;  // and the next damped solve's k_schur_obs
+    pre_sobs_pending = false;
     if (pre_done) {
         // k_jac_ne_u ran ahead at this x (its gate was open: the device took
         // this trial point, as the host did)
@@ -480,7 +501,10 @@ void Plan::jac(const double *dx, const JacLM *lm) {
             rs.row[rs.nrows++] = {0, ncol, 1, SL_ZERO};
             if (epi.do_xn) rs.row[rs.nrows++] = {pw, ncol, 0, SL_XN2};
             if (epi.do_gn) rs.row[rs.nrows++] = {2 * pw, ncol, 1, SL_GNORM};
-            if (red_defer_ok() && !timing) {  // rides in the next k_schur_init launch
+            if (sobs_ahead) {
+                // carried by the k_schur_obs enqueued with the Jacobian ahead
+                // of the decision (same rows: first = 0, gnorm)
+            } else if (red_defer_ok() && !timing) {  // rides in the next k_schur_init launch
                 pend_rs = rs;
                 pend_red = true;
             } else {
@@ -710,10 +734,13 @@ void Plan::solve_damped_enqueue(double lam, int dnorm_slot, bool defer, bool dno
         // square roots and divisions lengthen the latency-bound pass)
         if (!(lam == 0. && lb0_valid))  // else formed by the Jacobian's bundle pass
             launch_bundle_factor(s, P, d_Abb, d_Abg, d_g, d_diag, lam, d_Lb, d_tb, d_Wg, d_fail);
+        // W of this undamped solve already enqueued behind the gated Jacobian
+        const bool ahead = sobs_ahead && lam == 0. && lb0_valid && !rs_bnd;
+        sobs_ahead = false;
         lb0_valid = false;
         if (rs_bnd)  // W rows of the virtual observations
             launch_schur_obs_rs(s, PV, M, d_nloc, d_vobs, d_vcoff, d_J, d_Lb, d_W);
-        else {
+        else if (!ahead) {
             launch_schur_obs(s, P, d_J, d_Lb, d_W, pend_red ? &pend_rs : nullptr, d_partial,
                              d_scalar);
             pend_red = false;
@@ -1437,6 +1464,8 @@ int Plan::solve(double *x_inout, double *fvec_out, double *eu_out, double *ed_ou
         ++spec_replays;
         pre_jac_pending = false;
         pre_bnd_pending = false;
+        pre_sobs_pending = false;
+        sobs_ahead = false;
         seq_pending = false;
         mirror_pending = false;
         slots_staged = false;
@@ -1466,6 +1495,7 @@ int Plan::solve_once(double *x_inout, double *fvec_out, double *eu_out, double *
     t_func = t_jac = t_linear = 0.;
     cbk = cb;
     pre_hb_enq = false;
+    pre_sobs_pending = sobs_ahead = false;
     pre_hb_on = nranks == 1 && n > 0 && pre_jac && (fvec_out || eu_out || ed_out) &&
                 path_choice(MMBA_PATH_PRE_HANDBACK) != 0 &&
                 map_outputs(fvec_out, eu_out, ed_out, pre_hb_map);

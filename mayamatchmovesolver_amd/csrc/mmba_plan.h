@@ -497,6 +497,11 @@ struct Plan {
     DevProblem P_nojb() const;
     bool stall_done = false;  // MMBA_PATH_STALL_SHARD fired
     bool pre_bnd_pending = false;
+    // k_schur_obs enqueued behind the gated bundle pass too, with the
+    // Jacobian epilogue's deferred reduction (pre_jac_enqueue); sobs_ahead:
+    // the jac() that took the pre-enqueued pass hands it to the next damped
+    // solve, which then skips that launch
+    bool pre_sobs_pending = false, sobs_ahead = false;
     double *d_cf_part = nullptr;      // k_ne_cf_split partial sums
     unsigned *d_cf_ticket = nullptr;  // k_ne_cf_split tickets (monotonic)  // the bundle pass was enqueued with the pre-enqueued Jacobian
     void wait_event();

@@ -248,24 +248,27 @@ def test_k2_records_and_backsub_forms_bit_identical(solver_type, gpu_ctx, paths)
     re-evaluating each observation's bundle columns instead of reading the
     records the fused Jacobian pass stores (MMBA_PATH_JB_RECOMPUTE, jac_obs_u's
     arithmetic) and the trial back substitution forming W_i^T x itself
-    (MMBA_PATH_BACKSUB_ONEPASS, k_obs_wtx's sums) give the same bits: x, the
-    ||f|| trace and fvec identical in all four combinations.  300 frames: the
+    (MMBA_PATH_BACKSUB_ONEPASS, k_obs_wtx's sums) give the same bits, and so
+    does k_schur_obs enqueued ahead of the host's decision or after it
+    (MMBA_PATH_PRE_SCHUR): x, the ||f|| trace and fvec identical.  300 frames: the
     fused Jacobian + camera-frame pass (>= 256 camera-frames) is taken."""
     prob = S.make_config(3, frames=300, scale=0.06)
     # lmdif's maxfev counts the n FD evaluations of a Jacobian too
     its = 12 if solver_type == abi.SOLVER_TYPE_CMINPACK_LMDER else 2 * prob.num_params + 6
     opt = S.config_options(prob, solver_type=solver_type, iterations=its)
     runs = {}
-    for jb in (0, 1):
-        for one in (0, 1):
-            paths(abi.PATH_JB_RECOMPUTE, jb)
-            paths(abi.PATH_BACKSUB_ONEPASS, one)
-            s = Solver(prob, opt, context=gpu_ctx)
-            try:
-                runs[(jb, one)] = s.solve()
-            finally:
-                s.close()
-    ref = runs[(0, 0)]
+    for jb, one, pre in ((0, 0, 1), (0, 1, 1), (1, 0, 1), (1, 1, 1), (0, 0, 0)):
+        # pre: the next damped solve's k_schur_obs enqueued with the gated
+        # Jacobian (MMBA_PATH_PRE_SCHUR = 1) or after the decision (default)
+        paths(abi.PATH_JB_RECOMPUTE, jb)
+        paths(abi.PATH_BACKSUB_ONEPASS, one)
+        paths(abi.PATH_PRE_SCHUR, pre)
+        s = Solver(prob, opt, context=gpu_ctx)
+        try:
+            runs[(jb, one, pre)] = s.solve()
+        finally:
+            s.close()
+    ref = runs[(0, 0, 1)]
     assert ref.result["iterations"] > 2
     for k, r in runs.items():
         np.testing.assert_array_equal(r.x, ref.x, err_msg=str(k))
