@@ -516,17 +516,33 @@ __global__ void __launch_bounds__(256) k_residual(DevProblem P, const double *__
                 const int nl = nloc[i];
                 if (P.jcol_implicit) {
                     // uniform plans: column l is camera variant l (l < nv), then
-                    // the bundle's parameters (k_jacobian_u's order)
+                    // the bundle's parameters (k_jacobian_u's order).  Eight
+                    // columns' index, step and J loads issued before their
+                    // products (the sums in column order as before)
                     const int voff = P.cf_var_off[cf];
                     const int nv = P.cf_var_off[cf + 1] - voff - 1;
                     const int4 p4 = P.bnd_p4[b];
-                    for (int l = 0; l < nl; ++l) {
-                        const int a = l - nv;
-                        const int p = l < nv ? P.cf_var_param[voff + 1 + l]
-                                             : (a == 0 ? p4.x : (a == 1 ? p4.y : p4.z));
-                        const double pv = pstep[p];
-                        ax += J[(size_t)(2 * l) * M + i] * pv;
-                        ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+                    for (int l0 = 0; l0 < nl; l0 += 8) {
+                        double jx[8], jy[8], pv[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            const int l = l0 + k;
+                            if (l < nl) {
+                                const int a = l - nv;
+                                const int p = l < nv ? P.cf_var_param[voff + 1 + l]
+                                                     : (a == 0 ? p4.x : (a == 1 ? p4.y : p4.z));
+                                pv[k] = pstep[p];
+                                jx[k] = J[(size_t)(2 * l) * M + i];
+                                jy[k] = J[(size_t)(2 * l + 1) * M + i];
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            if (l0 + k < nl) {
+                                ax += jx[k] * pv[k];
+                                ay += jy[k] * pv[k];
+                            }
+                        }
                     }
                 } else {
                     for (int l = 0; l < nl; ++l) {
@@ -618,14 +634,27 @@ __global__ void __launch_bounds__(256) k_residual_jp_cf(
         if (own_obs(P, i)) {
             s += r.ex * r.ex + r.ey * r.ey;
             // column l is camera variant l (l < nv), then the bundle's
-            // parameters (k_residual<JP>'s implicit-jcol order)
+            // parameters (k_residual<JP>'s implicit-jcol order); every J row
+            // and step load issued before the products (nl <= PC + 3), the
+            // sums in column order as before
+            constexpr int NL = PC + 3;
+            double jx[NL], jy[NL], pv[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                if (l < nl) {
+                    const int a = l - nv;
+                    pv[l] = l < nv ? sP[l] : pstep[a == 0 ? p4.x : (a == 1 ? p4.y : p4.z)];
+                    jx[l] = J[(size_t)(2 * l) * M + i];
+                    jy[l] = J[(size_t)(2 * l + 1) * M + i];
+                }
+            }
             double ax = 0., ay = 0.;
-            for (int l = 0; l < nl; ++l) {
-                const int a = l - nv;
-                const double pv = l < nv ? sP[l]
-                                         : pstep[a == 0 ? p4.x : (a == 1 ? p4.y : p4.z)];
-                ax += J[(size_t)(2 * l) * M + i] * pv;
-                ay += J[(size_t)(2 * l + 1) * M + i] * pv;
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                if (l < nl) {
+                    ax += jx[l] * pv[l];
+                    ay += jy[l] * pv[l];
+                }
             }
             sj += ax * ax + ay * ay;
         }
@@ -3051,6 +3080,26 @@ __global__ void k_backsub_bundle(DevProblem P, const double *__restrict__ W,
         if (a < pb) x[P.bnd_par[po + a]] = xb[a];
 }
 
+// k_trial_prep's operations for parameter j with step xs_j; dj = diag[j] and
+// x0 = x[j] already loaded.
+__device__ __forceinline__ void trial_one_pre(const DevProblem &P, const TrialFold &T, int j,
+                                              double xsj, double dj, double x0, double &pn,
+                                              double &xn) {
+    const double st = -xsj;
+    const double xj = x0 + st;
+    const double w3 = dj * st;
+    T.wa1[j] = st;
+    T.wa2[j] = xj;
+    T.wa3[j] = w3;
+    param_prep_one(P, j, xj, T.ext, T.ext_pert, T.step, T.solver_type, T.delta, T.eps_dif);
+    set_attr_one(P, j, T.ext[j]);
+    if (own_mask(T.own, j)) {  // sharded: each parameter counted by its owner
+        pn += w3 * w3;
+        const double v = dj * xj;
+        xn += v * v;
+    }
+}
+
 // k_trial_prep's operations for parameter j with step xs_j.
 __device__ __forceinline__ void trial_one(const DevProblem &P, const TrialFold &T, int j,
                                           double xsj, double &pn, double &xn) {
@@ -3091,9 +3140,25 @@ __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double
             const int nG = P.nG;
             const int nCF = P.nR - nG;
             double s[3] = {tb[(size_t)b * 3], tb[(size_t)b * 3 + 1], tb[(size_t)b * 3 + 2]};
-            for (int q = P.bobs_off[b]; q < P.bobs_off[b + 1]; ++q) {
-                double u[3];
-                if (W) {  // one pass (MMBA_PATH_BACKSUB_ONEPASS): k_obs_wtx's arithmetic here
+            const int q0 = P.bobs_off[b], q1 = P.bobs_off[b + 1];
+            // the operands of the bundle's three parameters, loaded before the
+            // gather (independent of it): trial_one's reads, issued together
+            const int po = P.bnd_par_off[b];
+            int jj[3] = {-1, -1, -1};
+            double dgj[3] = {0., 0., 0.}, x0j[3] = {0., 0., 0.};
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                if (a < pb) jj[a] = P.bnd_par[po + a];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                if (a < pb) {
+                    dgj[a] = T.diag[jj[a]];
+                    x0j[a] = T.x[jj[a]];
+                }
+            if (W) {
+                for (int q = q0; q < q1; ++q) {
+                    // one pass (MMBA_PATH_BACKSUB_ONEPASS): k_obs_wtx's arithmetic here
+                    double u[3];
                     const int i = P.bobs[q];
                     const int cf = P.obs_cf[i];
                     const int pc = min(P.cf_pc[cf], P.wst / 3);
@@ -3104,15 +3169,28 @@ __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double
                         const double xv = xR[r0 + a];
                         for (int c = 0; c < 3; ++c) u[c] += row[a * 3 + c] * xv;
                     }
-                } else {
-                    const double4 uu = reinterpret_cast<const double4 *>(U)[P.bobs[q]];
-                    u[0] = uu.x;
-                    u[1] = uu.y;
-                    u[2] = uu.z;
+                    s[0] -= u[0];
+                    s[1] -= u[1];
+                    s[2] -= u[2];
                 }
-                s[0] -= u[0];
-                s[1] -= u[1];
-                s[2] -= u[2];
+            } else {
+                // u_i = W_i^T x from k_obs_wtx, four observations' loads issued
+                // before their (in-order) subtractions: two memory round trips
+                // per four observations instead of two per observation
+                const double4 *U4 = reinterpret_cast<const double4 *>(U);
+                for (int qb = q0; qb < q1; qb += 4) {
+                    double4 uu[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (qb + k < q1) uu[k] = U4[P.bobs[qb + k]];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (qb + k < q1) {
+                            s[0] -= uu[k].x;
+                            s[1] -= uu[k].y;
+                            s[2] -= uu[k].z;
+                        }
+                }
             }
             for (int q = 0; q < nG; ++q) {
                 const double xv = xR[nCF + q];
@@ -3131,13 +3209,12 @@ __global__ void __launch_bounds__(64) k_backsub_trial(DevProblem P, const double
                     if (k < pb) t -= L[k][a] * xb[k];
                 xb[a] = t / L[a][a];
             }
-            const int po = P.bnd_par_off[b];
 #pragma unroll
             for (int a = 0; a < 3; ++a)
                 if (a < pb) {
-                    const int j = P.bnd_par[po + a];
+                    const int j = jj[a];
                     x[j] = xb[a];
-                    trial_one(P, T, j, xb[a], pn, xn);
+                    trial_one_pre(P, T, j, xb[a], dgj[a], x0j[a], pn, xn);
                 }
         }
         // the bundle's record at the trial point (k_records' arithmetic; this
