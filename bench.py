@@ -158,6 +158,11 @@ def broadcast_bytes(dist, data: bytes | None, n: int) -> bytes:
 K2_REGEX = "k_jacobian|k_jac_ne|k_ne_|k_colnorms|k_jac_epilogue"
 VALU_F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
             "SQ_INSTS_VALU_TRANS_F64")
+# the reduced solve's kernels (Plan::solve_damped_enqueue's factorisations) and
+# their matrix-core counters: SQ_VALU_MFMA_BUSY_CYCLES counts cycles (summed
+# over the SIMDs), SQ_WAVE_CYCLES quad-cycles (MI355X_MICROARCH.md, PMC units)
+RED_REGEX = "k_pcr_solve|k_bcr_|k_band_factor|k_dense_|k_dgemm|k_bd_"
+MFMA_PASS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES")
 
 
 def pmc_traffic(args):
@@ -188,12 +193,13 @@ def pmc_traffic(args):
     tmp = tempfile.mkdtemp(prefix="mmba_pmc_", dir="/tmp")
     # one pass per counter group: FETCH_SIZE and WRITE_SIZE do not fit one
     # pass; the four fp64 VALU instruction counters (SQ) fit one
-    passes = (("FETCH_SIZE",), ("WRITE_SIZE",), VALU_F64)
+    passes = (("FETCH_SIZE",), ("WRITE_SIZE",), VALU_F64, MFMA_PASS)
     try:
         for group in passes:
             out = os.path.join(tmp, group[0])
+            rx = RED_REGEX if group is MFMA_PASS else K2_REGEX
             cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", *group,
-                   "--kernel-include-regex", K2_REGEX, "-d", out, "-o", "k2",
+                   "--kernel-include-regex", rx, "-d", out, "-o", "k2",
                    "--output-format", "csv", "--"] + base
             r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
                                stderr=subprocess.DEVNULL)
@@ -203,6 +209,9 @@ def pmc_traffic(args):
                 if group is VALU_F64:  # optional: the traffic stands without it
                     per["valu_error"] = "rocprofv3 --pmc pass failed (rc=%d)" % r.returncode
                     continue
+                if group is MFMA_PASS:
+                    per["mfma_error"] = "rocprofv3 --pmc pass failed (rc=%d)" % r.returncode
+                    continue
                 return None, "rocprofv3 --pmc %s pass failed (rc=%d)" % (group[0], r.returncode)
             acc = {}
             for row in csv.DictReader(open(files[0])):
@@ -210,7 +219,8 @@ def pmc_traffic(args):
                 c = row.get("Counter_Name", group[0])
                 acc.setdefault(c, {}).setdefault(k, []).append(float(row["Counter_Value"]))
             for c, kv in acc.items():
-                per[c] = {k: sum(v) / len(v) for k, v in kv.items()}
+                per[("red:" if group is MFMA_PASS else "") + c] = {
+                    k: sum(v) / len(v) for k, v in kv.items()}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     fetch = sum(per["FETCH_SIZE"].values()) * 1024.0
@@ -226,8 +236,18 @@ def pmc_traffic(args):
                 "per_kernel": {c: per[c] for c in VALU_F64},
                 "note": "64 x (2 FMA + ADD + MUL + TRANS) fp64 VALU instructions, rocprofv3 "
                         "--pmc, averaged per launch, summed over the K2 kernels"}
+    mfma = None
+    if all("red:" + c in per for c in MFMA_PASS):
+        # per launch of each reduced-solve kernel: matrix-core busy cycles and
+        # the waves' lifetime (quad-cycles x 4)
+        mfma = {k: {"mfma_busy_cycles": per["red:SQ_VALU_MFMA_BUSY_CYCLES"][k],
+                    "valu_instructions": per["red:SQ_INSTS_VALU"].get(k),
+                    "waves": per["red:SQ_WAVES"].get(k),
+                    "wave_cycles": 4.0 * per["red:SQ_WAVE_CYCLES"].get(k, 0.0)}
+                for k in per["red:SQ_VALU_MFMA_BUSY_CYCLES"]}
     detail = {"fetch_size_bytes_raw": fetch, "write_size_bytes": write,
               "valu_f64": valu, "valu_error": per.get("valu_error"),
+              "reduced_solve_mfma": mfma, "mfma_error": per.get("mfma_error"),
               "per_kernel_kib": {"FETCH_SIZE": per["FETCH_SIZE"],
                                  "WRITE_SIZE": per["WRITE_SIZE"]},
               "correction": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE "
@@ -591,6 +611,18 @@ def main():
                     "us_per_level": 1e3 * stats["chol_ms_avg"] / (lv + 1),
                     "model": "t = (levels + 1) x (K-step pivot chain + products + neighbour "
                              "hand-off); the last term is the uncoupled block's solve"}
+        mf = (traffic_detail or {}).get("reduced_solve_mfma")
+        if mf:
+            # matrix-core occupancy of the reduced solve (rocprofv3 --pmc):
+            # busy cycles over launch time x 2.4 GHz x 1,024 SIMDs
+            chol["mfma_pmc"] = {k: dict(v, busy_frac_of_chip=(
+                v["mfma_busy_cycles"] / (stats["chol_ms_avg"] * 1e-3 * 2.4e9 * 1024.0)
+                if stats["chol_ms_avg"] > 0 else None)) for k, v in mf.items()}
+            chol["mfma_pmc_note"] = ("SQ_VALU_MFMA_BUSY_CYCLES per launch (cycles, summed over "
+                                     "SIMDs), SQ_WAVE_CYCLES x 4; busy_frac_of_chip against the "
+                                     "damped solve's HIP-event time")
+        elif traffic_detail and traffic_detail.get("mfma_error"):
+            chol["mfma_pmc"] = traffic_detail["mfma_error"]
         if kind == 2 and stats["chol_ms_avg"] > 0:
             tf = stats["chol_flops"] / (stats["chol_ms_avg"] * 1e-3) / 1e12
             chol.update({"achieved_tflops": tf, "peak_tflops": FP64_MFMA_PEAK_TF,
