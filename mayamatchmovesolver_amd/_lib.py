@@ -90,7 +90,10 @@ def lib():
         L.mmba_plan_jacobian.restype = C.c_int
         L.mmba_plan_jacobian.argtypes = [C.c_void_p, dp, dp]
         L.mmba_plan_solve.restype = C.c_int
-        L.mmba_plan_solve.argtypes = [C.c_void_p, dp, dp, dp, dp, C.POINTER(abi.MmbaResult),
+        # (x and the three output lists as plain addresses: Solver.solve passes
+        # the arrays' data pointers, ~2 us each instead of ~5 for data_as)
+        L.mmba_plan_solve.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.POINTER(abi.MmbaResult),
                                       C.POINTER(abi.MmbaCallbacks), C.POINTER(abi.MmbaTrace)]
         L.mmba_plan_outputs.restype = C.c_int
         L.mmba_plan_outputs.argtypes = [C.c_void_p, dp, dp, dp]

@@ -24,6 +24,11 @@ def _dp(a):
     return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
 
 
+def _addr(a):
+    """Data address of a C-contiguous array (for c_void_p arguments)."""
+    return None if a is None else a.__array_interface__["data"][0]
+
+
 def _num(v):
     # mmstring::numberToString uses default 6 significant digits (B10)
     return "%g" % v
@@ -331,11 +336,17 @@ class Solver:
             assert fvec.size >= m and eu.size >= m and ed.size >= M
             assert fvec.flags.c_contiguous and eu.flags.c_contiguous and ed.flags.c_contiguous
         res = abi.MmbaResult()
-        tbuf = np.zeros(max(1, trace_capacity))
-        tr = abi.MmbaTrace(_dp(tbuf), trace_capacity, 0)
+        # the ||f|| trace buffer and its descriptor are kept across solves of
+        # the same capacity (the library resets count; the used part is copied)
+        if getattr(self, "_trace_cap", None) != trace_capacity:
+            self._tbuf = np.zeros(max(1, trace_capacity))
+            self._tr = abi.MmbaTrace(_dp(self._tbuf), trace_capacity, 0)
+            self._trace_cap = trace_capacity
+        tbuf, tr = self._tbuf, self._tr
         cbs = _callbacks(interrupt)
-        rc = lib().mmba_plan_solve(self._h, _dp(x), _dp(fvec), _dp(eu), _dp(ed), C.byref(res),
-                                   C.byref(cbs) if cbs is not None else None, C.byref(tr))
+        rc = lib().mmba_plan_solve(self._h, _addr(x), _addr(fvec), _addr(eu), _addr(ed),
+                                   C.byref(res), C.byref(cbs) if cbs is not None else None,
+                                   C.byref(tr))
         if rc not in (abi.MMBA_OK, abi.MMBA_ERR_INTERRUPTED):
             check(rc)
         return SolveResult(x=x, fvec=fvec, err_user=eu, err_dist=ed, result=res.as_dict(),
