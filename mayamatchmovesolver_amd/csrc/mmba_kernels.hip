@@ -955,8 +955,13 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i, const JacC
             jx = (r.x - r0.ex) / s;
             jy = (r.y - r0.ey) / s;
         }
+#ifdef MMBA_J_NT  // (A/B build: J rows stored non-temporal)
+        __builtin_nontemporal_store(jx, &J[(size_t)(2 * l) * M + i]);
+        __builtin_nontemporal_store(jy, &J[(size_t)(2 * l + 1) * M + i]);
+#else
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
+#endif
         if (wcol) jcol[(size_t)l * M + i] = p;
         if (p == pstale) hit = tag;
         ++l;
