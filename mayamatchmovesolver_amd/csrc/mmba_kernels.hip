@@ -955,13 +955,10 @@ __device__ __forceinline__ void jac_obs_u(const DevProblem &P, int i, const JacC
             jx = (r.x - r0.ex) / s;
             jy = (r.y - r0.ey) / s;
         }
-#ifdef MMBA_J_NT  // (A/B build: J rows stored non-temporal)
-        __builtin_nontemporal_store(jx, &J[(size_t)(2 * l) * M + i]);
-        __builtin_nontemporal_store(jy, &J[(size_t)(2 * l + 1) * M + i]);
-#else
+        // (stored non-temporal in a round-6 A/B build: C2 +1.5 %, C4 -2 % as its
+        // trial pass re-reads J from L2; profiles/r6_jnt/)
         J[(size_t)(2 * l) * M + i] = jx;
         J[(size_t)(2 * l + 1) * M + i] = jy;
-#endif
         if (wcol) jcol[(size_t)l * M + i] = p;
         if (p == pstale) hit = tag;
         ++l;
