@@ -2280,15 +2280,16 @@ __global__ void __launch_bounds__(256) k_reduce_multi(const double *__restrict__
             __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    for (int i = threadIdx.x; i < host_n; i += blockDim.x)
-        host[i] = __hip_atomic_load(&scalar[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (host_seq) {
-        // the mirror's writes, then its sequence word (the host polls it)
-        __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence_system();
-            __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the mirror by wave 0 alone (host_n <= 64 slots: one store per lane), its
+    // own system fence, then lane 0's release of the sequence word the host
+    // polls -- no workgroup barrier and no fence in the other waves
+    if (threadIdx.x < 64) {
+        for (int i = threadIdx.x; i < host_n; i += 64)
+            host[i] = __hip_atomic_load(&scalar[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (host_seq) {
+            __threadfence_system();  // the wave's mirror stores visible to the host
+            if (threadIdx.x == 0)
+                __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
